@@ -1,0 +1,170 @@
+/*
+ * pemp.h — C-ABI of libpemp.so, the MI355X (gfx950) kernels of the keypoint-graph hot path of
+ * nibox/Pose-Estimation-with-Message-Passing-Networks.
+ *
+ * Every function takes caller-owned DEVICE pointers (except where marked host), plain sizes and
+ * a hipStream_t passed as void*. Work is stream-ordered; nothing synchronises the host. The
+ * library owns no returned memory: outputs go to caller-allocated buffers, scratch goes to a
+ * caller-allocated workspace sized by the matching *_workspace_size() query.
+ * Return value: 0 (PEMP_OK) or a negative PEMP_ERR_*; pemp_last_error() gives a message
+ * (thread-local).
+ *
+ * Reference interfaces each entry point replaces (paths relative to the reference repo):
+ *   pemp_detect          ConstructGraph.py:1161-1209 joint_det_from_scoremap + cat_unique,
+ *                        Utils/Utils.py:15-20 non_maximum_suppression
+ *   pemp_pack_nodes      ConstructGraph.py:100-103,206-231 (node features, tags, batching)
+ *   pemp_fully_graph     ConstructGraph.py:376-381 fully_connected_mpn_graph (+ batch offsets :222-223)
+ *   pemp_knn_graph_*     ConstructGraph.py:363-368 knn_mpn_graph (torch_cluster knn_graph k=50,
+ *                        PyG to_undirected, remove_self_loops)
+ *   pemp_edge_features   ConstructGraph.py:289-359 (edge_attr)
+ *   pemp_mpn_forward     Models/MessagePassingNetwork/NodeClassificationMPNSimple.py:62-97 with
+ *                        layers.py:32-86 (MPLayer) / :157-274 (TypeAwareMPNLayer)
+ */
+#ifndef PEMP_H_
+#define PEMP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PEMP_ABI_VERSION 1
+
+enum {
+  PEMP_OK = 0,
+  PEMP_ERR_INVALID_ARG = -1,
+  PEMP_ERR_HIP = -2,
+  PEMP_ERR_WORKSPACE = -3,
+  PEMP_ERR_UNSUPPORTED = -4,
+};
+
+int pemp_abi_version(void);
+const char* pemp_last_error(void);
+/* 0 if the current HIP device is a gfx950 (MI355X); PEMP_ERR_UNSUPPORTED otherwise. */
+int pemp_device_check(void);
+
+/* ------------------------------------------------------------------------------------------
+ * Detection: NMS maxima (MaxPool2d(k,1,k//2) == s, -inf padding), s *= maxima (* mask),
+ * per-type top-k (ties: lower flat index first) + threshold set, cat_unique ordering:
+ *   [top-k dets of type 0..J-1, each sorted by (y,x), value != 0]
+ *   ++ [dets with s >= threshold not already listed, type-major then (y,x)].
+ * use_threshold = 0 restates the DETECT_THRESHOLD > 1.5 branch (top-20, +1e-10).
+ * Writes det_xyt[b][i] = (x, y, type) int64 and det_scores[b][i] for i < min(n, cap), and
+ * n_det[b] = n (the true count, which may exceed cap: re-run with stages = PEMP_DETECT_SELECT
+ * and a larger cap; the NMS stage's workspace is reused).
+ * ---------------------------------------------------------------------------------------- */
+enum { PEMP_DETECT_NMS = 1, PEMP_DETECT_SELECT = 2, PEMP_DETECT_ALL = 3 };
+size_t pemp_detect_workspace_size(int B, int J, int H, int W, int topk);
+int pemp_detect(const float* scoremaps /*[B,J,H,W]*/, const float* masks /*[B,H,W] or NULL*/,
+                int B, int J, int H, int W, int pool_kernel, float threshold, int use_threshold,
+                int topk, int stages, void* workspace, size_t workspace_bytes,
+                int64_t* det_xyt /*[B,cap,3]*/, float* det_scores /*[B,cap]*/,
+                int32_t* n_det /*[B]*/, int cap, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Node packing into the batched layout: x[g] = features[b,:,y,x], joint_det[g], joint_scores[g],
+ * batch_index[g] = b, joint_tags[g,:] = tagmaps[b,type,y,x,:] for g = node_off[b] + i.
+ * node_off: device [B+1] int64. tagmaps may be NULL (then joint_tags is not written).
+ * ---------------------------------------------------------------------------------------- */
+int pemp_pack_nodes(const float* features /*[B,C,H,W]*/, int C, const float* tagmaps /*[B,J,H,W,F]*/,
+                    int F, int B, int J, int H, int W, const int64_t* det_xyt, const float* det_scores,
+                    int cap, const int64_t* node_off, int64_t n_total, float* x /*[N,C]*/,
+                    int64_t* joint_det /*[N,3]*/, float* joint_scores /*[N]*/,
+                    int64_t* batch_index /*[N]*/, float* joint_tags /*[N,F]*/, void* stream);
+
+/* Fully connected graph per image: all (i,j), i != j, sorted by (src,dst), node-offset per image.
+ * node_off / edge_off: device [B+1] int64 with edge_off[b+1]-edge_off[b] = n_b (n_b - 1). */
+int pemp_fully_graph(const int64_t* node_off, const int64_t* edge_off, int B, int64_t e_total,
+                     int64_t* edge_index /*[2,E]*/, void* stream);
+
+/* knn graph per image (k nearest by squared integer distance, ties by node index; k+1 queried
+ * with self removed), symmetrised and sorted by (src,dst).
+ * Stage 1 (count): writes edge_count[b] (device int64 [B]). Host then sizes E and edge_off.
+ * Stage 2 (emit): writes edge_index with per-image offsets edge_off (device [B+1]).
+ * node_off_host: HOST [B+1] copy of node_off (grid sizing). Workspace is shared by both stages. */
+size_t pemp_knn_workspace_size(const int64_t* node_off_host, int B);
+int pemp_knn_graph_count(const int64_t* joint_det, const int64_t* node_off, const int64_t* node_off_host,
+                         int B, int k, void* workspace, size_t workspace_bytes, int64_t* edge_count,
+                         void* stream);
+int pemp_knn_graph_emit(const int64_t* node_off, const int64_t* node_off_host, int B,
+                        const int64_t* edge_off, int64_t e_total, void* workspace,
+                        size_t workspace_bytes, int64_t* edge_index, void* stream);
+
+/* Edge features. mode: */
+enum {
+  PEMP_EF_POSITION_CONNECTION = 0, /* [dx, dy, onehot(J)]       (J+2) */
+  PEMP_EF_CONNECTION = 1,          /* [onehot(J)]               (J)   */
+  PEMP_EF_NOTHING = 2,             /* [0]                       (1)   */
+  PEMP_EF_POSITION = 3,            /* [dx, dy]                  (2)   */
+  PEMP_EF_POSITION_ANGLE_CONNECTION = 4 /* [dx, dy, theta, onehot(J)] (J+3) */
+};
+int pemp_edge_features(const int64_t* joint_det /*[N,3]*/, const int64_t* edge_index /*[2,E]*/,
+                       int64_t e_total, int J, float norm_factor, int mode, float* edge_attr,
+                       void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Message-passing network, inference (eval-mode BatchNorm folded into the next Linear by the
+ * caller). All hidden widths are 64. Weights are fp32 row-major [out_pad][in_pad], zero padded
+ * to multiples of 16 (the caller's folding step; see the Python mirror pemp_amd/mpn/fold.py).
+ * ---------------------------------------------------------------------------------------- */
+enum { PEMP_AGGR_ATTN = 0, PEMP_AGGR_SUM = 1, PEMP_AGGR_MEAN = 2, PEMP_AGGR_MAX = 3 };
+
+typedef struct pemp_layer {
+  const float* w; /* [out_pad][in_pad] */
+  const float* b; /* [out_pad] */
+  int32_t in_dim, out_dim, relu, pad_;
+} pemp_layer;
+
+typedef struct pemp_mlp {
+  pemp_layer layer[4];
+  int32_t n_layers, pad_;
+} pemp_mlp;
+
+typedef struct pemp_mpn_weights {
+  pemp_mlp node_emb;   /* NODE_INPUT_DIM -> 64 */
+  pemp_mlp edge_emb;   /* EDGE_INPUT_DIM -> 64 */
+  const float* pre_w;  /* [128 + T*64][128]: W1[:, x_i], W1[:, x_j], W_t[:, x_i] (t < T) */
+  const float* pre_b;  /* [128 + T*64]:      0,          0,          b_t               */
+  const float* q0_w;   /* [64][64]  W1[:, e_init] */
+  const float* q0_b;   /* [64]      b1            */
+  const float* e1_w;   /* [64][64]  W1[:, e_cur]  */
+  const float* e2_w;   /* [64][64]  mlp_edge.2    */
+  const float* e2_b;   /* [64]                    */
+  const float* msg_w;  /* [T][64][64] W_t[:, e'] */
+  const float* attn_w; /* [64] attn_net.0.weight (PEMP_AGGR_ATTN) */
+  const float* upd_w;  /* [64][T*64] update_mlp.0.weight, or NULL (x_new = agg) */
+  const float* upd_b;  /* [64] */
+  pemp_mlp edge_head;  /* 64 -> .. -> 1 */
+  pemp_mlp node_head;  /* 64 -> .. -> 1 */
+  pemp_mlp class_head; /* 64 -> .. -> J */
+  float attn_b;
+  int32_t pad_;
+} pemp_mpn_weights;
+
+typedef struct pemp_mpn_desc {
+  int32_t num_types;      /* T: aggregation/message types (NUM_JOINTS, 6, 9) or 1 (MPLayer) */
+  int32_t num_joints;     /* J: class-head width */
+  int32_t steps;          /* STEPS */
+  int32_t aux_loss_steps; /* heads recorded at iterations it >= steps - aux - 1 */
+  int32_t aggr;           /* PEMP_AGGR_* */
+  int32_t hidden;         /* must be 64 */
+  int32_t edge_attr_dim;  /* EDGE_INPUT_DIM */
+  int32_t node_in_dim;    /* NODE_INPUT_DIM */
+} pemp_mpn_desc;
+
+size_t pemp_mpn_workspace_size(const pemp_mpn_desc* desc, int64_t N, int64_t E);
+/* x [N,node_in_dim], edge_attr [E,edge_attr_dim], edge_index [2,E] (row 0 source j, row 1
+ * target i), node_types [N] (already mapped by sum_node_types; values < T).
+ * Outputs, one slot per recorded iteration r (n_rec = min(aux+1, steps)):
+ *   edge_logits [n_rec][E], node_logits [n_rec][N], class_logits [n_rec][N][J]. */
+int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weights* weights, const float* x,
+                     const float* edge_attr, const int64_t* edge_index, const int64_t* node_types,
+                     int64_t N, int64_t E, float* edge_logits, float* node_logits, float* class_logits,
+                     void* workspace, size_t workspace_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PEMP_H_ */

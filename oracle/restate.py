@@ -1,0 +1,309 @@
+"""CPU restatement of the keypoint-graph hot path (the parity ORACLE and the timed CPU baseline).
+
+TEST INFRASTRUCTURE. Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may import this module, and only as the checker / the CPU baseline. The
+product package never imports it; the product path fails loudly without its HIP library.
+
+Restates, op for op on CPU torch fp32, the reference's inference path:
+  * detection        — ``src/Utils/Utils.py:15-20`` (NMS), ``src/graph_constructor/ConstructGraph.py:1161-1209``
+  * graph + features — ``ConstructGraph.py:46-68,100-103,206-249,251-381``
+  * MPN forward      — ``src/Models/MessagePassingNetwork/NodeClassificationMPNSimple.py:23-97``,
+                       ``layers.py:8-86,157-274``, ``utils.py:6-19``
+Pinned against the reference itself by ``tests/golden/*.npz`` (made by ``oracle/gen_golden.py``,
+which runs the reference's own files under ``oracle/ref_shims.py``).
+
+Defined where the reference is unpinned:
+  * top-k ties: lower flat index wins (the CUDA radix-select order the reference ran on);
+  * knn ties:   (squared integer distance, node index) — torch_cluster's order is unspecified.
+"""
+import torch
+import torch.nn.functional as F
+
+# ----------------------------------------------------------------------------------------
+# Detection (Utils.py:15-20, ConstructGraph.py:1161-1209)
+# ----------------------------------------------------------------------------------------
+
+
+def nms_maxima(scoremap: torch.Tensor, pool_kernel: int) -> torch.Tensor:
+    """Utils.py:15-20 — 1.0 where MaxPool2d(k,1,k//2) (implicit -inf padding) equals the input."""
+    assert pool_kernel % 2 == 1
+    pooled = F.max_pool2d(scoremap[None], pool_kernel, 1, pool_kernel // 2)[0]
+    return torch.eq(pooled, scoremap).float()
+
+
+def _topk_lowest_index(values: torch.Tensor, k: int):
+    """Row-wise top-k, ties broken towards the lower index (stable descending sort)."""
+    s, idx = torch.sort(values, dim=1, descending=True, stable=True)
+    return s[:, :k], idx[:, :k]
+
+
+def cat_unique(t1: torch.Tensor, t2: torch.Tensor) -> torch.Tensor:
+    """ConstructGraph.py:1199-1209 — append rows of t2 not present in t1, order preserved."""
+    if t1.shape[0] == 0 or t2.shape[0] == 0:
+        return torch.cat([t1, t2], 0)
+    same = (t1[:, None, :] == t2[None, :, :]).all(-1).any(0)
+    return torch.cat([t1, t2[~same]], 0)
+
+
+def joint_det_from_scoremap(scoremap, num_joints, threshold=0.007, pool_kernel=None, mask=None, hybrid_k=5):
+    """ConstructGraph.py:1161-1196. Returns det [N,3] int64 (x, y, type) and scores [N] f32."""
+    joint_map = nms_maxima(scoremap, pool_kernel)
+    if mask is not None:
+        joint_map = joint_map * mask[None]
+    sm = scoremap * joint_map
+    J, H, W = sm.shape
+    flat = sm.reshape(J, -1)
+    if threshold is not None:
+        k = min(hybrid_k, flat.shape[1])
+        vals, idx = _topk_lowest_index(flat, k)
+        container = torch.zeros_like(flat)
+        container.scatter_(1, idx, vals)
+        t, pos = container.nonzero(as_tuple=True)
+        top = torch.stack([pos % W, pos // W, t], 1)
+        # where(s < thr, 0, s).nonzero(): kept iff not (s < thr) and s != 0 (NaN counts as kept)
+        keep = ~(sm < threshold) & (sm != 0)
+        t2, y2, x2 = keep.nonzero(as_tuple=True)
+        thr = torch.stack([x2, y2, t2], 1)
+        det = cat_unique(top, thr)
+        scores = sm[det[:, 2], det[:, 1], det[:, 0]]
+    else:
+        k = 20
+        vals, idx = _topk_lowest_index(flat, k)
+        container = torch.zeros_like(flat)
+        container.scatter_(1, idx, vals + 1e-10)
+        t, pos = container.nonzero(as_tuple=True)
+        scores = container[t, pos]
+        assert t.shape[0] == k * num_joints
+        det = torch.stack([pos % W, pos // W, t], 1)
+    return det.long(), scores
+
+
+# ----------------------------------------------------------------------------------------
+# Graphs (ConstructGraph.py:363-381) and edge features (:289-359)
+# ----------------------------------------------------------------------------------------
+
+
+def fully_edge_index(n: int) -> torch.Tensor:
+    """dense_to_sparse(ones) -> to_undirected -> remove_self_loops: all i!=j, sorted by (src,dst)."""
+    src = torch.arange(n).repeat_interleave(n)
+    dst = torch.arange(n).repeat(n)
+    m = src != dst
+    return torch.stack([src[m], dst[m]], 0)
+
+
+def knn_edge_index(det: torch.Tensor, k: int = 50) -> torch.Tensor:
+    """knn_graph(xy, k) (k+1 queried, self removed) -> to_undirected -> remove_self_loops."""
+    n = det.shape[0]
+    if n == 0:
+        return torch.zeros(2, 0, dtype=torch.long)
+    xy = det[:, :2]
+    d2 = ((xy[:, None, :] - xy[None, :, :]) ** 2).sum(-1)            # exact integers
+    order = torch.argsort(d2 * n + torch.arange(n)[None, :], dim=1)[:, :k + 1]
+    adj = torch.zeros(n, n, dtype=torch.bool)
+    adj.scatter_(1, order, True)                                      # adj[i, j]: j among i's nearest
+    adj = adj | adj.t()
+    adj.fill_diagonal_(False)
+    src, dst = adj.nonzero(as_tuple=True)
+    return torch.stack([src, dst], 0)
+
+
+def edge_features(det: torch.Tensor, edge_index: torch.Tensor, num_joints: int, norm_factor,
+                  features_to_use) -> torch.Tensor:
+    """ConstructGraph.py:305-359 (modes without associative-embedding tags)."""
+    jx, jy, jt = det[:, 0], det[:, 1], det[:, 2]
+    s, d = edge_index[0], edge_index[1]
+    E = edge_index.shape[1]
+    onehot = torch.zeros(E, num_joints, dtype=torch.long)
+    ar = torch.arange(E)
+    onehot[ar, jt[s]] = 1
+    onehot[ar, jt[d]] = 1
+    dy = (jy[d] - jy[s]).float() / norm_factor
+    dx = (jx[d] - jx[s]).float() / norm_factor
+    mode = set(features_to_use)
+    if mode == {"position", "connection_type"}:
+        return torch.cat([dx[:, None], dy[:, None], onehot.float()], 1)
+    if mode == {"connection_type"}:
+        return onehot.float()
+    if mode == {"nothing"}:
+        return torch.zeros(E, 1)
+    if mode == {"position"}:
+        return torch.cat([dx[:, None], dy[:, None]], 1)
+    if mode == {"position", "angle", "connection_type"}:
+        ax, ay = (jx[s] - jx[d]).float(), (jy[s] - jy[d]).float()
+        theta = torch.abs(torch.acos(ax * torch.rsqrt(ax ** 2 + ay ** 2)))
+        theta[torch.isnan(theta)] = 0.0
+        return torch.cat([dx[:, None], dy[:, None], theta[:, None], onehot.float()], 1)
+    raise NotImplementedError(f"EDGE_FEATURES_TO_USE={features_to_use}")
+
+
+def construct_graph(scoremaps, features, tagmaps, masks, gc, num_joints):
+    """ConstructGraph.py:46-249, inference subset (joints_gt None). Returns the 15-tuple."""
+    B, J, H, W = scoremaps.shape
+    thr = gc.DETECT_THRESHOLD if gc.DETECT_THRESHOLD <= 1.5 else None
+    norm = max(W, H) if gc.NORM_NODE_DISTANCE else 1
+    xs, eas, eis, dets, scs, bis, tgs = [], [], [], [], [], [], []
+    off = 0
+    for b in range(B):
+        det, sc = joint_det_from_scoremap(scoremaps[b], num_joints, threshold=thr,
+                                          pool_kernel=gc.POOL_KERNEL_SIZE,
+                                          mask=masks[b] if gc.MASK_CROWDS else None, hybrid_k=gc.HYBRID_K)
+        x = features[b][:, det[:, 1], det[:, 0]].T
+        if gc.GRAPH_TYPE == "fully":
+            ei = fully_edge_index(det.shape[0])
+        elif gc.GRAPH_TYPE == "knn":
+            ei = knn_edge_index(det)
+        else:
+            raise NotImplementedError(gc.GRAPH_TYPE)
+        ea = edge_features(det, ei, num_joints, norm, gc.EDGE_FEATURES_TO_USE)
+        tg = tagmaps[b, det[:, 2], det[:, 1], det[:, 0]]
+        xs.append(x); eas.append(ea); eis.append(ei + off); dets.append(det); scs.append(sc)
+        bis.append(torch.full((det.shape[0],), b, dtype=torch.long)); tgs.append(tg)
+        off += det.shape[0]
+    return (torch.cat(xs, 0), torch.cat(eas, 0), torch.cat(eis, 1), None, None, None, None,
+            torch.cat(dets, 0), None, None, None, torch.cat(scs, 0), torch.cat(bis, 0), None,
+            torch.cat(tgs, 0))
+
+
+# ----------------------------------------------------------------------------------------
+# MPN (NodeClassificationMPNSimple.py, layers.py) on a state_dict
+# ----------------------------------------------------------------------------------------
+
+
+def _mlp(sd, prefix, x, sizes, bn, end_with_relu=False):
+    """layers.py:8-29 (_make_mlp) in eval mode: Linear, then ReLU [+BN] between layers."""
+    li = 0
+
+    def lin(v):
+        nonlocal li
+        out = F.linear(v, sd[f"{prefix}.{li}.weight"], sd[f"{prefix}.{li}.bias"])
+        li += 1
+        return out
+
+    def bnorm(v):
+        nonlocal li
+        out = F.batch_norm(v, sd[f"{prefix}.{li}.running_mean"], sd[f"{prefix}.{li}.running_var"],
+                           sd[f"{prefix}.{li}.weight"], sd[f"{prefix}.{li}.bias"], False, 0.0, 1e-5)
+        li += 1
+        return out
+
+    n = len(sizes)
+    x = lin(x)
+    if n != 1:
+        x = F.relu(x); li += 1
+        if bn:
+            x = bnorm(x)
+    for i in range(1, n):
+        x = lin(x)
+        if i != n - 1:
+            x = F.relu(x); li += 1
+            if bn:
+                x = bnorm(x)
+    if end_with_relu:
+        x = F.relu(x); li += 1
+        if bn:
+            x = bnorm(x)
+    return x
+
+
+def _segment_softmax(a, index, n):
+    """torch_scatter 2.0.4 scatter_softmax: exp(a - max_seg) / (sum_seg + 1e-12)."""
+    mx = torch.full((n,), float("-inf")).scatter_reduce(0, index, a, "amax", include_self=True)
+    mx = torch.where(torch.isneginf(mx), torch.zeros_like(mx), mx)
+    ex = (a - mx[index]).exp()
+    sm = torch.zeros(n).index_add_(0, index, ex)
+    return ex / (sm + 1e-12)[index]
+
+
+def _scatter(v, index, n, reduce):
+    out = torch.zeros(n, v.shape[1])
+    if reduce in ("add", "sum"):
+        return out.index_add_(0, index, v)
+    if reduce == "mean":
+        s = out.index_add_(0, index, v)
+        c = torch.zeros(n).index_add_(0, index, torch.ones(v.shape[0])).clamp(1)
+        return s / c[:, None]
+    if reduce == "max":
+        m = torch.full((n, v.shape[1]), float("-inf")).scatter_reduce(
+            0, index[:, None].expand_as(v), v, "amax", include_self=True)
+        return torch.where(torch.isneginf(m), torch.zeros_like(m), m)
+    raise ValueError(reduce)
+
+
+def _type_map(summary, types):
+    """utils.py:6-19 (sum_node_types)."""
+    if summary == "not":
+        return types
+    lut = {"left_right": [0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8],
+           "per_body_part": [0, 0, 0, 0, 0, 1, 1, 2, 3, 2, 3, 4, 5, 4, 5, 4, 5]}[summary]
+    return torch.tensor(lut, dtype=torch.long)[types]
+
+
+def mpn_layer(sd, cfg, x, e, edge_index, node_types):
+    """TypeAwareMPNLayer.forward (layers.py:207-258) / MPLayer.forward (layers.py:63-86)."""
+    p = "mpn_node_cls"
+    j, i = edge_index[0], edge_index[1]                   # message flows j (source) -> i (target)
+    n = x.shape[0]
+    h = F.relu(F.linear(torch.cat([x[i], x[j], e], 1), sd[f"{p}.mlp_edge.0.weight"], sd[f"{p}.mlp_edge.0.bias"]))
+    e_new = F.relu(F.linear(h, sd[f"{p}.mlp_edge.2.weight"], sd[f"{p}.mlp_edge.2.bias"]))
+    if cfg.AGGR_TYPE == "agnostic":
+        m = F.relu(F.linear(torch.cat([x[i], e_new], 1), sd[f"{p}.mlp_node.0.weight"], sd[f"{p}.mlp_node.0.bias"]))
+        agg = _scatter(m, i, n, cfg.AGGR)
+        if getattr(cfg, "USE_NODE_UPDATE_MLP", False):
+            agg = F.relu(F.linear(agg, sd[f"{p}.update_mlp.0.weight"], sd[f"{p}.update_mlp.0.bias"]))
+        return agg, e_new
+    src_type = node_types[j]
+    num_types = _num_types(cfg)
+    m = torch.zeros(e_new.shape[0], e_new.shape[1])
+    xi_e = torch.cat([x[i], e_new], 1)
+    for t in range(17):                                    # layers.py:271 hard-codes 17
+        sel = src_type == t
+        if sel.any():
+            m[sel] = F.relu(F.linear(xi_e[sel], sd[f"{p}.mlp_node.mlp.{t}.0.weight"], sd[f"{p}.mlp_node.mlp.{t}.0.bias"]))
+    upd = torch.zeros(n, num_types, m.shape[1])
+    if cfg.AGGR_SUB in ("node_edge_attn",):
+        a = F.linear(e_new, sd[f"{p}.attn_net.0.weight"], sd[f"{p}.attn_net.0.bias"])[:, 0]
+        for t in range(num_types):
+            sel = src_type == t
+            if sel.any():
+                alpha = _segment_softmax(a[sel], i[sel], n)
+                upd[:, t] = _scatter(m[sel] * alpha[:, None], i[sel], n, "add")
+    else:
+        for t in range(num_types):
+            sel = src_type == t
+            if sel.any():
+                upd[:, t] = _scatter(m[sel], i[sel], n, cfg.AGGR)
+    x_new = F.relu(F.linear(upd.reshape(n, -1), sd[f"{p}.update_mlp.0.weight"], sd[f"{p}.update_mlp.0.bias"]))
+    return x_new, e_new
+
+
+def _num_types(cfg):
+    return {"per_body_part": 6, "left_right": 9}.get(cfg.NODE_TYPE_SUMMARY, cfg.NUM_JOINTS)
+
+
+def mpn_forward(sd, cfg, x, edge_attr, edge_index, node_types):
+    """NodeClassificationMPNSimple.forward (NodeClassificationMPNSimple.py:62-97)."""
+    types = _type_map(cfg.NODE_TYPE_SUMMARY, node_types)
+    nf = _mlp(sd, "node_embedding", x, cfg.NODE_EMB.OUTPUT_SIZES, cfg.NODE_EMB.BN, cfg.NODE_EMB.END_WITH_RELU)
+    ef = _mlp(sd, "edge_embedding", edge_attr, cfg.EDGE_EMB.OUTPUT_SIZES, cfg.EDGE_EMB.BN, cfg.EDGE_EMB.END_WITH_RELU)
+    nf0, ef0 = nf, ef
+    pe, pn, pc = [], [], []
+
+    def heads(v, ev):
+        pn.append(_mlp(sd, "node_classification", v, cfg.NODE_CLASS.OUTPUT_SIZES, cfg.BN).squeeze())
+        pc.append(_mlp(sd, "classification", v, cfg.CLASS.OUTPUT_SIZES, cfg.BN))
+        if ev is not None:
+            pe.append(_mlp(sd, "edge_classification", ev, cfg.EDGE_CLASS.OUTPUT_SIZES, cfg.BN).squeeze())
+
+    aux = getattr(cfg, "AUX_LOSS_STEPS", 0)
+    for it in range(cfg.STEPS):
+        if cfg.SKIP:
+            nf = torch.cat([nf0, nf], 1)
+            ef = torch.cat([ef0, ef], 1)
+        nf, ef = mpn_layer(sd, cfg, nf, ef, edge_index, types)
+        if it >= cfg.STEPS - aux - 1:
+            heads(nf, ef)
+    for _ in range(getattr(cfg, "NODE_STEPS", 0)):
+        raise NotImplementedError("NODE_STEPS > 0")
+    pn.append(_mlp(sd, "node_classification", nf, cfg.NODE_CLASS.OUTPUT_SIZES, cfg.BN).squeeze())
+    pc.append(_mlp(sd, "classification", nf, cfg.CLASS.OUTPUT_SIZES, cfg.BN))
+    return pe, pn, pc, [None]

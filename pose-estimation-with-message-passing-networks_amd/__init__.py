@@ -1,0 +1,21 @@
+"""MI355X-native keypoint-graph hot path of nibox/Pose-Estimation-with-Message-Passing-Networks.
+
+Drop-in for the reference's ``get_graph_constructor(config, **kw).construct_graph()``
+(``src/graph_constructor/__init__.py:4-5``) and ``get_mpn_model(config.MODEL.MPN)``
+(``src/Models/MessagePassingNetwork/__init__.py:27-73``), computed by hand-written gfx950 HIP
+kernels behind the C-ABI library ``csrc/libpemp.so`` (``include/pemp.h``).
+
+Importing the package does not load the HIP library; the first compute call does, and fails
+loudly if it is missing or no HIP device is present.
+"""
+__version__ = "0.1.0"
+
+
+def get_graph_constructor(config, **kwargs):
+    from .graph_constructor import get_graph_constructor as _g
+    return _g(config, **kwargs)
+
+
+def get_mpn_model(config, **kwargs):
+    from .mpn import get_mpn_model as _m
+    return _m(config, **kwargs)

@@ -1,0 +1,119 @@
+"""ctypes binding of ``csrc/libpemp.so`` (C-ABI declared in ``include/pemp.h``).
+
+The product path has no CPU fallback: ``lib()`` raises if the library is missing, was built for
+another ABI, or no gfx950 device is present.
+"""
+import ctypes
+import os
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc", "libpemp.so")
+ABI_VERSION = 1
+
+ERR_INVALID_ARG, ERR_HIP, ERR_WORKSPACE, ERR_UNSUPPORTED = -1, -2, -3, -4
+
+c_i32, c_i64, c_f32, c_sz, c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
+
+
+class PempLayer(ctypes.Structure):
+    _fields_ = [("w", c_p), ("b", c_p), ("in_dim", c_i32), ("out_dim", c_i32), ("relu", c_i32), ("pad_", c_i32)]
+
+
+class PempMlp(ctypes.Structure):
+    _fields_ = [("layer", PempLayer * 4), ("n_layers", c_i32), ("pad_", c_i32)]
+
+
+class PempMpnWeights(ctypes.Structure):
+    _fields_ = [("node_emb", PempMlp), ("edge_emb", PempMlp),
+                ("pre_w", c_p), ("pre_b", c_p), ("q0_w", c_p), ("q0_b", c_p), ("e1_w", c_p),
+                ("e2_w", c_p), ("e2_b", c_p), ("msg_w", c_p), ("attn_w", c_p), ("upd_w", c_p), ("upd_b", c_p),
+                ("edge_head", PempMlp), ("node_head", PempMlp), ("class_head", PempMlp),
+                ("attn_b", c_f32), ("pad_", c_i32)]
+
+
+class PempMpnDesc(ctypes.Structure):
+    _fields_ = [("num_types", c_i32), ("num_joints", c_i32), ("steps", c_i32), ("aux_loss_steps", c_i32),
+                ("aggr", c_i32), ("hidden", c_i32), ("edge_attr_dim", c_i32), ("node_in_dim", c_i32)]
+
+
+# name -> (restype, argtypes); every symbol of include/pemp.h
+SIGNATURES = {
+    "pemp_abi_version": (c_i32, []),
+    "pemp_last_error": (ctypes.c_char_p, []),
+    "pemp_device_check": (c_i32, []),
+    "pemp_detect_workspace_size": (c_sz, [c_i32, c_i32, c_i32, c_i32, c_i32]),
+    "pemp_detect": (c_i32, [c_p, c_p, c_i32, c_i32, c_i32, c_i32, c_i32, c_f32, c_i32, c_i32, c_i32, c_p, c_sz,
+                            c_p, c_p, c_p, c_i32, c_p]),
+    "pemp_pack_nodes": (c_i32, [c_p, c_i32, c_p, c_i32, c_i32, c_i32, c_i32, c_i32, c_p, c_p, c_i32, c_p, c_i64,
+                                c_p, c_p, c_p, c_p, c_p, c_p]),
+    "pemp_fully_graph": (c_i32, [c_p, c_p, c_i32, c_i64, c_p, c_p]),
+    "pemp_knn_workspace_size": (c_sz, [c_p, c_i32]),
+    "pemp_knn_graph_count": (c_i32, [c_p, c_p, c_p, c_i32, c_i32, c_p, c_sz, c_p, c_p]),
+    "pemp_knn_graph_emit": (c_i32, [c_p, c_p, c_i32, c_p, c_i64, c_p, c_sz, c_p, c_p]),
+    "pemp_edge_features": (c_i32, [c_p, c_p, c_i64, c_i32, c_f32, c_i32, c_p, c_p]),
+    "pemp_mpn_workspace_size": (c_sz, [ctypes.POINTER(PempMpnDesc), c_i64, c_i64]),
+    "pemp_mpn_forward": (c_i32, [ctypes.POINTER(PempMpnDesc), ctypes.POINTER(PempMpnWeights), c_p, c_p, c_p, c_p,
+                                 c_i64, c_i64, c_p, c_p, c_p, c_p, c_sz, c_p]),
+}
+
+_LIB = None
+
+
+def load_cdll(path: str = LIB_PATH):
+    """Load and declare the library WITHOUT touching the GPU (used by the CPU symbol test)."""
+    if not os.path.exists(path):
+        raise RuntimeError(f"pemp_amd: {path} is missing - build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype, fn.argtypes = res, args
+    if L.pemp_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"pemp_amd: libpemp ABI {L.pemp_abi_version()} != {ABI_VERSION}")
+    return L
+
+
+def lib():
+    """The HIP library, ready for compute. Raises if no gfx950 HIP device is usable."""
+    global _LIB
+    if _LIB is None:
+        import torch  # torch's HIP runtime must be loaded first: libpemp binds to it by SONAME
+        if not torch.cuda.is_available():
+            raise RuntimeError("pemp_amd: no HIP device available - the HIP path has no CPU fallback")
+        L = load_cdll()
+        torch.cuda.init()
+        check(L.pemp_device_check(), L)
+        _LIB = L
+    return _LIB
+
+
+def check(rc: int, L=None):
+    if rc == 0:
+        return
+    msg = (L or _LIB).pemp_last_error().decode(errors="replace")
+    if rc == ERR_INVALID_ARG:
+        raise ValueError(msg)
+    if rc == ERR_UNSUPPORTED:
+        raise NotImplementedError(msg)
+    raise RuntimeError(f"libpemp error {rc}: {msg}")
+
+
+def ptr(t):
+    return None if t is None else c_p(t.data_ptr())
+
+
+def stream():
+    import torch
+    return c_p(torch.cuda.current_stream().cuda_stream)
+
+
+class Workspace:
+    """Grow-only device scratch owned by the caller side (one per use site)."""
+
+    def __init__(self):
+        self.buf = None
+
+    def get(self, nbytes: int, device):
+        import torch
+        nbytes = max(int(nbytes), 256)
+        if self.buf is None or self.buf.numel() < nbytes or self.buf.device != device:
+            self.buf = torch.empty(nbytes + (nbytes >> 3), dtype=torch.uint8, device=device)
+        return self.buf

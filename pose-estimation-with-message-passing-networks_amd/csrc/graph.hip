@@ -1,0 +1,398 @@
+// Graph construction for gfx950 — restates:
+//   ConstructGraph.py:100-103,262-269  node features x = features[:, y, x].T, joint tags
+//   ConstructGraph.py:206-231          batching (node offsets added to edge_index, cat)
+//   ConstructGraph.py:376-381          fully_connected_mpn_graph: all i != j sorted by (src, dst)
+//   ConstructGraph.py:363-368          knn_mpn_graph: knn_graph(k) -> to_undirected -> no self loops
+//   ConstructGraph.py:289-359          edge_attr = [dx, dy, onehot(type_src) | onehot(type_dst)]
+// All integer outputs are bit-exact; dx/dy are IEEE fp32 divisions of exact integer differences.
+#include <math.h>
+
+#include "pemp_common.h"
+
+namespace pemp {
+namespace {
+
+__device__ __forceinline__ int find_segment(const int64_t* off, int n, int64_t v) {
+  // largest b in [0, n) with off[b] <= v  (off non-decreasing, off[0] = 0)
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= v) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void pack_nodes_kernel(
+    const float* __restrict__ feat, int C, const float* __restrict__ tags, int F, int B, int J, int H, int W,
+    const int64_t* __restrict__ det, const float* __restrict__ det_sc, int cap, const int64_t* __restrict__ node_off,
+    int64_t n_total, float* __restrict__ x, int64_t* __restrict__ jdet, float* __restrict__ jsc,
+    int64_t* __restrict__ bidx, float* __restrict__ jtag) {
+  const int64_t total = n_total * C;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t g = idx / C;
+    const int c = (int)(idx - g * C);
+    const int b = find_segment(node_off, B, g);
+    const int64_t i = g - node_off[b];
+    const int64_t* d = det + ((size_t)b * cap + i) * 3;
+    const int64_t px = d[0], py = d[1], pt = d[2];
+    x[idx] = feat[(((size_t)b * C + c) * H + py) * W + px];
+    if (c == 0) {
+      jdet[g * 3 + 0] = px; jdet[g * 3 + 1] = py; jdet[g * 3 + 2] = pt;
+      jsc[g] = det_sc[(size_t)b * cap + i];
+      bidx[g] = b;
+    }
+    if (tags && c < F) jtag[g * F + c] = tags[((((size_t)b * J + pt) * H + py) * W + px) * F + c];
+  }
+}
+
+__global__ __launch_bounds__(256) void fully_graph_kernel(const int64_t* __restrict__ node_off,
+                                                          const int64_t* __restrict__ edge_off, int B,
+                                                          int64_t e_total, int64_t* __restrict__ ei) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < e_total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int b = find_segment(edge_off, B, e);
+    const int64_t n = node_off[b + 1] - node_off[b];
+    const int64_t el = e - edge_off[b];
+    const int64_t i = el / (n - 1), r = el - i * (n - 1);
+    const int64_t j = r < i ? r : r + 1;
+    ei[e] = node_off[b] + i;
+    ei[e_total + e] = node_off[b] + j;
+  }
+}
+
+__global__ __launch_bounds__(256) void edge_features_kernel(const int64_t* __restrict__ jdet,
+                                                            const int64_t* __restrict__ ei, int64_t E, int J,
+                                                            float norm, int mode, int A, float* __restrict__ out) {
+  const int64_t total = E * A;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = idx / A;
+    const int f = (int)(idx - e * A);
+    const int64_t s = ei[e], d = ei[E + e];
+    float v = 0.0f;
+    int oh = -1;   // one-hot column index, or -1
+    switch (mode) {
+      case PEMP_EF_POSITION_CONNECTION:
+        if (f == 0) v = (float)(jdet[d * 3 + 0] - jdet[s * 3 + 0]) / norm;
+        else if (f == 1) v = (float)(jdet[d * 3 + 1] - jdet[s * 3 + 1]) / norm;
+        else oh = f - 2;
+        break;
+      case PEMP_EF_CONNECTION: oh = f; break;
+      case PEMP_EF_NOTHING: v = 0.0f; break;
+      case PEMP_EF_POSITION:
+        v = (float)(jdet[d * 3 + f] - jdet[s * 3 + f]) / norm;
+        break;
+      case PEMP_EF_POSITION_ANGLE_CONNECTION:
+        if (f < 2) v = (float)(jdet[d * 3 + f] - jdet[s * 3 + f]) / norm;
+        else if (f == 2) {
+          const float ax = (float)(jdet[s * 3 + 0] - jdet[d * 3 + 0]);
+          const float ay = (float)(jdet[s * 3 + 1] - jdet[d * 3 + 1]);
+          const float th = fabsf(acosf(ax * (1.0f / sqrtf(ax * ax + ay * ay))));
+          v = isnan(th) ? 0.0f : th;
+        } else oh = f - 3;
+        break;
+    }
+    if (oh >= 0) v = (jdet[s * 3 + 2] == oh || jdet[d * 3 + 2] == oh) ? 1.0f : 0.0f;
+    out[idx] = v;
+  }
+}
+
+// ---- knn ----
+struct KnnWs {
+  unsigned long long* adj;   // per image: n_b rows x words_b  (A: j among i's nearest)
+  unsigned long long* adjt;  // transpose                      (T[j][i] = A[i][j])
+  int64_t* mat_off;          // [B+1] word offsets (device copy)
+};
+
+static size_t knn_words(const int64_t* node_off_host, int B, int64_t* mat_off_host) {
+  size_t w = 0;
+  for (int b = 0; b < B; ++b) {
+    if (mat_off_host) mat_off_host[b] = (int64_t)w;
+    const int64_t n = node_off_host[b + 1] - node_off_host[b];
+    w += (size_t)n * ((n + 63) / 64);
+  }
+  if (mat_off_host) mat_off_host[B] = (int64_t)w;
+  return w;
+}
+
+static KnnWs knn_carve(void* base, const int64_t* node_off_host, int B, size_t* bytes) {
+  Carver c(base);
+  const size_t w = knn_words(node_off_host, B, nullptr);
+  KnnWs k;
+  k.adj = c.take<unsigned long long>(w);
+  k.adjt = c.take<unsigned long long>(w);
+  k.mat_off = c.take<int64_t>(B + 1);
+  if (bytes) *bytes = c.used;
+  return k;
+}
+
+// One wave per query node i: the k+1 nearest (squared distance, then index), self dropped.
+__global__ __launch_bounds__(256) void knn_adj_kernel(const int64_t* __restrict__ jdet,
+                                                      const int64_t* __restrict__ node_off, int B, int64_t n_total,
+                                                      int kq, const int64_t* __restrict__ mat_off,
+                                                      unsigned long long* __restrict__ adj,
+                                                      unsigned long long* __restrict__ adjt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= n_total) return;
+  const int b = find_segment(node_off, B, g);
+  const int64_t base = node_off[b];
+  const int n = (int)(node_off[b + 1] - base);
+  const int i = (int)(g - base);
+  const int wpr = (n + 63) / 64;
+  unsigned long long* A = adj + mat_off[b];
+  unsigned long long* T = adjt + mat_off[b];
+  const int64_t xi = jdet[g * 3 + 0], yi = jdet[g * 3 + 1];
+  auto d2 = [&](int j) -> int64_t {
+    const int64_t dx = jdet[(base + j) * 3 + 0] - xi, dy = jdet[(base + j) * 3 + 1] - yi;
+    return dx * dx + dy * dy;
+  };
+  const int chunk = (n + 63) / 64;
+  const int j0 = lane * chunk, j1 = min(n, j0 + chunk);
+  if (n <= kq) {   // every node is among the k+1 nearest
+    for (int j = j0; j < j1; ++j) {
+      if (j == i) continue;
+      atomicOr(&A[(size_t)i * wpr + j / 64], 1ull << (j & 63));
+      atomicOr(&T[(size_t)j * wpr + i / 64], 1ull << (i & 63));
+    }
+    return;
+  }
+  // smallest tau with #{d2 <= tau} >= kq (binary search over the integer distance)
+  int64_t lo = 0, hi = 0;
+  for (int j = j0; j < j1; ++j) hi = max(hi, d2(j));
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) hi = max(hi, (int64_t)__shfl_xor((long long)hi, off));
+  while (lo < hi) {
+    const int64_t mid = lo + (hi - lo) / 2;
+    int c = 0;
+    for (int j = j0; j < j1; ++j) c += d2(j) <= mid;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off);
+    if (c >= kq) hi = mid; else lo = mid + 1;
+  }
+  const int64_t tau = lo;
+  int less = 0, ties = 0;
+  for (int j = j0; j < j1; ++j) { const int64_t d = d2(j); less += d < tau; ties += d == tau; }
+  int less_all = less;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) less_all += __shfl_xor(less_all, off);
+  int tie_pre = ties;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(tie_pre, off);
+    if (lane >= off) tie_pre += o;
+  }
+  int tie_rank = tie_pre - ties;   // ties in lower-index lanes
+  const int need = kq - less_all;  // ties admitted, lowest index first
+  for (int j = j0; j < j1; ++j) {
+    const int64_t d = d2(j);
+    bool take = d < tau;
+    if (d == tau) { take = tie_rank < need; ++tie_rank; }
+    if (take && j != i) {
+      atomicOr(&A[(size_t)i * wpr + j / 64], 1ull << (j & 63));
+      atomicOr(&T[(size_t)j * wpr + i / 64], 1ull << (i & 63));
+    }
+  }
+}
+
+__global__ void knn_matoff_kernel(const int64_t* __restrict__ node_off, int B, int64_t* __restrict__ mat_off) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int64_t w = 0;
+  for (int b = 0; b < B; ++b) {
+    mat_off[b] = w;
+    const int64_t n = node_off[b + 1] - node_off[b];
+    w += n * ((n + 63) / 64);
+  }
+  mat_off[B] = w;
+}
+
+__device__ __forceinline__ int row_degree(const unsigned long long* A, const unsigned long long* T, int a, int wpr) {
+  int c = 0;
+  for (int w = 0; w < wpr; ++w) c += __popcll(A[(size_t)a * wpr + w] | T[(size_t)a * wpr + w]);
+  return c;
+}
+
+__global__ __launch_bounds__(256) void knn_count_kernel(const int64_t* __restrict__ node_off, int B,
+                                                        const int64_t* __restrict__ mat_off,
+                                                        const unsigned long long* __restrict__ adj,
+                                                        const unsigned long long* __restrict__ adjt,
+                                                        int64_t* __restrict__ edge_count) {
+  const int b = blockIdx.x;
+  const int n = (int)(node_off[b + 1] - node_off[b]);
+  const int wpr = (n + 63) / 64;
+  __shared__ int64_t sh[4];
+  int64_t c = 0;
+  for (int a = threadIdx.x; a < n; a += blockDim.x) c += row_degree(adj + mat_off[b], adjt + mat_off[b], a, wpr);
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor((long long)c, off);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) edge_count[b] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+__global__ __launch_bounds__(1024) void knn_emit_kernel(const int64_t* __restrict__ node_off, int B,
+                                                        const int64_t* __restrict__ mat_off,
+                                                        const unsigned long long* __restrict__ adj,
+                                                        const unsigned long long* __restrict__ adjt,
+                                                        const int64_t* __restrict__ edge_off, int64_t e_total,
+                                                        int64_t* __restrict__ ei) {
+  const int b = blockIdx.x;
+  const int64_t base = node_off[b];
+  const int n = (int)(node_off[b + 1] - base);
+  const int wpr = (n + 63) / 64;
+  const unsigned long long* A = adj + mat_off[b];
+  const unsigned long long* T = adjt + mat_off[b];
+  __shared__ int64_t carry;
+  __shared__ int64_t wsum[16];
+  if (threadIdx.x == 0) carry = edge_off[b];
+  __syncthreads();
+  for (int a0 = 0; a0 < n; a0 += 1024) {
+    const int a = a0 + threadIdx.x;
+    const int deg = a < n ? row_degree(A, T, a, wpr) : 0;
+    int64_t x = deg;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int64_t o = __shfl_up((long long)x, off);
+      if (lane >= off) x += o;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    int64_t pre = carry;
+    for (int w = 0; w < wave; ++w) pre += wsum[w];
+    pre += x - deg;
+    if (a < n) {
+      int64_t pos = pre;
+      for (int w = 0; w < wpr; ++w) {
+        unsigned long long word = A[(size_t)a * wpr + w] | T[(size_t)a * wpr + w];
+        while (word) {
+          const int bit = __ffsll((long long)word) - 1;
+          word &= word - 1;
+          ei[pos] = base + a;
+          ei[e_total + pos] = base + w * 64 + bit;
+          ++pos;
+        }
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int64_t s = 0;
+      for (int w = 0; w < 16; ++w) s += wsum[w];
+      carry += s;
+    }
+    __syncthreads();
+  }
+}
+
+static int grid_for(int64_t total, int block, int cap_blocks = 65536) {
+  int64_t g = (total + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap_blocks) g = cap_blocks;
+  return (int)g;
+}
+
+}  // namespace
+}  // namespace pemp
+
+using namespace pemp;
+
+extern "C" int pemp_pack_nodes(const float* features, int C, const float* tagmaps, int F, int B, int J, int H, int W,
+                               const int64_t* det_xyt, const float* det_scores, int cap, const int64_t* node_off,
+                               int64_t n_total, float* x, int64_t* joint_det, float* joint_scores,
+                               int64_t* batch_index, float* joint_tags, void* stream) {
+  PEMP_CHECK_ARG(features && det_xyt && det_scores && node_off && x && joint_det && joint_scores && batch_index,
+                 "pemp_pack_nodes: null pointer");
+  PEMP_CHECK_ARG(C > 0 && B > 0 && J > 0 && H > 0 && W > 0 && n_total >= 0, "pemp_pack_nodes: bad shape");
+  PEMP_CHECK_ARG(!tagmaps || (joint_tags && F > 0 && F <= C), "pemp_pack_nodes: tags need F in [1, C]");
+  if (n_total == 0) return PEMP_OK;
+  hipLaunchKernelGGL(pack_nodes_kernel, dim3(grid_for(n_total * C, 256)), dim3(256), 0, as_stream(stream), features,
+                     C, tagmaps, F, B, J, H, W, det_xyt, det_scores, cap, node_off, n_total, x, joint_det,
+                     joint_scores, batch_index, joint_tags);
+  PEMP_LAUNCH_CHECK();
+  return PEMP_OK;
+}
+
+extern "C" int pemp_fully_graph(const int64_t* node_off, const int64_t* edge_off, int B, int64_t e_total,
+                                int64_t* edge_index, void* stream) {
+  PEMP_CHECK_ARG(node_off && edge_off && edge_index && B > 0 && e_total >= 0, "pemp_fully_graph: bad args");
+  if (e_total == 0) return PEMP_OK;
+  hipLaunchKernelGGL(fully_graph_kernel, dim3(grid_for(e_total, 256)), dim3(256), 0, as_stream(stream), node_off,
+                     edge_off, B, e_total, edge_index);
+  PEMP_LAUNCH_CHECK();
+  return PEMP_OK;
+}
+
+extern "C" int pemp_edge_features(const int64_t* joint_det, const int64_t* edge_index, int64_t e_total, int J,
+                                  float norm_factor, int mode, float* edge_attr, void* stream) {
+  PEMP_CHECK_ARG(joint_det && edge_index && edge_attr && J > 0 && e_total >= 0, "pemp_edge_features: bad args");
+  int A;
+  switch (mode) {
+    case PEMP_EF_POSITION_CONNECTION: A = J + 2; break;
+    case PEMP_EF_CONNECTION: A = J; break;
+    case PEMP_EF_NOTHING: A = 1; break;
+    case PEMP_EF_POSITION: A = 2; break;
+    case PEMP_EF_POSITION_ANGLE_CONNECTION: A = J + 3; break;
+    default: set_error("pemp_edge_features: unknown mode %d", mode); return PEMP_ERR_INVALID_ARG;
+  }
+  if (e_total == 0) return PEMP_OK;
+  hipLaunchKernelGGL(edge_features_kernel, dim3(grid_for(e_total * A, 256)), dim3(256), 0, as_stream(stream),
+                     joint_det, edge_index, e_total, J, norm_factor, mode, A, edge_attr);
+  PEMP_LAUNCH_CHECK();
+  return PEMP_OK;
+}
+
+extern "C" size_t pemp_knn_workspace_size(const int64_t* node_off_host, int B) {
+  if (!node_off_host || B <= 0) return 0;
+  size_t bytes = 0;
+  knn_carve(nullptr, node_off_host, B, &bytes);
+  return bytes;
+}
+
+extern "C" int pemp_knn_graph_count(const int64_t* joint_det, const int64_t* node_off, const int64_t* node_off_host,
+                                    int B, int k, void* workspace, size_t workspace_bytes, int64_t* edge_count,
+                                    void* stream) {
+  PEMP_CHECK_ARG(joint_det && node_off && node_off_host && workspace && edge_count && B > 0 && k >= 1,
+                 "pemp_knn_graph_count: bad args");
+  size_t need = 0;
+  knn_carve(nullptr, node_off_host, B, &need);
+  if (workspace_bytes < need) {
+    set_error("pemp_knn_graph_count: workspace %zu < %zu", workspace_bytes, need);
+    return PEMP_ERR_WORKSPACE;
+  }
+  const KnnWs w = knn_carve(workspace, node_off_host, B, nullptr);
+  const hipStream_t st = as_stream(stream);
+  const size_t words = knn_words(node_off_host, B, nullptr);
+  hipLaunchKernelGGL(knn_matoff_kernel, dim3(1), dim3(64), 0, st, node_off, B, w.mat_off);
+  PEMP_LAUNCH_CHECK();
+  PEMP_HIP(hipMemsetAsync(w.adj, 0, words * sizeof(unsigned long long), st));
+  PEMP_HIP(hipMemsetAsync(w.adjt, 0, words * sizeof(unsigned long long), st));
+  const int64_t n_total = node_off_host[B];
+  if (n_total > 0) {
+    hipLaunchKernelGGL(knn_adj_kernel, dim3((unsigned)((n_total + 3) / 4)), dim3(256), 0, st, joint_det, node_off, B,
+                       n_total, k + 1, w.mat_off, w.adj, w.adjt);
+    PEMP_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(knn_count_kernel, dim3(B), dim3(256), 0, st, node_off, B, w.mat_off, w.adj, w.adjt, edge_count);
+  PEMP_LAUNCH_CHECK();
+  return PEMP_OK;
+}
+
+extern "C" int pemp_knn_graph_emit(const int64_t* node_off, const int64_t* node_off_host, int B,
+                                   const int64_t* edge_off, int64_t e_total, void* workspace,
+                                   size_t workspace_bytes, int64_t* edge_index, void* stream) {
+  PEMP_CHECK_ARG(node_off && node_off_host && edge_off && workspace && edge_index && B > 0 && e_total >= 0,
+                 "pemp_knn_graph_emit: bad args");
+  size_t need = 0;
+  knn_carve(nullptr, node_off_host, B, &need);
+  if (workspace_bytes < need) {
+    set_error("pemp_knn_graph_emit: workspace %zu < %zu", workspace_bytes, need);
+    return PEMP_ERR_WORKSPACE;
+  }
+  const KnnWs w = knn_carve(workspace, node_off_host, B, nullptr);
+  if (e_total == 0) return PEMP_OK;
+  hipLaunchKernelGGL(knn_emit_kernel, dim3(B), dim3(1024), 0, as_stream(stream), node_off, B, w.mat_off, w.adj,
+                     w.adjt, edge_off, e_total, edge_index);
+  PEMP_LAUNCH_CHECK();
+  return PEMP_OK;
+}

@@ -1,0 +1,814 @@
+// Message-passing network, inference, for gfx950 — restates
+//   NodeClassificationMPNSimple.py:62-97  embeddings, STEPS iterations with skip concat, heads
+//   layers.py:157-258 TypeAwareMPNLayer (per-source-type messages, attention softmax per
+//                     (target, source type) segment, update_mlp)
+//   layers.py:32-86   MPLayer (single message MLP, scatter max/mean/add)
+//   torch_scatter 2.0.4 scatter_softmax (exp(a - max) / (sum + 1e-12)), scatter sum/mean/max
+//                     (empty segments -> 0).
+//
+// Layout (all fp32, hidden width 64). Edges are re-ordered once per call into type-major order
+// (source type t, target i, original edge id) so that every (i, t) aggregation segment is
+// contiguous and every 16-edge MFMA tile shares one message weight W_t. Per iteration:
+//   rows_linear_kernel : node table NT[n] = [W1_xi·x | W1_xj·x | W_t_xi·x + b_t (t < T)], x = [x0 | x]
+//   edge_step_kernel   : per 16-edge wave tile, three chained 64x64 MFMA GEMMs (edge MLP layer 1 on
+//                        e_cur, layer 2, message), attention logit, segmented online softmax, and
+//                        (recorded iterations) the fused edge-classification head. No atomics.
+//   node_update_kernel : x_new = ReLU(U·agg + b) (split over types, fixed-order reduction).
+// MFMA: v_mfma_f32_16x16x4_f32 (exact fp32). Fragment convention per wave: item (edge or node)
+// c = lane & 15 on the MFMA N dimension, features 16*blk + 4*(lane >> 4) + r in registers, so one
+// layer's accumulator is the next layer's B operand with no data movement.
+#include <math.h>
+
+#include "pemp_common.h"
+
+namespace pemp {
+namespace {
+
+constexpr int D = 64;
+constexpr int ITEM = 64;    // edges per wave work item
+constexpr int LDW = 72;     // LDS row stride of a 64x64 weight tile (conflict-free ds_read_b128)
+constexpr int MAXT = 17;
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float a, float b, float c, float d) {
+  *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
+}
+
+// acc[ob] += W[16ob + i][.] · in   (W row-major, row stride ldw; KB input / OB output blocks of 16)
+template <int KB, int OB>
+__device__ __forceinline__ void gemm_frag(const float* __restrict__ W, int ldw, const float (&in)[KB][4],
+                                          float (&acc)[OB][4]) {
+  const int lane = __lane_id(), i = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int ob = 0; ob < OB; ++ob) {
+    f32x4 c = {acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]};
+#pragma unroll
+    for (int mb = 0; mb < KB; ++mb) {
+      const float4 w = ld4(W + (16 * ob + i) * ldw + 16 * mb + 4 * g);
+      c = mfma4(w.x, in[mb][0], c);
+      c = mfma4(w.y, in[mb][1], c);
+      c = mfma4(w.z, in[mb][2], c);
+      c = mfma4(w.w, in[mb][3], c);
+    }
+    acc[ob][0] = c[0]; acc[ob][1] = c[1]; acc[ob][2] = c[2]; acc[ob][3] = c[3];
+  }
+}
+
+template <int NB>
+__device__ __forceinline__ void relu_frag(float (&v)[NB][4]) {
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[b][r] = fmaxf(v[b][r], 0.0f);
+}
+
+// One Linear (+ReLU) of a pemp_mlp with runtime dims <= 16*MAXB, weights from global memory.
+template <int MAXKB, int MAXOB>
+__device__ __forceinline__ void layer_rt(const pemp_layer& L, const float (&in)[MAXKB][4], float (&out)[MAXOB][4]) {
+  const int lane = __lane_id(), i = lane & 15, g = lane >> 4;
+  const int KB = (L.in_dim + 15) >> 4, OB = (L.out_dim + 15) >> 4, ldw = KB * 16;
+#pragma unroll
+  for (int ob = 0; ob < MAXOB; ++ob) {
+    f32x4 c = {0.f, 0.f, 0.f, 0.f};
+    if (ob < OB) {
+      const float4 bb = ld4(L.b + 16 * ob + 4 * g);
+      c[0] = bb.x; c[1] = bb.y; c[2] = bb.z; c[3] = bb.w;
+#pragma unroll
+      for (int mb = 0; mb < MAXKB; ++mb) {
+        if (mb < KB) {
+          const float4 w = ld4(L.w + (16 * ob + i) * ldw + 16 * mb + 4 * g);
+          c = mfma4(w.x, in[mb][0], c);
+          c = mfma4(w.y, in[mb][1], c);
+          c = mfma4(w.z, in[mb][2], c);
+          c = mfma4(w.w, in[mb][3], c);
+        }
+      }
+      if (L.relu) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) c[r] = fmaxf(c[r], 0.0f);
+      }
+    }
+    out[ob][0] = c[0]; out[ob][1] = c[1]; out[ob][2] = c[2]; out[ob][3] = c[3];
+  }
+}
+
+// Whole pemp_mlp on fragments (<= 4 layers, widths <= 16*MAXB). Result in `a`.
+template <int MAXB>
+__device__ __forceinline__ void mlp_frag(const pemp_mlp& m, float (&a)[MAXB][4], float (&b)[MAXB][4]) {
+  layer_rt<MAXB, MAXB>(m.layer[0], a, b);
+  if (m.n_layers > 1) layer_rt<MAXB, MAXB>(m.layer[1], b, a);
+  if (m.n_layers > 2) layer_rt<MAXB, MAXB>(m.layer[2], a, b);
+  if (m.n_layers > 3) layer_rt<MAXB, MAXB>(m.layer[3], b, a);
+  if (m.n_layers == 1 || m.n_layers == 3) {
+#pragma unroll
+    for (int x = 0; x < MAXB; ++x)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a[x][r] = b[x][r];
+  }
+}
+
+// ---- segmented scans across the 16 items of a wave tile (lanes c = lane & 15) ----
+struct SegMask {
+  bool f1, f2, f4, f8, b1, b2, b4, b8;
+};
+
+__device__ __forceinline__ SegMask seg_mask(int seg, int c) {
+  SegMask m;
+  m.f1 = c >= 1 && __shfl_up(seg, 1, 16) == seg;
+  m.f2 = c >= 2 && __shfl_up(seg, 2, 16) == seg;
+  m.f4 = c >= 4 && __shfl_up(seg, 4, 16) == seg;
+  m.f8 = c >= 8 && __shfl_up(seg, 8, 16) == seg;
+  m.b1 = c + 1 < 16 && __shfl_down(seg, 1, 16) == seg;
+  m.b2 = c + 2 < 16 && __shfl_down(seg, 2, 16) == seg;
+  m.b4 = c + 4 < 16 && __shfl_down(seg, 4, 16) == seg;
+  m.b8 = c + 8 < 16 && __shfl_down(seg, 8, 16) == seg;
+  return m;
+}
+
+__device__ __forceinline__ float scan_add(float v, const SegMask& m) {
+  float o;
+  o = __shfl_up(v, 1, 16); if (m.f1) v += o;
+  o = __shfl_up(v, 2, 16); if (m.f2) v += o;
+  o = __shfl_up(v, 4, 16); if (m.f4) v += o;
+  o = __shfl_up(v, 8, 16); if (m.f8) v += o;
+  return v;
+}
+
+__device__ __forceinline__ float scan_max(float v, const SegMask& m) {
+  float o;
+  o = __shfl_up(v, 1, 16); if (m.f1) v = fmaxf(v, o);
+  o = __shfl_up(v, 2, 16); if (m.f2) v = fmaxf(v, o);
+  o = __shfl_up(v, 4, 16); if (m.f4) v = fmaxf(v, o);
+  o = __shfl_up(v, 8, 16); if (m.f8) v = fmaxf(v, o);
+  return v;
+}
+
+__device__ __forceinline__ float scan_max_bwd(float v, const SegMask& m) {
+  float o;
+  o = __shfl_down(v, 1, 16); if (m.b1) v = fmaxf(v, o);
+  o = __shfl_down(v, 2, 16); if (m.b2) v = fmaxf(v, o);
+  o = __shfl_down(v, 4, 16); if (m.b4) v = fmaxf(v, o);
+  o = __shfl_down(v, 8, 16); if (m.b8) v = fmaxf(v, o);
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Workspace
+// ---------------------------------------------------------------------------------------------
+struct MpnWs {
+  int *cnt, *seg, *cursor, *wg_start, *perm, *s_src, *s_dst, *s_orig, *err;
+  float *X, *NT, *agg, *Q0, *EA, *EB;
+};
+
+static MpnWs mpn_carve(void* base, int T, int64_t N, int64_t E, size_t* bytes) {
+  Carver c(base);
+  MpnWs w;
+  const int64_t K = (int64_t)T * N;
+  w.cnt = c.take<int>(K + 1);
+  w.cursor = c.take<int>(K + 1);
+  w.err = c.take<int>(4);
+  w.seg = c.take<int>(K + 1);
+  w.wg_start = c.take<int>(MAXT + 2);
+  w.perm = c.take<int>(E);
+  w.s_src = c.take<int>(E);
+  w.s_dst = c.take<int>(E);
+  w.s_orig = c.take<int>(E);
+  w.X = c.take<float>(N * 128);
+  w.NT = c.take<float>(N * (128 + 64 * (int64_t)T));
+  w.agg = c.take<float>(N * T * D);
+  w.Q0 = c.take<float>(E * D);
+  w.EA = c.take<float>(E * D);
+  w.EB = c.take<float>(E * D);
+  if (bytes) *bytes = c.used;
+  return w;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Prepare: type-major counting sort of the edges (deterministic: ties kept in edge-id order)
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void mpn_count_kernel(const int64_t* __restrict__ ei, const int64_t* __restrict__ types,
+                                                        int64_t N, int64_t E, int T, int* __restrict__ cnt,
+                                                        int* __restrict__ err) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = ei[e], d = ei[E + e];
+    if (s < 0 || s >= N || d < 0 || d >= N) { atomicOr(err, 1); continue; }
+    const int64_t t = types[s];
+    if (t < 0 || t >= T) { atomicOr(err, 2); continue; }
+    atomicAdd(&cnt[t * N + d], 1);
+  }
+}
+
+__global__ __launch_bounds__(1024) void mpn_scan_kernel(const int* __restrict__ cnt, int64_t K, int64_t N, int T,
+                                                        int* __restrict__ seg, int* __restrict__ wg_start) {
+  __shared__ int sh[40];
+  const int per = (int)((K + 1023) / 1024);
+  const int64_t k0 = (int64_t)threadIdx.x * per;
+  int local = 0;
+  for (int k = 0; k < per; ++k)
+    if (k0 + k < K) local += cnt[k0 + k];
+  // block exclusive scan
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int x = local;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(x, off);
+    if (lane >= off) x += o;
+  }
+  if (lane == 63) sh[wave] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int run = 0;
+    for (int w = 0; w < 16; ++w) { const int v = sh[w]; sh[w] = run; run += v; }
+    sh[16] = run;
+  }
+  __syncthreads();
+  int run = sh[wave] + x - local;
+  for (int k = 0; k < per; ++k)
+    if (k0 + k < K) { seg[k0 + k] = run; run += cnt[k0 + k]; }
+  if (threadIdx.x == 0) seg[K] = sh[16];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    wg_start[0] = 0;
+    for (int t = 0; t < T; ++t) {
+      const int et = seg[(t + 1) * N] - seg[t * N];
+      const int items = (et + ITEM - 1) / ITEM;
+      acc += (items + 3) / 4;
+      wg_start[t + 1] = acc;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void mpn_scatter_kernel(const int64_t* __restrict__ ei, const int64_t* __restrict__ types,
+                                                          int64_t N, int64_t E, const int* __restrict__ seg,
+                                                          int* __restrict__ cursor, int* __restrict__ perm) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = ei[e], d = ei[E + e];
+    if (s < 0 || s >= N || d < 0 || d >= N) continue;
+    const int64_t key = types[s] * N + d;
+    perm[seg[key] + atomicAdd(&cursor[key], 1)] = (int)e;
+  }
+}
+
+// One wave per (type, target) key: order the key's edges by original id (rank by counting).
+__global__ __launch_bounds__(256) void mpn_segsort_kernel(const int64_t* __restrict__ ei, int64_t E, int64_t K,
+                                                          const int* __restrict__ seg, const int* __restrict__ perm,
+                                                          int* __restrict__ s_src, int* __restrict__ s_dst,
+                                                          int* __restrict__ s_orig) {
+  const int lane = threadIdx.x & 63;
+  const int64_t key = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (key >= K) return;
+  const int s0 = seg[key], n = seg[key + 1] - s0;
+  for (int a = lane; a < n; a += 64) {
+    const int v = perm[s0 + a];
+    int rank = 0;
+    for (int j = 0; j < n; ++j) rank += perm[s0 + j] < v;
+    const int pos = s0 + rank;
+    s_orig[pos] = v;
+    s_src[pos] = (int)ei[v];
+    s_dst[pos] = (int)ei[E + v];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Row MLPs (node embedding, node/class heads): 16 rows per workgroup, 4 waves split outputs.
+// ---------------------------------------------------------------------------------------------
+constexpr int RS = 136;  // LDS row stride (<= 128 features), = 8 mod 64 dwords: conflict-free b128
+
+struct RowsMlpArgs {
+  pemp_mlp mlp;
+  const float* in;
+  int64_t ld_in, M;
+  float* out;
+  int64_t ld_out;
+  float* out2;
+  int64_t ld_out2;
+};
+
+__global__ __launch_bounds__(256) void rows_mlp_kernel(RowsMlpArgs a) {
+  __shared__ __attribute__((aligned(16))) float act[2][16 * RS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, i = lane & 15, g = lane >> 4;
+  const int64_t row0 = (int64_t)blockIdx.x * 16;
+  const int K0 = a.mlp.layer[0].in_dim, KP = (K0 + 15) & ~15;
+  for (int idx = threadIdx.x; idx < 16 * KP; idx += 256) {
+    const int r = idx / KP, k = idx - r * KP;
+    act[0][r * RS + k] = (row0 + r < a.M && k < K0) ? a.in[(row0 + r) * a.ld_in + k] : 0.0f;
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int l = 0; l < a.mlp.n_layers; ++l) {
+    const pemp_layer& L = a.mlp.layer[l];
+    const int KB = (L.in_dim + 15) >> 4, OB = (L.out_dim + 15) >> 4, ldw = KB * 16;
+    for (int ob = wave; ob < OB; ob += 4) {
+      const float4 bb = ld4(L.b + 16 * ob + 4 * g);
+      f32x4 c = {bb.x, bb.y, bb.z, bb.w};
+      for (int mb = 0; mb < KB; ++mb) {
+        const float4 w = ld4(L.w + (16 * ob + i) * ldw + 16 * mb + 4 * g);
+        const float4 x = ld4(&act[cur][i * RS + 16 * mb + 4 * g]);
+        c = mfma4(w.x, x.x, c);
+        c = mfma4(w.y, x.y, c);
+        c = mfma4(w.z, x.z, c);
+        c = mfma4(w.w, x.w, c);
+      }
+      if (L.relu) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) c[r] = fmaxf(c[r], 0.0f);
+      }
+      st4(&act[cur ^ 1][i * RS + 16 * ob + 4 * g], c[0], c[1], c[2], c[3]);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  const int OD = a.mlp.layer[a.mlp.n_layers - 1].out_dim;
+  for (int idx = threadIdx.x; idx < 16 * OD; idx += 256) {
+    const int r = idx / OD, f = idx - r * OD;
+    if (row0 + r < a.M) {
+      const float v = act[cur][r * RS + f];
+      a.out[(row0 + r) * a.ld_out + f] = v;
+      if (a.out2) a.out2[(row0 + r) * a.ld_out2 + f] = v;
+    }
+  }
+}
+
+// Y[M, NO] = X[M, 128] · W^T + b  (node precompute); grid (M/16, NO/64), wave = 16 output columns.
+__global__ __launch_bounds__(256) void rows_linear_kernel(const float* __restrict__ X, int64_t M,
+                                                          const float* __restrict__ W, const float* __restrict__ b,
+                                                          int NO, float* __restrict__ Y) {
+  __shared__ __attribute__((aligned(16))) float xs[16 * RS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, i = lane & 15, g = lane >> 4;
+  const int64_t row0 = (int64_t)blockIdx.x * 16;
+  for (int idx = threadIdx.x; idx < 16 * 32; idx += 256) {
+    const int r = idx >> 5, k4 = (idx & 31) * 4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (row0 + r < M) v = ld4(X + (row0 + r) * 128 + k4);
+    *reinterpret_cast<float4*>(&xs[r * RS + k4]) = v;
+  }
+  __syncthreads();
+  const int ob = blockIdx.y * 4 + wave;
+  if (16 * ob >= NO) return;
+  const float4 bb = ld4(b + 16 * ob + 4 * g);
+  f32x4 c = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+  for (int mb = 0; mb < 8; ++mb) {
+    const float4 w = ld4(W + (int64_t)(16 * ob + i) * 128 + 16 * mb + 4 * g);
+    const float4 x = ld4(&xs[i * RS + 16 * mb + 4 * g]);
+    c = mfma4(w.x, x.x, c);
+    c = mfma4(w.y, x.y, c);
+    c = mfma4(w.z, x.z, c);
+    c = mfma4(w.w, x.w, c);
+  }
+  // C layout: lane holds Y[row i][16 ob + 4 g + r]
+  if (row0 + i < M) st4(Y + (row0 + i) * NO + 16 * ob + 4 * g, c[0], c[1], c[2], c[3]);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Edge embedding (sorted order): e_init = MLP(edge_attr[orig]); Q0 = W1_e_init·e_init + b1.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void edge_embed_kernel(pemp_mlp emb, const float* __restrict__ ea, int A,
+                                                         const int* __restrict__ s_orig, int64_t E,
+                                                         const float* __restrict__ q0_w,
+                                                         const float* __restrict__ q0_b, float* __restrict__ e0,
+                                                         float* __restrict__ q0) {
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int64_t p = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + c;
+  const bool valid = p < E;
+  const int64_t o = valid ? s_orig[p] : 0;
+  float a[8][4], b[8][4];
+#pragma unroll
+  for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int f = 16 * mb + 4 * g + r;
+      a[mb][r] = (valid && f < A) ? ea[o * A + f] : 0.0f;
+    }
+  mlp_frag<8>(emb, a, b);
+  float e[4][4], acc[4][4];
+#pragma unroll
+  for (int ob = 0; ob < 4; ++ob) {
+    const float4 bb = ld4(q0_b + 16 * ob + 4 * g);
+    acc[ob][0] = bb.x; acc[ob][1] = bb.y; acc[ob][2] = bb.z; acc[ob][3] = bb.w;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) e[ob][r] = a[ob][r];
+  }
+  gemm_frag<4, 4>(q0_w, 64, e, acc);
+  if (valid) {
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob) {
+      st4(e0 + p * D + 16 * ob + 4 * g, e[ob][0], e[ob][1], e[ob][2], e[ob][3]);
+      st4(q0 + p * D + 16 * ob + 4 * g, acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// One message-passing iteration over all edges.
+// ---------------------------------------------------------------------------------------------
+struct EdgeStepArgs {
+  int64_t N, E;
+  int T, t_nt_ld;   // node-table row length = 128 + 64 T
+  const int *seg, *wg_start, *s_src, *s_dst, *s_orig;
+  const float *NT, *Q0, *e_cur;
+  float* e_next;
+  const float *e1_w, *e2_w, *e2_b, *msg_w, *attn_w;
+  float attn_b;
+  float* agg;
+  pemp_mlp head;
+  float* edge_logits;
+  int write_next;
+};
+
+template <int AGG, bool HEAD>
+__global__ __launch_bounds__(256) void edge_step_kernel(EdgeStepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float wl[];   // [3][64][LDW]: e1_w, e2_w, msg_w[t]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
+  const int T = a.T;
+  const int blk = blockIdx.x;
+  if (blk >= a.wg_start[T]) return;                      // uniform for the block
+  int t = 0;
+  while (t + 1 < T && a.wg_start[t + 1] <= blk) ++t;
+  // stage the three 64x64 weight tiles of this type
+  const float* srcs[3] = {a.e1_w, a.e2_w, a.msg_w + (int64_t)t * D * D};
+  for (int idx = threadIdx.x; idx < 3 * D * 16; idx += 256) {
+    const int m = idx / (D * 16), rem = idx - m * D * 16, row = rem >> 4, c4 = (rem & 15) * 4;
+    *reinterpret_cast<float4*>(&wl[(m * D + row) * LDW + c4]) = ld4(srcs[m] + row * D + c4);
+  }
+  __syncthreads();
+  const float* W1 = wl;
+  const float* W2 = wl + D * LDW;
+  const float* WM = wl + 2 * D * LDW;
+
+  const int64_t N = a.N;
+  const int ts = a.seg[t * N], te = a.seg[(t + 1) * N];
+  const int item = (blk - a.wg_start[t]) * 4 + wave;
+  const int cs = ts + item * ITEM;
+  if (cs >= te) return;
+  const int ce = min(cs + ITEM, te);
+  int first = cs;
+  if (cs > ts && a.s_dst[cs] == a.s_dst[cs - 1]) first = a.seg[t * N + a.s_dst[cs] + 1];
+  const int end = (ce == te) ? te : a.seg[t * N + a.s_dst[ce - 1] + 1];
+  if (first >= end) return;
+
+  const float* ntP = a.NT + 128 + 64 * t;
+  float e2b[4][4], aw[4][4];
+#pragma unroll
+  for (int ob = 0; ob < 4; ++ob) {
+    const float4 x = ld4(a.e2_b + 16 * ob + 4 * g);
+    e2b[ob][0] = x.x; e2b[ob][1] = x.y; e2b[ob][2] = x.z; e2b[ob][3] = x.w;
+    if (AGG == PEMP_AGGR_ATTN) {
+      const float4 y = ld4(a.attn_w + 16 * ob + 4 * g);
+      aw[ob][0] = y.x; aw[ob][1] = y.y; aw[ob][2] = y.z; aw[ob][3] = y.w;
+    }
+  }
+  // carried state of the segment continuing into the next tile
+  int cseg = -1;
+  float cM = 0.f, cl = 0.f, cv[4][4];
+#pragma unroll
+  for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cv[ob][r] = 0.f;
+
+  for (int base = first; base < end; base += 16) {
+    const int p = base + c;
+    const bool valid = p < end;
+    const int pp = valid ? p : first;            // safe address for padding columns
+    const int64_t src = a.s_src[pp], dst = a.s_dst[pp];
+    const int seg = valid ? (int)dst : -1;
+    // layer 1: h = ReLU(Q0 + A[dst] + B[src] + W1_e_cur · e_cur)
+    float h[4][4], ein[4][4];
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob) {
+      const int f = 16 * ob + 4 * g;
+      const float4 q = ld4(a.Q0 + (int64_t)pp * D + f);
+      const float4 xa = ld4(a.NT + dst * a.t_nt_ld + f);
+      const float4 xb = ld4(a.NT + src * a.t_nt_ld + 64 + f);
+      const float4 ec = ld4(a.e_cur + (int64_t)pp * D + f);
+      h[ob][0] = q.x + xa.x + xb.x; h[ob][1] = q.y + xa.y + xb.y;
+      h[ob][2] = q.z + xa.z + xb.z; h[ob][3] = q.w + xa.w + xb.w;
+      ein[ob][0] = ec.x; ein[ob][1] = ec.y; ein[ob][2] = ec.z; ein[ob][3] = ec.w;
+    }
+    gemm_frag<4, 4>(W1, LDW, ein, h);
+    relu_frag<4>(h);
+    // layer 2: e' = ReLU(W2 · h + b2)
+    float ep[4][4];
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ep[ob][r] = e2b[ob][r];
+    gemm_frag<4, 4>(W2, LDW, h, ep);
+    relu_frag<4>(ep);
+    if (a.write_next && valid) {
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+        st4(a.e_next + (int64_t)p * D + 16 * ob + 4 * g, ep[ob][0], ep[ob][1], ep[ob][2], ep[ob][3]);
+    }
+    if (HEAD) {
+      float h1[4][4], h2[4][4];
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h1[ob][r] = ep[ob][r];
+      mlp_frag<4>(a.head, h1, h2);
+      if (valid && g == 0) a.edge_logits[a.s_orig[p]] = h1[0][0];
+    }
+    // message: m = ReLU(P_t[dst] + W_t_e · e')
+    float m[4][4];
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob) {
+      const float4 x = ld4(ntP + dst * a.t_nt_ld + 16 * ob + 4 * g);
+      m[ob][0] = x.x; m[ob][1] = x.y; m[ob][2] = x.z; m[ob][3] = x.w;
+    }
+    gemm_frag<4, 4>(WM, LDW, ep, m);
+    relu_frag<4>(m);
+
+    // ---- segmented aggregation over the 16 columns, carried across tiles ----
+    const SegMask sm = seg_mask(seg, c);
+    const bool tail = !sm.b1;
+    const int seg0 = __shfl(seg, lane & 48);
+    const bool last_tile = base + 16 >= end;
+    float v[4][4];
+    float M = 0.f, l = 0.f;
+    if (AGG == PEMP_AGGR_ATTN) {
+      float av = 0.f;
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) av = fmaf(aw[ob][r], ep[ob][r], av);
+      av += __shfl_xor(av, 16);
+      av += __shfl_xor(av, 32);
+      av += a.attn_b;
+      M = fmaxf(scan_max(av, sm), scan_max_bwd(av, sm));
+      const float pe = expf(av - M);
+      l = scan_add(pe, sm);
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[ob][r] = scan_add(pe * m[ob][r], sm);
+      if (tail && seg == cseg && seg0 == seg) {
+        const float Mn = fmaxf(cM, M), fc = expf(cM - Mn), fn = expf(M - Mn);
+        l = cl * fc + l * fn;
+#pragma unroll
+        for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[ob][r] = cv[ob][r] * fc + v[ob][r] * fn;
+        M = Mn;
+      }
+    } else {
+      l = scan_add(1.0f, sm);                      // chunk length
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          v[ob][r] = (AGG == PEMP_AGGR_MAX) ? scan_max(m[ob][r], sm) : scan_add(m[ob][r], sm);
+      if (tail && seg == cseg && seg0 == seg) {
+        l += cl;
+#pragma unroll
+        for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            v[ob][r] = (AGG == PEMP_AGGR_MAX) ? fmaxf(v[ob][r], cv[ob][r]) : v[ob][r] + cv[ob][r];
+      }
+    }
+    // the carried segment ended exactly at the previous tile: finalise it
+    if (cseg >= 0 && seg0 != cseg && c == 0) {
+      float* dstp = a.agg + ((int64_t)cseg * T + t) * D + 4 * g;
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob) {
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          o[r] = (AGG == PEMP_AGGR_ATTN) ? cv[ob][r] / (cl + 1e-12f)
+               : (AGG == PEMP_AGGR_MEAN) ? cv[ob][r] / cl : cv[ob][r];
+        st4(dstp + 16 * ob, o[0], o[1], o[2], o[3]);
+      }
+    }
+    const bool carry_out = !last_tile && c == 15;
+    if (tail && valid && !carry_out) {
+      float* dstp = a.agg + ((int64_t)seg * T + t) * D + 4 * g;
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob) {
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          o[r] = (AGG == PEMP_AGGR_ATTN) ? v[ob][r] / (l + 1e-12f)
+               : (AGG == PEMP_AGGR_MEAN) ? v[ob][r] / l : v[ob][r];
+        st4(dstp + 16 * ob, o[0], o[1], o[2], o[3]);
+      }
+    }
+    if (!last_tile) {
+      const int src_lane = (lane & 48) | 15;
+      cseg = __shfl(seg, src_lane);
+      cM = __shfl(M, src_lane);
+      cl = __shfl(l, src_lane);
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cv[ob][r] = __shfl(v[ob][r], src_lane);
+    }
+  }
+}
+
+// x_new = ReLU(b + sum_t U_t · agg[n, t]) (or agg[n, 0] when there is no update MLP) -> X[:, 64:128]
+__global__ __launch_bounds__(512) void node_update_kernel(const float* __restrict__ agg, const int* __restrict__ cnt,
+                                                          int T, int64_t N, const float* __restrict__ upd_w,
+                                                          const float* __restrict__ upd_b, float* __restrict__ X) {
+  __shared__ __attribute__((aligned(16))) float red[8][16 * 68];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
+  const int64_t n0 = (int64_t)blockIdx.x * 16;
+  if (!upd_w) {
+    for (int idx = threadIdx.x; idx < 16 * D; idx += 512) {
+      const int r = idx >> 6, f = idx & 63;
+      const int64_t n = n0 + r;
+      if (n < N) X[n * 128 + 64 + f] = cnt[n] > 0 ? agg[n * D + f] : 0.0f;
+    }
+    return;
+  }
+  const int64_t n = n0 + c;
+  float acc[4][4];
+#pragma unroll
+  for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[ob][r] = 0.f;
+  for (int t = wave; t < T; t += 8) {
+    const bool has = n < N && cnt[t * N + n] > 0;
+    float in[4][4];
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (has) x = ld4(agg + (n * T + t) * D + 16 * mb + 4 * g);
+      in[mb][0] = x.x; in[mb][1] = x.y; in[mb][2] = x.z; in[mb][3] = x.w;
+    }
+    gemm_frag<4, 4>(upd_w + 64 * t, 64 * T, in, acc);
+  }
+#pragma unroll
+  for (int ob = 0; ob < 4; ++ob) st4(&red[wave][c * 68 + 16 * ob + 4 * g], acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]);
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 16 * D; idx += 512) {
+    const int r = idx >> 6, f = idx & 63;
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) s += red[w][r * 68 + f];
+    const int64_t nn = n0 + r;
+    if (nn < N) X[nn * 128 + 64 + f] = fmaxf(s + upd_b[f], 0.0f);
+  }
+}
+
+static int grid1d(int64_t total, int block, int cap = 65536) {
+  int64_t g = (total + block - 1) / block;
+  return (int)(g < 1 ? 1 : (g > cap ? cap : g));
+}
+
+template <int AGG>
+static void launch_edge_step(const EdgeStepArgs& a, bool head, int grid, hipStream_t st) {
+  const size_t lds = (size_t)3 * D * LDW * sizeof(float);
+  if (head)
+    hipLaunchKernelGGL((edge_step_kernel<AGG, true>), dim3(grid), dim3(256), lds, st, a);
+  else
+    hipLaunchKernelGGL((edge_step_kernel<AGG, false>), dim3(grid), dim3(256), lds, st, a);
+}
+
+static int rows_mlp(const pemp_mlp& m, const float* in, int64_t ld_in, int64_t M, float* out, int64_t ld_out,
+                    float* out2, int64_t ld_out2, hipStream_t st) {
+  if (M <= 0) return PEMP_OK;
+  RowsMlpArgs a{m, in, ld_in, M, out, ld_out, out2, ld_out2};
+  hipLaunchKernelGGL(rows_mlp_kernel, dim3((unsigned)((M + 15) / 16)), dim3(256), 0, st, a);
+  PEMP_LAUNCH_CHECK();
+  return PEMP_OK;
+}
+
+static bool mlp_ok(const pemp_mlp& m, int in_max, int width_max) {
+  if (m.n_layers < 1 || m.n_layers > 4) return false;
+  for (int l = 0; l < m.n_layers; ++l) {
+    const pemp_layer& L = m.layer[l];
+    if (!L.w || !L.b || L.in_dim <= 0 || L.out_dim <= 0) return false;
+    if (L.in_dim > (l == 0 ? in_max : width_max) || L.out_dim > width_max) return false;
+    if (l > 0 && L.in_dim != m.layer[l - 1].out_dim) return false;
+  }
+  return true;
+}
+
+}  // namespace
+}  // namespace pemp
+
+using namespace pemp;
+
+extern "C" size_t pemp_mpn_workspace_size(const pemp_mpn_desc* desc, int64_t N, int64_t E) {
+  if (!desc || N < 0 || E < 0 || desc->num_types < 1) return 0;
+  size_t bytes = 0;
+  mpn_carve(nullptr, desc->num_types, N, E, &bytes);
+  return bytes;
+}
+
+extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weights* w, const float* x,
+                                const float* edge_attr, const int64_t* edge_index, const int64_t* node_types,
+                                int64_t N, int64_t E, float* edge_logits, float* node_logits, float* class_logits,
+                                void* workspace, size_t workspace_bytes, void* stream) {
+  PEMP_CHECK_ARG(desc && w, "pemp_mpn_forward: null desc/weights");
+  const int T = desc->num_types, J = desc->num_joints;
+  PEMP_CHECK_ARG(desc->hidden == 64, "pemp_mpn_forward: hidden width must be 64 (got %d)", desc->hidden);
+  PEMP_CHECK_ARG(T >= 1 && T <= MAXT, "pemp_mpn_forward: num_types must be in [1, %d]", MAXT);
+  PEMP_CHECK_ARG(N >= 0 && E >= 0 && N < (1ll << 30) && E < (1ll << 31) - 64 && (int64_t)T * N < (1ll << 30),
+                 "pemp_mpn_forward: N=%lld E=%lld out of range", (long long)N, (long long)E);
+  PEMP_CHECK_ARG(desc->steps >= 0 && desc->aux_loss_steps >= 0, "pemp_mpn_forward: bad steps");
+  PEMP_CHECK_ARG(desc->aggr >= PEMP_AGGR_ATTN && desc->aggr <= PEMP_AGGR_MAX, "pemp_mpn_forward: bad aggr");
+  PEMP_CHECK_ARG(desc->aggr != PEMP_AGGR_ATTN || w->attn_w, "pemp_mpn_forward: attention needs attn_w");
+  PEMP_CHECK_ARG(mlp_ok(w->node_emb, 128, 128) && w->node_emb.layer[w->node_emb.n_layers - 1].out_dim == 64 &&
+                     w->node_emb.layer[0].in_dim == desc->node_in_dim,
+                 "pemp_mpn_forward: node embedding must map node_in_dim (<=128) -> 64");
+  PEMP_CHECK_ARG(mlp_ok(w->edge_emb, 128, 128) && w->edge_emb.layer[w->edge_emb.n_layers - 1].out_dim == 64 &&
+                     w->edge_emb.layer[0].in_dim == desc->edge_attr_dim,
+                 "pemp_mpn_forward: edge embedding must map edge_attr_dim (<=128) -> 64");
+  PEMP_CHECK_ARG(mlp_ok(w->edge_head, 64, 64) && w->edge_head.layer[0].in_dim == 64 &&
+                     w->edge_head.layer[w->edge_head.n_layers - 1].out_dim == 1,
+                 "pemp_mpn_forward: edge head must map 64 -> 1 with widths <= 64");
+  PEMP_CHECK_ARG(mlp_ok(w->node_head, 64, 128) && mlp_ok(w->class_head, 64, 128) &&
+                     w->class_head.layer[w->class_head.n_layers - 1].out_dim == J,
+                 "pemp_mpn_forward: node/class heads must start at 64 and end at 1 / num_joints");
+  PEMP_CHECK_ARG(w->pre_w && w->pre_b && w->q0_w && w->q0_b && w->e1_w && w->e2_w && w->e2_b && w->msg_w,
+                 "pemp_mpn_forward: null layer weights");
+  PEMP_CHECK_ARG(N == 0 || (x && node_logits && class_logits && node_types), "pemp_mpn_forward: null node tensors");
+  PEMP_CHECK_ARG(E == 0 || (edge_attr && edge_index && edge_logits), "pemp_mpn_forward: null edge tensors");
+  size_t need = 0;
+  mpn_carve(nullptr, T, N, E, &need);
+  if (workspace_bytes < need) {
+    set_error("pemp_mpn_forward: workspace %zu < %zu bytes", workspace_bytes, need);
+    return PEMP_ERR_WORKSPACE;
+  }
+  if (N == 0) return PEMP_OK;
+  PEMP_CHECK_ARG(!(E > 0 && N == 0), "pemp_mpn_forward: edges without nodes");
+  const MpnWs ws = mpn_carve(workspace, T, N, E, nullptr);
+  const hipStream_t st = as_stream(stream);
+  const int64_t K = (int64_t)T * N;
+
+  // ---- prepare: type-major order ----
+  PEMP_HIP(hipMemsetAsync(ws.cnt, 0, (K + 1) * sizeof(int), st));
+  PEMP_HIP(hipMemsetAsync(ws.cursor, 0, (K + 1) * sizeof(int), st));
+  if (E > 0) {
+    hipLaunchKernelGGL(mpn_count_kernel, dim3(grid1d(E, 256)), dim3(256), 0, st, edge_index, node_types, N, E, T,
+                       ws.cnt, ws.err);
+    PEMP_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(mpn_scan_kernel, dim3(1), dim3(1024), 0, st, ws.cnt, K, N, T, ws.seg, ws.wg_start);
+  PEMP_LAUNCH_CHECK();
+  if (E > 0) {
+    hipLaunchKernelGGL(mpn_scatter_kernel, dim3(grid1d(E, 256)), dim3(256), 0, st, edge_index, node_types, N, E,
+                       ws.seg, ws.cursor, ws.perm);
+    PEMP_LAUNCH_CHECK();
+    hipLaunchKernelGGL(mpn_segsort_kernel, dim3((unsigned)((K + 3) / 4)), dim3(256), 0, st, edge_index, E, K, ws.seg,
+                       ws.perm, ws.s_src, ws.s_dst, ws.s_orig);
+    PEMP_LAUNCH_CHECK();
+  }
+
+  // ---- embeddings ----
+  int rc = rows_mlp(w->node_emb, x, desc->node_in_dim, N, ws.X, 128, ws.X + 64, 128, st);
+  if (rc) return rc;
+  if (E > 0) {
+    hipLaunchKernelGGL(edge_embed_kernel, dim3((unsigned)((E + 63) / 64)), dim3(256), 0, st, w->edge_emb, edge_attr,
+                       desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, ws.EA, ws.Q0);
+    PEMP_LAUNCH_CHECK();
+  }
+
+  // ---- iterations ----
+  const int NO = 128 + 64 * T;
+  const int steps = desc->steps, aux = desc->aux_loss_steps;
+  const int edge_grid = (int)(E / (4 * ITEM)) + 2 * T + 1;
+  float* e_cur = ws.EA;
+  float* e_nxt = ws.EB;
+  int rec = 0;
+  for (int it = 0; it < steps; ++it) {
+    const bool record = it >= steps - aux - 1;
+    hipLaunchKernelGGL(rows_linear_kernel, dim3((unsigned)((N + 15) / 16), (unsigned)((NO + 63) / 64)), dim3(256), 0,
+                       st, ws.X, N, w->pre_w, w->pre_b, NO, ws.NT);
+    PEMP_LAUNCH_CHECK();
+    if (E > 0) {
+      EdgeStepArgs ea{};
+      ea.N = N; ea.E = E; ea.T = T; ea.t_nt_ld = NO;
+      ea.seg = ws.seg; ea.wg_start = ws.wg_start; ea.s_src = ws.s_src; ea.s_dst = ws.s_dst; ea.s_orig = ws.s_orig;
+      ea.NT = ws.NT; ea.Q0 = ws.Q0; ea.e_cur = e_cur; ea.e_next = e_nxt;
+      ea.e1_w = w->e1_w; ea.e2_w = w->e2_w; ea.e2_b = w->e2_b; ea.msg_w = w->msg_w; ea.attn_w = w->attn_w;
+      ea.attn_b = w->attn_b; ea.agg = ws.agg; ea.head = w->edge_head;
+      ea.edge_logits = record ? edge_logits + (int64_t)rec * E : nullptr;
+      ea.write_next = it + 1 < steps;
+      switch (desc->aggr) {
+        case PEMP_AGGR_ATTN: launch_edge_step<PEMP_AGGR_ATTN>(ea, record, edge_grid, st); break;
+        case PEMP_AGGR_SUM: launch_edge_step<PEMP_AGGR_SUM>(ea, record, edge_grid, st); break;
+        case PEMP_AGGR_MEAN: launch_edge_step<PEMP_AGGR_MEAN>(ea, record, edge_grid, st); break;
+        default: launch_edge_step<PEMP_AGGR_MAX>(ea, record, edge_grid, st); break;
+      }
+      PEMP_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(node_update_kernel, dim3((unsigned)((N + 15) / 16)), dim3(512), 0, st, ws.agg, ws.cnt, T, N,
+                       w->upd_w, w->upd_b, ws.X);
+    PEMP_LAUNCH_CHECK();
+    if (record) {
+      if ((rc = rows_mlp(w->node_head, ws.X + 64, 128, N, node_logits + (int64_t)rec * N, 1, nullptr, 0, st))) return rc;
+      if ((rc = rows_mlp(w->class_head, ws.X + 64, 128, N, class_logits + (int64_t)rec * N * J, J, nullptr, 0, st)))
+        return rc;
+      ++rec;
+    }
+    float* tmp = e_cur; e_cur = e_nxt; e_nxt = tmp;
+  }
+  if ((rc = rows_mlp(w->node_head, ws.X + 64, 128, N, node_logits + (int64_t)rec * N, 1, nullptr, 0, st))) return rc;
+  if ((rc = rows_mlp(w->class_head, ws.X + 64, 128, N, class_logits + (int64_t)rec * N * J, J, nullptr, 0, st)))
+    return rc;
+  return PEMP_OK;
+}

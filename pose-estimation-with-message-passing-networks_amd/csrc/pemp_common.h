@@ -1,0 +1,70 @@
+// Shared device/host helpers for the gfx950 kernels of libpemp.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../../include/pemp.h"
+
+namespace pemp {
+
+// ---- error reporting (thread-local last error, returned through pemp_last_error) ----
+void set_error(const char* fmt, ...);
+
+#define PEMP_CHECK_ARG(cond, ...)                \
+  do {                                           \
+    if (!(cond)) {                               \
+      ::pemp::set_error(__VA_ARGS__);            \
+      return PEMP_ERR_INVALID_ARG;               \
+    }                                            \
+  } while (0)
+
+#define PEMP_HIP(call)                                                             \
+  do {                                                                             \
+    hipError_t e_ = (call);                                                        \
+    if (e_ != hipSuccess) {                                                        \
+      ::pemp::set_error("%s failed: %s (%s:%d)", #call, hipGetErrorString(e_),     \
+                        __FILE__, __LINE__);                                        \
+      return PEMP_ERR_HIP;                                                         \
+    }                                                                              \
+  } while (0)
+
+#define PEMP_LAUNCH_CHECK()                                                        \
+  do {                                                                             \
+    hipError_t e_ = hipGetLastError();                                             \
+    if (e_ != hipSuccess) {                                                        \
+      ::pemp::set_error("kernel launch failed: %s (%s:%d)", hipGetErrorString(e_), \
+                        __FILE__, __LINE__);                                        \
+      return PEMP_ERR_HIP;                                                         \
+    }                                                                              \
+  } while (0)
+
+static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// Workspace carving: bump allocator over a caller-owned buffer (256-B aligned slices).
+struct Carver {
+  char* base;
+  size_t used;
+  explicit Carver(void* b) : base(static_cast<char*>(b)), used(0) {}
+  template <typename T>
+  T* take(size_t count) {
+    used = align_up(used, 256);
+    T* p = reinterpret_cast<T*>(base ? base + used : nullptr);
+    used += count * sizeof(T);
+    return p;
+  }
+};
+
+// ---- device helpers ----
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  // v_mfma_f32_16x16x4_f32: exact f32 fma chain (k ordered), 16x16 tile, K = 4.
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+}  // namespace pemp

@@ -1,0 +1,171 @@
+"""Drop-in ``NaiveGraphConstructor`` (``src/graph_constructor/ConstructGraph.py:9-249``), inference path.
+
+Same constructor signature, same ``construct_graph()`` 15-tuple, same dtypes (int64 indices) and
+node/edge order as the reference; computed by ``libpemp.so`` (``pemp_detect``,
+``pemp_pack_nodes``, ``pemp_fully_graph`` / ``pemp_knn_graph_*``, ``pemp_edge_features``).
+Host synchronisation: one count read-back after detection (the reference syncs at every
+``nonzero``), plus one more for knn graphs.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+_EF_MODES = {
+    frozenset(["position", "connection_type"]): 0,
+    frozenset(["connection_type"]): 1,
+    frozenset(["nothing"]): 2,
+    frozenset(["position"]): 3,
+    frozenset(["position", "angle", "connection_type"]): 4,
+}
+
+
+def get_graph_constructor(config, **kwargs):
+    """``src/graph_constructor/__init__.py:4-5``."""
+    return NaiveGraphConstructor(config=config, **kwargs)
+
+
+class NaiveGraphConstructor:
+    _ws_detect = _lib.Workspace()
+    _ws_knn = _lib.Workspace()
+    _cap = 512   # detections per image kept between calls (grows on overflow)
+
+    def __init__(self, scoremaps, tagmaps, features, joints_gt, factor_list, masks, device, config, testing,
+                 heatmaps, num_joints):
+        if joints_gt is not None:
+            raise NotImplementedError("training-time label construction (joints_gt) is out of scope: "
+                                      "ConstructGraph.py:114-176 runs only with ground truth")
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("pemp_amd NaiveGraphConstructor runs on the HIP device only (no CPU fallback)")
+        self.scoremaps = scoremaps.to(self.device)
+        self.tagmaps = tagmaps.to(self.device) if tagmaps is not None else None
+        self.features = features.to(self.device)
+        self.masks = masks.to(self.device) if masks is not None else None
+        self.joints_gt = None
+        self.factor_list = factor_list
+        self.batch_size = scoremaps.shape[0]
+        self.num_joints = num_joints
+        self.mask_crowds = config.MASK_CROWDS
+        self.detect_threshold = config.DETECT_THRESHOLD if config.DETECT_THRESHOLD <= 1.5 else None
+        self.hybrid_k = config.HYBRID_K
+        self.mpn_graph_type = config.GRAPH_TYPE
+        self.normalize_node_distance = config.NORM_NODE_DISTANCE
+        self.edge_features_to_use = config.EDGE_FEATURES_TO_USE
+        self.pool_kernel_size = config.POOL_KERNEL_SIZE
+        self.testing = testing
+        if getattr(config, "USE_GT", False) or getattr(config, "IMAGE_CENTRIC_SAMPLING", False):
+            raise NotImplementedError("USE_GT / IMAGE_CENTRIC_SAMPLING need ground truth (training only)")
+
+    # ------------------------------------------------------------------------------------
+    def construct_graph(self):
+        L = _lib.lib()
+        st = _lib.stream()
+        sm = self.scoremaps
+        if sm.dtype != torch.float32:
+            sm = sm.float()
+        sm = sm.contiguous()
+        B, J, H, W = sm.shape
+        if J != self.num_joints:
+            raise ValueError(f"scoremaps have {J} types, num_joints={self.num_joints}")
+        if self.mask_crowds:
+            if self.masks is None:
+                raise TypeError("MASK_CROWDS is set but masks is None")   # reference: masks[batch] on None
+            masks = self.masks.float().contiguous()
+        else:
+            masks = None
+        use_thr = self.detect_threshold is not None
+        topk = self.hybrid_k if use_thr else 20
+        thr = float(self.detect_threshold) if use_thr else 0.0
+        dev = sm.device
+
+        # ---- detection (pemp_detect): one read-back of the per-image counts ----
+        ws_bytes = L.pemp_detect_workspace_size(B, J, H, W, topk)
+        ws = self._ws_detect.get(ws_bytes, dev)
+        cap = NaiveGraphConstructor._cap
+        det = torch.empty(B, cap, 3, dtype=torch.int64, device=dev)
+        dsc = torch.empty(B, cap, dtype=torch.float32, device=dev)
+        n_det = torch.empty(B, dtype=torch.int32, device=dev)
+        _lib.check(L.pemp_detect(_lib.ptr(sm), _lib.ptr(masks), B, J, H, W, self.pool_kernel_size, thr, int(use_thr),
+                                 topk, 3, _lib.ptr(ws), ws.numel(), _lib.ptr(det), _lib.ptr(dsc), _lib.ptr(n_det),
+                                 cap, st))
+        counts = n_det.cpu().numpy().astype(np.int64)
+        if counts.max(initial=0) > cap:
+            cap = int(counts.max())
+            NaiveGraphConstructor._cap = max(NaiveGraphConstructor._cap, cap)
+            det = torch.empty(B, cap, 3, dtype=torch.int64, device=dev)
+            dsc = torch.empty(B, cap, dtype=torch.float32, device=dev)
+            _lib.check(L.pemp_detect(_lib.ptr(sm), _lib.ptr(masks), B, J, H, W, self.pool_kernel_size, thr,
+                                     int(use_thr), topk, 2, _lib.ptr(ws), ws.numel(), _lib.ptr(det), _lib.ptr(dsc),
+                                     _lib.ptr(n_det), cap, st))
+        node_off_h = np.zeros(B + 1, np.int64)
+        node_off_h[1:] = np.cumsum(counts)
+        N = int(node_off_h[-1])
+        node_off = torch.from_numpy(node_off_h).to(dev, non_blocking=True)
+
+        # ---- nodes (pemp_pack_nodes) ----
+        feats = self.features
+        if feats.dtype != torch.float32:
+            feats = feats.float()
+        feats = feats.contiguous()
+        C = feats.shape[1]
+        tags = self.tagmaps
+        if tags is not None:
+            tags = tags.float().contiguous()
+            F = 1 if tags.dim() == 4 else int(np.prod(tags.shape[4:]))
+        else:
+            F = 1
+        x = torch.empty(N, C, dtype=torch.float32, device=dev)
+        joint_det = torch.empty(N, 3, dtype=torch.int64, device=dev)
+        joint_scores = torch.empty(N, dtype=torch.float32, device=dev)
+        batch_index = torch.empty(N, dtype=torch.int64, device=dev)
+        joint_tags = torch.empty(N, F, dtype=torch.float32, device=dev)
+        _lib.check(L.pemp_pack_nodes(_lib.ptr(feats), C, _lib.ptr(tags), F, B, J, H, W, _lib.ptr(det), _lib.ptr(dsc),
+                                     cap, _lib.ptr(node_off), N, _lib.ptr(x), _lib.ptr(joint_det),
+                                     _lib.ptr(joint_scores), _lib.ptr(batch_index), _lib.ptr(joint_tags), st))
+        if tags is not None:
+            joint_tags = joint_tags.view((N,) + tuple(tags.shape[4:])) if tags.dim() > 4 else joint_tags.view(N)
+        else:
+            joint_tags = None
+
+        # ---- edges ----
+        edge_index = self._edges(L, st, joint_det, node_off, node_off_h, B, dev)
+        E = edge_index.shape[1]
+        mode = _EF_MODES.get(frozenset(self.edge_features_to_use))
+        if mode is None:
+            raise NotImplementedError(f"EDGE_FEATURES_TO_USE={self.edge_features_to_use}")
+        A = {0: J + 2, 1: J, 2: 1, 3: 2, 4: J + 3}[mode]
+        norm = float(max(W, H)) if self.normalize_node_distance else 1.0
+        edge_attr = torch.empty(E, A, dtype=torch.float32, device=dev)
+        _lib.check(L.pemp_edge_features(_lib.ptr(joint_det), _lib.ptr(edge_index), E, J, norm, mode,
+                                        _lib.ptr(edge_attr), st))
+        return (x, edge_attr, edge_index, None, None, None, None, joint_det, None, None, None, joint_scores,
+                batch_index, None, joint_tags)
+
+    def _edges(self, L, st, joint_det, node_off, node_off_h, B, dev):
+        counts = np.diff(node_off_h)
+        if self.mpn_graph_type == "fully":
+            per = counts * np.maximum(counts - 1, 0)
+        elif self.mpn_graph_type == "knn":
+            nh = np.ascontiguousarray(node_off_h)
+            nh_p = nh.ctypes.data_as(ctypes.c_void_p)
+            ws = self._ws_knn.get(L.pemp_knn_workspace_size(nh_p, B), dev)
+            ecount = torch.empty(B, dtype=torch.int64, device=dev)
+            _lib.check(L.pemp_knn_graph_count(_lib.ptr(joint_det), _lib.ptr(node_off), nh_p, B, 50, _lib.ptr(ws),
+                                              ws.numel(), _lib.ptr(ecount), st))
+            per = ecount.cpu().numpy()
+        else:
+            raise NotImplementedError(f"GRAPH_TYPE={self.mpn_graph_type}")
+        edge_off_h = np.zeros(B + 1, np.int64)
+        edge_off_h[1:] = np.cumsum(per)
+        E = int(edge_off_h[-1])
+        edge_off = torch.from_numpy(edge_off_h).to(dev, non_blocking=True)
+        edge_index = torch.empty(2, E, dtype=torch.int64, device=dev)
+        if self.mpn_graph_type == "fully":
+            _lib.check(L.pemp_fully_graph(_lib.ptr(node_off), _lib.ptr(edge_off), B, E, _lib.ptr(edge_index), st))
+        else:
+            _lib.check(L.pemp_knn_graph_emit(_lib.ptr(node_off), nh_p, B, _lib.ptr(edge_off), E, _lib.ptr(ws),
+                                             ws.numel(), _lib.ptr(edge_index), st))
+        return edge_index

@@ -1,0 +1,146 @@
+"""Weight preparation for ``pemp_mpn_forward`` (done once per parameter version, on the host in fp64).
+
+* eval-mode ``BatchNorm1d`` after a ReLU (``layers.py:8-29``) is folded into the next Linear:
+  W' = W·diag(s), b' = W·o + b with s = γ/sqrt(var+eps), o = β − μ·s; a trailing BN becomes a
+  diagonal layer.
+* ``mlp_edge.0`` (input [x_i ‖ x_j ‖ e], ``layers.py:171-175,214``) is split by input block so the
+  kernels never materialise the 384-wide concat:  W1·[x_i‖x_j‖e_init‖e_cur] + b1
+      = A[i] + B[j] + (W1_e_init·e_init + b1) + W1_e_cur·e_cur,
+  with A = W1_xi·x and B = W1_xj·x computed per NODE (the ``pre_w`` block), and the e_init term
+  computed once per edge (``q0``). The type-t message MLP W_t·[x_i ‖ e'] + b_t is split the same
+  way into a per-node part P_t (``pre_w``) and a per-edge part (``msg_w``).
+* Everything is stored [out_pad][in_pad], zero padded to multiples of 16 (MFMA 16x16x4 tiles).
+The node table the kernels use holds x = [x_init ‖ x_cur] (128 wide); without skip connections
+the x_init/e_init columns get zero weights.
+"""
+import torch
+import torch.nn as nn
+
+from .. import _lib
+
+
+def _pad16(n):
+    return (n + 15) // 16 * 16
+
+
+def _bn_affine(bn: nn.BatchNorm1d):
+    s = bn.weight.double() / torch.sqrt(bn.running_var.double() + bn.eps)
+    o = bn.bias.double() - bn.running_mean.double() * s
+    return s, o
+
+
+def mlp_layers(seq: nn.Sequential):
+    """[(W fp64 [out,in], b fp64 [out], relu)] with BN folded."""
+    layers, pending = [], None
+    for m in seq:
+        if isinstance(m, nn.Linear):
+            W, b = m.weight.detach().double().cpu(), m.bias.detach().double().cpu()
+            if pending is not None:
+                s, o = pending
+                b = b + W @ o
+                W = W * s[None, :]
+                pending = None
+            layers.append([W, b, False])
+        elif isinstance(m, nn.ReLU):
+            layers[-1][2] = True
+        elif isinstance(m, nn.BatchNorm1d):
+            s, o = _bn_affine(m)
+            pending = (s.detach().cpu(), o.detach().cpu())
+        else:
+            raise NotImplementedError(type(m).__name__)
+    if pending is not None:
+        s, o = pending
+        layers.append([torch.diag(s), o, False])
+    if len(layers) > 4:
+        raise NotImplementedError("MLPs deeper than 4 Linear layers")
+    return layers
+
+
+def _padded(W, b, in_pad=None):
+    out, inn = W.shape
+    op, ip = _pad16(out), in_pad or _pad16(inn)
+    Wp = torch.zeros(op, ip, dtype=torch.float64)
+    Wp[:out, :inn] = W
+    bp = torch.zeros(op, dtype=torch.float64)
+    bp[:out] = b
+    return Wp, bp
+
+
+class Folded:
+    """Device copies + the ctypes struct pointing at them (kept alive together)."""
+
+    def __init__(self):
+        self.tensors = []
+        self.struct = _lib.PempMpnWeights()
+
+    def dev(self, t, device):
+        d = t.to(torch.float32).contiguous().to(device)
+        self.tensors.append(d)
+        return d
+
+    def mlp(self, seq, device):
+        m = _lib.PempMlp()
+        layers = mlp_layers(seq)
+        m.n_layers = len(layers)
+        for i, (W, b, relu) in enumerate(layers):
+            Wp, bp = _padded(W, b)
+            wd, bd = self.dev(Wp, device), self.dev(bp, device)
+            m.layer[i] = _lib.PempLayer(wd.data_ptr(), bd.data_ptr(), W.shape[1], W.shape[0], int(relu), 0)
+        return m
+
+
+def fold_weights(model, device) -> Folded:
+    f = Folded()
+    s = f.struct
+    layer = model.mpn_node_cls
+    skip = layer.skip
+    T = model.num_types
+    s.node_emb = f.mlp(model.node_embedding, device)
+    s.edge_emb = f.mlp(model.edge_embedding, device)
+    s.edge_head = f.mlp(model.edge_classification, device)
+    s.node_head = f.mlp(model.node_classification, device)
+    s.class_head = f.mlp(model.classification, device)
+
+    nx = 128 if skip else 64
+
+    def to_xtable(Wx):          # [64, nx] -> [64, 128] in the [x_init | x_cur] layout
+        if skip:
+            return Wx
+        out = torch.zeros(Wx.shape[0], 128, dtype=torch.float64)
+        out[:, 64:] = Wx
+        return out
+
+    W1 = layer.mlp_edge[0].weight.detach().double().cpu()
+    b1 = layer.mlp_edge[0].bias.detach().double().cpu()
+    A = to_xtable(W1[:, :nx])
+    Bm = to_xtable(W1[:, nx:2 * nx])
+    if skip:
+        q0 = W1[:, 2 * nx:2 * nx + 64]
+        e1 = W1[:, 2 * nx + 64:2 * nx + 128]
+    else:
+        q0 = torch.zeros(64, 64, dtype=torch.float64)
+        e1 = W1[:, 2 * nx:2 * nx + 64]
+    if T == 1 and not hasattr(layer.mlp_node, "mlp"):
+        msg_mods = [layer.mlp_node[0]]
+    else:
+        msg_mods = [layer.mlp_node.mlp[t][0] for t in range(T)]
+    pre_w = [A, Bm] + [to_xtable(m.weight.detach().double().cpu()[:, :nx]) for m in msg_mods]
+    pre_b = [torch.zeros(64, dtype=torch.float64)] * 2 + [m.bias.detach().double().cpu() for m in msg_mods]
+    msg_w = [m.weight.detach().double().cpu()[:, nx:nx + 64] for m in msg_mods]
+    s.pre_w = f.dev(torch.cat(pre_w, 0), device).data_ptr()
+    s.pre_b = f.dev(torch.cat(pre_b, 0), device).data_ptr()
+    s.q0_w = f.dev(q0, device).data_ptr()
+    s.q0_b = f.dev(b1, device).data_ptr()
+    s.e1_w = f.dev(e1, device).data_ptr()
+    s.e2_w = f.dev(layer.mlp_edge[2].weight.detach().double().cpu(), device).data_ptr()
+    s.e2_b = f.dev(layer.mlp_edge[2].bias.detach().double().cpu(), device).data_ptr()
+    s.msg_w = f.dev(torch.stack(msg_w, 0), device).data_ptr()
+    attn = getattr(layer, "attn_net", None)
+    if attn is not None:
+        s.attn_w = f.dev(attn[0].weight.detach().double().cpu().reshape(64), device).data_ptr()
+        s.attn_b = float(attn[0].bias.detach().double().cpu().item())
+    upd = layer.update_mlp
+    if upd is not None:
+        s.upd_w = f.dev(upd[0].weight.detach().double().cpu(), device).data_ptr()
+        s.upd_b = f.dev(upd[0].bias.detach().double().cpu(), device).data_ptr()
+    return f

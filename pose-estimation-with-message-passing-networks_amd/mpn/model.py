@@ -1,0 +1,188 @@
+"""Drop-in ``NodeClassificationMPNSimple`` (``NodeClassificationMPNSimple.py:23-97``).
+
+The module tree mirrors the reference's so that ``state_dict`` keys (and their order) are
+identical and reference checkpoints load unchanged:
+``mpn_node_cls.{mlp_edge,mlp_node,update_mlp,attn_net}``, ``edge_embedding``, ``node_embedding``,
+``edge_classification``, ``node_classification``, ``classification``. The parameters are plain
+containers; ``forward`` folds them once per parameter version (eval-mode BatchNorm into the next
+Linear) and runs the whole network in ``pemp_mpn_forward`` (libpemp.so). Inference only.
+"""
+import ctypes
+
+import torch
+import torch.nn as nn
+
+from .. import _lib
+from .fold import fold_weights
+
+AGGR_CODES = {"attn": 0, "add": 1, "sum": 1, "mean": 2, "max": 3}
+TYPE_LUTS = {"left_right": [0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8],
+             "per_body_part": [0, 0, 0, 0, 0, 1, 1, 2, 3, 2, 3, 4, 5, 4, 5, 4, 5]}
+
+
+def _make_mlp(input_dim, hidden_dims, bn=False, end_with_relu=False):
+    """Layer indices as ``layers.py:8-29``: Linear, then (ReLU, [BN]) between Linears."""
+    mods = [nn.Linear(input_dim, hidden_dims[0])]
+    last = len(hidden_dims) - 1
+    if last > 0:
+        mods.append(nn.ReLU(inplace=True))
+        if bn:
+            mods.append(nn.BatchNorm1d(hidden_dims[0]))
+    for i in range(1, last + 1):
+        mods.append(nn.Linear(hidden_dims[i - 1], hidden_dims[i]))
+        if i != last:
+            mods.append(nn.ReLU(inplace=True))
+            if bn:
+                mods.append(nn.BatchNorm1d(hidden_dims[i]))
+    if end_with_relu:
+        mods.append(nn.ReLU(inplace=True))
+        if bn:
+            mods.append(nn.BatchNorm1d(hidden_dims[-1]))
+    return nn.Sequential(*mods)
+
+
+class TypeAwareNodeUpdate(nn.Module):
+    """``layers.py:260-274``: 17 Linear+ReLU message MLPs selected by the source node type."""
+
+    def __init__(self, input_dim, output_dim):
+        super().__init__()
+        self.mlp = nn.ModuleList([nn.Sequential(nn.Linear(input_dim, output_dim), nn.ReLU(inplace=True))
+                                  for _ in range(17)])
+        self.output_dim = output_dim
+
+
+class TypeAwareMPNLayer(nn.Module):
+    """``layers.py:157-258`` (edge MLP agnostic, update ``mlp``)."""
+
+    def __init__(self, node_dim, edge_dim, edge_hidden, aggr, skip=False, edge_mlp="agnostic", num_types=17,
+                 aggr_sub=None, update_type="mlp"):
+        super().__init__()
+        if edge_mlp != "agnostic":
+            raise NotImplementedError(f"EDGE_MLP={edge_mlp}")
+        if update_type != "mlp":
+            raise NotImplementedError(f"UPDATE_TYPE={update_type}")
+        nf = 2 if skip else 1
+        self.aggr, self.aggr_sub, self.num_types, self.skip = aggr, aggr_sub, num_types, skip
+        self.mlp_edge = nn.Sequential(nn.Linear(node_dim * 2 * nf + edge_dim * nf, edge_hidden), nn.ReLU(inplace=True),
+                                      nn.Linear(edge_hidden, edge_dim), nn.ReLU(inplace=True))
+        self.mlp_node = TypeAwareNodeUpdate(node_dim * nf + edge_dim, node_dim)
+        self.update_mlp = nn.Sequential(nn.Linear(node_dim * num_types, node_dim), nn.ReLU(inplace=True))
+        if aggr_sub == "node_edge_attn":
+            self.attn_net = nn.Sequential(nn.Linear(edge_dim, 1))
+        elif aggr_sub == "node_edge_attn_per_type":
+            raise NotImplementedError("AGGR_SUB=node_edge_attn_per_type")
+        else:
+            self.attn_net = None
+
+
+class MPLayer(nn.Module):
+    """``layers.py:32-86`` (edge MLP agnostic)."""
+
+    def __init__(self, node_dim, edge_dim, edge_hidden, aggr, use_node_update_mlp, skip=False, edge_mlp="agnostic"):
+        super().__init__()
+        if edge_mlp != "agnostic":
+            raise NotImplementedError(f"EDGE_MLP={edge_mlp}")
+        nf = 2 if skip else 1
+        self.aggr, self.skip = aggr, skip
+        self.mlp_edge = nn.Sequential(nn.Linear(node_dim * 2 * nf + edge_dim * nf, edge_hidden), nn.ReLU(inplace=True),
+                                      nn.Linear(edge_hidden, edge_dim), nn.ReLU(inplace=True))
+        self.mlp_node = nn.Sequential(nn.Linear(node_dim * nf + edge_dim, node_dim), nn.ReLU(inplace=True))
+        self.update_mlp = (nn.Sequential(nn.Linear(node_dim, node_dim), nn.ReLU()) if use_node_update_mlp else None)
+
+
+class NodeClassificationMPNSimple(nn.Module):
+    """``NodeClassificationMPNSimple.py:23-97``."""
+
+    def __init__(self, config):
+        super().__init__()
+        self.use_skip_connections = config.SKIP
+        self.node_summary = config.NODE_TYPE_SUMMARY
+        for k, v in (("NODE_FEATURE_DIM", 64), ("EDGE_FEATURE_DIM", 64), ("EDGE_FEATURE_HIDDEN", 64)):
+            if config[k] != v:
+                raise NotImplementedError(f"{k}={config[k]}: the HIP kernels are built for width 64")
+        if config.get("LATE_FUSION_POS", False):
+            raise NotImplementedError("LATE_FUSION_POS")
+        if config.AGGR_TYPE == "agnostic":
+            self.mpn_node_cls = MPLayer(64, 64, 64, aggr=config.AGGR, skip=config.SKIP,
+                                        use_node_update_mlp=config.USE_NODE_UPDATE_MLP, edge_mlp=config.EDGE_MLP)
+            self.num_types = 1
+        elif config.AGGR_TYPE == "per_type":
+            self.num_types = {"per_body_part": 6, "not": config.NUM_JOINTS, "left_right": 9}[self.node_summary]
+            self.mpn_node_cls = TypeAwareMPNLayer(64, 64, 64, aggr=config.AGGR, skip=config.SKIP,
+                                                  edge_mlp=config.EDGE_MLP, num_types=self.num_types,
+                                                  aggr_sub=config.AGGR_SUB, update_type=config.UPDATE_TYPE)
+        else:
+            raise NotImplementedError(f"AGGR_TYPE={config.AGGR_TYPE}")
+        self.edge_embedding = _make_mlp(config.EDGE_INPUT_DIM, config.EDGE_EMB.OUTPUT_SIZES, bn=config.EDGE_EMB.BN,
+                                        end_with_relu=config.EDGE_EMB.END_WITH_RELU)
+        self.node_embedding = _make_mlp(config.NODE_INPUT_DIM, config.NODE_EMB.OUTPUT_SIZES, bn=config.NODE_EMB.BN,
+                                        end_with_relu=config.NODE_EMB.END_WITH_RELU)
+        self.edge_classification = _make_mlp(64, config.EDGE_CLASS.OUTPUT_SIZES, bn=config.BN)
+        self.node_classification = _make_mlp(64, config.NODE_CLASS.OUTPUT_SIZES, bn=config.BN)
+        self.classification = _make_mlp(64, config.CLASS.OUTPUT_SIZES, bn=config.BN)
+        self.edge_steps = config.STEPS
+        self.node_steps = config.NODE_STEPS
+        self.aux_loss_steps = config.AUX_LOSS_STEPS
+        self.num_joints = config.CLASS.OUTPUT_SIZES[-1]
+        if self.node_steps != 0:
+            raise NotImplementedError("NODE_STEPS > 0 (the reference calls the layer without node_types)")
+        if config.AGGR_TYPE == "per_type":
+            aggr = "attn" if config.AGGR_SUB == "node_edge_attn" else config.AGGR
+        else:
+            aggr = config.AGGR
+        if aggr not in AGGR_CODES:
+            raise NotImplementedError(f"AGGR={aggr}")
+        self.aggr_code = AGGR_CODES[aggr]
+        self._folded = None
+        self._folded_key = None
+        self._ws = _lib.Workspace()
+
+    # --------------------------------------------------------------------------------------
+    def _weights(self, device):
+        key = (device, tuple(p._version for p in self.parameters()), tuple(b._version for b in self.buffers()),
+               tuple(p.data_ptr() for p in self.parameters()))
+        if self._folded is None or self._folded_key != key:
+            self._folded = fold_weights(self, device)
+            self._folded_key = key
+        return self._folded
+
+    def forward(self, x, edge_attr, edge_index, **kwargs):
+        if self.training:
+            raise NotImplementedError("pemp_amd MPN is inference-only: call .eval() (BatchNorm uses running stats)")
+        if x.device.type != "cuda":
+            raise RuntimeError("pemp_amd MPN runs on the HIP device only (no CPU fallback)")
+        L = _lib.lib()
+        dev = x.device
+        node_types = kwargs["node_types"]
+        if self.node_summary != "not":
+            node_types = torch.tensor(TYPE_LUTS[self.node_summary], device=dev)[node_types]
+        N, E = x.shape[0], edge_index.shape[1]
+        x = x.float().contiguous()
+        edge_attr = edge_attr.float().contiguous()
+        edge_index = edge_index.long().contiguous()
+        node_types = node_types.long().contiguous()
+        fw = self._weights(dev)
+        steps, aux = self.edge_steps, self.aux_loss_steps
+        n_rec = sum(1 for i in range(steps) if i >= steps - aux - 1)
+        desc = _lib.PempMpnDesc(self.num_types, self.num_joints, steps, aux, self.aggr_code, 64,
+                                edge_attr.shape[1] if edge_attr.dim() == 2 else 1, x.shape[1])
+        edge_logits = torch.empty(max(n_rec, 1), E, dtype=torch.float32, device=dev)
+        node_logits = torch.empty(n_rec + 1, N, dtype=torch.float32, device=dev)
+        class_logits = torch.empty(n_rec + 1, N, self.num_joints, dtype=torch.float32, device=dev)
+        ws = self._ws.get(L.pemp_mpn_workspace_size(ctypes.byref(desc), N, E), dev)
+        _lib.check(L.pemp_mpn_forward(ctypes.byref(desc), ctypes.byref(fw.struct), _lib.ptr(x), _lib.ptr(edge_attr),
+                                      _lib.ptr(edge_index), _lib.ptr(node_types), N, E, _lib.ptr(edge_logits),
+                                      _lib.ptr(node_logits), _lib.ptr(class_logits), _lib.ptr(ws), ws.numel(),
+                                      _lib.stream()))
+        # list lengths and .squeeze() semantics of NodeClassificationMPNSimple.py:81-97
+        preds_edge = [edge_logits[r].view(E, 1).squeeze() for r in range(n_rec)]
+        preds_node = [node_logits[r].view(N, 1).squeeze() for r in range(n_rec + 1)]
+        preds_class = [class_logits[r] for r in range(n_rec + 1)]
+        return preds_edge, preds_node, preds_class, [None]
+
+
+def get_mpn_model(config, **kwargs):
+    """``src/Models/MessagePassingNetwork/__init__.py:27-73`` — the hot-path model only."""
+    if config.NAME == "NodeClassificationMPN":
+        return NodeClassificationMPNSimple(config)
+    raise NotImplementedError(f"MPN NAME={config.NAME}: only NodeClassificationMPN is on the accelerated path")

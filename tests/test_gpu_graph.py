@@ -1,0 +1,81 @@
+"""GPU parity of the graph-construction kernels (pemp_detect / pack / fully / knn / edge features)
+against the reference's own outputs (tests/golden) and the CPU oracle. Bit-exact: every output of
+construct_graph is integer or an exactly-rounded fp32 value."""
+import numpy as np
+import pytest
+import torch
+
+import pemp_amd
+from oracle import restate
+from pemp_amd import config as pcfg, synthetic as syn
+from tests import golden_util as gu
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def run_gc(gc, J, hm, feats, tags, masks):
+    return pemp_amd.get_graph_constructor(
+        gc, scoremaps=hm.to(DEV), features=feats.to(DEV), tagmaps=None if tags is None else tags.to(DEV),
+        joints_gt=None, factor_list=None, masks=None if masks is None else masks.to(DEV), device=DEV,
+        testing=True, heatmaps=None, num_joints=J).construct_graph()
+
+
+@pytest.mark.parametrize("name", gu.names("gc_"))
+def test_golden(name):
+    meta, a = gu.load(name)
+    hm, feats, tags, masks = gu.gc_inputs(meta, a)
+    out = run_gc(gu.gc_config(meta), meta["J"], hm, feats, tags, masks)
+    x, ea, ei, det, sc, bi, tg = [out[i].cpu() for i in (0, 1, 2, 7, 11, 12, 14)]
+    assert all(out[i] is None for i in (3, 4, 5, 6, 8, 9, 10, 13))
+    np.testing.assert_array_equal(det.numpy(), a["joint_det"])
+    np.testing.assert_array_equal(sc.numpy(), a["joint_scores"])
+    np.testing.assert_array_equal(bi.numpy(), a["batch_index"])
+    np.testing.assert_array_equal(tg.numpy(), a["joint_tags"])
+    assert ei.dtype == torch.int64 and det.dtype == torch.int64 and ea.dtype == torch.float32
+    assert gu.sha(ei) == meta["sha_edge_index"]
+    assert gu.sha(x) == meta["sha_x"]
+    assert gu.sha(ea) == meta["sha_edge_attr"]
+
+
+CASES = [
+    # B, J, H, W, persons, variant, graph, pool, thr, mask
+    (8, 17, 640, 640, 9, "clean", "fully", 5, 0.1, False),      # C3 shape
+    (1, 14, 640, 640, 36, "clean", "fully", 5, 0.1, False),     # C5 shape (CrowdPose-dense)
+    (3, 17, 200, 328, 5, "noisy", "knn", 3, 0.1, True),         # ragged W, masks, knn
+    (2, 17, 96, 136, 1, "realistic", "fully", 5, 0.1, False),   # bilinear plateaus (4 equal maxima)
+    (2, 17, 64, 64, 2, "noisy", "fully", 3, 2.0, False),        # DETECT_THRESHOLD > 1.5 branch
+    (1, 17, 33, 17, 1, "clean", "fully", 7, 0.1, False),        # tiny, odd sizes
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}x{c[1]}x{c[2]}x{c[3]}-{c[5]}-{c[6]}" for c in CASES])
+def test_vs_oracle(case):
+    B, J, H, W, persons, variant, graph, pool, thr, mask = case
+    hm = torch.from_numpy(syn.make_heatmaps(100 + H, B, J, H, W, persons, variant=variant, margin=4))
+    feats = torch.from_numpy(syn.closed_form((B, 128, H, W), 0.25))
+    tags = torch.from_numpy(syn.closed_form((B, J, H, W, 2), 0.75))
+    masks = torch.from_numpy((np.random.default_rng(H).random((B, H, W)) > 0.1).astype(np.float32)) if mask else None
+    gc = pcfg.inference_gc_config(graph, pool, mask)
+    gc.DETECT_THRESHOLD = thr
+    out = run_gc(gc, J, hm, feats, tags, masks)
+    ref = restate.construct_graph(hm, feats, tags, masks, gc, J)
+    for i in (7, 11, 12, 14, 2, 0, 1):
+        assert torch.equal(out[i].cpu(), ref[i]), f"output {i}"
+
+
+def test_empty_image_and_overflow_growth():
+    """An all-zero image yields no detections (N=0 rows) and a crowded one grows the capacity."""
+    J, H, W = 17, 64, 64
+    hm = torch.zeros(2, J, H, W)
+    crowd = torch.from_numpy(syn.make_heatmaps(5, 1, J, H, W, persons=1, variant="noisy"))
+    crowd[0, :, ::8, ::8] = 0.5 + torch.rand(J, 8, 8)          # many isolated maxima >= thr
+    hm[1] = crowd[0]
+    feats = torch.from_numpy(syn.closed_form((2, 128, H, W), 0.25))
+    gc = pcfg.inference_gc_config("fully", 3, False)
+    out = run_gc(gc, J, hm, feats, None, None)
+    ref = restate.construct_graph(hm, feats, torch.zeros(2, J, H, W), None, gc, J)
+    assert (out[12].cpu() == 0).sum() == 0
+    for i in (7, 11, 12, 2, 1):
+        assert torch.equal(out[i].cpu(), ref[i])
+    assert out[14] is None

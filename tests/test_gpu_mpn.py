@@ -1,0 +1,124 @@
+"""GPU parity of pemp_mpn_forward (NodeClassificationMPNSimple drop-in) against the reference's own
+logits (tests/golden) and the CPU oracle. Tolerance (north_star): edge/node/class logits within
+1e-4 absolute in fp32."""
+import numpy as np
+import pytest
+import torch
+
+import pemp_amd
+from oracle import restate
+from pemp_amd import config as pcfg, synthetic as syn
+from tests import golden_util as gu
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+TOL = 1e-4
+
+
+def make_model(cfg, salt):
+    m = pemp_amd.get_mpn_model(cfg)
+    sd = syn.closed_form_state_dict(m, salt)
+    m.load_state_dict(sd)
+    return m.eval().to(DEV), sd
+
+
+def run(model, x, ea, ei, types):
+    with torch.no_grad():
+        out = model(x.to(DEV), ea.to(DEV), ei.to(DEV), node_types=types.to(DEV))
+    torch.cuda.synchronize()
+    return out
+
+
+def max_err(a, b):
+    return (a.detach().cpu().float() - b.float()).abs().max().item() if a.numel() else 0.0
+
+
+@pytest.mark.parametrize("name", gu.names("mpn_"))
+def test_golden(name):
+    meta, a = gu.load(name)
+    cfg = gu.mpn_config(meta)
+    model, _ = make_model(cfg, meta["salt"])
+    pe, pn, pc, tag = run(model, *(torch.from_numpy(a[k]) for k in ("x", "edge_attr", "edge_index", "node_types")))
+    assert tag == [None]
+    assert len(pe) == int(a["n_edge_preds"]) and len(pn) == int(a["n_node_preds"]) and len(pc) == len(pn)
+    assert max_err(pe[-1], torch.from_numpy(a["edge_logits"])) < TOL
+    assert max_err(pn[-1], torch.from_numpy(a["node_logits"])) < TOL
+    assert max_err(pc[-1], torch.from_numpy(a["class_logits"])) < TOL
+    assert torch.equal(pn[0], pn[-1]) and torch.equal(pc[0], pc[-1])
+
+
+def graph(B, J, H, W, persons, gtype="fully", seed=7):
+    hm = torch.from_numpy(syn.make_heatmaps(seed, B, J, H, W, persons))
+    feats = torch.from_numpy(syn.closed_form((B, 128, H, W), 0.25))
+    gc = pcfg.inference_gc_config(gtype, 5, False)
+    return restate.construct_graph(hm, feats, torch.zeros(B, J, H, W), None, gc, J)
+
+
+CASES = [
+    # J, B, H, W, persons, variant, steps, aux, graph
+    (17, 8, 160, 160, 9, "attn", 3, 0, "fully"),     # C3-shaped batch (N ~ 150/img)
+    (14, 1, 256, 256, 36, "attn", 3, 0, "fully"),    # C5-shaped (N ~ 500, E ~ 250k)
+    (17, 2, 128, 128, 6, "attn", 10, 2, "knn"),      # published T=10 with aux heads, knn
+    (17, 2, 128, 128, 5, "max", 3, 0, "fully"),
+    (17, 1, 128, 128, 4, "mean", 2, 0, "knn"),
+    (17, 1, 128, 128, 4, "add", 2, 1, "fully"),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"J{c[0]}-B{c[1]}-{c[5]}-T{c[6]}-{c[8]}" for c in CASES])
+def test_vs_oracle(case):
+    J, B, H, W, persons, variant, steps, aux, gtype = case
+    g = graph(B, J, H, W, persons, gtype)
+    cfg = pcfg.published_mpn_config(J, steps, variant)
+    cfg.AUX_LOSS_STEPS = aux
+    model, sd = make_model(cfg, 0.125 * steps + J)
+    x, ea, ei, types = g[0], g[1], g[2], g[7][:, 2]
+    pe, pn, pc, _ = run(model, x, ea, ei, types)
+    rpe, rpn, rpc, _ = restate.mpn_forward(sd, cfg, x, ea, ei, types)
+    assert len(pe) == len(rpe) and len(pn) == len(rpn) and len(pc) == len(rpc)
+    for a, b in zip(pe + pn + pc, rpe + rpn + rpc):
+        assert a.shape == b.shape
+        assert max_err(a, b) < TOL
+
+
+def test_permuted_edges_and_isolated_nodes():
+    """Edge order is free (the kernels sort by (source type, target)); nodes with no incoming
+    edges of a type aggregate to 0 (torch_scatter empty segment)."""
+    J = 17
+    g = graph(1, J, 96, 96, 3)
+    x, ea, ei, types = g[0], g[1], g[2], g[7][:, 2]
+    keep = torch.arange(ei.shape[1]) % 3 != 0                 # ragged in-degrees
+    ei, ea = ei[:, keep], ea[keep]
+    perm = torch.from_numpy(np.random.default_rng(0).permutation(ei.shape[1]))
+    ei, ea = ei[:, perm], ea[perm]
+    cfg = pcfg.published_mpn_config(J, 3, "attn")
+    model, sd = make_model(cfg, 3.0)
+    pe, pn, pc, _ = run(model, x, ea, ei, types)
+    rpe, rpn, rpc, _ = restate.mpn_forward(sd, cfg, x, ea, ei, types)
+    for a, b in zip(pe + pn + pc, rpe + rpn + rpc):
+        assert max_err(a, b) < TOL
+
+
+def test_no_edges():
+    J = 17
+    x = torch.from_numpy(syn.closed_form((5, 128), 1.0))
+    cfg = pcfg.published_mpn_config(J, 2, "attn")
+    model, sd = make_model(cfg, 4.0)
+    ei = torch.zeros(2, 0, dtype=torch.long)
+    ea = torch.zeros(0, J + 2)
+    types = torch.tensor([0, 3, 3, 9, 16])
+    pe, pn, pc, _ = run(model, x, ea, ei, types)
+    rpe, rpn, rpc, _ = restate.mpn_forward(sd, cfg, x, ea, ei, types)
+    assert pe[-1].numel() == 0
+    assert max_err(pn[-1], rpn[-1]) < TOL and max_err(pc[-1], rpc[-1]) < TOL
+
+
+def test_state_dict_keys_match_reference_layout():
+    cfg = pcfg.published_mpn_config(17, 10, "attn")
+    keys = list(pemp_amd.get_mpn_model(cfg).state_dict().keys())
+    assert keys[0] == "mpn_node_cls.mlp_edge.0.weight"
+    assert "mpn_node_cls.mlp_node.mlp.16.0.bias" in keys and "mpn_node_cls.attn_net.0.weight" in keys
+    assert "edge_embedding.9.weight" in keys and "node_embedding.6.bias" in keys
+    assert "classification.4.weight" in keys
+    n = sum(v.numel() for k, v in pemp_amd.get_mpn_model(cfg).state_dict().items() if "num_batches" not in k)
+    assert n >= 368_596 - 1000

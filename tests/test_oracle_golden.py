@@ -1,0 +1,45 @@
+"""The oracle restatement reproduces the reference's own outputs (tests/golden, made by
+oracle/gen_golden.py running the reference files). CPU only."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import restate
+from tests import golden_util as gu
+
+
+@pytest.mark.parametrize("name", gu.names("gc_"))
+def test_construct_graph_matches_reference(name):
+    meta, a = gu.load(name)
+    hm, feats, tags, masks = gu.gc_inputs(meta, a)
+    out = restate.construct_graph(hm, feats, tags, masks, gu.gc_config(meta), meta["J"])
+    x, ea, ei, det, sc, bi, tg = out[0], out[1], out[2], out[7], out[11], out[12], out[14]
+    assert all(out[i] is None for i in (3, 4, 5, 6, 8, 9, 10, 13))
+    np.testing.assert_array_equal(det.numpy(), a["joint_det"])
+    np.testing.assert_array_equal(sc.numpy(), a["joint_scores"])
+    np.testing.assert_array_equal(bi.numpy(), a["batch_index"])
+    np.testing.assert_array_equal(tg.numpy(), a["joint_tags"])
+    assert gu.sha(x) == meta["sha_x"]
+    assert gu.sha(ea) == meta["sha_edge_attr"]
+    assert gu.sha(ei) == meta["sha_edge_index"]
+    assert ei.dtype == torch.int64 and det.dtype == torch.int64
+
+
+@pytest.mark.parametrize("name", gu.names("mpn_"))
+def test_mpn_matches_reference(name):
+    meta, a = gu.load(name)
+    cfg = gu.mpn_config(meta)
+    sd = _state_dict(cfg, meta["salt"])
+    pe, pn, pc, tag = restate.mpn_forward(sd, cfg, torch.from_numpy(a["x"]), torch.from_numpy(a["edge_attr"]),
+                                         torch.from_numpy(a["edge_index"]), torch.from_numpy(a["node_types"]))
+    assert len(pe) == int(a["n_edge_preds"]) and len(pn) == int(a["n_node_preds"]) and tag == [None]
+    np.testing.assert_allclose(pe[-1].numpy(), a["edge_logits"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(pn[-1].numpy(), a["node_logits"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(pc[-1].numpy(), a["class_logits"], atol=1e-5, rtol=0)
+
+
+def _state_dict(cfg, salt):
+    from pemp_amd.mpn.model import NodeClassificationMPNSimple
+    from pemp_amd import synthetic as syn
+    m = NodeClassificationMPNSimple(cfg)
+    return syn.closed_form_state_dict(m, salt)
