@@ -164,6 +164,10 @@ int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weights* weights,
                      int64_t N, int64_t E, float* edge_logits, float* node_logits, float* class_logits,
                      void* workspace, size_t workspace_bytes, void* stream);
 
+/* Synchronises `stream` and reports invalid edge_index / node_types seen by the last
+ * pemp_mpn_forward on this workspace (those edges were skipped). Optional validation step. */
+int pemp_mpn_status(const pemp_mpn_desc* desc, int64_t N, int64_t E, const void* workspace, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -53,6 +53,7 @@ SIGNATURES = {
     "pemp_mpn_workspace_size": (c_sz, [ctypes.POINTER(PempMpnDesc), c_i64, c_i64]),
     "pemp_mpn_forward": (c_i32, [ctypes.POINTER(PempMpnDesc), ctypes.POINTER(PempMpnWeights), c_p, c_p, c_p, c_p,
                                  c_i64, c_i64, c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "pemp_mpn_status": (c_i32, [ctypes.POINTER(PempMpnDesc), c_i64, c_i64, c_p, c_p]),
 }
 
 _LIB = None

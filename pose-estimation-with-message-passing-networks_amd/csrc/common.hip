@@ -1,11 +1,20 @@
 // Library-level entry points: ABI version, thread-local error string, device check.
 #include <stdarg.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "pemp_common.h"
 
 namespace pemp {
 static thread_local char g_err[512] = "";
+
+bool debug_sync() {
+  static const bool on = [] {
+    const char* v = getenv("PEMP_DEBUG_SYNC");
+    return v && v[0] && v[0] != '0';
+  }();
+  return on;
+}
 
 void set_error(const char* fmt, ...) {
   va_list ap;

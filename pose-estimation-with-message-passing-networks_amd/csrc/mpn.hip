@@ -113,15 +113,21 @@ struct SegMask {
 };
 
 __device__ __forceinline__ SegMask seg_mask(int seg, int c) {
+  // every lane must execute every shuffle (a lane masked off by a short-circuit would feed
+  // garbage to the lane that reads it), so evaluate the shuffles before the comparisons
+  const int u1 = __shfl_up(seg, 1, 16), u2 = __shfl_up(seg, 2, 16);
+  const int u4 = __shfl_up(seg, 4, 16), u8 = __shfl_up(seg, 8, 16);
+  const int d1 = __shfl_down(seg, 1, 16), d2 = __shfl_down(seg, 2, 16);
+  const int d4 = __shfl_down(seg, 4, 16), d8 = __shfl_down(seg, 8, 16);
   SegMask m;
-  m.f1 = c >= 1 && __shfl_up(seg, 1, 16) == seg;
-  m.f2 = c >= 2 && __shfl_up(seg, 2, 16) == seg;
-  m.f4 = c >= 4 && __shfl_up(seg, 4, 16) == seg;
-  m.f8 = c >= 8 && __shfl_up(seg, 8, 16) == seg;
-  m.b1 = c + 1 < 16 && __shfl_down(seg, 1, 16) == seg;
-  m.b2 = c + 2 < 16 && __shfl_down(seg, 2, 16) == seg;
-  m.b4 = c + 4 < 16 && __shfl_down(seg, 4, 16) == seg;
-  m.b8 = c + 8 < 16 && __shfl_down(seg, 8, 16) == seg;
+  m.f1 = c >= 1 && u1 == seg;
+  m.f2 = c >= 2 && u2 == seg;
+  m.f4 = c >= 4 && u4 == seg;
+  m.f8 = c >= 8 && u8 == seg;
+  m.b1 = c + 1 < 16 && d1 == seg;
+  m.b2 = c + 2 < 16 && d2 == seg;
+  m.b4 = c + 4 < 16 && d4 == seg;
+  m.b8 = c + 8 < 16 && d8 == seg;
   return m;
 }
 
@@ -192,7 +198,7 @@ __global__ __launch_bounds__(256) void mpn_count_kernel(const int64_t* __restric
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t s = ei[e], d = ei[E + e];
     if (s < 0 || s >= N || d < 0 || d >= N) { atomicOr(err, 1); continue; }
-    const int64_t t = types[s];
+    const int64_t t = T == 1 ? 0 : types[s];      // MPLayer (one message MLP) ignores types
     if (t < 0 || t >= T) { atomicOr(err, 2); continue; }
     atomicAdd(&cnt[t * N + d], 1);
   }
@@ -240,12 +246,14 @@ __global__ __launch_bounds__(1024) void mpn_scan_kernel(const int* __restrict__ 
 }
 
 __global__ __launch_bounds__(256) void mpn_scatter_kernel(const int64_t* __restrict__ ei, const int64_t* __restrict__ types,
-                                                          int64_t N, int64_t E, const int* __restrict__ seg,
+                                                          int64_t N, int64_t E, int T, const int* __restrict__ seg,
                                                           int* __restrict__ cursor, int* __restrict__ perm) {
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t s = ei[e], d = ei[E + e];
     if (s < 0 || s >= N || d < 0 || d >= N) continue;
-    const int64_t key = types[s] * N + d;
+    const int64_t t = T == 1 ? 0 : types[s];
+    if (t < 0 || t >= T) continue;
+    const int64_t key = t * N + d;
     perm[seg[key] + atomicAdd(&cursor[key], 1)] = (int)e;
   }
 }
@@ -742,6 +750,7 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
   // ---- prepare: type-major order ----
   PEMP_HIP(hipMemsetAsync(ws.cnt, 0, (K + 1) * sizeof(int), st));
   PEMP_HIP(hipMemsetAsync(ws.cursor, 0, (K + 1) * sizeof(int), st));
+  PEMP_HIP(hipMemsetAsync(ws.err, 0, 4 * sizeof(int), st));
   if (E > 0) {
     hipLaunchKernelGGL(mpn_count_kernel, dim3(grid1d(E, 256)), dim3(256), 0, st, edge_index, node_types, N, E, T,
                        ws.cnt, ws.err);
@@ -750,7 +759,7 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
   hipLaunchKernelGGL(mpn_scan_kernel, dim3(1), dim3(1024), 0, st, ws.cnt, K, N, T, ws.seg, ws.wg_start);
   PEMP_LAUNCH_CHECK();
   if (E > 0) {
-    hipLaunchKernelGGL(mpn_scatter_kernel, dim3(grid1d(E, 256)), dim3(256), 0, st, edge_index, node_types, N, E,
+    hipLaunchKernelGGL(mpn_scatter_kernel, dim3(grid1d(E, 256)), dim3(256), 0, st, edge_index, node_types, N, E, T,
                        ws.seg, ws.cursor, ws.perm);
     PEMP_LAUNCH_CHECK();
     hipLaunchKernelGGL(mpn_segsort_kernel, dim3((unsigned)((K + 3) / 4)), dim3(256), 0, st, edge_index, E, K, ws.seg,
@@ -810,5 +819,17 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
   if ((rc = rows_mlp(w->node_head, ws.X + 64, 128, N, node_logits + (int64_t)rec * N, 1, nullptr, 0, st))) return rc;
   if ((rc = rows_mlp(w->class_head, ws.X + 64, 128, N, class_logits + (int64_t)rec * N * J, J, nullptr, 0, st)))
     return rc;
+  return PEMP_OK;
+}
+
+extern "C" int pemp_mpn_status(const pemp_mpn_desc* desc, int64_t N, int64_t E, const void* workspace,
+                               void* stream) {
+  PEMP_CHECK_ARG(desc && workspace, "pemp_mpn_status: null args");
+  const MpnWs ws = mpn_carve(const_cast<void*>(workspace), desc->num_types, N, E, nullptr);
+  int err = 0;
+  PEMP_HIP(hipMemcpyAsync(&err, ws.err, sizeof(int), hipMemcpyDeviceToHost, as_stream(stream)));
+  PEMP_HIP(hipStreamSynchronize(as_stream(stream)));
+  if (err & 1) { set_error("edge_index has entries outside [0, N)"); return PEMP_ERR_INVALID_ARG; }
+  if (err & 2) { set_error("node_types has entries outside [0, num_types)"); return PEMP_ERR_INVALID_ARG; }
   return PEMP_OK;
 }

@@ -29,12 +29,18 @@ void set_error(const char* fmt, ...);
     }                                                                              \
   } while (0)
 
+// PEMP_DEBUG_SYNC=1 in the environment: synchronise after every launch and report the failing
+// kernel by source line (fault localisation in one run; never on in measured runs).
+bool debug_sync();
+
 #define PEMP_LAUNCH_CHECK()                                                        \
   do {                                                                             \
     hipError_t e_ = hipGetLastError();                                             \
+    if (e_ == hipSuccess && ::pemp::debug_sync()) e_ = hipDeviceSynchronize();     \
     if (e_ != hipSuccess) {                                                        \
-      ::pemp::set_error("kernel launch failed: %s (%s:%d)", hipGetErrorString(e_), \
+      ::pemp::set_error("kernel failed: %s (%s:%d)", hipGetErrorString(e_),        \
                         __FILE__, __LINE__);                                        \
+      fprintf(stderr, "[pemp] %s\n", ::pemp_last_error());                        \
       return PEMP_ERR_HIP;                                                         \
     }                                                                              \
   } while (0)

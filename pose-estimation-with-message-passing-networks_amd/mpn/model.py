@@ -8,6 +8,7 @@ containers; ``forward`` folds them once per parameter version (eval-mode BatchNo
 Linear) and runs the whole network in ``pemp_mpn_forward`` (libpemp.so). Inference only.
 """
 import ctypes
+import os
 
 import torch
 import torch.nn as nn
@@ -174,6 +175,8 @@ class NodeClassificationMPNSimple(nn.Module):
                                       _lib.ptr(edge_index), _lib.ptr(node_types), N, E, _lib.ptr(edge_logits),
                                       _lib.ptr(node_logits), _lib.ptr(class_logits), _lib.ptr(ws), ws.numel(),
                                       _lib.stream()))
+        if kwargs.get("validate", os.environ.get("PEMP_VALIDATE", "0") not in ("", "0")):
+            _lib.check(L.pemp_mpn_status(ctypes.byref(desc), N, E, _lib.ptr(ws), _lib.stream()))
         # list lengths and .squeeze() semantics of NodeClassificationMPNSimple.py:81-97
         preds_edge = [edge_logits[r].view(E, 1).squeeze() for r in range(n_rec)]
         preds_node = [node_logits[r].view(N, 1).squeeze() for r in range(n_rec + 1)]

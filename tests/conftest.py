@@ -7,6 +7,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 sys.dont_write_bytecode = True
+os.environ.setdefault("PEMP_VALIDATE", "1")   # tests check edge_index / node_types after every MPN call
 
 
 def pytest_configure(config):
