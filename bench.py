@@ -1,0 +1,258 @@
+#!/usr/bin/env python3
+"""Hot-path throughput on MI355X: heatmaps -> keypoint graph -> MPN logits.
+
+One step = ``get_graph_constructor(...).construct_graph()`` + ``NodeClassificationMPNSimple``
+forward over one batch of synthetic 640x640 COCO-shaped inputs already resident in HBM (the
+frozen backbone is out of scope). Multi-GPU: one process per GPU (torchrun), each rank owns its
+own images (weak scaling, no data-path collective); barrier + max-over-ranks timing.
+
+Prints ONE JSON line (rank 0). Extra fields: isolated-MPN edge-updates/s, live roofline of the
+dominant kernel (hipEvents on the launch stream), and the CPU oracle baseline (rank 0, N=1).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import pemp_amd  # noqa: E402
+from pemp_amd import _lib, config as pcfg, synthetic as syn  # noqa: E402
+
+METRIC = "images/sec (640px, HRNet-w48) + MPN edge-updates/sec at 1/2/4/8 MI355X"
+WORKLOADS = {
+    # BASELINE.json configs[2] (C3): COCO-val-shaped batch of 8 at 640px, 3 MPN iterations
+    "c3": dict(B=8, J=17, H=640, W=640, persons=9, steps=3, graph="fully", variant="attn"),
+    # configs[1] (C2): one 640px image, ~150 detections, dense graph, 3 iterations
+    "c2": dict(B=1, J=17, H=640, W=640, persons=9, steps=3, graph="fully", variant="attn"),
+    # configs[4] (C5): CrowdPose-dense, ~500 detections / ~250k directed edges per image
+    "c5": dict(B=1, J=14, H=640, W=640, persons=36, steps=3, graph="fully", variant="attn"),
+}
+FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: dense f32 MFMA (= f32 vector) peak
+HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+EDGE_FLOP = 3 * 2 * 64 * 64 + 2 * 64            # per edge-update: 3 chained 64x64 GEMMs + attention
+EDGE_HEAD_FLOP = 2 * (64 * 64 + 64 * 32 + 32)   # fused edge-classification head
+EDGE_BYTES = 3 * 64 * 4 + 2 * 4                 # Q0 + e_cur read, e' write, (src, dst) int32
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    return ap.parse_args()
+
+
+def setup_dist(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", rank=rank, world_size=world,
+                                             device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return rank, world, torch.device("cuda", local if world > 1 else 0)
+
+
+def barrier(world):
+    if world > 1:
+        torch.distributed.barrier()
+
+
+def max_over_ranks(v, world, dev):
+    if world == 1:
+        return v
+    t = torch.tensor([v], dtype=torch.float64, device=dev)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(v, world, dev):
+    if world == 1:
+        return v
+    t = torch.tensor([v], dtype=torch.float64, device=dev)
+    torch.distributed.all_reduce(t)
+    return float(t.item())
+
+
+def make_inputs(wl, rank, dev):
+    B, J, H, W = wl["B"], wl["J"], wl["H"], wl["W"]
+    hm = torch.from_numpy(syn.make_heatmaps(1000 + rank, B, J, H, W, wl["persons"])).to(dev)
+    g = torch.Generator(device=dev).manual_seed(77 + rank)
+    feats = torch.rand(B, 128, H, W, generator=g, device=dev) * 2 - 1
+    tags = torch.rand(B, J, H, W, 1, generator=g, device=dev)
+    return hm, feats, tags
+
+
+def make_model(wl, dev):
+    cfg = pcfg.published_mpn_config(wl["J"], wl["steps"], wl["variant"])
+    model = pemp_amd.get_mpn_model(cfg)
+    model.load_state_dict(syn.closed_form_state_dict(model, 0.5))
+    return model.eval().to(dev), cfg
+
+
+def run_step(wl, gc, model, hm, feats, tags, dev):
+    out = pemp_amd.get_graph_constructor(gc, scoremaps=hm, features=feats, tagmaps=tags, joints_gt=None,
+                                         factor_list=None, masks=None, device=dev, testing=True, heatmaps=None,
+                                         num_joints=wl["J"]).construct_graph()
+    pe, pn, pc, _ = model(out[0], out[1], out[2], node_types=out[7][:, 2])
+    return out, pe, pn, pc
+
+
+def roofline_for(label, stats, E, wl):
+    if label not in stats:
+        return None
+    n, ms = stats[label]
+    avg_s = ms / n / 1e3
+    B, J, H, W = wl["B"], wl["J"], wl["H"], wl["W"]
+    if label.startswith("edge_step"):
+        flop = E * (EDGE_FLOP + (EDGE_HEAD_FLOP if label == "edge_step_head" else 0))
+        ach = flop / avg_s / 1e12
+        return {"kernel": label, "bound": "mfma", "achieved": round(ach, 3), "peak": FP32_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                "avg_launch_us": round(avg_s * 1e6, 2), "launches": n,
+                "algorithmic": f"{EDGE_FLOP} FLOP x E={E} edges per launch",
+                "hbm_GBs_algorithmic": round(E * EDGE_BYTES / avg_s / 1e9, 1)}
+    if label == "detect_nms":
+        byts = B * J * H * W * 4 + B * J * H * ((W + 63) // 64) * 8
+        ach = byts / avg_s / 1e9
+        return {"kernel": label, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "avg_launch_us": round(avg_s * 1e6, 2),
+                "launches": n, "algorithmic": f"{byts} B per launch (heatmap read + bitmask write)"}
+    return {"kernel": label, "avg_launch_us": round(avg_s * 1e6, 2), "launches": n}
+
+
+def cpu_baseline(wl, gc, model, hm, feats, tags, budget_s):
+    """The oracle restatement (torch CPU fp32) on one image at a time of the same workload."""
+    from oracle import restate
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    mcfg = pcfg.published_mpn_config(wl["J"], wl["steps"], wl["variant"])
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    imgs, t_used, b = 0, 0.0, 0
+    while t_used < budget_s and imgs < 64:
+        i = b % wl["B"]
+        h, f, tg = hm[i:i + 1].cpu(), feats[i:i + 1].cpu(), tags[i:i + 1].cpu()
+        t0 = time.perf_counter()
+        g = restate.construct_graph(h, f, tg, None, gc, wl["J"])
+        restate.mpn_forward(sd, mcfg, g[0], g[1], g[2], g[7][:, 2])
+        t_used += time.perf_counter() - t0
+        imgs += 1
+        b += 1
+    return {"value": round(imgs / t_used, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{imgs} images of the {wl['B']}-image workload, one at a time, {t_used:.1f}s "
+                      f"(oracle/restate.py: construct_graph + mpn_forward, torch CPU fp32)",
+            "cpu_model": _cpu_model()}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    rank, world, dev = setup_dist(args.gpus)
+    wl = WORKLOADS[args.workload]
+    gc = pcfg.inference_gc_config(wl["graph"], 5, False)
+    hm, feats, tags = make_inputs(wl, rank, dev)
+    model, _ = make_model(wl, dev)
+    _lib.lib()
+
+    # warmup (also finds the dominant kernel with the profiler on for every kernel)
+    dominant = None
+    for w in range(max(args.warmup, 1)):
+        if w == max(args.warmup, 1) - 1 and not args.no_roofline:
+            _lib.prof_enable("*")
+        out, pe, pn, pc = run_step(wl, gc, model, hm, feats, tags, dev)
+    torch.cuda.synchronize()
+    N, E = int(out[0].shape[0]), int(out[2].shape[1])
+    if not args.no_roofline:
+        stats = _lib.prof_report()
+        _lib.prof_enable(None)
+        totals = {k: v[1] for k, v in stats.items()}
+        dominant = max(totals, key=totals.get) if totals else None
+        breakdown = {k: round(v[1] / v[0] * 1e3, 2) for k, v in stats.items()}
+
+    # timed region
+    if dominant:
+        _lib.prof_enable(dominant)
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run_step(wl, gc, model, hm, feats, tags, dev)
+    torch.cuda.synchronize()
+    barrier(world)
+    dt = time.perf_counter() - t0
+    stats_timed = _lib.prof_report() if dominant else {}
+    _lib.prof_enable(None)
+    dt_max = max_over_ranks(dt, world, dev)
+    imgs = wl["B"] * args.steps * world
+    value = imgs / dt_max
+    E_all = sum_over_ranks(E, world, dev)
+
+    # isolated MPN (same graphs): edge-updates/s
+    x, ea, ei, types = out[0], out[1], out[2], out[7][:, 2]
+    with torch.no_grad():
+        for _ in range(2):
+            model(x, ea, ei, node_types=types)
+    barrier(world)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    with torch.no_grad():
+        for _ in range(args.steps):
+            model(x, ea, ei, node_types=types)
+    torch.cuda.synchronize()
+    barrier(world)
+    dt_mpn = max_over_ranks(time.perf_counter() - t1, world, dev)
+    mpn_eups = E_all * wl["steps"] * args.steps / dt_mpn
+
+    roof = roofline_for(dominant, stats_timed, E, wl) if dominant else None
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(wl, gc, model, hm, feats, tags, args.cpu_seconds)
+
+    if rank == 0:
+        rec = {
+            "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt_max / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (seeded planted-Gaussian heatmaps, random features; closed-form MPN weights)",
+            "config": {"workload": f"{args.workload}: {wl['B']}x{wl['J']}x{wl['H']}x{wl['W']} heatmaps/GPU -> "
+                                   f"{wl['graph']} graph -> MPN TypeAware-attn T={wl['steps']}",
+                       "images_per_gpu": wl["B"], "global_batch": wl["B"] * world, "persons_per_image": wl["persons"],
+                       "nodes_per_gpu": N, "edges_per_gpu": E, "parallelism": f"image-sharded x{world}"},
+            "mpn_edge_updates_per_sec": round(mpn_eups, 1),
+            "mpn_ms_per_step": round(dt_mpn / args.steps * 1e3, 3),
+            "pipeline_edge_updates_per_sec": round(E_all * wl["steps"] * args.steps / dt_max, 1),
+            "roofline": roof,
+            "kernel_avg_us": breakdown if not args.no_roofline else None,
+            "cpu_baseline": cpu,
+        }
+        if cpu:
+            rec["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

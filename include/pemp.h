@@ -168,6 +168,14 @@ int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weights* weights,
  * pemp_mpn_forward on this workspace (those edges were skipped). Optional validation step. */
 int pemp_mpn_status(const pemp_mpn_desc* desc, int64_t N, int64_t E, const void* workspace, void* stream);
 
+/* Opt-in profiler: while enabled, hipEvents are recorded on the launch stream around every kernel
+ * whose label contains `filter` ("*" = all, NULL or "" = off). pemp_prof_report synchronises those
+ * events and writes "label count total_ms" lines into buf (returns the full length), then resets.
+ * Labels: detect_nms, detect_select, pack_nodes, fully_graph, edge_features, knn_adj, knn_emit,
+ * mpn_prepare, node_embed, edge_embed, node_table, edge_step, edge_step_head, node_update, heads. */
+int pemp_prof_enable(const char* filter);
+int pemp_prof_report(char* buf, size_t len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -54,6 +54,8 @@ SIGNATURES = {
     "pemp_mpn_forward": (c_i32, [ctypes.POINTER(PempMpnDesc), ctypes.POINTER(PempMpnWeights), c_p, c_p, c_p, c_p,
                                  c_i64, c_i64, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "pemp_mpn_status": (c_i32, [ctypes.POINTER(PempMpnDesc), c_i64, c_i64, c_p, c_p]),
+    "pemp_prof_enable": (c_i32, [ctypes.c_char_p]),
+    "pemp_prof_report": (c_i32, [ctypes.c_char_p, c_sz]),
 }
 
 _LIB = None
@@ -118,3 +120,19 @@ class Workspace:
         if self.buf is None or self.buf.numel() < nbytes or self.buf.device != device:
             self.buf = torch.empty(nbytes + (nbytes >> 3), dtype=torch.uint8, device=device)
         return self.buf
+
+
+def prof_enable(filt):
+    lib().pemp_prof_enable(None if filt is None else filt.encode())
+
+
+def prof_report():
+    """{label: (launches, total_ms)} for the kernels recorded since the last report (syncs)."""
+    L = lib()
+    buf = ctypes.create_string_buffer(1 << 16)
+    L.pemp_prof_report(buf, len(buf))
+    out = {}
+    for line in buf.value.decode().splitlines():
+        name, cnt, ms = line.split()
+        out[name] = (int(cnt), float(ms))
+    return out

@@ -3,6 +3,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
 #include "pemp_common.h"
 
 namespace pemp {
@@ -22,7 +27,86 @@ void set_error(const char* fmt, ...) {
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
 }
+
+// ---- opt-in event profiler: hipEvents recorded on the launch stream around selected kernels ----
+namespace {
+struct Pending {
+  std::string label;
+  hipEvent_t a, b;
+};
+std::mutex g_prof_mu;
+std::string g_prof_filter;
+std::vector<Pending> g_pending;
+std::vector<hipEvent_t> g_pool;
+struct Agg {
+  long count = 0;
+  double ms = 0.0;
+};
+std::map<std::string, Agg> g_agg;
+
+hipEvent_t take_event() {
+  if (!g_pool.empty()) {
+    hipEvent_t e = g_pool.back();
+    g_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+}  // namespace
+
+ProfScope::ProfScope(const char* label, hipStream_t st) : st_(st), slot_(-1) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  if (g_prof_filter.empty()) return;
+  if (g_prof_filter != "*" && std::string(label).find(g_prof_filter) == std::string::npos) return;
+  Pending p{label, take_event(), take_event()};
+  if (!p.a || !p.b) return;
+  (void)hipEventRecord(p.a, st);
+  g_pending.push_back(p);
+  slot_ = (int)g_pending.size() - 1;
+}
+
+ProfScope::~ProfScope() {
+  if (slot_ < 0) return;
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  (void)hipEventRecord(g_pending[slot_].b, st_);
+}
+
 }  // namespace pemp
+
+extern "C" int pemp_prof_enable(const char* filter) {
+  std::lock_guard<std::mutex> lk(pemp::g_prof_mu);
+  pemp::g_prof_filter = filter ? filter : "";
+  return PEMP_OK;
+}
+
+extern "C" int pemp_prof_report(char* buf, size_t len) {
+  std::lock_guard<std::mutex> lk(pemp::g_prof_mu);
+  for (auto& p : pemp::g_pending) {
+    float ms = 0.f;
+    PEMP_HIP(hipEventSynchronize(p.b));
+    PEMP_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+    auto& a = pemp::g_agg[p.label];
+    a.count += 1;
+    a.ms += ms;
+    pemp::g_pool.push_back(p.a);
+    pemp::g_pool.push_back(p.b);
+  }
+  pemp::g_pending.clear();
+  std::string out;
+  char line[160];
+  for (auto& kv : pemp::g_agg) {
+    snprintf(line, sizeof(line), "%s %ld %.6f\n", kv.first.c_str(), kv.second.count, kv.second.ms);
+    out += line;
+  }
+  pemp::g_agg.clear();
+  if (buf && len) {
+    strncpy(buf, out.c_str(), len - 1);
+    buf[len - 1] = 0;
+  }
+  return (int)out.size();
+}
 
 extern "C" int pemp_abi_version(void) { return PEMP_ABI_VERSION; }
 

@@ -378,12 +378,14 @@ static int launch_detect(const float* s, const float* masks, const DetectGeom& g
                          hipStream_t st) {
   if (stages & PEMP_DETECT_NMS) {
     const size_t lds = (size_t)((TR + 2 * g.p) + TR) * (TC + 2 * g.p) * sizeof(float);
+    ProfScope prof("detect_nms", st);
     hipLaunchKernelGGL(nms_tiles_kernel<KMAX>, dim3(g.tiles, g.J, g.B), dim3(NT1), lds, st, s, masks, g, thr,
                        use_thr, w.cand_v, w.cand_i, w.tile_count, w.bits);
     PEMP_LAUNCH_CHECK();
   }
   if (stages & PEMP_DETECT_SELECT) {
     const size_t lds = (size_t)2 * g.J * g.S * sizeof(int);
+    ProfScope prof("detect_select", st);
     hipLaunchKernelGGL(select_kernel<KMAX>, dim3(g.B), dim3(NT2), lds, st, s, masks, g, thr, use_thr, w.cand_v,
                        w.cand_i, w.tile_count, w.bits, det, scores, (int*)n_det, cap);
     PEMP_LAUNCH_CHECK();

@@ -306,6 +306,7 @@ extern "C" int pemp_pack_nodes(const float* features, int C, const float* tagmap
   PEMP_CHECK_ARG(C > 0 && B > 0 && J > 0 && H > 0 && W > 0 && n_total >= 0, "pemp_pack_nodes: bad shape");
   PEMP_CHECK_ARG(!tagmaps || (joint_tags && F > 0 && F <= C), "pemp_pack_nodes: tags need F in [1, C]");
   if (n_total == 0) return PEMP_OK;
+  ProfScope prof("pack_nodes", as_stream(stream));
   hipLaunchKernelGGL(pack_nodes_kernel, dim3(grid_for(n_total * C, 256)), dim3(256), 0, as_stream(stream), features,
                      C, tagmaps, F, B, J, H, W, det_xyt, det_scores, cap, node_off, n_total, x, joint_det,
                      joint_scores, batch_index, joint_tags);
@@ -317,6 +318,7 @@ extern "C" int pemp_fully_graph(const int64_t* node_off, const int64_t* edge_off
                                 int64_t* edge_index, void* stream) {
   PEMP_CHECK_ARG(node_off && edge_off && edge_index && B > 0 && e_total >= 0, "pemp_fully_graph: bad args");
   if (e_total == 0) return PEMP_OK;
+  ProfScope prof("fully_graph", as_stream(stream));
   hipLaunchKernelGGL(fully_graph_kernel, dim3(grid_for(e_total, 256)), dim3(256), 0, as_stream(stream), node_off,
                      edge_off, B, e_total, edge_index);
   PEMP_LAUNCH_CHECK();
@@ -336,6 +338,7 @@ extern "C" int pemp_edge_features(const int64_t* joint_det, const int64_t* edge_
     default: set_error("pemp_edge_features: unknown mode %d", mode); return PEMP_ERR_INVALID_ARG;
   }
   if (e_total == 0) return PEMP_OK;
+  ProfScope prof("edge_features", as_stream(stream));
   hipLaunchKernelGGL(edge_features_kernel, dim3(grid_for(e_total * A, 256)), dim3(256), 0, as_stream(stream),
                      joint_det, edge_index, e_total, J, norm_factor, mode, A, edge_attr);
   PEMP_LAUNCH_CHECK();
@@ -369,6 +372,7 @@ extern "C" int pemp_knn_graph_count(const int64_t* joint_det, const int64_t* nod
   PEMP_HIP(hipMemsetAsync(w.adjt, 0, words * sizeof(unsigned long long), st));
   const int64_t n_total = node_off_host[B];
   if (n_total > 0) {
+    ProfScope prof("knn_adj", st);
     hipLaunchKernelGGL(knn_adj_kernel, dim3((unsigned)((n_total + 3) / 4)), dim3(256), 0, st, joint_det, node_off, B,
                        n_total, k + 1, w.mat_off, w.adj, w.adjt);
     PEMP_LAUNCH_CHECK();
@@ -391,6 +395,7 @@ extern "C" int pemp_knn_graph_emit(const int64_t* node_off, const int64_t* node_
   }
   const KnnWs w = knn_carve(workspace, node_off_host, B, nullptr);
   if (e_total == 0) return PEMP_OK;
+  ProfScope prof("knn_emit", as_stream(stream));
   hipLaunchKernelGGL(knn_emit_kernel, dim3(B), dim3(1024), 0, as_stream(stream), node_off, B, w.mat_off, w.adj,
                      w.adjt, edge_off, e_total, edge_index);
   PEMP_LAUNCH_CHECK();

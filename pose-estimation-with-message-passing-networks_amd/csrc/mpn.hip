@@ -674,9 +674,10 @@ static void launch_edge_step(const EdgeStepArgs& a, bool head, int grid, hipStre
     hipLaunchKernelGGL((edge_step_kernel<AGG, false>), dim3(grid), dim3(256), lds, st, a);
 }
 
-static int rows_mlp(const pemp_mlp& m, const float* in, int64_t ld_in, int64_t M, float* out, int64_t ld_out,
-                    float* out2, int64_t ld_out2, hipStream_t st) {
+static int rows_mlp(const char* label, const pemp_mlp& m, const float* in, int64_t ld_in, int64_t M, float* out,
+                    int64_t ld_out, float* out2, int64_t ld_out2, hipStream_t st) {
   if (M <= 0) return PEMP_OK;
+  ProfScope prof(label, st);
   RowsMlpArgs a{m, in, ld_in, M, out, ld_out, out2, ld_out2};
   hipLaunchKernelGGL(rows_mlp_kernel, dim3((unsigned)((M + 15) / 16)), dim3(256), 0, st, a);
   PEMP_LAUNCH_CHECK();
@@ -748,6 +749,8 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
   const int64_t K = (int64_t)T * N;
 
   // ---- prepare: type-major order ----
+  {
+  ProfScope prof("mpn_prepare", st);
   PEMP_HIP(hipMemsetAsync(ws.cnt, 0, (K + 1) * sizeof(int), st));
   PEMP_HIP(hipMemsetAsync(ws.cursor, 0, (K + 1) * sizeof(int), st));
   PEMP_HIP(hipMemsetAsync(ws.err, 0, 4 * sizeof(int), st));
@@ -766,11 +769,13 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
                        ws.perm, ws.s_src, ws.s_dst, ws.s_orig);
     PEMP_LAUNCH_CHECK();
   }
+  }
 
   // ---- embeddings ----
-  int rc = rows_mlp(w->node_emb, x, desc->node_in_dim, N, ws.X, 128, ws.X + 64, 128, st);
+  int rc = rows_mlp("node_embed", w->node_emb, x, desc->node_in_dim, N, ws.X, 128, ws.X + 64, 128, st);
   if (rc) return rc;
   if (E > 0) {
+    ProfScope prof("edge_embed", st);
     hipLaunchKernelGGL(edge_embed_kernel, dim3((unsigned)((E + 63) / 64)), dim3(256), 0, st, w->edge_emb, edge_attr,
                        desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, ws.EA, ws.Q0);
     PEMP_LAUNCH_CHECK();
@@ -785,9 +790,12 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
   int rec = 0;
   for (int it = 0; it < steps; ++it) {
     const bool record = it >= steps - aux - 1;
+    {
+    ProfScope prof("node_table", st);
     hipLaunchKernelGGL(rows_linear_kernel, dim3((unsigned)((N + 15) / 16), (unsigned)((NO + 63) / 64)), dim3(256), 0,
                        st, ws.X, N, w->pre_w, w->pre_b, NO, ws.NT);
     PEMP_LAUNCH_CHECK();
+    }
     if (E > 0) {
       EdgeStepArgs ea{};
       ea.N = N; ea.E = E; ea.T = T; ea.t_nt_ld = NO;
@@ -797,6 +805,7 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
       ea.attn_b = w->attn_b; ea.agg = ws.agg; ea.head = w->edge_head;
       ea.edge_logits = record ? edge_logits + (int64_t)rec * E : nullptr;
       ea.write_next = it + 1 < steps;
+      ProfScope prof(record ? "edge_step_head" : "edge_step", st);
       switch (desc->aggr) {
         case PEMP_AGGR_ATTN: launch_edge_step<PEMP_AGGR_ATTN>(ea, record, edge_grid, st); break;
         case PEMP_AGGR_SUM: launch_edge_step<PEMP_AGGR_SUM>(ea, record, edge_grid, st); break;
@@ -805,19 +814,22 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
       }
       PEMP_LAUNCH_CHECK();
     }
+    {
+    ProfScope prof("node_update", st);
     hipLaunchKernelGGL(node_update_kernel, dim3((unsigned)((N + 15) / 16)), dim3(512), 0, st, ws.agg, ws.cnt, T, N,
                        w->upd_w, w->upd_b, ws.X);
     PEMP_LAUNCH_CHECK();
+    }
     if (record) {
-      if ((rc = rows_mlp(w->node_head, ws.X + 64, 128, N, node_logits + (int64_t)rec * N, 1, nullptr, 0, st))) return rc;
-      if ((rc = rows_mlp(w->class_head, ws.X + 64, 128, N, class_logits + (int64_t)rec * N * J, J, nullptr, 0, st)))
+      if ((rc = rows_mlp("heads", w->node_head, ws.X + 64, 128, N, node_logits + (int64_t)rec * N, 1, nullptr, 0, st))) return rc;
+      if ((rc = rows_mlp("heads", w->class_head, ws.X + 64, 128, N, class_logits + (int64_t)rec * N * J, J, nullptr, 0, st)))
         return rc;
       ++rec;
     }
     float* tmp = e_cur; e_cur = e_nxt; e_nxt = tmp;
   }
-  if ((rc = rows_mlp(w->node_head, ws.X + 64, 128, N, node_logits + (int64_t)rec * N, 1, nullptr, 0, st))) return rc;
-  if ((rc = rows_mlp(w->class_head, ws.X + 64, 128, N, class_logits + (int64_t)rec * N * J, J, nullptr, 0, st)))
+  if ((rc = rows_mlp("heads", w->node_head, ws.X + 64, 128, N, node_logits + (int64_t)rec * N, 1, nullptr, 0, st))) return rc;
+  if ((rc = rows_mlp("heads", w->class_head, ws.X + 64, 128, N, class_logits + (int64_t)rec * N * J, J, nullptr, 0, st)))
     return rc;
   return PEMP_OK;
 }

@@ -45,6 +45,17 @@ bool debug_sync();
     }                                                                              \
   } while (0)
 
+// RAII: records a hipEvent pair around a launch when the profiler is enabled for `label`.
+class ProfScope {
+ public:
+  ProfScope(const char* label, hipStream_t st);
+  ~ProfScope();
+
+ private:
+  hipStream_t st_;
+  int slot_;
+};
+
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
