@@ -20,7 +20,10 @@ namespace {
 constexpr int TR = 32;    // tile rows (= strip height)
 constexpr int TC = 128;   // tile cols (multiple of 64: a tile owns whole bitmask words)
 constexpr int NT1 = 256;  // stage-1 threads: 32 rows x 8 threads x 16 px
-constexpr int MAXR = 7;   // max pool radius (POOL_KERNEL_SIZE <= 15)
+#ifndef NMS_MIN_WAVES
+#define NMS_MIN_WAVES 4
+#endif
+constexpr int MAXR = 4;   // max pool radius (POOL_KERNEL_SIZE <= 9)
 constexpr int NT2 = 1024; // stage-2 threads
 constexpr int MAXJ = 32;
 
@@ -44,7 +47,7 @@ static DetectGeom geom(int B, int J, int H, int W, int pool_k, int K) {
 }
 
 struct DetectWs {
-  float* cand_v; int* cand_i; int* tile_count; unsigned long long* bits;
+  float *cand_v, *neg_v; int *cand_i, *neg_i, *tile_count, *tile_nonneg; unsigned long long* bits;
 };
 
 static DetectWs carve(void* base, const DetectGeom& g, size_t* bytes) {
@@ -53,114 +56,241 @@ static DetectWs carve(void* base, const DetectGeom& g, size_t* bytes) {
   size_t ncand = (size_t)g.B * g.J * g.tiles * 4 * g.K;
   w.cand_v = c.take<float>(ncand);
   w.cand_i = c.take<int>(ncand);
-  w.tile_count = c.take<int>((size_t)g.B * g.J * g.tiles);
+  w.neg_v = c.take<float>(ncand);
+  w.neg_i = c.take<int>(ncand);
+  w.tile_count = c.take<int>((size_t)g.B * g.J * g.tiles * 4);
+  w.tile_nonneg = c.take<int>((size_t)g.B * g.J * g.tiles * 4);
   w.bits = c.take<unsigned long long>((size_t)g.B * g.J * g.H * g.WW);
   if (bytes) *bytes = c.used;
   return w;
 }
 
-template <int KMAX>
-__global__ __launch_bounds__(NT1) void nms_tiles_kernel(
-    const float* __restrict__ s, const float* __restrict__ masks, DetectGeom g, float thr, int use_thr,
-    float* __restrict__ cand_v, int* __restrict__ cand_i, int* __restrict__ tile_count,
-    unsigned long long* __restrict__ bits) {
-  extern __shared__ float lds[];
-  __shared__ int wave_cnt[NT1 / 64];
-  const int tile = blockIdx.x, t = blockIdx.y, b = blockIdx.z;
+// Stage 1 (persistent): a workgroup walks tiles tl = blockIdx.x, +gridDim.x, ...; the next tile's
+// global loads are issued into registers before the current tile is processed. Tile = 32 rows x
+// 128 cols of one plane; LDS holds rows y0-P..y0+31+P, columns x0-4..x0+131 (P <= 4) at a
+// conflict-free row stride. A thread owns 16 consecutive pixels of one row.
+//
+// Candidates (exact):
+//   MODE_POS (threshold set in use): per tile the top-K of the POSITIVE values. Zero-valued top-k
+//     entries are never emitted, and negatives can enter a plane's top-k only when the plane has
+//     fewer than K non-negative pixels, so the tile also reports its non-negative count and, when
+//     that count is below K, the top-K of its negative values.
+//   MODE_ALL (DETECT_THRESHOLD > 1.5: every top-k entry is emitted as value + 1e-10): the exact
+//     top-K of all pixels.
+constexpr int HALO = 4;                   // staged columns on each side (>= P)
+constexpr int LQ = (TC + 2 * HALO) / 4;   // 34 float4 quads per staged row
+constexpr int LS = 140;                   // LDS row stride (floats): ds_read_b128 conflict-free here
+constexpr int INV = 0x7fffffff;
+enum { MODE_POS = 0, MODE_ALL = 1 };
+
+template <int CTRL>
+__device__ __forceinline__ void dpp_better(float& v, int& i) {
+  const float ov = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xF, 0xF, false));
+  const int oi = __builtin_amdgcn_update_dpp(i, i, CTRL, 0xF, 0xF, false);
+  if (better(ov, oi, v, i)) { v = ov; i = oi; }
+}
+
+// wave-wide argmax under (value desc, index asc); result is wave-uniform
+__device__ __forceinline__ void wave_best(float& v, int& i) {
+  dpp_better<0xB1>(v, i);    // quad_perm [1,0,3,2]
+  dpp_better<0x4E>(v, i);    // quad_perm [2,3,0,1]
+  dpp_better<0x141>(v, i);   // row_half_mirror
+  dpp_better<0x140>(v, i);   // row_mirror  -> every lane holds its 16-lane row's best
+  float bv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  int bi = __builtin_amdgcn_readlane(i, 0);
+#pragma unroll
+  for (int r = 1; r < 4; ++r) {
+    const float rv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16 * r));
+    const int ri = __builtin_amdgcn_readlane(i, 16 * r);
+    if (better(rv, ri, bv, bi)) { bv = rv; bi = ri; }
+  }
+  v = bv;
+  i = bi;
+}
+
+// K rounds: pop the wave's best among the lane's 16 values that pass `keep`; the winner lane
+// removes the value and rescans. Writes out_v/out_i[k] (sentinels once exhausted).
+template <typename Keep>
+__device__ __forceinline__ void wave_topk(float (&v)[16], int base_id, int K, Keep keep, float* out_v, int* out_i) {
+  const int lane = threadIdx.x & 63;
+  float lbv = -INFINITY;
+  int lbj = -1;
+#pragma unroll
+  for (int j = 0; j < 16; ++j)
+    if (keep(v[j]) && (lbj < 0 || v[j] > lbv)) { lbv = v[j]; lbj = j; }
+  for (int k = 0; k < K; ++k) {
+    float bv = lbj < 0 ? -INFINITY : lbv;
+    int bi = lbj < 0 ? INV : base_id + lbj;
+    wave_best(bv, bi);
+    if (lane == 0) { out_v[k] = bv; out_i[k] = bi; }
+    if (bi == INV) {                               // wave exhausted: fill with sentinels
+      for (int k2 = k + 1; k2 < K; ++k2)
+        if (lane == 0) { out_v[k2] = -INFINITY; out_i[k2] = INV; }
+      break;
+    }
+    if (lbj >= 0 && bi == base_id + lbj) {        // this lane owned the winner
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (j == lbj) v[j] = NAN;                  // removed (fails every keep predicate)
+      lbj = -1;
+      lbv = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (keep(v[j]) && (lbj < 0 || v[j] > lbv)) { lbv = v[j]; lbj = j; }
+    }
+  }
+}
+
+template <int P, bool VEC>
+__device__ __forceinline__ void load_tile(const float* __restrict__ s, const DetectGeom& g, int tl,
+                                          float4 (&q)[((TR + 2 * P) * LQ + NT1 - 1) / NT1]) {
+  constexpr int LH = TR + 2 * P;
+  constexpr int NQ = (LH * LQ + NT1 - 1) / NT1;
+  const int tile = tl % g.tiles, plane_i = tl / g.tiles;
   const int ty = tile / g.tiles_x, tx = tile - ty * g.tiles_x;
-  const int y0 = ty * TR, x0 = tx * TC;
-  const int p = g.p, H = g.H, W = g.W;
-  const int LW = TC + 2 * p, LH = TR + 2 * p;
-  float* in = lds;
-  float* vm = lds + LH * LW;
-  const float* plane = s + (size_t)(b * g.J + t) * H * W;
-
-  // stage tile + halo (-inf outside the plane, as MaxPool2d's implicit padding)
-  for (int idx = threadIdx.x; idx < LH * LW; idx += NT1) {
-    const int r = idx / LW, c = idx - r * LW;
-    const int y = y0 - p + r, x = x0 - p + c;
-    in[idx] = (y >= 0 && y < H && x >= 0 && x < W) ? plane[(size_t)y * W + x] : -INFINITY;
-  }
-  __syncthreads();
-  // vertical max over 2p+1 rows
-  for (int idx = threadIdx.x; idx < TR * LW; idx += NT1) {
-    const int r = idx / LW, c = idx - r * LW;
-    float m = in[r * LW + c];
-    for (int d = 1; d <= 2 * p; ++d) m = fmaxf(m, in[(r + d) * LW + c]);
-    vm[idx] = m;
-  }
-  __syncthreads();
-
-  const int r = threadIdx.x >> 3, cb = (threadIdx.x & 7) * 16;
-  const int y = y0 + r;
-  float tv[KMAX];
-  int ti[KMAX];
+  const int y0 = ty * TR, x0 = tx * TC, H = g.H, W = g.W;
+  const float* plane = s + (size_t)plane_i * H * W;
 #pragma unroll
-  for (int q = 0; q < KMAX; ++q) { tv[q] = -INFINITY; ti[q] = 0x7fffffff; }
-  unsigned int mybits = 0;
-  if (y < H) {
-    const float* mrow = masks ? masks + ((size_t)b * H + y) * W : nullptr;
-    for (int j = 0; j < 16; ++j) {
-      const int c = cb + j, x = x0 + c;
-      if (x >= W) break;
-      float m = vm[r * LW + c];
-      for (int d = 1; d <= 2 * p; ++d) m = fmaxf(m, vm[r * LW + c + d]);
-      const float sv = in[(r + p) * LW + c + p];
-      float jm = (m == sv) ? 1.0f : 0.0f;
-      if (mrow) jm = jm * mrow[x];
-      const float v = sv * jm;
-      const bool bit = use_thr && !(v < thr) && (v != 0.0f);
-      mybits |= (unsigned)bit << j;
-      float cv = v;
-      int ci = y * W + x;
+  for (int u = 0; u < NQ; ++u) {
+    const int idx = threadIdx.x + u * NT1;
+    const int r = idx / LQ, c4 = idx - r * LQ;
+    const int y = y0 - P + r, x = x0 - HALO + 4 * c4;
+    const bool yok = idx < LH * LQ && y >= 0 && y < H;
+    const float* row = plane + (size_t)min(max(y, 0), H - 1) * W;   // clamped: always a valid address
+    float4 v;
+    if (VEC) {
+      // W % 4 == 0: a quad is entirely inside or entirely outside the row
+      v = *reinterpret_cast<const float4*>(row + min(max(x, 0), W - 4));
+      const bool ok = yok && x >= 0 && x < W;
+      if (!ok) v = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    } else {
+      const float a0 = row[min(max(x, 0), W - 1)], a1 = row[min(max(x + 1, 0), W - 1)];
+      const float a2 = row[min(max(x + 2, 0), W - 1)], a3 = row[min(max(x + 3, 0), W - 1)];
+      v.x = (yok && x >= 0 && x < W) ? a0 : -INFINITY;
+      v.y = (yok && x + 1 >= 0 && x + 1 < W) ? a1 : -INFINITY;
+      v.z = (yok && x + 2 >= 0 && x + 2 < W) ? a2 : -INFINITY;
+      v.w = (yok && x + 3 >= 0 && x + 3 < W) ? a3 : -INFINITY;
+    }
+    q[u] = v;
+  }
+}
+
+// Per tile: two block barriers (stage the tile, then each wave works on its own 8-row strip:
+// vertical max, horizontal max, v, threshold bits, top-k). Each wave writes its own candidate
+// list (K entries) and counts: per tile 4 lists.
+template <int P, int MODE, bool VEC, bool MASKED>
+__global__ __launch_bounds__(NT1, NMS_MIN_WAVES) void nms_tiles_kernel(
+    const float* __restrict__ s, const float* __restrict__ masks, DetectGeom g, float thr, int use_thr,
+    float* __restrict__ cand_v, int* __restrict__ cand_i, float* __restrict__ neg_v, int* __restrict__ neg_i,
+    int* __restrict__ tile_count, int* __restrict__ tile_nonneg, unsigned long long* __restrict__ bits) {
+  constexpr int LH = TR + 2 * P;
+  constexpr int NQ = (LH * LQ + NT1 - 1) / NT1;
+  __shared__ __attribute__((aligned(16))) float in[LH * LS];
+  __shared__ __attribute__((aligned(16))) float vmax[TR * LS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int total = g.B * g.J * g.tiles;
+  const int H = g.H, W = g.W, K = g.K;
+  int tl = blockIdx.x;
+  float4 q[NQ];
+  if (tl < total) load_tile<P, VEC>(s, g, tl, q);
+  for (; tl < total; tl += gridDim.x) {
+    const int tile = tl % g.tiles, plane_i = tl / g.tiles, b = plane_i / g.J;
+    const int ty = tile / g.tiles_x, tx = tile - ty * g.tiles_x;
+    const int y0 = ty * TR, x0 = tx * TC;
+    __syncthreads();                               // previous tile's readers of `in` are done
 #pragma unroll
-      for (int q = 0; q < KMAX; ++q) {
-        if (better(cv, ci, tv[q], ti[q])) {
-          const float sv2 = tv[q]; const int si2 = ti[q];
-          tv[q] = cv; ti[q] = ci; cv = sv2; ci = si2;
-        }
+    for (int u = 0; u < NQ; ++u) {
+      const int idx = threadIdx.x + u * NT1;
+      if (idx < LH * LQ) {
+        const int r = idx / LQ, c4 = idx - r * LQ;
+        *reinterpret_cast<float4*>(&in[r * LS + 4 * c4]) = q[u];
       }
     }
-  }
+    if (tl + (int)gridDim.x < total) load_tile<P, VEC>(s, g, tl + gridDim.x, q);   // prefetch next tile
+    __syncthreads();
+    // vertical max of this wave's rows 8w..8w+7: lane = column quad, sliding window in registers
+    if (lane < LQ) {
+      float4 col[8 + 2 * P];
+#pragma unroll
+      for (int i = 0; i < 8 + 2 * P; ++i) col[i] = *reinterpret_cast<const float4*>(&in[(wave * 8 + i) * LS + 4 * lane]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float4 m = col[i];
+#pragma unroll
+        for (int d = 1; d <= 2 * P; ++d) {
+          m.x = fmaxf(m.x, col[i + d].x); m.y = fmaxf(m.y, col[i + d].y);
+          m.z = fmaxf(m.z, col[i + d].z); m.w = fmaxf(m.w, col[i + d].w);
+        }
+        *reinterpret_cast<float4*>(&vmax[(wave * 8 + i) * LS + 4 * lane]) = m;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int r = threadIdx.x >> 3, cb = (threadIdx.x & 7) * 16;
+    const int y = y0 + r;
+    const bool row_ok = y < H;
+    float vm[24], sc[16], mk[MASKED ? 16 : 1];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const float4 m = *reinterpret_cast<const float4*>(&vmax[r * LS + cb + 4 * k]);
+      vm[4 * k] = m.x; vm[4 * k + 1] = m.y; vm[4 * k + 2] = m.z; vm[4 * k + 3] = m.w;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float4 o = *reinterpret_cast<const float4*>(&in[(r + P) * LS + cb + HALO + 4 * k]);
+      sc[4 * k] = o.x; sc[4 * k + 1] = o.y; sc[4 * k + 2] = o.z; sc[4 * k + 3] = o.w;
+    }
+    if (MASKED) {
+      const float* mrow = masks + ((size_t)b * H + min(y, H - 1)) * W;
+#pragma unroll
+      for (int j = 0; j < (MASKED ? 16 : 1); ++j) mk[j] = mrow[min(x0 + cb + j, W - 1)];
+    }
+    // v = s * jm (ConstructGraph.py:1162-1165); NaN marks pixels outside the plane
+    float v[16];
+    unsigned int mybits = 0;
+    int nonneg = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      float m = vm[j + HALO - P];
+#pragma unroll
+      for (int d = 1; d <= 2 * P; ++d) m = fmaxf(m, vm[j + HALO - P + d]);
+      float jm = (m == sc[j]) ? 1.0f : 0.0f;
+      if (MASKED) jm = jm * mk[MASKED ? j : 0];
+      const float vj = sc[j] * jm;
+      const bool ok = row_ok && x0 + cb + j < W;
+      v[j] = ok ? vj : NAN;
+      mybits |= (unsigned)(ok && use_thr && !(vj < thr) && (vj != 0.0f)) << j;
+      nonneg += ok && vj >= 0.0f;
+    }
+    const int base_id = y * W + x0 + cb;
+    const size_t wl = (size_t)tl * 4 + wave;     // this wave's list
+    if (MODE == MODE_POS)
+      wave_topk(v, base_id, K, [](float x) { return x > 0.0f; }, cand_v + wl * K, cand_i + wl * K);
+    else
+      wave_topk(v, base_id, K, [](float x) { return x == x; }, cand_v + wl * K, cand_i + wl * K);
 
-  // wave-level exact top-K of the wave's pixels -> candidates
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const size_t plane_tile = (size_t)(b * g.J + t) * g.tiles + tile;
-  float* cv_out = cand_v + plane_tile * 4 * g.K + wave * g.K;
-  int* ci_out = cand_i + plane_tile * 4 * g.K + wave * g.K;
-  for (int q = 0; q < g.K; ++q) {
-    float bv = tv[0];
-    int bi = ti[0];
+    // threshold bitmask: 4 consecutive threads x 16 px = one 64-px word
+    unsigned int lo = (threadIdx.x & 3) < 2 ? (mybits << (16 * (threadIdx.x & 1))) : 0u;
+    unsigned int hi = (threadIdx.x & 3) >= 2 ? (mybits << (16 * (threadIdx.x & 1))) : 0u;
+    lo |= __shfl_xor(lo, 1); hi |= __shfl_xor(hi, 1);
+    lo |= __shfl_xor(lo, 2); hi |= __shfl_xor(hi, 2);
+    const int word = x0 / 64 + ((threadIdx.x & 7) >> 2);
+    if ((threadIdx.x & 3) == 0 && row_ok && word < g.WW)
+      bits[((size_t)plane_i * H + y) * g.WW + word] = ((unsigned long long)hi << 32) | lo;
+    int cnt = __popc(mybits);
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
-      const float ov = __shfl_xor(bv, off);
-      const int oi = __shfl_xor(bi, off);
-      if (better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+      cnt += __shfl_xor(cnt, off);
+      nonneg += __shfl_xor(nonneg, off);
     }
-    if (lane == 0) { cv_out[q] = bv; ci_out[q] = bi; }
-    if (ti[0] == bi && tv[0] == bv && bi != 0x7fffffff) {   // owner pops its head
-#pragma unroll
-      for (int k = 0; k < KMAX - 1; ++k) { tv[k] = tv[k + 1]; ti[k] = ti[k + 1]; }
-      tv[KMAX - 1] = -INFINITY; ti[KMAX - 1] = 0x7fffffff;
+    if (lane == 0) { tile_count[wl] = cnt; tile_nonneg[wl] = nonneg; }
+    if (MODE == MODE_POS) {
+      if (nonneg < K)      // degenerate strip: also keep its best negatives (see stage 2)
+        wave_topk(v, base_id, K, [](float x) { return x < 0.0f; }, neg_v + wl * K, neg_i + wl * K);
+      else if (lane < K) { neg_v[wl * K + lane] = -INFINITY; neg_i[wl * K + lane] = INV; }
     }
   }
-
-  // threshold bitmask: 4 consecutive threads x 16 px = one 64-px word
-  unsigned int lo = (threadIdx.x & 3) < 2 ? (mybits << (16 * (threadIdx.x & 1))) : 0u;
-  unsigned int hi = (threadIdx.x & 3) >= 2 ? (mybits << (16 * (threadIdx.x & 1))) : 0u;
-  lo |= __shfl_xor(lo, 1); hi |= __shfl_xor(hi, 1);
-  lo |= __shfl_xor(lo, 2); hi |= __shfl_xor(hi, 2);
-  const int word = x0 / 64 + ((threadIdx.x & 7) >> 2);
-  if ((threadIdx.x & 3) == 0 && y < H && word < g.WW)
-    bits[((size_t)(b * g.J + t) * H + y) * g.WW + word] = ((unsigned long long)hi << 32) | lo;
-
-  int cnt = __popc(mybits);
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
-  if (lane == 0) wave_cnt[wave] = cnt;
-  __syncthreads();
-  if (threadIdx.x == 0)
-    tile_count[plane_tile] = wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
 }
 
 __device__ __forceinline__ int block_excl_scan(int v, int* sh, int* total) {
@@ -191,16 +321,57 @@ __device__ __forceinline__ int block_excl_scan(int v, int* sh, int* total) {
   return res;
 }
 
+// Wave-level exact top-`take` of n candidates (value desc, index asc) into out (lane 0 writes);
+// returns the number of valid entries written.
+template <int KMAX>
+__device__ __forceinline__ int merge_candidates(const float* __restrict__ cv, const int* __restrict__ ci, int n,
+                                                int take, float* out_v, int* out_i) {
+  const int lane = threadIdx.x & 63;
+  float lv[KMAX];
+  int li[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) { lv[k] = -INFINITY; li[k] = INV; }
+  for (int c = lane; c < n; c += 64) {
+    float v = cv[c];
+    int i = ci[c];
+    if (i != INV && better(v, i, lv[KMAX - 1], li[KMAX - 1])) {
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) {
+        if (better(v, i, lv[k], li[k])) {
+          const float s2 = lv[k]; const int i2 = li[k];
+          lv[k] = v; li[k] = i; v = s2; i = i2;
+        }
+      }
+    }
+  }
+  int got = 0;
+  for (int q = 0; q < take; ++q) {
+    float bv = lv[0];
+    int bi = li[0];
+    wave_best(bv, bi);
+    if (bi == INV) break;
+    if (lane == 0) { out_v[q] = bv; out_i[q] = bi; }
+    ++got;
+    if (li[0] == bi) {
+#pragma unroll
+      for (int k = 0; k < KMAX - 1; ++k) { lv[k] = lv[k + 1]; li[k] = li[k + 1]; }
+      lv[KMAX - 1] = -INFINITY; li[KMAX - 1] = INV;
+    }
+  }
+  return got;
+}
+
 template <int KMAX>
 __global__ __launch_bounds__(NT2) void select_kernel(
     const float* __restrict__ s, const float* __restrict__ masks, DetectGeom g, float thr, int use_thr,
-    const float* __restrict__ cand_v, const int* __restrict__ cand_i, const int* __restrict__ tile_count,
+    const float* __restrict__ cand_v, const int* __restrict__ cand_i, const float* __restrict__ neg_v,
+    const int* __restrict__ neg_i, const int* __restrict__ tile_count, const int* __restrict__ tile_nonneg,
     const unsigned long long* __restrict__ bits, int64_t* __restrict__ det, float* __restrict__ scores,
     int* __restrict__ n_det, int cap) {
   extern __shared__ int sh_strip[];            // [J*S] counts, then [J*S] offsets
-  __shared__ float top_v[MAXJ][KMAX];
+  __shared__ float top_v[MAXJ][2 * KMAX];
   __shared__ float top_sc[MAXJ][KMAX];
-  __shared__ int top_i[MAXJ][KMAX];
+  __shared__ int top_i[MAXJ][2 * KMAX];
   __shared__ int top_bit[MAXJ][KMAX];
   __shared__ int n_top[MAXJ];
   __shared__ int scan_sh[40];
@@ -210,54 +381,45 @@ __global__ __launch_bounds__(NT2) void select_kernel(
   int* strip_cnt = sh_strip;
   int* strip_off = sh_strip + J * S;
 
-  // (a) exact per-type top-K from the tile candidates
-  const int ncand = g.tiles * 4 * K;
+  // (a) exact per-type top-k from the per-tile candidates: each lane keeps a sorted local list of
+  //     its candidates, then rounds of wave argmax pop the global order.
   for (int t = wave; t < J; t += nwaves) {
-    const float* cv = cand_v + (size_t)(b * J + t) * ncand;
-    const int* ci = cand_i + (size_t)(b * J + t) * ncand;
-    float pv = INFINITY;
-    int pi = -1;
-    for (int q = 0; q < K; ++q) {
-      float bv = -INFINITY;
-      int bi = 0x7fffffff;
-      for (int c = lane; c < ncand; c += 64) {
-        const float v = cv[c];
-        const int i = ci[c];
-        if (better(pv, pi, v, i) && better(v, i, bv, bi)) { bv = v; bi = i; }
-      }
+    const size_t pt = (size_t)(b * J + t) * g.tiles * 4;      // first wave list of the plane
+    int n = merge_candidates<KMAX>(cand_v + pt * K, cand_i + pt * K, g.tiles * 4 * K, K, top_v[t], top_i[t]);
+    if (use_thr) {
+      // degenerate plane (fewer than K non-negative pixels): its top-k also holds negatives
+      int nn = 0;
+      for (int c = lane; c < g.tiles * 4; c += 64) nn += tile_nonneg[pt + c];
 #pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) {
-        const float ov = __shfl_xor(bv, off);
-        const int oi = __shfl_xor(bi, off);
-        if (better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
-      }
-      if (lane == 0) { top_v[t][q] = bv; top_i[t][q] = bi; }
-      pv = bv; pi = bi;
+      for (int off = 32; off >= 1; off >>= 1) nn += __shfl_xor(nn, off);
+      if (nn < K)
+        n += merge_candidates<KMAX>(neg_v + pt * K, neg_i + pt * K, g.tiles * 4 * K, K - nn, top_v[t] + n,
+                                    top_i[t] + n);
     }
     if (lane == 0) {
       // keep value != 0 (ConstructGraph.py:1174 nonzero), then order by flat index (y, x)
-      int n = 0;
-      for (int q = 0; q < K; ++q) {
+      int m = 0;
+      for (int q = 0; q < n; ++q) {
         const float v = top_v[t][q];
         const float sc = use_thr ? v : v + 1e-10f;
         if (sc != 0.0f && top_i[t][q] != 0x7fffffff) {
-          top_v[t][n] = v; top_sc[t][n] = sc; top_i[t][n] = top_i[t][q];
-          ++n;
+          top_v[t][m] = v; top_sc[t][m] = sc; top_i[t][m] = top_i[t][q];
+          ++m;
         }
       }
-      for (int a = 1; a < n; ++a) {            // insertion sort by index
-        const float v = top_v[t][a], sc = top_sc[t][a];
-        const int i = top_i[t][a];
-        int c = a - 1;
+      for (int a2 = 1; a2 < m; ++a2) {            // insertion sort by index
+        const float v = top_v[t][a2], sc = top_sc[t][a2];
+        const int i = top_i[t][a2];
+        int c = a2 - 1;
         while (c >= 0 && top_i[t][c] > i) {
           top_v[t][c + 1] = top_v[t][c]; top_sc[t][c + 1] = top_sc[t][c]; top_i[t][c + 1] = top_i[t][c];
           --c;
         }
         top_v[t][c + 1] = v; top_sc[t][c + 1] = sc; top_i[t][c + 1] = i;
       }
-      for (int q = 0; q < n; ++q)
+      for (int q = 0; q < m; ++q)
         top_bit[t][q] = use_thr && !(top_v[t][q] < thr) && top_v[t][q] != 0.0f;
-      n_top[t] = n;
+      n_top[t] = m;
     }
   }
   __syncthreads();
@@ -267,8 +429,8 @@ __global__ __launch_bounds__(NT2) void select_kernel(
     const int t = e / S, st = e - t * S;
     int c = 0;
     if (use_thr) {
-      const int* tc = tile_count + (size_t)(b * J + t) * g.tiles + st * g.tiles_x;
-      for (int x = 0; x < g.tiles_x; ++x) c += tc[x];
+      const int* tc = tile_count + ((size_t)(b * J + t) * g.tiles + st * g.tiles_x) * 4;
+      for (int x = 0; x < 4 * g.tiles_x; ++x) c += tc[x];
       for (int q = 0; q < n_top[t]; ++q)
         if (top_bit[t][q] && top_i[t][q] / W / TR == st) --c;
     }
@@ -372,22 +534,63 @@ __global__ __launch_bounds__(NT2) void select_kernel(
   if (threadIdx.x == 0) n_det[b] = N;
 }
 
+static int num_cus() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) return 256;
+    return v;
+  }();
+  return n;
+}
+
+template <int P, int MODE, bool VEC>
+static void launch_nms(const float* s, const float* masks, const DetectGeom& g, float thr, int use_thr,
+                       const DetectWs& w, hipStream_t st) {
+  const int total = g.B * g.J * g.tiles;
+  const int grid = total < 4 * num_cus() ? total : 4 * num_cus();
+  if (masks)
+    hipLaunchKernelGGL((nms_tiles_kernel<P, MODE, VEC, true>), dim3(grid), dim3(NT1), 0, st, s, masks, g, thr, use_thr,
+                       w.cand_v, w.cand_i, w.neg_v, w.neg_i, w.tile_count, w.tile_nonneg, w.bits);
+  else
+    hipLaunchKernelGGL((nms_tiles_kernel<P, MODE, VEC, false>), dim3(grid), dim3(NT1), 0, st, s, masks, g, thr,
+                       use_thr, w.cand_v, w.cand_i, w.neg_v, w.neg_i, w.tile_count, w.tile_nonneg, w.bits);
+}
+
+template <int MODE, bool VEC>
+static void dispatch_nms(const float* s, const float* masks, const DetectGeom& g, float thr, int use_thr,
+                         const DetectWs& w, hipStream_t st) {
+  switch (g.p) {
+    case 0: launch_nms<0, MODE, VEC>(s, masks, g, thr, use_thr, w, st); break;
+    case 1: launch_nms<1, MODE, VEC>(s, masks, g, thr, use_thr, w, st); break;
+    case 2: launch_nms<2, MODE, VEC>(s, masks, g, thr, use_thr, w, st); break;
+    case 3: launch_nms<3, MODE, VEC>(s, masks, g, thr, use_thr, w, st); break;
+    default: launch_nms<4, MODE, VEC>(s, masks, g, thr, use_thr, w, st); break;
+  }
+}
+
 template <int KMAX>
 static int launch_detect(const float* s, const float* masks, const DetectGeom& g, float thr, int use_thr,
                          int stages, const DetectWs& w, int64_t* det, float* scores, int32_t* n_det, int cap,
                          hipStream_t st) {
   if (stages & PEMP_DETECT_NMS) {
-    const size_t lds = (size_t)((TR + 2 * g.p) + TR) * (TC + 2 * g.p) * sizeof(float);
     ProfScope prof("detect_nms", st);
-    hipLaunchKernelGGL(nms_tiles_kernel<KMAX>, dim3(g.tiles, g.J, g.B), dim3(NT1), lds, st, s, masks, g, thr,
-                       use_thr, w.cand_v, w.cand_i, w.tile_count, w.bits);
+    const bool vec = (g.W % 4) == 0 && (reinterpret_cast<uintptr_t>(s) % 16) == 0 &&
+                     (!masks || (reinterpret_cast<uintptr_t>(masks) % 16) == 0);
+    if (use_thr) {
+      if (vec) dispatch_nms<MODE_POS, true>(s, masks, g, thr, use_thr, w, st);
+      else dispatch_nms<MODE_POS, false>(s, masks, g, thr, use_thr, w, st);
+    } else {
+      if (vec) dispatch_nms<MODE_ALL, true>(s, masks, g, thr, use_thr, w, st);
+      else dispatch_nms<MODE_ALL, false>(s, masks, g, thr, use_thr, w, st);
+    }
     PEMP_LAUNCH_CHECK();
   }
   if (stages & PEMP_DETECT_SELECT) {
     const size_t lds = (size_t)2 * g.J * g.S * sizeof(int);
     ProfScope prof("detect_select", st);
     hipLaunchKernelGGL(select_kernel<KMAX>, dim3(g.B), dim3(NT2), lds, st, s, masks, g, thr, use_thr, w.cand_v,
-                       w.cand_i, w.tile_count, w.bits, det, scores, (int*)n_det, cap);
+                       w.cand_i, w.neg_v, w.neg_i, w.tile_count, w.tile_nonneg, w.bits, det, scores, (int*)n_det, cap);
     PEMP_LAUNCH_CHECK();
   }
   return PEMP_OK;

@@ -25,9 +25,10 @@ namespace pemp {
 namespace {
 
 constexpr int D = 64;
-constexpr int ITEM = 64;    // edges per wave work item
+constexpr int ITEM = 128;   // edges per wave work item
 constexpr int LDW = 72;     // LDS row stride of a 64x64 weight tile (conflict-free ds_read_b128)
 constexpr int MAXT = 17;
+constexpr int TRS = 68;    // row stride of the per-wave [16][64] staging tile (conflict-free b128 writes)
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float a, float b, float c, float d) {
@@ -425,21 +426,26 @@ struct EdgeStepArgs {
   int write_next;
 };
 
-template <int AGG, bool HEAD>
+// HEAD: 0 = no edge head, 1 = published head 64 -> 64 -> 32 -> 1 (ReLU, ReLU), 2 = generic pemp_mlp
+template <int AGG, int HEAD>
 __global__ __launch_bounds__(256) void edge_step_kernel(EdgeStepArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float wl[];   // [3][64][LDW]: e1_w, e2_w, msg_w[t]
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* wl = sm;                               // [3][64][LDW]: e1_w, e2_w, msg_w[t]
+  float* vec = sm + 3 * D * LDW;                // e2_b[64] | attn_w[64]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
+  float* tr = vec + 2 * D + wave * 16 * TRS;    // this wave's [16 edges][64 features] staging tile
   const int T = a.T;
   const int blk = blockIdx.x;
-  if (blk >= a.wg_start[T]) return;                      // uniform for the block
+  if (blk >= a.wg_start[T]) return;             // uniform for the block
   int t = 0;
   while (t + 1 < T && a.wg_start[t + 1] <= blk) ++t;
-  // stage the three 64x64 weight tiles of this type
   const float* srcs[3] = {a.e1_w, a.e2_w, a.msg_w + (int64_t)t * D * D};
   for (int idx = threadIdx.x; idx < 3 * D * 16; idx += 256) {
-    const int m = idx / (D * 16), rem = idx - m * D * 16, row = rem >> 4, c4 = (rem & 15) * 4;
-    *reinterpret_cast<float4*>(&wl[(m * D + row) * LDW + c4]) = ld4(srcs[m] + row * D + c4);
+    const int mtx = idx / (D * 16), rem = idx - mtx * D * 16, row = rem >> 4, c4 = (rem & 15) * 4;
+    *reinterpret_cast<float4*>(&wl[(mtx * D + row) * LDW + c4]) = ld4(srcs[mtx] + row * D + c4);
   }
+  if (threadIdx.x < D) vec[threadIdx.x] = a.e2_b[threadIdx.x];
+  else if (threadIdx.x < 2 * D) vec[threadIdx.x] = (AGG == PEMP_AGGR_ATTN) ? a.attn_w[threadIdx.x - D] : 0.0f;
   __syncthreads();
   const float* W1 = wl;
   const float* W2 = wl + D * LDW;
@@ -455,53 +461,72 @@ __global__ __launch_bounds__(256) void edge_step_kernel(EdgeStepArgs a) {
   if (cs > ts && a.s_dst[cs] == a.s_dst[cs - 1]) first = a.seg[t * N + a.s_dst[cs] + 1];
   const int end = (ce == te) ? te : a.seg[t * N + a.s_dst[ce - 1] + 1];
   if (first >= end) return;
-
   const float* ntP = a.NT + 128 + 64 * t;
-  float e2b[4][4], aw[4][4];
-#pragma unroll
-  for (int ob = 0; ob < 4; ++ob) {
-    const float4 x = ld4(a.e2_b + 16 * ob + 4 * g);
-    e2b[ob][0] = x.x; e2b[ob][1] = x.y; e2b[ob][2] = x.z; e2b[ob][3] = x.w;
-    if (AGG == PEMP_AGGR_ATTN) {
-      const float4 y = ld4(a.attn_w + 16 * ob + 4 * g);
-      aw[ob][0] = y.x; aw[ob][1] = y.y; aw[ob][2] = y.z; aw[ob][3] = y.w;
-    }
-  }
-  // carried state of the segment continuing into the next tile
+
+  // carry of the segment continuing into the next tile: per lane (= feature) + wave-uniform scalars
+  float cacc = 0.f;
   int cseg = -1;
-  float cM = 0.f, cl = 0.f, cv[4][4];
+  float cM = 0.f, cl = 0.f;
+
+  // two-stage software pipeline: indices of tile k+2 and gathered rows of tile k+1 are in flight
+  // while tile k computes.
+  auto load_idx = [&](int b, int& s_, int& d_) {
+    const int q = min(b + c, end - 1);
+    s_ = a.s_src[q];
+    d_ = a.s_dst[q];
+  };
+  struct Rows { float4 q[4], xa[4], xb[4], ec[4], xp[4]; };
+  auto load_rows = [&](int b, int s_, int d_, Rows& R) {
+    const int q = min(b + c, end - 1);
 #pragma unroll
-  for (int ob = 0; ob < 4; ++ob)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) cv[ob][r] = 0.f;
+    for (int ob = 0; ob < 4; ++ob) {
+      const int f = 16 * ob + 4 * g;
+      R.q[ob] = ld4(a.Q0 + (int64_t)q * D + f);
+      R.xa[ob] = ld4(a.NT + (int64_t)d_ * a.t_nt_ld + f);
+      R.xb[ob] = ld4(a.NT + (int64_t)s_ * a.t_nt_ld + 64 + f);
+      R.ec[ob] = ld4(a.e_cur + (int64_t)q * D + f);
+      R.xp[ob] = ld4(ntP + (int64_t)d_ * a.t_nt_ld + f);
+    }
+  };
+  int src_n, dst_n, src_nn = 0, dst_nn = 0;
+  load_idx(first, src_n, dst_n);
+  Rows R;
+  load_rows(first, src_n, dst_n, R);
+  int src = src_n, dst = dst_n;
+  if (first + 16 < end) load_idx(first + 16, src_nn, dst_nn);
 
   for (int base = first; base < end; base += 16) {
     const int p = base + c;
     const bool valid = p < end;
-    const int pp = valid ? p : first;            // safe address for padding columns
-    const int64_t src = a.s_src[pp], dst = a.s_dst[pp];
-    const int seg = valid ? (int)dst : -1;
-    // layer 1: h = ReLU(Q0 + A[dst] + B[src] + W1_e_cur · e_cur)
-    float h[4][4], ein[4][4];
+    const int seg = valid ? dst : -1;
+    const int nvalid = min(16, end - base);
+    const bool last_tile = base + 16 >= end;
+    // edge MLP layer 1: h = ReLU(Q0 + A[dst] + B[src] + W1_e_cur · e_cur)
+    float h[4][4], ein[4][4], m[4][4];
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob) {
-      const int f = 16 * ob + 4 * g;
-      const float4 q = ld4(a.Q0 + (int64_t)pp * D + f);
-      const float4 xa = ld4(a.NT + dst * a.t_nt_ld + f);
-      const float4 xb = ld4(a.NT + src * a.t_nt_ld + 64 + f);
-      const float4 ec = ld4(a.e_cur + (int64_t)pp * D + f);
-      h[ob][0] = q.x + xa.x + xb.x; h[ob][1] = q.y + xa.y + xb.y;
-      h[ob][2] = q.z + xa.z + xb.z; h[ob][3] = q.w + xa.w + xb.w;
-      ein[ob][0] = ec.x; ein[ob][1] = ec.y; ein[ob][2] = ec.z; ein[ob][3] = ec.w;
+      h[ob][0] = R.q[ob].x + R.xa[ob].x + R.xb[ob].x; h[ob][1] = R.q[ob].y + R.xa[ob].y + R.xb[ob].y;
+      h[ob][2] = R.q[ob].z + R.xa[ob].z + R.xb[ob].z; h[ob][3] = R.q[ob].w + R.xa[ob].w + R.xb[ob].w;
+      ein[ob][0] = R.ec[ob].x; ein[ob][1] = R.ec[ob].y; ein[ob][2] = R.ec[ob].z; ein[ob][3] = R.ec[ob].w;
+      m[ob][0] = R.xp[ob].x; m[ob][1] = R.xp[ob].y; m[ob][2] = R.xp[ob].z; m[ob][3] = R.xp[ob].w;
     }
+    // prefetch: rows of tile k+1 (indices already here), indices of tile k+2
+    const int src_c = src, dst_c = dst;
+    if (!last_tile) {
+      load_rows(base + 16, src_nn, dst_nn, R);
+      src = src_nn; dst = dst_nn;
+      if (base + 32 < end) load_idx(base + 32, src_nn, dst_nn);
+    }
+    (void)src_c; (void)dst_c;
     gemm_frag<4, 4>(W1, LDW, ein, h);
     relu_frag<4>(h);
     // layer 2: e' = ReLU(W2 · h + b2)
     float ep[4][4];
 #pragma unroll
-    for (int ob = 0; ob < 4; ++ob)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) ep[ob][r] = e2b[ob][r];
+    for (int ob = 0; ob < 4; ++ob) {
+      const float4 b2 = ld4(vec + 16 * ob + 4 * g);
+      ep[ob][0] = b2.x; ep[ob][1] = b2.y; ep[ob][2] = b2.z; ep[ob][3] = b2.w;
+    }
     gemm_frag<4, 4>(W2, LDW, h, ep);
     relu_frag<4>(ep);
     if (a.write_next && valid) {
@@ -509,108 +534,118 @@ __global__ __launch_bounds__(256) void edge_step_kernel(EdgeStepArgs a) {
       for (int ob = 0; ob < 4; ++ob)
         st4(a.e_next + (int64_t)p * D + 16 * ob + 4 * g, ep[ob][0], ep[ob][1], ep[ob][2], ep[ob][3]);
     }
-    if (HEAD) {
-      float h1[4][4], h2[4][4];
-#pragma unroll
-      for (int ob = 0; ob < 4; ++ob)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) h1[ob][r] = ep[ob][r];
-      mlp_frag<4>(a.head, h1, h2);
-      if (valid && g == 0) a.edge_logits[a.s_orig[p]] = h1[0][0];
-    }
-    // message: m = ReLU(P_t[dst] + W_t_e · e')
-    float m[4][4];
-#pragma unroll
-    for (int ob = 0; ob < 4; ++ob) {
-      const float4 x = ld4(ntP + dst * a.t_nt_ld + 16 * ob + 4 * g);
-      m[ob][0] = x.x; m[ob][1] = x.y; m[ob][2] = x.z; m[ob][3] = x.w;
-    }
-    gemm_frag<4, 4>(WM, LDW, ep, m);
-    relu_frag<4>(m);
-
-    // ---- segmented aggregation over the 16 columns, carried across tiles ----
-    const SegMask sm = seg_mask(seg, c);
-    const bool tail = !sm.b1;
-    const int seg0 = __shfl(seg, lane & 48);
-    const bool last_tile = base + 16 >= end;
-    float v[4][4];
-    float M = 0.f, l = 0.f;
+    float av = 0.f;
     if (AGG == PEMP_AGGR_ATTN) {
-      float av = 0.f;
 #pragma unroll
-      for (int ob = 0; ob < 4; ++ob)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) av = fmaf(aw[ob][r], ep[ob][r], av);
+      for (int ob = 0; ob < 4; ++ob) {
+        const float4 w = ld4(vec + D + 16 * ob + 4 * g);
+        av = fmaf(w.x, ep[ob][0], av); av = fmaf(w.y, ep[ob][1], av);
+        av = fmaf(w.z, ep[ob][2], av); av = fmaf(w.w, ep[ob][3], av);
+      }
       av += __shfl_xor(av, 16);
       av += __shfl_xor(av, 32);
       av += a.attn_b;
+    }
+    // message: m = ReLU(P_t[dst] + W_t_e · e')   (P row prefetched with the tile)
+    gemm_frag<4, 4>(WM, LDW, ep, m);
+    relu_frag<4>(m);
+
+    // ---- per-column chunk statistics (chunk = the part of a segment inside this tile) ----
+    const SegMask sm = seg_mask(seg, c);
+    float M = 0.f, l, pe = 1.0f;
+    if (AGG == PEMP_AGGR_ATTN) {
       M = fmaxf(scan_max(av, sm), scan_max_bwd(av, sm));
-      const float pe = expf(av - M);
-      l = scan_add(pe, sm);
-#pragma unroll
-      for (int ob = 0; ob < 4; ++ob)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[ob][r] = scan_add(pe * m[ob][r], sm);
-      if (tail && seg == cseg && seg0 == seg) {
-        const float Mn = fmaxf(cM, M), fc = expf(cM - Mn), fn = expf(M - Mn);
-        l = cl * fc + l * fn;
-#pragma unroll
-        for (int ob = 0; ob < 4; ++ob)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[ob][r] = cv[ob][r] * fc + v[ob][r] * fn;
-        M = Mn;
-      }
+      pe = expf(av - M);
+      l = scan_add(pe, sm);                      // chunk sum of exp at the chunk tail
     } else {
-      l = scan_add(1.0f, sm);                      // chunk length
+      l = scan_add(1.0f, sm);                    // chunk length at the chunk tail
+    }
+    // ---- stage pe * m as [edge][feature], then lanes = features walk the 16 edges ----
 #pragma unroll
-      for (int ob = 0; ob < 4; ++ob)
+    for (int ob = 0; ob < 4; ++ob)
+      st4(tr + c * TRS + 16 * ob + 4 * g, pe * m[ob][0], pe * m[ob][1], pe * m[ob][2], pe * m[ob][3]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (cseg >= 0 && __builtin_amdgcn_readlane(seg, 0) != cseg) {   // carried segment ended at the tile edge
+      const float o = (AGG == PEMP_AGGR_ATTN) ? cacc / (cl + 1e-12f) : (AGG == PEMP_AGGR_MEAN) ? cacc / cl : cacc;
+      a.agg[((int64_t)cseg * T + t) * D + lane] = o;
+      cseg = -1;
+    }
+    float acc = 0.f;
+    int h0 = 0;                                  // head column of the current chunk
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          v[ob][r] = (AGG == PEMP_AGGR_MAX) ? scan_max(m[ob][r], sm) : scan_add(m[ob][r], sm);
-      if (tail && seg == cseg && seg0 == seg) {
-        l += cl;
-#pragma unroll
-        for (int ob = 0; ob < 4; ++ob)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            v[ob][r] = (AGG == PEMP_AGGR_MAX) ? fmaxf(v[ob][r], cv[ob][r]) : v[ob][r] + cv[ob][r];
+    for (int e = 0; e < 16; ++e) {
+      if (e < nvalid) {
+        const int se = __builtin_amdgcn_readlane(seg, e);
+        const bool head = e == 0 || se != __builtin_amdgcn_readlane(seg, e > 0 ? e - 1 : 0);
+        const bool tail = e == nvalid - 1 || se != __builtin_amdgcn_readlane(seg, e < 15 ? e + 1 : 15);
+        const float x = tr[e * TRS + lane];
+        if (head) { acc = x; h0 = e; }
+        else acc = (AGG == PEMP_AGGR_MAX) ? fmaxf(acc, x) : acc + x;
+        if (tail) {
+          float Mc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(M), e));
+          float lc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l), e));
+          if (h0 == 0 && se == cseg) {           // first chunk continues the carried segment
+            if (AGG == PEMP_AGGR_ATTN) {
+              const float Mn = fmaxf(cM, Mc), fc = expf(cM - Mn), fn = expf(Mc - Mn);
+              acc = cacc * fc + acc * fn;
+              lc = cl * fc + lc * fn;
+              Mc = Mn;
+            } else if (AGG == PEMP_AGGR_MAX) {
+              acc = fmaxf(acc, cacc);
+              lc += cl;
+            } else {
+              acc += cacc;
+              lc += cl;
+            }
+            cseg = -1;
+          }
+          if (e == 15 && !last_tile) {           // may continue in the next tile
+            cacc = acc; cM = Mc; cl = lc; cseg = se;
+          } else {
+            const float o = (AGG == PEMP_AGGR_ATTN) ? acc / (lc + 1e-12f) : (AGG == PEMP_AGGR_MEAN) ? acc / lc : acc;
+            a.agg[((int64_t)se * T + t) * D + lane] = o;
+          }
+        }
       }
     }
-    // the carried segment ended exactly at the previous tile: finalise it
-    if (cseg >= 0 && seg0 != cseg && c == 0) {
-      float* dstp = a.agg + ((int64_t)cseg * T + t) * D + 4 * g;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (HEAD == 1) {   // fused edge-classification head on e' (after the aggregation: fewer live registers)
+      const pemp_layer& L1 = a.head.layer[0];
+      const pemp_layer& L2 = a.head.layer[1];
+      const pemp_layer& L3 = a.head.layer[2];
+      float h1[4][4], h2[2][4];
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob) {
-        float o[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          o[r] = (AGG == PEMP_AGGR_ATTN) ? cv[ob][r] / (cl + 1e-12f)
-               : (AGG == PEMP_AGGR_MEAN) ? cv[ob][r] / cl : cv[ob][r];
-        st4(dstp + 16 * ob, o[0], o[1], o[2], o[3]);
+        const float4 bb = ld4(L1.b + 16 * ob + 4 * g);
+        h1[ob][0] = bb.x; h1[ob][1] = bb.y; h1[ob][2] = bb.z; h1[ob][3] = bb.w;
       }
-    }
-    const bool carry_out = !last_tile && c == 15;
-    if (tail && valid && !carry_out) {
-      float* dstp = a.agg + ((int64_t)seg * T + t) * D + 4 * g;
+      gemm_frag<4, 4>(L1.w, 64, ep, h1);
+      relu_frag<4>(h1);
 #pragma unroll
-      for (int ob = 0; ob < 4; ++ob) {
-        float o[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          o[r] = (AGG == PEMP_AGGR_ATTN) ? v[ob][r] / (l + 1e-12f)
-               : (AGG == PEMP_AGGR_MEAN) ? v[ob][r] / l : v[ob][r];
-        st4(dstp + 16 * ob, o[0], o[1], o[2], o[3]);
+      for (int ob = 0; ob < 2; ++ob) {
+        const float4 bb = ld4(L2.b + 16 * ob + 4 * g);
+        h2[ob][0] = bb.x; h2[ob][1] = bb.y; h2[ob][2] = bb.z; h2[ob][3] = bb.w;
       }
-    }
-    if (!last_tile) {
-      const int src_lane = (lane & 48) | 15;
-      cseg = __shfl(seg, src_lane);
-      cM = __shfl(M, src_lane);
-      cl = __shfl(l, src_lane);
+      gemm_frag<4, 2>(L2.w, 64, h1, h2);
+      relu_frag<2>(h2);
+      float lg = 0.f;
 #pragma unroll
-      for (int ob = 0; ob < 4; ++ob)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) cv[ob][r] = __shfl(v[ob][r], src_lane);
+      for (int ob = 0; ob < 2; ++ob) {
+        const float4 w = ld4(L3.w + 16 * ob + 4 * g);
+        lg = fmaf(w.x, h2[ob][0], lg); lg = fmaf(w.y, h2[ob][1], lg);
+        lg = fmaf(w.z, h2[ob][2], lg); lg = fmaf(w.w, h2[ob][3], lg);
+      }
+      lg += __shfl_xor(lg, 16);
+      lg += __shfl_xor(lg, 32);
+      if (valid && g == 0) a.edge_logits[a.s_orig[p]] = lg + L3.b[0];
+    } else if (HEAD == 2) {
+      float h2[4][4];
+      mlp_frag<4>(a.head, ep, h2);
+      if (valid && g == 0) a.edge_logits[a.s_orig[p]] = ep[0][0];
     }
   }
 }
@@ -665,13 +700,21 @@ static int grid1d(int64_t total, int block, int cap = 65536) {
   return (int)(g < 1 ? 1 : (g > cap ? cap : g));
 }
 
+static bool published_head(const pemp_mlp& m) {
+  return m.n_layers == 3 && m.layer[0].in_dim == 64 && m.layer[0].out_dim == 64 && m.layer[0].relu &&
+         m.layer[1].in_dim == 64 && m.layer[1].out_dim == 32 && m.layer[1].relu && m.layer[2].in_dim == 32 &&
+         m.layer[2].out_dim == 1 && !m.layer[2].relu;
+}
+
 template <int AGG>
 static void launch_edge_step(const EdgeStepArgs& a, bool head, int grid, hipStream_t st) {
-  const size_t lds = (size_t)3 * D * LDW * sizeof(float);
-  if (head)
-    hipLaunchKernelGGL((edge_step_kernel<AGG, true>), dim3(grid), dim3(256), lds, st, a);
+  const size_t lds = ((size_t)3 * D * LDW + 2 * D + 4 * 16 * TRS) * sizeof(float);
+  if (!head)
+    hipLaunchKernelGGL((edge_step_kernel<AGG, 0>), dim3(grid), dim3(256), lds, st, a);
+  else if (published_head(a.head))
+    hipLaunchKernelGGL((edge_step_kernel<AGG, 1>), dim3(grid), dim3(256), lds, st, a);
   else
-    hipLaunchKernelGGL((edge_step_kernel<AGG, false>), dim3(grid), dim3(256), lds, st, a);
+    hipLaunchKernelGGL((edge_step_kernel<AGG, 2>), dim3(grid), dim3(256), lds, st, a);
 }
 
 static int rows_mlp(const char* label, const pemp_mlp& m, const float* in, int64_t ld_in, int64_t M, float* out,

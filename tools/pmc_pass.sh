@@ -1,0 +1,7 @@
+#!/bin/bash
+# usage: tools/pmc_pass.sh <outdir> <kernel-regex> <counter...>   (GPU box; separate run per counter set)
+set -e
+out=$1; shift; rx=$1; shift
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex "$rx" --output-format csv -d "$out" -o pmc -- \
+  python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-roofline > "$out.log" 2>&1
