@@ -13,6 +13,7 @@
  *   pemp_detect          ConstructGraph.py:1161-1209 joint_det_from_scoremap + cat_unique,
  *                        Utils/Utils.py:15-20 non_maximum_suppression
  *   pemp_pack_nodes      ConstructGraph.py:100-103,206-231 (node features, tags, batching)
+ *   pemp_graph_offsets   ConstructGraph.py:222-223 (per-image node/edge offsets, on the device)
  *   pemp_fully_graph     ConstructGraph.py:376-381 fully_connected_mpn_graph (+ batch offsets :222-223)
  *   pemp_knn_graph_*     ConstructGraph.py:363-368 knn_mpn_graph (torch_cluster knn_graph k=50,
  *                        PyG to_undirected, remove_self_loops)
@@ -73,6 +74,11 @@ int pemp_pack_nodes(const float* features /*[B,C,H,W]*/, int C, const float* tag
                     int cap, const int64_t* node_off, int64_t n_total, float* x /*[N,C]*/,
                     int64_t* joint_det /*[N,3]*/, float* joint_scores /*[N]*/,
                     int64_t* batch_index /*[N]*/, float* joint_tags /*[N,F]*/, void* stream);
+
+/* Batch offsets on the device from pemp_detect's per-image counts (replaces the host cumsum +
+ * upload of ConstructGraph.py:222-223): node_off[b] = sum_{b'<b} n_det[b'] ([B+1] int64) and, if
+ * fully_edge_off != NULL, fully_edge_off[b] = sum_{b'<b} n_b' (n_b' - 1) ([B+1] int64). */
+int pemp_graph_offsets(const int32_t* n_det, int B, int64_t* node_off, int64_t* fully_edge_off, void* stream);
 
 /* Fully connected graph per image: all (i,j), i != j, sorted by (src,dst), node-offset per image.
  * node_off / edge_off: device [B+1] int64 with edge_off[b+1]-edge_off[b] = n_b (n_b - 1). */

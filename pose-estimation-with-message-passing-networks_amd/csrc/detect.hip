@@ -8,8 +8,10 @@
 //   plane. Tile + halo staged in LDS, separable max, then per pixel v = s * jm. Emits, per tile:
 //   each wave's k best (v, flat index) candidates (ties -> lower index), the tile's count of
 //   threshold pixels, and the threshold bitmask (row-major, one bit per pixel, 64-px words).
-// Stage 2 (select_kernel): one workgroup per image. Merges the candidates into the exact
-//   per-type top-k, scans per-strip counts, and emits detections in the reference's order.
+// Stage 2a (plane_top_kernel): one workgroup per plane. Merges the candidates into the exact
+//   per-type top-k and counts threshold detections per 32-row strip.
+// Stage 2b (emit_kernel): one workgroup per plane. Offsets from the image's per-plane counts;
+//   emits detections in the reference's order.
 #include <math.h>
 
 #include "pemp_common.h"
@@ -24,7 +26,6 @@ constexpr int NT1 = 256;  // stage-1 threads: 32 rows x 8 threads x 16 px
 #define NMS_MIN_WAVES 4
 #endif
 constexpr int MAXR = 4;   // max pool radius (POOL_KERNEL_SIZE <= 9)
-constexpr int NT2 = 1024; // stage-2 threads
 constexpr int MAXJ = 32;
 
 __device__ __forceinline__ bool better(float v1, int i1, float v2, int i2) {
@@ -46,8 +47,12 @@ static DetectGeom geom(int B, int J, int H, int W, int pool_k, int K) {
   return g;
 }
 
+constexpr int KCAP = 32;   // max top-k (pemp_detect checks topk <= 32)
+
 struct DetectWs {
   float *cand_v, *neg_v; int *cand_i, *neg_i, *tile_count, *tile_nonneg; unsigned long long* bits;
+  // per plane (image, type): sorted top-k list, threshold-set counts per strip and in-plane offsets
+  float* ptop_sc; int *ptop_i, *ptop_bit, *pn_top, *pn_thr, *pstrip, *pstrip_off;
 };
 
 static DetectWs carve(void* base, const DetectGeom& g, size_t* bytes) {
@@ -61,6 +66,14 @@ static DetectWs carve(void* base, const DetectGeom& g, size_t* bytes) {
   w.tile_count = c.take<int>((size_t)g.B * g.J * g.tiles * 4);
   w.tile_nonneg = c.take<int>((size_t)g.B * g.J * g.tiles * 4);
   w.bits = c.take<unsigned long long>((size_t)g.B * g.J * g.H * g.WW);
+  const size_t np = (size_t)g.B * g.J;
+  w.ptop_sc = c.take<float>(np * KCAP);
+  w.ptop_i = c.take<int>(np * KCAP);
+  w.ptop_bit = c.take<int>(np * KCAP);
+  w.pn_top = c.take<int>(np);
+  w.pn_thr = c.take<int>(np);
+  w.pstrip = c.take<int>(np * g.S);
+  w.pstrip_off = c.take<int>(np * g.S);
   if (bytes) *bytes = c.used;
   return w;
 }
@@ -293,34 +306,6 @@ __global__ __launch_bounds__(NT1, NMS_MIN_WAVES) void nms_tiles_kernel(
   }
 }
 
-__device__ __forceinline__ int block_excl_scan(int v, int* sh, int* total) {
-  // 1024-thread exclusive scan; sh: >= 16 ints
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int x = v;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int o = __shfl_up(x, off);
-    if (lane >= off) x += o;
-  }
-  if (lane == 63) sh[wave] = x;
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    int w = threadIdx.x < (int)(blockDim.x >> 6) ? sh[threadIdx.x] : 0;
-    int inc = w;
-    for (int off = 1; off < 64; off <<= 1) {
-      const int o = __shfl_up(inc, off);
-      if (threadIdx.x >= off) inc += o;
-    }
-    if (threadIdx.x < (int)(blockDim.x >> 6)) sh[threadIdx.x] = inc - w;
-    if (threadIdx.x == (int)(blockDim.x >> 6) - 1) sh[32] = inc;
-  }
-  __syncthreads();
-  const int res = sh[wave] + x - v;
-  *total = sh[32];
-  __syncthreads();
-  return res;
-}
-
 // Wave-level exact top-`take` of n candidates (value desc, index asc) into out (lane 0 writes);
 // returns the number of valid entries written.
 template <int KMAX>
@@ -361,135 +346,168 @@ __device__ __forceinline__ int merge_candidates(const float* __restrict__ cv, co
   return got;
 }
 
+// Block-level exact top-`take` (take <= KMAX) of n candidates: each of the 4 waves reduces a
+// quarter to its own top-`take` in LDS, wave 0 merges those. Returns the count (all threads).
 template <int KMAX>
-__global__ __launch_bounds__(NT2) void select_kernel(
-    const float* __restrict__ s, const float* __restrict__ masks, DetectGeom g, float thr, int use_thr,
-    const float* __restrict__ cand_v, const int* __restrict__ cand_i, const float* __restrict__ neg_v,
-    const int* __restrict__ neg_i, const int* __restrict__ tile_count, const int* __restrict__ tile_nonneg,
-    const unsigned long long* __restrict__ bits, int64_t* __restrict__ det, float* __restrict__ scores,
-    int* __restrict__ n_det, int cap) {
-  extern __shared__ int sh_strip[];            // [J*S] counts, then [J*S] offsets
-  __shared__ float top_v[MAXJ][2 * KMAX];
-  __shared__ float top_sc[MAXJ][KMAX];
-  __shared__ int top_i[MAXJ][2 * KMAX];
-  __shared__ int top_bit[MAXJ][KMAX];
-  __shared__ int n_top[MAXJ];
-  __shared__ int scan_sh[40];
-  const int b = blockIdx.x;
-  const int J = g.J, H = g.H, W = g.W, K = g.K, S = g.S;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = NT2 / 64;
-  int* strip_cnt = sh_strip;
-  int* strip_off = sh_strip + J * S;
-
-  // (a) exact per-type top-k from the per-tile candidates: each lane keeps a sorted local list of
-  //     its candidates, then rounds of wave argmax pop the global order.
-  for (int t = wave; t < J; t += nwaves) {
-    const size_t pt = (size_t)(b * J + t) * g.tiles * 4;      // first wave list of the plane
-    int n = merge_candidates<KMAX>(cand_v + pt * K, cand_i + pt * K, g.tiles * 4 * K, K, top_v[t], top_i[t]);
-    if (use_thr) {
-      // degenerate plane (fewer than K non-negative pixels): its top-k also holds negatives
-      int nn = 0;
-      for (int c = lane; c < g.tiles * 4; c += 64) nn += tile_nonneg[pt + c];
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) nn += __shfl_xor(nn, off);
-      if (nn < K)
-        n += merge_candidates<KMAX>(neg_v + pt * K, neg_i + pt * K, g.tiles * 4 * K, K - nn, top_v[t] + n,
-                                    top_i[t] + n);
-    }
-    if (lane == 0) {
-      // keep value != 0 (ConstructGraph.py:1174 nonzero), then order by flat index (y, x)
-      int m = 0;
-      for (int q = 0; q < n; ++q) {
-        const float v = top_v[t][q];
-        const float sc = use_thr ? v : v + 1e-10f;
-        if (sc != 0.0f && top_i[t][q] != 0x7fffffff) {
-          top_v[t][m] = v; top_sc[t][m] = sc; top_i[t][m] = top_i[t][q];
-          ++m;
-        }
-      }
-      for (int a2 = 1; a2 < m; ++a2) {            // insertion sort by index
-        const float v = top_v[t][a2], sc = top_sc[t][a2];
-        const int i = top_i[t][a2];
-        int c = a2 - 1;
-        while (c >= 0 && top_i[t][c] > i) {
-          top_v[t][c + 1] = top_v[t][c]; top_sc[t][c + 1] = top_sc[t][c]; top_i[t][c + 1] = top_i[t][c];
-          --c;
-        }
-        top_v[t][c + 1] = v; top_sc[t][c + 1] = sc; top_i[t][c + 1] = i;
-      }
-      for (int q = 0; q < m; ++q)
-        top_bit[t][q] = use_thr && !(top_v[t][q] < thr) && top_v[t][q] != 0.0f;
-      n_top[t] = m;
-    }
+__device__ int block_topk(const float* __restrict__ cv, const int* __restrict__ ci, int n, int take, float* out_v,
+                          int* out_i, float (*lv)[KMAX], int (*li)[KMAX], int* cnt) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = (n + 3) / 4, lo = min(n, wave * q), hi = min(n, lo + q);
+  const int got = merge_candidates<KMAX>(cv + lo, ci + lo, hi - lo, take, lv[wave], li[wave]);
+  for (int k = got + lane; k < KMAX; k += 64) li[wave][k] = INV;
+  __syncthreads();
+  if (wave == 0) {
+    const int m = merge_candidates<KMAX>(&lv[0][0], &li[0][0], 4 * KMAX, take, out_v, out_i);
+    if (lane == 0) *cnt = m;
   }
   __syncthreads();
+  const int m = *cnt;
+  __syncthreads();
+  return m;
+}
 
-  // (b) per-strip threshold counts minus top-k entries already listed (cat_unique)
-  for (int e = threadIdx.x; e < J * S; e += NT2) {
-    const int t = e / S, st = e - t * S;
+// Stage 2a: one 256-thread workgroup per plane (image, type). Exact top-k from the stage-1 wave
+// lists (ConstructGraph.py:1166-1174: top-k, nonzero, ordered by flat index), plus per-strip
+// counts of threshold pixels not already in the top-k (cat_unique, ConstructGraph.py:1199-1209).
+template <int KMAX>
+__global__ __launch_bounds__(256) void plane_top_kernel(DetectGeom g, float thr, int use_thr,
+                                                        const float* __restrict__ cand_v,
+                                                        const int* __restrict__ cand_i,
+                                                        const float* __restrict__ neg_v,
+                                                        const int* __restrict__ neg_i,
+                                                        const int* __restrict__ tile_count,
+                                                        const int* __restrict__ tile_nonneg, DetectWs w) {
+  __shared__ float lv[4][KMAX];
+  __shared__ int li[4][KMAX];
+  __shared__ float top_v[2 * KMAX], top_sc[KMAX];
+  __shared__ int top_i[2 * KMAX], top_bit[KMAX], sh[8];
+  const int pl = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int K = g.K, W = g.W, S = g.S, nl = g.tiles * 4;
+  const size_t pt = (size_t)pl * nl;                  // first wave list of the plane
+  int n = block_topk<KMAX>(cand_v + pt * K, cand_i + pt * K, nl * K, K, top_v, top_i, lv, li, &sh[0]);
+  if (use_thr) {
+    // degenerate plane (fewer than K non-negative pixels): its top-k also holds negatives
+    int nn = 0;
+    for (int c = threadIdx.x; c < nl; c += 256) nn += tile_nonneg[pt + c];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) nn += __shfl_xor(nn, off);
+    if (lane == 0) sh[4 + wave] = nn;
+    __syncthreads();
+    nn = sh[4] + sh[5] + sh[6] + sh[7];
+    if (nn < K) n += block_topk<KMAX>(neg_v + pt * K, neg_i + pt * K, nl * K, K - nn, top_v + n, top_i + n, lv, li, &sh[1]);
+  }
+  if (threadIdx.x == 0) {
+    int m = 0;
+    for (int q = 0; q < n; ++q) {
+      const float v = top_v[q];
+      const float sc = use_thr ? v : v + 1e-10f;
+      if (sc != 0.0f && top_i[q] != INV) { top_v[m] = v; top_sc[m] = sc; top_i[m] = top_i[q]; ++m; }
+    }
+    for (int a2 = 1; a2 < m; ++a2) {            // insertion sort by flat index
+      const float v = top_v[a2], sc = top_sc[a2];
+      const int i = top_i[a2];
+      int c = a2 - 1;
+      while (c >= 0 && top_i[c] > i) { top_v[c + 1] = top_v[c]; top_sc[c + 1] = top_sc[c]; top_i[c + 1] = top_i[c]; --c; }
+      top_v[c + 1] = v; top_sc[c + 1] = sc; top_i[c + 1] = i;
+    }
+    for (int q = 0; q < m; ++q) {
+      top_bit[q] = use_thr && !(top_v[q] < thr) && top_v[q] != 0.0f;
+      w.ptop_i[(size_t)pl * KCAP + q] = top_i[q];
+      w.ptop_sc[(size_t)pl * KCAP + q] = top_sc[q];
+      w.ptop_bit[(size_t)pl * KCAP + q] = top_bit[q];
+    }
+    w.pn_top[pl] = m;
+    sh[0] = m;
+  }
+  __syncthreads();
+  const int m = sh[0];
+  // per-strip threshold counts minus the top-k entries already listed
+  for (int st = threadIdx.x; st < S; st += 256) {
     int c = 0;
     if (use_thr) {
-      const int* tc = tile_count + ((size_t)(b * J + t) * g.tiles + st * g.tiles_x) * 4;
+      const int* tc = tile_count + pt + (size_t)st * g.tiles_x * 4;
       for (int x = 0; x < 4 * g.tiles_x; ++x) c += tc[x];
-      for (int q = 0; q < n_top[t]; ++q)
-        if (top_bit[t][q] && top_i[t][q] / W / TR == st) --c;
+      for (int q = 0; q < m; ++q)
+        if (top_bit[q] && top_i[q] / W / TR == st) --c;
     }
-    strip_cnt[e] = c;
+    w.pstrip[(size_t)pl * S + st] = c;
   }
   __syncthreads();
-
-  // (c) offsets: [top dets of all types] ++ [threshold dets, type-major, strip order]
-  int n_top_all = 0;
-  for (int t = 0; t < J; ++t) n_top_all += n_top[t];
-  const int per = (J * S + NT2 - 1) / NT2;
-  int local = 0;
-  for (int k = 0; k < per; ++k) {
-    const int e = threadIdx.x * per + k;
-    if (e < J * S) local += strip_cnt[e];
+  // in-plane exclusive scan over strips (wave 0, chunks of 64)
+  if (wave == 0) {
+    int carry = 0;
+    for (int c0 = 0; c0 < S; c0 += 64) {
+      const int st = c0 + lane;
+      const int v = st < S ? w.pstrip[(size_t)pl * S + st] : 0;
+      int x = v;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(x, off);
+        if (lane >= off) x += o;
+      }
+      if (st < S) w.pstrip_off[(size_t)pl * S + st] = carry + x - v;
+      carry += __shfl(x, 63);
+    }
+    if (lane == 0) w.pn_thr[pl] = carry;
   }
-  int total_thr;
-  int base = block_excl_scan(local, scan_sh, &total_thr);
-  for (int k = 0; k < per; ++k) {
-    const int e = threadIdx.x * per + k;
-    if (e < J * S) { strip_off[e] = n_top_all + base; base += strip_cnt[e]; }
+}
+
+// Stage 2b: one workgroup per plane. The plane's output offsets follow from the per-plane counts
+// of its image: [top-k dets of types 0..J-1] ++ [threshold dets, type-major, strip order].
+__global__ __launch_bounds__(256) void emit_kernel(const float* __restrict__ s, const float* __restrict__ masks,
+                                                   DetectGeom g, const unsigned long long* __restrict__ bits,
+                                                   DetectWs w, int64_t* __restrict__ det,
+                                                   float* __restrict__ scores, int* __restrict__ n_det, int cap) {
+  __shared__ int top_i[KCAP], top_bit[KCAP], sh[4];
+  const int pl = blockIdx.x, J = g.J, b = pl / J, t = pl - b * J;
+  const int H = g.H, W = g.W, S = g.S;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (wave == 0) {
+    // J <= 32: one lane per type of this image
+    const int nt = lane < J ? w.pn_top[b * J + lane] : 0, nh = lane < J ? w.pn_thr[b * J + lane] : 0;
+    int top_before = lane < t ? nt : 0, thr_before = lane < t ? nh : 0, top_all = nt, thr_all = nh;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      top_before += __shfl_xor(top_before, off); thr_before += __shfl_xor(thr_before, off);
+      top_all += __shfl_xor(top_all, off); thr_all += __shfl_xor(thr_all, off);
+    }
+    const int ntop = __shfl(nt, t);
+    if (lane == 0) {
+      sh[0] = top_before; sh[1] = top_all + thr_before; sh[2] = ntop;
+      if (t == 0) n_det[b] = top_all + thr_all;
+    }
+    if (lane < ntop) { top_i[lane] = w.ptop_i[(size_t)pl * KCAP + lane]; top_bit[lane] = w.ptop_bit[(size_t)pl * KCAP + lane]; }
   }
   __syncthreads();
-  const int N = n_top_all + total_thr;
-
+  const int ntop = sh[2], top_base = sh[0], thr_base = sh[1];
   int64_t* dout = det + (size_t)b * cap * 3;
   float* sout = scores + (size_t)b * cap;
-  // (d) top-k detections
-  for (int e = threadIdx.x; e < J * KMAX; e += NT2) {
-    const int t = e / KMAX, q = e - t * KMAX;
-    if (t < J && q < n_top[t]) {
-      int pos = q;
-      for (int t2 = 0; t2 < t; ++t2) pos += n_top[t2];
-      if (pos < cap) {
-        const int idx = top_i[t][q];
-        dout[pos * 3 + 0] = idx % W;
-        dout[pos * 3 + 1] = idx / W;
-        dout[pos * 3 + 2] = t;
-        sout[pos] = top_sc[t][q];
-      }
+  if ((int)threadIdx.x < ntop) {
+    const int pos = top_base + threadIdx.x;
+    if (pos < cap) {
+      const int idx = top_i[threadIdx.x];
+      dout[pos * 3 + 0] = idx % W;
+      dout[pos * 3 + 1] = idx / W;
+      dout[pos * 3 + 2] = t;
+      sout[pos] = w.ptop_sc[(size_t)pl * KCAP + threadIdx.x];
     }
   }
-  // (e) threshold detections, one wave per non-empty strip
-  for (int e = wave; e < J * S; e += nwaves) {
-    if (strip_cnt[e] == 0) continue;             // wave-uniform
-    const int t = e / S, st = e - t * S;
+  // threshold detections, one wave per non-empty strip
+  for (int st = wave; st < S; st += 4) {
+    if (w.pstrip[(size_t)pl * S + st] == 0) continue;     // wave-uniform
     const int ry0 = st * TR, rows = min(TR, H - ry0);
     const int nw = rows * g.WW;
     const int chunk = (nw + 63) / 64;
-    const unsigned long long* wsrc = bits + ((size_t)(b * J + t) * H + ry0) * g.WW;
+    const unsigned long long* wsrc = bits + ((size_t)pl * H + ry0) * g.WW;
     int cnt = 0;
     for (int k = 0; k < chunk; ++k) {
       const int wi = lane * chunk + k;
       if (wi >= nw) break;
       unsigned long long word = wsrc[wi];
       if (word) {
-        for (int q = 0; q < n_top[t]; ++q) {
-          if (!top_bit[t][q]) continue;
-          const int idx = top_i[t][q], yy = idx / W, xx = idx - yy * W;
+        for (int q = 0; q < ntop; ++q) {
+          if (!top_bit[q]) continue;
+          const int idx = top_i[q], yy = idx / W, xx = idx - yy * W;
           if ((yy - ry0) * g.WW + xx / 64 == wi) word &= ~(1ull << (xx & 63));
         }
       }
@@ -501,16 +519,16 @@ __global__ __launch_bounds__(NT2) void select_kernel(
       const int o = __shfl_up(pre, off);
       if (lane >= off) pre += o;
     }
-    int pos = strip_off[e] + pre - cnt;
-    const float* plane = s + (size_t)(b * J + t) * H * W;
+    int pos = thr_base + w.pstrip_off[(size_t)pl * S + st] + pre - cnt;
+    const float* plane = s + (size_t)pl * H * W;
     for (int k = 0; k < chunk; ++k) {
       const int wi = lane * chunk + k;
       if (wi >= nw) break;
       unsigned long long word = wsrc[wi];
       if (!word) continue;
-      for (int q = 0; q < n_top[t]; ++q) {
-        if (!top_bit[t][q]) continue;
-        const int idx = top_i[t][q], yy = idx / W, xx = idx - yy * W;
+      for (int q = 0; q < ntop; ++q) {
+        if (!top_bit[q]) continue;
+        const int idx = top_i[q], yy = idx / W, xx = idx - yy * W;
         if ((yy - ry0) * g.WW + xx / 64 == wi) word &= ~(1ull << (xx & 63));
       }
       const int yy = ry0 + wi / g.WW, xw = (wi % g.WW) * 64;
@@ -531,7 +549,6 @@ __global__ __launch_bounds__(NT2) void select_kernel(
       }
     }
   }
-  if (threadIdx.x == 0) n_det[b] = N;
 }
 
 static int num_cus() {
@@ -587,10 +604,15 @@ static int launch_detect(const float* s, const float* masks, const DetectGeom& g
     PEMP_LAUNCH_CHECK();
   }
   if (stages & PEMP_DETECT_SELECT) {
-    const size_t lds = (size_t)2 * g.J * g.S * sizeof(int);
-    ProfScope prof("detect_select", st);
-    hipLaunchKernelGGL(select_kernel<KMAX>, dim3(g.B), dim3(NT2), lds, st, s, masks, g, thr, use_thr, w.cand_v,
-                       w.cand_i, w.neg_v, w.neg_i, w.tile_count, w.tile_nonneg, w.bits, det, scores, (int*)n_det, cap);
+    {
+      ProfScope prof("detect_top", st);
+      hipLaunchKernelGGL(plane_top_kernel<KMAX>, dim3(g.B * g.J), dim3(256), 0, st, g, thr, use_thr, w.cand_v,
+                         w.cand_i, w.neg_v, w.neg_i, w.tile_count, w.tile_nonneg, w);
+      PEMP_LAUNCH_CHECK();
+    }
+    ProfScope prof("detect_emit", st);
+    hipLaunchKernelGGL(emit_kernel, dim3(g.B * g.J), dim3(256), 0, st, s, masks, g, w.bits, w, det, scores,
+                       (int*)n_det, cap);
     PEMP_LAUNCH_CHECK();
   }
   return PEMP_OK;
@@ -622,7 +644,6 @@ extern "C" int pemp_detect(const float* scoremaps, const float* masks, int B, in
   PEMP_CHECK_ARG((size_t)H * W < 0x7fffffffull, "pemp_detect: plane too large");
   const int K = topk < H * W ? topk : H * W;
   const DetectGeom g = geom(B, J, H, W, pool_kernel, K);
-  PEMP_CHECK_ARG(g.S * J * 2 * sizeof(int) <= 48 * 1024, "pemp_detect: H too large for the select stage");
   size_t need = 0;
   carve(nullptr, g, &need);
   if (workspace_bytes < need) {

@@ -314,6 +314,47 @@ extern "C" int pemp_pack_nodes(const float* features, int C, const float* tagmap
   return PEMP_OK;
 }
 
+namespace pemp {
+namespace {
+// node_off[b] = sum_{b'<b} n_det[b'], fully_edge_off[b] = sum_{b'<b} n (n - 1): one wave, chunks of 64
+__global__ __launch_bounds__(64) void graph_offsets_kernel(const int32_t* __restrict__ n_det, int B,
+                                                           int64_t* __restrict__ node_off,
+                                                           int64_t* __restrict__ edge_off) {
+  const int lane = threadIdx.x;
+  long long cn = 0, ce = 0;
+  for (int c0 = 0; c0 < B; c0 += 64) {
+    const int b = c0 + lane;
+    const long long n = b < B ? n_det[b] : 0, e = n * (n > 0 ? n - 1 : 0);
+    long long xn = n, xe = e;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const long long on = __shfl_up(xn, off), oe = __shfl_up(xe, off);
+      if (lane >= off) { xn += on; xe += oe; }
+    }
+    if (b < B) {
+      node_off[b] = cn + xn - n;
+      if (edge_off) edge_off[b] = ce + xe - e;
+    }
+    cn += __shfl(xn, 63);
+    ce += __shfl(xe, 63);
+  }
+  if (lane == 0) {
+    node_off[B] = cn;
+    if (edge_off) edge_off[B] = ce;
+  }
+}
+}  // namespace
+}  // namespace pemp
+
+extern "C" int pemp_graph_offsets(const int32_t* n_det, int B, int64_t* node_off, int64_t* fully_edge_off,
+                                  void* stream) {
+  PEMP_CHECK_ARG(n_det && node_off && B > 0, "pemp_graph_offsets: bad args");
+  hipLaunchKernelGGL(graph_offsets_kernel, dim3(1), dim3(64), 0, as_stream(stream), n_det, B, node_off,
+                     fully_edge_off);
+  PEMP_LAUNCH_CHECK();
+  return PEMP_OK;
+}
+
 extern "C" int pemp_fully_graph(const int64_t* node_off, const int64_t* edge_off, int B, int64_t e_total,
                                 int64_t* edge_index, void* stream) {
   PEMP_CHECK_ARG(node_off && edge_off && edge_index && B > 0 && e_total >= 0, "pemp_fully_graph: bad args");

@@ -163,7 +163,7 @@ __device__ __forceinline__ float scan_max_bwd(float v, const SegMask& m) {
 // Workspace
 // ---------------------------------------------------------------------------------------------
 struct MpnWs {
-  int *cnt, *seg, *cursor, *wg_start, *perm, *s_src, *s_dst, *s_orig, *err;
+  int *cnt, *seg, *wg_start, *perm, *s_src, *s_dst, *s_orig, *err;
   float *X, *NT, *agg, *Q0, *EA, *EB;
 };
 
@@ -171,9 +171,9 @@ static MpnWs mpn_carve(void* base, int T, int64_t N, int64_t E, size_t* bytes) {
   Carver c(base);
   MpnWs w;
   const int64_t K = (int64_t)T * N;
-  w.cnt = c.take<int>(K + 1);
-  w.cursor = c.take<int>(K + 1);
-  w.err = c.take<int>(4);
+  w.err = c.take<int>(64);               // err[0..3] then cnt: zeroed together
+  w.cnt = w.err + 64;
+  c.take<int>(K + 1);
   w.seg = c.take<int>(K + 1);
   w.wg_start = c.take<int>(MAXT + 2);
   w.perm = c.take<int>(E);
@@ -205,40 +205,72 @@ __global__ __launch_bounds__(256) void mpn_count_kernel(const int64_t* __restric
   }
 }
 
+__global__ __launch_bounds__(256) void zero_words_kernel(int* __restrict__ p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = 0;
+}
+
+// Exclusive scan of the (type, target) counts -> seg[0..K]; then per-type first workgroup of
+// the edge-step grid (wg_start). One 1024-thread block, 16 contiguous counts per thread per pass
+// (all loads of a pass in flight together), carry across passes.
+constexpr int SCAN_SPT = 16;
 __global__ __launch_bounds__(1024) void mpn_scan_kernel(const int* __restrict__ cnt, int64_t K, int64_t N, int T,
                                                         int* __restrict__ seg, int* __restrict__ wg_start) {
   __shared__ int sh[40];
-  const int per = (int)((K + 1023) / 1024);
-  const int64_t k0 = (int64_t)threadIdx.x * per;
-  int local = 0;
-  for (int k = 0; k < per; ++k)
-    if (k0 + k < K) local += cnt[k0 + k];
-  // block exclusive scan
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int x = local;
+  int carry = 0;
+  for (int64_t base = 0; base < K; base += 1024 * SCAN_SPT) {
+    const int64_t k0 = base + (int64_t)threadIdx.x * SCAN_SPT;
+    int v[SCAN_SPT];
+    if (k0 + SCAN_SPT <= K) {
 #pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int o = __shfl_up(x, off);
-    if (lane >= off) x += o;
+      for (int j = 0; j < SCAN_SPT; j += 4) {
+        const int4 q = *reinterpret_cast<const int4*>(cnt + k0 + j);
+        v[j] = q.x; v[j + 1] = q.y; v[j + 2] = q.z; v[j + 3] = q.w;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < SCAN_SPT; ++j) v[j] = k0 + j < K ? cnt[k0 + j] : 0;
+    }
+    int local = 0;
+#pragma unroll
+    for (int j = 0; j < SCAN_SPT; ++j) local += v[j];
+    int x = local;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int o = __shfl_up(x, off);
+      if (lane >= off) x += o;
+    }
+    if (lane == 63) sh[wave] = x;
+    __syncthreads();
+    if (wave == 0) {
+      const int wv = lane < 16 ? sh[lane] : 0;
+      int inc = wv;
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) {
+        const int o = __shfl_up(inc, off);
+        if (lane >= off) inc += o;
+      }
+      if (lane < 16) sh[lane] = inc - wv;
+      if (lane == 15) sh[16] = inc;
+    }
+    __syncthreads();
+    int run = carry + sh[wave] + x - local;
+#pragma unroll
+    for (int j = 0; j < SCAN_SPT; ++j)
+      if (k0 + j < K) { seg[k0 + j] = run; run += v[j]; }
+    carry += sh[16];
+    __syncthreads();
   }
-  if (lane == 63) sh[wave] = x;
+  if (threadIdx.x == 0) seg[K] = carry;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int run = 0;
-    for (int w = 0; w < 16; ++w) { const int v = sh[w]; sh[w] = run; run += v; }
-    sh[16] = run;
-  }
-  __syncthreads();
-  int run = sh[wave] + x - local;
-  for (int k = 0; k < per; ++k)
-    if (k0 + k < K) { seg[k0 + k] = run; run += cnt[k0 + k]; }
-  if (threadIdx.x == 0) seg[K] = sh[16];
+  // wg_start: T + 1 reads of seg in parallel, then a short serial sum
+  if (threadIdx.x <= T) sh[20 + threadIdx.x] = seg[(int64_t)threadIdx.x * N];
   __syncthreads();
   if (threadIdx.x == 0) {
     int acc = 0;
     wg_start[0] = 0;
     for (int t = 0; t < T; ++t) {
-      const int et = seg[(t + 1) * N] - seg[t * N];
+      const int et = sh[20 + t + 1] - sh[20 + t];
       const int items = (et + ITEM - 1) / ITEM;
       acc += (items + 3) / 4;
       wg_start[t + 1] = acc;
@@ -246,16 +278,18 @@ __global__ __launch_bounds__(1024) void mpn_scan_kernel(const int* __restrict__ 
   }
 }
 
+// counts are consumed here: cnt[key] counts down, so edges land in a key's segment in arbitrary
+// order; mpn_segsort_kernel restores edge-id order inside each segment.
 __global__ __launch_bounds__(256) void mpn_scatter_kernel(const int64_t* __restrict__ ei, const int64_t* __restrict__ types,
                                                           int64_t N, int64_t E, int T, const int* __restrict__ seg,
-                                                          int* __restrict__ cursor, int* __restrict__ perm) {
+                                                          int* __restrict__ cnt, int* __restrict__ perm) {
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t s = ei[e], d = ei[E + e];
     if (s < 0 || s >= N || d < 0 || d >= N) continue;
     const int64_t t = T == 1 ? 0 : types[s];
     if (t < 0 || t >= T) continue;
     const int64_t key = t * N + d;
-    perm[seg[key] + atomicAdd(&cursor[key], 1)] = (int)e;
+    perm[seg[key] + atomicSub(&cnt[key], 1) - 1] = (int)e;
   }
 }
 
@@ -651,7 +685,7 @@ __global__ __launch_bounds__(256) void edge_step_kernel(EdgeStepArgs a) {
 }
 
 // x_new = ReLU(b + sum_t U_t · agg[n, t]) (or agg[n, 0] when there is no update MLP) -> X[:, 64:128]
-__global__ __launch_bounds__(512) void node_update_kernel(const float* __restrict__ agg, const int* __restrict__ cnt,
+__global__ __launch_bounds__(512) void node_update_kernel(const float* __restrict__ agg, const int* __restrict__ seg,
                                                           int T, int64_t N, const float* __restrict__ upd_w,
                                                           const float* __restrict__ upd_b, float* __restrict__ X) {
   __shared__ __attribute__((aligned(16))) float red[8][16 * 68];
@@ -661,7 +695,7 @@ __global__ __launch_bounds__(512) void node_update_kernel(const float* __restric
     for (int idx = threadIdx.x; idx < 16 * D; idx += 512) {
       const int r = idx >> 6, f = idx & 63;
       const int64_t n = n0 + r;
-      if (n < N) X[n * 128 + 64 + f] = cnt[n] > 0 ? agg[n * D + f] : 0.0f;
+      if (n < N) X[n * 128 + 64 + f] = seg[n + 1] > seg[n] ? agg[n * D + f] : 0.0f;
     }
     return;
   }
@@ -672,7 +706,7 @@ __global__ __launch_bounds__(512) void node_update_kernel(const float* __restric
 #pragma unroll
     for (int r = 0; r < 4; ++r) acc[ob][r] = 0.f;
   for (int t = wave; t < T; t += 8) {
-    const bool has = n < N && cnt[t * N + n] > 0;
+    const bool has = n < N && seg[t * N + n + 1] > seg[t * N + n];
     float in[4][4];
 #pragma unroll
     for (int mb = 0; mb < 4; ++mb) {
@@ -794,9 +828,9 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
   // ---- prepare: type-major order ----
   {
   ProfScope prof("mpn_prepare", st);
-  PEMP_HIP(hipMemsetAsync(ws.cnt, 0, (K + 1) * sizeof(int), st));
-  PEMP_HIP(hipMemsetAsync(ws.cursor, 0, (K + 1) * sizeof(int), st));
-  PEMP_HIP(hipMemsetAsync(ws.err, 0, 4 * sizeof(int), st));
+  hipLaunchKernelGGL(zero_words_kernel, dim3((unsigned)std::min<int64_t>((K + 64 + 255) / 256, 1024)), dim3(256), 0,
+                     st, ws.err, K + 65);
+  PEMP_LAUNCH_CHECK();
   if (E > 0) {
     hipLaunchKernelGGL(mpn_count_kernel, dim3(grid1d(E, 256)), dim3(256), 0, st, edge_index, node_types, N, E, T,
                        ws.cnt, ws.err);
@@ -806,7 +840,7 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
   PEMP_LAUNCH_CHECK();
   if (E > 0) {
     hipLaunchKernelGGL(mpn_scatter_kernel, dim3(grid1d(E, 256)), dim3(256), 0, st, edge_index, node_types, N, E, T,
-                       ws.seg, ws.cursor, ws.perm);
+                       ws.seg, ws.cnt, ws.perm);
     PEMP_LAUNCH_CHECK();
     hipLaunchKernelGGL(mpn_segsort_kernel, dim3((unsigned)((K + 3) / 4)), dim3(256), 0, st, edge_index, E, K, ws.seg,
                        ws.perm, ws.s_src, ws.s_dst, ws.s_orig);
@@ -859,7 +893,7 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
     }
     {
     ProfScope prof("node_update", st);
-    hipLaunchKernelGGL(node_update_kernel, dim3((unsigned)((N + 15) / 16)), dim3(512), 0, st, ws.agg, ws.cnt, T, N,
+    hipLaunchKernelGGL(node_update_kernel, dim3((unsigned)((N + 15) / 16)), dim3(512), 0, st, ws.agg, ws.seg, T, N,
                        w->upd_w, w->upd_b, ws.X);
     PEMP_LAUNCH_CHECK();
     }

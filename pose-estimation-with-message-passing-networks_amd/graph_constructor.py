@@ -103,7 +103,11 @@ class NaiveGraphConstructor:
         node_off_h = np.zeros(B + 1, np.int64)
         node_off_h[1:] = np.cumsum(counts)
         N = int(node_off_h[-1])
-        node_off = torch.from_numpy(node_off_h).to(dev, non_blocking=True)
+        # batch offsets are recomputed on the device from n_det (no host->device upload)
+        offs = torch.empty(2, B + 1, dtype=torch.int64, device=dev)
+        node_off, fully_off = offs[0], offs[1]
+        _lib.check(L.pemp_graph_offsets(_lib.ptr(n_det), B, _lib.ptr(node_off),
+                                        _lib.ptr(fully_off) if self.mpn_graph_type == "fully" else None, st))
 
         # ---- nodes (pemp_pack_nodes) ----
         feats = self.features
@@ -131,7 +135,7 @@ class NaiveGraphConstructor:
             joint_tags = None
 
         # ---- edges ----
-        edge_index = self._edges(L, st, joint_det, node_off, node_off_h, B, dev)
+        edge_index = self._edges(L, st, joint_det, node_off, fully_off, node_off_h, B, dev)
         E = edge_index.shape[1]
         mode = _EF_MODES.get(frozenset(self.edge_features_to_use))
         if mode is None:
@@ -144,7 +148,7 @@ class NaiveGraphConstructor:
         return (x, edge_attr, edge_index, None, None, None, None, joint_det, None, None, None, joint_scores,
                 batch_index, None, joint_tags)
 
-    def _edges(self, L, st, joint_det, node_off, node_off_h, B, dev):
+    def _edges(self, L, st, joint_det, node_off, fully_off, node_off_h, B, dev):
         counts = np.diff(node_off_h)
         if self.mpn_graph_type == "fully":
             per = counts * np.maximum(counts - 1, 0)
@@ -158,14 +162,14 @@ class NaiveGraphConstructor:
             per = ecount.cpu().numpy()
         else:
             raise NotImplementedError(f"GRAPH_TYPE={self.mpn_graph_type}")
-        edge_off_h = np.zeros(B + 1, np.int64)
-        edge_off_h[1:] = np.cumsum(per)
-        E = int(edge_off_h[-1])
-        edge_off = torch.from_numpy(edge_off_h).to(dev, non_blocking=True)
+        E = int(per.sum())
         edge_index = torch.empty(2, E, dtype=torch.int64, device=dev)
         if self.mpn_graph_type == "fully":
-            _lib.check(L.pemp_fully_graph(_lib.ptr(node_off), _lib.ptr(edge_off), B, E, _lib.ptr(edge_index), st))
+            _lib.check(L.pemp_fully_graph(_lib.ptr(node_off), _lib.ptr(fully_off), B, E, _lib.ptr(edge_index), st))
         else:
+            edge_off_h = np.zeros(B + 1, np.int64)
+            edge_off_h[1:] = np.cumsum(per)
+            edge_off = torch.from_numpy(edge_off_h).to(dev)
             _lib.check(L.pemp_knn_graph_emit(_lib.ptr(node_off), nh_p, B, _lib.ptr(edge_off), E, _lib.ptr(ws),
                                              ws.numel(), _lib.ptr(edge_index), st))
         return edge_index

@@ -136,12 +136,27 @@ class NodeClassificationMPNSimple(nn.Module):
         self.aggr_code = AGGR_CODES[aggr]
         self._folded = None
         self._folded_key = None
+        self._tensors = None
         self._ws = _lib.Workspace()
 
     # --------------------------------------------------------------------------------------
+    def _apply(self, fn, *args, **kwargs):
+        # .to()/.cuda()/.float() move or re-create tensors: drop the folded cache and tensor list
+        self._tensors = None
+        self._folded = None
+        return super()._apply(fn, *args, **kwargs)
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        self._tensors = None            # load_state_dict(assign=True) may swap tensor objects
+        return super()._load_from_state_dict(*args, **kwargs)
+
     def _weights(self, device):
-        key = (device, tuple(p._version for p in self.parameters()), tuple(b._version for b in self.buffers()),
-               tuple(p.data_ptr() for p in self.parameters()))
+        # The fold is cached against the version counters of every parameter/buffer (in-place
+        # updates such as load_state_dict bump them); the flat tensor list itself is cached
+        # because walking the module tree costs ~0.3 ms per call.
+        if self._tensors is None:
+            self._tensors = list(self.parameters()) + list(self.buffers())
+        key = (device, [t._version for t in self._tensors])
         if self._folded is None or self._folded_key != key:
             self._folded = fold_weights(self, device)
             self._folded_key = key

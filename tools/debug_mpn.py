@@ -29,7 +29,7 @@ def carve(ws, T, N, E):
         off += sz
 
     K = T * N
-    take("cnt", K + 1, torch.int32); take("cursor", K + 1, torch.int32); take("err", 4, torch.int32)
+    take("err", 64, torch.int32); take("cnt", K + 1, torch.int32)
     take("seg", K + 1, torch.int32); take("wg_start", 19, torch.int32)
     for n in ("perm", "s_src", "s_dst", "s_orig"):
         take(n, E, torch.int32)
