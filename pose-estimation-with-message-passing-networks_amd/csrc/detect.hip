@@ -551,16 +551,6 @@ __global__ __launch_bounds__(256) void emit_kernel(const float* __restrict__ s, 
   }
 }
 
-static int num_cus() {
-  static int n = [] {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 256;
-    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) return 256;
-    return v;
-  }();
-  return n;
-}
-
 template <int P, int MODE, bool VEC>
 static void launch_nms(const float* s, const float* masks, const DetectGeom& g, float thr, int use_thr,
                        const DetectWs& w, hipStream_t st) {

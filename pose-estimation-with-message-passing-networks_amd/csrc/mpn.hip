@@ -17,6 +17,9 @@
 // MFMA: v_mfma_f32_16x16x4_f32 (exact fp32). Fragment convention per wave: item (edge or node)
 // c = lane & 15 on the MFMA N dimension, features 16*blk + 4*(lane >> 4) + r in registers, so one
 // layer's accumulator is the next layer's B operand with no data movement.
+#include <limits.h>
+
+#include <algorithm>
 #include <math.h>
 
 #include "pemp_common.h"
@@ -25,10 +28,8 @@ namespace pemp {
 namespace {
 
 constexpr int D = 64;
-constexpr int ITEM = 128;   // edges per wave work item
 constexpr int LDW = 72;     // LDS row stride of a 64x64 weight tile (conflict-free ds_read_b128)
 constexpr int MAXT = 17;
-constexpr int TRS = 68;    // row stride of the per-wave [16][64] staging tile (conflict-free b128 writes)
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float a, float b, float c, float d) {
@@ -214,7 +215,7 @@ __global__ __launch_bounds__(256) void zero_words_kernel(int* __restrict__ p, in
 // (all loads of a pass in flight together), carry across passes.
 constexpr int SCAN_SPT = 16;
 __global__ __launch_bounds__(1024) void mpn_scan_kernel(const int* __restrict__ cnt, int64_t K, int64_t N, int T,
-                                                        int* __restrict__ seg, int* __restrict__ wg_start) {
+                                                        int G, int* __restrict__ seg, int* __restrict__ wg_start) {
   __shared__ int sh[40];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int carry = 0;
@@ -267,12 +268,37 @@ __global__ __launch_bounds__(1024) void mpn_scan_kernel(const int* __restrict__ 
   if (threadIdx.x <= T) sh[20 + threadIdx.x] = seg[(int64_t)threadIdx.x * N];
   __syncthreads();
   if (threadIdx.x == 0) {
+    // split G edge-pass workgroups (one per CU) over the types in proportion to their edge
+    // counts: floor shares, >= 1 per non-empty type, leftovers by largest remainder; sum <= G
+    const int64_t etot = carry;
+    int gt[MAXT];
+    int64_t rem[MAXT];
+    int used = 0;
+    for (int t = 0; t < T; ++t) {
+      const int64_t et = sh[20 + t + 1] - sh[20 + t];
+      gt[t] = et > 0 ? (int)(et * G / etot) : 0;
+      rem[t] = et > 0 ? (et * G) % etot : -1;
+      if (et > 0 && gt[t] == 0) { gt[t] = 1; rem[t] = -1; }
+      used += gt[t];
+    }
+    for (; used < G; ++used) {
+      int best = -1;
+      for (int t = 0; t < T; ++t)
+        if (rem[t] >= 0 && (best < 0 || rem[t] > rem[best])) best = t;
+      if (best < 0) break;
+      ++gt[best];
+      rem[best] = -1;
+    }
+    for (; used > G; --used) {
+      int big = 0;
+      for (int t = 1; t < T; ++t) if (gt[t] > gt[big]) big = t;
+      if (gt[big] <= 1) break;
+      --gt[big];
+    }
     int acc = 0;
     wg_start[0] = 0;
     for (int t = 0; t < T; ++t) {
-      const int et = sh[20 + t + 1] - sh[20 + t];
-      const int items = (et + ITEM - 1) / ITEM;
-      acc += (items + 3) / 4;
+      acc += gt[t];
       wg_start[t + 1] = acc;
     }
   }
@@ -460,98 +486,178 @@ struct EdgeStepArgs {
   int write_next;
 };
 
+// ---- in-row (16-lane) DPP primitives: lane c = lane & 15 of every row holds edge c of the tile ----
+constexpr int DPP_SHR1 = 0x111, DPP_SHR2 = 0x112, DPP_SHR4 = 0x114, DPP_SHR8 = 0x118;
+constexpr int DPP_SHL1 = 0x101, DPP_SHL2 = 0x102, DPP_SHL4 = 0x104, DPP_SHL8 = 0x108, DPP_SHL15 = 0x10F;
+
+// value of lane c -/+ k of the same row; lanes whose source is outside the row get `old`
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v, float old) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dppi(int v, int old) {
+  return __builtin_amdgcn_update_dpp(old, v, CTRL, 0xF, 0xF, false);
+}
+
+// Chunk structure of a tile: a chunk = the edges of one (target, type) segment inside the tile.
+// d = distance to the chunk head, u = distance to the chunk tail.
+struct Chunks {
+  int d, u;
+  bool head, tail;
+};
+
+__device__ __forceinline__ Chunks chunks_of(int seg, int c) {
+  const int prev = dppi<DPP_SHR1>(seg, INT_MIN), next = dppi<DPP_SHL1>(seg, INT_MIN);
+  Chunks k;
+  k.head = prev != seg;
+  k.tail = next != seg;
+  int hs = k.head ? c : 0, te = k.tail ? c : 15;
+  hs = max(hs, dppi<DPP_SHR1>(hs, 0)); te = min(te, dppi<DPP_SHL1>(te, 15));
+  hs = max(hs, dppi<DPP_SHR2>(hs, 0)); te = min(te, dppi<DPP_SHL2>(te, 15));
+  hs = max(hs, dppi<DPP_SHR4>(hs, 0)); te = min(te, dppi<DPP_SHL4>(te, 15));
+  hs = max(hs, dppi<DPP_SHR8>(hs, 0)); te = min(te, dppi<DPP_SHL8>(te, 15));
+  k.d = c - hs;
+  k.u = te - c;
+  return k;
+}
+
+// segmented inclusive scans along the row (Hillis-Steele; step k adds lane c-k when it is in
+// the same chunk)
+template <bool MAX>
+__device__ __forceinline__ float seg_scan(float v, int d) {
+  const float id = MAX ? -INFINITY : 0.0f;
+  float o;
+  o = dppf<DPP_SHR1>(v, id); v = MAX ? fmaxf(v, d >= 1 ? o : id) : v + (d >= 1 ? o : 0.0f);
+  o = dppf<DPP_SHR2>(v, id); v = MAX ? fmaxf(v, d >= 2 ? o : id) : v + (d >= 2 ? o : 0.0f);
+  o = dppf<DPP_SHR4>(v, id); v = MAX ? fmaxf(v, d >= 4 ? o : id) : v + (d >= 4 ? o : 0.0f);
+  o = dppf<DPP_SHR8>(v, id); v = MAX ? fmaxf(v, d >= 8 ? o : id) : v + (d >= 8 ? o : 0.0f);
+  return v;
+}
+
+// every lane of a chunk gets the value at the chunk tail (v non-decreasing along the chunk)
+__device__ __forceinline__ float seg_bcast_tail_max(float v, int u) {
+  float o;
+  o = dppf<DPP_SHL1>(v, -INFINITY); v = fmaxf(v, u >= 1 ? o : -INFINITY);
+  o = dppf<DPP_SHL2>(v, -INFINITY); v = fmaxf(v, u >= 2 ? o : -INFINITY);
+  o = dppf<DPP_SHL4>(v, -INFINITY); v = fmaxf(v, u >= 4 ? o : -INFINITY);
+  o = dppf<DPP_SHL8>(v, -INFINITY); v = fmaxf(v, u >= 8 ? o : -INFINITY);
+  return v;
+}
+
+__device__ __forceinline__ float readlane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+constexpr int EDGE_WAVES = 16;   // waves per edge-pass workgroup (one workgroup per CU)
+
+// LDS image of the edge pass (floats): three 64x64 weight tiles, e2_b | attn_w, and for the
+// fused published edge head (HEAD 1) its 64x64 and 32x64 tiles + biases + last row.
+constexpr int LDS_W = 3 * D * LDW;
+constexpr int LDS_VEC = 2 * D;
+constexpr int LDS_HEAD = (D + 32) * LDW + D + 32 + 32;
+
 // HEAD: 0 = no edge head, 1 = published head 64 -> 64 -> 32 -> 1 (ReLU, ReLU), 2 = generic pemp_mlp
+//
+// Work split (balanced, no atomics): the edges of source type t (contiguous in the type-major
+// order) are cut into wg_start[t+1]-wg_start[t] equal workgroup ranges, each cut into
+// EDGE_WAVES equal wave ranges; every range boundary is moved forward to the next segment
+// start, so each (target, type) segment is reduced by exactly one wave. A wave walks its range
+// in 16-edge tiles; a segment that crosses a tile boundary is carried in registers.
 template <int AGG, int HEAD>
-__global__ __launch_bounds__(256) void edge_step_kernel(EdgeStepArgs a) {
+__global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* wl = sm;                               // [3][64][LDW]: e1_w, e2_w, msg_w[t]
-  float* vec = sm + 3 * D * LDW;                // e2_b[64] | attn_w[64]
+  float* wl = sm;                               // [3][64][LDW]: e1_w (e_cur part), e2_w, msg_w[t]
+  float* vec = sm + LDS_W;                      // e2_b[64] | attn_w[64]
+  float* hw = vec + LDS_VEC;                    // HEAD 1: [64][LDW] L1.w, [32][LDW] L2.w, b1[64], b2[32], w3[32]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
-  float* tr = vec + 2 * D + wave * 16 * TRS;    // this wave's [16 edges][64 features] staging tile
   const int T = a.T;
   const int blk = blockIdx.x;
   if (blk >= a.wg_start[T]) return;             // uniform for the block
   int t = 0;
   while (t + 1 < T && a.wg_start[t + 1] <= blk) ++t;
-  const float* srcs[3] = {a.e1_w, a.e2_w, a.msg_w + (int64_t)t * D * D};
-  for (int idx = threadIdx.x; idx < 3 * D * 16; idx += 256) {
-    const int mtx = idx / (D * 16), rem = idx - mtx * D * 16, row = rem >> 4, c4 = (rem & 15) * 4;
-    *reinterpret_cast<float4*>(&wl[(mtx * D + row) * LDW + c4]) = ld4(srcs[mtx] + row * D + c4);
+  {
+    const float* srcs[3] = {a.e1_w, a.e2_w, a.msg_w + (int64_t)t * D * D};
+    for (int idx = threadIdx.x; idx < 3 * D * 16; idx += 64 * EDGE_WAVES) {
+      const int mtx = idx / (D * 16), rem = idx - mtx * D * 16, row = rem >> 4, c4 = (rem & 15) * 4;
+      *reinterpret_cast<float4*>(&wl[(mtx * D + row) * LDW + c4]) = ld4(srcs[mtx] + row * D + c4);
+    }
+    if (threadIdx.x < D) vec[threadIdx.x] = a.e2_b[threadIdx.x];
+    else if (threadIdx.x < 2 * D) vec[threadIdx.x] = (AGG == PEMP_AGGR_ATTN) ? a.attn_w[threadIdx.x - D] : 0.0f;
+    if (HEAD == 1) {
+      for (int idx = threadIdx.x; idx < (D + 32) * 16; idx += 64 * EDGE_WAVES) {
+        const int row = idx >> 4, c4 = (idx & 15) * 4;
+        const float* src = row < D ? a.head.layer[0].w + row * D : a.head.layer[1].w + (row - D) * D;
+        *reinterpret_cast<float4*>(&hw[row * LDW + c4]) = ld4(src + c4);
+      }
+      float* hb = hw + (D + 32) * LDW;
+      if (threadIdx.x < D) hb[threadIdx.x] = a.head.layer[0].b[threadIdx.x];
+      else if (threadIdx.x < D + 32) hb[threadIdx.x] = a.head.layer[1].b[threadIdx.x - D];
+      else if (threadIdx.x < D + 64) hb[threadIdx.x] = a.head.layer[2].w[threadIdx.x - D - 32];
+    }
   }
-  if (threadIdx.x < D) vec[threadIdx.x] = a.e2_b[threadIdx.x];
-  else if (threadIdx.x < 2 * D) vec[threadIdx.x] = (AGG == PEMP_AGGR_ATTN) ? a.attn_w[threadIdx.x - D] : 0.0f;
   __syncthreads();
-  const float* W1 = wl;
-  const float* W2 = wl + D * LDW;
-  const float* WM = wl + 2 * D * LDW;
 
+  // ---- this wave's range ----
   const int64_t N = a.N;
   const int ts = a.seg[t * N], te = a.seg[(t + 1) * N];
-  const int item = (blk - a.wg_start[t]) * 4 + wave;
-  const int cs = ts + item * ITEM;
-  if (cs >= te) return;
-  const int ce = min(cs + ITEM, te);
-  int first = cs;
-  if (cs > ts && a.s_dst[cs] == a.s_dst[cs - 1]) first = a.seg[t * N + a.s_dst[cs] + 1];
-  const int end = (ce == te) ? te : a.seg[t * N + a.s_dst[ce - 1] + 1];
+  const int gt = a.wg_start[t + 1] - a.wg_start[t], j = blk - a.wg_start[t];
+  const int64_t n_t = te - ts;
+  const int lo = ts + (int)(n_t * j / gt), hi = ts + (int)(n_t * (j + 1) / gt);
+  const int64_t n_b = hi - lo;
+  auto snap = [&](int p) -> int {               // first segment start at or after p
+    if (p <= ts || p >= te) return p;
+    const int dp = a.s_dst[p];
+    return dp == a.s_dst[p - 1] ? a.seg[t * N + dp + 1] : p;
+  };
+  const int first = snap(lo + (int)(n_b * wave / EDGE_WAVES));
+  const int end = snap(lo + (int)(n_b * (wave + 1) / EDGE_WAVES));
   if (first >= end) return;
   const float* ntP = a.NT + 128 + 64 * t;
 
-  // carry of the segment continuing into the next tile: per lane (= feature) + wave-uniform scalars
-  float cacc = 0.f;
-  int cseg = -1;
+  // carry of the chunk continuing into the next tile: features in lane c == 0 of each row,
+  // running max / normaliser wave-uniform
+  float cacc[4][4];
   float cM = 0.f, cl = 0.f;
+  bool have_carry = false;
 
-  // two-stage software pipeline: indices of tile k+2 and gathered rows of tile k+1 are in flight
-  // while tile k computes.
-  auto load_idx = [&](int b, int& s_, int& d_) {
-    const int q = min(b + c, end - 1);
-    s_ = a.s_src[q];
-    d_ = a.s_dst[q];
-  };
-  struct Rows { float4 q[4], xa[4], xb[4], ec[4], xp[4]; };
-  auto load_rows = [&](int b, int s_, int d_, Rows& R) {
-    const int q = min(b + c, end - 1);
-#pragma unroll
-    for (int ob = 0; ob < 4; ++ob) {
-      const int f = 16 * ob + 4 * g;
-      R.q[ob] = ld4(a.Q0 + (int64_t)q * D + f);
-      R.xa[ob] = ld4(a.NT + (int64_t)d_ * a.t_nt_ld + f);
-      R.xb[ob] = ld4(a.NT + (int64_t)s_ * a.t_nt_ld + 64 + f);
-      R.ec[ob] = ld4(a.e_cur + (int64_t)q * D + f);
-      R.xp[ob] = ld4(ntP + (int64_t)d_ * a.t_nt_ld + f);
-    }
-  };
-  int src_n, dst_n, src_nn = 0, dst_nn = 0;
-  load_idx(first, src_n, dst_n);
-  Rows R;
-  load_rows(first, src_n, dst_n, R);
-  int src = src_n, dst = dst_n;
-  if (first + 16 < end) load_idx(first + 16, src_nn, dst_nn);
-
+  int dst_n = a.s_dst[min(first + c, end - 1)];
+  int src_n = a.s_src[min(first + c, end - 1)];
   for (int base = first; base < end; base += 16) {
+    // opaque zero: keeps the compiler from hoisting the LDS weight fragments out of the loop
+    // (192+ VGPRs of loop-invariant loads would spill)
+    int z = 0;
+    asm volatile("" : "+s"(z));
+    const float* W1 = wl + z;
+    const float* W2 = wl + z + D * LDW;
+    const float* WM = wl + z + 2 * D * LDW;
+    const float* hwz = hw + z;
     const int p = base + c;
     const bool valid = p < end;
-    const int seg = valid ? dst : -1;
-    const int nvalid = min(16, end - base);
-    const bool last_tile = base + 16 >= end;
-    // edge MLP layer 1: h = ReLU(Q0 + A[dst] + B[src] + W1_e_cur · e_cur)
+    const int q = min(p, end - 1);
+    const int dst = dst_n, src = src_n;
+    const bool more = base + 16 < end;
+    if (more) {                                   // next tile's indices
+      const int qn = min(base + 16 + c, end - 1);
+      dst_n = a.s_dst[qn];
+      src_n = a.s_src[qn];
+    }
+    // gathers: Q0 / e_cur rows of the edge, node-table rows of target and source
     float h[4][4], ein[4][4], m[4][4];
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob) {
-      h[ob][0] = R.q[ob].x + R.xa[ob].x + R.xb[ob].x; h[ob][1] = R.q[ob].y + R.xa[ob].y + R.xb[ob].y;
-      h[ob][2] = R.q[ob].z + R.xa[ob].z + R.xb[ob].z; h[ob][3] = R.q[ob].w + R.xa[ob].w + R.xb[ob].w;
-      ein[ob][0] = R.ec[ob].x; ein[ob][1] = R.ec[ob].y; ein[ob][2] = R.ec[ob].z; ein[ob][3] = R.ec[ob].w;
-      m[ob][0] = R.xp[ob].x; m[ob][1] = R.xp[ob].y; m[ob][2] = R.xp[ob].z; m[ob][3] = R.xp[ob].w;
+      const int f = 16 * ob + 4 * g;
+      const float4 q0 = ld4(a.Q0 + (int64_t)q * D + f);
+      const float4 xa = ld4(a.NT + (int64_t)dst * a.t_nt_ld + f);
+      const float4 xb = ld4(a.NT + (int64_t)src * a.t_nt_ld + 64 + f);
+      const float4 ec = ld4(a.e_cur + (int64_t)q * D + f);
+      const float4 xp = ld4(ntP + (int64_t)dst * a.t_nt_ld + f);
+      h[ob][0] = q0.x + xa.x + xb.x; h[ob][1] = q0.y + xa.y + xb.y;
+      h[ob][2] = q0.z + xa.z + xb.z; h[ob][3] = q0.w + xa.w + xb.w;
+      ein[ob][0] = ec.x; ein[ob][1] = ec.y; ein[ob][2] = ec.z; ein[ob][3] = ec.w;
+      m[ob][0] = xp.x; m[ob][1] = xp.y; m[ob][2] = xp.z; m[ob][3] = xp.w;
     }
-    // prefetch: rows of tile k+1 (indices already here), indices of tile k+2
-    const int src_c = src, dst_c = dst;
-    if (!last_tile) {
-      load_rows(base + 16, src_nn, dst_nn, R);
-      src = src_nn; dst = dst_nn;
-      if (base + 32 < end) load_idx(base + 32, src_nn, dst_nn);
-    }
-    (void)src_c; (void)dst_c;
+    // edge MLP layer 1: h = ReLU(Q0 + A[dst] + B[src] + W1_e_cur · e_cur)
     gemm_frag<4, 4>(W1, LDW, ein, h);
     relu_frag<4>(h);
     // layer 2: e' = ReLU(W2 · h + b2)
@@ -580,102 +686,99 @@ __global__ __launch_bounds__(256) void edge_step_kernel(EdgeStepArgs a) {
       av += __shfl_xor(av, 32);
       av += a.attn_b;
     }
-    // message: m = ReLU(P_t[dst] + W_t_e · e')   (P row prefetched with the tile)
+    // message: m = ReLU(P_t[dst] + W_t_e · e')
     gemm_frag<4, 4>(WM, LDW, ep, m);
     relu_frag<4>(m);
 
-    // ---- per-column chunk statistics (chunk = the part of a segment inside this tile) ----
-    const SegMask sm = seg_mask(seg, c);
-    float M = 0.f, l, pe = 1.0f;
+    // ---- segmented reduction of the tile, carry in / out ----
+    const int seg = valid ? dst : -1 - c;        // padding lanes: singleton chunks, never written
+    const Chunks ck = chunks_of(seg, c);
+    const bool carry_in = have_carry;            // wave-uniform: set only when the segment continues
+    float M = 0.f, l = 1.0f, pe = 1.0f;
     if (AGG == PEMP_AGGR_ATTN) {
-      M = fmaxf(scan_max(av, sm), scan_max_bwd(av, sm));
+      M = seg_bcast_tail_max(seg_scan<true>(av, ck.d), ck.u);
+      if (carry_in && ck.d == c) M = fmaxf(M, cM);   // head chunk continues the carried segment
       pe = expf(av - M);
-      l = scan_add(pe, sm);                      // chunk sum of exp at the chunk tail
-    } else {
-      l = scan_add(1.0f, sm);                    // chunk length at the chunk tail
+      l = pe;
     }
-    // ---- stage pe * m as [edge][feature], then lanes = features walk the 16 edges ----
+    float v[4][4];
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob)
-      st4(tr + c * TRS + 16 * ob + 4 * g, pe * m[ob][0], pe * m[ob][1], pe * m[ob][2], pe * m[ob][3]);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (cseg >= 0 && __builtin_amdgcn_readlane(seg, 0) != cseg) {   // carried segment ended at the tile edge
-      const float o = (AGG == PEMP_AGGR_ATTN) ? cacc / (cl + 1e-12f) : (AGG == PEMP_AGGR_MEAN) ? cacc / cl : cacc;
-      a.agg[((int64_t)cseg * T + t) * D + lane] = o;
-      cseg = -1;
-    }
-    float acc = 0.f;
-    int h0 = 0;                                  // head column of the current chunk
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      if (e < nvalid) {
-        const int se = __builtin_amdgcn_readlane(seg, e);
-        const bool head = e == 0 || se != __builtin_amdgcn_readlane(seg, e > 0 ? e - 1 : 0);
-        const bool tail = e == nvalid - 1 || se != __builtin_amdgcn_readlane(seg, e < 15 ? e + 1 : 15);
-        const float x = tr[e * TRS + lane];
-        if (head) { acc = x; h0 = e; }
-        else acc = (AGG == PEMP_AGGR_MAX) ? fmaxf(acc, x) : acc + x;
-        if (tail) {
-          float Mc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(M), e));
-          float lc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l), e));
-          if (h0 == 0 && se == cseg) {           // first chunk continues the carried segment
-            if (AGG == PEMP_AGGR_ATTN) {
-              const float Mn = fmaxf(cM, Mc), fc = expf(cM - Mn), fn = expf(Mc - Mn);
-              acc = cacc * fc + acc * fn;
-              lc = cl * fc + lc * fn;
-              Mc = Mn;
-            } else if (AGG == PEMP_AGGR_MAX) {
-              acc = fmaxf(acc, cacc);
-              lc += cl;
-            } else {
-              acc += cacc;
-              lc += cl;
-            }
-            cseg = -1;
-          }
-          if (e == 15 && !last_tile) {           // may continue in the next tile
-            cacc = acc; cM = Mc; cl = lc; cseg = se;
-          } else {
-            const float o = (AGG == PEMP_AGGR_ATTN) ? acc / (lc + 1e-12f) : (AGG == PEMP_AGGR_MEAN) ? acc / lc : acc;
-            a.agg[((int64_t)se * T + t) * D + lane] = o;
-          }
-        }
+      for (int r = 0; r < 4; ++r) v[ob][r] = (AGG == PEMP_AGGR_ATTN) ? pe * m[ob][r] : m[ob][r];
+    if (carry_in && c == 0) {
+      if (AGG == PEMP_AGGR_ATTN) {
+        const float f = expf(cM - M);
+        l += cl * f;
+#pragma unroll
+        for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[ob][r] = fmaf(cacc[ob][r], f, v[ob][r]);
+      } else {
+        l += cl;
+#pragma unroll
+        for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            v[ob][r] = (AGG == PEMP_AGGR_MAX) ? fmaxf(v[ob][r], cacc[ob][r]) : v[ob][r] + cacc[ob][r];
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (HEAD == 1) {   // fused edge-classification head on e' (after the aggregation: fewer live registers)
-      const pemp_layer& L1 = a.head.layer[0];
-      const pemp_layer& L2 = a.head.layer[1];
-      const pemp_layer& L3 = a.head.layer[2];
+    if (AGG == PEMP_AGGR_ATTN || AGG == PEMP_AGGR_MEAN) l = seg_scan<false>(l, ck.d);   // normaliser / count
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[ob][r] = seg_scan<AGG == PEMP_AGGR_MAX>(v[ob][r], ck.d);
+    // the chunk at the tile end continues iff the next tile starts with the same target
+    const int seg15 = __builtin_amdgcn_readlane(seg, 15);
+    const bool carry_out = more && __builtin_amdgcn_readlane(dst_n, 0) == seg15;
+    if (carry_out) {
+      cl = readlane_f(l, 15);
+      cM = readlane_f(M, 15);
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cacc[ob][r] = dppf<DPP_SHL15>(v[ob][r], 0.0f);   // lane 15 -> lane 0
+    }
+    have_carry = carry_out;
+    if (valid && ck.tail && !(carry_out && c == 15)) {
+      const float inv = (AGG == PEMP_AGGR_ATTN) ? 1.0f / (l + 1e-12f) : (AGG == PEMP_AGGR_MEAN) ? 1.0f / l : 1.0f;
+      float* o = a.agg + ((int64_t)seg * T + t) * D + 4 * g;
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob) {
+        if (AGG == PEMP_AGGR_ATTN || AGG == PEMP_AGGR_MEAN)
+          st4(o + 16 * ob, v[ob][0] * inv, v[ob][1] * inv, v[ob][2] * inv, v[ob][3] * inv);
+        else
+          st4(o + 16 * ob, v[ob][0], v[ob][1], v[ob][2], v[ob][3]);
+      }
+    }
+
+    if (HEAD == 1) {   // fused edge-classification head on e'
+      const float* hb = hwz + (D + 32) * LDW;
       float h1[4][4], h2[2][4];
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob) {
-        const float4 bb = ld4(L1.b + 16 * ob + 4 * g);
+        const float4 bb = ld4(hb + 16 * ob + 4 * g);
         h1[ob][0] = bb.x; h1[ob][1] = bb.y; h1[ob][2] = bb.z; h1[ob][3] = bb.w;
       }
-      gemm_frag<4, 4>(L1.w, 64, ep, h1);
+      gemm_frag<4, 4>(hwz, LDW, ep, h1);
       relu_frag<4>(h1);
 #pragma unroll
       for (int ob = 0; ob < 2; ++ob) {
-        const float4 bb = ld4(L2.b + 16 * ob + 4 * g);
+        const float4 bb = ld4(hb + D + 16 * ob + 4 * g);
         h2[ob][0] = bb.x; h2[ob][1] = bb.y; h2[ob][2] = bb.z; h2[ob][3] = bb.w;
       }
-      gemm_frag<4, 2>(L2.w, 64, h1, h2);
+      gemm_frag<4, 2>(hwz + D * LDW, LDW, h1, h2);
       relu_frag<2>(h2);
       float lg = 0.f;
 #pragma unroll
       for (int ob = 0; ob < 2; ++ob) {
-        const float4 w = ld4(L3.w + 16 * ob + 4 * g);
+        const float4 w = ld4(hb + D + 32 + 16 * ob + 4 * g);
         lg = fmaf(w.x, h2[ob][0], lg); lg = fmaf(w.y, h2[ob][1], lg);
         lg = fmaf(w.z, h2[ob][2], lg); lg = fmaf(w.w, h2[ob][3], lg);
       }
       lg += __shfl_xor(lg, 16);
       lg += __shfl_xor(lg, 32);
-      if (valid && g == 0) a.edge_logits[a.s_orig[p]] = lg + L3.b[0];
+      if (valid && g == 0) a.edge_logits[a.s_orig[p]] = lg + a.head.layer[2].b[0];
     } else if (HEAD == 2) {
       float h2[4][4];
       mlp_frag<4>(a.head, ep, h2);
@@ -742,13 +845,14 @@ static bool published_head(const pemp_mlp& m) {
 
 template <int AGG>
 static void launch_edge_step(const EdgeStepArgs& a, bool head, int grid, hipStream_t st) {
-  const size_t lds = ((size_t)3 * D * LDW + 2 * D + 4 * 16 * TRS) * sizeof(float);
+  const size_t lds = (size_t)(LDS_W + LDS_VEC) * sizeof(float);
+  const dim3 blk(64 * EDGE_WAVES);
   if (!head)
-    hipLaunchKernelGGL((edge_step_kernel<AGG, 0>), dim3(grid), dim3(256), lds, st, a);
+    hipLaunchKernelGGL((edge_step_kernel<AGG, 0>), dim3(grid), blk, lds, st, a);
   else if (published_head(a.head))
-    hipLaunchKernelGGL((edge_step_kernel<AGG, 1>), dim3(grid), dim3(256), lds, st, a);
+    hipLaunchKernelGGL((edge_step_kernel<AGG, 1>), dim3(grid), blk, lds + LDS_HEAD * sizeof(float), st, a);
   else
-    hipLaunchKernelGGL((edge_step_kernel<AGG, 2>), dim3(grid), dim3(256), lds, st, a);
+    hipLaunchKernelGGL((edge_step_kernel<AGG, 2>), dim3(grid), blk, lds, st, a);
 }
 
 static int rows_mlp(const char* label, const pemp_mlp& m, const float* in, int64_t ld_in, int64_t M, float* out,
@@ -836,7 +940,8 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
                        ws.cnt, ws.err);
     PEMP_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(mpn_scan_kernel, dim3(1), dim3(1024), 0, st, ws.cnt, K, N, T, ws.seg, ws.wg_start);
+  hipLaunchKernelGGL(mpn_scan_kernel, dim3(1), dim3(1024), 0, st, ws.cnt, K, N, T, std::max(num_cus(), T), ws.seg,
+                     ws.wg_start);
   PEMP_LAUNCH_CHECK();
   if (E > 0) {
     hipLaunchKernelGGL(mpn_scatter_kernel, dim3(grid1d(E, 256)), dim3(256), 0, st, edge_index, node_types, N, E, T,
@@ -861,7 +966,7 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
   // ---- iterations ----
   const int NO = 128 + 64 * T;
   const int steps = desc->steps, aux = desc->aux_loss_steps;
-  const int edge_grid = (int)(E / (4 * ITEM)) + 2 * T + 1;
+  const int edge_grid = std::max(num_cus(), T);   // >= wg_start[T] (see mpn_scan_kernel)
   float* e_cur = ws.EA;
   float* e_nxt = ws.EB;
   int rec = 0;

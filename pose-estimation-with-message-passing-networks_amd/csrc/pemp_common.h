@@ -60,6 +60,17 @@ static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream
 
 static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+// compute units of the current device (cached per process; 256 on MI355X)
+static inline int num_cus() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) return 256;
+    return v;
+  }();
+  return n;
+}
+
 // Workspace carving: bump allocator over a caller-owned buffer (256-B aligned slices).
 struct Carver {
   char* base;
