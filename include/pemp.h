@@ -163,8 +163,9 @@ typedef struct pemp_mpn_desc {
 size_t pemp_mpn_workspace_size(const pemp_mpn_desc* desc, int64_t N, int64_t E);
 /* x [N,node_in_dim], edge_attr [E,edge_attr_dim], edge_index [2,E] (row 0 source j, row 1
  * target i), node_types [N] (already mapped by sum_node_types; values < T).
- * Outputs, one slot per recorded iteration r (n_rec = min(aux+1, steps)):
- *   edge_logits [n_rec][E], node_logits [n_rec][N], class_logits [n_rec][N][J]. */
+ * Outputs (n_rec = min(aux+1, steps) recorded iterations, NodeClassificationMPNSimple.py:81-94):
+ *   edge_logits [n_rec][E]; node_logits [n_rec+1][N] and class_logits [n_rec+1][N][J], whose
+ *   last slot is the head evaluation after the loop (:93-94). */
 int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weights* weights, const float* x,
                      const float* edge_attr, const int64_t* edge_index, const int64_t* node_types,
                      int64_t N, int64_t E, float* edge_logits, float* node_logits, float* class_logits,
@@ -177,7 +178,7 @@ int pemp_mpn_status(const pemp_mpn_desc* desc, int64_t N, int64_t E, const void*
 /* Opt-in profiler: while enabled, hipEvents are recorded on the launch stream around every kernel
  * whose label contains `filter` ("*" = all, NULL or "" = off). pemp_prof_report synchronises those
  * events and writes "label count total_ms" lines into buf (returns the full length), then resets.
- * Labels: detect_nms, detect_select, pack_nodes, fully_graph, edge_features, knn_adj, knn_emit,
+ * Labels: detect_nms, detect_top, detect_emit, pack_nodes, fully_graph, edge_features, knn_adj, knn_emit,
  * mpn_prepare, node_embed, edge_embed, node_table, edge_step, edge_step_head, node_update, heads. */
 int pemp_prof_enable(const char* filter);
 int pemp_prof_report(char* buf, size_t len);

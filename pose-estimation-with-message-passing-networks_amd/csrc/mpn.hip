@@ -30,6 +30,7 @@ namespace {
 constexpr int D = 64;
 constexpr int LDW = 72;     // LDS row stride of a 64x64 weight tile (conflict-free ds_read_b128)
 constexpr int MAXT = 17;
+constexpr int EDGE_WAVES = 16;   // waves per edge-pass / edge-embedding workgroup (one workgroup per CU)
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float a, float b, float c, float d) {
@@ -216,7 +217,7 @@ __global__ __launch_bounds__(256) void zero_words_kernel(int* __restrict__ p, in
 constexpr int SCAN_SPT = 16;
 __global__ __launch_bounds__(1024) void mpn_scan_kernel(const int* __restrict__ cnt, int64_t K, int64_t N, int T,
                                                         int G, int* __restrict__ seg, int* __restrict__ wg_start) {
-  __shared__ int sh[40];
+  __shared__ int sh[20 + 2 * (MAXT + 1)];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int carry = 0;
   for (int64_t base = 0; base < K; base += 1024 * SCAN_SPT) {
@@ -267,29 +268,39 @@ __global__ __launch_bounds__(1024) void mpn_scan_kernel(const int* __restrict__ 
   // wg_start: T + 1 reads of seg in parallel, then a short serial sum
   if (threadIdx.x <= T) sh[20 + threadIdx.x] = seg[(int64_t)threadIdx.x * N];
   __syncthreads();
+  // split G edge-pass workgroups (one per CU) over the types in proportion to their edge counts:
+  // floor shares, >= 1 per non-empty type, leftovers by largest remainder (ties: lower type);
+  // sum <= G. Thread t < T owns type t.
+  int* gt = sh + 20 + MAXT + 1;          // [MAXT] shares
+  __shared__ long long rem_sh[MAXT];
+  const int64_t etot = carry;
+  if (threadIdx.x < T) {
+    const int t = threadIdx.x;
+    const int64_t et = sh[20 + t + 1] - sh[20 + t];
+    int share = et > 0 ? (int)(et * G / etot) : 0;
+    long long r = et > 0 ? (et * G) % etot : -1;
+    if (et > 0 && share == 0) { share = 1; r = -1; }
+    gt[t] = share;
+    rem_sh[t] = r;
+  }
+  __syncthreads();
+  int add = 0;
+  if (threadIdx.x < T) {
+    const int t = threadIdx.x;
+    int used = 0, rank = 0;
+    for (int u = 0; u < T; ++u) {
+      used += gt[u];
+      rank += rem_sh[u] > rem_sh[t] || (rem_sh[u] == rem_sh[t] && u < t);
+    }
+    add = rem_sh[t] >= 0 && rank < G - used;
+  }
+  __syncthreads();
+  if (threadIdx.x < T) gt[threadIdx.x] += add;
+  __syncthreads();
   if (threadIdx.x == 0) {
-    // split G edge-pass workgroups (one per CU) over the types in proportion to their edge
-    // counts: floor shares, >= 1 per non-empty type, leftovers by largest remainder; sum <= G
-    const int64_t etot = carry;
-    int gt[MAXT];
-    int64_t rem[MAXT];
     int used = 0;
-    for (int t = 0; t < T; ++t) {
-      const int64_t et = sh[20 + t + 1] - sh[20 + t];
-      gt[t] = et > 0 ? (int)(et * G / etot) : 0;
-      rem[t] = et > 0 ? (et * G) % etot : -1;
-      if (et > 0 && gt[t] == 0) { gt[t] = 1; rem[t] = -1; }
-      used += gt[t];
-    }
-    for (; used < G; ++used) {
-      int best = -1;
-      for (int t = 0; t < T; ++t)
-        if (rem[t] >= 0 && (best < 0 || rem[t] > rem[best])) best = t;
-      if (best < 0) break;
-      ++gt[best];
-      rem[best] = -1;
-    }
-    for (; used > G; --used) {
+    for (int t = 0; t < T; ++t) used += gt[t];
+    for (; used > G; --used) {           // only when many tiny types were raised to 1
       int big = 0;
       for (int t = 1; t < T; ++t) if (gt[t] > gt[big]) big = t;
       if (gt[big] <= 1) break;
@@ -433,7 +444,8 @@ __global__ __launch_bounds__(256) void rows_linear_kernel(const float* __restric
 // ---------------------------------------------------------------------------------------------
 // Edge embedding (sorted order): e_init = MLP(edge_attr[orig]); Q0 = W1_e_init·e_init + b1.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void edge_embed_kernel(pemp_mlp emb, const float* __restrict__ ea, int A,
+// Widths up to 128 (not the published configuration): weights read from global memory.
+__global__ __launch_bounds__(256) void edge_embed_wide_kernel(pemp_mlp emb, const float* __restrict__ ea, int A,
                                                          const int* __restrict__ s_orig, int64_t E,
                                                          const float* __restrict__ q0_w,
                                                          const float* __restrict__ q0_b, float* __restrict__ e0,
@@ -465,6 +477,125 @@ __global__ __launch_bounds__(256) void edge_embed_kernel(pemp_mlp emb, const flo
     for (int ob = 0; ob < 4; ++ob) {
       st4(e0 + p * D + 16 * ob + 4 * g, e[ob][0], e[ob][1], e[ob][2], e[ob][3]);
       st4(q0 + p * D + 16 * ob + 4 * g, acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]);
+    }
+  }
+}
+
+// LDS row stride for a weight tile with in_pad columns: >= in_pad and = 8 (mod 64) dwords, so the
+// fragment reads (row = lane & 15, 16 B at column 4 * (lane >> 4)) are bank-conflict free.
+__host__ __device__ constexpr int lds_stride(int in_pad) { return (in_pad - 8 + 63) / 64 * 64 + 8; }
+
+// LDS image of the edge embedding: n layers + the Q0 tile, each [out_pad][stride], then biases.
+struct EmbedLayout {
+  int n, w_off[5], stride[5], kb[5], ob[5], b_off[5], relu[5], total;
+};
+
+static EmbedLayout embed_layout(const pemp_mlp& m) {
+  EmbedLayout L{};
+  L.n = m.n_layers;
+  int off = 0;
+  for (int l = 0; l <= L.n; ++l) {
+    const int in = l < L.n ? m.layer[l].in_dim : 64, out = l < L.n ? m.layer[l].out_dim : 64;
+    L.kb[l] = (in + 15) / 16;
+    L.ob[l] = (out + 15) / 16;
+    L.stride[l] = lds_stride(16 * L.kb[l]);
+    L.relu[l] = l < L.n ? m.layer[l].relu : 0;
+    L.w_off[l] = off;
+    off += 16 * L.ob[l] * L.stride[l];
+  }
+  for (int l = 0; l <= L.n; ++l) {
+    L.b_off[l] = off;
+    off += 16 * L.ob[l];
+  }
+  L.total = off;
+  return L;
+}
+
+// One Linear (+ReLU) on fragments, weights and bias in LDS, runtime block counts <= 4.
+__device__ __forceinline__ void layer_lds(const float* __restrict__ W, int ldw, const float* __restrict__ bias, int KB,
+                                          int OB, int relu, const float (&in)[4][4], float (&out)[4][4]) {
+  const int lane = __lane_id(), i = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int ob = 0; ob < 4; ++ob) {
+    if (ob < OB) {
+      const float4 bb = ld4(bias + 16 * ob + 4 * g);
+      f32x4 c = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) {
+        if (mb < KB) {
+          const float4 w = ld4(W + (16 * ob + i) * ldw + 16 * mb + 4 * g);
+          c = mfma4(w.x, in[mb][0], c);
+          c = mfma4(w.y, in[mb][1], c);
+          c = mfma4(w.z, in[mb][2], c);
+          c = mfma4(w.w, in[mb][3], c);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[ob][r] = relu ? fmaxf(c[r], 0.0f) : c[r];
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[ob][r] = 0.0f;
+    }
+  }
+}
+
+// Edge embedding (sorted order): e_init = MLP(edge_attr[orig]); Q0 = W1_e_init·e_init + b1.
+// One 16-wave workgroup per CU, weights staged once in LDS; a wave walks an equal share of the
+// sorted positions in 16-edge tiles.
+__global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp emb, EmbedLayout Lo,
+                                                                     const float* __restrict__ ea, int A,
+                                                                     const int* __restrict__ s_orig, int64_t E,
+                                                                     const float* __restrict__ q0_w,
+                                                                     const float* __restrict__ q0_b,
+                                                                     float* __restrict__ e0, float* __restrict__ q0) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
+  for (int l = 0; l <= Lo.n; ++l) {
+    const float* src = l < Lo.n ? emb.layer[l].w : q0_w;
+    const float* bsrc = l < Lo.n ? emb.layer[l].b : q0_b;
+    const int ip = 16 * Lo.kb[l], rows = 16 * Lo.ob[l], q4 = ip / 4;
+    for (int idx = threadIdx.x; idx < rows * q4; idx += 64 * EDGE_WAVES) {
+      const int row = idx / q4, c4 = (idx - row * q4) * 4;
+      *reinterpret_cast<float4*>(&sm[Lo.w_off[l] + row * Lo.stride[l] + c4]) = ld4(src + row * ip + c4);
+    }
+    for (int idx = threadIdx.x; idx < rows; idx += 64 * EDGE_WAVES) sm[Lo.b_off[l] + idx] = bsrc[idx];
+  }
+  __syncthreads();
+  const int64_t gw = (int64_t)blockIdx.x * EDGE_WAVES + wave, nw = (int64_t)gridDim.x * EDGE_WAVES;
+  const int64_t first = E * gw / nw, end = E * (gw + 1) / nw;
+  for (int64_t base = first; base < end; base += 16) {
+    int z = 0;
+    asm volatile("" : "+s"(z));                  // keep the LDS fragment reads inside the loop
+    const float* smz = sm + z;
+    const int64_t p = base + c;
+    const bool valid = p < end;
+    const int64_t o = s_orig[valid ? p : end - 1];
+    float x[4][4], y[4][4];
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int f = 16 * mb + 4 * g + r;
+        x[mb][r] = f < A ? ea[o * A + f] : 0.0f;
+      }
+    // layers alternate x -> y -> x ...; the result ends in x
+    for (int l = 0; l < Lo.n; ++l) {
+      if ((l & 1) == 0) layer_lds(smz + Lo.w_off[l], Lo.stride[l], smz + Lo.b_off[l], Lo.kb[l], Lo.ob[l], Lo.relu[l], x, y);
+      else layer_lds(smz + Lo.w_off[l], Lo.stride[l], smz + Lo.b_off[l], Lo.kb[l], Lo.ob[l], Lo.relu[l], y, x);
+    }
+    if (Lo.n & 1) {
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[ob][r] = y[ob][r];
+    }
+    layer_lds(smz + Lo.w_off[Lo.n], Lo.stride[Lo.n], smz + Lo.b_off[Lo.n], 4, 4, 0, x, y);
+    if (valid) {
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob) {
+        st4(e0 + p * D + 16 * ob + 4 * g, x[ob][0], x[ob][1], x[ob][2], x[ob][3]);
+        st4(q0 + p * D + 16 * ob + 4 * g, y[ob][0], y[ob][1], y[ob][2], y[ob][3]);
+      }
     }
   }
 }
@@ -549,7 +680,6 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
-constexpr int EDGE_WAVES = 16;   // waves per edge-pass workgroup (one workgroup per CU)
 
 // LDS image of the edge pass (floats): three 64x64 weight tiles, e2_b | attn_w, and for the
 // fused published edge head (HEAD 1) its 64x64 and 32x64 tiles + biases + last row.
@@ -958,8 +1088,16 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
   if (rc) return rc;
   if (E > 0) {
     ProfScope prof("edge_embed", st);
-    hipLaunchKernelGGL(edge_embed_kernel, dim3((unsigned)((E + 63) / 64)), dim3(256), 0, st, w->edge_emb, edge_attr,
-                       desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, ws.EA, ws.Q0);
+    if (mlp_ok(w->edge_emb, 64, 64)) {
+      const EmbedLayout lo = embed_layout(w->edge_emb);
+      const int grid = (int)std::min<int64_t>(num_cus(), (E + 16 * EDGE_WAVES - 1) / (16 * EDGE_WAVES));
+      hipLaunchKernelGGL(edge_embed_kernel, dim3(grid), dim3(64 * EDGE_WAVES), (size_t)lo.total * sizeof(float), st,
+                         w->edge_emb, lo, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, ws.EA,
+                         ws.Q0);
+    } else {
+      hipLaunchKernelGGL(edge_embed_wide_kernel, dim3((unsigned)((E + 63) / 64)), dim3(256), 0, st, w->edge_emb,
+                         edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, ws.EA, ws.Q0);
+    }
     PEMP_LAUNCH_CHECK();
   }
 
