@@ -22,7 +22,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import pemp_amd  # noqa: E402
-from pemp_amd import _lib, config as pcfg, synthetic as syn  # noqa: E402
+from pemp_amd import _lib, config as pcfg, dist as pdist, synthetic as syn  # noqa: E402
 
 METRIC = "images/sec (640px, HRNet-w48) + MPN edge-updates/sec at 1/2/4/8 MI355X"
 WORKLOADS = {
@@ -53,38 +53,12 @@ def parse():
 
 
 def setup_dist(n_gpus):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", rank=rank, world_size=world,
-                                             device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    return rank, world, torch.device("cuda", local if world > 1 else 0)
+    return pdist.init_from_env("nccl")
 
 
-def barrier(world):
-    if world > 1:
-        torch.distributed.barrier()
-
-
-def max_over_ranks(v, world, dev):
-    if world == 1:
-        return v
-    t = torch.tensor([v], dtype=torch.float64, device=dev)
-    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    return float(t.item())
-
-
-def sum_over_ranks(v, world, dev):
-    if world == 1:
-        return v
-    t = torch.tensor([v], dtype=torch.float64, device=dev)
-    torch.distributed.all_reduce(t)
-    return float(t.item())
+barrier = pdist.barrier
+max_over_ranks = pdist.max_over_ranks
+sum_over_ranks = pdist.sum_over_ranks
 
 
 def make_inputs(wl, rank, dev):

@@ -9,11 +9,11 @@
 // Layout (all fp32, hidden width 64). Edges are re-ordered once per call into type-major order
 // (source type t, target i, original edge id) so that every (i, t) aggregation segment is
 // contiguous and every 16-edge MFMA tile shares one message weight W_t. Per iteration:
-//   rows_linear_kernel : node table NT[n] = [W1_xi·x | W1_xj·x | W_t_xi·x + b_t (t < T)], x = [x0 | x]
+//   node_step_kernel   : node table NT[n] = [W1_xi·x | W1_xj·x | W_t_xi·x + b_t (t < T)], x = [x0 | x],
+//                        fused with the node update of the previous pass and the node/class heads
 //   edge_step_kernel   : per 16-edge wave tile, three chained 64x64 MFMA GEMMs (edge MLP layer 1 on
 //                        e_cur, layer 2, message), attention logit, segmented online softmax, and
 //                        (recorded iterations) the fused edge-classification head. No atomics.
-//   node_update_kernel : x_new = ReLU(U·agg + b) (split over types, fixed-order reduction).
 // MFMA: v_mfma_f32_16x16x4_f32 (exact fp32). Fragment convention per wave: item (edge or node)
 // c = lane & 15 on the MFMA N dimension, features 16*blk + 4*(lane >> 4) + r in registers, so one
 // layer's accumulator is the next layer's B operand with no data movement.
@@ -38,10 +38,34 @@ __device__ __forceinline__ void st4(float* p, float a, float b, float c, float d
 }
 
 // acc[ob] += W[16ob + i][.] · in   (W row-major, row stride ldw; KB input / OB output blocks of 16)
+#ifndef PEMP_GEMM_ORDER
+#define PEMP_GEMM_ORDER 0
+#endif
 template <int KB, int OB>
 __device__ __forceinline__ void gemm_frag(const float* __restrict__ W, int ldw, const float (&in)[KB][4],
                                           float (&acc)[OB][4]) {
   const int lane = __lane_id(), i = lane & 15, g = lane >> 4;
+  if (PEMP_GEMM_ORDER == 1) {   // k-outer: OB independent accumulation chains interleaved
+    f32x4 c[OB];
+#pragma unroll
+    for (int ob = 0; ob < OB; ++ob) c[ob] = f32x4{acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]};
+#pragma unroll
+    for (int mb = 0; mb < KB; ++mb) {
+#pragma unroll
+      for (int ob = 0; ob < OB; ++ob) {
+        const float4 w = ld4(W + (16 * ob + i) * ldw + 16 * mb + 4 * g);
+        c[ob] = mfma4(w.x, in[mb][0], c[ob]);
+        c[ob] = mfma4(w.y, in[mb][1], c[ob]);
+        c[ob] = mfma4(w.z, in[mb][2], c[ob]);
+        c[ob] = mfma4(w.w, in[mb][3], c[ob]);
+      }
+    }
+#pragma unroll
+    for (int ob = 0; ob < OB; ++ob) {
+      acc[ob][0] = c[ob][0]; acc[ob][1] = c[ob][1]; acc[ob][2] = c[ob][2]; acc[ob][3] = c[ob][3];
+    }
+    return;
+  }
 #pragma unroll
   for (int ob = 0; ob < OB; ++ob) {
     f32x4 c = {acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]};
@@ -410,37 +434,6 @@ __global__ __launch_bounds__(256) void rows_mlp_kernel(RowsMlpArgs a) {
   }
 }
 
-// Y[M, NO] = X[M, 128] · W^T + b  (node precompute); grid (M/16, NO/64), wave = 16 output columns.
-__global__ __launch_bounds__(256) void rows_linear_kernel(const float* __restrict__ X, int64_t M,
-                                                          const float* __restrict__ W, const float* __restrict__ b,
-                                                          int NO, float* __restrict__ Y) {
-  __shared__ __attribute__((aligned(16))) float xs[16 * RS];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, i = lane & 15, g = lane >> 4;
-  const int64_t row0 = (int64_t)blockIdx.x * 16;
-  for (int idx = threadIdx.x; idx < 16 * 32; idx += 256) {
-    const int r = idx >> 5, k4 = (idx & 31) * 4;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (row0 + r < M) v = ld4(X + (row0 + r) * 128 + k4);
-    *reinterpret_cast<float4*>(&xs[r * RS + k4]) = v;
-  }
-  __syncthreads();
-  const int ob = blockIdx.y * 4 + wave;
-  if (16 * ob >= NO) return;
-  const float4 bb = ld4(b + 16 * ob + 4 * g);
-  f32x4 c = {bb.x, bb.y, bb.z, bb.w};
-#pragma unroll
-  for (int mb = 0; mb < 8; ++mb) {
-    const float4 w = ld4(W + (int64_t)(16 * ob + i) * 128 + 16 * mb + 4 * g);
-    const float4 x = ld4(&xs[i * RS + 16 * mb + 4 * g]);
-    c = mfma4(w.x, x.x, c);
-    c = mfma4(w.y, x.y, c);
-    c = mfma4(w.z, x.z, c);
-    c = mfma4(w.w, x.w, c);
-  }
-  // C layout: lane holds Y[row i][16 ob + 4 g + r]
-  if (row0 + i < M) st4(Y + (row0 + i) * NO + 16 * ob + 4 * g, c[0], c[1], c[2], c[3]);
-}
-
 // ---------------------------------------------------------------------------------------------
 // Edge embedding (sorted order): e_init = MLP(edge_attr[orig]); Q0 = W1_e_init·e_init + b1.
 // ---------------------------------------------------------------------------------------------
@@ -654,15 +647,35 @@ __device__ __forceinline__ Chunks chunks_of(int seg, int c) {
 }
 
 // segmented inclusive scans along the row (Hillis-Steele; step k adds lane c-k when it is in
-// the same chunk)
-template <bool MAX>
-__device__ __forceinline__ float seg_scan(float v, int d) {
-  const float id = MAX ? -INFINITY : 0.0f;
+// the same chunk, i.e. when d >= k)
+template <int CTRL>
+__device__ __forceinline__ float dpp0(float v) {   // lane c -/+ k of the row, 0 outside the row
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+
+struct ScanMask {
+  float m1, m2, m4, m8;   // 1.0f where d >= k
+};
+
+__device__ __forceinline__ ScanMask scan_mask(int d) {
+  return {d >= 1 ? 1.0f : 0.0f, d >= 2 ? 1.0f : 0.0f, d >= 4 ? 1.0f : 0.0f, d >= 8 ? 1.0f : 0.0f};
+}
+
+// sum: one v_fmac_f32 with a DPP source per step
+__device__ __forceinline__ float seg_sum(float v, const ScanMask& m) {
+  v = fmaf(dpp0<DPP_SHR1>(v), m.m1, v);
+  v = fmaf(dpp0<DPP_SHR2>(v), m.m2, v);
+  v = fmaf(dpp0<DPP_SHR4>(v), m.m4, v);
+  v = fmaf(dpp0<DPP_SHR8>(v), m.m8, v);
+  return v;
+}
+
+__device__ __forceinline__ float seg_max(float v, int d) {
   float o;
-  o = dppf<DPP_SHR1>(v, id); v = MAX ? fmaxf(v, d >= 1 ? o : id) : v + (d >= 1 ? o : 0.0f);
-  o = dppf<DPP_SHR2>(v, id); v = MAX ? fmaxf(v, d >= 2 ? o : id) : v + (d >= 2 ? o : 0.0f);
-  o = dppf<DPP_SHR4>(v, id); v = MAX ? fmaxf(v, d >= 4 ? o : id) : v + (d >= 4 ? o : 0.0f);
-  o = dppf<DPP_SHR8>(v, id); v = MAX ? fmaxf(v, d >= 8 ? o : id) : v + (d >= 8 ? o : 0.0f);
+  o = dppf<DPP_SHR1>(v, -INFINITY); v = fmaxf(v, d >= 1 ? o : -INFINITY);
+  o = dppf<DPP_SHR2>(v, -INFINITY); v = fmaxf(v, d >= 2 ? o : -INFINITY);
+  o = dppf<DPP_SHR4>(v, -INFINITY); v = fmaxf(v, d >= 4 ? o : -INFINITY);
+  o = dppf<DPP_SHR8>(v, -INFINITY); v = fmaxf(v, d >= 8 ? o : -INFINITY);
   return v;
 }
 
@@ -820,13 +833,17 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
     gemm_frag<4, 4>(WM, LDW, ep, m);
     relu_frag<4>(m);
 
+#if defined(PEMP_EDGE_DIAG) && PEMP_EDGE_DIAG == 1   // timing experiment only: no aggregation
+    if (valid && g == 0) a.agg[p & 1023] = m[0][0] + av;
+    continue;
+#endif
     // ---- segmented reduction of the tile, carry in / out ----
     const int seg = valid ? dst : -1 - c;        // padding lanes: singleton chunks, never written
     const Chunks ck = chunks_of(seg, c);
     const bool carry_in = have_carry;            // wave-uniform: set only when the segment continues
     float M = 0.f, l = 1.0f, pe = 1.0f;
     if (AGG == PEMP_AGGR_ATTN) {
-      M = seg_bcast_tail_max(seg_scan<true>(av, ck.d), ck.u);
+      M = seg_bcast_tail_max(seg_max(av, ck.d), ck.u);
       if (carry_in && ck.d == c) M = fmaxf(M, cM);   // head chunk continues the carried segment
       pe = expf(av - M);
       l = pe;
@@ -853,11 +870,12 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
             v[ob][r] = (AGG == PEMP_AGGR_MAX) ? fmaxf(v[ob][r], cacc[ob][r]) : v[ob][r] + cacc[ob][r];
       }
     }
-    if (AGG == PEMP_AGGR_ATTN || AGG == PEMP_AGGR_MEAN) l = seg_scan<false>(l, ck.d);   // normaliser / count
+    const ScanMask smk = scan_mask(ck.d);
+    if (AGG == PEMP_AGGR_ATTN || AGG == PEMP_AGGR_MEAN) l = seg_sum(l, smk);   // normaliser / count
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[ob][r] = seg_scan<AGG == PEMP_AGGR_MAX>(v[ob][r], ck.d);
+      for (int r = 0; r < 4; ++r) v[ob][r] = (AGG == PEMP_AGGR_MAX) ? seg_max(v[ob][r], ck.d) : seg_sum(v[ob][r], smk);
     // the chunk at the tile end continues iff the next tile starts with the same target
     const int seg15 = __builtin_amdgcn_readlane(seg, 15);
     const bool carry_out = more && __builtin_amdgcn_readlane(dst_n, 0) == seg15;
@@ -917,48 +935,128 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
   }
 }
 
-// x_new = ReLU(b + sum_t U_t · agg[n, t]) (or agg[n, 0] when there is no update MLP) -> X[:, 64:128]
-__global__ __launch_bounds__(512) void node_update_kernel(const float* __restrict__ agg, const int* __restrict__ seg,
-                                                          int T, int64_t N, const float* __restrict__ upd_w,
-                                                          const float* __restrict__ upd_b, float* __restrict__ X) {
-  __shared__ __attribute__((aligned(16))) float red[8][16 * 68];
+// Node step, 16 nodes per workgroup (NODE_WAVES waves; NODE_SPLIT workgroups share the table
+// columns), fusing what follows an edge pass:
+//   (a) x_new = ReLU(b + sum_t U_t · agg[n, t]) (fixed-order reduction over types; agg[n, 0]
+//       when there is no update MLP; empty segments read as 0)  -> X[:, 64:128]
+//   (b) the next iteration's node table NT = [x0 | x] · pre_w^T + pre_b
+//   (c) the node / class heads on x (published widths <= 64), written to one or two slots
+struct NodeStepArgs {
+  const float* agg;
+  const int* seg;
+  int T, do_update;
+  int64_t N;
+  const float *upd_w, *upd_b;
+  float* X;
+  const float *pre_w, *pre_b;
+  int NO;
+  float* NT;
+  pemp_mlp node_head, class_head;
+  int J;
+  float *node_out, *node_out2, *class_out, *class_out2;
+};
+
+constexpr int NODE_WAVES = 16, NODE_SPLIT = 2;   // waves per node-step workgroup; table column split
+
+__global__ __launch_bounds__(64 * NODE_WAVES) void node_step_kernel(NodeStepArgs a) {
+  __shared__ __attribute__((aligned(16))) float red[NODE_WAVES][16 * 68];
+  __shared__ __attribute__((aligned(16))) float xs[16 * RS];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
-  const int64_t n0 = (int64_t)blockIdx.x * 16;
-  if (!upd_w) {
-    for (int idx = threadIdx.x; idx < 16 * D; idx += 512) {
-      const int r = idx >> 6, f = idx & 63;
-      const int64_t n = n0 + r;
-      if (n < N) X[n * 128 + 64 + f] = seg[n + 1] > seg[n] ? agg[n * D + f] : 0.0f;
-    }
-    return;
+  const int64_t n0 = (int64_t)blockIdx.x * 16, N = a.N;
+  const int T = a.T;
+  const bool owner = blockIdx.y == 0;           // writes X and the heads
+  // x0 half (and x when there is no update)
+  for (int idx = threadIdx.x; idx < 16 * 32; idx += 64 * NODE_WAVES) {
+    const int r = idx >> 5, k4 = (idx & 31) * 4;
+    if (a.do_update && k4 >= 64) continue;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (n0 + r < N) v = ld4(a.X + (n0 + r) * 128 + k4);
+    *reinterpret_cast<float4*>(&xs[r * RS + k4]) = v;
   }
-  const int64_t n = n0 + c;
-  float acc[4][4];
+  if (a.do_update) {
+    if (!a.upd_w) {
+      for (int idx = threadIdx.x; idx < 16 * D; idx += 64 * NODE_WAVES) {
+        const int r = idx >> 6, f = idx & 63;
+        const int64_t n = n0 + r;
+        const float v = (n < N && a.seg[n + 1] > a.seg[n]) ? a.agg[n * D + f] : 0.0f;
+        xs[r * RS + 64 + f] = v;
+        if (n < N && owner) a.X[n * 128 + 64 + f] = v;
+      }
+    } else {
+      const int64_t n = n0 + c;
+      float acc[4][4];
 #pragma unroll
-  for (int ob = 0; ob < 4; ++ob)
+      for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) acc[ob][r] = 0.f;
-  for (int t = wave; t < T; t += 8) {
-    const bool has = n < N && seg[t * N + n + 1] > seg[t * N + n];
-    float in[4][4];
+        for (int r = 0; r < 4; ++r) acc[ob][r] = 0.f;
+      for (int t = wave; t < T; t += NODE_WAVES) {
+        const bool has = n < N && a.seg[t * N + n + 1] > a.seg[t * N + n];
+        float in[4][4];
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+          float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (has) x = ld4(a.agg + (n * T + t) * D + 16 * mb + 4 * g);
+          in[mb][0] = x.x; in[mb][1] = x.y; in[mb][2] = x.z; in[mb][3] = x.w;
+        }
+        gemm_frag<4, 4>(a.upd_w + 64 * t, 64 * T, in, acc);
+      }
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+        st4(&red[wave][c * 68 + 16 * ob + 4 * g], acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]);
+      __syncthreads();
+      for (int idx = threadIdx.x; idx < 16 * D; idx += 64 * NODE_WAVES) {
+        const int r = idx >> 6, f = idx & 63;
+        float sum = 0.f;
+#pragma unroll
+        for (int w = 0; w < NODE_WAVES; ++w) sum += red[w][r * 68 + f];
+        const float v = fmaxf(sum + a.upd_b[f], 0.0f);
+        xs[r * RS + 64 + f] = v;
+        if (n0 + r < N && owner) a.X[(n0 + r) * 128 + 64 + f] = v;
+      }
+    }
+  }
+  __syncthreads();
+  if (a.NT) {   // next node table: lane holds NT[row c][16 ob + 4 g + r]
+    for (int ob = blockIdx.y * NODE_WAVES + wave; 16 * ob < a.NO; ob += NODE_WAVES * NODE_SPLIT) {
+      const float4 bb = ld4(a.pre_b + 16 * ob + 4 * g);
+      f32x4 acc = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb) {
+        const float4 w = ld4(a.pre_w + (int64_t)(16 * ob + c) * 128 + 16 * mb + 4 * g);
+        const float4 x = ld4(&xs[c * RS + 16 * mb + 4 * g]);
+        acc = mfma4(w.x, x.x, acc);
+        acc = mfma4(w.y, x.y, acc);
+        acc = mfma4(w.z, x.z, acc);
+        acc = mfma4(w.w, x.w, acc);
+      }
+      if (n0 + c < N) st4(a.NT + (n0 + c) * a.NO + 16 * ob + 4 * g, acc[0], acc[1], acc[2], acc[3]);
+    }
+  }
+  if (a.node_out && owner && wave < 2) {   // wave 0: node head, wave 1: class head
+    float in[4][4], tmp[4][4];
 #pragma unroll
     for (int mb = 0; mb < 4; ++mb) {
-      float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (has) x = ld4(agg + (n * T + t) * D + 16 * mb + 4 * g);
+      const float4 x = ld4(&xs[c * RS + 64 + 16 * mb + 4 * g]);
       in[mb][0] = x.x; in[mb][1] = x.y; in[mb][2] = x.z; in[mb][3] = x.w;
     }
-    gemm_frag<4, 4>(upd_w + 64 * t, 64 * T, in, acc);
-  }
+    const pemp_mlp& m = wave == 0 ? a.node_head : a.class_head;
+    mlp_frag<4>(m, in, tmp);
+    const int od = wave == 0 ? 1 : a.J;
+    float* o1 = wave == 0 ? a.node_out : a.class_out;
+    float* o2 = wave == 0 ? a.node_out2 : a.class_out2;
+    const int64_t n = n0 + c;
+    if (n < N) {
 #pragma unroll
-  for (int ob = 0; ob < 4; ++ob) st4(&red[wave][c * 68 + 16 * ob + 4 * g], acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]);
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < 16 * D; idx += 512) {
-    const int r = idx >> 6, f = idx & 63;
-    float s = 0.f;
+      for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
-    for (int w = 0; w < 8; ++w) s += red[w][r * 68 + f];
-    const int64_t nn = n0 + r;
-    if (nn < N) X[nn * 128 + 64 + f] = fmaxf(s + upd_b[f], 0.0f);
+        for (int r = 0; r < 4; ++r) {
+          const int f = 16 * ob + 4 * g + r;
+          if (f < od) {
+            o1[n * od + f] = in[ob][r];
+            if (o2) o2[n * od + f] = in[ob][r];
+          }
+        }
+    }
   }
 }
 
@@ -1105,17 +1203,45 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
   const int NO = 128 + 64 * T;
   const int steps = desc->steps, aux = desc->aux_loss_steps;
   const int edge_grid = std::max(num_cus(), T);   // >= wg_start[T] (see mpn_scan_kernel)
+  const bool fused_heads = mlp_ok(w->node_head, 64, 64) && mlp_ok(w->class_head, 64, 64);
+  const unsigned node_grid = (unsigned)((N + 15) / 16);
+  auto node_step = [&](const char* label, bool update, bool table, int slot, bool dup) -> int {
+    NodeStepArgs na{};
+    na.agg = ws.agg; na.seg = ws.seg; na.T = T; na.do_update = update; na.N = N;
+    na.upd_w = w->upd_w; na.upd_b = w->upd_b; na.X = ws.X;
+    na.pre_w = w->pre_w; na.pre_b = w->pre_b; na.NO = NO; na.NT = table ? ws.NT : nullptr;
+    na.node_head = w->node_head; na.class_head = w->class_head; na.J = J;
+    if (slot >= 0 && fused_heads) {
+      na.node_out = node_logits + (int64_t)slot * N;
+      na.class_out = class_logits + (int64_t)slot * N * J;
+      na.node_out2 = dup ? na.node_out + N : nullptr;
+      na.class_out2 = dup ? na.class_out + N * J : nullptr;
+    }
+    {
+      ProfScope prof(label, st);
+      hipLaunchKernelGGL(node_step_kernel, dim3(node_grid, NODE_SPLIT), dim3(64 * NODE_WAVES), 0, st, na);
+      PEMP_LAUNCH_CHECK();
+    }
+    if (slot >= 0 && !fused_heads) {
+      for (int k = 0; k < (dup ? 2 : 1); ++k) {
+        int r2;
+        if ((r2 = rows_mlp("heads", w->node_head, ws.X + 64, 128, N, node_logits + (int64_t)(slot + k) * N, 1, nullptr, 0, st)))
+          return r2;
+        if ((r2 = rows_mlp("heads", w->class_head, ws.X + 64, 128, N, class_logits + (int64_t)(slot + k) * N * J, J,
+                           nullptr, 0, st)))
+          return r2;
+      }
+    }
+    return PEMP_OK;
+  };
+  // node table of the first iteration (or, without iterations, the heads on the embedding)
+  if ((rc = node_step("node_table", false, steps > 0, steps > 0 ? -1 : 0, false))) return rc;
   float* e_cur = ws.EA;
   float* e_nxt = ws.EB;
   int rec = 0;
   for (int it = 0; it < steps; ++it) {
     const bool record = it >= steps - aux - 1;
-    {
-    ProfScope prof("node_table", st);
-    hipLaunchKernelGGL(rows_linear_kernel, dim3((unsigned)((N + 15) / 16), (unsigned)((NO + 63) / 64)), dim3(256), 0,
-                       st, ws.X, N, w->pre_w, w->pre_b, NO, ws.NT);
-    PEMP_LAUNCH_CHECK();
-    }
+    const bool last = it + 1 == steps;
     if (E > 0) {
       EdgeStepArgs ea{};
       ea.N = N; ea.E = E; ea.T = T; ea.t_nt_ld = NO;
@@ -1124,7 +1250,7 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
       ea.e1_w = w->e1_w; ea.e2_w = w->e2_w; ea.e2_b = w->e2_b; ea.msg_w = w->msg_w; ea.attn_w = w->attn_w;
       ea.attn_b = w->attn_b; ea.agg = ws.agg; ea.head = w->edge_head;
       ea.edge_logits = record ? edge_logits + (int64_t)rec * E : nullptr;
-      ea.write_next = it + 1 < steps;
+      ea.write_next = !last;
       ProfScope prof(record ? "edge_step_head" : "edge_step", st);
       switch (desc->aggr) {
         case PEMP_AGGR_ATTN: launch_edge_step<PEMP_AGGR_ATTN>(ea, record, edge_grid, st); break;
@@ -1134,23 +1260,12 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
       }
       PEMP_LAUNCH_CHECK();
     }
-    {
-    ProfScope prof("node_update", st);
-    hipLaunchKernelGGL(node_update_kernel, dim3((unsigned)((N + 15) / 16)), dim3(512), 0, st, ws.agg, ws.seg, T, N,
-                       w->upd_w, w->upd_b, ws.X);
-    PEMP_LAUNCH_CHECK();
-    }
-    if (record) {
-      if ((rc = rows_mlp("heads", w->node_head, ws.X + 64, 128, N, node_logits + (int64_t)rec * N, 1, nullptr, 0, st))) return rc;
-      if ((rc = rows_mlp("heads", w->class_head, ws.X + 64, 128, N, class_logits + (int64_t)rec * N * J, J, nullptr, 0, st)))
-        return rc;
-      ++rec;
-    }
+    // node update + next node table; heads when recorded (the last iteration's heads also fill
+    // the post-loop slot: NODE_STEPS = 0 leaves x unchanged, NodeClassificationMPNSimple.py:93-94)
+    if ((rc = node_step("node_update", true, !last, record ? rec : -1, last))) return rc;
+    if (record) ++rec;
     float* tmp = e_cur; e_cur = e_nxt; e_nxt = tmp;
   }
-  if ((rc = rows_mlp("heads", w->node_head, ws.X + 64, 128, N, node_logits + (int64_t)rec * N, 1, nullptr, 0, st))) return rc;
-  if ((rc = rows_mlp("heads", w->class_head, ws.X + 64, 128, N, class_logits + (int64_t)rec * N * J, J, nullptr, 0, st)))
-    return rc;
   return PEMP_OK;
 }
 
