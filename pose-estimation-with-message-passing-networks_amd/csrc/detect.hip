@@ -4,12 +4,15 @@
 //                                 threshold set; (DETECT_THRESHOLD > 1.5: top-20 + 1e-10)
 //   ConstructGraph.py:1199-1209   cat_unique ordering
 //
-// Stage 1 (nms_tiles_kernel, HBM-bound): one workgroup per 32x128 tile of one (image, type)
-//   plane. Tile + halo staged in LDS, separable max, then per pixel v = s * jm. Emits, per tile:
-//   each wave's k best (v, flat index) candidates (ties -> lower index), the tile's count of
-//   threshold pixels, and the threshold bitmask (row-major, one bit per pixel, 64-px words).
+// Stage 1 (nms_strips_kernel, HBM-bound, no LDS): one WAVE per unit = 16 rows x (64 - 2P)
+//   columns of one (image, type) plane; lane c owns column x0 - P + c (lanes < P and >= 64 - P
+//   are the halo). The lane's column is loaded once (16 + 2P rows, coalesced across lanes, the
+//   next unit's rows already in flight), the vertical max runs in registers, the horizontal max
+//   with DPP whole-wave lane shifts; per-row predicates accumulate as per-lane row bitmasks
+//   (counts are popcounts). Emits per unit: the K best (v, flat index) candidates (ties -> lower
+//   index), threshold / non-negative counts, and the lanes' 16-bit threshold column masks.
 // Stage 2a (plane_top_kernel): one workgroup per plane. Merges the candidates into the exact
-//   per-type top-k and counts threshold detections per 32-row strip.
+//   per-type top-k and counts threshold detections per 16-row band.
 // Stage 2b (emit_kernel): one workgroup per plane. Offsets from the image's per-plane counts;
 //   emits detections in the reference's order.
 #include <math.h>
@@ -19,53 +22,62 @@
 namespace pemp {
 namespace {
 
-constexpr int TR = 32;    // tile rows (= strip height)
-constexpr int TC = 128;   // tile cols (multiple of 64: a tile owns whole bitmask words)
-constexpr int NT1 = 256;  // stage-1 threads: 32 rows x 8 threads x 16 px
-#ifndef NMS_MIN_WAVES
-#define NMS_MIN_WAVES 4
+#ifndef NMS_SR
+#define NMS_SR 16
 #endif
+#ifndef NMS_PREFETCH
+#define NMS_PREFETCH 1
+#endif
+constexpr int SR = NMS_SR;  // rows per unit (= band height of the threshold bitmask)
+static_assert(SR <= 16, "column masks are 16-bit");
 constexpr int MAXR = 4;   // max pool radius (POOL_KERNEL_SIZE <= 9)
 constexpr int MAXJ = 32;
+constexpr int MAXB = 256;   // max bands per plane (H <= 4096)
+constexpr int NT1 = 256;  // stage-1 workgroup: 4 independent waves
+constexpr int INV = 0x7fffffff;
+enum { MODE_POS = 0, MODE_ALL = 1 };
 
 __device__ __forceinline__ bool better(float v1, int i1, float v2, int i2) {
   return v1 > v2 || (v1 == v2 && i1 < i2);
 }
 
+// Unit grid: nb bands of SR rows x nsx strips of sc = 64 - 2p columns per plane; lane c of a
+// unit owns column x = strip * sc - p + c.
 struct DetectGeom {
-  int B, J, H, W, p, K, tiles_x, tiles_y, tiles, WW, S;
+  int B, J, H, W, p, K, sc, nsx, nb, units, S;
 };
 
 static DetectGeom geom(int B, int J, int H, int W, int pool_k, int K) {
   DetectGeom g;
   g.B = B; g.J = J; g.H = H; g.W = W; g.p = pool_k / 2; g.K = K;
-  g.tiles_x = (W + TC - 1) / TC;
-  g.tiles_y = (H + TR - 1) / TR;
-  g.tiles = g.tiles_x * g.tiles_y;
-  g.WW = (W + 63) / 64;
-  g.S = g.tiles_y;
+  g.sc = 64 - 2 * g.p;
+  g.nsx = (W + g.sc - 1) / g.sc;
+  g.nb = (H + SR - 1) / SR;
+  g.units = g.nb * g.nsx;
+  g.S = g.nb;
   return g;
 }
 
 constexpr int KCAP = 32;   // max top-k (pemp_detect checks topk <= 32)
 
 struct DetectWs {
-  float *cand_v, *neg_v; int *cand_i, *neg_i, *tile_count, *tile_nonneg; unsigned long long* bits;
-  // per plane (image, type): sorted top-k list, threshold-set counts per strip and in-plane offsets
+  float *cand_v, *neg_v; int *cand_i, *neg_i, *tile_count, *tile_nonneg;
+  uint16_t* cbits;   // threshold bits per (unit, lane): bit j <-> row y0 + j of the lane's column
+  // per plane (image, type): sorted top-k list, threshold-set counts per band and in-plane offsets
   float* ptop_sc; int *ptop_i, *ptop_bit, *pn_top, *pn_thr, *pstrip, *pstrip_off;
 };
 
 static DetectWs carve(void* base, const DetectGeom& g, size_t* bytes) {
   Carver c(base);
   DetectWs w;
-  size_t ncand = (size_t)g.B * g.J * g.tiles * 4 * g.K;
-  w.cand_v = c.take<float>(ncand);
-  w.cand_i = c.take<int>(ncand);
-  w.neg_v = c.take<float>(ncand);
-  w.neg_i = c.take<int>(ncand);
-  w.tile_count = c.take<int>((size_t)g.B * g.J * g.tiles * 4);
-  w.tile_nonneg = c.take<int>((size_t)g.B * g.J * g.tiles * 4);
-  w.bits = c.take<unsigned long long>((size_t)g.B * g.J * g.H * g.WW);
+  const size_t nu = (size_t)g.B * g.J * g.units;
+  w.cand_v = c.take<float>(nu * g.K);
+  w.cand_i = c.take<int>(nu * g.K);
+  w.neg_v = c.take<float>(nu * g.K);
+  w.neg_i = c.take<int>(nu * g.K);
+  w.tile_count = c.take<int>(nu);
+  w.tile_nonneg = c.take<int>(nu);
+  w.cbits = c.take<uint16_t>(nu * 64);
   const size_t np = (size_t)g.B * g.J;
   w.ptop_sc = c.take<float>(np * KCAP);
   w.ptop_i = c.take<int>(np * KCAP);
@@ -78,23 +90,13 @@ static DetectWs carve(void* base, const DetectGeom& g, size_t* bytes) {
   return w;
 }
 
-// Stage 1 (persistent): a workgroup walks tiles tl = blockIdx.x, +gridDim.x, ...; the next tile's
-// global loads are issued into registers before the current tile is processed. Tile = 32 rows x
-// 128 cols of one plane; LDS holds rows y0-P..y0+31+P, columns x0-4..x0+131 (P <= 4) at a
-// conflict-free row stride. A thread owns 16 consecutive pixels of one row.
-//
-// Candidates (exact, see DESIGN.md §Detection):
-//   MODE_POS (threshold set in use): per tile the top-K of the POSITIVE values. Zero-valued top-k
+// Candidates (exact):
+//   MODE_POS (threshold set in use): per unit the top-K of the POSITIVE values. Zero-valued top-k
 //     entries are never emitted, and negatives can enter a plane's top-k only when the plane has
-//     fewer than K non-negative pixels, so the tile also reports its non-negative count and, when
+//     fewer than K non-negative pixels, so the unit also reports its non-negative count and, when
 //     that count is below K, the top-K of its negative values.
 //   MODE_ALL (DETECT_THRESHOLD > 1.5: every top-k entry is emitted as value + 1e-10): the exact
 //     top-K of all pixels.
-constexpr int HALO = 4;                   // staged columns on each side (>= P)
-constexpr int LQ = (TC + 2 * HALO) / 4;   // 34 float4 quads per staged row
-constexpr int LS = 140;                   // LDS row stride (floats): ds_read_b128 conflict-free here
-constexpr int INV = 0x7fffffff;
-enum { MODE_POS = 0, MODE_ALL = 1 };
 
 template <int CTRL>
 __device__ __forceinline__ void dpp_better(float& v, int& i) {
@@ -121,19 +123,21 @@ __device__ __forceinline__ void wave_best(float& v, int& i) {
   i = bi;
 }
 
-// K rounds: pop the wave's best among the lane's 16 values that pass `keep`; the winner lane
-// removes the value and rescans. Writes out_v/out_i[k] (sentinels once exhausted).
+// K rounds: pop the wave's best among the lane's SR values that pass `keep` (value j has flat index
+// base_id + j * stride, increasing in j); the winner lane removes the value and rescans. Writes
+// out_v/out_i[k] (sentinels once exhausted).
 template <typename Keep>
-__device__ __forceinline__ void wave_topk(float (&v)[16], int base_id, int K, Keep keep, float* out_v, int* out_i) {
+__device__ __forceinline__ void wave_topk(float (&v)[SR], int base_id, int stride, int K, Keep keep, float* out_v,
+                                          int* out_i) {
   const int lane = threadIdx.x & 63;
   float lbv = -INFINITY;
   int lbj = -1;
 #pragma unroll
-  for (int j = 0; j < 16; ++j)
+  for (int j = 0; j < SR; ++j)
     if (keep(v[j]) && (lbj < 0 || v[j] > lbv)) { lbv = v[j]; lbj = j; }
   for (int k = 0; k < K; ++k) {
     float bv = lbj < 0 ? -INFINITY : lbv;
-    int bi = lbj < 0 ? INV : base_id + lbj;
+    int bi = lbj < 0 ? INV : base_id + lbj * stride;
     wave_best(bv, bi);
     if (lane == 0) { out_v[k] = bv; out_i[k] = bi; }
     if (bi == INV) {                               // wave exhausted: fill with sentinels
@@ -141,167 +145,141 @@ __device__ __forceinline__ void wave_topk(float (&v)[16], int base_id, int K, Ke
         if (lane == 0) { out_v[k2] = -INFINITY; out_i[k2] = INV; }
       break;
     }
-    if (lbj >= 0 && bi == base_id + lbj) {        // this lane owned the winner
+    if (lbj >= 0 && bi == base_id + lbj * stride) {   // this lane owned the winner
 #pragma unroll
-      for (int j = 0; j < 16; ++j)
+      for (int j = 0; j < SR; ++j)
         if (j == lbj) v[j] = NAN;                  // removed (fails every keep predicate)
       lbj = -1;
       lbv = -INFINITY;
 #pragma unroll
-      for (int j = 0; j < 16; ++j)
+      for (int j = 0; j < SR; ++j)
         if (keep(v[j]) && (lbj < 0 || v[j] > lbv)) { lbv = v[j]; lbj = j; }
     }
   }
 }
 
-template <int P, bool VEC>
-__device__ __forceinline__ void load_tile(const float* __restrict__ s, const DetectGeom& g, int tl,
-                                          float4 (&q)[((TR + 2 * P) * LQ + NT1 - 1) / NT1]) {
-  constexpr int LH = TR + 2 * P;
-  constexpr int NQ = (LH * LQ + NT1 - 1) / NT1;
-  const int tile = tl % g.tiles, plane_i = tl / g.tiles;
-  const int ty = tile / g.tiles_x, tx = tile - ty * g.tiles_x;
-  const int y0 = ty * TR, x0 = tx * TC, H = g.H, W = g.W;
-  const float* plane = s + (size_t)plane_i * H * W;
+__device__ __forceinline__ void write_sentinels(float* out_v, int* out_i, int K) {
+  const int lane = threadIdx.x & 63;
+  if (lane < K) { out_v[lane] = -INFINITY; out_i[lane] = INV; }
+}
+
+// whole-wave lane shifts (gfx9 DPP wave_shr:1 / wave_shl:1); lanes without a source get 0 —
+// only halo lanes see that, and their outputs are discarded.
+__device__ __forceinline__ float wave_shr1(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float wave_shl1(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xF, 0xF, true));
+}
+
+// rows y0 - P .. y0 + SR - 1 + P of the lane's column; -inf outside the plane (MaxPool padding)
+template <int P>
+__device__ __forceinline__ void load_unit(const float* __restrict__ s, const DetectGeom& g, int u,
+                                          float (&r)[SR + 2 * P]) {
+  const int lane = threadIdx.x & 63;
+  const int plane = u / g.units, rem = u - plane * g.units, band = rem / g.nsx, strip = rem - band * g.nsx;
+  const int y0 = band * SR, x = strip * g.sc - P + lane;
+  const bool xok = x >= 0 && x < g.W;
+  const int xo = min(max(x, 0), g.W - 1);
+  const int* pl = reinterpret_cast<const int*>(s) + (size_t)plane * g.H * g.W;
+  // Loads are unconditional (clamped addresses) and the -inf padding is applied with integer bit
+  // masks: a select would let the compiler sink each load into a divergent branch with its own
+  // vmcnt(0) wait, serialising the 16 + 2P loads of a unit.
+  const int xmask = xok ? -1 : 0;
+  if (y0 - P >= 0 && y0 + SR + P <= g.H) {                    // interior band: one running pointer
+    const int* p = pl + (y0 - P) * g.W + xo;
 #pragma unroll
-  for (int u = 0; u < NQ; ++u) {
-    const int idx = threadIdx.x + u * NT1;
-    const int r = idx / LQ, c4 = idx - r * LQ;
-    const int y = y0 - P + r, x = x0 - HALO + 4 * c4;
-    const bool yok = idx < LH * LQ && y >= 0 && y < H;
-    const float* row = plane + (size_t)min(max(y, 0), H - 1) * W;   // clamped: always a valid address
-    float4 v;
-    if (VEC) {
-      // W % 4 == 0: a quad is entirely inside or entirely outside the row
-      v = *reinterpret_cast<const float4*>(row + min(max(x, 0), W - 4));
-      const bool ok = yok && x >= 0 && x < W;
-      if (!ok) v = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
-    } else {
-      const float a0 = row[min(max(x, 0), W - 1)], a1 = row[min(max(x + 1, 0), W - 1)];
-      const float a2 = row[min(max(x + 2, 0), W - 1)], a3 = row[min(max(x + 3, 0), W - 1)];
-      v.x = (yok && x >= 0 && x < W) ? a0 : -INFINITY;
-      v.y = (yok && x + 1 >= 0 && x + 1 < W) ? a1 : -INFINITY;
-      v.z = (yok && x + 2 >= 0 && x + 2 < W) ? a2 : -INFINITY;
-      v.w = (yok && x + 3 >= 0 && x + 3 < W) ? a3 : -INFINITY;
+    for (int i = 0; i < SR + 2 * P; ++i) {
+      const int bits_v = p[0];
+      p += g.W;
+      r[i] = __int_as_float((bits_v & xmask) | (int)(0xff800000u & ~(unsigned)xmask));
     }
-    q[u] = v;
+  } else {
+#pragma unroll
+    for (int i = 0; i < SR + 2 * P; ++i) {
+      const int y = y0 - P + i;
+      const int off = min(max(y, 0), g.H - 1) * g.W + xo;    // clamped: always a valid address
+      const int m = (y >= 0 && y < g.H) ? xmask : 0;
+      const int bits_v = pl[off];
+      r[i] = __int_as_float((bits_v & m) | (int)(0xff800000u & ~(unsigned)m));
+    }
   }
 }
 
-// Per tile: two block barriers (stage the tile, then each wave works on its own 8-row strip:
-// vertical max, horizontal max, v, threshold bits, top-k). Each wave writes its own candidate
-// list (K entries) and counts: per tile 4 lists.
-template <int P, int MODE, bool VEC, bool MASKED>
-__global__ __launch_bounds__(NT1, NMS_MIN_WAVES) void nms_tiles_kernel(
+template <int P, int MODE, bool MASKED>
+__global__ __launch_bounds__(NT1) void nms_strips_kernel(
     const float* __restrict__ s, const float* __restrict__ masks, DetectGeom g, float thr, int use_thr,
     float* __restrict__ cand_v, int* __restrict__ cand_i, float* __restrict__ neg_v, int* __restrict__ neg_i,
-    int* __restrict__ tile_count, int* __restrict__ tile_nonneg, unsigned long long* __restrict__ bits) {
-  constexpr int LH = TR + 2 * P;
-  constexpr int NQ = (LH * LQ + NT1 - 1) / NT1;
-  __shared__ __attribute__((aligned(16))) float in[LH * LS];
-  __shared__ __attribute__((aligned(16))) float vmax[TR * LS];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int total = g.B * g.J * g.tiles;
+    int* __restrict__ tile_count, int* __restrict__ tile_nonneg, uint16_t* __restrict__ cbits) {
+  const int lane = threadIdx.x & 63;
+  const int total = g.B * g.J * g.units, stride_u = gridDim.x * (NT1 / 64);
   const int H = g.H, W = g.W, K = g.K;
-  int tl = blockIdx.x;
-  float4 q[NQ];
-  if (tl < total) load_tile<P, VEC>(s, g, tl, q);
-  for (; tl < total; tl += gridDim.x) {
-    const int tile = tl % g.tiles, plane_i = tl / g.tiles, b = plane_i / g.J;
-    const int ty = tile / g.tiles_x, tx = tile - ty * g.tiles_x;
-    const int y0 = ty * TR, x0 = tx * TC;
-    __syncthreads();                               // previous tile's readers of `in` are done
+  // the unit index is wave-uniform: keep it (and all address math derived from it) scalar
+  int u = __builtin_amdgcn_readfirstlane(blockIdx.x * (NT1 / 64) + (threadIdx.x >> 6));
+  float r[SR + 2 * P];
+  if (NMS_PREFETCH && u < total) load_unit<P>(s, g, u, r);
+  for (; u < total; u += stride_u) {
+    if (!NMS_PREFETCH) load_unit<P>(s, g, u, r);
+    const int plane = u / g.units, rem = u - plane * g.units, band = rem / g.nsx, strip = rem - band * g.nsx;
+    const int b = plane / g.J;
+    const int y0 = band * SR, x = strip * g.sc - P + lane;
+    const bool lane_ok = lane >= P && lane < 64 - P && x < W;
+    float cur[SR + 2 * P];
 #pragma unroll
-    for (int u = 0; u < NQ; ++u) {
-      const int idx = threadIdx.x + u * NT1;
-      if (idx < LH * LQ) {
-        const int r = idx / LQ, c4 = idx - r * LQ;
-        *reinterpret_cast<float4*>(&in[r * LS + 4 * c4]) = q[u];
+    for (int i = 0; i < SR + 2 * P; ++i) cur[i] = r[i];
+    if (NMS_PREFETCH && u + stride_u < total) load_unit<P>(s, g, u + stride_u, r);   // next unit's rows in flight
+    float vm[SR], c[SR];
+#pragma unroll
+    for (int j = 0; j < SR; ++j) {
+      float m = cur[j];
+#pragma unroll
+      for (int d = 1; d <= 2 * P; ++d) m = fmaxf(m, cur[j + d]);
+      vm[j] = m;
+      c[j] = cur[j + P];
+    }
+    // horizontal: P rounds of a 3-wide max over neighbouring lanes -> window [x - P, x + P]
+#pragma unroll
+    for (int q = 0; q < P; ++q)
+#pragma unroll
+      for (int j = 0; j < SR; ++j) {
+        const float t = fmaxf(vm[j], wave_shr1(vm[j]));
+        vm[j] = fmaxf(t, wave_shl1(vm[j]));
       }
-    }
-    if (tl + (int)gridDim.x < total) load_tile<P, VEC>(s, g, tl + gridDim.x, q);   // prefetch next tile
-    __syncthreads();
-    // vertical max of this wave's rows 8w..8w+7: lane = column quad, sliding window in registers
-    if (lane < LQ) {
-      float4 col[8 + 2 * P];
+    // per lane: threshold bits and non-negative bits over the unit's rows, the largest value
+    float v[SR];
+    unsigned int tbits = 0, nnbits = 0;
+    float vmax_l = -INFINITY;
+    const int rows = min(SR, H - y0);
 #pragma unroll
-      for (int i = 0; i < 8 + 2 * P; ++i) col[i] = *reinterpret_cast<const float4*>(&in[(wave * 8 + i) * LS + 4 * lane]);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        float4 m = col[i];
-#pragma unroll
-        for (int d = 1; d <= 2 * P; ++d) {
-          m.x = fmaxf(m.x, col[i + d].x); m.y = fmaxf(m.y, col[i + d].y);
-          m.z = fmaxf(m.z, col[i + d].z); m.w = fmaxf(m.w, col[i + d].w);
-        }
-        *reinterpret_cast<float4*>(&vmax[(wave * 8 + i) * LS + 4 * lane]) = m;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int r = threadIdx.x >> 3, cb = (threadIdx.x & 7) * 16;
-    const int y = y0 + r;
-    const bool row_ok = y < H;
-    float vm[24], sc[16], mk[MASKED ? 16 : 1];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      const float4 m = *reinterpret_cast<const float4*>(&vmax[r * LS + cb + 4 * k]);
-      vm[4 * k] = m.x; vm[4 * k + 1] = m.y; vm[4 * k + 2] = m.z; vm[4 * k + 3] = m.w;
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float4 o = *reinterpret_cast<const float4*>(&in[(r + P) * LS + cb + HALO + 4 * k]);
-      sc[4 * k] = o.x; sc[4 * k + 1] = o.y; sc[4 * k + 2] = o.z; sc[4 * k + 3] = o.w;
-    }
-    if (MASKED) {
-      const float* mrow = masks + ((size_t)b * H + min(y, H - 1)) * W;
-#pragma unroll
-      for (int j = 0; j < (MASKED ? 16 : 1); ++j) mk[j] = mrow[min(x0 + cb + j, W - 1)];
-    }
-    // v = s * jm (ConstructGraph.py:1162-1165); NaN marks pixels outside the plane
-    float v[16];
-    unsigned int mybits = 0;
-    int nonneg = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      float m = vm[j + HALO - P];
-#pragma unroll
-      for (int d = 1; d <= 2 * P; ++d) m = fmaxf(m, vm[j + HALO - P + d]);
-      float jm = (m == sc[j]) ? 1.0f : 0.0f;
-      if (MASKED) jm = jm * mk[MASKED ? j : 0];
-      const float vj = sc[j] * jm;
-      const bool ok = row_ok && x0 + cb + j < W;
+    for (int j = 0; j < SR; ++j) {
+      float jm = (vm[j] == c[j]) ? 1.0f : 0.0f;
+      if (MASKED) jm = jm * masks[((size_t)b * H + min(y0 + j, H - 1)) * W + min(max(x, 0), W - 1)];
+      const float vj = c[j] * jm;                       // ConstructGraph.py:1162-1165
+      const bool ok = lane_ok && j < rows;
       v[j] = ok ? vj : NAN;
-      mybits |= (unsigned)(ok && use_thr && !(vj < thr) && (vj != 0.0f)) << j;
-      nonneg += ok && vj >= 0.0f;
+      tbits |= (unsigned)(ok && !(vj < thr) && vj != 0.0f) << j;
+      nnbits |= (unsigned)(ok && vj >= 0.0f) << j;
+      vmax_l = fmaxf(vmax_l, v[j]);                     // NaN (invalid) is ignored by fmaxf
     }
-    const int base_id = y * W + x0 + cb;
-    const size_t wl = (size_t)tl * 4 + wave;     // this wave's list
-    if (MODE == MODE_POS)
-      wave_topk(v, base_id, K, [](float x) { return x > 0.0f; }, cand_v + wl * K, cand_i + wl * K);
-    else
-      wave_topk(v, base_id, K, [](float x) { return x == x; }, cand_v + wl * K, cand_i + wl * K);
-
-    // threshold bitmask: 4 consecutive threads x 16 px = one 64-px word
-    unsigned int lo = (threadIdx.x & 3) < 2 ? (mybits << (16 * (threadIdx.x & 1))) : 0u;
-    unsigned int hi = (threadIdx.x & 3) >= 2 ? (mybits << (16 * (threadIdx.x & 1))) : 0u;
-    lo |= __shfl_xor(lo, 1); hi |= __shfl_xor(hi, 1);
-    lo |= __shfl_xor(lo, 2); hi |= __shfl_xor(hi, 2);
-    const int word = x0 / 64 + ((threadIdx.x & 7) >> 2);
-    if ((threadIdx.x & 3) == 0 && row_ok && word < g.WW)
-      bits[((size_t)plane_i * H + y) * g.WW + word] = ((unsigned long long)hi << 32) | lo;
-    int cnt = __popc(mybits);
+    if (!use_thr) tbits = 0;
+    cbits[(size_t)u * 64 + lane] = (uint16_t)tbits;
+    int cnt = __popc(tbits), nonneg = __popc(nnbits);
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
       cnt += __shfl_xor(cnt, off);
       nonneg += __shfl_xor(nonneg, off);
     }
-    if (lane == 0) { tile_count[wl] = cnt; tile_nonneg[wl] = nonneg; }
+    const bool anypos = __ballot(vmax_l > 0.0f) != 0;
+    if (lane == 0) { tile_count[u] = cnt; tile_nonneg[u] = nonneg; }
+    const int base_id = y0 * W + x;
     if (MODE == MODE_POS) {
-      if (nonneg < K)      // degenerate strip: also keep its best negatives (see stage 2)
-        wave_topk(v, base_id, K, [](float x) { return x < 0.0f; }, neg_v + wl * K, neg_i + wl * K);
-      else if (lane < K) { neg_v[wl * K + lane] = -INFINITY; neg_i[wl * K + lane] = INV; }
+      if (anypos) wave_topk(v, base_id, W, K, [](float a) { return a > 0.0f; }, cand_v + (size_t)u * K, cand_i + (size_t)u * K);
+      else write_sentinels(cand_v + (size_t)u * K, cand_i + (size_t)u * K, K);
+      if (nonneg < K)      // degenerate unit: also keep its best negatives (see stage 2)
+        wave_topk(v, base_id, W, K, [](float a) { return a < 0.0f; }, neg_v + (size_t)u * K, neg_i + (size_t)u * K);
+      else write_sentinels(neg_v + (size_t)u * K, neg_i + (size_t)u * K, K);
+    } else {
+      wave_topk(v, base_id, W, K, [](float a) { return a == a; }, cand_v + (size_t)u * K, cand_i + (size_t)u * K);
     }
   }
 }
@@ -382,7 +360,7 @@ __global__ __launch_bounds__(256) void plane_top_kernel(DetectGeom g, float thr,
   __shared__ float top_v[2 * KMAX], top_sc[KMAX];
   __shared__ int top_i[2 * KMAX], top_bit[KMAX], sh[8];
   const int pl = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int K = g.K, W = g.W, S = g.S, nl = g.tiles * 4;
+  const int K = g.K, W = g.W, S = g.S, nl = g.units;
   const size_t pt = (size_t)pl * nl;                  // first wave list of the plane
   int n = block_topk<KMAX>(cand_v + pt * K, cand_i + pt * K, nl * K, K, top_v, top_i, lv, li, &sh[0]);
   if (use_thr) {
@@ -421,31 +399,39 @@ __global__ __launch_bounds__(256) void plane_top_kernel(DetectGeom g, float thr,
   }
   __syncthreads();
   const int m = sh[0];
-  // per-strip threshold counts minus the top-k entries already listed
-  for (int st = threadIdx.x; st < S; st += 256) {
-    int c = 0;
-    if (use_thr) {
-      const int* tc = tile_count + pt + (size_t)st * g.tiles_x * 4;
-      for (int x = 0; x < 4 * g.tiles_x; ++x) c += tc[x];
-      for (int q = 0; q < m; ++q)
-        if (top_bit[q] && top_i[q] / W / TR == st) --c;
+  // per-band threshold counts (all units of the plane in parallel, integer LDS atomics) minus the
+  // top-k entries already listed
+  __shared__ int band_cnt[MAXB];
+  for (int st = threadIdx.x; st < S; st += 256) band_cnt[st] = 0;
+  __syncthreads();
+  if (use_thr) {
+    for (int idx = threadIdx.x; idx < nl; idx += 256) {
+      const int v = tile_count[pt + idx];
+      if (v) atomicAdd(&band_cnt[idx / g.nsx], v);
     }
-    w.pstrip[(size_t)pl * S + st] = c;
   }
   __syncthreads();
-  // in-plane exclusive scan over strips (wave 0, chunks of 64)
+  if (threadIdx.x == 0) {
+    for (int q = 0; q < m; ++q)
+      if (top_bit[q]) band_cnt[top_i[q] / W / SR] -= 1;
+  }
+  __syncthreads();
+  // in-plane exclusive scan over bands (wave 0, chunks of 64)
   if (wave == 0) {
     int carry = 0;
     for (int c0 = 0; c0 < S; c0 += 64) {
       const int st = c0 + lane;
-      const int v = st < S ? w.pstrip[(size_t)pl * S + st] : 0;
+      const int v = st < S ? band_cnt[st] : 0;
       int x = v;
 #pragma unroll
       for (int off = 1; off < 64; off <<= 1) {
         const int o = __shfl_up(x, off);
         if (lane >= off) x += o;
       }
-      if (st < S) w.pstrip_off[(size_t)pl * S + st] = carry + x - v;
+      if (st < S) {
+        w.pstrip[(size_t)pl * S + st] = v;
+        w.pstrip_off[(size_t)pl * S + st] = carry + x - v;
+      }
       carry += __shfl(x, 63);
     }
     if (lane == 0) w.pn_thr[pl] = carry;
@@ -455,7 +441,7 @@ __global__ __launch_bounds__(256) void plane_top_kernel(DetectGeom g, float thr,
 // Stage 2b: one workgroup per plane. The plane's output offsets follow from the per-plane counts
 // of its image: [top-k dets of types 0..J-1] ++ [threshold dets, type-major, strip order].
 __global__ __launch_bounds__(256) void emit_kernel(const float* __restrict__ s, const float* __restrict__ masks,
-                                                   DetectGeom g, const unsigned long long* __restrict__ bits,
+                                                   DetectGeom g, const uint16_t* __restrict__ cbits,
                                                    DetectWs w, int64_t* __restrict__ det,
                                                    float* __restrict__ scores, int* __restrict__ n_det, int cap) {
   __shared__ int top_i[KCAP], top_bit[KCAP], sh[4];
@@ -492,87 +478,92 @@ __global__ __launch_bounds__(256) void emit_kernel(const float* __restrict__ s, 
       sout[pos] = w.ptop_sc[(size_t)pl * KCAP + threadIdx.x];
     }
   }
-  // threshold detections, one wave per non-empty strip
+  // threshold detections, one wave per non-empty band. The band's non-empty units (strips) are
+  // found from their counts; their column masks go to LDS; row words are rebuilt with one ballot
+  // per (row, non-empty strip), visited in (y, x) order; a lane's output slot is the running base
+  // plus the set bits below it (mbcnt).
+  __shared__ uint16_t cm_sh[4][64][64];
+  __shared__ int nz_sh[4][64];
   for (int st = wave; st < S; st += 4) {
     if (w.pstrip[(size_t)pl * S + st] == 0) continue;     // wave-uniform
-    const int ry0 = st * TR, rows = min(TR, H - ry0);
-    const int nw = rows * g.WW;
-    const int chunk = (nw + 63) / 64;
-    const unsigned long long* wsrc = bits + ((size_t)pl * H + ry0) * g.WW;
-    int cnt = 0;
-    for (int k = 0; k < chunk; ++k) {
-      const int wi = lane * chunk + k;
-      if (wi >= nw) break;
-      unsigned long long word = wsrc[wi];
-      if (word) {
-        for (int q = 0; q < ntop; ++q) {
-          if (!top_bit[q]) continue;
-          const int idx = top_i[q], yy = idx / W, xx = idx - yy * W;
-          if ((yy - ry0) * g.WW + xx / 64 == wi) word &= ~(1ull << (xx & 63));
-        }
-      }
-      cnt += __popcll(word);
-    }
-    int pre = cnt;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int o = __shfl_up(pre, off);
-      if (lane >= off) pre += o;
-    }
-    int pos = thr_base + w.pstrip_off[(size_t)pl * S + st] + pre - cnt;
+    const int ry0 = st * SR, rows = min(SR, H - ry0);
+    int pos = thr_base + w.pstrip_off[(size_t)pl * S + st];
     const float* plane = s + (size_t)pl * H * W;
-    for (int k = 0; k < chunk; ++k) {
-      const int wi = lane * chunk + k;
-      if (wi >= nw) break;
-      unsigned long long word = wsrc[wi];
-      if (!word) continue;
-      for (int q = 0; q < ntop; ++q) {
-        if (!top_bit[q]) continue;
-        const int idx = top_i[q], yy = idx / W, xx = idx - yy * W;
-        if ((yy - ry0) * g.WW + xx / 64 == wi) word &= ~(1ull << (xx & 63));
-      }
-      const int yy = ry0 + wi / g.WW, xw = (wi % g.WW) * 64;
-      while (word) {
-        const int bit = __ffsll((long long)word) - 1;
-        word &= word - 1;
-        const int xx = xw + bit;
-        if (pos < cap) {
-          const float sv = plane[(size_t)yy * W + xx];
-          float jm = 1.0f;
-          if (masks) jm = jm * masks[((size_t)b * H + yy) * W + xx];
-          dout[pos * 3 + 0] = xx;
-          dout[pos * 3 + 1] = yy;
-          dout[pos * 3 + 2] = t;
-          sout[pos] = sv * jm;
+    const size_t u0 = ((size_t)pl * g.nb + st) * g.nsx;   // first unit of the band (nsx <= 64)
+    const unsigned long long nzm = __ballot(lane < g.nsx && w.tile_count[u0 + lane] > 0);
+    int nnz = 0;
+    unsigned rows_any = 0;
+    for (unsigned long long m = nzm; m; m &= m - 1) {
+      const int sx = __builtin_ctzll(m);
+      const unsigned cm = cbits[(u0 + sx) * 64 + lane];
+      cm_sh[wave][nnz][lane] = (uint16_t)cm;
+      if (lane == 0) nz_sh[wave][nnz] = sx;
+      unsigned ra = cm;
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) ra |= __shfl_xor(ra, off);
+      rows_any |= ra;
+      ++nnz;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (unsigned rm = rows_any & ((1u << rows) - 1u); rm; rm &= rm - 1) {
+      const int j = __builtin_ctz(rm), yy = ry0 + j;
+      for (int k = 0; k < nnz; ++k) {
+        const int sx = nz_sh[wave][k];
+        unsigned long long word = __ballot((cm_sh[wave][k][lane] >> j) & 1u);
+        if (!word) continue;
+        for (int q = 0; q < ntop; ++q) {               // already listed as a top-k detection
+          if (!top_bit[q]) continue;
+          const int idx = top_i[q], ty = idx / W, tx = idx - ty * W, tsx = tx / g.sc;
+          if (ty == yy && tsx == sx) word &= ~(1ull << (tx - tsx * g.sc + g.p));
         }
-        ++pos;
+        if ((word >> lane) & 1ull) {
+          const int xx = sx * g.sc - g.p + lane;
+          const int o = pos + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(word >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((unsigned)word, 0u));
+          if (o < cap) {
+            const float sv = plane[(size_t)yy * W + xx];
+            float jm = 1.0f;
+            if (masks) jm = jm * masks[((size_t)b * H + yy) * W + xx];
+            dout[o * 3 + 0] = xx;
+            dout[o * 3 + 1] = yy;
+            dout[o * 3 + 2] = t;
+            sout[o] = sv * jm;
+          }
+        }
+        pos += __popcll(word);
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
-template <int P, int MODE, bool VEC>
+template <int P, int MODE>
 static void launch_nms(const float* s, const float* masks, const DetectGeom& g, float thr, int use_thr,
                        const DetectWs& w, hipStream_t st) {
-  const int total = g.B * g.J * g.tiles;
-  const int grid = total < 4 * num_cus() ? total : 4 * num_cus();
+  const int total = g.B * g.J * g.units;
+  const int want = (total + NT1 / 64 - 1) / (NT1 / 64);
+  const int grid = want < 4 * num_cus() ? want : 4 * num_cus();   // 4 waves/SIMD resident (<= 128 VGPRs)
   if (masks)
-    hipLaunchKernelGGL((nms_tiles_kernel<P, MODE, VEC, true>), dim3(grid), dim3(NT1), 0, st, s, masks, g, thr, use_thr,
-                       w.cand_v, w.cand_i, w.neg_v, w.neg_i, w.tile_count, w.tile_nonneg, w.bits);
+    hipLaunchKernelGGL((nms_strips_kernel<P, MODE, true>), dim3(grid), dim3(NT1), 0, st, s, masks, g, thr, use_thr,
+                       w.cand_v, w.cand_i, w.neg_v, w.neg_i, w.tile_count, w.tile_nonneg, w.cbits);
   else
-    hipLaunchKernelGGL((nms_tiles_kernel<P, MODE, VEC, false>), dim3(grid), dim3(NT1), 0, st, s, masks, g, thr,
-                       use_thr, w.cand_v, w.cand_i, w.neg_v, w.neg_i, w.tile_count, w.tile_nonneg, w.bits);
+    hipLaunchKernelGGL((nms_strips_kernel<P, MODE, false>), dim3(grid), dim3(NT1), 0, st, s, masks, g, thr, use_thr,
+                       w.cand_v, w.cand_i, w.neg_v, w.neg_i, w.tile_count, w.tile_nonneg, w.cbits);
 }
 
-template <int MODE, bool VEC>
+template <int MODE>
 static void dispatch_nms(const float* s, const float* masks, const DetectGeom& g, float thr, int use_thr,
                          const DetectWs& w, hipStream_t st) {
   switch (g.p) {
-    case 0: launch_nms<0, MODE, VEC>(s, masks, g, thr, use_thr, w, st); break;
-    case 1: launch_nms<1, MODE, VEC>(s, masks, g, thr, use_thr, w, st); break;
-    case 2: launch_nms<2, MODE, VEC>(s, masks, g, thr, use_thr, w, st); break;
-    case 3: launch_nms<3, MODE, VEC>(s, masks, g, thr, use_thr, w, st); break;
-    default: launch_nms<4, MODE, VEC>(s, masks, g, thr, use_thr, w, st); break;
+    case 0: launch_nms<0, MODE>(s, masks, g, thr, use_thr, w, st); break;
+    case 1: launch_nms<1, MODE>(s, masks, g, thr, use_thr, w, st); break;
+    case 2: launch_nms<2, MODE>(s, masks, g, thr, use_thr, w, st); break;
+    case 3: launch_nms<3, MODE>(s, masks, g, thr, use_thr, w, st); break;
+    default: launch_nms<4, MODE>(s, masks, g, thr, use_thr, w, st); break;
   }
 }
 
@@ -582,15 +573,8 @@ static int launch_detect(const float* s, const float* masks, const DetectGeom& g
                          hipStream_t st) {
   if (stages & PEMP_DETECT_NMS) {
     ProfScope prof("detect_nms", st);
-    const bool vec = (g.W % 4) == 0 && (reinterpret_cast<uintptr_t>(s) % 16) == 0 &&
-                     (!masks || (reinterpret_cast<uintptr_t>(masks) % 16) == 0);
-    if (use_thr) {
-      if (vec) dispatch_nms<MODE_POS, true>(s, masks, g, thr, use_thr, w, st);
-      else dispatch_nms<MODE_POS, false>(s, masks, g, thr, use_thr, w, st);
-    } else {
-      if (vec) dispatch_nms<MODE_ALL, true>(s, masks, g, thr, use_thr, w, st);
-      else dispatch_nms<MODE_ALL, false>(s, masks, g, thr, use_thr, w, st);
-    }
+    if (use_thr) dispatch_nms<MODE_POS>(s, masks, g, thr, use_thr, w, st);
+    else dispatch_nms<MODE_ALL>(s, masks, g, thr, use_thr, w, st);
     PEMP_LAUNCH_CHECK();
   }
   if (stages & PEMP_DETECT_SELECT) {
@@ -601,7 +585,7 @@ static int launch_detect(const float* s, const float* masks, const DetectGeom& g
       PEMP_LAUNCH_CHECK();
     }
     ProfScope prof("detect_emit", st);
-    hipLaunchKernelGGL(emit_kernel, dim3(g.B * g.J), dim3(256), 0, st, s, masks, g, w.bits, w, det, scores,
+    hipLaunchKernelGGL(emit_kernel, dim3(g.B * g.J), dim3(256), 0, st, s, masks, g, w.cbits, w, det, scores,
                        (int*)n_det, cap);
     PEMP_LAUNCH_CHECK();
   }
@@ -617,7 +601,7 @@ extern "C" size_t pemp_detect_workspace_size(int B, int J, int H, int W, int top
   if (B <= 0 || J <= 0 || H <= 0 || W <= 0) return 0;
   const int K = topk < H * W ? topk : H * W;
   size_t bytes = 0;
-  carve(nullptr, geom(B, J, H, W, 1, K), &bytes);
+  carve(nullptr, geom(B, J, H, W, 2 * MAXR + 1, K), &bytes);   // widest halo = most strips (upper bound)
   return bytes;
 }
 
@@ -634,6 +618,8 @@ extern "C" int pemp_detect(const float* scoremaps, const float* masks, int B, in
   PEMP_CHECK_ARG((size_t)H * W < 0x7fffffffull, "pemp_detect: plane too large");
   const int K = topk < H * W ? topk : H * W;
   const DetectGeom g = geom(B, J, H, W, pool_kernel, K);
+  PEMP_CHECK_ARG(g.nsx <= 64, "pemp_detect: W=%d too wide (max %d for pool_kernel %d)", W, 64 * g.sc, pool_kernel);
+  PEMP_CHECK_ARG(g.nb <= MAXB, "pemp_detect: H=%d too tall (max %d)", H, MAXB * SR);
   size_t need = 0;
   carve(nullptr, g, &need);
   if (workspace_bytes < need) {

@@ -1,5 +1,6 @@
 #!/bin/bash
 # usage: tools/pmc_pass.sh <outdir> <kernel-regex> <counter...>   (GPU box; separate run per counter set)
+# honours PEMP_LIB (A/B library variants under build_ab/)
 set -e
 out=$1; shift; rx=$1; shift
 export TMPDIR=/tmp
