@@ -294,15 +294,27 @@ __device__ __forceinline__ int merge_candidates(const float* __restrict__ cv, co
   int li[KMAX];
 #pragma unroll
   for (int k = 0; k < KMAX; ++k) { lv[k] = -INFINITY; li[k] = INV; }
-  for (int c = lane; c < n; c += 64) {
-    float v = cv[c];
-    int i = ci[c];
-    if (i != INV && better(v, i, lv[KMAX - 1], li[KMAX - 1])) {
+  // 4 candidates per lane per round: their loads are in flight together
+  for (int c0 = lane; c0 < n; c0 += 256) {
+    float vq[4];
+    int iq[4];
 #pragma unroll
-      for (int k = 0; k < KMAX; ++k) {
-        if (better(v, i, lv[k], li[k])) {
-          const float s2 = lv[k]; const int i2 = li[k];
-          lv[k] = v; li[k] = i; v = s2; i = i2;
+    for (int r = 0; r < 4; ++r) {
+      const int c = c0 + 64 * r;
+      vq[r] = c < n ? cv[c] : -INFINITY;
+      iq[r] = c < n ? ci[c] : INV;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = vq[r];
+      int i = iq[r];
+      if (i != INV && better(v, i, lv[KMAX - 1], li[KMAX - 1])) {
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+          if (better(v, i, lv[k], li[k])) {
+            const float s2 = lv[k]; const int i2 = li[k];
+            lv[k] = v; li[k] = i; v = s2; i = i2;
+          }
         }
       }
     }

@@ -61,40 +61,55 @@ __global__ __launch_bounds__(256) void fully_graph_kernel(const int64_t* __restr
   }
 }
 
+// 256 edges per step: per-edge values (dx, dy, theta, the two types) go to LDS once, then the
+// block writes the 256 x A output rows as one contiguous, coalesced range.
 __global__ __launch_bounds__(256) void edge_features_kernel(const int64_t* __restrict__ jdet,
                                                             const int64_t* __restrict__ ei, int64_t E, int J,
                                                             float norm, int mode, int A, float* __restrict__ out) {
-  const int64_t total = E * A;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e = idx / A;
-    const int f = (int)(idx - e * A);
-    const int64_t s = ei[e], d = ei[E + e];
-    float v = 0.0f;
-    int oh = -1;   // one-hot column index, or -1
-    switch (mode) {
-      case PEMP_EF_POSITION_CONNECTION:
-        if (f == 0) v = (float)(jdet[d * 3 + 0] - jdet[s * 3 + 0]) / norm;
-        else if (f == 1) v = (float)(jdet[d * 3 + 1] - jdet[s * 3 + 1]) / norm;
-        else oh = f - 2;
-        break;
-      case PEMP_EF_CONNECTION: oh = f; break;
-      case PEMP_EF_NOTHING: v = 0.0f; break;
-      case PEMP_EF_POSITION:
-        v = (float)(jdet[d * 3 + f] - jdet[s * 3 + f]) / norm;
-        break;
-      case PEMP_EF_POSITION_ANGLE_CONNECTION:
-        if (f < 2) v = (float)(jdet[d * 3 + f] - jdet[s * 3 + f]) / norm;
-        else if (f == 2) {
-          const float ax = (float)(jdet[s * 3 + 0] - jdet[d * 3 + 0]);
-          const float ay = (float)(jdet[s * 3 + 1] - jdet[d * 3 + 1]);
-          const float th = fabsf(acosf(ax * (1.0f / sqrtf(ax * ax + ay * ay))));
-          v = isnan(th) ? 0.0f : th;
-        } else oh = f - 3;
-        break;
+  __shared__ float dx_s[256], dy_s[256], th_s[256];
+  __shared__ int ts_s[256], td_s[256];
+  for (int64_t base = (int64_t)blockIdx.x * 256; base < E; base += (int64_t)gridDim.x * 256) {
+    const int64_t e = base + threadIdx.x;
+    if (e < E) {
+      const int64_t s = ei[e], d = ei[E + e];
+      const int64_t sx = jdet[s * 3 + 0], sy = jdet[s * 3 + 1], dx = jdet[d * 3 + 0], dy = jdet[d * 3 + 1];
+      dx_s[threadIdx.x] = (float)(dx - sx) / norm;            // ConstructGraph.py:311-317 (IEEE division)
+      dy_s[threadIdx.x] = (float)(dy - sy) / norm;
+      ts_s[threadIdx.x] = (int)jdet[s * 3 + 2];
+      td_s[threadIdx.x] = (int)jdet[d * 3 + 2];
+      if (mode == PEMP_EF_POSITION_ANGLE_CONNECTION) {
+        const float ax = (float)(sx - dx), ay = (float)(sy - dy);
+        const float th = fabsf(acosf(ax * (1.0f / sqrtf(ax * ax + ay * ay))));
+        th_s[threadIdx.x] = isnan(th) ? 0.0f : th;
+      }
     }
-    if (oh >= 0) v = (jdet[s * 3 + 2] == oh || jdet[d * 3 + 2] == oh) ? 1.0f : 0.0f;
-    out[idx] = v;
+    __syncthreads();
+    const int n = (int)min<int64_t>(256, E - base), total = n * A;
+    float* o = out + base * A;
+    for (int k = threadIdx.x; k < total; k += 256) {
+      const int el = k / A, f = k - el * A;
+      float v = 0.0f;
+      int oh = -1;   // one-hot column index, or -1
+      switch (mode) {
+        case PEMP_EF_POSITION_CONNECTION:
+          if (f == 0) v = dx_s[el];
+          else if (f == 1) v = dy_s[el];
+          else oh = f - 2;
+          break;
+        case PEMP_EF_CONNECTION: oh = f; break;
+        case PEMP_EF_NOTHING: v = 0.0f; break;
+        case PEMP_EF_POSITION: v = f == 0 ? dx_s[el] : dy_s[el]; break;
+        case PEMP_EF_POSITION_ANGLE_CONNECTION:
+          if (f == 0) v = dx_s[el];
+          else if (f == 1) v = dy_s[el];
+          else if (f == 2) v = th_s[el];
+          else oh = f - 3;
+          break;
+      }
+      if (oh >= 0) v = (ts_s[el] == oh || td_s[el] == oh) ? 1.0f : 0.0f;
+      o[k] = v;
+    }
+    __syncthreads();
   }
 }
 
@@ -380,7 +395,7 @@ extern "C" int pemp_edge_features(const int64_t* joint_det, const int64_t* edge_
   }
   if (e_total == 0) return PEMP_OK;
   ProfScope prof("edge_features", as_stream(stream));
-  hipLaunchKernelGGL(edge_features_kernel, dim3(grid_for(e_total * A, 256)), dim3(256), 0, as_stream(stream),
+  hipLaunchKernelGGL(edge_features_kernel, dim3(grid_for(e_total, 256)), dim3(256), 0, as_stream(stream),
                      joint_det, edge_index, e_total, J, norm_factor, mode, A, edge_attr);
   PEMP_LAUNCH_CHECK();
   return PEMP_OK;
