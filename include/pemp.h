@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define PEMP_ABI_VERSION 1
+#define PEMP_ABI_VERSION 2
 
 enum {
   PEMP_OK = 0,
@@ -117,6 +117,13 @@ int pemp_edge_features(const int64_t* joint_det /*[N,3]*/, const int64_t* edge_i
  * ---------------------------------------------------------------------------------------- */
 enum { PEMP_AGGR_ATTN = 0, PEMP_AGGR_SUM = 1, PEMP_AGGR_MEAN = 2, PEMP_AGGR_MAX = 3 };
 
+/* Arithmetic of the per-edge GEMMs (edge MLP, message, edge head); node-side GEMMs are fp32.
+ *   PEMP_PREC_FP32   exact fp32 MFMA (v_mfma_f32_16x16x4_f32)
+ *   PEMP_PREC_BF16X3 x·w ~= xh·wh + xl·wh + xh·wl with bf16 hi/lo parts and fp32 accumulation
+ *                    (v_mfma_f32_16x16x32_bf16): ~2^-16 relative error per product. Needs the
+ *                    *_bf weight packs. */
+enum { PEMP_PREC_FP32 = 0, PEMP_PREC_BF16X3 = 1 };
+
 typedef struct pemp_layer {
   const float* w; /* [out_pad][in_pad] */
   const float* b; /* [out_pad] */
@@ -147,6 +154,12 @@ typedef struct pemp_mpn_weights {
   pemp_mlp class_head; /* 64 -> .. -> J */
   float attn_b;
   int32_t pad_;
+  /* PEMP_PREC_BF16X3 weight packs (bf16 bit patterns): per matrix [hi | lo][out][64] with the input
+   * columns in MFMA slot order: slot 32 kb + 8 g + j holds input 32 kb + 16 (j >> 2) + 4 g + (j & 3). */
+  const uint16_t* e1_bf;   /* [2][64][64]    */
+  const uint16_t* e2_bf;   /* [2][64][64]    */
+  const uint16_t* msg_bf;  /* [T][2][64][64] */
+  const uint16_t* head_bf; /* edge head layers 1, 2 (published 64->64->32->1): [2][64][64] then [2][32][64], or NULL */
 } pemp_mpn_weights;
 
 typedef struct pemp_mpn_desc {
@@ -158,6 +171,8 @@ typedef struct pemp_mpn_desc {
   int32_t hidden;         /* must be 64 */
   int32_t edge_attr_dim;  /* EDGE_INPUT_DIM */
   int32_t node_in_dim;    /* NODE_INPUT_DIM */
+  int32_t precision;      /* PEMP_PREC_* */
+  int32_t pad_;
 } pemp_mpn_desc;
 
 size_t pemp_mpn_workspace_size(const pemp_mpn_desc* desc, int64_t N, int64_t E);

@@ -8,7 +8,7 @@ import os
 
 LIB_PATH = os.environ.get("PEMP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc",
                                                      "libpemp.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 ERR_INVALID_ARG, ERR_HIP, ERR_WORKSPACE, ERR_UNSUPPORTED = -1, -2, -3, -4
 
@@ -28,12 +28,14 @@ class PempMpnWeights(ctypes.Structure):
                 ("pre_w", c_p), ("pre_b", c_p), ("q0_w", c_p), ("q0_b", c_p), ("e1_w", c_p),
                 ("e2_w", c_p), ("e2_b", c_p), ("msg_w", c_p), ("attn_w", c_p), ("upd_w", c_p), ("upd_b", c_p),
                 ("edge_head", PempMlp), ("node_head", PempMlp), ("class_head", PempMlp),
-                ("attn_b", c_f32), ("pad_", c_i32)]
+                ("attn_b", c_f32), ("pad_", c_i32),
+                ("e1_bf", c_p), ("e2_bf", c_p), ("msg_bf", c_p), ("head_bf", c_p)]
 
 
 class PempMpnDesc(ctypes.Structure):
     _fields_ = [("num_types", c_i32), ("num_joints", c_i32), ("steps", c_i32), ("aux_loss_steps", c_i32),
-                ("aggr", c_i32), ("hidden", c_i32), ("edge_attr_dim", c_i32), ("node_in_dim", c_i32)]
+                ("aggr", c_i32), ("hidden", c_i32), ("edge_attr_dim", c_i32), ("node_in_dim", c_i32),
+                ("precision", c_i32), ("pad_", c_i32)]
 
 
 # name -> (restype, argtypes); every symbol of include/pemp.h

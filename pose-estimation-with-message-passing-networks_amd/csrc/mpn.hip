@@ -603,6 +603,7 @@ struct EdgeStepArgs {
   const float *NT, *Q0, *e_cur;
   float* e_next;
   const float *e1_w, *e2_w, *e2_b, *msg_w, *attn_w;
+  const uint16_t *e1_bf, *e2_bf, *msg_bf, *head_bf;   // PREC 1: [hi | lo][out][64] k-permuted bf16
   float attn_b;
   float* agg;
   pemp_mlp head;
@@ -694,6 +695,62 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
 }
 
 
+// ---- bf16x3 split precision (PREC 1): x·w ~= xh·wh + xl·wh + xh·wl with x = xh + xl, w = wh + wl,
+// each part bf16 (RNE) and fp32 accumulation in v_mfma_f32_16x16x32_bf16; the dropped xl·wl term
+// and the rounding of the low parts leave ~2^-16 relative error per product. Fragment mapping:
+// B (activations) lane (g, c) holds, for k-block kb, slots 8g + j = features
+// 32 kb + 16 (j >> 2) + 4 g + (j & 3) — exactly its fp32 accumulator registers x[2 kb + (j >> 2)][j & 3]
+// — so layer outputs feed the next layer unchanged; the host stores the weights with their input
+// columns in the same slot order (mpn/fold.py::bf16_pack).
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split_bf16(const float (&x)[4][4], bf16x8_t (&hi)[2], bf16x8_t (&lo)[2]) {
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float f = x[2 * kb + (j >> 2)][j & 3];
+      const __bf16 h = (__bf16)f;
+      hi[kb][j] = h;
+      lo[kb][j] = (__bf16)(f - (float)h);
+    }
+}
+
+// acc[ob] += W[16 ob + i][.] · x   with W hi / lo parts in LDS ([out][LDW] bf16 each), K = 64
+template <int OB>
+__device__ __forceinline__ void gemm_bf3(const __bf16* __restrict__ Wh, const __bf16* __restrict__ Wl,
+                                         const bf16x8_t (&hi)[2], const bf16x8_t (&lo)[2], float (&acc)[OB][4]) {
+  const int lane = __lane_id(), i = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int ob = 0; ob < OB; ++ob) {
+    f32x4 c = {acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]};
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const int o = (16 * ob + i) * LDW + 32 * kb + 8 * g;
+      const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(Wh + o);
+      const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(Wl + o);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, hi[kb], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, lo[kb], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, hi[kb], c, 0, 0, 0);
+    }
+    acc[ob][0] = c[0]; acc[ob][1] = c[1]; acc[ob][2] = c[2]; acc[ob][3] = c[3];
+  }
+}
+
+// one layer on fragments in the chosen precision; W points at the LDS image of the matrix
+// (PREC 0: fp32 [out][LDW]; PREC 1: bf16 hi [out][LDW] then lo [out][LDW])
+template <int PREC, int OB>
+__device__ __forceinline__ void gemm_p(const void* W, int out_rows, const float (&x)[4][4], float (&acc)[OB][4]) {
+  if (PREC == 0) {
+    gemm_frag<4, OB>(static_cast<const float*>(W), LDW, x, acc);
+  } else {
+    bf16x8_t hi[2], lo[2];
+    split_bf16(x, hi, lo);
+    const __bf16* Wh = static_cast<const __bf16*>(W);
+    gemm_bf3<OB>(Wh, Wh + out_rows * LDW, hi, lo, acc);
+  }
+}
+
 // LDS image of the edge pass (floats): three 64x64 weight tiles, e2_b | attn_w, and for the
 // fused published edge head (HEAD 1) its 64x64 and 32x64 tiles + biases + last row.
 constexpr int LDS_W = 3 * D * LDW;
@@ -707,12 +764,15 @@ constexpr int LDS_HEAD = (D + 32) * LDW + D + 32 + 32;
 // EDGE_WAVES equal wave ranges; every range boundary is moved forward to the next segment
 // start, so each (target, type) segment is reduced by exactly one wave. A wave walks its range
 // in 16-edge tiles; a segment that crosses a tile boundary is carried in registers.
-template <int AGG, int HEAD>
+// PREC: 0 = exact fp32 MFMA (v_mfma_f32_16x16x4_f32), 1 = bf16x3 split precision (see gemm_bf3).
+// The LDS image has the same size in both: a 64 x LDW fp32 tile = its bf16 hi and lo tiles.
+template <int AGG, int HEAD, int PREC>
 __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* wl = sm;                               // [3][64][LDW]: e1_w (e_cur part), e2_w, msg_w[t]
   float* vec = sm + LDS_W;                      // e2_b[64] | attn_w[64]
   float* hw = vec + LDS_VEC;                    // HEAD 1: [64][LDW] L1.w, [32][LDW] L2.w, b1[64], b2[32], w3[32]
+  float* hb_l = hw + (D + 32) * LDW;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
   const int T = a.T;
   const int blk = blockIdx.x;
@@ -720,20 +780,40 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
   int t = 0;
   while (t + 1 < T && a.wg_start[t + 1] <= blk) ++t;
   {
-    const float* srcs[3] = {a.e1_w, a.e2_w, a.msg_w + (int64_t)t * D * D};
-    for (int idx = threadIdx.x; idx < 3 * D * 16; idx += 64 * EDGE_WAVES) {
-      const int mtx = idx / (D * 16), rem = idx - mtx * D * 16, row = rem >> 4, c4 = (rem & 15) * 4;
-      *reinterpret_cast<float4*>(&wl[(mtx * D + row) * LDW + c4]) = ld4(srcs[mtx] + row * D + c4);
+    if (PREC == 0) {
+      const float* srcs[3] = {a.e1_w, a.e2_w, a.msg_w + (int64_t)t * D * D};
+      for (int idx = threadIdx.x; idx < 3 * D * 16; idx += 64 * EDGE_WAVES) {
+        const int mtx = idx / (D * 16), rem = idx - mtx * D * 16, row = rem >> 4, c4 = (rem & 15) * 4;
+        *reinterpret_cast<float4*>(&wl[(mtx * D + row) * LDW + c4]) = ld4(srcs[mtx] + row * D + c4);
+      }
+    } else {
+      // 3 matrices x (hi, lo) x 64 rows of 64 bf16 (8 x 16 B) -> bf16 rows of stride LDW
+      const uint16_t* srcs[3] = {a.e1_bf, a.e2_bf, a.msg_bf + (int64_t)t * 2 * D * D};
+      __bf16* wb = reinterpret_cast<__bf16*>(wl);
+      for (int idx = threadIdx.x; idx < 3 * 2 * D * 8; idx += 64 * EDGE_WAVES) {
+        const int mtx = idx / (2 * D * 8), rem = idx - mtx * 2 * D * 8, row = rem >> 3, c8 = (rem & 7) * 8;
+        *reinterpret_cast<uint4*>(&wb[(mtx * 2 * D + row) * LDW + c8]) =
+            *reinterpret_cast<const uint4*>(srcs[mtx] + row * D + c8);
+      }
     }
     if (threadIdx.x < D) vec[threadIdx.x] = a.e2_b[threadIdx.x];
     else if (threadIdx.x < 2 * D) vec[threadIdx.x] = (AGG == PEMP_AGGR_ATTN) ? a.attn_w[threadIdx.x - D] : 0.0f;
     if (HEAD == 1) {
-      for (int idx = threadIdx.x; idx < (D + 32) * 16; idx += 64 * EDGE_WAVES) {
-        const int row = idx >> 4, c4 = (idx & 15) * 4;
-        const float* src = row < D ? a.head.layer[0].w + row * D : a.head.layer[1].w + (row - D) * D;
-        *reinterpret_cast<float4*>(&hw[row * LDW + c4]) = ld4(src + c4);
+      if (PREC == 0) {
+        for (int idx = threadIdx.x; idx < (D + 32) * 16; idx += 64 * EDGE_WAVES) {
+          const int row = idx >> 4, c4 = (idx & 15) * 4;
+          const float* src = row < D ? a.head.layer[0].w + row * D : a.head.layer[1].w + (row - D) * D;
+          *reinterpret_cast<float4*>(&hw[row * LDW + c4]) = ld4(src + c4);
+        }
+      } else {
+        // head_bf: L1 [hi|lo][64][64], then L2 [hi|lo][32][64] -> same row order in LDS
+        __bf16* hwb = reinterpret_cast<__bf16*>(hw);
+        for (int idx = threadIdx.x; idx < 2 * (D + 32) * 8; idx += 64 * EDGE_WAVES) {
+          const int row = idx >> 3, c8 = (idx & 7) * 8;
+          *reinterpret_cast<uint4*>(&hwb[row * LDW + c8]) = *reinterpret_cast<const uint4*>(a.head_bf + row * D + c8);
+        }
       }
-      float* hb = hw + (D + 32) * LDW;
+      float* hb = hb_l;
       if (threadIdx.x < D) hb[threadIdx.x] = a.head.layer[0].b[threadIdx.x];
       else if (threadIdx.x < D + 32) hb[threadIdx.x] = a.head.layer[1].b[threadIdx.x - D];
       else if (threadIdx.x < D + 64) hb[threadIdx.x] = a.head.layer[2].w[threadIdx.x - D - 32];
@@ -771,7 +851,7 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
     // (192+ VGPRs of loop-invariant loads would spill)
     int z = 0;
     asm volatile("" : "+s"(z));
-    const float* W1 = wl + z;
+    const float* W1 = wl + z;                     // each matrix: 64 x LDW floats (or its hi + lo bf16)
     const float* W2 = wl + z + D * LDW;
     const float* WM = wl + z + 2 * D * LDW;
     const float* hwz = hw + z;
@@ -801,7 +881,7 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
       m[ob][0] = xp.x; m[ob][1] = xp.y; m[ob][2] = xp.z; m[ob][3] = xp.w;
     }
     // edge MLP layer 1: h = ReLU(Q0 + A[dst] + B[src] + W1_e_cur · e_cur)
-    gemm_frag<4, 4>(W1, LDW, ein, h);
+    gemm_p<PREC, 4>(W1, D, ein, h);
     relu_frag<4>(h);
     // layer 2: e' = ReLU(W2 · h + b2)
     float ep[4][4];
@@ -810,7 +890,7 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
       const float4 b2 = ld4(vec + 16 * ob + 4 * g);
       ep[ob][0] = b2.x; ep[ob][1] = b2.y; ep[ob][2] = b2.z; ep[ob][3] = b2.w;
     }
-    gemm_frag<4, 4>(W2, LDW, h, ep);
+    gemm_p<PREC, 4>(W2, D, h, ep);
     relu_frag<4>(ep);
     if (a.write_next && valid) {
 #pragma unroll
@@ -830,13 +910,9 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
       av += a.attn_b;
     }
     // message: m = ReLU(P_t[dst] + W_t_e · e')
-    gemm_frag<4, 4>(WM, LDW, ep, m);
+    gemm_p<PREC, 4>(WM, D, ep, m);
     relu_frag<4>(m);
 
-#if defined(PEMP_EDGE_DIAG) && PEMP_EDGE_DIAG == 1   // timing experiment only: no aggregation
-    if (valid && g == 0) a.agg[p & 1023] = m[0][0] + av;
-    continue;
-#endif
     // ---- segmented reduction of the tile, carry in / out ----
     const int seg = valid ? dst : -1 - c;        // padding lanes: singleton chunks, never written
     const Chunks ck = chunks_of(seg, c);
@@ -901,21 +977,22 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
     }
 
     if (HEAD == 1) {   // fused edge-classification head on e'
-      const float* hb = hwz + (D + 32) * LDW;
+      const float* hb = hb_l + z;
       float h1[4][4], h2[2][4];
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob) {
         const float4 bb = ld4(hb + 16 * ob + 4 * g);
         h1[ob][0] = bb.x; h1[ob][1] = bb.y; h1[ob][2] = bb.z; h1[ob][3] = bb.w;
       }
-      gemm_frag<4, 4>(hwz, LDW, ep, h1);
+      gemm_p<PREC, 4>(hwz, D, ep, h1);
       relu_frag<4>(h1);
 #pragma unroll
       for (int ob = 0; ob < 2; ++ob) {
         const float4 bb = ld4(hb + D + 16 * ob + 4 * g);
         h2[ob][0] = bb.x; h2[ob][1] = bb.y; h2[ob][2] = bb.z; h2[ob][3] = bb.w;
       }
-      gemm_frag<4, 2>(hwz + D * LDW, LDW, h1, h2);
+      gemm_p<PREC, 2>(PREC == 0 ? (const void*)(hwz + D * LDW) : (const void*)(reinterpret_cast<const __bf16*>(hwz) + 2 * D * LDW),
+                      32, h1, h2);
       relu_frag<2>(h2);
       float lg = 0.f;
 #pragma unroll
@@ -956,7 +1033,13 @@ struct NodeStepArgs {
   float *node_out, *node_out2, *class_out, *class_out2;
 };
 
-constexpr int NODE_WAVES = 16, NODE_SPLIT = 2;   // waves per node-step workgroup; table column split
+#ifndef PEMP_NODE_WAVES
+#define PEMP_NODE_WAVES 16
+#endif
+#ifndef PEMP_NODE_SPLIT
+#define PEMP_NODE_SPLIT 2
+#endif
+constexpr int NODE_WAVES = PEMP_NODE_WAVES, NODE_SPLIT = PEMP_NODE_SPLIT;   // waves per node-step WG; table split
 
 __global__ __launch_bounds__(64 * NODE_WAVES) void node_step_kernel(NodeStepArgs a) {
   __shared__ __attribute__((aligned(16))) float red[NODE_WAVES][16 * 68];
@@ -1071,16 +1154,22 @@ static bool published_head(const pemp_mlp& m) {
          m.layer[2].out_dim == 1 && !m.layer[2].relu;
 }
 
-template <int AGG>
-static void launch_edge_step(const EdgeStepArgs& a, bool head, int grid, hipStream_t st) {
+template <int AGG, int PREC>
+static void launch_edge_step_p(const EdgeStepArgs& a, bool head, int grid, hipStream_t st) {
   const size_t lds = (size_t)(LDS_W + LDS_VEC) * sizeof(float);
   const dim3 blk(64 * EDGE_WAVES);
   if (!head)
-    hipLaunchKernelGGL((edge_step_kernel<AGG, 0>), dim3(grid), blk, lds, st, a);
-  else if (published_head(a.head))
-    hipLaunchKernelGGL((edge_step_kernel<AGG, 1>), dim3(grid), blk, lds + LDS_HEAD * sizeof(float), st, a);
+    hipLaunchKernelGGL((edge_step_kernel<AGG, 0, PREC>), dim3(grid), blk, lds, st, a);
+  else if (published_head(a.head) && (PREC == 0 || a.head_bf))
+    hipLaunchKernelGGL((edge_step_kernel<AGG, 1, PREC>), dim3(grid), blk, lds + LDS_HEAD * sizeof(float), st, a);
   else
-    hipLaunchKernelGGL((edge_step_kernel<AGG, 2>), dim3(grid), blk, lds, st, a);
+    hipLaunchKernelGGL((edge_step_kernel<AGG, 2, PREC>), dim3(grid), blk, lds, st, a);
+}
+
+template <int AGG>
+static void launch_edge_step(const EdgeStepArgs& a, bool head, int grid, int prec, hipStream_t st) {
+  if (prec == PEMP_PREC_BF16X3) launch_edge_step_p<AGG, 1>(a, head, grid, st);
+  else launch_edge_step_p<AGG, 0>(a, head, grid, st);
 }
 
 static int rows_mlp(const char* label, const pemp_mlp& m, const float* in, int64_t ld_in, int64_t M, float* out,
@@ -1143,6 +1232,10 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
                  "pemp_mpn_forward: node/class heads must start at 64 and end at 1 / num_joints");
   PEMP_CHECK_ARG(w->pre_w && w->pre_b && w->q0_w && w->q0_b && w->e1_w && w->e2_w && w->e2_b && w->msg_w,
                  "pemp_mpn_forward: null layer weights");
+  PEMP_CHECK_ARG(desc->precision == PEMP_PREC_FP32 || desc->precision == PEMP_PREC_BF16X3,
+                 "pemp_mpn_forward: unknown precision %d", desc->precision);
+  PEMP_CHECK_ARG(desc->precision != PEMP_PREC_BF16X3 || (w->e1_bf && w->e2_bf && w->msg_bf),
+                 "pemp_mpn_forward: PEMP_PREC_BF16X3 needs the e1_bf / e2_bf / msg_bf weight packs");
   PEMP_CHECK_ARG(N == 0 || (x && node_logits && class_logits && node_types), "pemp_mpn_forward: null node tensors");
   PEMP_CHECK_ARG(E == 0 || (edge_attr && edge_index && edge_logits), "pemp_mpn_forward: null edge tensors");
   size_t need = 0;
@@ -1249,14 +1342,15 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
       ea.NT = ws.NT; ea.Q0 = ws.Q0; ea.e_cur = e_cur; ea.e_next = e_nxt;
       ea.e1_w = w->e1_w; ea.e2_w = w->e2_w; ea.e2_b = w->e2_b; ea.msg_w = w->msg_w; ea.attn_w = w->attn_w;
       ea.attn_b = w->attn_b; ea.agg = ws.agg; ea.head = w->edge_head;
+      ea.e1_bf = w->e1_bf; ea.e2_bf = w->e2_bf; ea.msg_bf = w->msg_bf; ea.head_bf = w->head_bf;
       ea.edge_logits = record ? edge_logits + (int64_t)rec * E : nullptr;
       ea.write_next = !last;
       ProfScope prof(record ? "edge_step_head" : "edge_step", st);
       switch (desc->aggr) {
-        case PEMP_AGGR_ATTN: launch_edge_step<PEMP_AGGR_ATTN>(ea, record, edge_grid, st); break;
-        case PEMP_AGGR_SUM: launch_edge_step<PEMP_AGGR_SUM>(ea, record, edge_grid, st); break;
-        case PEMP_AGGR_MEAN: launch_edge_step<PEMP_AGGR_MEAN>(ea, record, edge_grid, st); break;
-        default: launch_edge_step<PEMP_AGGR_MAX>(ea, record, edge_grid, st); break;
+        case PEMP_AGGR_ATTN: launch_edge_step<PEMP_AGGR_ATTN>(ea, record, edge_grid, desc->precision, st); break;
+        case PEMP_AGGR_SUM: launch_edge_step<PEMP_AGGR_SUM>(ea, record, edge_grid, desc->precision, st); break;
+        case PEMP_AGGR_MEAN: launch_edge_step<PEMP_AGGR_MEAN>(ea, record, edge_grid, desc->precision, st); break;
+        default: launch_edge_step<PEMP_AGGR_MAX>(ea, record, edge_grid, desc->precision, st); break;
       }
       PEMP_LAUNCH_CHECK();
     }

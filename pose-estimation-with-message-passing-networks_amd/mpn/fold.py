@@ -66,6 +66,26 @@ def _padded(W, b, in_pad=None):
     return Wp, bp
 
 
+def bf16_slot_perm():
+    """Input column of each MFMA k-slot (v_mfma_f32_16x16x32_bf16 fragments, csrc/mpn.hip gemm_bf3):
+    slot 32 kb + 8 g + j <- input 32 kb + 16 (j >> 2) + 4 g + (j & 3)."""
+    perm = []
+    for kb in range(2):
+        for g in range(4):
+            for j in range(8):
+                perm.append(32 * kb + 16 * (j >> 2) + 4 * g + (j & 3))
+    return torch.tensor(perm)
+
+
+def bf16_pack(W):
+    """[out, 64] weights -> [2, out, 64] bf16 bit patterns (hi, lo), columns in slot order. The split
+    starts from the fp32 value the fp32 path uses: hi = bf16(w), lo = bf16(w - hi) (RNE)."""
+    w = W.to(torch.float32)[:, bf16_slot_perm()]
+    hi = w.to(torch.bfloat16)
+    lo = (w - hi.to(torch.float32)).to(torch.bfloat16)
+    return torch.stack([hi, lo], 0).contiguous().view(torch.int16)
+
+
 class Folded:
     """Device copies + the ctypes struct pointing at them (kept alive together)."""
 
@@ -75,6 +95,11 @@ class Folded:
 
     def dev(self, t, device):
         d = t.to(torch.float32).contiguous().to(device)
+        self.tensors.append(d)
+        return d
+
+    def dev_raw(self, t, device):
+        d = t.contiguous().to(device)
         self.tensors.append(d)
         return d
 
@@ -135,6 +160,16 @@ def fold_weights(model, device) -> Folded:
     s.e2_w = f.dev(layer.mlp_edge[2].weight.detach().double().cpu(), device).data_ptr()
     s.e2_b = f.dev(layer.mlp_edge[2].bias.detach().double().cpu(), device).data_ptr()
     s.msg_w = f.dev(torch.stack(msg_w, 0), device).data_ptr()
+    # bf16x3 packs of the per-edge GEMMs (PEMP_PREC_BF16X3)
+    e2 = layer.mlp_edge[2].weight.detach().double().cpu()
+    s.e1_bf = f.dev_raw(bf16_pack(e1), device).data_ptr()
+    s.e2_bf = f.dev_raw(bf16_pack(e2), device).data_ptr()
+    s.msg_bf = f.dev_raw(torch.stack([bf16_pack(w) for w in msg_w], 0), device).data_ptr()
+    head = mlp_layers(model.edge_classification)
+    if (len(head) == 3 and head[0][0].shape == (64, 64) and head[1][0].shape == (32, 64)
+            and head[0][2] and head[1][2] and not head[2][2] and head[2][0].shape[0] == 1):
+        s.head_bf = f.dev_raw(torch.cat([bf16_pack(head[0][0]).reshape(-1), bf16_pack(head[1][0]).reshape(-1)]),
+                              device).data_ptr()
     attn = getattr(layer, "attn_net", None)
     if attn is not None:
         s.attn_w = f.dev(attn[0].weight.detach().double().cpu().reshape(64), device).data_ptr()

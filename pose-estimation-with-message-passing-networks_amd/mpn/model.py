@@ -17,6 +17,19 @@ from .. import _lib
 from .fold import fold_weights
 
 AGGR_CODES = {"attn": 0, "add": 1, "sum": 1, "mean": 2, "max": 3}
+PRECISIONS = {"fp32": 0, "bf16x3": 1}
+
+
+def default_precision(aggr_code):
+    """Arithmetic of the per-edge GEMMs. ``PEMP_PRECISION`` (fp32 | bf16x3) overrides; otherwise the
+    attention variant (published model, bounded softmax-weighted messages) uses bf16x3 split
+    precision and the sum/mean/max variants exact fp32 (unnormalised sums grow with the in-degree)."""
+    env = os.environ.get("PEMP_PRECISION", "")
+    if env:
+        if env not in PRECISIONS:
+            raise ValueError(f"PEMP_PRECISION={env!r}: expected one of {sorted(PRECISIONS)}")
+        return env
+    return "bf16x3" if aggr_code == AGGR_CODES["attn"] else "fp32"
 TYPE_LUTS = {"left_right": [0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8],
              "per_body_part": [0, 0, 0, 0, 0, 1, 1, 2, 3, 2, 3, 4, 5, 4, 5, 4, 5]}
 
@@ -134,6 +147,7 @@ class NodeClassificationMPNSimple(nn.Module):
         if aggr not in AGGR_CODES:
             raise NotImplementedError(f"AGGR={aggr}")
         self.aggr_code = AGGR_CODES[aggr]
+        self.precision = default_precision(self.aggr_code)   # "fp32" | "bf16x3", settable
         self._folded = None
         self._folded_key = None
         self._tensors = None
@@ -180,8 +194,11 @@ class NodeClassificationMPNSimple(nn.Module):
         fw = self._weights(dev)
         steps, aux = self.edge_steps, self.aux_loss_steps
         n_rec = sum(1 for i in range(steps) if i >= steps - aux - 1)
+        if self.precision not in PRECISIONS:
+            raise ValueError(f"precision={self.precision!r}: expected one of {sorted(PRECISIONS)}")
         desc = _lib.PempMpnDesc(self.num_types, self.num_joints, steps, aux, self.aggr_code, 64,
-                                edge_attr.shape[1] if edge_attr.dim() == 2 else 1, x.shape[1])
+                                edge_attr.shape[1] if edge_attr.dim() == 2 else 1, x.shape[1],
+                                PRECISIONS[self.precision], 0)
         edge_logits = torch.empty(max(n_rec, 1), E, dtype=torch.float32, device=dev)
         node_logits = torch.empty(n_rec + 1, N, dtype=torch.float32, device=dev)
         class_logits = torch.empty(n_rec + 1, N, self.num_joints, dtype=torch.float32, device=dev)

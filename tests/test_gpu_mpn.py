@@ -18,11 +18,17 @@ TOL = 1e-4          # north_star: logits within 1e-4 (fp32)
 REL_SUM = 2e-6
 
 
-def make_model(cfg, salt):
+def make_model(cfg, salt, precision=None):
     m = pemp_amd.get_mpn_model(cfg)
     sd = syn.closed_form_state_dict(m, salt)
     m.load_state_dict(sd)
+    if precision:
+        m.precision = precision
     return m.eval().to(DEV), sd
+
+
+# per-edge GEMM arithmetic: exact fp32 MFMA and bf16x3 split precision (the attention default)
+PRECS = ["fp32", "bf16x3"]
 
 
 def run(model, x, ea, ei, types):
@@ -39,11 +45,14 @@ def max_err(a, b, rel=0.0):
     return ((a.detach().cpu().float() - b).abs() - rel * b.abs()).max().item()
 
 
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("name", gu.names("mpn_"))
-def test_golden(name):
+def test_golden(name, prec):
     meta, a = gu.load(name)
     cfg = gu.mpn_config(meta)
-    model, _ = make_model(cfg, meta["salt"])
+    if prec == "bf16x3" and "attn" not in name:
+        pytest.skip("bf16x3 is offered for the attention variant")
+    model, _ = make_model(cfg, meta["salt"], prec)
     pe, pn, pc, tag = run(model, *(torch.from_numpy(a[k]) for k in ("x", "edge_attr", "edge_index", "node_types")))
     assert tag == [None]
     assert len(pe) == int(a["n_edge_preds"]) and len(pn) == int(a["n_node_preds"]) and len(pc) == len(pn)
@@ -71,13 +80,16 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("case", CASES, ids=[f"J{c[0]}-B{c[1]}-{c[5]}-T{c[6]}-{c[8]}" for c in CASES])
-def test_vs_oracle(case):
+def test_vs_oracle(case, prec):
     J, B, H, W, persons, variant, steps, aux, gtype = case
+    if prec == "bf16x3" and variant != "attn":
+        pytest.skip("bf16x3 is offered for the attention variant")
     g = graph(B, J, H, W, persons, gtype)
     cfg = pcfg.published_mpn_config(J, steps, variant)
     cfg.AUX_LOSS_STEPS = aux
-    model, sd = make_model(cfg, 0.125 * steps + J)
+    model, sd = make_model(cfg, 0.125 * steps + J, prec)
     x, ea, ei, types = g[0], g[1], g[2], g[7][:, 2]
     pe, pn, pc, _ = run(model, x, ea, ei, types)
     rpe, rpn, rpc, _ = restate.mpn_forward(sd, cfg, x, ea, ei, types)
@@ -88,7 +100,8 @@ def test_vs_oracle(case):
         assert max_err(a, b, rel) < TOL
 
 
-def test_permuted_edges_and_isolated_nodes():
+@pytest.mark.parametrize("prec", PRECS)
+def test_permuted_edges_and_isolated_nodes(prec):
     """Edge order is free (the kernels sort by (source type, target)); nodes with no incoming
     edges of a type aggregate to 0 (torch_scatter empty segment)."""
     J = 17
@@ -99,7 +112,7 @@ def test_permuted_edges_and_isolated_nodes():
     perm = torch.from_numpy(np.random.default_rng(0).permutation(ei.shape[1]))
     ei, ea = ei[:, perm], ea[perm]
     cfg = pcfg.published_mpn_config(J, 3, "attn")
-    model, sd = make_model(cfg, 3.0)
+    model, sd = make_model(cfg, 3.0, prec)
     pe, pn, pc, _ = run(model, x, ea, ei, types)
     rpe, rpn, rpc, _ = restate.mpn_forward(sd, cfg, x, ea, ei, types)
     for a, b in zip(pe + pn + pc, rpe + rpn + rpc):
