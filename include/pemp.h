@@ -160,6 +160,8 @@ typedef struct pemp_mpn_weights {
   const uint16_t* e2_bf;   /* [2][64][64]    */
   const uint16_t* msg_bf;  /* [T][2][64][64] */
   const uint16_t* head_bf; /* edge head layers 1, 2 (published 64->64->32->1): [2][64][64] then [2][32][64], or NULL */
+  const uint16_t* emb_bf;  /* edge embedding layers then the e_init block of mlp_edge.0 (q0): per layer
+                              [2][out_pad16][in_pad32], concatenated; or NULL (embedding stays fp32) */
 } pemp_mpn_weights;
 
 typedef struct pemp_mpn_desc {

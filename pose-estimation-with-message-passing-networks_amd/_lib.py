@@ -29,7 +29,7 @@ class PempMpnWeights(ctypes.Structure):
                 ("e2_w", c_p), ("e2_b", c_p), ("msg_w", c_p), ("attn_w", c_p), ("upd_w", c_p), ("upd_b", c_p),
                 ("edge_head", PempMlp), ("node_head", PempMlp), ("class_head", PempMlp),
                 ("attn_b", c_f32), ("pad_", c_i32),
-                ("e1_bf", c_p), ("e2_bf", c_p), ("msg_bf", c_p), ("head_bf", c_p)]
+                ("e1_bf", c_p), ("e2_bf", c_p), ("msg_bf", c_p), ("head_bf", c_p), ("emb_bf", c_p)]
 
 
 class PempMpnDesc(ctypes.Structure):

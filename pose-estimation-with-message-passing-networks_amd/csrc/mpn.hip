@@ -474,27 +474,103 @@ __global__ __launch_bounds__(256) void edge_embed_wide_kernel(pemp_mlp emb, cons
   }
 }
 
+// ---- bf16x3 split precision (PREC 1): x·w ~= xh·wh + xl·wh + xh·wl with x = xh + xl, w = wh + wl,
+// each part bf16 (RNE) and fp32 accumulation in v_mfma_f32_16x16x32_bf16; the dropped xl·wl term
+// and the rounding of the low parts leave ~2^-16 relative error per product. Fragment mapping:
+// B (activations) lane (g, c) holds, for k-block kb, slots 8g + j = features
+// 32 kb + 16 (j >> 2) + 4 g + (j & 3) — exactly its fp32 accumulator registers x[2 kb + (j >> 2)][j & 3]
+// — so layer outputs feed the next layer unchanged; the host stores the weights with their input
+// columns in the same slot order (mpn/fold.py::bf16_pack).
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split_bf16(const float (&x)[4][4], bf16x8_t (&hi)[2], bf16x8_t (&lo)[2]) {
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float f = x[2 * kb + (j >> 2)][j & 3];
+      const __bf16 h = (__bf16)f;
+      hi[kb][j] = h;
+      lo[kb][j] = (__bf16)(f - (float)h);
+    }
+}
+
+// acc[ob] += W[16 ob + i][.] · x   with W hi / lo parts in LDS ([out][LDW] bf16 each), K = 64
+template <int OB>
+__device__ __forceinline__ void gemm_bf3(const __bf16* __restrict__ Wh, const __bf16* __restrict__ Wl,
+                                         const bf16x8_t (&hi)[2], const bf16x8_t (&lo)[2], float (&acc)[OB][4]) {
+  const int lane = __lane_id(), i = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int ob = 0; ob < OB; ++ob) {
+    f32x4 c = {acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]};
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const int o = (16 * ob + i) * LDW + 32 * kb + 8 * g;
+      const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(Wh + o);
+      const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(Wl + o);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, hi[kb], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, lo[kb], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, hi[kb], c, 0, 0, 0);
+    }
+    acc[ob][0] = c[0]; acc[ob][1] = c[1]; acc[ob][2] = c[2]; acc[ob][3] = c[3];
+  }
+}
+
+// one layer on fragments in the chosen precision; W points at the LDS image of the matrix
+// (PREC 0: fp32 [out][LDW]; PREC 1: bf16 hi [out][LDW] then lo [out][LDW])
+template <int PREC, int OB>
+__device__ __forceinline__ void gemm_p(const void* W, int out_rows, const float (&x)[4][4], float (&acc)[OB][4]) {
+  if (PREC == 0) {
+    gemm_frag<4, OB>(static_cast<const float*>(W), LDW, x, acc);
+  } else {
+    bf16x8_t hi[2], lo[2];
+    split_bf16(x, hi, lo);
+    const __bf16* Wh = static_cast<const __bf16*>(W);
+    gemm_bf3<OB>(Wh, Wh + out_rows * LDW, hi, lo, acc);
+  }
+}
+
 // LDS row stride for a weight tile with in_pad columns: >= in_pad and = 8 (mod 64) dwords, so the
 // fragment reads (row = lane & 15, 16 B at column 4 * (lane >> 4)) are bank-conflict free.
 __host__ __device__ constexpr int lds_stride(int in_pad) { return (in_pad - 8 + 63) / 64 * 64 + 8; }
 
-// LDS image of the edge embedding: n layers + the Q0 tile, each [out_pad][stride], then biases.
+// LDS image of the edge embedding: n layers + the Q0 tile, then biases (floats).
+//   PREC 0: each layer [out_pad][stride] fp32, in_pad = 16 kb
+//   PREC 1: each layer bf16 hi [out_pad][stride] then lo [out_pad][stride], in_pad = 32 kb; the
+//           global pack (pemp_mpn_weights.emb_bf) is [2][out_pad][in_pad] per layer, concatenated.
 struct EmbedLayout {
-  int n, w_off[5], stride[5], kb[5], ob[5], b_off[5], relu[5], total;
+  int n, prec, w_off[5], stride[5], kb[5], ob[5], b_off[5], relu[5], g_off[5], total;
 };
 
-static EmbedLayout embed_layout(const pemp_mlp& m) {
+// bf16 row stride (elements) for in_pad columns: 4 * odd dwords, so 16 rows x 16 B reads hit
+// 16 distinct bank groups
+static int lds_stride_bf(int in_pad) {
+  int dw = (in_pad / 2 + 3) / 4 * 4;
+  if ((dw / 4) % 2 == 0) dw += 4;
+  return 2 * dw;
+}
+
+static EmbedLayout embed_layout(const pemp_mlp& m, int prec) {
   EmbedLayout L{};
   L.n = m.n_layers;
-  int off = 0;
+  L.prec = prec;
+  int off = 0, goff = 0;
   for (int l = 0; l <= L.n; ++l) {
     const int in = l < L.n ? m.layer[l].in_dim : 64, out = l < L.n ? m.layer[l].out_dim : 64;
-    L.kb[l] = (in + 15) / 16;
     L.ob[l] = (out + 15) / 16;
-    L.stride[l] = lds_stride(16 * L.kb[l]);
     L.relu[l] = l < L.n ? m.layer[l].relu : 0;
     L.w_off[l] = off;
-    off += 16 * L.ob[l] * L.stride[l];
+    if (prec == PEMP_PREC_BF16X3) {
+      L.kb[l] = (in + 31) / 32;
+      L.stride[l] = lds_stride_bf(32 * L.kb[l]);
+      off += 16 * L.ob[l] * L.stride[l];                 // hi + lo bf16 = stride floats per row
+      L.g_off[l] = goff;
+      goff += 2 * 16 * L.ob[l] * 32 * L.kb[l];
+    } else {
+      L.kb[l] = (in + 15) / 16;
+      L.stride[l] = lds_stride(16 * L.kb[l]);
+      off += 16 * L.ob[l] * L.stride[l];
+    }
   }
   for (int l = 0; l <= L.n; ++l) {
     L.b_off[l] = off;
@@ -532,10 +608,44 @@ __device__ __forceinline__ void layer_lds(const float* __restrict__ W, int ldw, 
   }
 }
 
+// bf16x3 variant: W = hi rows [16 OB][ldw] then lo rows; KB32 (<= 2) k-blocks of 32 inputs.
+__device__ __forceinline__ void layer_lds_bf(const __bf16* __restrict__ W, int ldw, const float* __restrict__ bias,
+                                             int KB32, int OB, int relu, const float (&in)[4][4], float (&out)[4][4]) {
+  const int lane = __lane_id(), i = lane & 15, g = lane >> 4;
+  bf16x8_t hi[2], lo[2];
+  split_bf16(in, hi, lo);
+  const __bf16* Wl = W + 16 * OB * ldw;
+#pragma unroll
+  for (int ob = 0; ob < 4; ++ob) {
+    if (ob < OB) {
+      const float4 bb = ld4(bias + 16 * ob + 4 * g);
+      f32x4 c = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        if (kb < KB32) {
+          const int o = (16 * ob + i) * ldw + 32 * kb + 8 * g;
+          const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(W + o);
+          const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(Wl + o);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, hi[kb], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, lo[kb], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, hi[kb], c, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[ob][r] = relu ? fmaxf(c[r], 0.0f) : c[r];
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[ob][r] = 0.0f;
+    }
+  }
+}
+
 // Edge embedding (sorted order): e_init = MLP(edge_attr[orig]); Q0 = W1_e_init·e_init + b1.
 // One 16-wave workgroup per CU, weights staged once in LDS; a wave walks an equal share of the
 // sorted positions in 16-edge tiles.
+template <int PREC>
 __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp emb, EmbedLayout Lo,
+                                                                     const uint16_t* __restrict__ emb_bf,
                                                                      const float* __restrict__ ea, int A,
                                                                      const int* __restrict__ s_orig, int64_t E,
                                                                      const float* __restrict__ q0_w,
@@ -544,12 +654,23 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp em
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
   for (int l = 0; l <= Lo.n; ++l) {
-    const float* src = l < Lo.n ? emb.layer[l].w : q0_w;
     const float* bsrc = l < Lo.n ? emb.layer[l].b : q0_b;
-    const int ip = 16 * Lo.kb[l], rows = 16 * Lo.ob[l], q4 = ip / 4;
-    for (int idx = threadIdx.x; idx < rows * q4; idx += 64 * EDGE_WAVES) {
-      const int row = idx / q4, c4 = (idx - row * q4) * 4;
-      *reinterpret_cast<float4*>(&sm[Lo.w_off[l] + row * Lo.stride[l] + c4]) = ld4(src + row * ip + c4);
+    const int rows = 16 * Lo.ob[l];
+    if (PREC == 0) {
+      const float* src = l < Lo.n ? emb.layer[l].w : q0_w;
+      const int ip = 16 * Lo.kb[l], q4 = ip / 4;
+      for (int idx = threadIdx.x; idx < rows * q4; idx += 64 * EDGE_WAVES) {
+        const int row = idx / q4, c4 = (idx - row * q4) * 4;
+        *reinterpret_cast<float4*>(&sm[Lo.w_off[l] + row * Lo.stride[l] + c4]) = ld4(src + row * ip + c4);
+      }
+    } else {
+      const uint16_t* src = emb_bf + Lo.g_off[l];
+      const int ip = 32 * Lo.kb[l], q8 = ip / 8;
+      __bf16* dstb = reinterpret_cast<__bf16*>(sm + Lo.w_off[l]);
+      for (int idx = threadIdx.x; idx < 2 * rows * q8; idx += 64 * EDGE_WAVES) {   // hi rows, then lo rows
+        const int row = idx / q8, c8 = (idx - row * q8) * 8;
+        *reinterpret_cast<uint4*>(&dstb[row * Lo.stride[l] + c8]) = *reinterpret_cast<const uint4*>(src + row * ip + c8);
+      }
     }
     for (int idx = threadIdx.x; idx < rows; idx += 64 * EDGE_WAVES) sm[Lo.b_off[l] + idx] = bsrc[idx];
   }
@@ -571,18 +692,28 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp em
         const int f = 16 * mb + 4 * g + r;
         x[mb][r] = f < A ? ea[o * A + f] : 0.0f;
       }
-    // layers alternate x -> y -> x ...; the result ends in x
-    for (int l = 0; l < Lo.n; ++l) {
-      if ((l & 1) == 0) layer_lds(smz + Lo.w_off[l], Lo.stride[l], smz + Lo.b_off[l], Lo.kb[l], Lo.ob[l], Lo.relu[l], x, y);
-      else layer_lds(smz + Lo.w_off[l], Lo.stride[l], smz + Lo.b_off[l], Lo.kb[l], Lo.ob[l], Lo.relu[l], y, x);
-    }
-    if (Lo.n & 1) {
+    // layers alternate x -> y -> x ...; the result ends in x, then Q0 -> y
+    for (int l = 0; l <= Lo.n; ++l) {
+      const float* W = smz + Lo.w_off[l];
+      const float* bias = smz + Lo.b_off[l];
+      const int relu = Lo.relu[l];
+      const bool odd = (l & 1) != 0;
+      if (l == Lo.n && (Lo.n & 1)) {               // the embedding result is in y: move it to x
 #pragma unroll
-      for (int ob = 0; ob < 4; ++ob)
+        for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) x[ob][r] = y[ob][r];
+          for (int r = 0; r < 4; ++r) x[ob][r] = y[ob][r];
+      }
+      const bool to_y = l == Lo.n || !odd;
+      if (PREC == 0) {
+        if (to_y) layer_lds(W, Lo.stride[l], bias, Lo.kb[l], Lo.ob[l], relu, x, y);
+        else layer_lds(W, Lo.stride[l], bias, Lo.kb[l], Lo.ob[l], relu, y, x);
+      } else {
+        const __bf16* Wb = reinterpret_cast<const __bf16*>(W);
+        if (to_y) layer_lds_bf(Wb, Lo.stride[l], bias, Lo.kb[l], Lo.ob[l], relu, x, y);
+        else layer_lds_bf(Wb, Lo.stride[l], bias, Lo.kb[l], Lo.ob[l], relu, y, x);
+      }
     }
-    layer_lds(smz + Lo.w_off[Lo.n], Lo.stride[Lo.n], smz + Lo.b_off[Lo.n], 4, 4, 0, x, y);
     if (valid) {
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob) {
@@ -694,62 +825,6 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
-
-// ---- bf16x3 split precision (PREC 1): x·w ~= xh·wh + xl·wh + xh·wl with x = xh + xl, w = wh + wl,
-// each part bf16 (RNE) and fp32 accumulation in v_mfma_f32_16x16x32_bf16; the dropped xl·wl term
-// and the rounding of the low parts leave ~2^-16 relative error per product. Fragment mapping:
-// B (activations) lane (g, c) holds, for k-block kb, slots 8g + j = features
-// 32 kb + 16 (j >> 2) + 4 g + (j & 3) — exactly its fp32 accumulator registers x[2 kb + (j >> 2)][j & 3]
-// — so layer outputs feed the next layer unchanged; the host stores the weights with their input
-// columns in the same slot order (mpn/fold.py::bf16_pack).
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-
-__device__ __forceinline__ void split_bf16(const float (&x)[4][4], bf16x8_t (&hi)[2], bf16x8_t (&lo)[2]) {
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float f = x[2 * kb + (j >> 2)][j & 3];
-      const __bf16 h = (__bf16)f;
-      hi[kb][j] = h;
-      lo[kb][j] = (__bf16)(f - (float)h);
-    }
-}
-
-// acc[ob] += W[16 ob + i][.] · x   with W hi / lo parts in LDS ([out][LDW] bf16 each), K = 64
-template <int OB>
-__device__ __forceinline__ void gemm_bf3(const __bf16* __restrict__ Wh, const __bf16* __restrict__ Wl,
-                                         const bf16x8_t (&hi)[2], const bf16x8_t (&lo)[2], float (&acc)[OB][4]) {
-  const int lane = __lane_id(), i = lane & 15, g = lane >> 4;
-#pragma unroll
-  for (int ob = 0; ob < OB; ++ob) {
-    f32x4 c = {acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]};
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      const int o = (16 * ob + i) * LDW + 32 * kb + 8 * g;
-      const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(Wh + o);
-      const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(Wl + o);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, hi[kb], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, lo[kb], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, hi[kb], c, 0, 0, 0);
-    }
-    acc[ob][0] = c[0]; acc[ob][1] = c[1]; acc[ob][2] = c[2]; acc[ob][3] = c[3];
-  }
-}
-
-// one layer on fragments in the chosen precision; W points at the LDS image of the matrix
-// (PREC 0: fp32 [out][LDW]; PREC 1: bf16 hi [out][LDW] then lo [out][LDW])
-template <int PREC, int OB>
-__device__ __forceinline__ void gemm_p(const void* W, int out_rows, const float (&x)[4][4], float (&acc)[OB][4]) {
-  if (PREC == 0) {
-    gemm_frag<4, OB>(static_cast<const float*>(W), LDW, x, acc);
-  } else {
-    bf16x8_t hi[2], lo[2];
-    split_bf16(x, hi, lo);
-    const __bf16* Wh = static_cast<const __bf16*>(W);
-    gemm_bf3<OB>(Wh, Wh + out_rows * LDW, hi, lo, acc);
-  }
-}
 
 // LDS image of the edge pass (floats): three 64x64 weight tiles, e2_b | attn_w, and for the
 // fused published edge head (HEAD 1) its 64x64 and 32x64 tiles + biases + last row.
@@ -1280,11 +1355,17 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
   if (E > 0) {
     ProfScope prof("edge_embed", st);
     if (mlp_ok(w->edge_emb, 64, 64)) {
-      const EmbedLayout lo = embed_layout(w->edge_emb);
+      const int prec = desc->precision == PEMP_PREC_BF16X3 && w->emb_bf ? PEMP_PREC_BF16X3 : PEMP_PREC_FP32;
+      const EmbedLayout lo = embed_layout(w->edge_emb, prec);
       const int grid = (int)std::min<int64_t>(num_cus(), (E + 16 * EDGE_WAVES - 1) / (16 * EDGE_WAVES));
-      hipLaunchKernelGGL(edge_embed_kernel, dim3(grid), dim3(64 * EDGE_WAVES), (size_t)lo.total * sizeof(float), st,
-                         w->edge_emb, lo, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, ws.EA,
-                         ws.Q0);
+      if (prec == PEMP_PREC_BF16X3)
+        hipLaunchKernelGGL(edge_embed_kernel<1>, dim3(grid), dim3(64 * EDGE_WAVES), (size_t)lo.total * sizeof(float),
+                           st, w->edge_emb, lo, w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w,
+                           w->q0_b, ws.EA, ws.Q0);
+      else
+        hipLaunchKernelGGL(edge_embed_kernel<0>, dim3(grid), dim3(64 * EDGE_WAVES), (size_t)lo.total * sizeof(float),
+                           st, w->edge_emb, lo, w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w,
+                           w->q0_b, ws.EA, ws.Q0);
     } else {
       hipLaunchKernelGGL(edge_embed_wide_kernel, dim3((unsigned)((E + 63) / 64)), dim3(256), 0, st, w->edge_emb,
                          edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, ws.EA, ws.Q0);

@@ -66,11 +66,11 @@ def _padded(W, b, in_pad=None):
     return Wp, bp
 
 
-def bf16_slot_perm():
+def bf16_slot_perm(n_kb=2):
     """Input column of each MFMA k-slot (v_mfma_f32_16x16x32_bf16 fragments, csrc/mpn.hip gemm_bf3):
     slot 32 kb + 8 g + j <- input 32 kb + 16 (j >> 2) + 4 g + (j & 3)."""
     perm = []
-    for kb in range(2):
+    for kb in range(n_kb):
         for g in range(4):
             for j in range(8):
                 perm.append(32 * kb + 16 * (j >> 2) + 4 * g + (j & 3))
@@ -78,9 +78,14 @@ def bf16_slot_perm():
 
 
 def bf16_pack(W):
-    """[out, 64] weights -> [2, out, 64] bf16 bit patterns (hi, lo), columns in slot order. The split
-    starts from the fp32 value the fp32 path uses: hi = bf16(w), lo = bf16(w - hi) (RNE)."""
-    w = W.to(torch.float32)[:, bf16_slot_perm()]
+    """[out, in] weights -> [2, out_pad16, in_pad32] bf16 bit patterns (hi, lo), zero padded, columns
+    in slot order. The split starts from the fp32 value the fp32 path uses: hi = bf16(w),
+    lo = bf16(w - hi) (RNE)."""
+    out, inn = W.shape
+    n_kb = (inn + 31) // 32
+    Wp = torch.zeros(_pad16(out), 32 * n_kb, dtype=torch.float64)
+    Wp[:out, :inn] = W
+    w = Wp.to(torch.float32)[:, bf16_slot_perm(n_kb)]
     hi = w.to(torch.bfloat16)
     lo = (w - hi.to(torch.float32)).to(torch.bfloat16)
     return torch.stack([hi, lo], 0).contiguous().view(torch.int16)
@@ -170,6 +175,10 @@ def fold_weights(model, device) -> Folded:
             and head[0][2] and head[1][2] and not head[2][2] and head[2][0].shape[0] == 1):
         s.head_bf = f.dev_raw(torch.cat([bf16_pack(head[0][0]).reshape(-1), bf16_pack(head[1][0]).reshape(-1)]),
                               device).data_ptr()
+    emb = mlp_layers(model.edge_embedding)
+    if all(W.shape[0] <= 64 and W.shape[1] <= 64 for W, _, _ in emb):
+        packs = [bf16_pack(W).reshape(-1) for W, _, _ in emb] + [bf16_pack(q0).reshape(-1)]
+        s.emb_bf = f.dev_raw(torch.cat(packs), device).data_ptr()
     attn = getattr(layer, "attn_net", None)
     if attn is not None:
         s.attn_w = f.dev(attn[0].weight.detach().double().cpu().reshape(64), device).data_ptr()
