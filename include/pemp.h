@@ -14,6 +14,7 @@
  *                        Utils/Utils.py:15-20 non_maximum_suppression
  *   pemp_pack_nodes      ConstructGraph.py:100-103,206-231 (node features, tags, batching)
  *   pemp_graph_offsets   ConstructGraph.py:222-223 (per-image node/edge offsets, on the device)
+ *   pemp_fully_graph_build  the four above fused for GRAPH_TYPE fully (one launch)
  *   pemp_fully_graph     ConstructGraph.py:376-381 fully_connected_mpn_graph (+ batch offsets :222-223)
  *   pemp_knn_graph_*     ConstructGraph.py:363-368 knn_mpn_graph (torch_cluster knn_graph k=50,
  *                        PyG to_undirected, remove_self_loops)
@@ -79,6 +80,17 @@ int pemp_pack_nodes(const float* features /*[B,C,H,W]*/, int C, const float* tag
  * upload of ConstructGraph.py:222-223): node_off[b] = sum_{b'<b} n_det[b'] ([B+1] int64) and, if
  * fully_edge_off != NULL, fully_edge_off[b] = sum_{b'<b} n_b' (n_b' - 1) ([B+1] int64). */
 int pemp_graph_offsets(const int32_t* n_det, int B, int64_t* node_off, int64_t* fully_edge_off, void* stream);
+
+/* The whole fully-connected graph in ONE launch after the count read-back (equivalent to
+ * pemp_graph_offsets + pemp_pack_nodes + pemp_fully_graph + pemp_edge_features, same outputs
+ * bit for bit): node offsets from n_det, node packing, edge_index of every image, edge_attr
+ * (mode = PEMP_EF_*, width J+2 / J / 1 / 2 / J+3). B <= 1024.
+ * n_total = sum n_det, e_total = sum n (n - 1). tagmaps / joint_tags may be NULL. */
+int pemp_fully_graph_build(const int32_t* n_det, int B, const int64_t* det_xyt, const float* det_scores, int cap,
+                           const float* features, int C, const float* tagmaps, int F, int J, int H, int W,
+                           int64_t n_total, int64_t e_total, float norm_factor, int mode, float* x,
+                           int64_t* joint_det, float* joint_scores, int64_t* batch_index, float* joint_tags,
+                           int64_t* edge_index, float* edge_attr, void* stream);
 
 /* Fully connected graph per image: all (i,j), i != j, sorted by (src,dst), node-offset per image.
  * node_off / edge_off: device [B+1] int64 with edge_off[b+1]-edge_off[b] = n_b (n_b - 1). */
@@ -174,12 +186,13 @@ typedef struct pemp_mpn_desc {
   int32_t edge_attr_dim;  /* EDGE_INPUT_DIM */
   int32_t node_in_dim;    /* NODE_INPUT_DIM */
   int32_t precision;      /* PEMP_PREC_* */
-  int32_t pad_;
+  int32_t types_stride;   /* element stride of node_types (e.g. 3 for joint_det[:, 2]); 0 or 1 = dense */
 } pemp_mpn_desc;
 
 size_t pemp_mpn_workspace_size(const pemp_mpn_desc* desc, int64_t N, int64_t E);
 /* x [N,node_in_dim], edge_attr [E,edge_attr_dim], edge_index [2,E] (row 0 source j, row 1
- * target i), node_types [N] (already mapped by sum_node_types; values < T).
+ * target i), node_types [N] with element stride desc->types_stride (already mapped by
+ * sum_node_types; values < T).
  * Outputs (n_rec = min(aux+1, steps) recorded iterations, NodeClassificationMPNSimple.py:81-94):
  *   edge_logits [n_rec][E]; node_logits [n_rec+1][N] and class_logits [n_rec+1][N][J], whose
  *   last slot is the head evaluation after the loop (:93-94). */

@@ -35,7 +35,7 @@ class PempMpnWeights(ctypes.Structure):
 class PempMpnDesc(ctypes.Structure):
     _fields_ = [("num_types", c_i32), ("num_joints", c_i32), ("steps", c_i32), ("aux_loss_steps", c_i32),
                 ("aggr", c_i32), ("hidden", c_i32), ("edge_attr_dim", c_i32), ("node_in_dim", c_i32),
-                ("precision", c_i32), ("pad_", c_i32)]
+                ("precision", c_i32), ("types_stride", c_i32)]
 
 
 # name -> (restype, argtypes); every symbol of include/pemp.h
@@ -49,6 +49,8 @@ SIGNATURES = {
     "pemp_pack_nodes": (c_i32, [c_p, c_i32, c_p, c_i32, c_i32, c_i32, c_i32, c_i32, c_p, c_p, c_i32, c_p, c_i64,
                                 c_p, c_p, c_p, c_p, c_p, c_p]),
     "pemp_graph_offsets": (c_i32, [c_p, c_i32, c_p, c_p, c_p]),
+    "pemp_fully_graph_build": (c_i32, [c_p, c_i32, c_p, c_p, c_i32, c_p, c_i32, c_p, c_i32, c_i32, c_i32, c_i32,
+                                       c_i64, c_i64, c_f32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "pemp_fully_graph": (c_i32, [c_p, c_p, c_i32, c_i64, c_p, c_p]),
     "pemp_knn_workspace_size": (c_sz, [c_p, c_i32]),
     "pemp_knn_graph_count": (c_i32, [c_p, c_p, c_p, c_i32, c_i32, c_p, c_sz, c_p, c_p]),

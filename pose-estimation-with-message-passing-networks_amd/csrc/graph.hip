@@ -331,6 +331,169 @@ extern "C" int pemp_pack_nodes(const float* features, int C, const float* tagmap
 
 namespace pemp {
 namespace {
+constexpr int FUSED_MAXB = 1024;   // images per batch handled by the fused build (offsets in LDS)
+
+struct FusedGraphArgs {
+  const int32_t* n_det;
+  int B, cap, C, F, J, H, W, mode, A;
+  const int64_t* det;
+  const float *det_sc, *feat, *tags;
+  float norm;
+  int64_t n_total, e_total;
+  int node_blocks;
+  float *x, *jsc, *jtag, *edge_attr;
+  int64_t *jdet, *bidx, *ei;
+};
+
+// One launch for the whole fully-connected graph after the count read-back: every block derives
+// the per-image node / edge offsets from n_det in LDS; blocks [0, node_blocks) pack nodes
+// (pack_nodes_kernel), the rest emit 256 edges each: (src, dst) of the fully graph
+// (fully_graph_kernel) and their edge_attr rows (edge_features_kernel), the endpoints read
+// straight from the detections.
+__global__ __launch_bounds__(256) void fused_fully_graph_kernel(FusedGraphArgs a) {
+  __shared__ long long noff[FUSED_MAXB + 1], eoff[FUSED_MAXB + 1];
+  __shared__ float dx_s[256], dy_s[256], th_s[256];
+  __shared__ int ts_s[256], td_s[256];
+  const int B = a.B;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    long long cn = 0, ce = 0;
+    for (int c0 = 0; c0 < B; c0 += 64) {
+      const int b = c0 + lane;
+      const long long n = b < B ? a.n_det[b] : 0, e = n * (n > 0 ? n - 1 : 0);
+      long long xn = n, xe = e;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const long long on = __shfl_up(xn, off), oe = __shfl_up(xe, off);
+        if (lane >= off) { xn += on; xe += oe; }
+      }
+      if (b < B) { noff[b] = cn + xn - n; eoff[b] = ce + xe - e; }
+      cn += __shfl(xn, 63);
+      ce += __shfl(xe, 63);
+    }
+    if (lane == 0) { noff[B] = cn; eoff[B] = ce; }
+  }
+  __syncthreads();
+  auto seg = [&](const long long* off, long long v) {
+    int lo = 0, hi = B - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (off[mid] <= v) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+  };
+  if ((int)blockIdx.x < a.node_blocks) {   // ---- nodes ----
+    const int64_t total = a.n_total * a.C;
+    for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)a.node_blocks * 256) {
+      const int64_t g = idx / a.C;
+      const int c = (int)(idx - g * a.C);
+      const int b = seg(noff, g);
+      const int64_t i = g - noff[b];
+      const int64_t* d = a.det + ((size_t)b * a.cap + i) * 3;
+      const int64_t px = d[0], py = d[1], pt = d[2];
+      a.x[idx] = a.feat[(((size_t)b * a.C + c) * a.H + py) * a.W + px];
+      if (c == 0) {
+        a.jdet[g * 3 + 0] = px; a.jdet[g * 3 + 1] = py; a.jdet[g * 3 + 2] = pt;
+        a.jsc[g] = a.det_sc[(size_t)b * a.cap + i];
+        a.bidx[g] = b;
+      }
+      if (a.tags && c < a.F) a.jtag[g * a.F + c] = a.tags[((((size_t)b * a.J + pt) * a.H + py) * a.W + px) * a.F + c];
+    }
+    return;
+  }
+  // ---- edges ----
+  const int eb = blockIdx.x - a.node_blocks, nbe = gridDim.x - a.node_blocks;
+  for (int64_t base = (int64_t)eb * 256; base < a.e_total; base += (int64_t)nbe * 256) {
+    const int64_t e = base + threadIdx.x;
+    if (e < a.e_total) {
+      const int b = seg(eoff, e);
+      const int64_t n = noff[b + 1] - noff[b];
+      const int64_t el = e - eoff[b];
+      const int64_t i = el / (n - 1), r = el - i * (n - 1);
+      const int64_t j = r < i ? r : r + 1;                 // all (i, j), i != j, sorted by (i, j)
+      a.ei[e] = noff[b] + i;
+      a.ei[a.e_total + e] = noff[b] + j;
+      const int64_t* ds = a.det + ((size_t)b * a.cap + i) * 3;   // source = edge_index[0]
+      const int64_t* dd = a.det + ((size_t)b * a.cap + j) * 3;   // target = edge_index[1]
+      const int64_t sx = ds[0], sy = ds[1], dx = dd[0], dy = dd[1];
+      dx_s[threadIdx.x] = (float)(dx - sx) / a.norm;            // ConstructGraph.py:311-317
+      dy_s[threadIdx.x] = (float)(dy - sy) / a.norm;
+      ts_s[threadIdx.x] = (int)ds[2];
+      td_s[threadIdx.x] = (int)dd[2];
+      if (a.mode == PEMP_EF_POSITION_ANGLE_CONNECTION) {
+        const float ax = (float)(sx - dx), ay = (float)(sy - dy);
+        const float th = fabsf(acosf(ax * (1.0f / sqrtf(ax * ax + ay * ay))));
+        th_s[threadIdx.x] = isnan(th) ? 0.0f : th;
+      }
+    }
+    __syncthreads();
+    const int cnt = (int)min<int64_t>(256, a.e_total - base), total = cnt * a.A;
+    float* o = a.edge_attr + base * a.A;
+    for (int k = threadIdx.x; k < total; k += 256) {
+      const int el = k / a.A, f = k - el * a.A;
+      float v = 0.0f;
+      int oh = -1;
+      switch (a.mode) {
+        case PEMP_EF_POSITION_CONNECTION:
+          if (f == 0) v = dx_s[el]; else if (f == 1) v = dy_s[el]; else oh = f - 2;
+          break;
+        case PEMP_EF_CONNECTION: oh = f; break;
+        case PEMP_EF_NOTHING: v = 0.0f; break;
+        case PEMP_EF_POSITION: v = f == 0 ? dx_s[el] : dy_s[el]; break;
+        case PEMP_EF_POSITION_ANGLE_CONNECTION:
+          if (f == 0) v = dx_s[el]; else if (f == 1) v = dy_s[el]; else if (f == 2) v = th_s[el]; else oh = f - 3;
+          break;
+      }
+      if (oh >= 0) v = (ts_s[el] == oh || td_s[el] == oh) ? 1.0f : 0.0f;
+      o[k] = v;
+    }
+    __syncthreads();
+  }
+}
+}  // namespace
+}  // namespace pemp
+
+static int ef_width(int mode, int J) {
+  switch (mode) {
+    case PEMP_EF_POSITION_CONNECTION: return J + 2;
+    case PEMP_EF_CONNECTION: return J;
+    case PEMP_EF_NOTHING: return 1;
+    case PEMP_EF_POSITION: return 2;
+    case PEMP_EF_POSITION_ANGLE_CONNECTION: return J + 3;
+    default: return -1;
+  }
+}
+
+extern "C" int pemp_fully_graph_build(const int32_t* n_det, int B, const int64_t* det_xyt, const float* det_scores,
+                                      int cap, const float* features, int C, const float* tagmaps, int F, int J,
+                                      int H, int W, int64_t n_total, int64_t e_total, float norm_factor, int mode,
+                                      float* x, int64_t* joint_det, float* joint_scores, int64_t* batch_index,
+                                      float* joint_tags, int64_t* edge_index, float* edge_attr, void* stream) {
+  PEMP_CHECK_ARG(n_det && det_xyt && det_scores && features && x && joint_det && joint_scores && batch_index,
+                 "pemp_fully_graph_build: null pointer");
+  PEMP_CHECK_ARG(B > 0 && B <= FUSED_MAXB && C > 0 && J > 0 && H > 0 && W > 0 && n_total >= 0 && e_total >= 0,
+                 "pemp_fully_graph_build: bad shape (B must be in [1, %d])", FUSED_MAXB);
+  PEMP_CHECK_ARG(!tagmaps || (joint_tags && F > 0 && F <= C), "pemp_fully_graph_build: tags need F in [1, C]");
+  PEMP_CHECK_ARG(e_total == 0 || (edge_index && edge_attr), "pemp_fully_graph_build: null edge outputs");
+  const int A = ef_width(mode, J);
+  if (A < 0) { set_error("pemp_fully_graph_build: unknown edge feature mode %d", mode); return PEMP_ERR_INVALID_ARG; }
+  if (n_total == 0) return PEMP_OK;
+  FusedGraphArgs a{};
+  a.n_det = n_det; a.B = B; a.cap = cap; a.C = C; a.F = F; a.J = J; a.H = H; a.W = W; a.mode = mode; a.A = A;
+  a.det = det_xyt; a.det_sc = det_scores; a.feat = features; a.tags = tagmaps; a.norm = norm_factor;
+  a.n_total = n_total; a.e_total = e_total;
+  a.node_blocks = grid_for(n_total * C, 256, 4096);
+  const int edge_blocks = e_total > 0 ? grid_for(e_total, 256, 8192) : 0;
+  a.x = x; a.jsc = joint_scores; a.jtag = joint_tags; a.edge_attr = edge_attr;
+  a.jdet = joint_det; a.bidx = batch_index; a.ei = edge_index;
+  ProfScope prof("graph_build", as_stream(stream));
+  hipLaunchKernelGGL(fused_fully_graph_kernel, dim3(a.node_blocks + edge_blocks), dim3(256), 0, as_stream(stream), a);
+  PEMP_LAUNCH_CHECK();
+  return PEMP_OK;
+}
+
+namespace pemp {
+namespace {
 // node_off[b] = sum_{b'<b} n_det[b'], fully_edge_off[b] = sum_{b'<b} n (n - 1): one wave, chunks of 64
 __global__ __launch_bounds__(64) void graph_offsets_kernel(const int32_t* __restrict__ n_det, int B,
                                                            int64_t* __restrict__ node_off,

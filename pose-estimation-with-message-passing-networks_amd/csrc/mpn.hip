@@ -220,12 +220,12 @@ static MpnWs mpn_carve(void* base, int T, int64_t N, int64_t E, size_t* bytes) {
 // Prepare: type-major counting sort of the edges (deterministic: ties kept in edge-id order)
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void mpn_count_kernel(const int64_t* __restrict__ ei, const int64_t* __restrict__ types,
-                                                        int64_t N, int64_t E, int T, int* __restrict__ cnt,
+                                                        int64_t ts, int64_t N, int64_t E, int T, int* __restrict__ cnt,
                                                         int* __restrict__ err) {
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t s = ei[e], d = ei[E + e];
     if (s < 0 || s >= N || d < 0 || d >= N) { atomicOr(err, 1); continue; }
-    const int64_t t = T == 1 ? 0 : types[s];      // MPLayer (one message MLP) ignores types
+    const int64_t t = T == 1 ? 0 : types[s * ts];   // MPLayer (one message MLP) ignores types
     if (t < 0 || t >= T) { atomicOr(err, 2); continue; }
     atomicAdd(&cnt[t * N + d], 1);
   }
@@ -342,12 +342,12 @@ __global__ __launch_bounds__(1024) void mpn_scan_kernel(const int* __restrict__ 
 // counts are consumed here: cnt[key] counts down, so edges land in a key's segment in arbitrary
 // order; mpn_segsort_kernel restores edge-id order inside each segment.
 __global__ __launch_bounds__(256) void mpn_scatter_kernel(const int64_t* __restrict__ ei, const int64_t* __restrict__ types,
-                                                          int64_t N, int64_t E, int T, const int* __restrict__ seg,
+                                                          int64_t ts, int64_t N, int64_t E, int T, const int* __restrict__ seg,
                                                           int* __restrict__ cnt, int* __restrict__ perm) {
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t s = ei[e], d = ei[E + e];
     if (s < 0 || s >= N || d < 0 || d >= N) continue;
-    const int64_t t = T == 1 ? 0 : types[s];
+    const int64_t t = T == 1 ? 0 : types[s * ts];
     if (t < 0 || t >= T) continue;
     const int64_t key = t * N + d;
     perm[seg[key] + atomicSub(&cnt[key], 1) - 1] = (int)e;
@@ -1094,6 +1094,9 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
 //   (b) the next iteration's node table NT = [x0 | x] · pre_w^T + pre_b
 //   (c) the node / class heads on x (published widths <= 64), written to one or two slots
 struct NodeStepArgs {
+  const float* x_in;     // embed mode: node inputs [N][in_ld] -> X = [emb | emb] (NodeClassificationMPNSimple.py:67-69)
+  int in_ld;
+  pemp_mlp emb;
   const float* agg;
   const int* seg;
   int T, do_update;
@@ -1123,8 +1126,54 @@ __global__ __launch_bounds__(64 * NODE_WAVES) void node_step_kernel(NodeStepArgs
   const int64_t n0 = (int64_t)blockIdx.x * 16, N = a.N;
   const int T = a.T;
   const bool owner = blockIdx.y == 0;           // writes X and the heads
+  if (a.x_in) {
+    // node embedding MLP on the block's 16 rows (waves split each layer's output blocks), the
+    // result is both halves of x = [x_init | x_cur]
+    float* act0 = &red[0][0];
+    float* act1 = act0 + 16 * RS;
+    const int K0 = a.emb.layer[0].in_dim, KP = (K0 + 15) & ~15;
+    for (int idx = threadIdx.x; idx < 16 * KP; idx += 64 * NODE_WAVES) {
+      const int r = idx / KP, k = idx - r * KP;
+      act0[r * RS + k] = (n0 + r < N && k < K0) ? a.x_in[(n0 + r) * a.in_ld + k] : 0.0f;
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int l = 0; l < a.emb.n_layers; ++l) {
+      const pemp_layer& L = a.emb.layer[l];
+      const int KB = (L.in_dim + 15) >> 4, OB = (L.out_dim + 15) >> 4, ldw = KB * 16;
+      const float* src = cur ? act1 : act0;
+      float* dst = cur ? act0 : act1;
+      for (int ob = wave; ob < OB; ob += NODE_WAVES) {
+        const float4 bb = ld4(L.b + 16 * ob + 4 * g);
+        f32x4 acc = {bb.x, bb.y, bb.z, bb.w};
+        for (int mb = 0; mb < KB; ++mb) {
+          const float4 w = ld4(L.w + (16 * ob + c) * ldw + 16 * mb + 4 * g);
+          const float4 xv = ld4(&src[c * RS + 16 * mb + 4 * g]);
+          acc = mfma4(w.x, xv.x, acc);
+          acc = mfma4(w.y, xv.y, acc);
+          acc = mfma4(w.z, xv.z, acc);
+          acc = mfma4(w.w, xv.w, acc);
+        }
+        if (L.relu) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[r] = fmaxf(acc[r], 0.0f);
+        }
+        st4(&dst[c * RS + 16 * ob + 4 * g], acc[0], acc[1], acc[2], acc[3]);
+      }
+      __syncthreads();
+      cur ^= 1;
+    }
+    const float* res = cur ? act1 : act0;
+    for (int idx = threadIdx.x; idx < 16 * D; idx += 64 * NODE_WAVES) {
+      const int r = idx >> 6, f = idx & 63;
+      const float v = res[r * RS + f];
+      xs[r * RS + f] = v;
+      xs[r * RS + 64 + f] = v;
+      if (owner && n0 + r < N) { a.X[(n0 + r) * 128 + f] = v; a.X[(n0 + r) * 128 + 64 + f] = v; }
+    }
+  }
   // x0 half (and x when there is no update)
-  for (int idx = threadIdx.x; idx < 16 * 32; idx += 64 * NODE_WAVES) {
+  for (int idx = threadIdx.x; idx < 16 * 32 && !a.x_in; idx += 64 * NODE_WAVES) {
     const int r = idx >> 5, k4 = (idx & 31) * 4;
     if (a.do_update && k4 >= 64) continue;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1323,6 +1372,7 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
   PEMP_CHECK_ARG(!(E > 0 && N == 0), "pemp_mpn_forward: edges without nodes");
   const MpnWs ws = mpn_carve(workspace, T, N, E, nullptr);
   const hipStream_t st = as_stream(stream);
+  const int64_t tstride = desc->types_stride > 0 ? desc->types_stride : 1;   // node_types may be a strided view
   const int64_t K = (int64_t)T * N;
 
   // ---- prepare: type-major order ----
@@ -1332,7 +1382,7 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
                      st, ws.err, K + 65);
   PEMP_LAUNCH_CHECK();
   if (E > 0) {
-    hipLaunchKernelGGL(mpn_count_kernel, dim3(grid1d(E, 256)), dim3(256), 0, st, edge_index, node_types, N, E, T,
+    hipLaunchKernelGGL(mpn_count_kernel, dim3(grid1d(E, 256)), dim3(256), 0, st, edge_index, node_types, tstride, N, E, T,
                        ws.cnt, ws.err);
     PEMP_LAUNCH_CHECK();
   }
@@ -1340,7 +1390,7 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
                      ws.wg_start);
   PEMP_LAUNCH_CHECK();
   if (E > 0) {
-    hipLaunchKernelGGL(mpn_scatter_kernel, dim3(grid1d(E, 256)), dim3(256), 0, st, edge_index, node_types, N, E, T,
+    hipLaunchKernelGGL(mpn_scatter_kernel, dim3(grid1d(E, 256)), dim3(256), 0, st, edge_index, node_types, tstride, N, E, T,
                        ws.seg, ws.cnt, ws.perm);
     PEMP_LAUNCH_CHECK();
     hipLaunchKernelGGL(mpn_segsort_kernel, dim3((unsigned)((K + 3) / 4)), dim3(256), 0, st, edge_index, E, K, ws.seg,
@@ -1349,9 +1399,8 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
   }
   }
 
-  // ---- embeddings ----
-  int rc = rows_mlp("node_embed", w->node_emb, x, desc->node_in_dim, N, ws.X, 128, ws.X + 64, 128, st);
-  if (rc) return rc;
+  // ---- edge embedding (the node embedding is fused into the first node step) ----
+  int rc = 0;
   if (E > 0) {
     ProfScope prof("edge_embed", st);
     if (mlp_ok(w->edge_emb, 64, 64)) {
@@ -1379,8 +1428,9 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
   const int edge_grid = std::max(num_cus(), T);   // >= wg_start[T] (see mpn_scan_kernel)
   const bool fused_heads = mlp_ok(w->node_head, 64, 64) && mlp_ok(w->class_head, 64, 64);
   const unsigned node_grid = (unsigned)((N + 15) / 16);
-  auto node_step = [&](const char* label, bool update, bool table, int slot, bool dup) -> int {
+  auto node_step = [&](const char* label, bool update, bool table, int slot, bool dup, bool embed = false) -> int {
     NodeStepArgs na{};
+    if (embed) { na.x_in = x; na.in_ld = desc->node_in_dim; na.emb = w->node_emb; }
     na.agg = ws.agg; na.seg = ws.seg; na.T = T; na.do_update = update; na.N = N;
     na.upd_w = w->upd_w; na.upd_b = w->upd_b; na.X = ws.X;
     na.pre_w = w->pre_w; na.pre_b = w->pre_b; na.NO = NO; na.NT = table ? ws.NT : nullptr;
@@ -1408,8 +1458,13 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
     }
     return PEMP_OK;
   };
-  // node table of the first iteration (or, without iterations, the heads on the embedding)
-  if ((rc = node_step("node_table", false, steps > 0, steps > 0 ? -1 : 0, false))) return rc;
+  // node embedding + node table of the first iteration (or, without iterations, the heads on the
+  // embedding); embedding widths > 128 would not fit the node step's LDS rows: separate launch
+  const bool fused_embed = mlp_ok(w->node_emb, 128, 128);
+  if (!fused_embed) {
+    if ((rc = rows_mlp("node_embed", w->node_emb, x, desc->node_in_dim, N, ws.X, 128, ws.X + 64, 128, st))) return rc;
+  }
+  if ((rc = node_step("node_table", false, steps > 0, steps > 0 ? -1 : 0, false, fused_embed))) return rc;
   float* e_cur = ws.EA;
   float* e_nxt = ws.EB;
   int rec = 0;

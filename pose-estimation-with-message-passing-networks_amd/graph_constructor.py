@@ -91,25 +91,7 @@ class NaiveGraphConstructor:
         _lib.check(L.pemp_detect(_lib.ptr(sm), _lib.ptr(masks), B, J, H, W, self.pool_kernel_size, thr, int(use_thr),
                                  topk, 3, _lib.ptr(ws), ws.numel(), _lib.ptr(det), _lib.ptr(dsc), _lib.ptr(n_det),
                                  cap, st))
-        counts = n_det.cpu().numpy().astype(np.int64)
-        if counts.max(initial=0) > cap:
-            cap = int(counts.max())
-            NaiveGraphConstructor._cap = max(NaiveGraphConstructor._cap, cap)
-            det = torch.empty(B, cap, 3, dtype=torch.int64, device=dev)
-            dsc = torch.empty(B, cap, dtype=torch.float32, device=dev)
-            _lib.check(L.pemp_detect(_lib.ptr(sm), _lib.ptr(masks), B, J, H, W, self.pool_kernel_size, thr,
-                                     int(use_thr), topk, 2, _lib.ptr(ws), ws.numel(), _lib.ptr(det), _lib.ptr(dsc),
-                                     _lib.ptr(n_det), cap, st))
-        node_off_h = np.zeros(B + 1, np.int64)
-        node_off_h[1:] = np.cumsum(counts)
-        N = int(node_off_h[-1])
-        # batch offsets are recomputed on the device from n_det (no host->device upload)
-        offs = torch.empty(2, B + 1, dtype=torch.int64, device=dev)
-        node_off, fully_off = offs[0], offs[1]
-        _lib.check(L.pemp_graph_offsets(_lib.ptr(n_det), B, _lib.ptr(node_off),
-                                        _lib.ptr(fully_off) if self.mpn_graph_type == "fully" else None, st))
-
-        # ---- nodes (pemp_pack_nodes) ----
+        # host-side preparation of the graph stage, while the detection kernels run
         feats = self.features
         if feats.dtype != torch.float32:
             feats = feats.float()
@@ -121,30 +103,55 @@ class NaiveGraphConstructor:
             F = 1 if tags.dim() == 4 else int(np.prod(tags.shape[4:]))
         else:
             F = 1
-        x = torch.empty(N, C, dtype=torch.float32, device=dev)
-        joint_det = torch.empty(N, 3, dtype=torch.int64, device=dev)
-        joint_scores = torch.empty(N, dtype=torch.float32, device=dev)
-        batch_index = torch.empty(N, dtype=torch.int64, device=dev)
-        joint_tags = torch.empty(N, F, dtype=torch.float32, device=dev)
-        _lib.check(L.pemp_pack_nodes(_lib.ptr(feats), C, _lib.ptr(tags), F, B, J, H, W, _lib.ptr(det), _lib.ptr(dsc),
-                                     cap, _lib.ptr(node_off), N, _lib.ptr(x), _lib.ptr(joint_det),
-                                     _lib.ptr(joint_scores), _lib.ptr(batch_index), _lib.ptr(joint_tags), st))
-        if tags is not None:
-            joint_tags = joint_tags.view((N,) + tuple(tags.shape[4:])) if tags.dim() > 4 else joint_tags.view(N)
-        else:
-            joint_tags = None
-
-        # ---- edges ----
-        edge_index = self._edges(L, st, joint_det, node_off, fully_off, node_off_h, B, dev)
-        E = edge_index.shape[1]
         mode = _EF_MODES.get(frozenset(self.edge_features_to_use))
         if mode is None:
             raise NotImplementedError(f"EDGE_FEATURES_TO_USE={self.edge_features_to_use}")
         A = {0: J + 2, 1: J, 2: 1, 3: 2, 4: J + 3}[mode]
         norm = float(max(W, H)) if self.normalize_node_distance else 1.0
-        edge_attr = torch.empty(E, A, dtype=torch.float32, device=dev)
-        _lib.check(L.pemp_edge_features(_lib.ptr(joint_det), _lib.ptr(edge_index), E, J, norm, mode,
-                                        _lib.ptr(edge_attr), st))
+
+        counts = n_det.cpu().numpy().astype(np.int64)      # the one host read-back of the batch
+        if counts.max(initial=0) > cap:
+            cap = int(counts.max())
+            NaiveGraphConstructor._cap = max(NaiveGraphConstructor._cap, cap)
+            det = torch.empty(B, cap, 3, dtype=torch.int64, device=dev)
+            dsc = torch.empty(B, cap, dtype=torch.float32, device=dev)
+            _lib.check(L.pemp_detect(_lib.ptr(sm), _lib.ptr(masks), B, J, H, W, self.pool_kernel_size, thr,
+                                     int(use_thr), topk, 2, _lib.ptr(ws), ws.numel(), _lib.ptr(det), _lib.ptr(dsc),
+                                     _lib.ptr(n_det), cap, st))
+        N = int(counts.sum())
+        x = torch.empty(N, C, dtype=torch.float32, device=dev)
+        joint_det = torch.empty(N, 3, dtype=torch.int64, device=dev)
+        joint_scores = torch.empty(N, dtype=torch.float32, device=dev)
+        batch_index = torch.empty(N, dtype=torch.int64, device=dev)
+        joint_tags = torch.empty(N, F, dtype=torch.float32, device=dev) if tags is not None else None
+
+        if self.mpn_graph_type == "fully" and B <= 1024:
+            # one launch: offsets + nodes + edge_index + edge_attr (pemp_fully_graph_build)
+            E = int((counts * np.maximum(counts - 1, 0)).sum())
+            edge_index = torch.empty(2, E, dtype=torch.int64, device=dev)
+            edge_attr = torch.empty(E, A, dtype=torch.float32, device=dev)
+            _lib.check(L.pemp_fully_graph_build(
+                _lib.ptr(n_det), B, _lib.ptr(det), _lib.ptr(dsc), cap, _lib.ptr(feats), C, _lib.ptr(tags), F, J, H, W,
+                N, E, norm, mode, _lib.ptr(x), _lib.ptr(joint_det), _lib.ptr(joint_scores), _lib.ptr(batch_index),
+                _lib.ptr(joint_tags), _lib.ptr(edge_index), _lib.ptr(edge_attr), st))
+        else:
+            node_off_h = np.zeros(B + 1, np.int64)
+            node_off_h[1:] = np.cumsum(counts)
+            # batch offsets are recomputed on the device from n_det (no host->device upload)
+            offs = torch.empty(2, B + 1, dtype=torch.int64, device=dev)
+            node_off, fully_off = offs[0], offs[1]
+            _lib.check(L.pemp_graph_offsets(_lib.ptr(n_det), B, _lib.ptr(node_off),
+                                            _lib.ptr(fully_off) if self.mpn_graph_type == "fully" else None, st))
+            _lib.check(L.pemp_pack_nodes(_lib.ptr(feats), C, _lib.ptr(tags), F, B, J, H, W, _lib.ptr(det),
+                                         _lib.ptr(dsc), cap, _lib.ptr(node_off), N, _lib.ptr(x), _lib.ptr(joint_det),
+                                         _lib.ptr(joint_scores), _lib.ptr(batch_index), _lib.ptr(joint_tags), st))
+            edge_index = self._edges(L, st, joint_det, node_off, fully_off, node_off_h, B, dev)
+            E = edge_index.shape[1]
+            edge_attr = torch.empty(E, A, dtype=torch.float32, device=dev)
+            _lib.check(L.pemp_edge_features(_lib.ptr(joint_det), _lib.ptr(edge_index), E, J, norm, mode,
+                                            _lib.ptr(edge_attr), st))
+        if tags is not None:
+            joint_tags = joint_tags.view((N,) + tuple(tags.shape[4:])) if tags.dim() > 4 else joint_tags.view(N)
         return (x, edge_attr, edge_index, None, None, None, None, joint_det, None, None, None, joint_scores,
                 batch_index, None, joint_tags)
 

@@ -190,7 +190,10 @@ class NodeClassificationMPNSimple(nn.Module):
         x = x.float().contiguous()
         edge_attr = edge_attr.float().contiguous()
         edge_index = edge_index.long().contiguous()
-        node_types = node_types.long().contiguous()
+        node_types = node_types.long()
+        if node_types.dim() != 1 or (N > 0 and node_types.stride(0) < 1):
+            node_types = node_types.reshape(-1).contiguous()
+        t_stride = node_types.stride(0) if N > 0 else 1       # joint_det[:, 2] is read in place
         fw = self._weights(dev)
         steps, aux = self.edge_steps, self.aux_loss_steps
         n_rec = sum(1 for i in range(steps) if i >= steps - aux - 1)
@@ -198,7 +201,7 @@ class NodeClassificationMPNSimple(nn.Module):
             raise ValueError(f"precision={self.precision!r}: expected one of {sorted(PRECISIONS)}")
         desc = _lib.PempMpnDesc(self.num_types, self.num_joints, steps, aux, self.aggr_code, 64,
                                 edge_attr.shape[1] if edge_attr.dim() == 2 else 1, x.shape[1],
-                                PRECISIONS[self.precision], 0)
+                                PRECISIONS[self.precision], t_stride)
         edge_logits = torch.empty(max(n_rec, 1), E, dtype=torch.float32, device=dev)
         node_logits = torch.empty(n_rec + 1, N, dtype=torch.float32, device=dev)
         class_logits = torch.empty(n_rec + 1, N, self.num_joints, dtype=torch.float32, device=dev)
