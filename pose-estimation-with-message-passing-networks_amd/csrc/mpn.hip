@@ -1196,14 +1196,23 @@ __global__ __launch_bounds__(64 * NODE_WAVES) void node_step_kernel(NodeStepArgs
       for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[ob][r] = 0.f;
+      const int64_t nc = n < N ? n : N - 1;          // clamped: every load below is unconditional
       for (int t = wave; t < T; t += NODE_WAVES) {
-        const bool has = n < N && a.seg[t * N + n + 1] > a.seg[t * N + n];
+        // agg rows and the segment bounds are loaded together; an empty (n, t) segment was never
+        // written by the edge pass and reads as 0 (torch_scatter), applied with a bit mask so the
+        // loads are not sunk behind the segment test
+        float4 xv[4];
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) xv[mb] = ld4(a.agg + (nc * T + t) * D + 16 * mb + 4 * g);
+        const int s0 = a.seg[t * N + nc], s1 = a.seg[t * N + nc + 1];
+        const int keep = (n < N && s1 > s0) ? -1 : 0;
         float in[4][4];
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb) {
-          float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (has) x = ld4(a.agg + (n * T + t) * D + 16 * mb + 4 * g);
-          in[mb][0] = x.x; in[mb][1] = x.y; in[mb][2] = x.z; in[mb][3] = x.w;
+          in[mb][0] = __int_as_float(__float_as_int(xv[mb].x) & keep);
+          in[mb][1] = __int_as_float(__float_as_int(xv[mb].y) & keep);
+          in[mb][2] = __int_as_float(__float_as_int(xv[mb].z) & keep);
+          in[mb][3] = __int_as_float(__float_as_int(xv[mb].w) & keep);
         }
         gemm_frag<4, 4>(a.upd_w + 64 * t, 64 * T, in, acc);
       }
