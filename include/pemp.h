@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PEMP_ABI_VERSION 2
+#define PEMP_ABI_VERSION 3
 
 enum {
   PEMP_OK = 0,
@@ -174,6 +174,8 @@ typedef struct pemp_mpn_weights {
   const uint16_t* head_bf; /* edge head layers 1, 2 (published 64->64->32->1): [2][64][64] then [2][32][64], or NULL */
   const uint16_t* emb_bf;  /* edge embedding layers then the e_init block of mlp_edge.0 (q0): per layer
                               [2][out_pad16][in_pad32], concatenated; or NULL (embedding stays fp32) */
+  const uint16_t* upd_bf;  /* per type t: U_t = upd_w[:, 64 t : 64 t + 64] as [T][2][64][64], or NULL */
+  const uint16_t* pre_bf;  /* node table weights [2][128 + T*64][128] (K = 128, 4 slot blocks), or NULL */
 } pemp_mpn_weights;
 
 typedef struct pemp_mpn_desc {

@@ -8,7 +8,7 @@ import os
 
 LIB_PATH = os.environ.get("PEMP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc",
                                                      "libpemp.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 ERR_INVALID_ARG, ERR_HIP, ERR_WORKSPACE, ERR_UNSUPPORTED = -1, -2, -3, -4
 
@@ -29,7 +29,8 @@ class PempMpnWeights(ctypes.Structure):
                 ("e2_w", c_p), ("e2_b", c_p), ("msg_w", c_p), ("attn_w", c_p), ("upd_w", c_p), ("upd_b", c_p),
                 ("edge_head", PempMlp), ("node_head", PempMlp), ("class_head", PempMlp),
                 ("attn_b", c_f32), ("pad_", c_i32),
-                ("e1_bf", c_p), ("e2_bf", c_p), ("msg_bf", c_p), ("head_bf", c_p), ("emb_bf", c_p)]
+                ("e1_bf", c_p), ("e2_bf", c_p), ("msg_bf", c_p), ("head_bf", c_p), ("emb_bf", c_p),
+                ("upd_bf", c_p), ("pre_bf", c_p)]
 
 
 class PempMpnDesc(ctypes.Structure):
@@ -106,12 +107,21 @@ def check(rc: int, L=None):
 
 
 def ptr(t):
-    return None if t is None else c_p(t.data_ptr())
+    # ctypes converts a Python int for a c_void_p argument; None is NULL
+    return None if t is None else t.data_ptr()
 
 
-def stream():
+def stream(device=None):
+    """Raw hipStream_t of the current stream of `device` (a torch.device, an index or None for the
+    current device) -- the launch stream of every libpemp call."""
     import torch
-    return c_p(torch.cuda.current_stream().cuda_stream)
+    if device is None:
+        idx = torch.cuda.current_device()
+    else:
+        idx = device if isinstance(device, int) else device.index
+        if idx is None:
+            idx = torch.cuda.current_device()
+    return torch._C._cuda_getCurrentRawStream(idx)
 
 
 class Workspace:

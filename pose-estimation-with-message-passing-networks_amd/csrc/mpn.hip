@@ -190,8 +190,10 @@ __device__ __forceinline__ float scan_max_bwd(float v, const SegMask& m) {
 // ---------------------------------------------------------------------------------------------
 struct MpnWs {
   int *cnt, *seg, *wg_start, *perm, *s_src, *s_dst, *s_orig, *err;
-  float *X, *NT, *agg, *Q0, *EA, *EB;
+  float *X, *NT, *agg, *Q0, *EA, *EB, *img;
 };
+
+constexpr int IMG_FLOATS = 112 * 1024;  // >= LDS image of a node embedding (<= 4 layers, <= 128 wide) + both heads (<= 64 wide)
 
 static MpnWs mpn_carve(void* base, int T, int64_t N, int64_t E, size_t* bytes) {
   Carver c(base);
@@ -212,6 +214,7 @@ static MpnWs mpn_carve(void* base, int T, int64_t N, int64_t E, size_t* bytes) {
   w.Q0 = c.take<float>(E * D);
   w.EA = c.take<float>(E * D);
   w.EB = c.take<float>(E * D);
+  w.img = c.take<float>(IMG_FLOATS);
   if (bytes) *bytes = c.used;
   return w;
 }
@@ -231,9 +234,7 @@ __global__ __launch_bounds__(256) void mpn_count_kernel(const int64_t* __restric
   }
 }
 
-__global__ __launch_bounds__(256) void zero_words_kernel(int* __restrict__ p, int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = 0;
-}
+
 
 // Exclusive scan of the (type, target) counts -> seg[0..K]; then per-type first workgroup of
 // the edge-step grid (wg_start). One 1024-thread block, 16 contiguous counts per thread per pass
@@ -242,6 +243,7 @@ constexpr int SCAN_SPT = 16;
 __global__ __launch_bounds__(1024) void mpn_scan_kernel(const int* __restrict__ cnt, int64_t K, int64_t N, int T,
                                                         int G, int* __restrict__ seg, int* __restrict__ wg_start) {
   __shared__ int sh[20 + 2 * (MAXT + 1)];
+  __shared__ int out[1024 * SCAN_SPT];          // one pass of exclusive offsets, stored coalesced
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int carry = 0;
   for (int64_t base = 0; base < K; base += 1024 * SCAN_SPT) {
@@ -282,9 +284,11 @@ __global__ __launch_bounds__(1024) void mpn_scan_kernel(const int* __restrict__ 
     __syncthreads();
     int run = carry + sh[wave] + x - local;
 #pragma unroll
-    for (int j = 0; j < SCAN_SPT; ++j)
-      if (k0 + j < K) { seg[k0 + j] = run; run += v[j]; }
+    for (int j = 0; j < SCAN_SPT; ++j) { out[threadIdx.x * SCAN_SPT + j] = run; run += v[j]; }
     carry += sh[16];
+    __syncthreads();
+    const int64_t lim = K - base < 1024 * SCAN_SPT ? K - base : 1024 * SCAN_SPT;
+    for (int k = threadIdx.x; k < lim; k += 1024) seg[base + k] = out[k];
     __syncthreads();
   }
   if (threadIdx.x == 0) seg[K] = carry;
@@ -354,16 +358,16 @@ __global__ __launch_bounds__(256) void mpn_scatter_kernel(const int64_t* __restr
   }
 }
 
-// One wave per (type, target) key: order the key's edges by original id (rank by counting).
+// 16 lanes per (type, target) key: order the key's edges by original id (rank by counting).
 __global__ __launch_bounds__(256) void mpn_segsort_kernel(const int64_t* __restrict__ ei, int64_t E, int64_t K,
                                                           const int* __restrict__ seg, const int* __restrict__ perm,
                                                           int* __restrict__ s_src, int* __restrict__ s_dst,
                                                           int* __restrict__ s_orig) {
-  const int lane = threadIdx.x & 63;
-  const int64_t key = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int sub = threadIdx.x & 15;
+  const int64_t key = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
   if (key >= K) return;
   const int s0 = seg[key], n = seg[key + 1] - s0;
-  for (int a = lane; a < n; a += 64) {
+  for (int a = sub; a < n; a += 16) {
     const int v = perm[s0 + a];
     int rank = 0;
     for (int j = 0; j < n; ++j) rank += perm[s0 + j] < v;
@@ -735,6 +739,8 @@ struct EdgeStepArgs {
   float* e_next;
   const float *e1_w, *e2_w, *e2_b, *msg_w, *attn_w;
   const uint16_t *e1_bf, *e2_bf, *msg_bf, *head_bf;   // PREC 1: [hi | lo][out][64] k-permuted bf16
+  const float* upd_w;        // UPD 1: update_mlp.0.weight [64][64 T] (U_t = columns 64 t .. 64 t + 63)
+  const uint16_t* upd_bf;    // UPD 1, PREC 1: [T][hi | lo][64][64]
   float attn_b;
   float* agg;
   pemp_mlp head;
@@ -833,6 +839,10 @@ constexpr int LDS_VEC = 2 * D;
 constexpr int LDS_HEAD = (D + 32) * LDW + D + 32 + 32;
 
 // HEAD: 0 = no edge head, 1 = published head 64 -> 64 -> 32 -> 1 (ReLU, ReLU), 2 = generic pemp_mlp
+// UPD 1 (linear aggregations with an update MLP): each message is multiplied by the type's update
+// block U_t before aggregation, so agg holds U_t · agg[n, t] (the per-type term of update_mlp.0,
+// layers.py:253-258) and the node update is a plain sum over types. The U_t tile sits after the
+// rest of the LDS image.
 //
 // Work split (balanced, no atomics): the edges of source type t (contiguous in the type-major
 // order) are cut into wg_start[t+1]-wg_start[t] equal workgroup ranges, each cut into
@@ -841,13 +851,14 @@ constexpr int LDS_HEAD = (D + 32) * LDW + D + 32 + 32;
 // in 16-edge tiles; a segment that crosses a tile boundary is carried in registers.
 // PREC: 0 = exact fp32 MFMA (v_mfma_f32_16x16x4_f32), 1 = bf16x3 split precision (see gemm_bf3).
 // The LDS image has the same size in both: a 64 x LDW fp32 tile = its bf16 hi and lo tiles.
-template <int AGG, int HEAD, int PREC>
+template <int AGG, int HEAD, int PREC, int UPD>
 __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* wl = sm;                               // [3][64][LDW]: e1_w (e_cur part), e2_w, msg_w[t]
   float* vec = sm + LDS_W;                      // e2_b[64] | attn_w[64]
   float* hw = vec + LDS_VEC;                    // HEAD 1: [64][LDW] L1.w, [32][LDW] L2.w, b1[64], b2[32], w3[32]
   float* hb_l = hw + (D + 32) * LDW;
+  float* uw = hw + (HEAD == 1 ? LDS_HEAD : 0);  // UPD 1: [64][LDW] U_t (or its hi + lo bf16)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
   const int T = a.T;
   const int blk = blockIdx.x;
@@ -892,6 +903,22 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
       if (threadIdx.x < D) hb[threadIdx.x] = a.head.layer[0].b[threadIdx.x];
       else if (threadIdx.x < D + 32) hb[threadIdx.x] = a.head.layer[1].b[threadIdx.x - D];
       else if (threadIdx.x < D + 64) hb[threadIdx.x] = a.head.layer[2].w[threadIdx.x - D - 32];
+    }
+    if (UPD) {
+      if (PREC == 0) {
+        const float* src = a.upd_w + 64 * t;      // row r: upd_w[r][64 t + k]
+        for (int idx = threadIdx.x; idx < D * 16; idx += 64 * EDGE_WAVES) {
+          const int row = idx >> 4, c4 = (idx & 15) * 4;
+          *reinterpret_cast<float4*>(&uw[row * LDW + c4]) = ld4(src + (int64_t)row * 64 * T + c4);
+        }
+      } else {
+        const uint16_t* src = a.upd_bf + (int64_t)t * 2 * D * D;
+        __bf16* uwb = reinterpret_cast<__bf16*>(uw);
+        for (int idx = threadIdx.x; idx < 2 * D * 8; idx += 64 * EDGE_WAVES) {
+          const int row = idx >> 3, c8 = (idx & 7) * 8;
+          *reinterpret_cast<uint4*>(&uwb[row * LDW + c8]) = *reinterpret_cast<const uint4*>(src + row * D + c8);
+        }
+      }
     }
   }
   __syncthreads();
@@ -984,9 +1011,58 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
       av += __shfl_xor(av, 32);
       av += a.attn_b;
     }
+    if (HEAD == 1) {   // fused edge-classification head on e'
+      const float* hb = hb_l + z;
+      float h1[4][4], h2[2][4];
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob) {
+        const float4 bb = ld4(hb + 16 * ob + 4 * g);
+        h1[ob][0] = bb.x; h1[ob][1] = bb.y; h1[ob][2] = bb.z; h1[ob][3] = bb.w;
+      }
+      gemm_p<PREC, 4>(hwz, D, ep, h1);
+      relu_frag<4>(h1);
+#pragma unroll
+      for (int ob = 0; ob < 2; ++ob) {
+        const float4 bb = ld4(hb + D + 16 * ob + 4 * g);
+        h2[ob][0] = bb.x; h2[ob][1] = bb.y; h2[ob][2] = bb.z; h2[ob][3] = bb.w;
+      }
+      gemm_p<PREC, 2>(PREC == 0 ? (const void*)(hwz + D * LDW) : (const void*)(reinterpret_cast<const __bf16*>(hwz) + 2 * D * LDW),
+                      32, h1, h2);
+      relu_frag<2>(h2);
+      float lg = 0.f;
+#pragma unroll
+      for (int ob = 0; ob < 2; ++ob) {
+        const float4 w = ld4(hb + D + 32 + 16 * ob + 4 * g);
+        lg = fmaf(w.x, h2[ob][0], lg); lg = fmaf(w.y, h2[ob][1], lg);
+        lg = fmaf(w.z, h2[ob][2], lg); lg = fmaf(w.w, h2[ob][3], lg);
+      }
+      lg += __shfl_xor(lg, 16);
+      lg += __shfl_xor(lg, 32);
+      if (valid && g == 0) a.edge_logits[a.s_orig[p]] = lg + a.head.layer[2].b[0];
+    } else if (HEAD == 2) {
+      float h1[4][4], h2[4][4];                  // mlp_frag overwrites its input: work on a copy of e'
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h1[ob][r] = ep[ob][r];
+      mlp_frag<4>(a.head, h1, h2);
+      if (valid && g == 0) a.edge_logits[a.s_orig[p]] = h1[0][0];
+    }
     // message: m = ReLU(P_t[dst] + W_t_e · e')
     gemm_p<PREC, 4>(WM, D, ep, m);
     relu_frag<4>(m);
+    if (UPD) {                                    // m <- U_t · m (no bias: added once per node)
+      float u[4][4];
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) u[ob][r] = 0.0f;
+      gemm_p<PREC, 4>(uw + z, D, m, u);
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) m[ob][r] = u[ob][r];
+    }
 
     // ---- segmented reduction of the tile, carry in / out ----
     const int seg = valid ? dst : -1 - c;        // padding lanes: singleton chunks, never written
@@ -1051,103 +1127,293 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
       }
     }
 
-    if (HEAD == 1) {   // fused edge-classification head on e'
-      const float* hb = hb_l + z;
-      float h1[4][4], h2[2][4];
-#pragma unroll
-      for (int ob = 0; ob < 4; ++ob) {
-        const float4 bb = ld4(hb + 16 * ob + 4 * g);
-        h1[ob][0] = bb.x; h1[ob][1] = bb.y; h1[ob][2] = bb.z; h1[ob][3] = bb.w;
+  }
+}
+
+// Node update (separate launch, the whole edge pass must have finished): one workgroup per
+// (16-node tile, 16-output block), one wave per type (wave w: types w and w + 16, T <= 17);
+// fixed-order reduction over waves.
+//   x_new[n] = ReLU(b + sum_t U_t · agg[n, t])   (layers.py:253-258; empty segments read as 0)
+//   without an update MLP: x_new[n] = agg[n, 0]  (MPLayer, layers.py:32-86)
+// Written to X[:, 64:128]. Every load of a wave is issued before its first MFMA.
+struct NodeUpdateArgs {
+  const float* agg;
+  const int* seg;
+  int T;
+  int64_t N;
+  const float *upd_w, *upd_b;
+  float* X;
+};
+
+constexpr int UPD_WAVES = 16;
+
+__global__ __launch_bounds__(64 * UPD_WAVES) void node_update_kernel(NodeUpdateArgs a) {
+  __shared__ __attribute__((aligned(16))) float red[UPD_WAVES][16 * 17];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
+  const int64_t n0 = (int64_t)blockIdx.x * 16, N = a.N;
+  const int ob = blockIdx.y, T = a.T;
+  if (!a.upd_w) {   // x_new = agg[n, 0] (T == 1), this block's 16 features
+    if (threadIdx.x < 256) {
+      const int r = threadIdx.x >> 4, f = threadIdx.x & 15;
+      const int64_t n = n0 + r;
+      if (n < N) {
+        const float v = a.seg[n + 1] > a.seg[n] ? a.agg[n * D + 16 * ob + f] : 0.0f;
+        a.X[n * 128 + 64 + 16 * ob + f] = v;
       }
-      gemm_p<PREC, 4>(hwz, D, ep, h1);
-      relu_frag<4>(h1);
+    }
+    return;
+  }
+  const int64_t n = n0 + c, nc = n < N ? n : N - 1;   // clamped: every load below is unconditional
+  const int ldu = 64 * T;
+  const float* wrow = a.upd_w + (int64_t)(16 * ob + c) * ldu + 4 * g;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (wave < T) {
+    const int tt[2] = {wave, min(wave + UPD_WAVES, T - 1)};
+    float4 xv[2][4], wv[2][4];
+    int s0[2], s1[2];
 #pragma unroll
-      for (int ob = 0; ob < 2; ++ob) {
-        const float4 bb = ld4(hb + D + 16 * ob + 4 * g);
-        h2[ob][0] = bb.x; h2[ob][1] = bb.y; h2[ob][2] = bb.z; h2[ob][3] = bb.w;
-      }
-      gemm_p<PREC, 2>(PREC == 0 ? (const void*)(hwz + D * LDW) : (const void*)(reinterpret_cast<const __bf16*>(hwz) + 2 * D * LDW),
-                      32, h1, h2);
-      relu_frag<2>(h2);
-      float lg = 0.f;
+    for (int k = 0; k < 2; ++k) {
 #pragma unroll
-      for (int ob = 0; ob < 2; ++ob) {
-        const float4 w = ld4(hb + D + 32 + 16 * ob + 4 * g);
-        lg = fmaf(w.x, h2[ob][0], lg); lg = fmaf(w.y, h2[ob][1], lg);
-        lg = fmaf(w.z, h2[ob][2], lg); lg = fmaf(w.w, h2[ob][3], lg);
+      for (int mb = 0; mb < 4; ++mb) {
+        xv[k][mb] = ld4(a.agg + (nc * T + tt[k]) * D + 16 * mb + 4 * g);
+        wv[k][mb] = ld4(wrow + 64 * tt[k] + 16 * mb);
       }
-      lg += __shfl_xor(lg, 16);
-      lg += __shfl_xor(lg, 32);
-      if (valid && g == 0) a.edge_logits[a.s_orig[p]] = lg + a.head.layer[2].b[0];
-    } else if (HEAD == 2) {
-      float h2[4][4];
-      mlp_frag<4>(a.head, ep, h2);
-      if (valid && g == 0) a.edge_logits[a.s_orig[p]] = ep[0][0];
+      s0[k] = a.seg[tt[k] * N + nc];
+      s1[k] = a.seg[tt[k] * N + nc + 1];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      // an empty (n, t) segment was never written by the edge pass; the second slot is live only
+      // for wave + 16 < T
+      const int keep = (n < N && s1[k] > s0[k] && (k == 0 || wave + UPD_WAVES < T)) ? -1 : 0;
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) {
+        acc = mfma4(wv[k][mb].x, __int_as_float(__float_as_int(xv[k][mb].x) & keep), acc);
+        acc = mfma4(wv[k][mb].y, __int_as_float(__float_as_int(xv[k][mb].y) & keep), acc);
+        acc = mfma4(wv[k][mb].z, __int_as_float(__float_as_int(xv[k][mb].z) & keep), acc);
+        acc = mfma4(wv[k][mb].w, __int_as_float(__float_as_int(xv[k][mb].w) & keep), acc);
+      }
+    }
+  }
+  // lane (c, g) holds outputs 16 ob + 4 g + r of node c
+  *reinterpret_cast<float4*>(&red[wave][c * 17 + 4 * g]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  __syncthreads();
+  if (threadIdx.x < 256) {
+    const int r = threadIdx.x >> 4, f = threadIdx.x & 15;
+    float sum = 0.f;
+#pragma unroll
+    for (int w = 0; w < UPD_WAVES; ++w) sum += red[w][r * 17 + f];
+    if (n0 + r < N) a.X[(n0 + r) * 128 + 64 + 16 * ob + f] = fmaxf(sum + a.upd_b[16 * ob + f], 0.0f);
+  }
+}
+
+// ---- small MLPs staged in LDS (node embedding, node/class heads) ----
+// Layer l of a pemp_mlp: weights [16 OB][16 KB] (fold.py zero-pads to 16) -> LDS rows of stride
+// lds_stride(16 KB), then the bias (16 OB floats).
+__host__ __device__ inline int mlp_lds_floats(const pemp_mlp& m) {
+  int n = 0;
+  for (int l = 0; l < m.n_layers; ++l) {
+    const int KB = (m.layer[l].in_dim + 15) >> 4, OB = (m.layer[l].out_dim + 15) >> 4;
+    n += 16 * OB * lds_stride(16 * KB) + 16 * OB;
+  }
+  return n;
+}
+
+// all threads of the block: issue 8 float4 loads per thread, then 8 LDS stores
+__device__ __forceinline__ void stage_rows(float* __restrict__ lds, int ld, const float* __restrict__ src, int rows,
+                                           int cols) {
+  const int q = cols >> 2, total = rows * q;
+  for (int base = threadIdx.x; base < total; base += 8 * blockDim.x) {
+    float4 t[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t[k] = ld4(src + 4 * min(base + k * (int)blockDim.x, total - 1));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int idx = base + k * (int)blockDim.x;
+      if (idx < total) {
+        const int r = idx / q, c4 = (idx - r * q) * 4;
+        *reinterpret_cast<float4*>(&lds[r * ld + c4]) = t[k];
+      }
     }
   }
 }
 
-// Node step, 16 nodes per workgroup (NODE_WAVES waves; NODE_SPLIT workgroups share the table
-// columns), fusing what follows an edge pass:
-//   (a) x_new = ReLU(b + sum_t U_t · agg[n, t]) (fixed-order reduction over types; agg[n, 0]
-//       when there is no update MLP; empty segments read as 0)  -> X[:, 64:128]
-//   (b) the next iteration's node table NT = [x0 | x] · pre_w^T + pre_b
-//   (c) the node / class heads on x (published widths <= 64), written to one or two slots
-struct NodeStepArgs {
-  const float* x_in;     // embed mode: node inputs [N][in_ld] -> X = [emb | emb] (NodeClassificationMPNSimple.py:67-69)
+// Stage up to three MLPs back to back (the layout mlp_lds_frag / mlp_lds_floats assume) with ONE
+// batched pass: every thread issues 8 float4 loads before its first LDS store, over the
+// concatenation of all weight and bias segments (weights row-major [16 OB][16 KB], biases one row).
+// The segment table is built on the host and passed by value (kernel arguments, scalar loads).
+constexpr int STAGE_MAXSEG = 24;
+struct StagePlan {
+  const float* src[STAGE_MAXSEG];
+  int q[STAGE_MAXSEG], ld[STAGE_MAXSEG], dst[STAGE_MAXSEG], cum[STAGE_MAXSEG];
+  int n, total;
+};
+
+static StagePlan stage_plan(const pemp_mlp* m0, const pemp_mlp* m1 = nullptr, const pemp_mlp* m2 = nullptr) {
+  StagePlan p{};
+  int off = 0;
+  for (const pemp_mlp* m : {m0, m1, m2}) {
+    if (!m) continue;
+    for (int l = 0; l < m->n_layers; ++l) {
+      const pemp_layer& L = m->layer[l];
+      const int KB = (L.in_dim + 15) >> 4, OB = (L.out_dim + 15) >> 4, ld = lds_stride(16 * KB);
+      p.src[p.n] = L.w; p.q[p.n] = 4 * KB; p.ld[p.n] = ld; p.dst[p.n] = off; p.cum[p.n] = p.total; ++p.n;
+      p.total += 16 * OB * 4 * KB;
+      off += 16 * OB * ld;
+      p.src[p.n] = L.b; p.q[p.n] = 4 * OB; p.ld[p.n] = 0; p.dst[p.n] = off; p.cum[p.n] = p.total; ++p.n;
+      p.total += 4 * OB;
+      off += 16 * OB;
+    }
+  }
+  return p;
+}
+
+// one element (float4) of the LDS image described by a plan: source address and image offset
+__device__ inline void plan_element(const StagePlan& p, int idx, const float** src, int* dst) {
+  const float* sp = p.src[0];
+  int q = p.q[0], ld = p.ld[0], d0 = p.dst[0], cum = 0;
+  for (int j = 1; j < p.n; ++j)
+    if (idx >= p.cum[j]) { sp = p.src[j]; q = p.q[j]; ld = p.ld[j]; d0 = p.dst[j]; cum = p.cum[j]; }
+  const int local = idx - cum, r = local / q;
+  *src = sp + 4 * local;
+  *dst = d0 + r * ld + 4 * (local - r * q);
+}
+
+// First kernel of a forward: zero the counters, and build the LDS image of the node-side MLPs
+// (node embedding, node head, class head) in the workspace, so the node kernels stage it with a
+// flat copy.
+__global__ __launch_bounds__(256) void zero_words_kernel(int* __restrict__ p, int64_t n, StagePlan plan,
+                                                         float* __restrict__ img) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, gs = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = gid; i < n; i += gs) p[i] = 0;
+  for (int64_t i = gid; i < plan.total; i += gs) {
+    const float* src;
+    int dst;
+    plan_element(plan, (int)i, &src, &dst);
+    *reinterpret_cast<float4*>(img + dst) = ld4(src);
+  }
+}
+
+// flat copy of `n` floats (multiple of 4) from global to LDS, 8 float4 loads in flight per thread
+__device__ inline void copy_to_lds(float* __restrict__ lds, const float* __restrict__ src, int n) {
+  const int n4 = n >> 2, bs = blockDim.x;
+  for (int base = threadIdx.x; base < n4; base += 8 * bs) {
+    float4 t[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t[k] = ld4(src + 4 * min(base + k * bs, n4 - 1));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (base + k * bs < n4) *reinterpret_cast<float4*>(&lds[4 * (base + k * bs)]) = t[k];
+  }
+}
+
+// whole staged MLP on one wave's fragments (widths <= 64); result in `a`
+__device__ inline void mlp_lds_frag(const float* lds, const pemp_mlp& m, float (&a)[4][4]) {
+  float b[4][4];
+  int off = 0;
+  for (int l = 0; l < m.n_layers; ++l) {
+    const pemp_layer& L = m.layer[l];
+    const int KB = (L.in_dim + 15) >> 4, OB = (L.out_dim + 15) >> 4, ld = lds_stride(16 * KB);
+    layer_lds(lds + off, ld, lds + off + 16 * OB * ld, KB, OB, L.relu, a, b);
+    off += 16 * OB * ld + 16 * OB;
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a[x][r] = b[x][r];
+  }
+}
+
+// Node rows: one workgroup per 16-node tile (256 threads), producing x = X[:, 64:128] by mode and
+// optionally the node / class heads on it (published widths <= 64, weights staged in LDS).
+//   ROWS_EMBED: node embedding MLP -> X = [emb | emb] (NodeClassificationMPNSimple.py:67-69)
+//   ROWS_SUM:   x_new = ReLU(b + sum_t y[n, t]), y[n, t] = U_t · agg[n, t] written by the edge pass
+//               (UPD 1); empty (n, t) segments were never written and read as 0 (layers.py:253-258)
+//   ROWS_COPY:  x_new = agg[n, 0] (MPLayer without an update MLP; empty segment -> 0)
+//   ROWS_NONE:  x already in X (node_update_kernel ran): heads only
+// Dynamic LDS (floats): xs [16][RS] | embed: act [2][16][RS] + staged embedding | heads.
+enum { ROWS_NONE = 0, ROWS_EMBED = 1, ROWS_SUM = 2, ROWS_COPY = 3 };
+
+struct NodeRowsArgs {
+  int mode;
+  const float* x_in;     // ROWS_EMBED: node inputs [N][in_ld]
   int in_ld;
   pemp_mlp emb;
-  const float* agg;
+  const float* agg;      // [N][T][64]
   const int* seg;
-  int T, do_update;
+  int T;
+  const float* upd_b;
   int64_t N;
-  const float *upd_w, *upd_b;
   float* X;
-  const float *pre_w, *pre_b;
-  int NO;
-  float* NT;
   pemp_mlp node_head, class_head;
   int J;
   float *node_out, *node_out2, *class_out, *class_out2;
+  const float* img;      // LDS image [emb | node head | class head] built by zero_words_kernel
+  int head_off, head_floats;   // heads block: offset (= embedding image size, or 0) and size
 };
 
-#ifndef PEMP_NODE_WAVES
-#define PEMP_NODE_WAVES 16
-#endif
-#ifndef PEMP_NODE_SPLIT
-#define PEMP_NODE_SPLIT 2
-#endif
-constexpr int NODE_WAVES = PEMP_NODE_WAVES, NODE_SPLIT = PEMP_NODE_SPLIT;   // waves per node-step WG; table split
+static int max_layer_floats(const pemp_mlp& m) {
+  int mx = 0;
+  for (int l = 0; l < m.n_layers; ++l) {
+    const int KB = (m.layer[l].in_dim + 15) >> 4, OB = (m.layer[l].out_dim + 15) >> 4;
+    mx = std::max(mx, 16 * OB * lds_stride(16 * KB) + 16 * OB);
+  }
+  return mx;
+}
 
-__global__ __launch_bounds__(64 * NODE_WAVES) void node_step_kernel(NodeStepArgs a) {
-  __shared__ __attribute__((aligned(16))) float red[NODE_WAVES][16 * 68];
-  __shared__ __attribute__((aligned(16))) float xs[16 * RS];
+static size_t node_rows_lds_bytes(const NodeRowsArgs& a) {
+  int region = 0;
+  if (a.mode == ROWS_EMBED) region = max_layer_floats(a.emb);
+  if (a.node_out) region = std::max(region, a.head_floats);
+  return (size_t)(3 * 16 * RS + region) * sizeof(float);
+}
+
+__global__ __launch_bounds__(256) void node_rows_kernel(NodeRowsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* xs = lds;
+  float* act0 = lds + 16 * RS;
+  float* act1 = act0 + 16 * RS;
+  float* wreg = act1 + 16 * RS;                  // one embedding layer at a time, then the heads
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
   const int64_t n0 = (int64_t)blockIdx.x * 16, N = a.N;
-  const int T = a.T;
-  const bool owner = blockIdx.y == 0;           // writes X and the heads
-  if (a.x_in) {
-    // node embedding MLP on the block's 16 rows (waves split each layer's output blocks), the
-    // result is both halves of x = [x_init | x_cur]
-    float* act0 = &red[0][0];
-    float* act1 = act0 + 16 * RS;
+  const bool heads = a.node_out != nullptr;
+  const int r = threadIdx.x >> 4, q = threadIdx.x & 15;   // row r of the tile, features 4 q .. 4 q + 3
+  const int64_t n = n0 + r, nc = n < N ? n : N - 1;
+  if (a.mode == ROWS_EMBED) {
     const int K0 = a.emb.layer[0].in_dim, KP = (K0 + 15) & ~15;
-    for (int idx = threadIdx.x; idx < 16 * KP; idx += 64 * NODE_WAVES) {
-      const int r = idx / KP, k = idx - r * KP;
-      act0[r * RS + k] = (n0 + r < N && k < K0) ? a.x_in[(n0 + r) * a.in_ld + k] : 0.0f;
+    for (int base = threadIdx.x; base < 16 * KP; base += 8 * 256) {   // 16 x K0 inputs, 8 loads in flight
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int idx = base + 256 * k, rr = idx / KP, kk = idx - rr * KP;
+        v[k] = (idx < 16 * KP && kk < K0) ? a.x_in[min(n0 + rr, N - 1) * a.in_ld + kk] : 0.0f;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int idx = base + 256 * k, rr = idx / KP, kk = idx - rr * KP;
+        if (idx < 16 * KP) act0[rr * RS + kk] = v[k];
+      }
     }
-    __syncthreads();
-    int cur = 0;
+    int cur = 0, off = 0;
     for (int l = 0; l < a.emb.n_layers; ++l) {
       const pemp_layer& L = a.emb.layer[l];
-      const int KB = (L.in_dim + 15) >> 4, OB = (L.out_dim + 15) >> 4, ldw = KB * 16;
+      const int KB = (L.in_dim + 15) >> 4, OB = (L.out_dim + 15) >> 4, ld = lds_stride(16 * KB);
+      const int lf = 16 * OB * ld + 16 * OB;
+      if (l > 0) __syncthreads();                // the previous layer is done with wreg
+      copy_to_lds(wreg, a.img + off, lf);
+      off += lf;
+      __syncthreads();
+      const float* Wl = wreg;
+      const float* bl = Wl + 16 * OB * ld;
       const float* src = cur ? act1 : act0;
       float* dst = cur ? act0 : act1;
-      for (int ob = wave; ob < OB; ob += NODE_WAVES) {
-        const float4 bb = ld4(L.b + 16 * ob + 4 * g);
+      for (int ob = wave; ob < OB; ob += 4) {
+        const float4 bb = ld4(bl + 16 * ob + 4 * g);
         f32x4 acc = {bb.x, bb.y, bb.z, bb.w};
         for (int mb = 0; mb < KB; ++mb) {
-          const float4 w = ld4(L.w + (16 * ob + c) * ldw + 16 * mb + 4 * g);
+          const float4 w = ld4(Wl + (16 * ob + c) * ld + 16 * mb + 4 * g);
           const float4 xv = ld4(&src[c * RS + 16 * mb + 4 * g]);
           acc = mfma4(w.x, xv.x, acc);
           acc = mfma4(w.y, xv.y, acc);
@@ -1156,123 +1422,172 @@ __global__ __launch_bounds__(64 * NODE_WAVES) void node_step_kernel(NodeStepArgs
         }
         if (L.relu) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[r] = fmaxf(acc[r], 0.0f);
+          for (int k = 0; k < 4; ++k) acc[k] = fmaxf(acc[k], 0.0f);
         }
         st4(&dst[c * RS + 16 * ob + 4 * g], acc[0], acc[1], acc[2], acc[3]);
       }
-      __syncthreads();
       cur ^= 1;
     }
+    __syncthreads();
+    if (heads) copy_to_lds(wreg, a.img + a.head_off, a.head_floats);
     const float* res = cur ? act1 : act0;
-    for (int idx = threadIdx.x; idx < 16 * D; idx += 64 * NODE_WAVES) {
-      const int r = idx >> 6, f = idx & 63;
-      const float v = res[r * RS + f];
-      xs[r * RS + f] = v;
-      xs[r * RS + 64 + f] = v;
-      if (owner && n0 + r < N) { a.X[(n0 + r) * 128 + f] = v; a.X[(n0 + r) * 128 + 64 + f] = v; }
+    const float4 v = ld4(&res[r * RS + 4 * q]);
+    *reinterpret_cast<float4*>(&xs[r * RS + 64 + 4 * q]) = v;
+    if (n < N) {
+      *reinterpret_cast<float4*>(a.X + n * 128 + 4 * q) = v;
+      *reinterpret_cast<float4*>(a.X + n * 128 + 64 + 4 * q) = v;
     }
-  }
-  // x0 half (and x when there is no update)
-  for (int idx = threadIdx.x; idx < 16 * 32 && !a.x_in; idx += 64 * NODE_WAVES) {
-    const int r = idx >> 5, k4 = (idx & 31) * 4;
-    if (a.do_update && k4 >= 64) continue;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (n0 + r < N) v = ld4(a.X + (n0 + r) * 128 + k4);
-    *reinterpret_cast<float4*>(&xs[r * RS + k4]) = v;
-  }
-  if (a.do_update) {
-    if (!a.upd_w) {
-      for (int idx = threadIdx.x; idx < 16 * D; idx += 64 * NODE_WAVES) {
-        const int r = idx >> 6, f = idx & 63;
-        const int64_t n = n0 + r;
-        const float v = (n < N && a.seg[n + 1] > a.seg[n]) ? a.agg[n * D + f] : 0.0f;
-        xs[r * RS + 64 + f] = v;
-        if (n < N && owner) a.X[n * 128 + 64 + f] = v;
+  } else {
+    if (heads) copy_to_lds(wreg, a.img + a.head_off, a.head_floats);
+    float4 v;
+    if (a.mode == ROWS_SUM) {
+      // all T rows and segment bounds in flight together; fixed summation order t = 0 .. T-1
+      float4 y[MAXT];
+      int s0[MAXT], s1[MAXT];
+      const int T = a.T;
+#pragma unroll
+      for (int t = 0; t < MAXT; ++t) {
+        const int tc = min(t, T - 1);
+        y[t] = ld4(a.agg + (nc * T + tc) * D + 4 * q);
+        s0[t] = a.seg[tc * N + nc];
+        s1[t] = a.seg[tc * N + nc + 1];
       }
+      v = ld4(a.upd_b + 4 * q);
+#pragma unroll
+      for (int t = 0; t < MAXT; ++t) {
+        if (t < T && s1[t] > s0[t]) { v.x += y[t].x; v.y += y[t].y; v.z += y[t].z; v.w += y[t].w; }
+      }
+      v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+    } else if (a.mode == ROWS_COPY) {
+      const float4 y = ld4(a.agg + nc * D + 4 * q);
+      v = a.seg[nc + 1] > a.seg[nc] ? y : make_float4(0.f, 0.f, 0.f, 0.f);
     } else {
-      const int64_t n = n0 + c;
-      float acc[4][4];
-#pragma unroll
-      for (int ob = 0; ob < 4; ++ob)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[ob][r] = 0.f;
-      const int64_t nc = n < N ? n : N - 1;          // clamped: every load below is unconditional
-      for (int t = wave; t < T; t += NODE_WAVES) {
-        // agg rows and the segment bounds are loaded together; an empty (n, t) segment was never
-        // written by the edge pass and reads as 0 (torch_scatter), applied with a bit mask so the
-        // loads are not sunk behind the segment test
-        float4 xv[4];
-#pragma unroll
-        for (int mb = 0; mb < 4; ++mb) xv[mb] = ld4(a.agg + (nc * T + t) * D + 16 * mb + 4 * g);
-        const int s0 = a.seg[t * N + nc], s1 = a.seg[t * N + nc + 1];
-        const int keep = (n < N && s1 > s0) ? -1 : 0;
-        float in[4][4];
-#pragma unroll
-        for (int mb = 0; mb < 4; ++mb) {
-          in[mb][0] = __int_as_float(__float_as_int(xv[mb].x) & keep);
-          in[mb][1] = __int_as_float(__float_as_int(xv[mb].y) & keep);
-          in[mb][2] = __int_as_float(__float_as_int(xv[mb].z) & keep);
-          in[mb][3] = __int_as_float(__float_as_int(xv[mb].w) & keep);
-        }
-        gemm_frag<4, 4>(a.upd_w + 64 * t, 64 * T, in, acc);
-      }
-#pragma unroll
-      for (int ob = 0; ob < 4; ++ob)
-        st4(&red[wave][c * 68 + 16 * ob + 4 * g], acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]);
-      __syncthreads();
-      for (int idx = threadIdx.x; idx < 16 * D; idx += 64 * NODE_WAVES) {
-        const int r = idx >> 6, f = idx & 63;
-        float sum = 0.f;
-#pragma unroll
-        for (int w = 0; w < NODE_WAVES; ++w) sum += red[w][r * 68 + f];
-        const float v = fmaxf(sum + a.upd_b[f], 0.0f);
-        xs[r * RS + 64 + f] = v;
-        if (n0 + r < N && owner) a.X[(n0 + r) * 128 + 64 + f] = v;
-      }
+      v = ld4(a.X + nc * 128 + 64 + 4 * q);
     }
+    *reinterpret_cast<float4*>(&xs[r * RS + 64 + 4 * q]) = v;
+    if (a.mode != ROWS_NONE && n < N) *reinterpret_cast<float4*>(a.X + n * 128 + 64 + 4 * q) = v;
   }
+  if (!heads) return;
   __syncthreads();
-  if (a.NT) {   // next node table: lane holds NT[row c][16 ob + 4 g + r]
-    for (int ob = blockIdx.y * NODE_WAVES + wave; 16 * ob < a.NO; ob += NODE_WAVES * NODE_SPLIT) {
-      const float4 bb = ld4(a.pre_b + 16 * ob + 4 * g);
-      f32x4 acc = {bb.x, bb.y, bb.z, bb.w};
-#pragma unroll
-      for (int mb = 0; mb < 8; ++mb) {
-        const float4 w = ld4(a.pre_w + (int64_t)(16 * ob + c) * 128 + 16 * mb + 4 * g);
-        const float4 x = ld4(&xs[c * RS + 16 * mb + 4 * g]);
-        acc = mfma4(w.x, x.x, acc);
-        acc = mfma4(w.y, x.y, acc);
-        acc = mfma4(w.z, x.z, acc);
-        acc = mfma4(w.w, x.w, acc);
-      }
-      if (n0 + c < N) st4(a.NT + (n0 + c) * a.NO + 16 * ob + 4 * g, acc[0], acc[1], acc[2], acc[3]);
-    }
-  }
-  if (a.node_out && owner && wave < 2) {   // wave 0: node head, wave 1: class head
-    float in[4][4], tmp[4][4];
+  if (wave < 2) {   // wave 0: node head, wave 1: class head
+    float in[4][4];
 #pragma unroll
     for (int mb = 0; mb < 4; ++mb) {
       const float4 x = ld4(&xs[c * RS + 64 + 16 * mb + 4 * g]);
       in[mb][0] = x.x; in[mb][1] = x.y; in[mb][2] = x.z; in[mb][3] = x.w;
     }
     const pemp_mlp& m = wave == 0 ? a.node_head : a.class_head;
-    mlp_frag<4>(m, in, tmp);
+    mlp_lds_frag(wave == 0 ? wreg : wreg + mlp_lds_floats(a.node_head), m, in);
     const int od = wave == 0 ? 1 : a.J;
     float* o1 = wave == 0 ? a.node_out : a.class_out;
     float* o2 = wave == 0 ? a.node_out2 : a.class_out2;
-    const int64_t n = n0 + c;
-    if (n < N) {
+    const int64_t nn = n0 + c;
+    if (nn < N) {
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int f = 16 * ob + 4 * g + r;
+        for (int k = 0; k < 4; ++k) {
+          const int f = 16 * ob + 4 * g + k;
           if (f < od) {
-            o1[n * od + f] = in[ob][r];
-            if (o2) o2[n * od + f] = in[ob][r];
+            o1[nn * od + f] = in[ob][k];
+            if (o2) o2[nn * od + f] = in[ob][k];
           }
         }
     }
+  }
+}
+
+// Node table NT = [x0 | x] · pre_w^T + pre_b for the next edge pass. 1-D grid of
+// (64-node chunk, 64-column group) workgroups, chunk-major; each of the 4 waves owns one 16-column
+// block (weight fragment in registers, loaded before the barrier) and walks the chunk's 4 node
+// tiles from LDS. HBM/L2 traffic ~ X · groups + pre_w · chunks (~24 MB at C3, vs ~55 MB tile-major).
+// PREC 1: bf16x3 (pre_bf pack, K = 128 = 4 slot blocks).
+struct NodeTableArgs {
+  const float* X;
+  int64_t N;
+  const float *pre_w, *pre_b;
+  const uint16_t* pre_bf;
+  int NO, groups;
+  float* NT;
+};
+
+constexpr int TBL_TILES = 4;
+
+template <int PREC>
+__global__ __launch_bounds__(256) void node_table_kernel(NodeTableArgs a) {
+  __shared__ __attribute__((aligned(16))) float xs[16 * TBL_TILES * RS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
+  const int chunk = blockIdx.x / a.groups, grp = blockIdx.x - chunk * a.groups;
+  const int64_t n0 = (int64_t)chunk * 16 * TBL_TILES, N = a.N;
+  const int nob = a.NO / 16, ob = grp * 4 + wave, obc = min(ob, nob - 1);
+  // this wave's weight fragment (rows 16 ob + c), issued first
+  float4 w[8];
+  bf16x8_t wh[4], wlo[4];
+  if (PREC == 0) {
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb) w[mb] = ld4(a.pre_w + (int64_t)(16 * obc + c) * 128 + 16 * mb + 4 * g);
+  } else {
+    const __bf16* Wb = reinterpret_cast<const __bf16*>(a.pre_bf);
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      const int64_t o = (int64_t)(16 * obc + c) * 128 + 32 * kb + 8 * g;
+      wh[kb] = *reinterpret_cast<const bf16x8_t*>(Wb + o);
+      wlo[kb] = *reinterpret_cast<const bf16x8_t*>(Wb + (int64_t)a.NO * 128 + o);
+    }
+  }
+  const float4 bb = ld4(a.pre_b + 16 * obc + 4 * g);
+  // X chunk -> LDS: 64 rows x 32 float4, 8 per thread
+  {
+    float4 t[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int idx = threadIdx.x + 256 * k, row = idx >> 5, c4 = (idx & 31) * 4;
+      const int64_t nn = min(n0 + row, N - 1);
+      t[k] = ld4(a.X + nn * 128 + c4);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int idx = threadIdx.x + 256 * k, row = idx >> 5, c4 = (idx & 31) * 4;
+      *reinterpret_cast<float4*>(&xs[row * RS + c4]) = t[k];
+    }
+  }
+  __syncthreads();
+  if (ob >= nob) return;
+#pragma unroll
+  for (int tile = 0; tile < TBL_TILES; ++tile) {
+    const int64_t nn = n0 + 16 * tile + c;
+    if (n0 + 16 * tile >= N) break;               // uniform
+    float x[8][4];
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb) {
+      const float4 v = ld4(&xs[(16 * tile + c) * RS + 16 * mb + 4 * g]);
+      x[mb][0] = v.x; x[mb][1] = v.y; x[mb][2] = v.z; x[mb][3] = v.w;
+    }
+    f32x4 acc = {bb.x, bb.y, bb.z, bb.w};
+    if (PREC == 0) {
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb) {
+        acc = mfma4(w[mb].x, x[mb][0], acc);
+        acc = mfma4(w[mb].y, x[mb][1], acc);
+        acc = mfma4(w[mb].z, x[mb][2], acc);
+        acc = mfma4(w[mb].w, x[mb][3], acc);
+      }
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float (&xh)[4][4] = *reinterpret_cast<const float (*)[4][4]>(&x[4 * h][0]);
+        bf16x8_t hi[2], lo[2];
+        split_bf16(xh, hi, lo);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlo[2 * h + kb], hi[kb], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[2 * h + kb], lo[kb], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[2 * h + kb], hi[kb], acc, 0, 0, 0);
+        }
+      }
+    }
+    if (nn < N) st4(a.NT + nn * a.NO + 16 * ob + 4 * g, acc[0], acc[1], acc[2], acc[3]);
   }
 }
 
@@ -1287,22 +1602,29 @@ static bool published_head(const pemp_mlp& m) {
          m.layer[2].out_dim == 1 && !m.layer[2].relu;
 }
 
-template <int AGG, int PREC>
+template <int AGG, int PREC, int UPD>
 static void launch_edge_step_p(const EdgeStepArgs& a, bool head, int grid, hipStream_t st) {
-  const size_t lds = (size_t)(LDS_W + LDS_VEC) * sizeof(float);
+  const size_t lds = (size_t)(LDS_W + LDS_VEC + (UPD ? D * LDW : 0)) * sizeof(float);
   const dim3 blk(64 * EDGE_WAVES);
   if (!head)
-    hipLaunchKernelGGL((edge_step_kernel<AGG, 0, PREC>), dim3(grid), blk, lds, st, a);
+    hipLaunchKernelGGL((edge_step_kernel<AGG, 0, PREC, UPD>), dim3(grid), blk, lds, st, a);
   else if (published_head(a.head) && (PREC == 0 || a.head_bf))
-    hipLaunchKernelGGL((edge_step_kernel<AGG, 1, PREC>), dim3(grid), blk, lds + LDS_HEAD * sizeof(float), st, a);
+    hipLaunchKernelGGL((edge_step_kernel<AGG, 1, PREC, UPD>), dim3(grid), blk, lds + LDS_HEAD * sizeof(float), st, a);
   else
-    hipLaunchKernelGGL((edge_step_kernel<AGG, 2, PREC>), dim3(grid), blk, lds, st, a);
+    hipLaunchKernelGGL((edge_step_kernel<AGG, 2, PREC, UPD>), dim3(grid), blk, lds, st, a);
 }
 
+// UPD is instantiated for the linear aggregations only (U · max(m) != max(U · m))
 template <int AGG>
-static void launch_edge_step(const EdgeStepArgs& a, bool head, int grid, int prec, hipStream_t st) {
-  if (prec == PEMP_PREC_BF16X3) launch_edge_step_p<AGG, 1>(a, head, grid, st);
-  else launch_edge_step_p<AGG, 0>(a, head, grid, st);
+static void launch_edge_step(const EdgeStepArgs& a, bool head, int grid, int prec, bool upd, hipStream_t st) {
+  constexpr int U = AGG == PEMP_AGGR_MAX ? 0 : 1;
+  if (prec == PEMP_PREC_BF16X3) {
+    if (U && upd) launch_edge_step_p<AGG, 1, U>(a, head, grid, st);
+    else launch_edge_step_p<AGG, 1, 0>(a, head, grid, st);
+  } else {
+    if (U && upd) launch_edge_step_p<AGG, 0, U>(a, head, grid, st);
+    else launch_edge_step_p<AGG, 0, 0>(a, head, grid, st);
+  }
 }
 
 static int rows_mlp(const char* label, const pemp_mlp& m, const float* in, int64_t ld_in, int64_t M, float* out,
@@ -1384,11 +1706,16 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
   const int64_t tstride = desc->types_stride > 0 ? desc->types_stride : 1;   // node_types may be a strided view
   const int64_t K = (int64_t)T * N;
 
+  const bool fused_heads_ = mlp_ok(w->node_head, 64, 64) && mlp_ok(w->class_head, 64, 64);
+  const bool fused_embed_ = mlp_ok(w->node_emb, 128, 128);   // one layer at a time in LDS (<= 70 KB)
   // ---- prepare: type-major order ----
   {
   ProfScope prof("mpn_prepare", st);
-  hipLaunchKernelGGL(zero_words_kernel, dim3((unsigned)std::min<int64_t>((K + 64 + 255) / 256, 1024)), dim3(256), 0,
-                     st, ws.err, K + 65);
+  // LDS image of the node-side MLPs: [emb | node head | class head] (layouts of mlp_lds_floats)
+  StagePlan plan = stage_plan(fused_embed_ ? &w->node_emb : nullptr, fused_heads_ ? &w->node_head : nullptr,
+                              fused_heads_ ? &w->class_head : nullptr);
+  hipLaunchKernelGGL(zero_words_kernel, dim3((unsigned)std::min<int64_t>((K + 64 + 255) / 256 + 8, 1024)), dim3(256), 0,
+                     st, ws.err, K + 65, plan, ws.img);
   PEMP_LAUNCH_CHECK();
   if (E > 0) {
     hipLaunchKernelGGL(mpn_count_kernel, dim3(grid1d(E, 256)), dim3(256), 0, st, edge_index, node_types, tstride, N, E, T,
@@ -1402,7 +1729,7 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
     hipLaunchKernelGGL(mpn_scatter_kernel, dim3(grid1d(E, 256)), dim3(256), 0, st, edge_index, node_types, tstride, N, E, T,
                        ws.seg, ws.cnt, ws.perm);
     PEMP_LAUNCH_CHECK();
-    hipLaunchKernelGGL(mpn_segsort_kernel, dim3((unsigned)((K + 3) / 4)), dim3(256), 0, st, edge_index, E, K, ws.seg,
+    hipLaunchKernelGGL(mpn_segsort_kernel, dim3((unsigned)((K + 15) / 16)), dim3(256), 0, st, edge_index, E, K, ws.seg,
                        ws.perm, ws.s_src, ws.s_dst, ws.s_orig);
     PEMP_LAUNCH_CHECK();
   }
@@ -1437,12 +1764,25 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
   const int edge_grid = std::max(num_cus(), T);   // >= wg_start[T] (see mpn_scan_kernel)
   const bool fused_heads = mlp_ok(w->node_head, 64, 64) && mlp_ok(w->class_head, 64, 64);
   const unsigned node_grid = (unsigned)((N + 15) / 16);
-  auto node_step = [&](const char* label, bool update, bool table, int slot, bool dup, bool embed = false) -> int {
-    NodeStepArgs na{};
-    if (embed) { na.x_in = x; na.in_ld = desc->node_in_dim; na.emb = w->node_emb; }
-    na.agg = ws.agg; na.seg = ws.seg; na.T = T; na.do_update = update; na.N = N;
-    na.upd_w = w->upd_w; na.upd_b = w->upd_b; na.X = ws.X;
-    na.pre_w = w->pre_w; na.pre_b = w->pre_b; na.NO = NO; na.NT = table ? ws.NT : nullptr;
+  // U_t pre-applied in the edge pass (linear aggregations with an update MLP): the node update is a sum
+  const bool upd_fused = desc->aggr != PEMP_AGGR_MAX && w->upd_w &&
+                         (desc->precision == PEMP_PREC_FP32 || w->upd_bf);
+  const int table_prec = desc->precision == PEMP_PREC_BF16X3 && w->pre_bf ? PEMP_PREC_BF16X3 : PEMP_PREC_FP32;
+  const int table_groups = (NO / 16 + 3) / 4;
+  const unsigned table_grid = (unsigned)(((N + 16 * TBL_TILES - 1) / (16 * TBL_TILES)) * table_groups);
+  // x for the next stage (mode) + heads when slot >= 0, then the node table when `table`
+  auto node_step = [&](int mode, bool table, int slot, bool dup) -> int {
+    if (mode == -1) {                                  // update MLP on non-linear aggregates
+      NodeUpdateArgs ua{ws.agg, ws.seg, T, N, w->upd_w, w->upd_b, ws.X};
+      ProfScope prof("node_update", st);
+      hipLaunchKernelGGL(node_update_kernel, dim3(node_grid, 4), dim3(64 * UPD_WAVES), 0, st, ua);
+      PEMP_LAUNCH_CHECK();
+      mode = ROWS_NONE;
+    }
+    NodeRowsArgs na{};
+    na.mode = mode;
+    if (mode == ROWS_EMBED) { na.x_in = x; na.in_ld = desc->node_in_dim; }
+    na.agg = ws.agg; na.seg = ws.seg; na.T = T; na.upd_b = w->upd_b; na.N = N; na.X = ws.X;
     na.node_head = w->node_head; na.class_head = w->class_head; na.J = J;
     if (slot >= 0 && fused_heads) {
       na.node_out = node_logits + (int64_t)slot * N;
@@ -1450,9 +1790,13 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
       na.node_out2 = dup ? na.node_out + N : nullptr;
       na.class_out2 = dup ? na.class_out + N * J : nullptr;
     }
-    {
-      ProfScope prof(label, st);
-      hipLaunchKernelGGL(node_step_kernel, dim3(node_grid, NODE_SPLIT), dim3(64 * NODE_WAVES), 0, st, na);
+    na.emb = w->node_emb;
+    na.img = ws.img;
+    na.head_off = fused_embed_ ? mlp_lds_floats(w->node_emb) : 0;
+    na.head_floats = mlp_lds_floats(w->node_head) + mlp_lds_floats(w->class_head);
+    if (mode != ROWS_NONE || na.node_out) {
+      ProfScope prof(mode == ROWS_EMBED ? "node_embed" : "node_update", st);
+      hipLaunchKernelGGL(node_rows_kernel, dim3(node_grid), dim3(256), node_rows_lds_bytes(na), st, na);
       PEMP_LAUNCH_CHECK();
     }
     if (slot >= 0 && !fused_heads) {
@@ -1465,15 +1809,24 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
           return r2;
       }
     }
+    if (table) {
+      NodeTableArgs ta{ws.X, N, w->pre_w, w->pre_b, w->pre_bf, NO, table_groups, ws.NT};
+      ProfScope prof("node_table", st);
+      if (table_prec == PEMP_PREC_BF16X3)
+        hipLaunchKernelGGL(node_table_kernel<1>, dim3(table_grid), dim3(256), 0, st, ta);
+      else
+        hipLaunchKernelGGL(node_table_kernel<0>, dim3(table_grid), dim3(256), 0, st, ta);
+      PEMP_LAUNCH_CHECK();
+    }
     return PEMP_OK;
   };
   // node embedding + node table of the first iteration (or, without iterations, the heads on the
   // embedding); embedding widths > 128 would not fit the node step's LDS rows: separate launch
-  const bool fused_embed = mlp_ok(w->node_emb, 128, 128);
+  const bool fused_embed = fused_embed_;
   if (!fused_embed) {
     if ((rc = rows_mlp("node_embed", w->node_emb, x, desc->node_in_dim, N, ws.X, 128, ws.X + 64, 128, st))) return rc;
   }
-  if ((rc = node_step("node_table", false, steps > 0, steps > 0 ? -1 : 0, false, fused_embed))) return rc;
+  if ((rc = node_step(fused_embed ? ROWS_EMBED : ROWS_NONE, steps > 0, steps > 0 ? -1 : 0, false))) return rc;
   float* e_cur = ws.EA;
   float* e_nxt = ws.EB;
   int rec = 0;
@@ -1488,20 +1841,22 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
       ea.e1_w = w->e1_w; ea.e2_w = w->e2_w; ea.e2_b = w->e2_b; ea.msg_w = w->msg_w; ea.attn_w = w->attn_w;
       ea.attn_b = w->attn_b; ea.agg = ws.agg; ea.head = w->edge_head;
       ea.e1_bf = w->e1_bf; ea.e2_bf = w->e2_bf; ea.msg_bf = w->msg_bf; ea.head_bf = w->head_bf;
+      ea.upd_w = w->upd_w; ea.upd_bf = w->upd_bf;
       ea.edge_logits = record ? edge_logits + (int64_t)rec * E : nullptr;
       ea.write_next = !last;
       ProfScope prof(record ? "edge_step_head" : "edge_step", st);
       switch (desc->aggr) {
-        case PEMP_AGGR_ATTN: launch_edge_step<PEMP_AGGR_ATTN>(ea, record, edge_grid, desc->precision, st); break;
-        case PEMP_AGGR_SUM: launch_edge_step<PEMP_AGGR_SUM>(ea, record, edge_grid, desc->precision, st); break;
-        case PEMP_AGGR_MEAN: launch_edge_step<PEMP_AGGR_MEAN>(ea, record, edge_grid, desc->precision, st); break;
-        default: launch_edge_step<PEMP_AGGR_MAX>(ea, record, edge_grid, desc->precision, st); break;
+        case PEMP_AGGR_ATTN: launch_edge_step<PEMP_AGGR_ATTN>(ea, record, edge_grid, desc->precision, upd_fused, st); break;
+        case PEMP_AGGR_SUM: launch_edge_step<PEMP_AGGR_SUM>(ea, record, edge_grid, desc->precision, upd_fused, st); break;
+        case PEMP_AGGR_MEAN: launch_edge_step<PEMP_AGGR_MEAN>(ea, record, edge_grid, desc->precision, upd_fused, st); break;
+        default: launch_edge_step<PEMP_AGGR_MAX>(ea, record, edge_grid, desc->precision, false, st); break;
       }
       PEMP_LAUNCH_CHECK();
     }
     // node update + next node table; heads when recorded (the last iteration's heads also fill
     // the post-loop slot: NODE_STEPS = 0 leaves x unchanged, NodeClassificationMPNSimple.py:93-94)
-    if ((rc = node_step("node_update", true, !last, record ? rec : -1, last))) return rc;
+    const int mode = upd_fused ? ROWS_SUM : w->upd_w ? -1 : ROWS_COPY;
+    if ((rc = node_step(mode, !last, record ? rec : -1, last))) return rc;
     if (record) ++rec;
     float* tmp = e_cur; e_cur = e_nxt; e_nxt = tmp;
   }

@@ -62,7 +62,7 @@ class NaiveGraphConstructor:
     # ------------------------------------------------------------------------------------
     def construct_graph(self):
         L = _lib.lib()
-        st = _lib.stream()
+        st = _lib.stream(self.device)
         sm = self.scoremaps
         if sm.dtype != torch.float32:
             sm = sm.float()
@@ -109,16 +109,17 @@ class NaiveGraphConstructor:
         A = {0: J + 2, 1: J, 2: 1, 3: 2, 4: J + 3}[mode]
         norm = float(max(W, H)) if self.normalize_node_distance else 1.0
 
-        counts = n_det.cpu().numpy().astype(np.int64)      # the one host read-back of the batch
-        if counts.max(initial=0) > cap:
-            cap = int(counts.max())
+        counts_l = n_det.tolist()                           # the one host read-back of the batch
+        mx = max(counts_l) if counts_l else 0
+        if mx > cap:
+            cap = mx
             NaiveGraphConstructor._cap = max(NaiveGraphConstructor._cap, cap)
             det = torch.empty(B, cap, 3, dtype=torch.int64, device=dev)
             dsc = torch.empty(B, cap, dtype=torch.float32, device=dev)
             _lib.check(L.pemp_detect(_lib.ptr(sm), _lib.ptr(masks), B, J, H, W, self.pool_kernel_size, thr,
                                      int(use_thr), topk, 2, _lib.ptr(ws), ws.numel(), _lib.ptr(det), _lib.ptr(dsc),
                                      _lib.ptr(n_det), cap, st))
-        N = int(counts.sum())
+        N = sum(counts_l)
         x = torch.empty(N, C, dtype=torch.float32, device=dev)
         joint_det = torch.empty(N, 3, dtype=torch.int64, device=dev)
         joint_scores = torch.empty(N, dtype=torch.float32, device=dev)
@@ -127,7 +128,7 @@ class NaiveGraphConstructor:
 
         if self.mpn_graph_type == "fully" and B <= 1024:
             # one launch: offsets + nodes + edge_index + edge_attr (pemp_fully_graph_build)
-            E = int((counts * np.maximum(counts - 1, 0)).sum())
+            E = sum(c * (c - 1) for c in counts_l if c > 1)
             edge_index = torch.empty(2, E, dtype=torch.int64, device=dev)
             edge_attr = torch.empty(E, A, dtype=torch.float32, device=dev)
             _lib.check(L.pemp_fully_graph_build(
@@ -136,7 +137,7 @@ class NaiveGraphConstructor:
                 _lib.ptr(joint_tags), _lib.ptr(edge_index), _lib.ptr(edge_attr), st))
         else:
             node_off_h = np.zeros(B + 1, np.int64)
-            node_off_h[1:] = np.cumsum(counts)
+            node_off_h[1:] = np.cumsum(np.asarray(counts_l, np.int64))
             # batch offsets are recomputed on the device from n_det (no host->device upload)
             offs = torch.empty(2, B + 1, dtype=torch.int64, device=dev)
             node_off, fully_off = offs[0], offs[1]

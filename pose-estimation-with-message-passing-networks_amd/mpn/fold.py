@@ -13,6 +13,8 @@
 The node table the kernels use holds x = [x_init ‖ x_cur] (128 wide); without skip connections
 the x_init/e_init columns get zero weights.
 """
+import ctypes
+
 import torch
 import torch.nn as nn
 
@@ -97,6 +99,7 @@ class Folded:
     def __init__(self):
         self.tensors = []
         self.struct = _lib.PempMpnWeights()
+        self.struct_ref = ctypes.byref(self.struct)
 
     def dev(self, t, device):
         d = t.to(torch.float32).contiguous().to(device)
@@ -157,7 +160,9 @@ def fold_weights(model, device) -> Folded:
     pre_w = [A, Bm] + [to_xtable(m.weight.detach().double().cpu()[:, :nx]) for m in msg_mods]
     pre_b = [torch.zeros(64, dtype=torch.float64)] * 2 + [m.bias.detach().double().cpu() for m in msg_mods]
     msg_w = [m.weight.detach().double().cpu()[:, nx:nx + 64] for m in msg_mods]
-    s.pre_w = f.dev(torch.cat(pre_w, 0), device).data_ptr()
+    pre_full = torch.cat(pre_w, 0)
+    s.pre_w = f.dev(pre_full, device).data_ptr()
+    s.pre_bf = f.dev_raw(bf16_pack(pre_full), device).data_ptr()
     s.pre_b = f.dev(torch.cat(pre_b, 0), device).data_ptr()
     s.q0_w = f.dev(q0, device).data_ptr()
     s.q0_b = f.dev(b1, device).data_ptr()
@@ -187,4 +192,8 @@ def fold_weights(model, device) -> Folded:
     if upd is not None:
         s.upd_w = f.dev(upd[0].weight.detach().double().cpu(), device).data_ptr()
         s.upd_b = f.dev(upd[0].bias.detach().double().cpu(), device).data_ptr()
+        U = upd[0].weight.detach().double().cpu()
+        if U.shape == (64, 64 * T):
+            s.upd_bf = f.dev_raw(torch.stack([bf16_pack(U[:, 64 * t:64 * t + 64]) for t in range(T)], 0),
+                                 device).data_ptr()
     return f

@@ -16,6 +16,8 @@ import torch.nn as nn
 from .. import _lib
 from .fold import fold_weights
 
+_VALIDATE = os.environ.get("PEMP_VALIDATE", "0") not in ("", "0")   # read once at import
+
 AGGR_CODES = {"attn": 0, "add": 1, "sum": 1, "mean": 2, "max": 3}
 PRECISIONS = {"fp32": 0, "bf16x3": 1}
 
@@ -152,6 +154,7 @@ class NodeClassificationMPNSimple(nn.Module):
         self._folded_key = None
         self._tensors = None
         self._ws = _lib.Workspace()
+        self._desc_key = None
 
     # --------------------------------------------------------------------------------------
     def _apply(self, fn, *args, **kwargs):
@@ -187,36 +190,47 @@ class NodeClassificationMPNSimple(nn.Module):
         if self.node_summary != "not":
             node_types = torch.tensor(TYPE_LUTS[self.node_summary], device=dev)[node_types]
         N, E = x.shape[0], edge_index.shape[1]
-        x = x.float().contiguous()
-        edge_attr = edge_attr.float().contiguous()
-        edge_index = edge_index.long().contiguous()
-        node_types = node_types.long()
+        x = _as(x, torch.float32)
+        edge_attr = _as(edge_attr, torch.float32)
+        edge_index = _as(edge_index, torch.int64)
+        if node_types.dtype != torch.int64:
+            node_types = node_types.long()
         if node_types.dim() != 1 or (N > 0 and node_types.stride(0) < 1):
             node_types = node_types.reshape(-1).contiguous()
         t_stride = node_types.stride(0) if N > 0 else 1       # joint_det[:, 2] is read in place
         fw = self._weights(dev)
-        steps, aux = self.edge_steps, self.aux_loss_steps
-        n_rec = sum(1 for i in range(steps) if i >= steps - aux - 1)
         if self.precision not in PRECISIONS:
             raise ValueError(f"precision={self.precision!r}: expected one of {sorted(PRECISIONS)}")
-        desc = _lib.PempMpnDesc(self.num_types, self.num_joints, steps, aux, self.aggr_code, 64,
-                                edge_attr.shape[1] if edge_attr.dim() == 2 else 1, x.shape[1],
-                                PRECISIONS[self.precision], t_stride)
+        A = edge_attr.shape[1] if edge_attr.dim() == 2 else 1
+        dkey = (A, x.shape[1], self.precision, t_stride)
+        if self._desc_key != dkey:
+            steps, aux = self.edge_steps, self.aux_loss_steps
+            self._n_rec = sum(1 for i in range(steps) if i >= steps - aux - 1)
+            self._desc = _lib.PempMpnDesc(self.num_types, self.num_joints, steps, aux, self.aggr_code, 64, A,
+                                          x.shape[1], PRECISIONS[self.precision], t_stride)
+            self._desc_ref = ctypes.byref(self._desc)
+            self._desc_key = dkey
+        desc, n_rec = self._desc_ref, self._n_rec
         edge_logits = torch.empty(max(n_rec, 1), E, dtype=torch.float32, device=dev)
         node_logits = torch.empty(n_rec + 1, N, dtype=torch.float32, device=dev)
         class_logits = torch.empty(n_rec + 1, N, self.num_joints, dtype=torch.float32, device=dev)
-        ws = self._ws.get(L.pemp_mpn_workspace_size(ctypes.byref(desc), N, E), dev)
-        _lib.check(L.pemp_mpn_forward(ctypes.byref(desc), ctypes.byref(fw.struct), _lib.ptr(x), _lib.ptr(edge_attr),
-                                      _lib.ptr(edge_index), _lib.ptr(node_types), N, E, _lib.ptr(edge_logits),
-                                      _lib.ptr(node_logits), _lib.ptr(class_logits), _lib.ptr(ws), ws.numel(),
-                                      _lib.stream()))
-        if kwargs.get("validate", os.environ.get("PEMP_VALIDATE", "0") not in ("", "0")):
-            _lib.check(L.pemp_mpn_status(ctypes.byref(desc), N, E, _lib.ptr(ws), _lib.stream()))
+        ws = self._ws.get(L.pemp_mpn_workspace_size(desc, N, E), dev)
+        _lib.check(L.pemp_mpn_forward(desc, fw.struct_ref, x.data_ptr(), edge_attr.data_ptr(), edge_index.data_ptr(),
+                                      node_types.data_ptr(), N, E, edge_logits.data_ptr(), node_logits.data_ptr(),
+                                      class_logits.data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream(dev)))
+        if kwargs.get("validate", _VALIDATE):
+            _lib.check(L.pemp_mpn_status(desc, N, E, _lib.ptr(ws), _lib.stream(dev)))
         # list lengths and .squeeze() semantics of NodeClassificationMPNSimple.py:81-97
         preds_edge = [edge_logits[r].view(E, 1).squeeze() for r in range(n_rec)]
         preds_node = [node_logits[r].view(N, 1).squeeze() for r in range(n_rec + 1)]
         preds_class = [class_logits[r] for r in range(n_rec + 1)]
         return preds_edge, preds_node, preds_class, [None]
+
+
+def _as(t, dtype):
+    if t.dtype != dtype:
+        t = t.to(dtype)
+    return t if t.is_contiguous() else t.contiguous()
 
 
 def get_mpn_model(config, **kwargs):
