@@ -207,23 +207,23 @@ def _mlp(sd, prefix, x, sizes, bn, end_with_relu=False):
 
 def _segment_softmax(a, index, n):
     """torch_scatter 2.0.4 scatter_softmax: exp(a - max_seg) / (sum_seg + 1e-12)."""
-    mx = torch.full((n,), float("-inf")).scatter_reduce(0, index, a, "amax", include_self=True)
+    mx = torch.full((n,), float("-inf"), dtype=a.dtype).scatter_reduce(0, index, a, "amax", include_self=True)
     mx = torch.where(torch.isneginf(mx), torch.zeros_like(mx), mx)
     ex = (a - mx[index]).exp()
-    sm = torch.zeros(n).index_add_(0, index, ex)
+    sm = torch.zeros(n, dtype=a.dtype).index_add_(0, index, ex)
     return ex / (sm + 1e-12)[index]
 
 
 def _scatter(v, index, n, reduce):
-    out = torch.zeros(n, v.shape[1])
+    out = torch.zeros(n, v.shape[1], dtype=v.dtype)
     if reduce in ("add", "sum"):
         return out.index_add_(0, index, v)
     if reduce == "mean":
         s = out.index_add_(0, index, v)
-        c = torch.zeros(n).index_add_(0, index, torch.ones(v.shape[0])).clamp(1)
+        c = torch.zeros(n, dtype=v.dtype).index_add_(0, index, torch.ones(v.shape[0], dtype=v.dtype)).clamp(1)
         return s / c[:, None]
     if reduce == "max":
-        m = torch.full((n, v.shape[1]), float("-inf")).scatter_reduce(
+        m = torch.full((n, v.shape[1]), float("-inf"), dtype=v.dtype).scatter_reduce(
             0, index[:, None].expand_as(v), v, "amax", include_self=True)
         return torch.where(torch.isneginf(m), torch.zeros_like(m), m)
     raise ValueError(reduce)
@@ -253,13 +253,13 @@ def mpn_layer(sd, cfg, x, e, edge_index, node_types):
         return agg, e_new
     src_type = node_types[j]
     num_types = _num_types(cfg)
-    m = torch.zeros(e_new.shape[0], e_new.shape[1])
+    m = torch.zeros(e_new.shape[0], e_new.shape[1], dtype=e_new.dtype)
     xi_e = torch.cat([x[i], e_new], 1)
     for t in range(17):                                    # layers.py:271 hard-codes 17
         sel = src_type == t
         if sel.any():
             m[sel] = F.relu(F.linear(xi_e[sel], sd[f"{p}.mlp_node.mlp.{t}.0.weight"], sd[f"{p}.mlp_node.mlp.{t}.0.bias"]))
-    upd = torch.zeros(n, num_types, m.shape[1])
+    upd = torch.zeros(n, num_types, m.shape[1], dtype=m.dtype)
     if cfg.AGGR_SUB in ("node_edge_attn",):
         a = F.linear(e_new, sd[f"{p}.attn_net.0.weight"], sd[f"{p}.attn_net.0.bias"])[:, 0]
         for t in range(num_types):

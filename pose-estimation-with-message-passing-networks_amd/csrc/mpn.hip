@@ -445,8 +445,8 @@ __global__ __launch_bounds__(256) void rows_mlp_kernel(RowsMlpArgs a) {
 __global__ __launch_bounds__(256) void edge_embed_wide_kernel(pemp_mlp emb, const float* __restrict__ ea, int A,
                                                          const int* __restrict__ s_orig, int64_t E,
                                                          const float* __restrict__ q0_w,
-                                                         const float* __restrict__ q0_b, float* __restrict__ e0,
-                                                         float* __restrict__ q0) {
+                                                         const float* __restrict__ q0_b, const float* __restrict__ e1_w,
+                                                         float* __restrict__ r0, float* __restrict__ q0) {
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int64_t p = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + c;
   const bool valid = p < E;
@@ -471,10 +471,12 @@ __global__ __launch_bounds__(256) void edge_embed_wide_kernel(pemp_mlp emb, cons
   gemm_frag<4, 4>(q0_w, 64, e, acc);
   if (valid) {
 #pragma unroll
-    for (int ob = 0; ob < 4; ++ob) {
-      st4(e0 + p * D + 16 * ob + 4 * g, e[ob][0], e[ob][1], e[ob][2], e[ob][3]);
-      st4(q0 + p * D + 16 * ob + 4 * g, acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]);
-    }
+    for (int ob = 0; ob < 4; ++ob) st4(q0 + p * D + 16 * ob + 4 * g, acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]);
+  }
+  gemm_frag<4, 4>(e1_w, 64, e, acc);              // R0 = Q0 + W1_e_cur · e_init
+  if (valid) {
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob) st4(r0 + p * D + 16 * ob + 4 * g, acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]);
   }
 }
 
@@ -499,19 +501,21 @@ __device__ __forceinline__ void split_bf16(const float (&x)[4][4], bf16x8_t (&hi
     }
 }
 
-// acc[ob] += W[16 ob + i][.] · x   with W hi / lo parts in LDS ([out][LDW] bf16 each), K = 64
+// acc[ob] += W[16 ob + i][.] · x, K = 64, W in LDS as interleaved bf16 rows of 2 LDW elements:
+// [hi 64 | lo 64 | pad 16]. The row stride (LDW = 72 dwords, = 8 mod 64) keeps the fragment reads
+// (row = lane & 15, 16 B at 8 (lane >> 4)) bank-conflict free for both parts (ds_read_b128 lane groups).
 template <int OB>
-__device__ __forceinline__ void gemm_bf3(const __bf16* __restrict__ Wh, const __bf16* __restrict__ Wl,
-                                         const bf16x8_t (&hi)[2], const bf16x8_t (&lo)[2], float (&acc)[OB][4]) {
+__device__ __forceinline__ void gemm_bf3(const __bf16* __restrict__ W, const bf16x8_t (&hi)[2], const bf16x8_t (&lo)[2],
+                                         float (&acc)[OB][4]) {
   const int lane = __lane_id(), i = lane & 15, g = lane >> 4;
 #pragma unroll
   for (int ob = 0; ob < OB; ++ob) {
     f32x4 c = {acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]};
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
-      const int o = (16 * ob + i) * LDW + 32 * kb + 8 * g;
-      const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(Wh + o);
-      const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(Wl + o);
+      const int o = (16 * ob + i) * 2 * LDW + 32 * kb + 8 * g;
+      const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(W + o);
+      const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(W + o + 64);
       c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, hi[kb], c, 0, 0, 0);
       c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, lo[kb], c, 0, 0, 0);
       c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, hi[kb], c, 0, 0, 0);
@@ -521,17 +525,23 @@ __device__ __forceinline__ void gemm_bf3(const __bf16* __restrict__ Wh, const __
 }
 
 // one layer on fragments in the chosen precision; W points at the LDS image of the matrix
-// (PREC 0: fp32 [out][LDW]; PREC 1: bf16 hi [out][LDW] then lo [out][LDW])
+// (PREC 0: fp32 [out][LDW]; PREC 1: interleaved bf16 rows [out][hi 64 | lo 64 | pad], see gemm_bf3)
 template <int PREC, int OB>
-__device__ __forceinline__ void gemm_p(const void* W, int out_rows, const float (&x)[4][4], float (&acc)[OB][4]) {
+__device__ __forceinline__ void gemm_p(const void* W, const float (&x)[4][4], float (&acc)[OB][4]) {
   if (PREC == 0) {
     gemm_frag<4, OB>(static_cast<const float*>(W), LDW, x, acc);
   } else {
     bf16x8_t hi[2], lo[2];
     split_bf16(x, hi, lo);
-    const __bf16* Wh = static_cast<const __bf16*>(W);
-    gemm_bf3<OB>(Wh, Wh + out_rows * LDW, hi, lo, acc);
+    gemm_bf3<OB>(static_cast<const __bf16*>(W), hi, lo, acc);
   }
+}
+
+// global [hi rows][lo rows] bf16 pack row `row` (< 2 rows_per_part) -> its place in an interleaved
+// LDS image with rows of `ld` bf16 elements and parts of `part_len` elements
+__device__ __forceinline__ int interleaved_slot(int row, int rows_per_part, int ld, int part_len) {
+  const int part = row >= rows_per_part, r = row - part * rows_per_part;
+  return r * ld + part * part_len;
 }
 
 // LDS row stride for a weight tile with in_pad columns: >= in_pad and = 8 (mod 64) dwords, so the
@@ -546,13 +556,9 @@ struct EmbedLayout {
   int n, prec, w_off[5], stride[5], kb[5], ob[5], b_off[5], relu[5], g_off[5], total;
 };
 
-// bf16 row stride (elements) for in_pad columns: 4 * odd dwords, so 16 rows x 16 B reads hit
-// 16 distinct bank groups
-static int lds_stride_bf(int in_pad) {
-  int dw = (in_pad / 2 + 3) / 4 * 4;
-  if ((dw / 4) % 2 == 0) dw += 4;
-  return 2 * dw;
-}
+// interleaved bf16 row [hi in_pad | lo in_pad | pad 16] (elements): in_pad + 8 dwords, = 8 * odd
+// (mod 64) for in_pad = 32 kb, which keeps the ds_read_b128 fragment reads conflict free
+static int lds_stride_bf(int in_pad) { return 2 * in_pad + 16; }
 
 static EmbedLayout embed_layout(const pemp_mlp& m, int prec) {
   EmbedLayout L{};
@@ -567,7 +573,7 @@ static EmbedLayout embed_layout(const pemp_mlp& m, int prec) {
     if (prec == PEMP_PREC_BF16X3) {
       L.kb[l] = (in + 31) / 32;
       L.stride[l] = lds_stride_bf(32 * L.kb[l]);
-      off += 16 * L.ob[l] * L.stride[l];                 // hi + lo bf16 = stride floats per row
+      off += 16 * L.ob[l] * L.stride[l] / 2;             // interleaved hi | lo rows, stride bf16 elements
       L.g_off[l] = goff;
       goff += 2 * 16 * L.ob[l] * 32 * L.kb[l];
     } else {
@@ -612,13 +618,14 @@ __device__ __forceinline__ void layer_lds(const float* __restrict__ W, int ldw, 
   }
 }
 
-// bf16x3 variant: W = hi rows [16 OB][ldw] then lo rows; KB32 (<= 2) k-blocks of 32 inputs.
+// bf16x3 variant: W = interleaved rows [16 OB][hi 32 KB32 | lo 32 KB32 | pad], stride ldw; KB32 (<= 2)
+// k-blocks of 32 inputs.
 __device__ __forceinline__ void layer_lds_bf(const __bf16* __restrict__ W, int ldw, const float* __restrict__ bias,
                                              int KB32, int OB, int relu, const float (&in)[4][4], float (&out)[4][4]) {
   const int lane = __lane_id(), i = lane & 15, g = lane >> 4;
   bf16x8_t hi[2], lo[2];
   split_bf16(in, hi, lo);
-  const __bf16* Wl = W + 16 * OB * ldw;
+  const int lo_off = 32 * KB32;                 // interleaved rows: [hi | lo | pad]
 #pragma unroll
   for (int ob = 0; ob < 4; ++ob) {
     if (ob < OB) {
@@ -629,7 +636,7 @@ __device__ __forceinline__ void layer_lds_bf(const __bf16* __restrict__ W, int l
         if (kb < KB32) {
           const int o = (16 * ob + i) * ldw + 32 * kb + 8 * g;
           const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(W + o);
-          const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(Wl + o);
+          const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(W + o + lo_off);
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, hi[kb], c, 0, 0, 0);
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, lo[kb], c, 0, 0, 0);
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, hi[kb], c, 0, 0, 0);
@@ -644,7 +651,93 @@ __device__ __forceinline__ void layer_lds_bf(const __bf16* __restrict__ W, int l
   }
 }
 
-// Edge embedding (sorted order): e_init = MLP(edge_attr[orig]); Q0 = W1_e_init·e_init + b1.
+// Stage the edge-embedding LDS image (layers, then the Q0 tile, then biases; EmbedLayout).
+template <int PREC>
+__device__ inline void stage_embed(float* sm, const pemp_mlp& emb, const EmbedLayout& Lo, const uint16_t* emb_bf,
+                                   const float* q0_w, const float* q0_b) {
+  for (int l = 0; l <= Lo.n; ++l) {
+    const float* bsrc = l < Lo.n ? emb.layer[l].b : q0_b;
+    const int rows = 16 * Lo.ob[l];
+    if (PREC == 0) {
+      const float* src = l < Lo.n ? emb.layer[l].w : q0_w;
+      const int ip = 16 * Lo.kb[l], q4 = ip / 4;
+      for (int idx = threadIdx.x; idx < rows * q4; idx += blockDim.x) {
+        const int row = idx / q4, c4 = (idx - row * q4) * 4;
+        *reinterpret_cast<float4*>(&sm[Lo.w_off[l] + row * Lo.stride[l] + c4]) = ld4(src + row * ip + c4);
+      }
+    } else {
+      const uint16_t* src = emb_bf + Lo.g_off[l];
+      const int ip = 32 * Lo.kb[l], q8 = ip / 8;
+      __bf16* dstb = reinterpret_cast<__bf16*>(sm + Lo.w_off[l]);
+      for (int idx = threadIdx.x; idx < 2 * rows * q8; idx += blockDim.x) {   // hi rows, then lo rows
+        const int row = idx / q8, c8 = (idx - row * q8) * 8;
+        *reinterpret_cast<uint4*>(&dstb[interleaved_slot(row, rows, Lo.stride[l], ip) + c8]) =
+            *reinterpret_cast<const uint4*>(src + row * ip + c8);
+      }
+    }
+    for (int idx = threadIdx.x; idx < rows; idx += blockDim.x) sm[Lo.b_off[l] + idx] = bsrc[idx];
+  }
+}
+
+// edge_attr row of the tile's edge (lane column c): features 16 mb + 4 g + r < A
+__device__ __forceinline__ void load_edge_attr(const float* __restrict__ ea, int A, int64_t o, float (&x)[4][4]) {
+  const int g = __lane_id() >> 4;
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int f = 16 * mb + 4 * g + r;
+      x[mb][r] = f < A ? ea[o * A + f] : 0.0f;
+    }
+}
+
+// embedding MLP then the Q0 layer on one tile: in x = edge_attr; out x = e_init, y = Q0 (+ b1)
+template <int PREC>
+__device__ __forceinline__ void embed_tile(const float* smz, const EmbedLayout& Lo, float (&x)[4][4], float (&y)[4][4]) {
+  // layers alternate x -> y -> x ...; the result ends in x, then Q0 -> y
+  for (int l = 0; l <= Lo.n; ++l) {
+    const float* W = smz + Lo.w_off[l];
+    const float* bias = smz + Lo.b_off[l];
+    const int relu = Lo.relu[l];
+    const bool odd = (l & 1) != 0;
+    if (l == Lo.n && (Lo.n & 1)) {               // the embedding result is in y: move it to x
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[ob][r] = y[ob][r];
+    }
+    const bool to_y = l == Lo.n || !odd;
+    if (PREC == 0) {
+      if (to_y) layer_lds(W, Lo.stride[l], bias, Lo.kb[l], Lo.ob[l], relu, x, y);
+      else layer_lds(W, Lo.stride[l], bias, Lo.kb[l], Lo.ob[l], relu, y, x);
+    } else {
+      const __bf16* Wb = reinterpret_cast<const __bf16*>(W);
+      if (to_y) layer_lds_bf(Wb, Lo.stride[l], bias, Lo.kb[l], Lo.ob[l], relu, x, y);
+      else layer_lds_bf(Wb, Lo.stride[l], bias, Lo.kb[l], Lo.ob[l], relu, y, x);
+    }
+  }
+}
+
+// Stage one 64x64 edge-pass matrix into LDS (PREC 0: fp32 rows of LDW; PREC 1: interleaved bf16)
+template <int PREC>
+__device__ __forceinline__ void stage_tile64(float* dst, const float* w32, int64_t ld32, const uint16_t* wbf) {
+  if (PREC == 0) {
+    for (int idx = threadIdx.x; idx < D * 16; idx += blockDim.x) {
+      const int row = idx >> 4, c4 = (idx & 15) * 4;
+      *reinterpret_cast<float4*>(&dst[row * LDW + c4]) = ld4(w32 + row * ld32 + c4);
+    }
+  } else {
+    __bf16* db = reinterpret_cast<__bf16*>(dst);
+    for (int idx = threadIdx.x; idx < 2 * D * 8; idx += blockDim.x) {
+      const int row = idx >> 3, c8 = (idx & 7) * 8;
+      *reinterpret_cast<uint4*>(&db[interleaved_slot(row, D, 2 * LDW, D) + c8]) =
+          *reinterpret_cast<const uint4*>(wbf + row * D + c8);
+    }
+  }
+}
+
+// Edge embedding (sorted order), the fallback of the fused first pass: e_init = MLP(edge_attr[orig]),
+// Q0 = W1_e_init·e_init + b1 and R0 = Q0 + W1_e_cur·e_init (the first pass's layer-1 input).
 // One 16-wave workgroup per CU, weights staged once in LDS; a wave walks an equal share of the
 // sorted positions in 16-edge tiles.
 template <int PREC>
@@ -654,9 +747,12 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp em
                                                                      const int* __restrict__ s_orig, int64_t E,
                                                                      const float* __restrict__ q0_w,
                                                                      const float* __restrict__ q0_b,
-                                                                     float* __restrict__ e0, float* __restrict__ q0) {
+                                                                     const float* __restrict__ e1_w,
+                                                                     const uint16_t* __restrict__ e1_bf,
+                                                                     float* __restrict__ r0, float* __restrict__ q0) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
+  stage_tile64<PREC>(sm + Lo.total, e1_w, D, e1_bf);   // W1_e_cur after the embedding image
   for (int l = 0; l <= Lo.n; ++l) {
     const float* bsrc = l < Lo.n ? emb.layer[l].b : q0_b;
     const int rows = 16 * Lo.ob[l];
@@ -673,7 +769,8 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp em
       __bf16* dstb = reinterpret_cast<__bf16*>(sm + Lo.w_off[l]);
       for (int idx = threadIdx.x; idx < 2 * rows * q8; idx += 64 * EDGE_WAVES) {   // hi rows, then lo rows
         const int row = idx / q8, c8 = (idx - row * q8) * 8;
-        *reinterpret_cast<uint4*>(&dstb[row * Lo.stride[l] + c8]) = *reinterpret_cast<const uint4*>(src + row * ip + c8);
+        *reinterpret_cast<uint4*>(&dstb[interleaved_slot(row, rows, Lo.stride[l], ip) + c8]) =
+            *reinterpret_cast<const uint4*>(src + row * ip + c8);
       }
     }
     for (int idx = threadIdx.x; idx < rows; idx += 64 * EDGE_WAVES) sm[Lo.b_off[l] + idx] = bsrc[idx];
@@ -689,41 +786,16 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp em
     const bool valid = p < end;
     const int64_t o = s_orig[valid ? p : end - 1];
     float x[4][4], y[4][4];
-#pragma unroll
-    for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int f = 16 * mb + 4 * g + r;
-        x[mb][r] = f < A ? ea[o * A + f] : 0.0f;
-      }
-    // layers alternate x -> y -> x ...; the result ends in x, then Q0 -> y
-    for (int l = 0; l <= Lo.n; ++l) {
-      const float* W = smz + Lo.w_off[l];
-      const float* bias = smz + Lo.b_off[l];
-      const int relu = Lo.relu[l];
-      const bool odd = (l & 1) != 0;
-      if (l == Lo.n && (Lo.n & 1)) {               // the embedding result is in y: move it to x
-#pragma unroll
-        for (int ob = 0; ob < 4; ++ob)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) x[ob][r] = y[ob][r];
-      }
-      const bool to_y = l == Lo.n || !odd;
-      if (PREC == 0) {
-        if (to_y) layer_lds(W, Lo.stride[l], bias, Lo.kb[l], Lo.ob[l], relu, x, y);
-        else layer_lds(W, Lo.stride[l], bias, Lo.kb[l], Lo.ob[l], relu, y, x);
-      } else {
-        const __bf16* Wb = reinterpret_cast<const __bf16*>(W);
-        if (to_y) layer_lds_bf(Wb, Lo.stride[l], bias, Lo.kb[l], Lo.ob[l], relu, x, y);
-        else layer_lds_bf(Wb, Lo.stride[l], bias, Lo.kb[l], Lo.ob[l], relu, y, x);
-      }
-    }
+    load_edge_attr(ea, A, o, x);
+    embed_tile<PREC>(smz, Lo, x, y);
     if (valid) {
 #pragma unroll
-      for (int ob = 0; ob < 4; ++ob) {
-        st4(e0 + p * D + 16 * ob + 4 * g, x[ob][0], x[ob][1], x[ob][2], x[ob][3]);
-        st4(q0 + p * D + 16 * ob + 4 * g, y[ob][0], y[ob][1], y[ob][2], y[ob][3]);
-      }
+      for (int ob = 0; ob < 4; ++ob) st4(q0 + p * D + 16 * ob + 4 * g, y[ob][0], y[ob][1], y[ob][2], y[ob][3]);
+    }
+    gemm_p<PREC, 4>(smz + Lo.total, x, y);        // R0 = Q0 + W1_e_cur · e_init
+    if (valid) {
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob) st4(r0 + p * D + 16 * ob + 4 * g, y[ob][0], y[ob][1], y[ob][2], y[ob][3]);
     }
   }
 }
@@ -735,8 +807,14 @@ struct EdgeStepArgs {
   int64_t N, E;
   int T, t_nt_ld;   // node-table row length = 128 + 64 T
   const int *seg, *wg_start, *s_src, *s_dst, *s_orig;
-  const float *NT, *Q0, *e_cur;
-  float* e_next;
+  const float *NT, *Q0, *r_cur;   // r = Q0 + W1_e_cur · e_cur (layer-1 input without the node terms)
+  float *r_next, *q0_out;         // r_next = Q0 + W1_e_cur · e' (unless the last pass); FIRST: Q0 out
+  const float* ea;                // STAGE_FIRST: edge_attr [E][A] and the embedding (LDS image at emb_off)
+  int A, emb_off;
+  EmbedLayout Lo;
+  pemp_mlp emb;
+  const uint16_t* emb_bf;
+  const float *q0_w, *q0_b;
   const float *e1_w, *e2_w, *e2_b, *msg_w, *attn_w;
   const uint16_t *e1_bf, *e2_bf, *msg_bf, *head_bf;   // PREC 1: [hi | lo][out][64] k-permuted bf16
   const float* upd_w;        // UPD 1: update_mlp.0.weight [64][64 T] (U_t = columns 64 t .. 64 t + 63)
@@ -851,8 +929,20 @@ constexpr int LDS_HEAD = (D + 32) * LDW + D + 32 + 32;
 // in 16-edge tiles; a segment that crosses a tile boundary is carried in registers.
 // PREC: 0 = exact fp32 MFMA (v_mfma_f32_16x16x4_f32), 1 = bf16x3 split precision (see gemm_bf3).
 // The LDS image has the same size in both: a 64 x LDW fp32 tile = its bf16 hi and lo tiles.
-template <int AGG, int HEAD, int PREC, int UPD>
-__global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs a) {
+enum { STAGE_FIRST = 0, STAGE_MID = 1, STAGE_LAST = 2 };
+#ifndef PEMP_FUSED_FIRST
+#define PEMP_FUSED_FIRST 0
+#endif
+
+// STAGE_FIRST: the first pass with the edge embedding fused (reads edge_attr, writes Q0 and r_next);
+// STAGE_MID reads r_cur and Q0 and writes r_next; STAGE_LAST reads r_cur only.
+// waves per workgroup: 16 (<= 128 VGPRs); the embedding-fused first pass needs more registers: 8
+template <int STAGE>
+constexpr int edge_waves() { return STAGE == STAGE_FIRST ? 8 : EDGE_WAVES; }
+
+template <int AGG, int HEAD, int PREC, int UPD, int STAGE>
+__global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(EdgeStepArgs a) {
+  constexpr int NW = edge_waves<STAGE>();
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* wl = sm;                               // [3][64][LDW]: e1_w (e_cur part), e2_w, msg_w[t]
   float* vec = sm + LDS_W;                      // e2_b[64] | attn_w[64]
@@ -868,7 +958,7 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
   {
     if (PREC == 0) {
       const float* srcs[3] = {a.e1_w, a.e2_w, a.msg_w + (int64_t)t * D * D};
-      for (int idx = threadIdx.x; idx < 3 * D * 16; idx += 64 * EDGE_WAVES) {
+      for (int idx = threadIdx.x; idx < 3 * D * 16; idx += 64 * NW) {
         const int mtx = idx / (D * 16), rem = idx - mtx * D * 16, row = rem >> 4, c4 = (rem & 15) * 4;
         *reinterpret_cast<float4*>(&wl[(mtx * D + row) * LDW + c4]) = ld4(srcs[mtx] + row * D + c4);
       }
@@ -876,9 +966,9 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
       // 3 matrices x (hi, lo) x 64 rows of 64 bf16 (8 x 16 B) -> bf16 rows of stride LDW
       const uint16_t* srcs[3] = {a.e1_bf, a.e2_bf, a.msg_bf + (int64_t)t * 2 * D * D};
       __bf16* wb = reinterpret_cast<__bf16*>(wl);
-      for (int idx = threadIdx.x; idx < 3 * 2 * D * 8; idx += 64 * EDGE_WAVES) {
+      for (int idx = threadIdx.x; idx < 3 * 2 * D * 8; idx += 64 * NW) {
         const int mtx = idx / (2 * D * 8), rem = idx - mtx * 2 * D * 8, row = rem >> 3, c8 = (rem & 7) * 8;
-        *reinterpret_cast<uint4*>(&wb[(mtx * 2 * D + row) * LDW + c8]) =
+        *reinterpret_cast<uint4*>(&wb[mtx * 2 * D * LDW + interleaved_slot(row, D, 2 * LDW, D) + c8]) =
             *reinterpret_cast<const uint4*>(srcs[mtx] + row * D + c8);
       }
     }
@@ -886,7 +976,7 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
     else if (threadIdx.x < 2 * D) vec[threadIdx.x] = (AGG == PEMP_AGGR_ATTN) ? a.attn_w[threadIdx.x - D] : 0.0f;
     if (HEAD == 1) {
       if (PREC == 0) {
-        for (int idx = threadIdx.x; idx < (D + 32) * 16; idx += 64 * EDGE_WAVES) {
+        for (int idx = threadIdx.x; idx < (D + 32) * 16; idx += 64 * NW) {
           const int row = idx >> 4, c4 = (idx & 15) * 4;
           const float* src = row < D ? a.head.layer[0].w + row * D : a.head.layer[1].w + (row - D) * D;
           *reinterpret_cast<float4*>(&hw[row * LDW + c4]) = ld4(src + c4);
@@ -894,9 +984,11 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
       } else {
         // head_bf: L1 [hi|lo][64][64], then L2 [hi|lo][32][64] -> same row order in LDS
         __bf16* hwb = reinterpret_cast<__bf16*>(hw);
-        for (int idx = threadIdx.x; idx < 2 * (D + 32) * 8; idx += 64 * EDGE_WAVES) {
+        for (int idx = threadIdx.x; idx < 2 * (D + 32) * 8; idx += 64 * NW) {
           const int row = idx >> 3, c8 = (idx & 7) * 8;
-          *reinterpret_cast<uint4*>(&hwb[row * LDW + c8]) = *reinterpret_cast<const uint4*>(a.head_bf + row * D + c8);
+          const int slot = row < 2 * D ? interleaved_slot(row, D, 2 * LDW, D)
+                                       : 2 * D * LDW + interleaved_slot(row - 2 * D, 32, 2 * LDW, D);
+          *reinterpret_cast<uint4*>(&hwb[slot + c8]) = *reinterpret_cast<const uint4*>(a.head_bf + row * D + c8);
         }
       }
       float* hb = hb_l;
@@ -904,22 +996,8 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
       else if (threadIdx.x < D + 32) hb[threadIdx.x] = a.head.layer[1].b[threadIdx.x - D];
       else if (threadIdx.x < D + 64) hb[threadIdx.x] = a.head.layer[2].w[threadIdx.x - D - 32];
     }
-    if (UPD) {
-      if (PREC == 0) {
-        const float* src = a.upd_w + 64 * t;      // row r: upd_w[r][64 t + k]
-        for (int idx = threadIdx.x; idx < D * 16; idx += 64 * EDGE_WAVES) {
-          const int row = idx >> 4, c4 = (idx & 15) * 4;
-          *reinterpret_cast<float4*>(&uw[row * LDW + c4]) = ld4(src + (int64_t)row * 64 * T + c4);
-        }
-      } else {
-        const uint16_t* src = a.upd_bf + (int64_t)t * 2 * D * D;
-        __bf16* uwb = reinterpret_cast<__bf16*>(uw);
-        for (int idx = threadIdx.x; idx < 2 * D * 8; idx += 64 * EDGE_WAVES) {
-          const int row = idx >> 3, c8 = (idx & 7) * 8;
-          *reinterpret_cast<uint4*>(&uwb[row * LDW + c8]) = *reinterpret_cast<const uint4*>(src + row * D + c8);
-        }
-      }
-    }
+    if (UPD) stage_tile64<PREC>(uw, a.upd_w + 64 * t, 64 * T, PREC == 1 ? a.upd_bf + (int64_t)t * 2 * D * D : nullptr);
+    if (STAGE == STAGE_FIRST) stage_embed<PREC>(sm + a.emb_off, a.emb, a.Lo, a.emb_bf, a.q0_w, a.q0_b);
   }
   __syncthreads();
 
@@ -935,8 +1013,8 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
     const int dp = a.s_dst[p];
     return dp == a.s_dst[p - 1] ? a.seg[t * N + dp + 1] : p;
   };
-  const int first = snap(lo + (int)(n_b * wave / EDGE_WAVES));
-  const int end = snap(lo + (int)(n_b * (wave + 1) / EDGE_WAVES));
+  const int first = snap(lo + (int)(n_b * wave / NW));
+  const int end = snap(lo + (int)(n_b * (wave + 1) / NW));
   if (first >= end) return;
   const float* ntP = a.NT + 128 + 64 * t;
 
@@ -967,23 +1045,50 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
       dst_n = a.s_dst[qn];
       src_n = a.s_src[qn];
     }
-    // gathers: Q0 / e_cur rows of the edge, node-table rows of target and source
-    float h[4][4], ein[4][4], m[4][4];
+    // gathers: r (or edge_attr) and Q0 rows of the edge, node-table rows of target and source
+    float h[4][4], m[4][4], q0r[4][4];
+    if (STAGE == STAGE_FIRST) {
+      // embedding first (few live registers), then the node-table gathers
+      float x[4][4];
+      load_edge_attr(a.ea, a.A, a.s_orig[q], x);
+      embed_tile<PREC>(sm + a.emb_off + z, a.Lo, x, q0r);    // x = e_init, q0r = Q0
+      if (a.q0_out && valid) {
 #pragma unroll
-    for (int ob = 0; ob < 4; ++ob) {
-      const int f = 16 * ob + 4 * g;
-      const float4 q0 = ld4(a.Q0 + (int64_t)q * D + f);
-      const float4 xa = ld4(a.NT + (int64_t)dst * a.t_nt_ld + f);
-      const float4 xb = ld4(a.NT + (int64_t)src * a.t_nt_ld + 64 + f);
-      const float4 ec = ld4(a.e_cur + (int64_t)q * D + f);
-      const float4 xp = ld4(ntP + (int64_t)dst * a.t_nt_ld + f);
-      h[ob][0] = q0.x + xa.x + xb.x; h[ob][1] = q0.y + xa.y + xb.y;
-      h[ob][2] = q0.z + xa.z + xb.z; h[ob][3] = q0.w + xa.w + xb.w;
-      ein[ob][0] = ec.x; ein[ob][1] = ec.y; ein[ob][2] = ec.z; ein[ob][3] = ec.w;
-      m[ob][0] = xp.x; m[ob][1] = xp.y; m[ob][2] = xp.z; m[ob][3] = xp.w;
+        for (int ob = 0; ob < 4; ++ob)
+          st4(a.q0_out + (int64_t)p * D + 16 * ob + 4 * g, q0r[ob][0], q0r[ob][1], q0r[ob][2], q0r[ob][3]);
+      }
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) h[ob][k] = q0r[ob][k];
+      gemm_p<PREC, 4>(W1, x, h);                  // r = Q0 + W1_e_cur · e_init
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob) {
+        const int f = 16 * ob + 4 * g;
+        const float4 xa = ld4(a.NT + (int64_t)dst * a.t_nt_ld + f);
+        const float4 xb = ld4(a.NT + (int64_t)src * a.t_nt_ld + 64 + f);
+        const float4 xp = ld4(ntP + (int64_t)dst * a.t_nt_ld + f);
+        h[ob][0] += xa.x + xb.x; h[ob][1] += xa.y + xb.y; h[ob][2] += xa.z + xb.z; h[ob][3] += xa.w + xb.w;
+        m[ob][0] = xp.x; m[ob][1] = xp.y; m[ob][2] = xp.z; m[ob][3] = xp.w;
+      }
+    } else {
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob) {
+        const int f = 16 * ob + 4 * g;
+        const float4 rr = ld4(a.r_cur + (int64_t)q * D + f);
+        const float4 xa = ld4(a.NT + (int64_t)dst * a.t_nt_ld + f);
+        const float4 xb = ld4(a.NT + (int64_t)src * a.t_nt_ld + 64 + f);
+        const float4 xp = ld4(ntP + (int64_t)dst * a.t_nt_ld + f);
+        if (STAGE == STAGE_MID) {
+          const float4 qq = ld4(a.Q0 + (int64_t)q * D + f);
+          q0r[ob][0] = qq.x; q0r[ob][1] = qq.y; q0r[ob][2] = qq.z; q0r[ob][3] = qq.w;
+        }
+        h[ob][0] = rr.x + xa.x + xb.x; h[ob][1] = rr.y + xa.y + xb.y;
+        h[ob][2] = rr.z + xa.z + xb.z; h[ob][3] = rr.w + xa.w + xb.w;
+        m[ob][0] = xp.x; m[ob][1] = xp.y; m[ob][2] = xp.z; m[ob][3] = xp.w;
+      }
     }
-    // edge MLP layer 1: h = ReLU(Q0 + A[dst] + B[src] + W1_e_cur · e_cur)
-    gemm_p<PREC, 4>(W1, D, ein, h);
+    // edge MLP layer 1: h = ReLU(r + A[dst] + B[src]), r = Q0 + W1_e_cur · e_cur
     relu_frag<4>(h);
     // layer 2: e' = ReLU(W2 · h + b2)
     float ep[4][4];
@@ -992,12 +1097,15 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
       const float4 b2 = ld4(vec + 16 * ob + 4 * g);
       ep[ob][0] = b2.x; ep[ob][1] = b2.y; ep[ob][2] = b2.z; ep[ob][3] = b2.w;
     }
-    gemm_p<PREC, 4>(W2, D, h, ep);
+    gemm_p<PREC, 4>(W2, h, ep);
     relu_frag<4>(ep);
-    if (a.write_next && valid) {
+    if (STAGE != STAGE_LAST && a.write_next) {    // next pass's r = Q0 + W1_e_cur · e'
+      gemm_p<PREC, 4>(W1, ep, q0r);
+      if (valid) {
 #pragma unroll
-      for (int ob = 0; ob < 4; ++ob)
-        st4(a.e_next + (int64_t)p * D + 16 * ob + 4 * g, ep[ob][0], ep[ob][1], ep[ob][2], ep[ob][3]);
+        for (int ob = 0; ob < 4; ++ob)
+          st4(a.r_next + (int64_t)p * D + 16 * ob + 4 * g, q0r[ob][0], q0r[ob][1], q0r[ob][2], q0r[ob][3]);
+      }
     }
     float av = 0.f;
     if (AGG == PEMP_AGGR_ATTN) {
@@ -1019,7 +1127,7 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
         const float4 bb = ld4(hb + 16 * ob + 4 * g);
         h1[ob][0] = bb.x; h1[ob][1] = bb.y; h1[ob][2] = bb.z; h1[ob][3] = bb.w;
       }
-      gemm_p<PREC, 4>(hwz, D, ep, h1);
+      gemm_p<PREC, 4>(hwz, ep, h1);
       relu_frag<4>(h1);
 #pragma unroll
       for (int ob = 0; ob < 2; ++ob) {
@@ -1027,7 +1135,7 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
         h2[ob][0] = bb.x; h2[ob][1] = bb.y; h2[ob][2] = bb.z; h2[ob][3] = bb.w;
       }
       gemm_p<PREC, 2>(PREC == 0 ? (const void*)(hwz + D * LDW) : (const void*)(reinterpret_cast<const __bf16*>(hwz) + 2 * D * LDW),
-                      32, h1, h2);
+                      h1, h2);
       relu_frag<2>(h2);
       float lg = 0.f;
 #pragma unroll
@@ -1049,7 +1157,7 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
       if (valid && g == 0) a.edge_logits[a.s_orig[p]] = h1[0][0];
     }
     // message: m = ReLU(P_t[dst] + W_t_e · e')
-    gemm_p<PREC, 4>(WM, D, ep, m);
+    gemm_p<PREC, 4>(WM, ep, m);
     relu_frag<4>(m);
     if (UPD) {                                    // m <- U_t · m (no bias: added once per node)
       float u[4][4];
@@ -1057,7 +1165,7 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_step_kernel(EdgeStepArgs
       for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
         for (int r = 0; r < 4; ++r) u[ob][r] = 0.0f;
-      gemm_p<PREC, 4>(uw + z, D, m, u);
+      gemm_p<PREC, 4>(uw + z, m, u);
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
@@ -1602,28 +1710,49 @@ static bool published_head(const pemp_mlp& m) {
          m.layer[2].out_dim == 1 && !m.layer[2].relu;
 }
 
-template <int AGG, int PREC, int UPD>
-static void launch_edge_step_p(const EdgeStepArgs& a, bool head, int grid, hipStream_t st) {
-  const size_t lds = (size_t)(LDS_W + LDS_VEC + (UPD ? D * LDW : 0)) * sizeof(float);
-  const dim3 blk(64 * EDGE_WAVES);
+// LDS floats of the edge-pass image before the (STAGE_FIRST) embedding image
+static int edge_lds_base(bool pub_head, bool upd) {
+  return LDS_W + LDS_VEC + (pub_head ? LDS_HEAD : 0) + (upd ? D * LDW : 0);
+}
+
+template <int AGG, int PREC, int UPD, int STAGE>
+static void launch_edge_step_s(const EdgeStepArgs& a, bool head, int grid, hipStream_t st) {
+  const dim3 blk(64 * edge_waves<STAGE>());
+  if constexpr (STAGE == STAGE_FIRST) {          // never with a recorded head (host falls back)
+    const size_t lds = (size_t)(a.emb_off + a.Lo.total) * sizeof(float);
+    hipLaunchKernelGGL((edge_step_kernel<AGG, 0, PREC, UPD, STAGE_FIRST>), dim3(grid), blk, lds, st, a);
+    return;
+  }
+  const bool pub = head && published_head(a.head) && (PREC == 0 || a.head_bf);
+  const size_t lds = (size_t)edge_lds_base(pub, UPD) * sizeof(float);
   if (!head)
-    hipLaunchKernelGGL((edge_step_kernel<AGG, 0, PREC, UPD>), dim3(grid), blk, lds, st, a);
-  else if (published_head(a.head) && (PREC == 0 || a.head_bf))
-    hipLaunchKernelGGL((edge_step_kernel<AGG, 1, PREC, UPD>), dim3(grid), blk, lds + LDS_HEAD * sizeof(float), st, a);
+    hipLaunchKernelGGL((edge_step_kernel<AGG, 0, PREC, UPD, STAGE>), dim3(grid), blk, lds, st, a);
+  else if (pub)
+    hipLaunchKernelGGL((edge_step_kernel<AGG, 1, PREC, UPD, STAGE>), dim3(grid), blk, lds, st, a);
   else
-    hipLaunchKernelGGL((edge_step_kernel<AGG, 2, PREC, UPD>), dim3(grid), blk, lds, st, a);
+    hipLaunchKernelGGL((edge_step_kernel<AGG, 2, PREC, UPD, STAGE>), dim3(grid), blk, lds, st, a);
+}
+
+template <int AGG, int PREC, int UPD>
+static void launch_edge_step_p(const EdgeStepArgs& a, bool head, int grid, int stage, hipStream_t st) {
+#if PEMP_FUSED_FIRST
+  if (stage == STAGE_FIRST) launch_edge_step_s<AGG, PREC, UPD, STAGE_FIRST>(a, head, grid, st);
+  else
+#endif
+  if (stage == STAGE_MID) launch_edge_step_s<AGG, PREC, UPD, STAGE_MID>(a, head, grid, st);
+  else launch_edge_step_s<AGG, PREC, UPD, STAGE_LAST>(a, head, grid, st);
 }
 
 // UPD is instantiated for the linear aggregations only (U · max(m) != max(U · m))
 template <int AGG>
-static void launch_edge_step(const EdgeStepArgs& a, bool head, int grid, int prec, bool upd, hipStream_t st) {
-  constexpr int U = AGG == PEMP_AGGR_MAX ? 0 : 1;
+static void launch_edge_step(const EdgeStepArgs& a, bool head, int grid, int prec, bool upd, int stage, hipStream_t st) {
+  constexpr int U = AGG == PEMP_AGGR_ATTN || AGG == PEMP_AGGR_MEAN ? 1 : 0;
   if (prec == PEMP_PREC_BF16X3) {
-    if (U && upd) launch_edge_step_p<AGG, 1, U>(a, head, grid, st);
-    else launch_edge_step_p<AGG, 1, 0>(a, head, grid, st);
+    if (U && upd) launch_edge_step_p<AGG, 1, U>(a, head, grid, stage, st);
+    else launch_edge_step_p<AGG, 1, 0>(a, head, grid, stage, st);
   } else {
-    if (U && upd) launch_edge_step_p<AGG, 0, U>(a, head, grid, st);
-    else launch_edge_step_p<AGG, 0, 0>(a, head, grid, st);
+    if (U && upd) launch_edge_step_p<AGG, 0, U>(a, head, grid, stage, st);
+    else launch_edge_step_p<AGG, 0, 0>(a, head, grid, stage, st);
   }
 }
 
@@ -1735,38 +1864,49 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
   }
   }
 
-  // ---- edge embedding (the node embedding is fused into the first node step) ----
+  // ---- edge embedding: fused into the first edge pass (STAGE_FIRST) when the first pass records
+  // no head and the embedding's LDS image fits next to the pass's weights; otherwise a separate
+  // launch writes Q0 and R0 = Q0 + W1_e_cur · e_init ----
   int rc = 0;
-  if (E > 0) {
+  const int steps = desc->steps, aux = desc->aux_loss_steps;
+  // U_t pre-applied in the edge pass (linear aggregations with an update MLP): the node update is a sum
+  // (ATTN / MEAN only: for the unnormalised SUM the reordered fp32 rounding of sum_e U m_e vs
+  // U sum_e m_e grows with the in-degree past the logit tolerance)
+  const bool upd_fused = (desc->aggr == PEMP_AGGR_ATTN || desc->aggr == PEMP_AGGR_MEAN) && w->upd_w &&
+                         (desc->precision == PEMP_PREC_FP32 || w->upd_bf);
+  const bool emb_lds = mlp_ok(w->edge_emb, 64, 64);
+  const int emb_prec = desc->precision == PEMP_PREC_BF16X3 && w->emb_bf ? PEMP_PREC_BF16X3 : PEMP_PREC_FP32;
+  const EmbedLayout emb_lo = embed_layout(w->edge_emb, emb_prec);
+  // PEMP_FUSED_FIRST (build flag, default off): the fused first pass runs 8 waves per CU (register
+  // budget of the embedding) and measured slower than embedding + a 16-wave pass (95 vs ~82 us at C3)
+  const bool first_fused = PEMP_FUSED_FIRST && E > 0 && steps >= 1 && steps > aux + 1 && emb_lds &&
+                           emb_prec == desc->precision &&
+                           (size_t)(edge_lds_base(false, upd_fused) + emb_lo.total) * sizeof(float) <= 160 * 1024;
+  if (E > 0 && steps >= 1 && !first_fused) {
     ProfScope prof("edge_embed", st);
-    if (mlp_ok(w->edge_emb, 64, 64)) {
-      const int prec = desc->precision == PEMP_PREC_BF16X3 && w->emb_bf ? PEMP_PREC_BF16X3 : PEMP_PREC_FP32;
-      const EmbedLayout lo = embed_layout(w->edge_emb, prec);
+    if (emb_lds) {
       const int grid = (int)std::min<int64_t>(num_cus(), (E + 16 * EDGE_WAVES - 1) / (16 * EDGE_WAVES));
-      if (prec == PEMP_PREC_BF16X3)
-        hipLaunchKernelGGL(edge_embed_kernel<1>, dim3(grid), dim3(64 * EDGE_WAVES), (size_t)lo.total * sizeof(float),
-                           st, w->edge_emb, lo, w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w,
-                           w->q0_b, ws.EA, ws.Q0);
+      const size_t lds = (size_t)(emb_lo.total + D * LDW) * sizeof(float);
+      if (emb_prec == PEMP_PREC_BF16X3)
+        hipLaunchKernelGGL(edge_embed_kernel<1>, dim3(grid), dim3(64 * EDGE_WAVES), lds, st, w->edge_emb, emb_lo,
+                           w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, w->e1_bf,
+                           ws.EA, ws.Q0);
       else
-        hipLaunchKernelGGL(edge_embed_kernel<0>, dim3(grid), dim3(64 * EDGE_WAVES), (size_t)lo.total * sizeof(float),
-                           st, w->edge_emb, lo, w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w,
-                           w->q0_b, ws.EA, ws.Q0);
+        hipLaunchKernelGGL(edge_embed_kernel<0>, dim3(grid), dim3(64 * EDGE_WAVES), lds, st, w->edge_emb, emb_lo,
+                           w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, w->e1_bf,
+                           ws.EA, ws.Q0);
     } else {
       hipLaunchKernelGGL(edge_embed_wide_kernel, dim3((unsigned)((E + 63) / 64)), dim3(256), 0, st, w->edge_emb,
-                         edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, ws.EA, ws.Q0);
+                         edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, ws.EA, ws.Q0);
     }
     PEMP_LAUNCH_CHECK();
   }
 
   // ---- iterations ----
   const int NO = 128 + 64 * T;
-  const int steps = desc->steps, aux = desc->aux_loss_steps;
   const int edge_grid = std::max(num_cus(), T);   // >= wg_start[T] (see mpn_scan_kernel)
   const bool fused_heads = mlp_ok(w->node_head, 64, 64) && mlp_ok(w->class_head, 64, 64);
   const unsigned node_grid = (unsigned)((N + 15) / 16);
-  // U_t pre-applied in the edge pass (linear aggregations with an update MLP): the node update is a sum
-  const bool upd_fused = desc->aggr != PEMP_AGGR_MAX && w->upd_w &&
-                         (desc->precision == PEMP_PREC_FP32 || w->upd_bf);
   const int table_prec = desc->precision == PEMP_PREC_BF16X3 && w->pre_bf ? PEMP_PREC_BF16X3 : PEMP_PREC_FP32;
   const int table_groups = (NO / 16 + 3) / 4;
   const unsigned table_grid = (unsigned)(((N + 16 * TBL_TILES - 1) / (16 * TBL_TILES)) * table_groups);
@@ -1827,7 +1967,7 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
     if ((rc = rows_mlp("node_embed", w->node_emb, x, desc->node_in_dim, N, ws.X, 128, ws.X + 64, 128, st))) return rc;
   }
   if ((rc = node_step(fused_embed ? ROWS_EMBED : ROWS_NONE, steps > 0, steps > 0 ? -1 : 0, false))) return rc;
-  float* e_cur = ws.EA;
+  float* e_cur = ws.EA;                           // r of the pass (R0 from the separate embedding)
   float* e_nxt = ws.EB;
   int rec = 0;
   for (int it = 0; it < steps; ++it) {
@@ -1837,7 +1977,14 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
       EdgeStepArgs ea{};
       ea.N = N; ea.E = E; ea.T = T; ea.t_nt_ld = NO;
       ea.seg = ws.seg; ea.wg_start = ws.wg_start; ea.s_src = ws.s_src; ea.s_dst = ws.s_dst; ea.s_orig = ws.s_orig;
-      ea.NT = ws.NT; ea.Q0 = ws.Q0; ea.e_cur = e_cur; ea.e_next = e_nxt;
+      const int stage = it == 0 && first_fused ? STAGE_FIRST : last ? STAGE_LAST : STAGE_MID;
+      ea.NT = ws.NT; ea.Q0 = ws.Q0; ea.r_cur = e_cur; ea.r_next = e_nxt;
+      if (stage == STAGE_FIRST) {
+        ea.q0_out = steps > 1 ? ws.Q0 : nullptr;
+        ea.ea = edge_attr; ea.A = desc->edge_attr_dim; ea.Lo = emb_lo; ea.emb = w->edge_emb; ea.emb_bf = w->emb_bf;
+        ea.q0_w = w->q0_w; ea.q0_b = w->q0_b;
+        ea.emb_off = edge_lds_base(false, upd_fused);
+      }
       ea.e1_w = w->e1_w; ea.e2_w = w->e2_w; ea.e2_b = w->e2_b; ea.msg_w = w->msg_w; ea.attn_w = w->attn_w;
       ea.attn_b = w->attn_b; ea.agg = ws.agg; ea.head = w->edge_head;
       ea.e1_bf = w->e1_bf; ea.e2_bf = w->e2_bf; ea.msg_bf = w->msg_bf; ea.head_bf = w->head_bf;
@@ -1846,10 +1993,10 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
       ea.write_next = !last;
       ProfScope prof(record ? "edge_step_head" : "edge_step", st);
       switch (desc->aggr) {
-        case PEMP_AGGR_ATTN: launch_edge_step<PEMP_AGGR_ATTN>(ea, record, edge_grid, desc->precision, upd_fused, st); break;
-        case PEMP_AGGR_SUM: launch_edge_step<PEMP_AGGR_SUM>(ea, record, edge_grid, desc->precision, upd_fused, st); break;
-        case PEMP_AGGR_MEAN: launch_edge_step<PEMP_AGGR_MEAN>(ea, record, edge_grid, desc->precision, upd_fused, st); break;
-        default: launch_edge_step<PEMP_AGGR_MAX>(ea, record, edge_grid, desc->precision, false, st); break;
+        case PEMP_AGGR_ATTN: launch_edge_step<PEMP_AGGR_ATTN>(ea, record, edge_grid, desc->precision, upd_fused, stage, st); break;
+        case PEMP_AGGR_SUM: launch_edge_step<PEMP_AGGR_SUM>(ea, record, edge_grid, desc->precision, upd_fused, stage, st); break;
+        case PEMP_AGGR_MEAN: launch_edge_step<PEMP_AGGR_MEAN>(ea, record, edge_grid, desc->precision, upd_fused, stage, st); break;
+        default: launch_edge_step<PEMP_AGGR_MAX>(ea, record, edge_grid, desc->precision, false, stage, st); break;
       }
       PEMP_LAUNCH_CHECK();
     }

@@ -92,7 +92,14 @@ def test_vs_oracle(case, prec):
     model, sd = make_model(cfg, 0.125 * steps + J, prec)
     x, ea, ei, types = g[0], g[1], g[2], g[7][:, 2]
     pe, pn, pc, _ = run(model, x, ea, ei, types)
-    rpe, rpn, rpc, _ = restate.mpn_forward(sd, cfg, x, ea, ei, types)
+    if variant == "add":
+        # the unnormalised sum is ill-conditioned (activations grow with the in-degree): the fp32
+        # oracle itself is 1.1e-4 from fp64 on the class logits of this case, so both fp32 paths are
+        # held to the same bar against the oracle evaluated in fp64
+        sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
+        rpe, rpn, rpc, _ = restate.mpn_forward(sd64, cfg, x.double(), ea.double(), ei, types)
+    else:
+        rpe, rpn, rpc, _ = restate.mpn_forward(sd, cfg, x, ea, ei, types)
     assert len(pe) == len(rpe) and len(pn) == len(rpn) and len(pc) == len(rpc)
     rel = REL_SUM if variant == "add" else 0.0
     for a, b in zip(pe + pn + pc, rpe + rpn + rpc):
