@@ -92,6 +92,18 @@ int pemp_fully_graph_build(const int32_t* n_det, int B, const int64_t* det_xyt, 
                            int64_t* joint_det, float* joint_scores, int64_t* batch_index, float* joint_tags,
                            int64_t* edge_index, float* edge_attr, void* stream);
 
+/* Capacity mode of pemp_fully_graph_build, launched BEFORE the host reads the counts back (the
+ * reference's nonzero/cat syncs, ConstructGraph.py:1170-1196, become one host read that overlaps
+ * this launch): the totals come from n_det on the device; x / joint_* hold n_cap rows, edge_attr
+ * e_cap rows and edge_index 2 * e_cap entries written as a contiguous [2, E] array. When the batch
+ * exceeds either capacity nothing is written: the caller compares its read-back totals with the
+ * capacities and then calls pemp_fully_graph_build with exact sizes. */
+int pemp_fully_graph_build_cap(const int32_t* n_det, int B, const int64_t* det_xyt, const float* det_scores, int cap,
+                               const float* features, int C, const float* tagmaps, int F, int J, int H, int W,
+                               int64_t n_cap, int64_t e_cap, float norm_factor, int mode, float* x,
+                               int64_t* joint_det, float* joint_scores, int64_t* batch_index, float* joint_tags,
+                               int64_t* edge_index, float* edge_attr, void* stream);
+
 /* Fully connected graph per image: all (i,j), i != j, sorted by (src,dst), node-offset per image.
  * node_off / edge_off: device [B+1] int64 with edge_off[b+1]-edge_off[b] = n_b (n_b - 1). */
 int pemp_fully_graph(const int64_t* node_off, const int64_t* edge_off, int B, int64_t e_total,

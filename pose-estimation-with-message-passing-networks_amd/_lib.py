@@ -52,6 +52,8 @@ SIGNATURES = {
     "pemp_graph_offsets": (c_i32, [c_p, c_i32, c_p, c_p, c_p]),
     "pemp_fully_graph_build": (c_i32, [c_p, c_i32, c_p, c_p, c_i32, c_p, c_i32, c_p, c_i32, c_i32, c_i32, c_i32,
                                        c_i64, c_i64, c_f32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "pemp_fully_graph_build_cap": (c_i32, [c_p, c_i32, c_p, c_p, c_i32, c_p, c_i32, c_p, c_i32, c_i32, c_i32, c_i32,
+                                           c_i64, c_i64, c_f32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "pemp_fully_graph": (c_i32, [c_p, c_p, c_i32, c_i64, c_p, c_p]),
     "pemp_knn_workspace_size": (c_sz, [c_p, c_i32]),
     "pemp_knn_graph_count": (c_i32, [c_p, c_p, c_p, c_i32, c_i32, c_p, c_sz, c_p, c_p]),

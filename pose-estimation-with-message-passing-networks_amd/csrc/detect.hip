@@ -294,18 +294,25 @@ __device__ __forceinline__ int merge_candidates(const float* __restrict__ cv, co
   int li[KMAX];
 #pragma unroll
   for (int k = 0; k < KMAX; ++k) { lv[k] = -INFINITY; li[k] = INV; }
-  // 4 candidates per lane per round: their loads are in flight together
-  for (int c0 = lane; c0 < n; c0 += 256) {
-    float vq[4];
-    int iq[4];
+  // 16 candidates per lane per round: their loads are issued together (clamped addresses, masked
+  // values), so a wave's whole list usually costs one memory round trip
+  constexpr int PER = 16;
+  for (int c0 = lane; c0 < n; c0 += 64 * PER) {
+    float vq[PER];
+    int iq[PER];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int c = c0 + 64 * r;
-      vq[r] = c < n ? cv[c] : -INFINITY;
-      iq[r] = c < n ? ci[c] : INV;
+    for (int r = 0; r < PER; ++r) {
+      const int c = min(c0 + 64 * r, n - 1);
+      vq[r] = cv[c];
+      iq[r] = ci[c];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+      if (c0 + 64 * r >= n) iq[r] = INV;
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < PER; ++r) {
       float v = vq[r];
       int i = iq[r];
       if (i != INV && better(v, i, lv[KMAX - 1], li[KMAX - 1])) {
@@ -374,11 +381,22 @@ __global__ __launch_bounds__(256) void plane_top_kernel(DetectGeom g, float thr,
   const int pl = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int K = g.K, W = g.W, S = g.S, nl = g.units;
   const size_t pt = (size_t)pl * nl;                  // first wave list of the plane
+  // the plane's per-unit counts (first UPT x 256 units) are loaded together with the candidates
+  constexpr int UPT = 4;
+  int tc[UPT], tn[UPT];
+#pragma unroll
+  for (int k = 0; k < UPT; ++k) {
+    const int c = min((int)threadIdx.x + 256 * k, nl - 1);
+    tc[k] = tile_count[pt + c];
+    tn[k] = tile_nonneg[pt + c];
+  }
   int n = block_topk<KMAX>(cand_v + pt * K, cand_i + pt * K, nl * K, K, top_v, top_i, lv, li, &sh[0]);
   if (use_thr) {
     // degenerate plane (fewer than K non-negative pixels): its top-k also holds negatives
     int nn = 0;
-    for (int c = threadIdx.x; c < nl; c += 256) nn += tile_nonneg[pt + c];
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) nn += (int)threadIdx.x + 256 * k < nl ? tn[k] : 0;
+    for (int c = threadIdx.x + 256 * UPT; c < nl; c += 256) nn += tile_nonneg[pt + c];
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) nn += __shfl_xor(nn, off);
     if (lane == 0) sh[4 + wave] = nn;
@@ -417,7 +435,12 @@ __global__ __launch_bounds__(256) void plane_top_kernel(DetectGeom g, float thr,
   for (int st = threadIdx.x; st < S; st += 256) band_cnt[st] = 0;
   __syncthreads();
   if (use_thr) {
-    for (int idx = threadIdx.x; idx < nl; idx += 256) {
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+      const int idx = threadIdx.x + 256 * k;
+      if (idx < nl && tc[k]) atomicAdd(&band_cnt[idx / g.nsx], tc[k]);
+    }
+    for (int idx = threadIdx.x + 256 * UPT; idx < nl; idx += 256) {
       const int v = tile_count[pt + idx];
       if (v) atomicAdd(&band_cnt[idx / g.nsx], v);
     }
@@ -457,9 +480,41 @@ __global__ __launch_bounds__(256) void emit_kernel(const float* __restrict__ s, 
                                                    DetectWs w, int64_t* __restrict__ det,
                                                    float* __restrict__ scores, int* __restrict__ n_det, int cap) {
   __shared__ int top_i[KCAP], top_bit[KCAP], sh[4];
+  __shared__ int band_n[MAXB], band_off[MAXB];
+  __shared__ unsigned band_nz[MAXB][2];      // non-empty strips of each band (bit = strip, nsx <= 64)
   const int pl = blockIdx.x, J = g.J, b = pl / J, t = pl - b * J;
   const int H = g.H, W = g.W, S = g.S;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // every per-plane input is requested up front (one memory round trip): band counts and offsets,
+  // unit counts (first 4 x 256 units), then the image's per-type counts (wave 0)
+  const size_t pt = (size_t)pl * g.units;
+  constexpr int UPT = 4;
+  int tc[UPT];
+#pragma unroll
+  for (int k = 0; k < UPT; ++k) tc[k] = w.tile_count[pt + min((int)threadIdx.x + 256 * k, g.units - 1)];
+  const int bn = (int)threadIdx.x < S ? w.pstrip[(size_t)pl * S + threadIdx.x] : 0;
+  const int bo = (int)threadIdx.x < S ? w.pstrip_off[(size_t)pl * S + threadIdx.x] : 0;
+  if ((int)threadIdx.x < S) {
+    band_n[threadIdx.x] = bn;
+    band_off[threadIdx.x] = bo;
+    band_nz[threadIdx.x][0] = 0u;
+    band_nz[threadIdx.x][1] = 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < UPT; ++k) {
+    const int idx = threadIdx.x + 256 * k;
+    if (idx < g.units && tc[k] > 0) {
+      const int band = idx / g.nsx, sx = idx - band * g.nsx;
+      atomicOr(&band_nz[band][sx >> 5], 1u << (sx & 31));
+    }
+  }
+  for (int idx = threadIdx.x + 256 * UPT; idx < g.units; idx += 256) {
+    if (w.tile_count[pt + idx] > 0) {
+      const int band = idx / g.nsx, sx = idx - band * g.nsx;
+      atomicOr(&band_nz[band][sx >> 5], 1u << (sx & 31));
+    }
+  }
   if (wave == 0) {
     // J <= 32: one lane per type of this image
     const int nt = lane < J ? w.pn_top[b * J + lane] : 0, nh = lane < J ? w.pn_thr[b * J + lane] : 0;
@@ -496,18 +551,31 @@ __global__ __launch_bounds__(256) void emit_kernel(const float* __restrict__ s, 
   // plus the set bits below it (mbcnt).
   __shared__ uint16_t cm_sh[4][64][64];
   __shared__ int nz_sh[4][64];
-  for (int st = wave; st < S; st += 4) {
-    if (w.pstrip[(size_t)pl * S + st] == 0) continue;     // wave-uniform
+  // non-empty bands, round-robin over the waves (the wave's k-th band is the (4k + wave)-th one)
+  int kb = 0;
+  for (int st = 0; st < S; ++st) {
+    if (band_n[st] == 0) continue;                       // uniform
+    if ((kb++ & 3) != wave) continue;
     const int ry0 = st * SR, rows = min(SR, H - ry0);
-    int pos = thr_base + w.pstrip_off[(size_t)pl * S + st];
+    int pos = thr_base + band_off[st];
     const float* plane = s + (size_t)pl * H * W;
     const size_t u0 = ((size_t)pl * g.nb + st) * g.nsx;   // first unit of the band (nsx <= 64)
-    const unsigned long long nzm = __ballot(lane < g.nsx && w.tile_count[u0 + lane] > 0);
+    const unsigned long long nzm = (unsigned long long)band_nz[st][0] | ((unsigned long long)band_nz[st][1] << 32);
     int nnz = 0;
     unsigned rows_any = 0;
+    unsigned cms[4];
+    {                                                    // the first 4 strips' column masks together
+      unsigned long long m = nzm;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int sx = m ? __builtin_ctzll(m) : 0;
+        cms[k] = cbits[(u0 + sx) * 64 + lane];
+        if (m) m &= m - 1;
+      }
+    }
     for (unsigned long long m = nzm; m; m &= m - 1) {
       const int sx = __builtin_ctzll(m);
-      const unsigned cm = cbits[(u0 + sx) * 64 + lane];
+      const unsigned cm = nnz < 4 ? cms[nnz & 3] : cbits[(u0 + sx) * 64 + lane];
       cm_sh[wave][nnz][lane] = (uint16_t)cm;
       if (lane == 0) nz_sh[wave][nnz] = sx;
       unsigned ra = cm;

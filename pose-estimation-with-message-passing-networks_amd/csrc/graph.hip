@@ -339,7 +339,8 @@ struct FusedGraphArgs {
   const int64_t* det;
   const float *det_sc, *feat, *tags;
   float norm;
-  int64_t n_total, e_total;
+  int64_t n_total, e_total;   // exact totals, or capacities (capacity mode)
+  int capacity;               // 1: totals come from n_det on the device; nothing is written if they exceed
   int node_blocks;
   float *x, *jsc, *jtag, *edge_attr;
   int64_t *jdet, *bidx, *ei;
@@ -374,6 +375,11 @@ __global__ __launch_bounds__(256) void fused_fully_graph_kernel(FusedGraphArgs a
     if (lane == 0) { noff[B] = cn; eoff[B] = ce; }
   }
   __syncthreads();
+  // capacity mode (launched before the host has read the counts back): device totals; a batch that
+  // does not fit writes nothing and the host rebuilds it with exact sizes
+  const int64_t n_total = a.capacity ? (int64_t)noff[B] : a.n_total;
+  const int64_t e_total = a.capacity ? (int64_t)eoff[B] : a.e_total;
+  if (a.capacity && (n_total > a.n_total || e_total > a.e_total)) return;
   auto seg = [&](const long long* off, long long v) {
     int lo = 0, hi = B - 1;
     while (lo < hi) {
@@ -383,7 +389,7 @@ __global__ __launch_bounds__(256) void fused_fully_graph_kernel(FusedGraphArgs a
     return lo;
   };
   if ((int)blockIdx.x < a.node_blocks) {   // ---- nodes ----
-    const int64_t total = a.n_total * a.C;
+    const int64_t total = n_total * a.C;
     for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)a.node_blocks * 256) {
       const int64_t g = idx / a.C;
       const int c = (int)(idx - g * a.C);
@@ -403,16 +409,16 @@ __global__ __launch_bounds__(256) void fused_fully_graph_kernel(FusedGraphArgs a
   }
   // ---- edges ----
   const int eb = blockIdx.x - a.node_blocks, nbe = gridDim.x - a.node_blocks;
-  for (int64_t base = (int64_t)eb * 256; base < a.e_total; base += (int64_t)nbe * 256) {
+  for (int64_t base = (int64_t)eb * 256; base < e_total; base += (int64_t)nbe * 256) {
     const int64_t e = base + threadIdx.x;
-    if (e < a.e_total) {
+    if (e < e_total) {
       const int b = seg(eoff, e);
       const int64_t n = noff[b + 1] - noff[b];
       const int64_t el = e - eoff[b];
       const int64_t i = el / (n - 1), r = el - i * (n - 1);
       const int64_t j = r < i ? r : r + 1;                 // all (i, j), i != j, sorted by (i, j)
       a.ei[e] = noff[b] + i;
-      a.ei[a.e_total + e] = noff[b] + j;
+      a.ei[e_total + e] = noff[b] + j;
       const int64_t* ds = a.det + ((size_t)b * a.cap + i) * 3;   // source = edge_index[0]
       const int64_t* dd = a.det + ((size_t)b * a.cap + j) * 3;   // target = edge_index[1]
       const int64_t sx = ds[0], sy = ds[1], dx = dd[0], dy = dd[1];
@@ -427,7 +433,7 @@ __global__ __launch_bounds__(256) void fused_fully_graph_kernel(FusedGraphArgs a
       }
     }
     __syncthreads();
-    const int cnt = (int)min<int64_t>(256, a.e_total - base), total = cnt * a.A;
+    const int cnt = (int)min<int64_t>(256, e_total - base), total = cnt * a.A;
     float* o = a.edge_attr + base * a.A;
     for (int k = threadIdx.x; k < total; k += 256) {
       const int el = k / a.A, f = k - el * a.A;
@@ -464,11 +470,37 @@ static int ef_width(int mode, int J) {
   }
 }
 
+static int fully_graph_build(const int32_t* n_det, int B, const int64_t* det_xyt, const float* det_scores, int cap,
+                             const float* features, int C, const float* tagmaps, int F, int J, int H, int W,
+                             int64_t n_total, int64_t e_total, float norm_factor, int mode, float* x,
+                             int64_t* joint_det, float* joint_scores, int64_t* batch_index, float* joint_tags,
+                             int64_t* edge_index, float* edge_attr, int capacity, void* stream);
+
 extern "C" int pemp_fully_graph_build(const int32_t* n_det, int B, const int64_t* det_xyt, const float* det_scores,
                                       int cap, const float* features, int C, const float* tagmaps, int F, int J,
                                       int H, int W, int64_t n_total, int64_t e_total, float norm_factor, int mode,
                                       float* x, int64_t* joint_det, float* joint_scores, int64_t* batch_index,
                                       float* joint_tags, int64_t* edge_index, float* edge_attr, void* stream) {
+  return fully_graph_build(n_det, B, det_xyt, det_scores, cap, features, C, tagmaps, F, J, H, W, n_total, e_total,
+                           norm_factor, mode, x, joint_det, joint_scores, batch_index, joint_tags, edge_index,
+                           edge_attr, 0, stream);
+}
+
+extern "C" int pemp_fully_graph_build_cap(const int32_t* n_det, int B, const int64_t* det_xyt, const float* det_scores,
+                                          int cap, const float* features, int C, const float* tagmaps, int F, int J,
+                                          int H, int W, int64_t n_cap, int64_t e_cap, float norm_factor, int mode,
+                                          float* x, int64_t* joint_det, float* joint_scores, int64_t* batch_index,
+                                          float* joint_tags, int64_t* edge_index, float* edge_attr, void* stream) {
+  return fully_graph_build(n_det, B, det_xyt, det_scores, cap, features, C, tagmaps, F, J, H, W, n_cap, e_cap,
+                           norm_factor, mode, x, joint_det, joint_scores, batch_index, joint_tags, edge_index,
+                           edge_attr, 1, stream);
+}
+
+static int fully_graph_build(const int32_t* n_det, int B, const int64_t* det_xyt, const float* det_scores, int cap,
+                             const float* features, int C, const float* tagmaps, int F, int J, int H, int W,
+                             int64_t n_total, int64_t e_total, float norm_factor, int mode, float* x,
+                             int64_t* joint_det, float* joint_scores, int64_t* batch_index, float* joint_tags,
+                             int64_t* edge_index, float* edge_attr, int capacity, void* stream) {
   PEMP_CHECK_ARG(n_det && det_xyt && det_scores && features && x && joint_det && joint_scores && batch_index,
                  "pemp_fully_graph_build: null pointer");
   PEMP_CHECK_ARG(B > 0 && B <= FUSED_MAXB && C > 0 && J > 0 && H > 0 && W > 0 && n_total >= 0 && e_total >= 0,
@@ -481,7 +513,7 @@ extern "C" int pemp_fully_graph_build(const int32_t* n_det, int B, const int64_t
   FusedGraphArgs a{};
   a.n_det = n_det; a.B = B; a.cap = cap; a.C = C; a.F = F; a.J = J; a.H = H; a.W = W; a.mode = mode; a.A = A;
   a.det = det_xyt; a.det_sc = det_scores; a.feat = features; a.tags = tagmaps; a.norm = norm_factor;
-  a.n_total = n_total; a.e_total = e_total;
+  a.n_total = n_total; a.e_total = e_total; a.capacity = capacity;
   a.node_blocks = grid_for(n_total * C, 256, 4096);
   const int edge_blocks = e_total > 0 ? grid_for(e_total, 256, 8192) : 0;
   a.x = x; a.jsc = joint_scores; a.jtag = joint_tags; a.edge_attr = edge_attr;

@@ -31,6 +31,25 @@ class NaiveGraphConstructor:
     _ws_detect = _lib.Workspace()
     _ws_knn = _lib.Workspace()
     _cap = 512   # detections per image kept between calls (grows on overflow)
+    _graph_hint = {}   # (shape key) -> (node, edge) capacities of the fully-graph capacity build
+    _pinned = {}
+    _events = {}
+
+    @classmethod
+    def _pinned_counts(cls, B):
+        buf = cls._pinned.get("counts")
+        if buf is None or buf.numel() < B:
+            buf = torch.empty(max(B, 64), dtype=torch.int32, pin_memory=True)
+            cls._pinned["counts"] = buf
+        return buf[:B]
+
+    @classmethod
+    def _copy_event(cls, dev):
+        ev = cls._events.get(dev)
+        if ev is None:
+            ev = torch.cuda.Event()
+            cls._events[dev] = ev
+        return ev
 
     def __init__(self, scoremaps, tagmaps, features, joints_gt, factor_list, masks, device, config, testing,
                  heatmaps, num_joints):
@@ -109,8 +128,35 @@ class NaiveGraphConstructor:
         A = {0: J + 2, 1: J, 2: 1, 3: 2, 4: J + 3}[mode]
         norm = float(max(W, H)) if self.normalize_node_distance else 1.0
 
-        counts_l = n_det.tolist()                           # the one host read-back of the batch
+        fully = self.mpn_graph_type == "fully" and B <= 1024
+        gkey = (B, J, H, W, C, F, A, dev)
+        hint = NaiveGraphConstructor._graph_hint.get(gkey) if fully else None
+        built = None
+        if hint is not None:
+            # capacity mode: the graph build is queued behind the count copy, so the GPU builds the
+            # graph while the host waits for (and reads) the counts (pemp_fully_graph_build_cap)
+            n_cap, e_cap = hint
+            host = self._pinned_counts(B)
+            host.copy_(n_det, non_blocking=True)
+            ev = self._copy_event(dev)
+            ev.record(torch.cuda.current_stream(dev))
+            bufs = (torch.empty(n_cap, C, dtype=torch.float32, device=dev),
+                    torch.empty(n_cap, 3, dtype=torch.int64, device=dev),
+                    torch.empty(n_cap, dtype=torch.float32, device=dev),
+                    torch.empty(n_cap, dtype=torch.int64, device=dev),
+                    torch.empty(n_cap, F, dtype=torch.float32, device=dev) if tags is not None else None,
+                    torch.empty(2 * e_cap, dtype=torch.int64, device=dev),
+                    torch.empty(e_cap, A, dtype=torch.float32, device=dev))
+            _lib.check(L.pemp_fully_graph_build_cap(
+                _lib.ptr(n_det), B, _lib.ptr(det), _lib.ptr(dsc), cap, _lib.ptr(feats), C, _lib.ptr(tags), F, J, H, W,
+                n_cap, e_cap, norm, mode, *[_lib.ptr(t) for t in bufs], st))
+            ev.synchronize()
+            counts_l = host.tolist()
+            built = bufs
+        else:
+            counts_l = n_det.tolist()                       # the one host read-back of the batch
         mx = max(counts_l) if counts_l else 0
+        cap_used = cap                                      # the detections the capacity build read
         if mx > cap:
             cap = mx
             NaiveGraphConstructor._cap = max(NaiveGraphConstructor._cap, cap)
@@ -120,13 +166,29 @@ class NaiveGraphConstructor:
                                      int(use_thr), topk, 2, _lib.ptr(ws), ws.numel(), _lib.ptr(det), _lib.ptr(dsc),
                                      _lib.ptr(n_det), cap, st))
         N = sum(counts_l)
+        E_fully = sum(c * (c - 1) for c in counts_l if c > 1)
+        if fully:   # capacities for the next batch of this shape: 25 % headroom over this one
+            n_hint = (N + N // 4 + 16, E_fully + E_fully // 4 + 256)
+            old = NaiveGraphConstructor._graph_hint.get(gkey)
+            NaiveGraphConstructor._graph_hint[gkey] = n_hint if old is None else (max(old[0], n_hint[0]),
+                                                                                 max(old[1], n_hint[1]))
+        if built is not None and mx <= cap_used and N <= built[0].shape[0] and E_fully <= built[6].shape[0]:
+            # the capacity build fit: the outputs are leading (contiguous) slices of its buffers
+            x, joint_det, joint_scores, batch_index = built[0][:N], built[1][:N], built[2][:N], built[3][:N]
+            joint_tags = built[4][:N] if tags is not None else None
+            edge_index = built[5][:2 * E_fully].view(2, E_fully)
+            edge_attr = built[6][:E_fully]
+            if tags is not None:
+                joint_tags = joint_tags.view((N,) + tuple(tags.shape[4:])) if tags.dim() > 4 else joint_tags.view(N)
+            return (x, edge_attr, edge_index, None, None, None, None, joint_det, None, None, None, joint_scores,
+                    batch_index, None, joint_tags)
         x = torch.empty(N, C, dtype=torch.float32, device=dev)
         joint_det = torch.empty(N, 3, dtype=torch.int64, device=dev)
         joint_scores = torch.empty(N, dtype=torch.float32, device=dev)
         batch_index = torch.empty(N, dtype=torch.int64, device=dev)
         joint_tags = torch.empty(N, F, dtype=torch.float32, device=dev) if tags is not None else None
 
-        if self.mpn_graph_type == "fully" and B <= 1024:
+        if fully:
             # one launch: offsets + nodes + edge_index + edge_attr (pemp_fully_graph_build)
             E = sum(c * (c - 1) for c in counts_l if c > 1)
             edge_index = torch.empty(2, E, dtype=torch.int64, device=dev)

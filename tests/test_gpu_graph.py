@@ -79,3 +79,21 @@ def test_empty_image_and_overflow_growth():
     for i in (7, 11, 12, 2, 1):
         assert torch.equal(out[i].cpu(), ref[i])
     assert out[14] is None
+
+
+def test_capacity_build_fit_and_overflow():
+    """Repeated batches of one shape take the capacity build (pemp_fully_graph_build_cap, launched
+    before the count read-back); a batch larger than the capacities falls back to the exact build.
+    Every call must equal the oracle bit for bit."""
+    B, J, H, W = 2, 17, 96, 96
+    gc = pcfg.inference_gc_config("fully", 5, False)
+    feats = torch.from_numpy(syn.closed_form((B, 128, H, W), 0.25))
+    tags = torch.from_numpy(syn.closed_form((B, J, H, W, 1), 0.75))
+    # persons: first call sets the capacities, then smaller (fits), equal, then larger (overflow)
+    for seed, persons in ((1, 3), (2, 2), (3, 3), (4, 6), (5, 1)):
+        hm = torch.from_numpy(syn.make_heatmaps(seed, B, J, H, W, persons, margin=4))
+        out = run_gc(gc, J, hm, feats, tags, None)
+        ref = restate.construct_graph(hm, feats, tags, None, gc, J)
+        for i in (0, 1, 2, 7, 11, 12, 14):
+            assert out[i].is_contiguous()
+            assert torch.equal(out[i].cpu(), ref[i]), (seed, i)
