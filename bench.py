@@ -37,9 +37,9 @@ FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: dense f32 MFMA (= f32 
 HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 BF16_MFMA_PEAK_TFLOPS = 2500.0     # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
 REF_EDGE_FLOP = 82048              # the reference's FLOP per edge-update (before the node/edge split)
-EDGE_FLOP = 3 * 2 * 64 * 64 + 2 * 64            # per edge-update: 3 chained 64x64 GEMMs + attention
+GEMM64 = 2 * 64 * 64                            # one 64x64 GEMM per edge
 EDGE_HEAD_FLOP = 2 * (64 * 64 + 64 * 32 + 32)   # fused edge-classification head
-EDGE_BYTES = 3 * 64 * 4 + 2 * 4                 # Q0 + e_cur read, e' write, (src, dst) int32
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_latest.json")   # tools/gpu_profile.sh + tools/pmc_json.py
 
 
 def parse():
@@ -87,15 +87,37 @@ def run_step(wl, gc, model, hm, feats, tags, dev):
     return out, pe, pn, pc
 
 
-def roofline_for(label, stats, E, wl, precision):
+def edge_pass_cost(head, upd):
+    """Executed FLOP and algorithmic HBM bytes per edge of one edge pass (mpn.hip edge_step_kernel).
+    A middle pass (no head) computes e' = ReLU(W2 h + b2) from h = ReLU(r + A[dst] + B[src]), the
+    message W_t e', the update block U_t m (upd), the next r = Q0 + W1_e e', and the attention dot;
+    it reads r and Q0 (2 x 256 B) and writes the next r (256 B) plus 2 int32 indices. The last pass
+    (head) drops the next r and Q0 and runs the fused edge head, writing a 4 B logit."""
+    gemms = 2 + (1 if upd else 0) + (0 if head else 1)
+    flop = gemms * GEMM64 + 2 * 64 + (EDGE_HEAD_FLOP if head else 0)
+    byts = (256 + 8 + 4) if head else (2 * 256 + 256 + 8)
+    return flop, byts
+
+
+def pmc_traffic(kernel_prefix):
+    """HBM bytes per dispatch of the kernel from the committed PMC passes (profiles/pmc_latest.json),
+    or None when no pass covers it."""
+    try:
+        ks = json.load(open(PMC_FILE))["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    hits = [v for k, v in ks.items() if k.startswith(kernel_prefix)]
+    return hits[0]["bytes"] if len(hits) == 1 else None
+
+
+def roofline_for(label, stats, E, wl, precision, upd):
     """Roofline of the dominant kernel from its measured average launch time.
 
-    edge_step*: per edge-update 24,704 FLOP executed (3 chained 64x64 GEMMs + attention dot; the
-    edge head adds 12,352) and ALGORITHMIC HBM bytes Q0 + e_cur read (2 x 256 B), e' write (256 B,
-    not on the last iteration; the head writes a 4 B logit instead) and 2 int32 indices; node-table
-    gathers are L2-resident and not counted. fp32: bound = fp32 MFMA peak. bf16x3: the MFMA work
+    edge_step*: executed FLOP and ALGORITHMIC HBM bytes per edge from edge_pass_cost (node-table
+    gathers are L2-resident and not counted). fp32: bound = fp32 MFMA peak. bf16x3: the MFMA work
     is 3 bf16 products per fp32 product, so the compute floor is 3 x FLOP / bf16 dense peak; the
-    bound reported is whichever floor (compute, HBM) is larger."""
+    bound reported is whichever floor (compute, HBM) is larger. `traffic` = measured HBM bytes per
+    launch (PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_latest.json)."""
     if label not in stats:
         return None
     n, ms = stats[label]
@@ -103,11 +125,13 @@ def roofline_for(label, stats, E, wl, precision):
     B, J, H, W = wl["B"], wl["J"], wl["H"], wl["W"]
     if label.startswith("edge_step"):
         head = label == "edge_step_head"
-        flop = E * (EDGE_FLOP + (EDGE_HEAD_FLOP if head else 0))
-        byts = E * (2 * 256 + 8 + (4 + 4 if head else 256))
+        f1, b1 = edge_pass_cost(head, upd)
+        flop, byts = E * f1, E * b1
         gbs = byts / avg_s / 1e9
-        common = {"kernel": label, "avg_launch_us": round(avg_s * 1e6, 2), "launches": n, "traffic": None,
-                  "algorithmic": f"{flop // E} FLOP and {byts // E} B HBM x E={E} edges per launch",
+        traffic = pmc_traffic("pemp::edge_step_kernel<0," + ("1" if head else "0"))
+        common = {"kernel": label, "avg_launch_us": round(avg_s * 1e6, 2), "launches": n, "traffic": traffic,
+                  "traffic_source": "profiles/pmc_latest.json" if traffic else None,
+                  "algorithmic": f"{f1} FLOP and {b1} B HBM x E={E} edges per launch",
                   "tflops_executed": round(flop / avg_s / 1e12, 2), "hbm_GBs_algorithmic": round(gbs, 1),
                   "ref_equiv_tflops": round(E * REF_EDGE_FLOP / avg_s / 1e12, 2), "precision": precision}
         if precision == "fp32":
@@ -125,9 +149,12 @@ def roofline_for(label, stats, E, wl, precision):
     if label == "detect_nms":
         byts = B * J * H * W * 4
         ach = byts / avg_s / 1e9
+        traffic = pmc_traffic("pemp::nms_strips_kernel")
         return {"kernel": label, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "avg_launch_us": round(avg_s * 1e6, 2),
-                "launches": n, "algorithmic": f"{byts} B per launch (heatmap read once)"}
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_source": "profiles/pmc_latest.json" if traffic else None,
+                "avg_launch_us": round(avg_s * 1e6, 2), "launches": n,
+                "algorithmic": f"{byts} B per launch (heatmap read once)"}
     return {"kernel": label, "avg_launch_us": round(avg_s * 1e6, 2), "launches": n}
 
 
@@ -233,7 +260,8 @@ def main():
     dt_mpn = max_over_ranks(time.perf_counter() - t1, world, dev)
     mpn_eups = E_all * wl["steps"] * args.steps / dt_mpn
 
-    roof = roofline_for(dominant, stats_timed, E, wl, model.precision) if dominant else None
+    upd = wl["variant"] in ("attn", "mean")      # update block pre-applied in the edge pass (mpn.hip UPD)
+    roof = roofline_for(dominant, stats_timed, E, wl, model.precision, upd) if dominant else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(wl, gc, model, hm, feats, tags, args.cpu_seconds)

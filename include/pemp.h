@@ -188,6 +188,8 @@ typedef struct pemp_mpn_weights {
                               [2][out_pad16][in_pad32], concatenated; or NULL (embedding stays fp32) */
   const uint16_t* upd_bf;  /* per type t: U_t = upd_w[:, 64 t : 64 t + 64] as [T][2][64][64], or NULL */
   const uint16_t* pre_bf;  /* node table weights [2][128 + T*64][128] (K = 128, 4 slot blocks), or NULL */
+  const float* node_img;   /* node embedding + head weights in the kernels' LDS layout (pemp_mpn_node_image),
+                              or NULL: then every forward builds it in its workspace */
 } pemp_mpn_weights;
 
 typedef struct pemp_mpn_desc {
@@ -201,7 +203,10 @@ typedef struct pemp_mpn_desc {
   int32_t node_in_dim;    /* NODE_INPUT_DIM */
   int32_t precision;      /* PEMP_PREC_* */
   int32_t types_stride;   /* element stride of node_types (e.g. 3 for joint_det[:, 2]); 0 or 1 = dense */
+  int32_t flags;          /* PEMP_MPN_PREPARED: pemp_mpn_prepare already ran on this workspace and stream */
 } pemp_mpn_desc;
+
+#define PEMP_MPN_PREPARED 1
 
 size_t pemp_mpn_workspace_size(const pemp_mpn_desc* desc, int64_t N, int64_t E);
 /* x [N,node_in_dim], edge_attr [E,edge_attr_dim], edge_index [2,E] (row 0 source j, row 1
@@ -214,6 +219,19 @@ int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weights* weights,
                      const float* edge_attr, const int64_t* edge_index, const int64_t* node_types,
                      int64_t N, int64_t E, float* edge_logits, float* node_logits, float* class_logits,
                      void* workspace, size_t workspace_bytes, void* stream);
+
+/* The edge-ordering part of pemp_mpn_forward (type-major counting sort of edge_index by (source type,
+ * target)), callable ahead of it: it needs no weights, so a caller can queue it as soon as the graph
+ * exists and then call pemp_mpn_forward with desc->flags |= PEMP_MPN_PREPARED on the same workspace
+ * and stream. */
+int pemp_mpn_prepare(const pemp_mpn_desc* desc, const int64_t* edge_index, const int64_t* node_types, int64_t N,
+                     int64_t E, void* workspace, size_t workspace_bytes, void* stream);
+
+/* The node embedding / node head / class head weights in the node kernels' LDS layout, built once
+ * per weight set (stream-ordered) instead of once per forward: image of
+ * pemp_mpn_node_image_floats(weights) floats, then weights->node_img = image. */
+size_t pemp_mpn_node_image_floats(const pemp_mpn_weights* weights);
+int pemp_mpn_node_image(const pemp_mpn_weights* weights, float* image, size_t floats, void* stream);
 
 /* Synchronises `stream` and reports invalid edge_index / node_types seen by the last
  * pemp_mpn_forward on this workspace (those edges were skipped). Optional validation step. */

@@ -30,13 +30,13 @@ class PempMpnWeights(ctypes.Structure):
                 ("edge_head", PempMlp), ("node_head", PempMlp), ("class_head", PempMlp),
                 ("attn_b", c_f32), ("pad_", c_i32),
                 ("e1_bf", c_p), ("e2_bf", c_p), ("msg_bf", c_p), ("head_bf", c_p), ("emb_bf", c_p),
-                ("upd_bf", c_p), ("pre_bf", c_p)]
+                ("upd_bf", c_p), ("pre_bf", c_p), ("node_img", c_p)]
 
 
 class PempMpnDesc(ctypes.Structure):
     _fields_ = [("num_types", c_i32), ("num_joints", c_i32), ("steps", c_i32), ("aux_loss_steps", c_i32),
                 ("aggr", c_i32), ("hidden", c_i32), ("edge_attr_dim", c_i32), ("node_in_dim", c_i32),
-                ("precision", c_i32), ("types_stride", c_i32)]
+                ("precision", c_i32), ("types_stride", c_i32), ("flags", c_i32)]
 
 
 # name -> (restype, argtypes); every symbol of include/pemp.h
@@ -62,6 +62,9 @@ SIGNATURES = {
     "pemp_mpn_workspace_size": (c_sz, [ctypes.POINTER(PempMpnDesc), c_i64, c_i64]),
     "pemp_mpn_forward": (c_i32, [ctypes.POINTER(PempMpnDesc), ctypes.POINTER(PempMpnWeights), c_p, c_p, c_p, c_p,
                                  c_i64, c_i64, c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "pemp_mpn_prepare": (c_i32, [ctypes.POINTER(PempMpnDesc), c_p, c_p, c_i64, c_i64, c_p, c_sz, c_p]),
+    "pemp_mpn_node_image_floats": (c_sz, [ctypes.POINTER(PempMpnWeights)]),
+    "pemp_mpn_node_image": (c_i32, [ctypes.POINTER(PempMpnWeights), c_p, c_sz, c_p]),
     "pemp_mpn_status": (c_i32, [ctypes.POINTER(PempMpnDesc), c_i64, c_i64, c_p, c_p]),
     "pemp_prof_enable": (c_i32, [ctypes.c_char_p]),
     "pemp_prof_report": (c_i32, [ctypes.c_char_p, c_sz]),

@@ -73,6 +73,11 @@ ProfScope::~ProfScope() {
   (void)hipEventRecord(g_pending[slot_].b, st_);
 }
 
+bool prof_active() {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  return !g_prof_filter.empty();
+}
+
 }  // namespace pemp
 
 extern "C" int pemp_prof_enable(const char* filter) {

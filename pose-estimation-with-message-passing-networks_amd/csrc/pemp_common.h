@@ -33,6 +33,9 @@ void set_error(const char* fmt, ...);
 // kernel by source line (fault localisation in one run; never on in measured runs).
 bool debug_sync();
 
+// true while the opt-in event profiler records (its hipEvent calls must not be graph-captured)
+bool prof_active();
+
 #define PEMP_LAUNCH_CHECK()                                                        \
   do {                                                                             \
     hipError_t e_ = hipGetLastError();                                             \

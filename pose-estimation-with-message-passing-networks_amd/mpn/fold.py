@@ -196,4 +196,12 @@ def fold_weights(model, device) -> Folded:
         if U.shape == (64, 64 * T):
             s.upd_bf = f.dev_raw(torch.stack([bf16_pack(U[:, 64 * t:64 * t + 64]) for t in range(T)], 0),
                                  device).data_ptr()
+    # node embedding / head weights in the node kernels' LDS layout, built once per weight set
+    L = _lib.lib()
+    n = L.pemp_mpn_node_image_floats(f.struct_ref)
+    if n:
+        img = torch.empty(n, dtype=torch.float32, device=device)
+        _lib.check(L.pemp_mpn_node_image(f.struct_ref, img.data_ptr(), n, _lib.stream(device)))
+        f.tensors.append(img)
+        s.node_img = img.data_ptr()
     return f

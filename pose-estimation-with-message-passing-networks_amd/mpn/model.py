@@ -198,7 +198,6 @@ class NodeClassificationMPNSimple(nn.Module):
         if node_types.dim() != 1 or (N > 0 and node_types.stride(0) < 1):
             node_types = node_types.reshape(-1).contiguous()
         t_stride = node_types.stride(0) if N > 0 else 1       # joint_det[:, 2] is read in place
-        fw = self._weights(dev)
         if self.precision not in PRECISIONS:
             raise ValueError(f"precision={self.precision!r}: expected one of {sorted(PRECISIONS)}")
         A = edge_attr.shape[1] if edge_attr.dim() == 2 else 1
@@ -207,17 +206,19 @@ class NodeClassificationMPNSimple(nn.Module):
             steps, aux = self.edge_steps, self.aux_loss_steps
             self._n_rec = sum(1 for i in range(steps) if i >= steps - aux - 1)
             self._desc = _lib.PempMpnDesc(self.num_types, self.num_joints, steps, aux, self.aggr_code, 64, A,
-                                          x.shape[1], PRECISIONS[self.precision], t_stride)
+                                          x.shape[1], PRECISIONS[self.precision], t_stride, 0)
             self._desc_ref = ctypes.byref(self._desc)
             self._desc_key = dkey
         desc, n_rec = self._desc_ref, self._n_rec
+        ws = self._ws.get(L.pemp_mpn_workspace_size(desc, N, E), dev)
+        st = _lib.stream(dev)
+        fw = self._weights(dev)
         edge_logits = torch.empty(max(n_rec, 1), E, dtype=torch.float32, device=dev)
         node_logits = torch.empty(n_rec + 1, N, dtype=torch.float32, device=dev)
         class_logits = torch.empty(n_rec + 1, N, self.num_joints, dtype=torch.float32, device=dev)
-        ws = self._ws.get(L.pemp_mpn_workspace_size(desc, N, E), dev)
         _lib.check(L.pemp_mpn_forward(desc, fw.struct_ref, x.data_ptr(), edge_attr.data_ptr(), edge_index.data_ptr(),
                                       node_types.data_ptr(), N, E, edge_logits.data_ptr(), node_logits.data_ptr(),
-                                      class_logits.data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream(dev)))
+                                      class_logits.data_ptr(), ws.data_ptr(), ws.numel(), st))
         if kwargs.get("validate", _VALIDATE):
             _lib.check(L.pemp_mpn_status(desc, N, E, _lib.ptr(ws), _lib.stream(dev)))
         # list lengths and .squeeze() semantics of NodeClassificationMPNSimple.py:81-97

@@ -12,3 +12,4 @@ timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$rx" --outp
   python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-roofline > gpurun_out/${tag}_pmc_fetch.log 2>&1
 timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$rx" --output-format csv -d gpurun_out/${tag}_pmc_write -o pmc -- \
   python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-roofline > gpurun_out/${tag}_pmc_write.log 2>&1
+python tools/pmc_json.py gpurun_out/${tag}_pmc.json gpurun_out/${tag}_pmc_*/pmc_counter_collection.csv > /dev/null
