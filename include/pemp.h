@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define PEMP_ABI_VERSION 3
+#define PEMP_ABI_VERSION 4
 
 enum {
   PEMP_OK = 0,
@@ -170,7 +170,7 @@ typedef struct pemp_mpn_weights {
   const float* e2_w;   /* [64][64]  mlp_edge.2    */
   const float* e2_b;   /* [64]                    */
   const float* msg_w;  /* [T][64][64] W_t[:, e'] */
-  const float* attn_w; /* [64] attn_net.0.weight (PEMP_AGGR_ATTN) */
+  const float* attn_w; /* [64] attn_net.0.weight (PEMP_AGGR_ATTN); [17][64] when attn_bv is set */
   const float* upd_w;  /* [64][T*64] update_mlp.0.weight, or NULL (x_new = agg) */
   const float* upd_b;  /* [64] */
   pemp_mlp edge_head;  /* 64 -> .. -> 1 */
@@ -190,6 +190,9 @@ typedef struct pemp_mpn_weights {
   const uint16_t* pre_bf;  /* node table weights [2][128 + T*64][128] (K = 128, 4 slot blocks), or NULL */
   const float* node_img;   /* node embedding + head weights in the kernels' LDS layout (pemp_mpn_node_image),
                               or NULL: then every forward builds it in its workspace */
+  const float* attn_bv;    /* AGGR_SUB node_edge_attn_per_type (layers.py:199-201, 245-246): [17] attn_net.0.bias;
+                              messages from source type t use row t of attn_w and attn_bv[t]. NULL: one shared
+                              row attn_w[64] with bias attn_b (node_edge_attn) */
 } pemp_mpn_weights;
 
 typedef struct pemp_mpn_desc {

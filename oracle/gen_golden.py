@@ -101,7 +101,7 @@ def make_mpn_case(MPN, name, meta, graph):
     torch.manual_seed(0)
     cfg = mpn_cfg(meta)
     model = MPN(cfg)
-    sd = syn.closed_form_state_dict(model, meta["salt"])
+    sd = syn.closed_form_state_dict(model, meta["salt"], meta.get("attn_gain", 1.0))
     model.load_state_dict(sd)
     model.eval()
     x, ea, ei, det = graph[0], graph[1], graph[2], graph[7]
@@ -151,18 +151,34 @@ MPN_CASES = {
     "mpn_pertype_max_t2": (dict(J=17, steps=2, variant="attn", salt=8.5, aggr_sub="None", aggr="max"),
                            "gc_small_fully"),
     "mpn_attn_c2_t3": (dict(J=17, steps=3, variant="attn", salt=9.5), "gc_c2_like"),
+    "mpn_attn_pertype_t2": (dict(J=17, steps=2, variant="attn", salt=10.5, aggr_sub="node_edge_attn_per_type",
+                                 aggr="add", attn_gain=16.0), "gc_realistic_knn"),
 }
 
 
-def main():
+def main(only=()):
+    """Regenerate every case, or only the MPN cases named in `only` (their source graphs are rebuilt
+    in memory; graph fixtures are rewritten only when named)."""
     os.makedirs(OUT, exist_ok=True)
     cg, MPN, _ = load_reference()
     graphs = {}
+    mpn_names = [n for n in MPN_CASES if not only or n in only]
+    need = {MPN_CASES[n][1] for n in mpn_names}
     for name, (meta, full) in GC_CASES.items():
-        graphs[name] = make_gc_case(cg, name, dict(meta), full)
-    for name, (meta, src) in MPN_CASES.items():
+        if only and name not in only and name not in need:
+            continue
+        if only and name not in only:    # re-run the reference on the stored case's (final) seed
+            stored = json.loads(str(np.load(os.path.join(OUT, f"{name}.npz"))["meta"]))
+            m = dict(meta, seed=stored["seed"])
+            hm, feats, tags, masks = gc_inputs(m)
+            graphs[name] = run_reference_gc(cg, m, hm, feats, tags, masks)
+            assert sha(graphs[name][2]) == stored["sha_edge_index"], f"{name}: stored fixture not reproduced"
+        else:
+            graphs[name] = make_gc_case(cg, name, dict(meta), full)
+    for name in mpn_names:
+        meta, src = MPN_CASES[name]
         make_mpn_case(MPN, name, dict(meta), graphs[src])
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]))

@@ -260,12 +260,13 @@ def mpn_layer(sd, cfg, x, e, edge_index, node_types):
         if sel.any():
             m[sel] = F.relu(F.linear(xi_e[sel], sd[f"{p}.mlp_node.mlp.{t}.0.weight"], sd[f"{p}.mlp_node.mlp.{t}.0.bias"]))
     upd = torch.zeros(n, num_types, m.shape[1], dtype=m.dtype)
-    if cfg.AGGR_SUB in ("node_edge_attn",):
-        a = F.linear(e_new, sd[f"{p}.attn_net.0.weight"], sd[f"{p}.attn_net.0.bias"])[:, 0]
+    if cfg.AGGR_SUB in ("node_edge_attn", "node_edge_attn_per_type"):    # layers.py:240-251
+        a = F.linear(e_new, sd[f"{p}.attn_net.0.weight"], sd[f"{p}.attn_net.0.bias"])
         for t in range(num_types):
+            col = 0 if cfg.AGGR_SUB == "node_edge_attn" else t        # attn_index, layers.py:245
             sel = src_type == t
             if sel.any():
-                alpha = _segment_softmax(a[sel], i[sel], n)
+                alpha = _segment_softmax(a[sel, col], i[sel], n)
                 upd[:, t] = _scatter(m[sel] * alpha[:, None], i[sel], n, "add")
     else:
         for t in range(num_types):

@@ -115,7 +115,7 @@ def update_config_command(cfg: CfgNode, opts) -> CfgNode:
 
 def published_mpn_config(num_joints: int = 17, steps: int = 10, variant: str = "attn") -> CfgNode:
     """``MODEL.MPN`` of ``experiments/hybrid_class_agnostic_end2end/model_58_4.yaml:91-139`` (variant
-    "attn") or ``experiments/connectivity/fully_54_3.yaml:91-134`` (variant "max")."""
+    "attn"; "attn_per_type" swaps in AGGR_SUB node_edge_attn_per_type) or ``experiments/connectivity/fully_54_3.yaml:91-134`` (variant "max")."""
     mlp = lambda sizes, bn=True: CfgNode({"BN": bn, "END_WITH_RELU": False, "OUTPUT_SIZES": sizes}, True)
     c = get_config().MODEL.MPN
     c.merge({
@@ -129,8 +129,9 @@ def published_mpn_config(num_joints: int = 17, steps: int = 10, variant: str = "
     c.EDGE_CLASS = CfgNode({"BN": True, "OUTPUT_SIZES": [64, 32, 1]}, True)
     c.NODE_CLASS = CfgNode({"BN": True, "OUTPUT_SIZES": [64, 32, 1]}, True)
     c.CLASS = CfgNode({"BN": True, "OUTPUT_SIZES": [64, 32, num_joints]}, True)
-    if variant == "attn":
-        c.merge({"AGGR_TYPE": "per_type", "AGGR": "add", "AGGR_SUB": "node_edge_attn", "UPDATE_TYPE": "mlp"})
+    if variant in ("attn", "attn_per_type"):
+        sub = "node_edge_attn" if variant == "attn" else "node_edge_attn_per_type"
+        c.merge({"AGGR_TYPE": "per_type", "AGGR": "add", "AGGR_SUB": sub, "UPDATE_TYPE": "mlp"})
     else:
         c.merge({"AGGR_TYPE": "agnostic", "AGGR": variant})
     return c

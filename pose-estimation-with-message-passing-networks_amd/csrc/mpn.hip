@@ -822,6 +822,7 @@ struct EdgeStepArgs {
   const float* upd_w;        // UPD 1: update_mlp.0.weight [64][64 T] (U_t = columns 64 t .. 64 t + 63)
   const uint16_t* upd_bf;    // UPD 1, PREC 1: [T][hi | lo][64][64]
   float attn_b;
+  const float* attn_bv;      // per-type attention (node_edge_attn_per_type): bias [17], attn_w [17][64]
   float* agg;
   pemp_mlp head;
   float* edge_logits;
@@ -957,6 +958,7 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
   if (blk >= a.wg_start[T]) return;             // uniform for the block
   int t = 0;
   while (t + 1 < T && a.wg_start[t + 1] <= blk) ++t;
+  const float attn_b = a.attn_bv ? a.attn_bv[t] : a.attn_b;
   {
     if (PREC == 0) {
       const float* srcs[3] = {a.e1_w, a.e2_w, a.msg_w + (int64_t)t * D * D};
@@ -975,7 +977,8 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
       }
     }
     if (threadIdx.x < D) vec[threadIdx.x] = a.e2_b[threadIdx.x];
-    else if (threadIdx.x < 2 * D) vec[threadIdx.x] = (AGG == PEMP_AGGR_ATTN) ? a.attn_w[threadIdx.x - D] : 0.0f;
+    else if (threadIdx.x < 2 * D)   // messages of source type t use attention row t when per-type
+      vec[threadIdx.x] = (AGG == PEMP_AGGR_ATTN) ? a.attn_w[(a.attn_bv ? t * D : 0) + threadIdx.x - D] : 0.0f;
     if (HEAD == 1) {
       if (PREC == 0) {
         for (int idx = threadIdx.x; idx < (D + 32) * 16; idx += 64 * NW) {
@@ -1119,7 +1122,7 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
       }
       av += __shfl_xor(av, 16);
       av += __shfl_xor(av, 32);
-      av += a.attn_b;
+      av += attn_b;
     }
     if (HEAD == 1) {   // fused edge-classification head on e'
       const float* hb = hb_l + z;
@@ -2025,7 +2028,7 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
         ea.emb_off = edge_lds_base(false, upd_fused);
       }
       ea.e1_w = w->e1_w; ea.e2_w = w->e2_w; ea.e2_b = w->e2_b; ea.msg_w = w->msg_w; ea.attn_w = w->attn_w;
-      ea.attn_b = w->attn_b; ea.agg = ws.agg; ea.head = w->edge_head;
+      ea.attn_b = w->attn_b; ea.attn_bv = w->attn_bv; ea.agg = ws.agg; ea.head = w->edge_head;
       ea.e1_bf = w->e1_bf; ea.e2_bf = w->e2_bf; ea.msg_bf = w->msg_bf; ea.head_bf = w->head_bf;
       ea.upd_w = w->upd_w; ea.upd_bf = w->upd_bf;
       ea.edge_logits = record ? edge_logits + (int64_t)rec * E : nullptr;

@@ -185,9 +185,12 @@ def fold_weights(model, device) -> Folded:
         packs = [bf16_pack(W).reshape(-1) for W, _, _ in emb] + [bf16_pack(q0).reshape(-1)]
         s.emb_bf = f.dev_raw(torch.cat(packs), device).data_ptr()
     attn = getattr(layer, "attn_net", None)
-    if attn is not None:
+    if attn is not None and attn[0].out_features == 1:       # node_edge_attn: one shared row
         s.attn_w = f.dev(attn[0].weight.detach().double().cpu().reshape(64), device).data_ptr()
         s.attn_b = float(attn[0].bias.detach().double().cpu().item())
+    elif attn is not None:                                     # node_edge_attn_per_type: row t for type t
+        s.attn_w = f.dev(attn[0].weight.detach().double().cpu().reshape(-1), device).data_ptr()
+        s.attn_bv = f.dev(attn[0].bias.detach().double().cpu(), device).data_ptr()
     upd = layer.update_mlp
     if upd is not None:
         s.upd_w = f.dev(upd[0].weight.detach().double().cpu(), device).data_ptr()

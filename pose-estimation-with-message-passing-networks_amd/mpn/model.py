@@ -86,7 +86,8 @@ class TypeAwareMPNLayer(nn.Module):
         if aggr_sub == "node_edge_attn":
             self.attn_net = nn.Sequential(nn.Linear(edge_dim, 1))
         elif aggr_sub == "node_edge_attn_per_type":
-            raise NotImplementedError("AGGR_SUB=node_edge_attn_per_type")
+            # one attention row per source type (layers.py:199-201, 245-246): always 17 outputs
+            self.attn_net = nn.Sequential(nn.Linear(edge_dim, 17))
         else:
             self.attn_net = None
 
@@ -143,7 +144,7 @@ class NodeClassificationMPNSimple(nn.Module):
         if self.node_steps != 0:
             raise NotImplementedError("NODE_STEPS > 0 (the reference calls the layer without node_types)")
         if config.AGGR_TYPE == "per_type":
-            aggr = "attn" if config.AGGR_SUB == "node_edge_attn" else config.AGGR
+            aggr = "attn" if config.AGGR_SUB in ("node_edge_attn", "node_edge_attn_per_type") else config.AGGR
         else:
             aggr = config.AGGR
         if aggr not in AGGR_CODES:

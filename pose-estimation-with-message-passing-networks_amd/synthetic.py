@@ -90,8 +90,10 @@ def closed_form(shape, salt: float) -> np.ndarray:
     return ((v - np.floor(v)) * 2.0 - 1.0).astype(np.float32)
 
 
-def closed_form_state_dict(module_or_sd, salt: float = 0.0):
-    """Deterministic weights for every tensor of a state_dict (BN stats kept non-trivial)."""
+def closed_form_state_dict(module_or_sd, salt: float = 0.0, attn_gain: float = 1.0):
+    """Deterministic weights for every tensor of a state_dict (BN stats kept non-trivial).
+    `attn_gain` scales the attention net so its softmax is far from uniform (a fixture then tells
+    which attention row was used)."""
     import torch
     sd = module_or_sd.state_dict() if hasattr(module_or_sd, "state_dict") else module_or_sd
     out = {}
@@ -110,5 +112,7 @@ def closed_form_state_dict(module_or_sd, salt: float = 0.0):
             t = h * (1.6 / math.sqrt(v.shape[1]))
         else:
             t = 0.05 * h
+        if ".attn_net." in k:
+            t = t * attn_gain
         out[k] = t.to(v.dtype)
     return out

@@ -18,9 +18,9 @@ TOL = 1e-4          # north_star: logits within 1e-4 (fp32)
 REL_SUM = 2e-6
 
 
-def make_model(cfg, salt, precision=None):
+def make_model(cfg, salt, precision=None, attn_gain=1.0):
     m = pemp_amd.get_mpn_model(cfg)
-    sd = syn.closed_form_state_dict(m, salt)
+    sd = syn.closed_form_state_dict(m, salt, attn_gain)
     m.load_state_dict(sd)
     if precision:
         m.precision = precision
@@ -52,7 +52,7 @@ def test_golden(name, prec):
     cfg = gu.mpn_config(meta)
     if prec == "bf16x3" and "attn" not in name:
         pytest.skip("bf16x3 is offered for the attention variant")
-    model, _ = make_model(cfg, meta["salt"], prec)
+    model, _ = make_model(cfg, meta["salt"], prec, meta.get("attn_gain", 1.0))
     pe, pn, pc, tag = run(model, *(torch.from_numpy(a[k]) for k in ("x", "edge_attr", "edge_index", "node_types")))
     assert tag == [None]
     assert len(pe) == int(a["n_edge_preds"]) and len(pn) == int(a["n_node_preds"]) and len(pc) == len(pn)
@@ -77,6 +77,7 @@ CASES = [
     (17, 2, 128, 128, 5, "max", 3, 0, "fully"),
     (17, 1, 128, 128, 4, "mean", 2, 0, "knn"),
     (17, 1, 128, 128, 4, "add", 2, 1, "fully"),
+    (17, 2, 128, 128, 6, "attn_per_type", 3, 0, "fully"),   # AGGR_SUB node_edge_attn_per_type
 ]
 
 
@@ -84,12 +85,13 @@ CASES = [
 @pytest.mark.parametrize("case", CASES, ids=[f"J{c[0]}-B{c[1]}-{c[5]}-T{c[6]}-{c[8]}" for c in CASES])
 def test_vs_oracle(case, prec):
     J, B, H, W, persons, variant, steps, aux, gtype = case
-    if prec == "bf16x3" and variant != "attn":
+    if prec == "bf16x3" and not variant.startswith("attn"):
         pytest.skip("bf16x3 is offered for the attention variant")
     g = graph(B, J, H, W, persons, gtype)
     cfg = pcfg.published_mpn_config(J, steps, variant)
     cfg.AUX_LOSS_STEPS = aux
-    model, sd = make_model(cfg, 0.125 * steps + J, prec)
+    # per-type attention: sharpened so that using the wrong attention row fails the bar
+    model, sd = make_model(cfg, 0.125 * steps + J, prec, 16.0 if variant == "attn_per_type" else 1.0)
     x, ea, ei, types = g[0], g[1], g[2], g[7][:, 2]
     pe, pn, pc, _ = run(model, x, ea, ei, types)
     if variant == "add":

@@ -29,7 +29,7 @@ def test_construct_graph_matches_reference(name):
 def test_mpn_matches_reference(name):
     meta, a = gu.load(name)
     cfg = gu.mpn_config(meta)
-    sd = _state_dict(cfg, meta["salt"])
+    sd = _state_dict(cfg, meta["salt"], meta.get("attn_gain", 1.0))
     pe, pn, pc, tag = restate.mpn_forward(sd, cfg, torch.from_numpy(a["x"]), torch.from_numpy(a["edge_attr"]),
                                          torch.from_numpy(a["edge_index"]), torch.from_numpy(a["node_types"]))
     assert len(pe) == int(a["n_edge_preds"]) and len(pn) == int(a["n_node_preds"]) and tag == [None]
@@ -38,8 +38,21 @@ def test_mpn_matches_reference(name):
     np.testing.assert_allclose(pc[-1].numpy(), a["class_logits"], atol=1e-5, rtol=0)
 
 
-def _state_dict(cfg, salt):
+def _state_dict(cfg, salt, attn_gain=1.0):
     from pemp_amd.mpn.model import NodeClassificationMPNSimple
     from pemp_amd import synthetic as syn
     m = NodeClassificationMPNSimple(cfg)
-    return syn.closed_form_state_dict(m, salt)
+    return syn.closed_form_state_dict(m, salt, attn_gain)
+
+
+def test_per_type_attention_golden_distinguishes_rows():
+    """The per-type case must not be reproducible with the shared attention row (column 0)."""
+    meta, a = gu.load("mpn_attn_pertype_t2")
+    cfg = gu.mpn_config(meta)
+    assert cfg.AGGR_SUB == "node_edge_attn_per_type"
+    sd = _state_dict(cfg, meta["salt"], meta.get("attn_gain", 1.0))
+    assert sd["mpn_node_cls.attn_net.0.weight"].shape == (17, 64)
+    cfg.AGGR_SUB = "node_edge_attn"
+    pe, pn, pc, _ = restate.mpn_forward(sd, cfg, torch.from_numpy(a["x"]), torch.from_numpy(a["edge_attr"]),
+                                        torch.from_numpy(a["edge_index"]), torch.from_numpy(a["node_types"]))
+    assert np.abs(pc[-1].numpy() - a["class_logits"]).max() > 5e-4      # 5x the logit tolerance
