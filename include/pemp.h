@@ -18,6 +18,7 @@
  *   pemp_fully_graph     ConstructGraph.py:376-381 fully_connected_mpn_graph (+ batch offsets :222-223)
  *   pemp_knn_graph_*     ConstructGraph.py:363-368 knn_mpn_graph (torch_cluster knn_graph k=50,
  *                        PyG to_undirected, remove_self_loops)
+ *   pemp_score_graph     ConstructGraph.py:405-422 score_based_graph (k = 75 roots)
  *   pemp_edge_features   ConstructGraph.py:289-359 (edge_attr)
  *   pemp_mpn_forward     Models/MessagePassingNetwork/NodeClassificationMPNSimple.py:62-97 with
  *                        layers.py:32-86 (MPLayer) / :157-274 (TypeAwareMPNLayer)
@@ -121,6 +122,15 @@ int pemp_knn_graph_count(const int64_t* joint_det, const int64_t* node_off, cons
 int pemp_knn_graph_emit(const int64_t* node_off, const int64_t* node_off_host, int B,
                         const int64_t* edge_off, int64_t e_total, void* workspace,
                         size_t workspace_bytes, int64_t* edge_index, void* stream);
+
+/* score_based graph per image (ConstructGraph.py:405-422 score_based_graph, k = 75 there): the k
+ * highest-scoring nodes are roots (ties: lower node index; torch.topk leaves them unspecified);
+ * edge (a, b), a != b, exists iff a or b is a root, sorted by (src, dst) with the per-image node
+ * offsets added. Every image needs n >= k (the reference's topk raises otherwise: INVALID_ARG);
+ * e_total must be sum over images of k (2 n - k - 1). */
+size_t pemp_score_graph_workspace_size(const int64_t* node_off_host, int B, int k);
+int pemp_score_graph(const float* joint_scores, const int64_t* node_off, const int64_t* node_off_host, int B, int k,
+                     int64_t e_total, void* workspace, size_t workspace_bytes, int64_t* edge_index, void* stream);
 
 /* Edge features. mode: */
 enum {
@@ -243,7 +253,7 @@ int pemp_mpn_status(const pemp_mpn_desc* desc, int64_t N, int64_t E, const void*
 /* Opt-in profiler: while enabled, hipEvents are recorded on the launch stream around every kernel
  * whose label contains `filter` ("*" = all, NULL or "" = off). pemp_prof_report synchronises those
  * events and writes "label count total_ms" lines into buf (returns the full length), then resets.
- * Labels: detect_nms, detect_top, detect_emit, pack_nodes, fully_graph, edge_features, knn_adj, knn_emit,
+ * Labels: detect_nms, detect_top, detect_emit, pack_nodes, fully_graph, edge_features, knn_adj, knn_emit, score_graph,
  * mpn_prepare, node_embed, edge_embed, node_table, edge_step, edge_step_head, node_update, heads. */
 int pemp_prof_enable(const char* filter);
 int pemp_prof_report(char* buf, size_t len);

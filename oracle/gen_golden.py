@@ -135,6 +135,10 @@ GC_CASES = {
                           graph="knn", pool=3, thr=0.1, mask_crowds=False), False),
     "gc_no_threshold": (dict(seed=7, B=1, J=17, H=64, W=80, C=128, F=1, persons=2, variant="noisy",
                              graph="fully", pool=3, thr=2.0, mask_crowds=False), False),
+    "gc_score_based": (dict(seed=8, B=2, J=17, H=128, W=128, C=128, F=1, persons=6, variant="clean",
+                            graph="score_based", pool=5, thr=0.1, mask_crowds=False), False),
+    "gc_score_based_nothr": (dict(seed=9, B=1, J=17, H=64, W=80, C=128, F=1, persons=2, variant="noisy",
+                                  graph="score_based", pool=3, thr=2.0, mask_crowds=False), False),
 }
 
 MPN_CASES = {

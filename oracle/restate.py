@@ -14,7 +14,8 @@ which runs the reference's own files under ``oracle/ref_shims.py``).
 
 Defined where the reference is unpinned:
   * top-k ties: lower flat index wins (the CUDA radix-select order the reference ran on);
-  * knn ties:   (squared integer distance, node index) — torch_cluster's order is unspecified.
+  * knn ties:   (squared integer distance, node index) — torch_cluster's order is unspecified;
+  * score_based root ties: (score descending, node index) — torch.topk's tie order is unspecified.
 """
 import torch
 import torch.nn.functional as F
@@ -107,6 +108,23 @@ def knn_edge_index(det: torch.Tensor, k: int = 50) -> torch.Tensor:
     return torch.stack([src, dst], 0)
 
 
+def score_based_edge_index(scores: torch.Tensor, k: int = 75) -> torch.Tensor:
+    """score_based_graph (ConstructGraph.py:405-422): the k best-scoring nodes are roots; rows of
+    roots in a dense adjacency -> to_undirected -> remove_self_loops. Edge (a, b), a != b, exists
+    iff a or b is a root; sorted by (src, dst). Roots at tied scores: lower node index first (the
+    reference's torch.topk leaves the tie order unspecified)."""
+    n = scores.shape[0]
+    if n < k:   # torch.topk raises for k > n (ConstructGraph.py:414)
+        raise RuntimeError(f"score_based graph: selected index k={k} out of range for {n} detections")
+    order = sorted(range(n), key=lambda i: (-float(scores[i]), i))
+    root = torch.zeros(n, dtype=torch.bool)
+    root[order[:k]] = True
+    adj = root[:, None] | root[None, :]
+    adj.fill_diagonal_(False)
+    src, dst = adj.nonzero(as_tuple=True)
+    return torch.stack([src, dst], 0)
+
+
 def edge_features(det: torch.Tensor, edge_index: torch.Tensor, num_joints: int, norm_factor,
                   features_to_use) -> torch.Tensor:
     """ConstructGraph.py:305-359 (modes without associative-embedding tags)."""
@@ -152,6 +170,8 @@ def construct_graph(scoremaps, features, tagmaps, masks, gc, num_joints):
             ei = fully_edge_index(det.shape[0])
         elif gc.GRAPH_TYPE == "knn":
             ei = knn_edge_index(det)
+        elif gc.GRAPH_TYPE == "score_based":
+            ei = score_based_edge_index(sc, 75)
         else:
             raise NotImplementedError(gc.GRAPH_TYPE)
         ea = edge_features(det, ei, num_joints, norm, gc.EDGE_FEATURES_TO_USE)

@@ -3,6 +3,7 @@
 //   ConstructGraph.py:206-231          batching (node offsets added to edge_index, cat)
 //   ConstructGraph.py:376-381          fully_connected_mpn_graph: all i != j sorted by (src, dst)
 //   ConstructGraph.py:363-368          knn_mpn_graph: knn_graph(k) -> to_undirected -> no self loops
+//   ConstructGraph.py:405-422          score_based_graph: k best-scoring roots, every edge touching one
 //   ConstructGraph.py:289-359          edge_attr = [dx, dy, onehot(type_src) | onehot(type_dst)]
 // All integer outputs are bit-exact; dx/dy are IEEE fp32 divisions of exact integer differences.
 #include <math.h>
@@ -553,6 +554,108 @@ __global__ __launch_bounds__(64) void graph_offsets_kernel(const int32_t* __rest
     if (edge_off) edge_off[B] = ce;
   }
 }
+// ---- score_based_graph (ConstructGraph.py:405-422) -------------------------------------------
+// Roots are the k best-scoring nodes of an image (ties: lower node index). Edge (a, b), a != b,
+// exists iff a or b is a root, sorted by (a, b): a root row lists every other node, a non-root row
+// lists the roots in index order. Row a starts at  a*k + roots_before(a)*(n-1-k)  in its image.
+constexpr int SCORE_LDS = 8192;   // scores of an image staged in LDS up to this many nodes
+
+struct ScoreWs {
+  int* rinfo;     // [N]    2 * roots_before(node) + is_root
+  int* roots;     // [B*k]  local indices of the roots, ascending
+  int64_t* eoff;  // [B]    first edge of each image
+};
+
+inline size_t score_ws_bytes(int64_t n_total, int B, int k) {
+  return align_up((size_t)n_total * 4, 256) + align_up((size_t)B * k * 4, 256) + align_up((size_t)B * 8, 256);
+}
+
+inline ScoreWs score_carve(void* ws, int64_t n_total, int B, int k) {
+  char* p = static_cast<char*>(ws);
+  ScoreWs w;
+  w.rinfo = reinterpret_cast<int*>(p); p += align_up((size_t)n_total * 4, 256);
+  w.roots = reinterpret_cast<int*>(p); p += align_up((size_t)B * k * 4, 256);
+  w.eoff = reinterpret_cast<int64_t*>(p);
+  return w;
+}
+
+__global__ __launch_bounds__(256) void score_roots_kernel(const float* __restrict__ scores,
+                                                          const int64_t* __restrict__ node_off, int B, int k,
+                                                          ScoreWs w) {
+  __shared__ float sl[SCORE_LDS];
+  __shared__ int wcnt[4];
+  __shared__ int64_t wsum[4];
+  const int b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t base = node_off[b];
+  const int n = (int)(node_off[b + 1] - base);
+  // first edge of this image: sum over the images before it of k (2 n - k - 1)
+  int64_t acc = 0;
+  for (int q = threadIdx.x; q < b; q += 256) {
+    const int64_t m = node_off[q + 1] - node_off[q];
+    acc += m > 0 ? (int64_t)k * (2 * m - k - 1) : 0;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor((long long)acc, off);
+  if (lane == 0) wsum[wave] = acc;
+  const float* s = scores + base;
+  const bool in_lds = n <= SCORE_LDS;
+  if (in_lds)
+    for (int i = threadIdx.x; i < n; i += 256) sl[i] = s[i];
+  __syncthreads();
+  if (threadIdx.x == 0) w.eoff[b] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  const float* sv = in_lds ? sl : s;
+  int carry = 0;
+  for (int i0 = 0; i0 < n; i0 += 256) {
+    const int i = i0 + threadIdx.x;
+    bool root = false;
+    if (i < n) {
+      const float si = sv[i];
+      int rank = 0;
+      for (int j = 0; j < n; ++j) {
+        const float sj = sv[j];
+        rank += (sj > si) || (sj == si && j < i);
+      }
+      root = rank < k;
+    }
+    const unsigned long long m = __ballot(root);
+    const int pos = __popcll(m & ((1ull << lane) - 1));
+    if (lane == 0) wcnt[wave] = __popcll(m);
+    __syncthreads();
+    int pre = carry;
+    for (int q = 0; q < wave; ++q) pre += wcnt[q];
+    pre += pos;
+    if (i < n) {
+      w.rinfo[base + i] = 2 * pre + (root ? 1 : 0);
+      if (root) w.roots[(int64_t)b * k + pre] = i;
+    }
+    carry += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    __syncthreads();
+  }
+}
+
+// one wave per row; consecutive lanes write consecutive edges
+__global__ __launch_bounds__(256) void score_emit_kernel(const int64_t* __restrict__ node_off, int B, int k,
+                                                         const ScoreWs w, int64_t n_total, int64_t e_total,
+                                                         int64_t* __restrict__ ei) {
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n_total; r += stride) {
+    const int b = find_segment(node_off, B, r);
+    const int64_t base = node_off[b];
+    const int n = (int)(node_off[b + 1] - base), i = (int)(r - base);
+    const int v = w.rinfo[r];
+    const bool root = v & 1;
+    const int64_t e0 = w.eoff[b] + (int64_t)i * k + (int64_t)(v >> 1) * (n - 1 - k);
+    const int cnt = root ? n - 1 : k;
+    const int* rl = w.roots + (int64_t)b * k;
+    for (int c = lane; c < cnt; c += 64) {
+      const int col = root ? c + (c >= i) : rl[c];
+      ei[e0 + c] = r;
+      ei[e_total + e0 + c] = base + col;
+    }
+  }
+}
+
 }  // namespace
 }  // namespace pemp
 
@@ -649,6 +752,45 @@ extern "C" int pemp_knn_graph_emit(const int64_t* node_off, const int64_t* node_
   ProfScope prof("knn_emit", as_stream(stream));
   hipLaunchKernelGGL(knn_emit_kernel, dim3(B), dim3(1024), 0, as_stream(stream), node_off, B, w.mat_off, w.adj,
                      w.adjt, edge_off, e_total, edge_index);
+  PEMP_LAUNCH_CHECK();
+  return PEMP_OK;
+}
+
+extern "C" size_t pemp_score_graph_workspace_size(const int64_t* node_off_host, int B, int k) {
+  if (!node_off_host || B <= 0 || k < 1) return 0;
+  return score_ws_bytes(node_off_host[B], B, k);
+}
+
+extern "C" int pemp_score_graph(const float* joint_scores, const int64_t* node_off, const int64_t* node_off_host,
+                                int B, int k, int64_t e_total, void* workspace, size_t workspace_bytes,
+                                int64_t* edge_index, void* stream) {
+  PEMP_CHECK_ARG(joint_scores && node_off && node_off_host && workspace && B > 0 && k >= 1,
+                 "pemp_score_graph: bad args");
+  int64_t e_need = 0;
+  for (int b = 0; b < B; ++b) {
+    const int64_t n = node_off_host[b + 1] - node_off_host[b];
+    if (n < k) {   // the reference's joint_scores.topk(k) raises (ConstructGraph.py:414)
+      set_error("pemp_score_graph: image %d has %lld detections < k = %d", b, (long long)n, k);
+      return PEMP_ERR_INVALID_ARG;
+    }
+    e_need += (int64_t)k * (2 * n - k - 1);
+  }
+  PEMP_CHECK_ARG(e_total == e_need, "pemp_score_graph: e_total does not match k (2 n - k - 1) per image");
+  PEMP_CHECK_ARG(e_total == 0 || edge_index, "pemp_score_graph: null edge_index");
+  const int64_t n_total = node_off_host[B];
+  if (workspace_bytes < score_ws_bytes(n_total, B, k)) {
+    set_error("pemp_score_graph: workspace %zu < %zu", workspace_bytes, score_ws_bytes(n_total, B, k));
+    return PEMP_ERR_WORKSPACE;
+  }
+  if (e_total == 0) return PEMP_OK;
+  const ScoreWs w = score_carve(workspace, n_total, B, k);
+  const hipStream_t st = as_stream(stream);
+  ProfScope prof("score_graph", st);
+  hipLaunchKernelGGL(score_roots_kernel, dim3(B), dim3(256), 0, st, joint_scores, node_off, B, k, w);
+  PEMP_LAUNCH_CHECK();
+  const int64_t blocks = std::min<int64_t>((n_total + 3) / 4, 4096);
+  hipLaunchKernelGGL(score_emit_kernel, dim3((unsigned)blocks), dim3(256), 0, st, node_off, B, k, w, n_total,
+                     e_total, edge_index);
   PEMP_LAUNCH_CHECK();
   return PEMP_OK;
 }

@@ -2,7 +2,8 @@
 
 Same constructor signature, same ``construct_graph()`` 15-tuple, same dtypes (int64 indices) and
 node/edge order as the reference; computed by ``libpemp.so`` (``pemp_detect``,
-``pemp_pack_nodes``, ``pemp_fully_graph`` / ``pemp_knn_graph_*``, ``pemp_edge_features``).
+``pemp_pack_nodes``, ``pemp_fully_graph_build`` / ``pemp_knn_graph_*`` / ``pemp_score_graph``,
+``pemp_edge_features``). GRAPH_TYPE fully, knn and score_based (``ConstructGraph.py:272-283``).
 Host synchronisation: one count read-back after detection (the reference syncs at every
 ``nonzero``), plus one more for knn graphs.
 """
@@ -13,6 +14,7 @@ import torch
 
 from . import _lib
 
+_SCORE_BASED_K = 75        # ConstructGraph.py:280 (score_based_graph roots)
 _EF_MODES = {
     frozenset(["position", "connection_type"]): 0,
     frozenset(["connection_type"]): 1,
@@ -208,7 +210,7 @@ class NaiveGraphConstructor:
             _lib.check(L.pemp_pack_nodes(_lib.ptr(feats), C, _lib.ptr(tags), F, B, J, H, W, _lib.ptr(det),
                                          _lib.ptr(dsc), cap, _lib.ptr(node_off), N, _lib.ptr(x), _lib.ptr(joint_det),
                                          _lib.ptr(joint_scores), _lib.ptr(batch_index), _lib.ptr(joint_tags), st))
-            edge_index = self._edges(L, st, joint_det, node_off, fully_off, node_off_h, B, dev)
+            edge_index = self._edges(L, st, joint_det, joint_scores, node_off, fully_off, node_off_h, B, dev)
             E = edge_index.shape[1]
             edge_attr = torch.empty(E, A, dtype=torch.float32, device=dev)
             _lib.check(L.pemp_edge_features(_lib.ptr(joint_det), _lib.ptr(edge_index), E, J, norm, mode,
@@ -218,7 +220,7 @@ class NaiveGraphConstructor:
         return (x, edge_attr, edge_index, None, None, None, None, joint_det, None, None, None, joint_scores,
                 batch_index, None, joint_tags)
 
-    def _edges(self, L, st, joint_det, node_off, fully_off, node_off_h, B, dev):
+    def _edges(self, L, st, joint_det, joint_scores, node_off, fully_off, node_off_h, B, dev):
         counts = np.diff(node_off_h)
         if self.mpn_graph_type == "fully":
             per = counts * np.maximum(counts - 1, 0)
@@ -230,12 +232,24 @@ class NaiveGraphConstructor:
             _lib.check(L.pemp_knn_graph_count(_lib.ptr(joint_det), _lib.ptr(node_off), nh_p, B, 50, _lib.ptr(ws),
                                               ws.numel(), _lib.ptr(ecount), st))
             per = ecount.cpu().numpy()
+        elif self.mpn_graph_type == "score_based":
+            k = _SCORE_BASED_K
+            if counts.size and counts.min() < k:   # the reference's joint_scores.topk(k) raises
+                raise RuntimeError(f"score_based graph: selected index k={k} out of range for "
+                                   f"{int(counts.min())} detections")
+            per = k * (2 * counts - k - 1)
         else:
             raise NotImplementedError(f"GRAPH_TYPE={self.mpn_graph_type}")
         E = int(per.sum())
         edge_index = torch.empty(2, E, dtype=torch.int64, device=dev)
         if self.mpn_graph_type == "fully":
             _lib.check(L.pemp_fully_graph(_lib.ptr(node_off), _lib.ptr(fully_off), B, E, _lib.ptr(edge_index), st))
+        elif self.mpn_graph_type == "score_based":
+            nh = np.ascontiguousarray(node_off_h)
+            nh_p = nh.ctypes.data_as(ctypes.c_void_p)
+            ws = self._ws_knn.get(L.pemp_score_graph_workspace_size(nh_p, B, _SCORE_BASED_K), dev)
+            _lib.check(L.pemp_score_graph(_lib.ptr(joint_scores), _lib.ptr(node_off), nh_p, B, _SCORE_BASED_K, E,
+                                          _lib.ptr(ws), ws.numel(), _lib.ptr(edge_index), st))
         else:
             edge_off_h = np.zeros(B + 1, np.int64)
             edge_off_h[1:] = np.cumsum(per)

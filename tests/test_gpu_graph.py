@@ -46,6 +46,8 @@ CASES = [
     (2, 17, 96, 136, 1, "realistic", "fully", 5, 0.1, False),   # bilinear plateaus (4 equal maxima)
     (2, 17, 64, 64, 2, "noisy", "fully", 3, 2.0, False),        # DETECT_THRESHOLD > 1.5 branch
     (1, 17, 33, 17, 1, "clean", "fully", 7, 0.1, False),        # tiny, odd sizes
+    (8, 17, 640, 640, 9, "clean", "score_based", 5, 0.1, False),  # C3 shape, score_based (k = 75 roots)
+    (1, 14, 640, 640, 36, "clean", "score_based", 5, 0.1, False), # C5 shape, score_based
 ]
 
 
@@ -97,3 +99,15 @@ def test_capacity_build_fit_and_overflow():
         for i in (0, 1, 2, 7, 11, 12, 14):
             assert out[i].is_contiguous()
             assert torch.equal(out[i].cpu(), ref[i]), (seed, i)
+
+
+def test_score_based_needs_k_detections():
+    """score_based_graph takes topk(k=75) of the scores: the reference raises for fewer detections."""
+    J, H, W = 17, 64, 64
+    hm = torch.from_numpy(syn.make_heatmaps(3, 1, J, H, W, persons=2))
+    feats = torch.from_numpy(syn.closed_form((1, 128, H, W), 0.25))
+    gc = pcfg.inference_gc_config("score_based", 5, False)
+    with pytest.raises(RuntimeError, match="out of range"):
+        run_gc(gc, J, hm, feats, None, None)
+    with pytest.raises(RuntimeError, match="out of range"):
+        restate.construct_graph(hm, feats, torch.zeros(1, J, H, W), None, gc, J)
