@@ -85,7 +85,7 @@ int pemp_graph_offsets(const int32_t* n_det, int B, int64_t* node_off, int64_t* 
 /* The whole fully-connected graph in ONE launch after the count read-back (equivalent to
  * pemp_graph_offsets + pemp_pack_nodes + pemp_fully_graph + pemp_edge_features, same outputs
  * bit for bit): node offsets from n_det, node packing, edge_index of every image, edge_attr
- * (mode = PEMP_EF_*, width J+2 / J / 1 / 2 / J+3). B <= 1024.
+ * (mode = PEMP_EF_*; the AE modes read the tags from tagmaps). B <= 1024.
  * n_total = sum n_det, e_total = sum n (n - 1). tagmaps / joint_tags may be NULL. */
 int pemp_fully_graph_build(const int32_t* n_det, int B, const int64_t* det_xyt, const float* det_scores, int cap,
                            const float* features, int C, const float* tagmaps, int F, int J, int H, int W,
@@ -138,11 +138,18 @@ enum {
   PEMP_EF_CONNECTION = 1,          /* [onehot(J)]               (J)   */
   PEMP_EF_NOTHING = 2,             /* [0]                       (1)   */
   PEMP_EF_POSITION = 3,            /* [dx, dy]                  (2)   */
-  PEMP_EF_POSITION_ANGLE_CONNECTION = 4 /* [dx, dy, theta, onehot(J)] (J+3) */
+  PEMP_EF_POSITION_ANGLE_CONNECTION = 4, /* [dx, dy, theta, onehot(J)] (J+3) */
+  /* associative-embedding modes (ConstructGraph.py:337-357); dist = ||tag[dst] - tag[src]||_2 over
+   * F = 1 or 2 tag dims, rounded as torch.norm on CPU: sqrt(fma(d1, d1, d0 * d0)) */
+  PEMP_EF_POSITION_CONNECTION_AE = 5,    /* {position, connection_type, ae_normed}: [dx, dy, onehot(J), dist] (J+3) */
+  PEMP_EF_AE = 6,                        /* {ae}: [dist] (1), F = 1 */
+  PEMP_EF_AE_NORMED = 7,                 /* {ae_normed}: [round(dist) * 100 - score[src]] (1), F = 2 */
+  PEMP_EF_AE_TRACKING = 8                /* {ae_tracking_1}: [(1.8425 - dist) / 1.8425] (1) */
 };
-int pemp_edge_features(const int64_t* joint_det /*[N,3]*/, const int64_t* edge_index /*[2,E]*/,
-                       int64_t e_total, int J, float norm_factor, int mode, float* edge_attr,
-                       void* stream);
+/* joint_tags [N,F] / joint_scores [N] are read by the AE modes only (may be NULL otherwise). */
+int pemp_edge_features(const int64_t* joint_det /*[N,3]*/, const float* joint_tags, int F, const float* joint_scores,
+                       const int64_t* edge_index /*[2,E]*/, int64_t e_total, int J, float norm_factor, int mode,
+                       float* edge_attr, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Message-passing network, inference (eval-mode BatchNorm folded into the next Linear by the

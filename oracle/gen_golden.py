@@ -49,6 +49,8 @@ def gc_inputs(meta):
 def gc_config(meta):
     g = pcfg.inference_gc_config(meta["graph"], meta["pool"], meta["mask_crowds"])
     g.DETECT_THRESHOLD = meta["thr"]
+    if "features" in meta:
+        g.EDGE_FEATURES_TO_USE = list(meta["features"])
     return g
 
 
@@ -94,6 +96,8 @@ def mpn_cfg(meta):
         c.AGGR = meta["aggr"]
     if meta.get("update_mlp"):
         c.USE_NODE_UPDATE_MLP = True
+    if meta.get("edge_in"):
+        c.EDGE_INPUT_DIM = meta["edge_in"]
     return c
 
 
@@ -135,6 +139,18 @@ GC_CASES = {
                           graph="knn", pool=3, thr=0.1, mask_crowds=False), False),
     "gc_no_threshold": (dict(seed=7, B=1, J=17, H=64, W=80, C=128, F=1, persons=2, variant="noisy",
                              graph="fully", pool=3, thr=2.0, mask_crowds=False), False),
+    "gc_ae_pos_conn_f2": (dict(seed=10, B=2, J=17, H=96, W=96, C=128, F=2, persons=2, variant="clean",
+                               graph="fully", pool=5, thr=0.1, mask_crowds=False,
+                               features=["ae_normed", "position", "connection_type"]), True),
+    "gc_ae_pos_conn_f1": (dict(seed=11, B=1, J=17, H=96, W=96, C=128, F=1, persons=3, variant="clean",
+                               graph="knn", pool=5, thr=0.1, mask_crowds=False,
+                               features=["ae_normed", "position", "connection_type"]), False),
+    "gc_ae": (dict(seed=12, B=1, J=14, H=80, W=96, C=128, F=1, persons=2, variant="noisy",
+                   graph="fully", pool=3, thr=0.1, mask_crowds=False, features=["ae"]), False),
+    "gc_ae_normed_f2": (dict(seed=13, B=1, J=14, H=80, W=96, C=128, F=2, persons=2, variant="clean",
+                             graph="fully", pool=5, thr=0.1, mask_crowds=False, features=["ae_normed"]), False),
+    "gc_ae_tracking_f2": (dict(seed=14, B=2, J=17, H=64, W=64, C=128, F=2, persons=2, variant="clean",
+                               graph="fully", pool=5, thr=0.1, mask_crowds=False, features=["ae_tracking_1"]), False),
     "gc_score_based": (dict(seed=8, B=2, J=17, H=128, W=128, C=128, F=1, persons=6, variant="clean",
                             graph="score_based", pool=5, thr=0.1, mask_crowds=False), False),
     "gc_score_based_nothr": (dict(seed=9, B=1, J=17, H=64, W=80, C=128, F=1, persons=2, variant="noisy",
@@ -155,6 +171,7 @@ MPN_CASES = {
     "mpn_pertype_max_t2": (dict(J=17, steps=2, variant="attn", salt=8.5, aggr_sub="None", aggr="max"),
                            "gc_small_fully"),
     "mpn_attn_c2_t3": (dict(J=17, steps=3, variant="attn", salt=9.5), "gc_c2_like"),
+    "mpn_attn_ae_t2": (dict(J=17, steps=2, variant="attn", salt=11.5, edge_in=20), "gc_ae_pos_conn_f2"),
     "mpn_attn_pertype_t2": (dict(J=17, steps=2, variant="attn", salt=10.5, aggr_sub="node_edge_attn_per_type",
                                  aggr="add", attn_gain=16.0), "gc_realistic_knn"),
 }

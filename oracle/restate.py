@@ -17,6 +17,8 @@ Defined where the reference is unpinned:
   * knn ties:   (squared integer distance, node index) — torch_cluster's order is unspecified;
   * score_based root ties: (score descending, node index) — torch.topk's tie order is unspecified.
 """
+import math
+
 import torch
 import torch.nn.functional as F
 
@@ -126,8 +128,9 @@ def score_based_edge_index(scores: torch.Tensor, k: int = 75) -> torch.Tensor:
 
 
 def edge_features(det: torch.Tensor, edge_index: torch.Tensor, num_joints: int, norm_factor,
-                  features_to_use) -> torch.Tensor:
-    """ConstructGraph.py:305-359 (modes without associative-embedding tags)."""
+                  features_to_use, joint_tags=None, joint_scores=None) -> torch.Tensor:
+    """ConstructGraph.py:305-359. joint_tags is the reference's ``tag_maps[type, y, x]`` of the
+    squeezed tag maps: [N] for one tag dim, [N, F] otherwise."""
     jx, jy, jt = det[:, 0], det[:, 1], det[:, 2]
     s, d = edge_index[0], edge_index[1]
     E = edge_index.shape[1]
@@ -151,6 +154,19 @@ def edge_features(det: torch.Tensor, edge_index: torch.Tensor, num_joints: int, 
         theta = torch.abs(torch.acos(ax * torch.rsqrt(ax ** 2 + ay ** 2)))
         theta[torch.isnan(theta)] = 0.0
         return torch.cat([dx[:, None], dy[:, None], theta[:, None], onehot.float()], 1)
+    if mode == {"ae"}:                                                      # :337-339
+        return torch.unsqueeze(joint_tags[d] - joint_tags[s], 1).norm(p=None, dim=1, keepdim=True)
+    if mode == {"ae_normed"}:                                               # :340-343
+        return ((joint_tags[d] - joint_tags[s]).norm(p=None, dim=1, keepdim=True).round() * 100
+                - joint_scores[s, None])
+    jt2 = joint_tags[:, None] if joint_tags is not None and joint_tags.dim() == 1 else joint_tags
+    if mode == {"ae_tracking_1"}:                                           # :344-351
+        t_a = 1.8425
+        dist = (jt2[d] - jt2[s]).norm(p=None, dim=1, keepdim=True)
+        return torch.div(t_a - dist, t_a)
+    if mode == {"position", "connection_type", "ae_normed"}:                # :352-357
+        dist = (jt2[d] - jt2[s]).norm(p=None, dim=1, keepdim=True)
+        return torch.cat([dx[:, None], dy[:, None], onehot.float(), dist], 1)
     raise NotImplementedError(f"EDGE_FEATURES_TO_USE={features_to_use}")
 
 
@@ -174,8 +190,11 @@ def construct_graph(scoremaps, features, tagmaps, masks, gc, num_joints):
             ei = score_based_edge_index(sc, 75)
         else:
             raise NotImplementedError(gc.GRAPH_TYPE)
-        ea = edge_features(det, ei, num_joints, norm, gc.EDGE_FEATURES_TO_USE)
         tg = tagmaps[b, det[:, 2], det[:, 1], det[:, 0]]
+        nf = math.prod(tg.shape[1:])                        # tag dims per node (1 for [B, J, H, W] maps)
+        jt = tg.reshape(tg.shape[0], nf)
+        jt = jt[:, 0] if nf == 1 else jt                    # tagmaps[batch].squeeze() (ConstructGraph.py:100)
+        ea = edge_features(det, ei, num_joints, norm, gc.EDGE_FEATURES_TO_USE, jt, sc)
         xs.append(x); eas.append(ea); eis.append(ei + off); dets.append(det); scs.append(sc)
         bis.append(torch.full((det.shape[0],), b, dtype=torch.long)); tgs.append(tg)
         off += det.shape[0]

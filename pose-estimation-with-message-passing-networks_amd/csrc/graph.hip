@@ -23,6 +23,63 @@ __device__ __forceinline__ int find_segment(const int64_t* off, int n, int64_t v
   return lo;
 }
 
+// ---- edge_attr (ConstructGraph.py:289-357) --------------------------------------------------
+// Per edge the kernels stage dx, dy, the endpoint types and one extra scalar `aux`: theta for the
+// angle mode, the tag term for the associative-embedding modes. ef_value() then lays out column f.
+
+// ||tag[dst] - tag[src]||_2 rounded as the reference's CPU torch.norm: sqrt(fma(d1, d1, d0 * d0))
+// (F = 2); F = 1 is |d| exactly. Contraction is spelled out so the compiler cannot re-fuse it.
+// sqrtf, not __fsqrt_rn: on gfx950 the latter lowers to the bare 1-ulp v_sqrt_f32, while sqrtf
+// gets the correctly rounded sequence.
+__device__ __forceinline__ float tag_distance(const float* ts, const float* td, int F) {
+  const float d0 = __fsub_rn(td[0], ts[0]);
+  if (F == 1) return fabsf(d0);
+  const float d1 = __fsub_rn(td[1], ts[1]);
+  return sqrtf(fmaf(d1, d1, __fmul_rn(d0, d0)));
+}
+
+// ConstructGraph.py:337-357: ae -> dist; ae_normed -> round(dist) * 100 - score[src];
+// ae_tracking_1 -> (t_a - dist) / t_a with t_a = 1.8425 (fp32 ops, no contraction)
+__device__ __forceinline__ float ae_term(int mode, float dist, float score_src) {
+  if (mode == PEMP_EF_AE_NORMED) return __fsub_rn(__fmul_rn(rintf(dist), 100.0f), score_src);
+  if (mode == PEMP_EF_AE_TRACKING) return __fdiv_rn(__fsub_rn(1.8425f, dist), 1.8425f);
+  return dist;
+}
+
+__device__ __forceinline__ bool ef_uses_tags(int mode) {
+  return mode == PEMP_EF_POSITION_CONNECTION_AE || mode == PEMP_EF_AE || mode == PEMP_EF_AE_NORMED ||
+         mode == PEMP_EF_AE_TRACKING;
+}
+
+// theta (angle mode) from the integer endpoint coordinates, ConstructGraph.py:319-321
+__device__ __forceinline__ float edge_theta(int64_t sx, int64_t sy, int64_t dx, int64_t dy) {
+  const float ax = (float)(sx - dx), ay = (float)(sy - dy);
+  const float th = fabsf(acosf(ax * (1.0f / sqrtf(ax * ax + ay * ay))));
+  return isnan(th) ? 0.0f : th;
+}
+
+__device__ __forceinline__ float ef_value(int mode, int f, int J, float dx, float dy, float aux, int ts, int td) {
+  int oh = -1;   // one-hot column index, or -1
+  float v = 0.0f;
+  switch (mode) {
+    case PEMP_EF_POSITION_CONNECTION:
+      if (f == 0) v = dx; else if (f == 1) v = dy; else oh = f - 2;
+      break;
+    case PEMP_EF_CONNECTION: oh = f; break;
+    case PEMP_EF_NOTHING: break;
+    case PEMP_EF_POSITION: v = f == 0 ? dx : dy; break;
+    case PEMP_EF_POSITION_ANGLE_CONNECTION:
+      if (f == 0) v = dx; else if (f == 1) v = dy; else if (f == 2) v = aux; else oh = f - 3;
+      break;
+    case PEMP_EF_POSITION_CONNECTION_AE:
+      if (f == 0) v = dx; else if (f == 1) v = dy; else if (f == J + 2) v = aux; else oh = f - 2;
+      break;
+    default: v = aux; break;   // AE, AE_NORMED, AE_TRACKING: one column
+  }
+  if (oh >= 0) v = (ts == oh || td == oh) ? 1.0f : 0.0f;
+  return v;
+}
+
 __global__ __launch_bounds__(256) void pack_nodes_kernel(
     const float* __restrict__ feat, int C, const float* __restrict__ tags, int F, int B, int J, int H, int W,
     const int64_t* __restrict__ det, const float* __restrict__ det_sc, int cap, const int64_t* __restrict__ node_off,
@@ -65,9 +122,11 @@ __global__ __launch_bounds__(256) void fully_graph_kernel(const int64_t* __restr
 // 256 edges per step: per-edge values (dx, dy, theta, the two types) go to LDS once, then the
 // block writes the 256 x A output rows as one contiguous, coalesced range.
 __global__ __launch_bounds__(256) void edge_features_kernel(const int64_t* __restrict__ jdet,
+                                                            const float* __restrict__ jtag, int F,
+                                                            const float* __restrict__ jsc,
                                                             const int64_t* __restrict__ ei, int64_t E, int J,
                                                             float norm, int mode, int A, float* __restrict__ out) {
-  __shared__ float dx_s[256], dy_s[256], th_s[256];
+  __shared__ float dx_s[256], dy_s[256], aux_s[256];
   __shared__ int ts_s[256], td_s[256];
   for (int64_t base = (int64_t)blockIdx.x * 256; base < E; base += (int64_t)gridDim.x * 256) {
     const int64_t e = base + threadIdx.x;
@@ -78,37 +137,15 @@ __global__ __launch_bounds__(256) void edge_features_kernel(const int64_t* __res
       dy_s[threadIdx.x] = (float)(dy - sy) / norm;
       ts_s[threadIdx.x] = (int)jdet[s * 3 + 2];
       td_s[threadIdx.x] = (int)jdet[d * 3 + 2];
-      if (mode == PEMP_EF_POSITION_ANGLE_CONNECTION) {
-        const float ax = (float)(sx - dx), ay = (float)(sy - dy);
-        const float th = fabsf(acosf(ax * (1.0f / sqrtf(ax * ax + ay * ay))));
-        th_s[threadIdx.x] = isnan(th) ? 0.0f : th;
-      }
+      if (mode == PEMP_EF_POSITION_ANGLE_CONNECTION) aux_s[threadIdx.x] = edge_theta(sx, sy, dx, dy);
+      else if (ef_uses_tags(mode)) aux_s[threadIdx.x] = ae_term(mode, tag_distance(jtag + s * F, jtag + d * F, F), jsc[s]);
     }
     __syncthreads();
     const int n = (int)min<int64_t>(256, E - base), total = n * A;
     float* o = out + base * A;
     for (int k = threadIdx.x; k < total; k += 256) {
       const int el = k / A, f = k - el * A;
-      float v = 0.0f;
-      int oh = -1;   // one-hot column index, or -1
-      switch (mode) {
-        case PEMP_EF_POSITION_CONNECTION:
-          if (f == 0) v = dx_s[el];
-          else if (f == 1) v = dy_s[el];
-          else oh = f - 2;
-          break;
-        case PEMP_EF_CONNECTION: oh = f; break;
-        case PEMP_EF_NOTHING: v = 0.0f; break;
-        case PEMP_EF_POSITION: v = f == 0 ? dx_s[el] : dy_s[el]; break;
-        case PEMP_EF_POSITION_ANGLE_CONNECTION:
-          if (f == 0) v = dx_s[el];
-          else if (f == 1) v = dy_s[el];
-          else if (f == 2) v = th_s[el];
-          else oh = f - 3;
-          break;
-      }
-      if (oh >= 0) v = (ts_s[el] == oh || td_s[el] == oh) ? 1.0f : 0.0f;
-      o[k] = v;
+      o[k] = ef_value(mode, f, J, dx_s[el], dy_s[el], aux_s[el], ts_s[el], td_s[el]);
     }
     __syncthreads();
   }
@@ -354,7 +391,7 @@ struct FusedGraphArgs {
 // straight from the detections.
 __global__ __launch_bounds__(256) void fused_fully_graph_kernel(FusedGraphArgs a) {
   __shared__ long long noff[FUSED_MAXB + 1], eoff[FUSED_MAXB + 1];
-  __shared__ float dx_s[256], dy_s[256], th_s[256];
+  __shared__ float dx_s[256], dy_s[256], aux_s[256];
   __shared__ int ts_s[256], td_s[256];
   const int B = a.B;
   if (threadIdx.x < 64) {
@@ -428,9 +465,12 @@ __global__ __launch_bounds__(256) void fused_fully_graph_kernel(FusedGraphArgs a
       ts_s[threadIdx.x] = (int)ds[2];
       td_s[threadIdx.x] = (int)dd[2];
       if (a.mode == PEMP_EF_POSITION_ANGLE_CONNECTION) {
-        const float ax = (float)(sx - dx), ay = (float)(sy - dy);
-        const float th = fabsf(acosf(ax * (1.0f / sqrtf(ax * ax + ay * ay))));
-        th_s[threadIdx.x] = isnan(th) ? 0.0f : th;
+        aux_s[threadIdx.x] = edge_theta(sx, sy, dx, dy);
+      } else if (ef_uses_tags(a.mode)) {   // tags straight from the tag maps [B, J, H, W, F]
+        const float* tg = a.tags + (size_t)b * a.J * a.H * a.W * a.F;
+        const float* t_s = tg + (((size_t)ds[2] * a.H + sy) * a.W + sx) * a.F;
+        const float* t_d = tg + (((size_t)dd[2] * a.H + dy) * a.W + dx) * a.F;
+        aux_s[threadIdx.x] = ae_term(a.mode, tag_distance(t_s, t_d, a.F), a.det_sc[(size_t)b * a.cap + i]);
       }
     }
     __syncthreads();
@@ -438,21 +478,7 @@ __global__ __launch_bounds__(256) void fused_fully_graph_kernel(FusedGraphArgs a
     float* o = a.edge_attr + base * a.A;
     for (int k = threadIdx.x; k < total; k += 256) {
       const int el = k / a.A, f = k - el * a.A;
-      float v = 0.0f;
-      int oh = -1;
-      switch (a.mode) {
-        case PEMP_EF_POSITION_CONNECTION:
-          if (f == 0) v = dx_s[el]; else if (f == 1) v = dy_s[el]; else oh = f - 2;
-          break;
-        case PEMP_EF_CONNECTION: oh = f; break;
-        case PEMP_EF_NOTHING: v = 0.0f; break;
-        case PEMP_EF_POSITION: v = f == 0 ? dx_s[el] : dy_s[el]; break;
-        case PEMP_EF_POSITION_ANGLE_CONNECTION:
-          if (f == 0) v = dx_s[el]; else if (f == 1) v = dy_s[el]; else if (f == 2) v = th_s[el]; else oh = f - 3;
-          break;
-      }
-      if (oh >= 0) v = (ts_s[el] == oh || td_s[el] == oh) ? 1.0f : 0.0f;
-      o[k] = v;
+      o[k] = ef_value(a.mode, f, a.J, dx_s[el], dy_s[el], aux_s[el], ts_s[el], td_s[el]);
     }
     __syncthreads();
   }
@@ -467,8 +493,24 @@ static int ef_width(int mode, int J) {
     case PEMP_EF_NOTHING: return 1;
     case PEMP_EF_POSITION: return 2;
     case PEMP_EF_POSITION_ANGLE_CONNECTION: return J + 3;
+    case PEMP_EF_POSITION_CONNECTION_AE: return J + 3;
+    case PEMP_EF_AE: case PEMP_EF_AE_NORMED: case PEMP_EF_AE_TRACKING: return 1;
     default: return -1;
   }
+}
+
+// The associative-embedding modes need the tags; F = 1 or 2 (torch.norm's rounding is pinned for
+// those); ae needs F = 1 and ae_normed F = 2 (the reference fails otherwise, :337-341).
+static int ef_tag_check(int mode, const float* tags, int F, const char* fn) {
+  if (mode != PEMP_EF_POSITION_CONNECTION_AE && mode != PEMP_EF_AE && mode != PEMP_EF_AE_NORMED &&
+      mode != PEMP_EF_AE_TRACKING)
+    return 0;
+  if (!tags) { set_error("%s: edge feature mode %d needs the tags", fn, mode); return PEMP_ERR_INVALID_ARG; }
+  if (F < 1 || F > 2 || (mode == PEMP_EF_AE && F != 1) || (mode == PEMP_EF_AE_NORMED && F != 2)) {
+    set_error("%s: edge feature mode %d with %d tag dims is not supported", fn, mode, F);
+    return PEMP_ERR_UNSUPPORTED;
+  }
+  return 0;
 }
 
 static int fully_graph_build(const int32_t* n_det, int B, const int64_t* det_xyt, const float* det_scores, int cap,
@@ -510,6 +552,7 @@ static int fully_graph_build(const int32_t* n_det, int B, const int64_t* det_xyt
   PEMP_CHECK_ARG(e_total == 0 || (edge_index && edge_attr), "pemp_fully_graph_build: null edge outputs");
   const int A = ef_width(mode, J);
   if (A < 0) { set_error("pemp_fully_graph_build: unknown edge feature mode %d", mode); return PEMP_ERR_INVALID_ARG; }
+  if (const int rc = ef_tag_check(mode, tagmaps, F, "pemp_fully_graph_build")) return rc;
   if (n_total == 0) return PEMP_OK;
   FusedGraphArgs a{};
   a.n_det = n_det; a.B = B; a.cap = cap; a.C = C; a.F = F; a.J = J; a.H = H; a.W = W; a.mode = mode; a.A = A;
@@ -679,22 +722,18 @@ extern "C" int pemp_fully_graph(const int64_t* node_off, const int64_t* edge_off
   return PEMP_OK;
 }
 
-extern "C" int pemp_edge_features(const int64_t* joint_det, const int64_t* edge_index, int64_t e_total, int J,
-                                  float norm_factor, int mode, float* edge_attr, void* stream) {
+extern "C" int pemp_edge_features(const int64_t* joint_det, const float* joint_tags, int F, const float* joint_scores,
+                                  const int64_t* edge_index, int64_t e_total, int J, float norm_factor, int mode,
+                                  float* edge_attr, void* stream) {
   PEMP_CHECK_ARG(joint_det && edge_index && edge_attr && J > 0 && e_total >= 0, "pemp_edge_features: bad args");
-  int A;
-  switch (mode) {
-    case PEMP_EF_POSITION_CONNECTION: A = J + 2; break;
-    case PEMP_EF_CONNECTION: A = J; break;
-    case PEMP_EF_NOTHING: A = 1; break;
-    case PEMP_EF_POSITION: A = 2; break;
-    case PEMP_EF_POSITION_ANGLE_CONNECTION: A = J + 3; break;
-    default: set_error("pemp_edge_features: unknown mode %d", mode); return PEMP_ERR_INVALID_ARG;
-  }
+  const int A = ef_width(mode, J);
+  if (A < 0) { set_error("pemp_edge_features: unknown mode %d", mode); return PEMP_ERR_INVALID_ARG; }
+  if (const int rc = ef_tag_check(mode, joint_tags, F, "pemp_edge_features")) return rc;
+  PEMP_CHECK_ARG(mode != PEMP_EF_AE_NORMED || joint_scores, "pemp_edge_features: ae_normed needs joint_scores");
   if (e_total == 0) return PEMP_OK;
   ProfScope prof("edge_features", as_stream(stream));
   hipLaunchKernelGGL(edge_features_kernel, dim3(grid_for(e_total, 256)), dim3(256), 0, as_stream(stream),
-                     joint_det, edge_index, e_total, J, norm_factor, mode, A, edge_attr);
+                     joint_det, joint_tags, F, joint_scores, edge_index, e_total, J, norm_factor, mode, A, edge_attr);
   PEMP_LAUNCH_CHECK();
   return PEMP_OK;
 }

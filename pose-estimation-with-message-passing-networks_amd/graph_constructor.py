@@ -21,7 +21,12 @@ _EF_MODES = {
     frozenset(["nothing"]): 2,
     frozenset(["position"]): 3,
     frozenset(["position", "angle", "connection_type"]): 4,
+    frozenset(["position", "connection_type", "ae_normed"]): 5,   # associative-embedding modes,
+    frozenset(["ae"]): 6,                                         # ConstructGraph.py:337-357
+    frozenset(["ae_normed"]): 7,
+    frozenset(["ae_tracking_1"]): 8,
 }
+_EF_TAG_MODES = (5, 6, 7, 8)
 
 
 def get_graph_constructor(config, **kwargs):
@@ -127,7 +132,9 @@ class NaiveGraphConstructor:
         mode = _EF_MODES.get(frozenset(self.edge_features_to_use))
         if mode is None:
             raise NotImplementedError(f"EDGE_FEATURES_TO_USE={self.edge_features_to_use}")
-        A = {0: J + 2, 1: J, 2: 1, 3: 2, 4: J + 3}[mode]
+        if mode in _EF_TAG_MODES and tags is None:
+            raise TypeError(f"EDGE_FEATURES_TO_USE={self.edge_features_to_use} needs tagmaps")
+        A = {0: J + 2, 1: J, 2: 1, 3: 2, 4: J + 3, 5: J + 3, 6: 1, 7: 1, 8: 1}[mode]
         norm = float(max(W, H)) if self.normalize_node_distance else 1.0
 
         fully = self.mpn_graph_type == "fully" and B <= 1024
@@ -213,7 +220,8 @@ class NaiveGraphConstructor:
             edge_index = self._edges(L, st, joint_det, joint_scores, node_off, fully_off, node_off_h, B, dev)
             E = edge_index.shape[1]
             edge_attr = torch.empty(E, A, dtype=torch.float32, device=dev)
-            _lib.check(L.pemp_edge_features(_lib.ptr(joint_det), _lib.ptr(edge_index), E, J, norm, mode,
+            _lib.check(L.pemp_edge_features(_lib.ptr(joint_det), _lib.ptr(joint_tags), F, _lib.ptr(joint_scores),
+                                            _lib.ptr(edge_index), E, J, norm, mode,
                                             _lib.ptr(edge_attr), st))
         if tags is not None:
             joint_tags = joint_tags.view((N,) + tuple(tags.shape[4:])) if tags.dim() > 4 else joint_tags.view(N)

@@ -39,6 +39,8 @@ def gc_inputs(meta, arrays):
 def gc_config(meta):
     g = pcfg.inference_gc_config(meta["graph"], meta["pool"], meta["mask_crowds"])
     g.DETECT_THRESHOLD = meta["thr"]
+    if "features" in meta:
+        g.EDGE_FEATURES_TO_USE = list(meta["features"])
     return g
 
 
@@ -49,4 +51,6 @@ def mpn_config(meta):
         c.AGGR = meta["aggr"]
     if meta.get("update_mlp"):
         c.USE_NODE_UPDATE_MLP = True
+    if meta.get("edge_in"):
+        c.EDGE_INPUT_DIM = meta["edge_in"]
     return c
