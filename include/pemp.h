@@ -57,6 +57,10 @@ int pemp_device_check(void);
  * Writes det_xyt[b][i] = (x, y, type) int64 and det_scores[b][i] for i < min(n, cap), and
  * n_det[b] = n (the true count, which may exceed cap: re-run with stages = PEMP_DETECT_SELECT
  * and a larger cap; the NMS stage's workspace is reused).
+ * n_det_host (optional): host memory from pemp_host_alloc. Each n is stored into it by the device
+ * when the selection stage starts writing the detections: the caller sets it to -1, launches, and
+ * reads it while the stream keeps running (the one count read-back of ConstructGraph.py's
+ * nonzero calls, without a copy or an event wait).
  * ---------------------------------------------------------------------------------------- */
 enum { PEMP_DETECT_NMS = 1, PEMP_DETECT_SELECT = 2, PEMP_DETECT_ALL = 3 };
 size_t pemp_detect_workspace_size(int B, int J, int H, int W, int topk);
@@ -64,7 +68,10 @@ int pemp_detect(const float* scoremaps /*[B,J,H,W]*/, const float* masks /*[B,H,
                 int B, int J, int H, int W, int pool_kernel, float threshold, int use_threshold,
                 int topk, int stages, void* workspace, size_t workspace_bytes,
                 int64_t* det_xyt /*[B,cap,3]*/, float* det_scores /*[B,cap]*/,
-                int32_t* n_det /*[B]*/, int cap, void* stream);
+                int32_t* n_det /*[B]*/, int cap, int32_t* n_det_host /*[B] or NULL*/, void* stream);
+/* Mapped, coherent host memory (hipHostMalloc) that kernels may store into; NULL on failure. */
+void* pemp_host_alloc(size_t bytes);
+int pemp_host_free(void* p);
 
 /* ------------------------------------------------------------------------------------------
  * Node packing into the batched layout: x[g] = features[b,:,y,x], joint_det[g], joint_scores[g],

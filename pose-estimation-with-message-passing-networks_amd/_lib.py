@@ -46,7 +46,9 @@ SIGNATURES = {
     "pemp_device_check": (c_i32, []),
     "pemp_detect_workspace_size": (c_sz, [c_i32, c_i32, c_i32, c_i32, c_i32]),
     "pemp_detect": (c_i32, [c_p, c_p, c_i32, c_i32, c_i32, c_i32, c_i32, c_f32, c_i32, c_i32, c_i32, c_p, c_sz,
-                            c_p, c_p, c_p, c_i32, c_p]),
+                            c_p, c_p, c_p, c_i32, c_p, c_p]),
+    "pemp_host_alloc": (c_p, [c_sz]),
+    "pemp_host_free": (c_i32, [c_p]),
     "pemp_pack_nodes": (c_i32, [c_p, c_i32, c_p, c_i32, c_i32, c_i32, c_i32, c_i32, c_p, c_p, c_i32, c_p, c_i64,
                                 c_p, c_p, c_p, c_p, c_p, c_p]),
     "pemp_graph_offsets": (c_i32, [c_p, c_i32, c_p, c_p, c_p]),

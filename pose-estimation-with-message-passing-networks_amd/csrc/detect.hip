@@ -478,7 +478,8 @@ __global__ __launch_bounds__(256) void plane_top_kernel(DetectGeom g, float thr,
 __global__ __launch_bounds__(256) void emit_kernel(const float* __restrict__ s, const float* __restrict__ masks,
                                                    DetectGeom g, const uint16_t* __restrict__ cbits,
                                                    DetectWs w, int64_t* __restrict__ det,
-                                                   float* __restrict__ scores, int* __restrict__ n_det, int cap) {
+                                                   float* __restrict__ scores, int* __restrict__ n_det, int cap,
+                                                   int* __restrict__ n_host) {
   __shared__ int top_i[KCAP], top_bit[KCAP], sh[4];
   __shared__ int band_n[MAXB], band_off[MAXB];
   __shared__ unsigned band_nz[MAXB][2];      // non-empty strips of each band (bit = strip, nsx <= 64)
@@ -527,7 +528,12 @@ __global__ __launch_bounds__(256) void emit_kernel(const float* __restrict__ s, 
     const int ntop = __shfl(nt, t);
     if (lane == 0) {
       sh[0] = top_before; sh[1] = top_all + thr_before; sh[2] = ntop;
-      if (t == 0) n_det[b] = top_all + thr_all;
+      if (t == 0) {
+        n_det[b] = top_all + thr_all;
+        // straight into the caller's mapped host memory: the host reads the count while this
+        // kernel writes the detections and the graph kernels run (no copy, no event wait)
+        if (n_host) __hip_atomic_store(&n_host[b], top_all + thr_all, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     }
     if (lane < ntop) { top_i[lane] = w.ptop_i[(size_t)pl * KCAP + lane]; top_bit[lane] = w.ptop_bit[(size_t)pl * KCAP + lane]; }
   }
@@ -650,7 +656,7 @@ static void dispatch_nms(const float* s, const float* masks, const DetectGeom& g
 template <int KMAX>
 static int launch_detect(const float* s, const float* masks, const DetectGeom& g, float thr, int use_thr,
                          int stages, const DetectWs& w, int64_t* det, float* scores, int32_t* n_det, int cap,
-                         hipStream_t st) {
+                         int32_t* n_host, hipStream_t st) {
   if (stages & PEMP_DETECT_NMS) {
     ProfScope prof("detect_nms", st);
     if (use_thr) dispatch_nms<MODE_POS>(s, masks, g, thr, use_thr, w, st);
@@ -666,7 +672,7 @@ static int launch_detect(const float* s, const float* masks, const DetectGeom& g
     }
     ProfScope prof("detect_emit", st);
     hipLaunchKernelGGL(emit_kernel, dim3(g.B * g.J), dim3(256), 0, st, s, masks, g, w.cbits, w, det, scores,
-                       (int*)n_det, cap);
+                       (int*)n_det, cap, (int*)n_host);
     PEMP_LAUNCH_CHECK();
   }
   return PEMP_OK;
@@ -688,7 +694,7 @@ extern "C" size_t pemp_detect_workspace_size(int B, int J, int H, int W, int top
 extern "C" int pemp_detect(const float* scoremaps, const float* masks, int B, int J, int H, int W, int pool_kernel,
                            float threshold, int use_threshold, int topk, int stages, void* workspace,
                            size_t workspace_bytes, int64_t* det_xyt, float* det_scores, int32_t* n_det, int cap,
-                           void* stream) {
+                           int32_t* n_det_host, void* stream) {
   PEMP_CHECK_ARG(scoremaps && workspace && det_xyt && det_scores && n_det, "pemp_detect: null pointer");
   PEMP_CHECK_ARG(B > 0 && J > 0 && J <= MAXJ && H > 0 && W > 0, "pemp_detect: bad shape B=%d J=%d H=%d W=%d", B, J, H, W);
   PEMP_CHECK_ARG(pool_kernel % 2 == 1 && pool_kernel >= 1 && pool_kernel / 2 <= MAXR,
@@ -708,9 +714,28 @@ extern "C" int pemp_detect(const float* scoremaps, const float* masks, int B, in
   }
   const DetectWs w = carve(workspace, g, nullptr);
   const hipStream_t st = as_stream(stream);
+  int32_t* n_host = nullptr;   // device address of the caller's mapped host counts
+  if (n_det_host) {
+    PEMP_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&n_host), n_det_host, 0));
+  }
   if (K <= 8)
     return launch_detect<8>(scoremaps, masks, g, threshold, use_threshold, stages, w, det_xyt, det_scores, n_det,
-                            cap, st);
+                            cap, n_host, st);
   return launch_detect<32>(scoremaps, masks, g, threshold, use_threshold, stages, w, det_xyt, det_scores, n_det,
-                           cap, st);
+                           cap, n_host, st);
+}
+
+// Mapped, coherent host memory for pemp_detect's n_det_host (the kernels store into it directly).
+extern "C" void* pemp_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes ? bytes : 4, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+    set_error("pemp_host_alloc: hipHostMalloc(%zu) failed", bytes);
+    return nullptr;
+  }
+  return p;
+}
+
+extern "C" int pemp_host_free(void* p) {
+  if (p) PEMP_HIP(hipHostFree(p));
+  return PEMP_OK;
 }

@@ -240,13 +240,16 @@ __global__ __launch_bounds__(256) void mpn_count_kernel(const int64_t* __restric
 
 // Exclusive scan of the (type, target) counts -> seg[0..K]; then per-type first workgroup of
 // the edge-step grid (wg_start). One 1024-thread block, 16 contiguous counts per thread per pass
-// (all loads of a pass in flight together), carry across passes.
+// (all loads of a pass in flight together), carry across passes. The per-type segment starts
+// seg[t*N] are captured from LDS on the way out (no read-back of seg).
 constexpr int SCAN_SPT = 16;
 __global__ __launch_bounds__(1024) void mpn_scan_kernel(const int* __restrict__ cnt, int64_t K, int64_t N, int T,
                                                         int G, int* __restrict__ seg, int* __restrict__ wg_start) {
   __shared__ int sh[20 + 2 * (MAXT + 1)];
   __shared__ int out[1024 * SCAN_SPT];          // one pass of exclusive offsets, stored coalesced
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (threadIdx.x <= T) sh[20 + threadIdx.x] = 0;   // (K = 0: every segment start is 0)
+  __syncthreads();
   int carry = 0;
   for (int64_t base = 0; base < K; base += 1024 * SCAN_SPT) {
     const int64_t k0 = base + (int64_t)threadIdx.x * SCAN_SPT;
@@ -291,12 +294,16 @@ __global__ __launch_bounds__(1024) void mpn_scan_kernel(const int* __restrict__ 
     __syncthreads();
     const int64_t lim = K - base < 1024 * SCAN_SPT ? K - base : 1024 * SCAN_SPT;
     for (int k = threadIdx.x; k < lim; k += 1024) seg[base + k] = out[k];
+    if (threadIdx.x < T) {                                  // seg[t * N] of this pass
+      const int64_t key = (int64_t)threadIdx.x * N;
+      if (key >= base && key < base + lim) sh[20 + threadIdx.x] = out[key - base];
+    }
     __syncthreads();
   }
-  if (threadIdx.x == 0) seg[K] = carry;
-  __syncthreads();
-  // wg_start: T + 1 reads of seg in parallel, then a short serial sum
-  if (threadIdx.x <= T) sh[20 + threadIdx.x] = seg[(int64_t)threadIdx.x * N];
+  if (threadIdx.x == 0) {
+    seg[K] = carry;
+    sh[20 + T] = carry;
+  }
   __syncthreads();
   // split G edge-pass workgroups (one per CU) over the types in proportion to their edge counts:
   // floor shares, >= 1 per non-empty type, leftovers by largest remainder (ties: lower type);
@@ -1892,10 +1899,6 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
 
   const bool fused_heads_ = node_heads_fused(*w);
   const bool fused_embed_ = node_embed_fused(*w);
-  if (!(desc->flags & PEMP_MPN_PREPARED)) {
-    const int rc0 = launch_prepare(desc, edge_index, node_types, N, E, ws, st);
-    if (rc0) return rc0;
-  }
   // LDS image of the node-side MLPs: the caller's (pemp_mpn_node_image) or built here
   const float* node_img = w->node_img;
   if (!node_img && (fused_heads_ || fused_embed_)) {
@@ -1924,6 +1927,13 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
   const bool first_fused = PEMP_FUSED_FIRST && E > 0 && steps >= 1 && steps > aux + 1 && emb_lds &&
                            emb_prec == desc->precision &&
                            (size_t)(edge_lds_base(false, upd_fused) + emb_lo.total) * sizeof(float) <= 160 * 1024;
+  // launched after the node embedding + first node table (which need no edge order), so that the
+  // host issues the short prepare kernels while the GPU runs those node kernels
+  auto edge_prelude = [&]() -> int {
+  if (!(desc->flags & PEMP_MPN_PREPARED)) {
+    const int rc0 = launch_prepare(desc, edge_index, node_types, N, E, ws, st);
+    if (rc0) return rc0;
+  }
   if (E > 0 && steps >= 1 && !first_fused) {
     ProfScope prof("edge_embed", st);
     if (emb_lds) {
@@ -1943,6 +1953,8 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
     }
     PEMP_LAUNCH_CHECK();
   }
+  return PEMP_OK;
+  };
 
   // ---- iterations ----
   const int NO = 128 + 64 * T;
@@ -2009,6 +2021,7 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
     if ((rc = rows_mlp("node_embed", w->node_emb, x, desc->node_in_dim, N, ws.X, 128, ws.X + 64, 128, st))) return rc;
   }
   if ((rc = node_step(fused_embed ? ROWS_EMBED : ROWS_NONE, steps > 0, steps > 0 ? -1 : 0, false))) return rc;
+  if ((rc = edge_prelude())) return rc;
   float* e_cur = ws.EA;                           // r of the pass (R0 from the separate embedding)
   float* e_nxt = ws.EB;
   int rec = 0;

@@ -39,24 +39,35 @@ class NaiveGraphConstructor:
     _ws_knn = _lib.Workspace()
     _cap = 512   # detections per image kept between calls (grows on overflow)
     _graph_hint = {}   # (shape key) -> (node, edge) capacities of the fully-graph capacity build
-    _pinned = {}
-    _events = {}
+    _host_counts_buf = {}   # device index -> (capacity, address, int32 view) of mapped host memory
 
     @classmethod
-    def _pinned_counts(cls, B):
-        buf = cls._pinned.get("counts")
-        if buf is None or buf.numel() < B:
-            buf = torch.empty(max(B, 64), dtype=torch.int32, pin_memory=True)
-            cls._pinned["counts"] = buf
-        return buf[:B]
+    def _host_counts(cls, L, dev, B):
+        """[B] int32 view of mapped host memory that pemp_detect stores the per-image counts into."""
+        ent = cls._host_counts_buf.get(dev.index)
+        if ent is None or ent[0] < B:
+            cap = max(B, 64)
+            addr = L.pemp_host_alloc(4 * cap)
+            if not addr:
+                raise RuntimeError(f"libpemp: {L.pemp_last_error().decode()}")
+            if ent is not None:
+                L.pemp_host_free(ent[1])
+            ent = (cap, addr, np.ctypeslib.as_array((ctypes.c_int32 * cap).from_address(addr)))
+            cls._host_counts_buf[dev.index] = ent
+        return ent[2][:B]
 
-    @classmethod
-    def _copy_event(cls, dev):
-        ev = cls._events.get(dev)
-        if ev is None:
-            ev = torch.cuda.Event()
-            cls._events[dev] = ev
-        return ev
+    @staticmethod
+    def _wait_counts(counts, dev):
+        """Spin until the device has stored every image's count (pemp_detect's n_det_host): the host
+        learns the counts while the emit and graph kernels still run. A stream sync bounds the wait."""
+        spins = 0
+        while counts.min() < 0:
+            spins += 1
+            if spins > 200000:
+                torch.cuda.current_stream(dev).synchronize()
+                if counts.min() < 0:
+                    raise RuntimeError("pemp_detect: the device did not publish the detection counts")
+        return counts.tolist()
 
     def __init__(self, scoremaps, tagmaps, features, joints_gt, factor_list, masks, device, config, testing,
                  heatmaps, num_joints):
@@ -114,9 +125,11 @@ class NaiveGraphConstructor:
         det = torch.empty(B, cap, 3, dtype=torch.int64, device=dev)
         dsc = torch.empty(B, cap, dtype=torch.float32, device=dev)
         n_det = torch.empty(B, dtype=torch.int32, device=dev)
+        counts_h = self._host_counts(L, dev, B)
+        counts_h.fill(-1)
         _lib.check(L.pemp_detect(_lib.ptr(sm), _lib.ptr(masks), B, J, H, W, self.pool_kernel_size, thr, int(use_thr),
                                  topk, 3, _lib.ptr(ws), ws.numel(), _lib.ptr(det), _lib.ptr(dsc), _lib.ptr(n_det),
-                                 cap, st))
+                                 cap, counts_h.ctypes.data, st))
         # host-side preparation of the graph stage, while the detection kernels run
         feats = self.features
         if feats.dtype != torch.float32:
@@ -142,13 +155,9 @@ class NaiveGraphConstructor:
         hint = NaiveGraphConstructor._graph_hint.get(gkey) if fully else None
         built = None
         if hint is not None:
-            # capacity mode: the graph build is queued behind the count copy, so the GPU builds the
-            # graph while the host waits for (and reads) the counts (pemp_fully_graph_build_cap)
+            # capacity mode: the graph build is queued before the counts are read, so the GPU builds
+            # the graph while the host waits for them (pemp_fully_graph_build_cap)
             n_cap, e_cap = hint
-            host = self._pinned_counts(B)
-            host.copy_(n_det, non_blocking=True)
-            ev = self._copy_event(dev)
-            ev.record(torch.cuda.current_stream(dev))
             bufs = (torch.empty(n_cap, C, dtype=torch.float32, device=dev),
                     torch.empty(n_cap, 3, dtype=torch.int64, device=dev),
                     torch.empty(n_cap, dtype=torch.float32, device=dev),
@@ -159,11 +168,10 @@ class NaiveGraphConstructor:
             _lib.check(L.pemp_fully_graph_build_cap(
                 _lib.ptr(n_det), B, _lib.ptr(det), _lib.ptr(dsc), cap, _lib.ptr(feats), C, _lib.ptr(tags), F, J, H, W,
                 n_cap, e_cap, norm, mode, *[_lib.ptr(t) for t in bufs], st))
-            ev.synchronize()
-            counts_l = host.tolist()
+            counts_l = self._wait_counts(counts_h, dev)
             built = bufs
         else:
-            counts_l = n_det.tolist()                       # the one host read-back of the batch
+            counts_l = self._wait_counts(counts_h, dev)      # the one host read-back of the batch
         mx = max(counts_l) if counts_l else 0
         cap_used = cap                                      # the detections the capacity build read
         if mx > cap:
@@ -173,7 +181,7 @@ class NaiveGraphConstructor:
             dsc = torch.empty(B, cap, dtype=torch.float32, device=dev)
             _lib.check(L.pemp_detect(_lib.ptr(sm), _lib.ptr(masks), B, J, H, W, self.pool_kernel_size, thr,
                                      int(use_thr), topk, 2, _lib.ptr(ws), ws.numel(), _lib.ptr(det), _lib.ptr(dsc),
-                                     _lib.ptr(n_det), cap, st))
+                                     _lib.ptr(n_det), cap, None, st))
         N = sum(counts_l)
         E_fully = sum(c * (c - 1) for c in counts_l if c > 1)
         if fully:   # capacities for the next batch of this shape: 25 % headroom over this one
