@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PEMP_ABI_VERSION 4
+#define PEMP_ABI_VERSION 5
 
 enum {
   PEMP_OK = 0,
@@ -217,6 +217,9 @@ typedef struct pemp_mpn_weights {
   const float* attn_bv;    /* AGGR_SUB node_edge_attn_per_type (layers.py:199-201, 245-246): [17] attn_net.0.bias;
                               messages from source type t use row t of attn_w and attn_bv[t]. NULL: one shared
                               row attn_w[64] with bias attn_b (node_edge_attn) */
+  pemp_mlp upd_mlp;        /* UPDATE_TYPE hierarch_mlp / hierarch_cnn (layers.py:89-154) folded into dense
+                              layers over agg[n] flattened to [T*64] (ReLU each; widths % 16 == 0, last 64);
+                              n_layers = 0 otherwise. Excludes upd_w. */
 } pemp_mpn_weights;
 
 typedef struct pemp_mpn_desc {

@@ -98,6 +98,8 @@ def mpn_cfg(meta):
         c.USE_NODE_UPDATE_MLP = True
     if meta.get("edge_in"):
         c.EDGE_INPUT_DIM = meta["edge_in"]
+    if meta.get("update_type"):
+        c.UPDATE_TYPE = meta["update_type"]
     return c
 
 
@@ -172,6 +174,12 @@ MPN_CASES = {
                            "gc_small_fully"),
     "mpn_attn_c2_t3": (dict(J=17, steps=3, variant="attn", salt=9.5), "gc_c2_like"),
     "mpn_attn_ae_t2": (dict(J=17, steps=2, variant="attn", salt=11.5, edge_in=20), "gc_ae_pos_conn_f2"),
+    "mpn_attn_hmlp_t2": (dict(J=17, steps=2, variant="attn", salt=12.5, update_type="hierarch_mlp"),
+                         "gc_small_fully"),
+    "mpn_max_hmlp_j14_t2": (dict(J=14, steps=2, variant="attn", salt=13.5, update_type="hierarch_mlp",
+                                 aggr_sub="None", aggr="max"), "gc_noisy_masked_j14"),
+    "mpn_attn_hcnn_t3": (dict(J=17, steps=3, variant="attn", salt=14.5, update_type="hierarch_cnn"),
+                         "gc_realistic_knn"),
     "mpn_attn_pertype_t2": (dict(J=17, steps=2, variant="attn", salt=10.5, aggr_sub="node_edge_attn_per_type",
                                  aggr="add", attn_gain=16.0), "gc_realistic_knn"),
 }

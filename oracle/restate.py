@@ -312,8 +312,47 @@ def mpn_layer(sd, cfg, x, e, edge_index, node_types):
             sel = src_type == t
             if sel.any():
                 upd[:, t] = _scatter(m[sel], i[sel], n, cfg.AGGR)
-    x_new = F.relu(F.linear(upd.reshape(n, -1), sd[f"{p}.update_mlp.0.weight"], sd[f"{p}.update_mlp.0.bias"]))
+    utype = getattr(cfg, "UPDATE_TYPE", "mlp")
+    if utype == "hierarch_mlp":
+        x_new = _hierarch_mlp(sd, f"{p}.update_mlp", upd, num_types)
+    elif utype == "hierarch_cnn":
+        x_new = _hierarch_cnn(sd, f"{p}.update_mlp", upd)
+    else:
+        x_new = F.relu(F.linear(upd.reshape(n, -1), sd[f"{p}.update_mlp.0.weight"], sd[f"{p}.update_mlp.0.bias"]))
     return x_new, e_new
+
+
+def _hierarch_mlp(sd, p, update, num_joints):
+    """HierarchUpdateMlp.forward (layers.py:109-128)."""
+    n = update.shape[0]
+    if num_joints == 17:
+        order_1 = [(0, 1, 2, 3, 4), (5, 6), (7, 9), (8, 10), (11, 12), (13, 15), (14, 16)]
+    else:
+        order_1 = [(0, 1), (2, 3), (4, 6), (5, 7), (8, 9), (10, 12), (11, 13)]
+    order_2 = [(0, 1), (1, 2), (1, 3), (1, 4), (4, 5), (4, 6)]
+    d2 = update.shape[2] // 2
+    out_1 = torch.zeros(n, 7, d2, dtype=update.dtype)
+    out_2 = torch.zeros(n, 6, d2, dtype=update.dtype)
+    for i, types in enumerate(order_1):
+        out_1[:, i] = F.relu(F.linear(update[:, list(types)].reshape(n, -1), sd[f"{p}.first_layer.{i}.weight"],
+                                      sd[f"{p}.first_layer.{i}.bias"]))
+    for i, types in enumerate(order_2):
+        out_2[:, i] = F.relu(F.linear(out_1[:, list(types)].reshape(n, -1), sd[f"{p}.second_layer.{i}.weight"],
+                                      sd[f"{p}.second_layer.{i}.bias"]))
+    return F.relu(F.linear(out_2.reshape(n, -1), sd[f"{p}.final.weight"], sd[f"{p}.final.bias"]))
+
+
+def _hierarch_cnn(sd, p, update):
+    """HierarchUpdateCnn.forward (layers.py:142-154)."""
+    n = update.shape[0]
+    update = update.permute(0, 2, 1)
+    order_1 = [5, 6, 7, 9, 8, 10, 11, 12, 13, 15, 14, 16]
+    order_2 = [0, 1, 0, 2, 0, 3, 3, 4, 3, 5]
+    out_1 = F.relu(F.conv1d(update[:, :, order_1], sd[f"{p}.conv_1.weight"], sd[f"{p}.conv_1.bias"], stride=2))
+    head = F.relu(F.linear(update[:, :, :4].reshape(n, -1), sd[f"{p}.head_layer.weight"], sd[f"{p}.head_layer.bias"]))
+    update = torch.cat([head[:, :, None], out_1], dim=2)
+    update = F.relu(F.conv1d(update[:, :, order_2], sd[f"{p}.conv_2.weight"], sd[f"{p}.conv_2.bias"], stride=2))
+    return F.relu(F.linear(update.reshape(n, -1), sd[f"{p}.final.weight"], sd[f"{p}.final.bias"]))
 
 
 def _num_types(cfg):

@@ -1256,6 +1256,82 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
 //   x_new[n] = ReLU(b + sum_t U_t · agg[n, t])   (layers.py:253-258; empty segments read as 0)
 //   without an update MLP: x_new[n] = agg[n, 0]  (MPLayer, layers.py:32-86)
 // Written to X[:, 64:128]. Every load of a wave is issued before its first MFMA.
+// ---- generic node-update MLP on the per-type aggregates (UPDATE_TYPE hierarch_mlp / hierarch_cnn,
+// layers.py:89-154): the host folds each variant into up to 4 dense layers over agg[n] flattened
+// to [T*64] (block-sparse structure as explicit zeros, the Conv1d / permute / reshape orders as
+// column permutations), every layer ReLU'd. One 256-thread block per 16 nodes; activations stay in
+// LDS; layer l: each wave owns 16-output blocks, K in chunks of 16 on v_mfma_f32_16x16x4_f32
+// (weights float4 from global / L2, activations float4 from LDS).
+struct NodeMlpArgs {
+  const float* agg;
+  const int* seg;
+  int T;
+  int64_t N;
+  pemp_mlp mlp;
+  int max_out;      // widest layer output
+  float* X;
+};
+
+__host__ __device__ inline int nmlp_stride(int k) { return (k + 15) / 16 * 16 + 8; }   // 8 * odd mod 64 dwords
+
+__global__ __launch_bounds__(256) void node_mlp_kernel(NodeMlpArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
+  const int64_t n0 = (int64_t)blockIdx.x * 16, N = a.N;
+  const int T = a.T, K0 = 64 * T;
+  const int S[2] = {nmlp_stride(K0 > a.max_out ? K0 : a.max_out), nmlp_stride(a.max_out)};
+  float* buf[2] = {lds, lds + 16 * S[0]};
+  // agg rows of the 16 nodes; an empty (n, t) segment was never written by the edge pass -> 0
+  for (int idx = threadIdx.x; idx < 16 * K0 / 4; idx += 256) {
+    const int r = idx / (K0 / 4), col = (idx - r * (K0 / 4)) * 4, t = col >> 6;
+    const int64_t n = n0 + r;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (n < N && a.seg[t * N + n + 1] > a.seg[t * N + n]) v = ld4(a.agg + n * K0 + col);
+    *reinterpret_cast<float4*>(&buf[0][r * S[0] + col]) = v;
+  }
+  __syncthreads();
+  const int L = a.mlp.n_layers;
+  for (int l = 0; l < L; ++l) {
+    const pemp_layer ly = a.mlp.layer[l];
+    const float* in = buf[l & 1];
+    float* out = buf[(l + 1) & 1];
+    const int si = S[l & 1], so = S[(l + 1) & 1];
+    const int K = ly.in_dim, M = ly.out_dim;
+    const bool last = l + 1 == L;
+    for (int jb = wave; jb < M / 16; jb += 4) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const float* wrow = ly.w + (int64_t)(16 * jb + c) * K + 4 * g;
+      const float* arow = in + c * si + 4 * g;
+      for (int k0 = 0; k0 < K; k0 += 16) {
+        const float4 w4 = ld4(wrow + k0);
+        const float4 x4 = *reinterpret_cast<const float4*>(arow + k0);
+        acc = mfma4(w4.x, x4.x, acc);
+        acc = mfma4(w4.y, x4.y, acc);
+        acc = mfma4(w4.z, x4.z, acc);
+        acc = mfma4(w4.w, x4.w, acc);
+      }
+      // lane (c, g) holds outputs 16 jb + 4 g + r of node c
+      const float4 b4 = ld4(ly.b + 16 * jb + 4 * g);
+      float4 o = make_float4(acc[0] + b4.x, acc[1] + b4.y, acc[2] + b4.z, acc[3] + b4.w);
+      if (ly.relu) { o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f); }
+      if (!last) *reinterpret_cast<float4*>(&out[c * so + 16 * jb + 4 * g]) = o;
+      else if (n0 + c < N) *reinterpret_cast<float4*>(&a.X[(n0 + c) * 128 + 64 + 16 * jb + 4 * g]) = o;
+    }
+    __syncthreads();
+  }
+}
+
+inline int nmlp_max_out(const pemp_mlp& m) {
+  int mx = 0;
+  for (int l = 0; l < m.n_layers; ++l) mx = std::max(mx, m.layer[l].out_dim);
+  return mx;
+}
+
+inline size_t nmlp_lds_bytes(int T, const pemp_mlp& m) {
+  const int mo = nmlp_max_out(m);
+  return (size_t)16 * (nmlp_stride(std::max(64 * T, mo)) + nmlp_stride(mo)) * sizeof(float);
+}
+
 struct NodeUpdateArgs {
   const float* agg;
   const int* seg;
@@ -1864,6 +1940,18 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
   PEMP_CHECK_ARG(desc->steps >= 0 && desc->aux_loss_steps >= 0, "pemp_mpn_forward: bad steps");
   PEMP_CHECK_ARG(desc->aggr >= PEMP_AGGR_ATTN && desc->aggr <= PEMP_AGGR_MAX, "pemp_mpn_forward: bad aggr");
   PEMP_CHECK_ARG(desc->aggr != PEMP_AGGR_ATTN || w->attn_w, "pemp_mpn_forward: attention needs attn_w");
+  if (w->upd_mlp.n_layers > 0) {   // hierarchical update (dense-folded): T*64 -> ... -> 64, widths % 16
+    const pemp_mlp& m = w->upd_mlp;
+    PEMP_CHECK_ARG(!w->upd_w && m.n_layers <= 4, "pemp_mpn_forward: upd_mlp excludes upd_w (<= 4 layers)");
+    for (int l = 0; l < m.n_layers; ++l) {
+      const pemp_layer& ly = m.layer[l];
+      PEMP_CHECK_ARG(ly.w && ly.b && ly.in_dim % 16 == 0 && ly.out_dim % 16 == 0 && ly.out_dim > 0 &&
+                         ly.in_dim == (l == 0 ? 64 * desc->num_types : m.layer[l - 1].out_dim),
+                     "pemp_mpn_forward: upd_mlp layer %d is %d -> %d", l, ly.in_dim, ly.out_dim);
+    }
+    PEMP_CHECK_ARG(m.layer[m.n_layers - 1].out_dim == 64, "pemp_mpn_forward: upd_mlp must end at 64");
+    PEMP_CHECK_ARG(nmlp_lds_bytes(desc->num_types, m) <= 160 * 1024, "pemp_mpn_forward: upd_mlp too wide");
+  }
   PEMP_CHECK_ARG(mlp_ok(w->node_emb, 128, 128) && w->node_emb.layer[w->node_emb.n_layers - 1].out_dim == 64 &&
                      w->node_emb.layer[0].in_dim == desc->node_in_dim,
                  "pemp_mpn_forward: node embedding must map node_in_dim (<=128) -> 64");
@@ -1966,7 +2054,13 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
   const unsigned table_grid = (unsigned)(((N + 16 * TBL_TILES - 1) / (16 * TBL_TILES)) * table_groups);
   // x for the next stage (mode) + heads when slot >= 0, then the node table when `table`
   auto node_step = [&](int mode, bool table, int slot, bool dup) -> int {
-    if (mode == -1) {                                  // update MLP on non-linear aggregates
+    if (mode == -1 && w->upd_mlp.n_layers > 0) {     // hierarchical update MLP (dense-folded)
+      NodeMlpArgs ma{ws.agg, ws.seg, T, N, w->upd_mlp, nmlp_max_out(w->upd_mlp), ws.X};
+      ProfScope prof("node_update", st);
+      hipLaunchKernelGGL(node_mlp_kernel, dim3(node_grid), dim3(256), nmlp_lds_bytes(T, w->upd_mlp), st, ma);
+      PEMP_LAUNCH_CHECK();
+      mode = ROWS_NONE;
+    } else if (mode == -1) {                           // update MLP on non-linear aggregates
       NodeUpdateArgs ua{ws.agg, ws.seg, T, N, w->upd_w, w->upd_b, ws.X};
       ProfScope prof("node_update", st);
       hipLaunchKernelGGL(node_update_kernel, dim3(node_grid, 4), dim3(64 * UPD_WAVES), 0, st, ua);
@@ -2057,7 +2151,7 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
     }
     // node update + next node table; heads when recorded (the last iteration's heads also fill
     // the post-loop slot: NODE_STEPS = 0 leaves x unchanged, NodeClassificationMPNSimple.py:93-94)
-    const int mode = upd_fused ? ROWS_SUM : w->upd_w ? -1 : ROWS_COPY;
+    const int mode = upd_fused ? ROWS_SUM : (w->upd_w || w->upd_mlp.n_layers > 0) ? -1 : ROWS_COPY;
     if ((rc = node_step(mode, !last, record ? rec : -1, last))) return rc;
     if (record) ++rec;
     float* tmp = e_cur; e_cur = e_nxt; e_nxt = tmp;

@@ -9,6 +9,8 @@
   with A = W1_xi·x and B = W1_xj·x computed per NODE (the ``pre_w`` block), and the e_init term
   computed once per edge (``q0``). The type-t message MLP W_t·[x_i ‖ e'] + b_t is split the same
   way into a per-node part P_t (``pre_w``) and a per-edge part (``msg_w``).
+* UPDATE_TYPE hierarch_mlp / hierarch_cnn (``layers.py:89-154``) become up to three dense layers
+  over the flattened per-type aggregates (``hierarch_dense_layers``), run by ``node_mlp_kernel``.
 * Everything is stored [out_pad][in_pad], zero padded to multiples of 16 (MFMA 16x16x4 tiles).
 The node table the kernels use holds x = [x_init ‖ x_cur] (128 wide); without skip connections
 the x_init/e_init columns get zero weights.
@@ -19,6 +21,8 @@ import torch
 import torch.nn as nn
 
 from .. import _lib
+from .hierarch import (HIERARCH_CNN_ORDER_1, HIERARCH_CNN_ORDER_2, HIERARCH_ORDER_1, HIERARCH_ORDER_2,
+                          HierarchUpdateCnn, HierarchUpdateMlp)
 
 
 def _pad16(n):
@@ -122,6 +126,62 @@ class Folded:
         return m
 
 
+def hierarch_dense_layers(upd, T):
+    """UPDATE_TYPE hierarch_mlp / hierarch_cnn as dense fp64 layers over agg[n] flattened to [T*64]
+    (index t*64 + d), each followed by ReLU as in the reference. Block-sparse structure becomes
+    explicit zeros; the reference's view / permute / reshape orders become column permutations.
+    Returns [(W [out, in], b [out])]."""
+    D = 64
+    h = D // 2
+    g = lambda p: p.detach().double().cpu()
+    if isinstance(upd, HierarchUpdateMlp):               # layers.py:109-128
+        order_1 = HIERARCH_ORDER_1[upd.num_joints]
+        W1 = torch.zeros(7 * h, T * D, dtype=torch.float64)
+        b1 = torch.zeros(7 * h, dtype=torch.float64)
+        for i, types in enumerate(order_1):              # update[:, types].view(N, -1): type-major
+            Wi = g(upd.first_layer[i].weight)
+            for q, t in enumerate(types):
+                W1[i * h:(i + 1) * h, t * D:(t + 1) * D] += Wi[:, q * D:(q + 1) * D]
+            b1[i * h:(i + 1) * h] = g(upd.first_layer[i].bias)
+        W2 = torch.zeros(6 * h, 7 * h, dtype=torch.float64)
+        b2 = torch.zeros(6 * h, dtype=torch.float64)
+        for i, pair in enumerate(HIERARCH_ORDER_2):
+            Wi = g(upd.second_layer[i].weight)
+            for q, j in enumerate(pair):
+                W2[i * h:(i + 1) * h, j * h:(j + 1) * h] += Wi[:, q * h:(q + 1) * h]
+            b2[i * h:(i + 1) * h] = g(upd.second_layer[i].bias)
+        return [(W1, b1), (W2, b2), (g(upd.final.weight), g(upd.final.bias))]
+    # HierarchUpdateCnn, layers.py:142-154. U = agg.permute(0, 2, 1): U[n, d, t] = agg[n, t, d].
+    # layer 1 outputs: position 0 = head, positions 1..6 = conv_1 outputs; index pos * 32 + o
+    W1 = torch.zeros(7 * h, T * D, dtype=torch.float64)
+    b1 = torch.zeros(7 * h, dtype=torch.float64)
+    Wh = g(upd.head_layer.weight)                        # U[:, :, :4].reshape(N, -1): index d * 4 + t
+    for t in range(4):
+        W1[0:h, t * D:(t + 1) * D] += Wh[:, t::4]
+    b1[0:h] = g(upd.head_layer.bias)
+    Wc = g(upd.conv_1.weight)                            # [32, 64, 2]
+    for p in range(6):
+        for k in range(2):
+            t = HIERARCH_CNN_ORDER_1[2 * p + k]
+            W1[(1 + p) * h:(2 + p) * h, t * D:(t + 1) * D] += Wc[:, :, k]
+        b1[(1 + p) * h:(2 + p) * h] = g(upd.conv_1.bias)
+    # layer 2: conv_2 over positions order_2 -> 5 outputs, index q * 32 + o
+    W2 = torch.zeros(5 * h, 7 * h, dtype=torch.float64)
+    b2 = torch.zeros(5 * h, dtype=torch.float64)
+    Wc2 = g(upd.conv_2.weight)                           # [32, 32, 2]
+    for q in range(5):
+        for k in range(2):
+            pos = HIERARCH_CNN_ORDER_2[2 * q + k]
+            W2[q * h:(q + 1) * h, pos * h:(pos + 1) * h] += Wc2[:, :, k]
+        b2[q * h:(q + 1) * h] = g(upd.conv_2.bias)
+    # final on update.reshape(N, -1) of [N, 32, 5]: index o * 5 + q
+    Wf = g(upd.final.weight)
+    W3 = torch.zeros(D, 5 * h, dtype=torch.float64)
+    for q in range(5):
+        W3[:, q * h:(q + 1) * h] = Wf[:, q::5]
+    return [(W1, b1), (W2, b2), (W3, g(upd.final.bias))]
+
+
 def fold_weights(model, device) -> Folded:
     f = Folded()
     s = f.struct
@@ -192,7 +252,15 @@ def fold_weights(model, device) -> Folded:
         s.attn_w = f.dev(attn[0].weight.detach().double().cpu().reshape(-1), device).data_ptr()
         s.attn_bv = f.dev(attn[0].bias.detach().double().cpu(), device).data_ptr()
     upd = layer.update_mlp
-    if upd is not None:
+    if isinstance(upd, (HierarchUpdateMlp, HierarchUpdateCnn)):
+        layers = hierarch_dense_layers(upd, T)
+        m = _lib.PempMlp()
+        m.n_layers = len(layers)
+        for i, (W, b) in enumerate(layers):
+            wd, bd = f.dev(W, device), f.dev(b, device)
+            m.layer[i] = _lib.PempLayer(wd.data_ptr(), bd.data_ptr(), W.shape[1], W.shape[0], 1, 0)
+        s.upd_mlp = m
+    elif upd is not None:
         s.upd_w = f.dev(upd[0].weight.detach().double().cpu(), device).data_ptr()
         s.upd_b = f.dev(upd[0].bias.detach().double().cpu(), device).data_ptr()
         U = upd[0].weight.detach().double().cpu()

@@ -15,6 +15,7 @@ import torch.nn as nn
 
 from .. import _lib
 from .fold import fold_weights
+from .hierarch import HierarchUpdateCnn, HierarchUpdateMlp
 
 _VALIDATE = os.environ.get("PEMP_VALIDATE", "0") not in ("", "0")   # read once at import
 
@@ -68,21 +69,29 @@ class TypeAwareNodeUpdate(nn.Module):
 
 
 class TypeAwareMPNLayer(nn.Module):
-    """``layers.py:157-258`` (edge MLP agnostic, update ``mlp``)."""
+    """``layers.py:157-258`` (edge MLP agnostic; update ``mlp``, ``hierarch_mlp`` or ``hierarch_cnn``)."""
 
     def __init__(self, node_dim, edge_dim, edge_hidden, aggr, skip=False, edge_mlp="agnostic", num_types=17,
                  aggr_sub=None, update_type="mlp"):
         super().__init__()
         if edge_mlp != "agnostic":
             raise NotImplementedError(f"EDGE_MLP={edge_mlp}")
-        if update_type != "mlp":
+        if update_type not in ("mlp", "hierarch_mlp", "hierarch_cnn"):
             raise NotImplementedError(f"UPDATE_TYPE={update_type}")
+        if update_type == "hierarch_cnn" and num_types != 17:
+            raise NotImplementedError("UPDATE_TYPE=hierarch_cnn indexes types up to 16 (layers.py:148)")
         nf = 2 if skip else 1
         self.aggr, self.aggr_sub, self.num_types, self.skip = aggr, aggr_sub, num_types, skip
         self.mlp_edge = nn.Sequential(nn.Linear(node_dim * 2 * nf + edge_dim * nf, edge_hidden), nn.ReLU(inplace=True),
                                       nn.Linear(edge_hidden, edge_dim), nn.ReLU(inplace=True))
         self.mlp_node = TypeAwareNodeUpdate(node_dim * nf + edge_dim, node_dim)
-        self.update_mlp = nn.Sequential(nn.Linear(node_dim * num_types, node_dim), nn.ReLU(inplace=True))
+        self.update_type = update_type
+        if update_type == "mlp":
+            self.update_mlp = nn.Sequential(nn.Linear(node_dim * num_types, node_dim), nn.ReLU(inplace=True))
+        elif update_type == "hierarch_mlp":
+            self.update_mlp = HierarchUpdateMlp(node_dim, num_types)
+        else:
+            self.update_mlp = HierarchUpdateCnn(node_dim)
         if aggr_sub == "node_edge_attn":
             self.attn_net = nn.Sequential(nn.Linear(edge_dim, 1))
         elif aggr_sub == "node_edge_attn_per_type":

@@ -53,4 +53,6 @@ def mpn_config(meta):
         c.USE_NODE_UPDATE_MLP = True
     if meta.get("edge_in"):
         c.EDGE_INPUT_DIM = meta["edge_in"]
+    if meta.get("update_type"):
+        c.UPDATE_TYPE = meta["update_type"]
     return c

@@ -170,3 +170,18 @@ def test_repeated_calls_and_in_place_inputs():
     rpe, rpn, rpc, _ = restate.mpn_forward(sd, cfg, g[0] * 0.5, g[1], g[2], g[7][:, 2])
     for a, b in zip(o[0] + o[1] + o[2], rpe + rpn + rpc):
         assert max_err(a, b) < TOL
+
+
+@pytest.mark.parametrize("utype", ["hierarch_mlp", "hierarch_cnn"])
+def test_hierarch_update_c3_shape(utype):
+    """UPDATE_TYPE hierarch_* (node_mlp_kernel on the dense-folded layers) at a C3-shaped batch."""
+    g = graph(8, 17, 160, 160, 9, "fully")
+    cfg = pcfg.published_mpn_config(17, 3, "attn")
+    cfg.UPDATE_TYPE = utype
+    model, sd = make_model(cfg, 5.5, "fp32")
+    x, ea, ei, types = g[0], g[1], g[2], g[7][:, 2]
+    pe, pn, pc, _ = run(model, x, ea, ei, types)
+    rpe, rpn, rpc, _ = restate.mpn_forward(sd, cfg, x, ea, ei, types)
+    for a, b in zip(pe + pn + pc, rpe + rpn + rpc):
+        assert a.shape == b.shape
+        assert max_err(a, b) < TOL
