@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PEMP_ABI_VERSION 5
+#define PEMP_ABI_VERSION 6
 
 enum {
   PEMP_OK = 0,
@@ -220,6 +220,11 @@ typedef struct pemp_mpn_weights {
   pemp_mlp upd_mlp;        /* UPDATE_TYPE hierarch_mlp / hierarch_cnn (layers.py:89-154) folded into dense
                               layers over agg[n] flattened to [T*64] (ReLU each; widths % 16 == 0, last 64);
                               n_layers = 0 otherwise. Excludes upd_w. */
+  /* EDGE_MLP per_type (TypeAwareEdgeUpdate, layers.py:275-303; attention aggregation), or NULL:
+   *   e' = ReLU(O1 ReLU(L1[t_dst] x_dst + c1) + O2 ReLU(L2[t_src] x_src + c2) + e2_w ReLU(q0 + e1_w e) + e2_b)
+   * with q0_w / q0_b / e1_w = edge_layer (e_init / e_cur columns), e2_w / e2_b = the e-block of out.1 and
+   * the A / B rows of pre_w zero. L1, L2: [T][64][128] on [x_init | x_cur]; c1, c2: [T][64]; O1, O2: [64][64]. */
+  const float *ept_l1_w, *ept_l1_b, *ept_l2_w, *ept_l2_b, *ept_o1_w, *ept_o2_w;
 } pemp_mpn_weights;
 
 typedef struct pemp_mpn_desc {

@@ -100,6 +100,8 @@ def mpn_cfg(meta):
         c.EDGE_INPUT_DIM = meta["edge_in"]
     if meta.get("update_type"):
         c.UPDATE_TYPE = meta["update_type"]
+    if meta.get("edge_mlp"):
+        c.EDGE_MLP = meta["edge_mlp"]
     return c
 
 
@@ -180,6 +182,9 @@ MPN_CASES = {
                                  aggr_sub="None", aggr="max"), "gc_noisy_masked_j14"),
     "mpn_attn_hcnn_t3": (dict(J=17, steps=3, variant="attn", salt=14.5, update_type="hierarch_cnn"),
                          "gc_realistic_knn"),
+    "mpn_attn_ept_t2": (dict(J=17, steps=2, variant="attn", salt=15.5, edge_mlp="per_type"), "gc_realistic_knn"),
+    "mpn_attn_ept_pt_t3": (dict(J=17, steps=3, variant="attn", salt=16.5, edge_mlp="per_type",
+                                aggr_sub="node_edge_attn_per_type", aggr="add", attn_gain=16.0), "gc_small_fully"),
     "mpn_attn_pertype_t2": (dict(J=17, steps=2, variant="attn", salt=10.5, aggr_sub="node_edge_attn_per_type",
                                  aggr="add", attn_gain=16.0), "gc_realistic_knn"),
 }

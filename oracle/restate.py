@@ -282,8 +282,12 @@ def mpn_layer(sd, cfg, x, e, edge_index, node_types):
     p = "mpn_node_cls"
     j, i = edge_index[0], edge_index[1]                   # message flows j (source) -> i (target)
     n = x.shape[0]
-    h = F.relu(F.linear(torch.cat([x[i], x[j], e], 1), sd[f"{p}.mlp_edge.0.weight"], sd[f"{p}.mlp_edge.0.bias"]))
-    e_new = F.relu(F.linear(h, sd[f"{p}.mlp_edge.2.weight"], sd[f"{p}.mlp_edge.2.bias"]))
+    if getattr(cfg, "EDGE_MLP", "agnostic") == "per_type":
+        e_new = _type_aware_edge_update(sd, f"{p}.mlp_edge", x[i], x[j], e, node_types[i], node_types[j],
+                                        _num_types(cfg))
+    else:
+        h = F.relu(F.linear(torch.cat([x[i], x[j], e], 1), sd[f"{p}.mlp_edge.0.weight"], sd[f"{p}.mlp_edge.0.bias"]))
+        e_new = F.relu(F.linear(h, sd[f"{p}.mlp_edge.2.weight"], sd[f"{p}.mlp_edge.2.bias"]))
     if cfg.AGGR_TYPE == "agnostic":
         m = F.relu(F.linear(torch.cat([x[i], e_new], 1), sd[f"{p}.mlp_node.0.weight"], sd[f"{p}.mlp_node.0.bias"]))
         agg = _scatter(m, i, n, cfg.AGGR)
@@ -320,6 +324,23 @@ def mpn_layer(sd, cfg, x, e, edge_index, node_types):
     else:
         x_new = F.relu(F.linear(upd.reshape(n, -1), sd[f"{p}.update_mlp.0.weight"], sd[f"{p}.update_mlp.0.bias"]))
     return x_new, e_new
+
+
+def _type_aware_edge_update(sd, p, nodes_1, nodes_2, edges, types_1, types_2, num_joints):
+    """TypeAwareEdgeUpdate.forward (layers.py:288-303)."""
+    rows = nodes_1.shape[0]
+    out_dim = sd[f"{p}.edge_layer.bias"].shape[0]
+    tmp_1 = torch.zeros(rows, out_dim, dtype=nodes_1.dtype)
+    tmp_2 = torch.zeros(rows, out_dim, dtype=nodes_1.dtype)
+    for t in range(num_joints):
+        sel = types_1 == t
+        tmp_1[sel] = F.linear(nodes_1[sel], sd[f"{p}.layer_1.{t}.weight"], sd[f"{p}.layer_1.{t}.bias"])
+    for t in range(num_joints):
+        sel = types_2 == t
+        tmp_2[sel] = F.linear(nodes_2[sel], sd[f"{p}.layer_2.{t}.weight"], sd[f"{p}.layer_2.{t}.bias"])
+    ed = F.linear(edges, sd[f"{p}.edge_layer.weight"], sd[f"{p}.edge_layer.bias"])
+    cat = F.relu(torch.cat([tmp_1, tmp_2, ed], 1))
+    return F.relu(F.linear(cat, sd[f"{p}.out.1.weight"], sd[f"{p}.out.1.bias"]))
 
 
 def _hierarch_mlp(sd, p, update, num_joints):

@@ -8,7 +8,7 @@ import os
 
 LIB_PATH = os.environ.get("PEMP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc",
                                                      "libpemp.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 ERR_INVALID_ARG, ERR_HIP, ERR_WORKSPACE, ERR_UNSUPPORTED = -1, -2, -3, -4
 
@@ -31,7 +31,9 @@ class PempMpnWeights(ctypes.Structure):
                 ("attn_b", c_f32), ("pad_", c_i32),
                 ("e1_bf", c_p), ("e2_bf", c_p), ("msg_bf", c_p), ("head_bf", c_p), ("emb_bf", c_p),
                 ("upd_bf", c_p), ("pre_bf", c_p), ("node_img", c_p), ("attn_bv", c_p),
-                ("upd_mlp", PempMlp)]
+                ("upd_mlp", PempMlp),
+                ("ept_l1_w", c_p), ("ept_l1_b", c_p), ("ept_l2_w", c_p), ("ept_l2_b", c_p), ("ept_o1_w", c_p),
+                ("ept_o2_w", c_p)]
 
 
 class PempMpnDesc(ctypes.Structure):

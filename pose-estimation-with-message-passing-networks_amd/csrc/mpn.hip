@@ -939,7 +939,7 @@ constexpr int LDS_HEAD = (D + 32) * LDW + D + 32 + 32;
 // in 16-edge tiles; a segment that crosses a tile boundary is carried in registers.
 // PREC: 0 = exact fp32 MFMA (v_mfma_f32_16x16x4_f32), 1 = bf16x3 split precision (see gemm_bf3).
 // The LDS image has the same size in both: a 64 x LDW fp32 tile = its bf16 hi and lo tiles.
-enum { STAGE_FIRST = 0, STAGE_MID = 1, STAGE_LAST = 2 };
+enum { STAGE_FIRST = 0, STAGE_MID = 1, STAGE_LAST = 2, STAGE_EPT = 4 };
 #ifndef PEMP_FUSED_FIRST
 #define PEMP_FUSED_FIRST 0
 #endif
@@ -953,6 +953,10 @@ constexpr int edge_waves() { return STAGE == STAGE_FIRST ? 8 : EDGE_WAVES; }
 template <int AGG, int HEAD, int PREC, int UPD, int STAGE>
 __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(EdgeStepArgs a) {
   constexpr int NW = edge_waves<STAGE>();
+  // STAGE bit 2 (STAGE_EPT): EDGE_MLP per_type (TypeAwareEdgeUpdate, layers.py:275-303). The node
+  // terms A'[dst] + B'[src] (already through their own ReLU and out-block, node_ept_kernel) join
+  // after the e-block GEMM instead of inside the first ReLU.
+  constexpr bool EPT = (STAGE & STAGE_EPT) != 0;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* wl = sm;                               // [3][64][LDW]: e1_w (e_cur part), e2_w, msg_w[t]
   float* vec = sm + LDS_W;                      // e2_b[64] | attn_w[64]
@@ -1009,7 +1013,7 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
       else if (threadIdx.x < D + 64) hb[threadIdx.x] = a.head.layer[2].w[threadIdx.x - D - 32];
     }
     if (UPD) stage_tile64<PREC>(uw, a.upd_w + 64 * t, 64 * T, PREC == 1 ? a.upd_bf + (int64_t)t * 2 * D * D : nullptr);
-    if (STAGE == STAGE_FIRST) stage_embed<PREC>(sm + a.emb_off, a.emb, a.Lo, a.emb_bf, a.q0_w, a.q0_b);
+    if ((STAGE & 3) == STAGE_FIRST) stage_embed<PREC>(sm + a.emb_off, a.emb, a.Lo, a.emb_bf, a.q0_w, a.q0_b);
   }
   __syncthreads();
 
@@ -1059,7 +1063,8 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
     }
     // gathers: r (or edge_attr) and Q0 rows of the edge, node-table rows of target and source
     float h[4][4], m[4][4], q0r[4][4];
-    if (STAGE == STAGE_FIRST) {
+    float ab[4][4];                               // EPT: A'[dst] + B'[src]
+    if ((STAGE & 3) == STAGE_FIRST) {
       // embedding first (few live registers), then the node-table gathers
       float x[4][4];
       load_edge_attr(a.ea, a.A, a.s_orig[q], x);
@@ -1091,12 +1096,17 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
         const float4 xa = ld4(a.NT + (int64_t)dst * a.t_nt_ld + f);
         const float4 xb = ld4(a.NT + (int64_t)src * a.t_nt_ld + 64 + f);
         const float4 xp = ld4(ntP + (int64_t)dst * a.t_nt_ld + f);
-        if (STAGE == STAGE_MID) {
+        if ((STAGE & 3) == STAGE_MID) {
           const float4 qq = ld4(a.Q0 + (int64_t)q * D + f);
           q0r[ob][0] = qq.x; q0r[ob][1] = qq.y; q0r[ob][2] = qq.z; q0r[ob][3] = qq.w;
         }
-        h[ob][0] = rr.x + xa.x + xb.x; h[ob][1] = rr.y + xa.y + xb.y;
-        h[ob][2] = rr.z + xa.z + xb.z; h[ob][3] = rr.w + xa.w + xb.w;
+        if (EPT) {
+          h[ob][0] = rr.x; h[ob][1] = rr.y; h[ob][2] = rr.z; h[ob][3] = rr.w;
+          ab[ob][0] = xa.x + xb.x; ab[ob][1] = xa.y + xb.y; ab[ob][2] = xa.z + xb.z; ab[ob][3] = xa.w + xb.w;
+        } else {
+          h[ob][0] = rr.x + xa.x + xb.x; h[ob][1] = rr.y + xa.y + xb.y;
+          h[ob][2] = rr.z + xa.z + xb.z; h[ob][3] = rr.w + xa.w + xb.w;
+        }
         m[ob][0] = xp.x; m[ob][1] = xp.y; m[ob][2] = xp.z; m[ob][3] = xp.w;
       }
     }
@@ -1108,10 +1118,11 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
     for (int ob = 0; ob < 4; ++ob) {
       const float4 b2 = ld4(vec + 16 * ob + 4 * g);
       ep[ob][0] = b2.x; ep[ob][1] = b2.y; ep[ob][2] = b2.z; ep[ob][3] = b2.w;
+      if (EPT) { ep[ob][0] += ab[ob][0]; ep[ob][1] += ab[ob][1]; ep[ob][2] += ab[ob][2]; ep[ob][3] += ab[ob][3]; }
     }
     gemm_p<PREC, 4>(W2, h, ep);
     relu_frag<4>(ep);
-    if (STAGE != STAGE_LAST && a.write_next) {    // next pass's r = Q0 + W1_e_cur · e'
+    if ((STAGE & 3) != STAGE_LAST && a.write_next) {    // next pass's r = Q0 + W1_e_cur · e'
       gemm_p<PREC, 4>(W1, ep, q0r);
       if (valid) {
 #pragma unroll
@@ -1317,6 +1328,89 @@ __global__ __launch_bounds__(256) void node_mlp_kernel(NodeMlpArgs a) {
       if (!last) *reinterpret_cast<float4*>(&out[c * so + 16 * jb + 4 * g]) = o;
       else if (n0 + c < N) *reinterpret_cast<float4*>(&a.X[(n0 + c) * 128 + 64 + 16 * jb + 4 * g]) = o;
     }
+    __syncthreads();
+  }
+}
+
+// ---- EDGE_MLP per_type node terms (TypeAwareEdgeUpdate, layers.py:288-303) -------------------
+// NT[n][0:64]   = O1 · ReLU(L1[type n] · x_n + c1[type n])   (the x_i = target block)
+// NT[n][64:128] = O2 · ReLU(L2[type n] · x_n + c2[type n])   (the x_j = source block)
+// Nodes of a type >= T keep zero (the reference leaves their rows of tmp_1 / tmp_2 at 0). One block
+// per 16 nodes: for every type present in the tile the 16 rows run through that type's weights on
+// fp32 MFMA and only the rows of that type are kept; then the shared out-block GEMM.
+struct NodeEptArgs {
+  const float* X;             // [N][128] = [x_init | x_cur]
+  const int64_t* types;
+  int64_t ts;                 // node_types stride
+  int T;
+  int64_t N;
+  const float *l1_w, *l1_b, *l2_w, *l2_b, *o1_w, *o2_w;
+  float* NT;
+  int ldnt;
+};
+
+__global__ __launch_bounds__(256) void node_ept_kernel(NodeEptArgs a) {
+  __shared__ __attribute__((aligned(16))) float xs[16 * 136];   // strides 136, 72: 8 * odd mod 64 dwords
+  __shared__ __attribute__((aligned(16))) float us[16 * 72];
+  __shared__ int tys[16];
+  __shared__ unsigned tmask;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
+  const int64_t n0 = (int64_t)blockIdx.x * 16, N = a.N;
+  for (int idx = threadIdx.x; idx < 16 * 32; idx += 256) {
+    const int r = idx >> 5, c4 = (idx & 31) * 4;
+    const int64_t n = n0 + r;
+    *reinterpret_cast<float4*>(&xs[r * 136 + c4]) = n < N ? ld4(a.X + n * 128 + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (threadIdx.x < 16) {
+    const int64_t n = n0 + threadIdx.x;
+    const int64_t t = n < N ? a.types[n * a.ts] : -1;
+    tys[threadIdx.x] = (t >= 0 && t < a.T) ? (int)t : -1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned m = 0;
+    for (int i = 0; i < 16; ++i) m |= tys[i] >= 0 ? 1u << tys[i] : 0u;
+    tmask = m;
+  }
+  const int jb = wave;                              // 4 waves x 16 outputs = 64
+  for (int part = 0; part < 2; ++part) {
+    for (int idx = threadIdx.x; idx < 16 * 72; idx += 256) us[idx] = 0.f;
+    __syncthreads();
+    const float* Lw = part ? a.l2_w : a.l1_w;
+    const float* Lb = part ? a.l2_b : a.l1_b;
+    for (unsigned m = tmask; m; m &= m - 1) {
+      const int t = __ffs(m) - 1;
+      const float* wrow = Lw + ((int64_t)t * 64 + 16 * jb + c) * 128 + 4 * g;
+      const float* xrow = xs + c * 136 + 4 * g;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k0 = 0; k0 < 128; k0 += 16) {
+        const float4 w4 = ld4(wrow + k0);
+        const float4 x4 = *reinterpret_cast<const float4*>(xrow + k0);
+        acc = mfma4(w4.x, x4.x, acc); acc = mfma4(w4.y, x4.y, acc);
+        acc = mfma4(w4.z, x4.z, acc); acc = mfma4(w4.w, x4.w, acc);
+      }
+      if (tys[c] == t) {   // lane (c, g): outputs 16 jb + 4 g + r of node c
+        const float4 b4 = ld4(Lb + t * 64 + 16 * jb + 4 * g);
+        *reinterpret_cast<float4*>(&us[c * 72 + 16 * jb + 4 * g]) =
+            make_float4(fmaxf(acc[0] + b4.x, 0.f), fmaxf(acc[1] + b4.y, 0.f), fmaxf(acc[2] + b4.z, 0.f),
+                        fmaxf(acc[3] + b4.w, 0.f));
+      }
+    }
+    __syncthreads();
+    const float* orow = (part ? a.o2_w : a.o1_w) + (16 * jb + c) * 64 + 4 * g;
+    const float* urow = us + c * 72 + 4 * g;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k0 = 0; k0 < 64; k0 += 16) {
+      const float4 w4 = ld4(orow + k0);
+      const float4 u4 = *reinterpret_cast<const float4*>(urow + k0);
+      acc = mfma4(w4.x, u4.x, acc); acc = mfma4(w4.y, u4.y, acc);
+      acc = mfma4(w4.z, u4.z, acc); acc = mfma4(w4.w, u4.w, acc);
+    }
+    if (n0 + c < N)
+      *reinterpret_cast<float4*>(&a.NT[(n0 + c) * a.ldnt + 64 * part + 16 * jb + 4 * g]) =
+          make_float4(acc[0], acc[1], acc[2], acc[3]);
     __syncthreads();
   }
 }
@@ -1829,6 +1923,10 @@ static void launch_edge_step_p(const EdgeStepArgs& a, bool head, int grid, int s
   if (stage == STAGE_FIRST) launch_edge_step_s<AGG, PREC, UPD, STAGE_FIRST>(a, head, grid, st);
   else
 #endif
+  if constexpr (AGG == PEMP_AGGR_ATTN) {          // EDGE_MLP per_type: the published configs use attention
+    if (stage == (STAGE_MID | STAGE_EPT)) { launch_edge_step_s<AGG, PREC, UPD, STAGE_MID | STAGE_EPT>(a, head, grid, st); return; }
+    if (stage == (STAGE_LAST | STAGE_EPT)) { launch_edge_step_s<AGG, PREC, UPD, STAGE_LAST | STAGE_EPT>(a, head, grid, st); return; }
+  }
   if (stage == STAGE_MID) launch_edge_step_s<AGG, PREC, UPD, STAGE_MID>(a, head, grid, st);
   else launch_edge_step_s<AGG, PREC, UPD, STAGE_LAST>(a, head, grid, st);
 }
@@ -1940,6 +2038,14 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
   PEMP_CHECK_ARG(desc->steps >= 0 && desc->aux_loss_steps >= 0, "pemp_mpn_forward: bad steps");
   PEMP_CHECK_ARG(desc->aggr >= PEMP_AGGR_ATTN && desc->aggr <= PEMP_AGGR_MAX, "pemp_mpn_forward: bad aggr");
   PEMP_CHECK_ARG(desc->aggr != PEMP_AGGR_ATTN || w->attn_w, "pemp_mpn_forward: attention needs attn_w");
+  if (w->ept_l1_w) {   // EDGE_MLP per_type
+    PEMP_CHECK_ARG(w->ept_l1_b && w->ept_l2_w && w->ept_l2_b && w->ept_o1_w && w->ept_o2_w,
+                   "pemp_mpn_forward: EDGE_MLP per_type needs every ept_* array");
+    if (desc->aggr != PEMP_AGGR_ATTN) {
+      set_error("pemp_mpn_forward: EDGE_MLP per_type is built for the attention aggregation");
+      return PEMP_ERR_UNSUPPORTED;
+    }
+  }
   if (w->upd_mlp.n_layers > 0) {   // hierarchical update (dense-folded): T*64 -> ... -> 64, widths % 16
     const pemp_mlp& m = w->upd_mlp;
     PEMP_CHECK_ARG(!w->upd_w && m.n_layers <= 4, "pemp_mpn_forward: upd_mlp excludes upd_w (<= 4 layers)");
@@ -2012,7 +2118,8 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
   const EmbedLayout emb_lo = embed_layout(w->edge_emb, emb_prec);
   // PEMP_FUSED_FIRST (build flag, default off): the fused first pass runs 8 waves per CU (register
   // budget of the embedding) and measured slower than embedding + a 16-wave pass (95 vs ~82 us at C3)
-  const bool first_fused = PEMP_FUSED_FIRST && E > 0 && steps >= 1 && steps > aux + 1 && emb_lds &&
+  const bool ept = w->ept_l1_w != nullptr;
+  const bool first_fused = PEMP_FUSED_FIRST && !ept && E > 0 && steps >= 1 && steps > aux + 1 && emb_lds &&
                            emb_prec == desc->precision &&
                            (size_t)(edge_lds_base(false, upd_fused) + emb_lo.total) * sizeof(float) <= 160 * 1024;
   // launched after the node embedding + first node table (which need no edge order), so that the
@@ -2105,6 +2212,12 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
       else
         hipLaunchKernelGGL(node_table_kernel<0>, dim3(table_grid), dim3(256), 0, st, ta);
       PEMP_LAUNCH_CHECK();
+      if (ept) {   // columns 0..127 of the table: the per-type node terms (zero rows in pre_w)
+        NodeEptArgs xa{ws.X, node_types, tstride, T, N, w->ept_l1_w, w->ept_l1_b, w->ept_l2_w, w->ept_l2_b,
+                       w->ept_o1_w, w->ept_o2_w, ws.NT, NO};
+        hipLaunchKernelGGL(node_ept_kernel, dim3(node_grid), dim3(256), 0, st, xa);
+        PEMP_LAUNCH_CHECK();
+      }
     }
     return PEMP_OK;
   };
@@ -2126,7 +2239,7 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
       EdgeStepArgs ea{};
       ea.N = N; ea.E = E; ea.T = T; ea.t_nt_ld = NO;
       ea.seg = ws.seg; ea.wg_start = ws.wg_start; ea.s_src = ws.s_src; ea.s_dst = ws.s_dst; ea.s_orig = ws.s_orig;
-      const int stage = it == 0 && first_fused ? STAGE_FIRST : last ? STAGE_LAST : STAGE_MID;
+      const int stage = (it == 0 && first_fused ? STAGE_FIRST : last ? STAGE_LAST : STAGE_MID) | (ept ? STAGE_EPT : 0);
       ea.NT = ws.NT; ea.Q0 = ws.Q0; ea.r_cur = e_cur; ea.r_next = e_nxt;
       if (stage == STAGE_FIRST) {
         ea.q0_out = steps > 1 ? ws.Q0 : nullptr;

@@ -21,6 +21,7 @@ import torch
 import torch.nn as nn
 
 from .. import _lib
+from .edge_type import TypeAwareEdgeUpdate
 from .hierarch import (HIERARCH_CNN_ORDER_1, HIERARCH_CNN_ORDER_2, HIERARCH_ORDER_1, HIERARCH_ORDER_2,
                           HierarchUpdateCnn, HierarchUpdateMlp)
 
@@ -203,16 +204,35 @@ def fold_weights(model, device) -> Folded:
         out[:, 64:] = Wx
         return out
 
-    W1 = layer.mlp_edge[0].weight.detach().double().cpu()
-    b1 = layer.mlp_edge[0].bias.detach().double().cpu()
-    A = to_xtable(W1[:, :nx])
-    Bm = to_xtable(W1[:, nx:2 * nx])
+    g = lambda p: p.detach().double().cpu()
+    ept = isinstance(layer.mlp_edge, TypeAwareEdgeUpdate)
+    if ept:
+        # EDGE_MLP per_type (layers.py:288-303): the edge Linear takes the place of W1's e-columns, the
+        # e-block of out.1 that of mlp_edge.2; the node blocks go to node_ept_kernel (A, B rows zero)
+        W1, b1 = g(layer.mlp_edge.edge_layer.weight), g(layer.mlp_edge.edge_layer.bias)
+        Wo, bo = g(layer.mlp_edge.out[1].weight), g(layer.mlp_edge.out[1].bias)
+        A = Bm = torch.zeros(64, 128, dtype=torch.float64)
+        e_cols = 0
+        e2_full, e2_bias = Wo[:, 128:192], bo
+        s.ept_l1_w = f.dev(torch.stack([to_xtable(g(m.weight)) for m in layer.mlp_edge.layer_1]), device).data_ptr()
+        s.ept_l1_b = f.dev(torch.stack([g(m.bias) for m in layer.mlp_edge.layer_1]), device).data_ptr()
+        s.ept_l2_w = f.dev(torch.stack([to_xtable(g(m.weight)) for m in layer.mlp_edge.layer_2]), device).data_ptr()
+        s.ept_l2_b = f.dev(torch.stack([g(m.bias) for m in layer.mlp_edge.layer_2]), device).data_ptr()
+        s.ept_o1_w = f.dev(Wo[:, 0:64], device).data_ptr()
+        s.ept_o2_w = f.dev(Wo[:, 64:128], device).data_ptr()
+    else:
+        W1 = g(layer.mlp_edge[0].weight)
+        b1 = g(layer.mlp_edge[0].bias)
+        A = to_xtable(W1[:, :nx])
+        Bm = to_xtable(W1[:, nx:2 * nx])
+        e_cols = 2 * nx
+        e2_full, e2_bias = g(layer.mlp_edge[2].weight), g(layer.mlp_edge[2].bias)
     if skip:
-        q0 = W1[:, 2 * nx:2 * nx + 64]
-        e1 = W1[:, 2 * nx + 64:2 * nx + 128]
+        q0 = W1[:, e_cols:e_cols + 64]
+        e1 = W1[:, e_cols + 64:e_cols + 128]
     else:
         q0 = torch.zeros(64, 64, dtype=torch.float64)
-        e1 = W1[:, 2 * nx:2 * nx + 64]
+        e1 = W1[:, e_cols:e_cols + 64]
     if T == 1 and not hasattr(layer.mlp_node, "mlp"):
         msg_mods = [layer.mlp_node[0]]
     else:
@@ -227,11 +247,11 @@ def fold_weights(model, device) -> Folded:
     s.q0_w = f.dev(q0, device).data_ptr()
     s.q0_b = f.dev(b1, device).data_ptr()
     s.e1_w = f.dev(e1, device).data_ptr()
-    s.e2_w = f.dev(layer.mlp_edge[2].weight.detach().double().cpu(), device).data_ptr()
-    s.e2_b = f.dev(layer.mlp_edge[2].bias.detach().double().cpu(), device).data_ptr()
+    s.e2_w = f.dev(e2_full, device).data_ptr()
+    s.e2_b = f.dev(e2_bias, device).data_ptr()
     s.msg_w = f.dev(torch.stack(msg_w, 0), device).data_ptr()
     # bf16x3 packs of the per-edge GEMMs (PEMP_PREC_BF16X3)
-    e2 = layer.mlp_edge[2].weight.detach().double().cpu()
+    e2 = e2_full
     s.e1_bf = f.dev_raw(bf16_pack(e1), device).data_ptr()
     s.e2_bf = f.dev_raw(bf16_pack(e2), device).data_ptr()
     s.msg_bf = f.dev_raw(torch.stack([bf16_pack(w) for w in msg_w], 0), device).data_ptr()

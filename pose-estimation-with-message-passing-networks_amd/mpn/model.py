@@ -15,6 +15,7 @@ import torch.nn as nn
 
 from .. import _lib
 from .fold import fold_weights
+from .edge_type import TypeAwareEdgeUpdate
 from .hierarch import HierarchUpdateCnn, HierarchUpdateMlp
 
 _VALIDATE = os.environ.get("PEMP_VALIDATE", "0") not in ("", "0")   # read once at import
@@ -74,7 +75,7 @@ class TypeAwareMPNLayer(nn.Module):
     def __init__(self, node_dim, edge_dim, edge_hidden, aggr, skip=False, edge_mlp="agnostic", num_types=17,
                  aggr_sub=None, update_type="mlp"):
         super().__init__()
-        if edge_mlp != "agnostic":
+        if edge_mlp not in ("agnostic", "per_type"):
             raise NotImplementedError(f"EDGE_MLP={edge_mlp}")
         if update_type not in ("mlp", "hierarch_mlp", "hierarch_cnn"):
             raise NotImplementedError(f"UPDATE_TYPE={update_type}")
@@ -82,8 +83,12 @@ class TypeAwareMPNLayer(nn.Module):
             raise NotImplementedError("UPDATE_TYPE=hierarch_cnn indexes types up to 16 (layers.py:148)")
         nf = 2 if skip else 1
         self.aggr, self.aggr_sub, self.num_types, self.skip = aggr, aggr_sub, num_types, skip
-        self.mlp_edge = nn.Sequential(nn.Linear(node_dim * 2 * nf + edge_dim * nf, edge_hidden), nn.ReLU(inplace=True),
-                                      nn.Linear(edge_hidden, edge_dim), nn.ReLU(inplace=True))
+        self.edge_mlp = edge_mlp
+        if edge_mlp == "agnostic":
+            self.mlp_edge = nn.Sequential(nn.Linear(node_dim * 2 * nf + edge_dim * nf, edge_hidden),
+                                          nn.ReLU(inplace=True), nn.Linear(edge_hidden, edge_dim), nn.ReLU(inplace=True))
+        else:   # layers.py:177-179 (edge_dim * node_factor, as the reference writes it)
+            self.mlp_edge = TypeAwareEdgeUpdate(node_dim * nf, edge_dim * nf, edge_hidden, num_types)
         self.mlp_node = TypeAwareNodeUpdate(node_dim * nf + edge_dim, node_dim)
         self.update_type = update_type
         if update_type == "mlp":
@@ -106,6 +111,9 @@ class MPLayer(nn.Module):
 
     def __init__(self, node_dim, edge_dim, edge_hidden, aggr, use_node_update_mlp, skip=False, edge_mlp="agnostic"):
         super().__init__()
+        if edge_mlp == "per_type":   # the reference omits TypeAwareEdgeUpdate's num_joints here (layers.py:52-53)
+            raise NotImplementedError("EDGE_MLP=per_type with AGGR_TYPE agnostic: the reference's MPLayer "
+                                      "raises TypeError constructing it")
         if edge_mlp != "agnostic":
             raise NotImplementedError(f"EDGE_MLP={edge_mlp}")
         nf = 2 if skip else 1

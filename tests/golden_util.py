@@ -55,4 +55,6 @@ def mpn_config(meta):
         c.EDGE_INPUT_DIM = meta["edge_in"]
     if meta.get("update_type"):
         c.UPDATE_TYPE = meta["update_type"]
+    if meta.get("edge_mlp"):
+        c.EDGE_MLP = meta["edge_mlp"]
     return c

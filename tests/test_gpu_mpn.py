@@ -185,3 +185,18 @@ def test_hierarch_update_c3_shape(utype):
     for a, b in zip(pe + pn + pc, rpe + rpn + rpc):
         assert a.shape == b.shape
         assert max_err(a, b) < TOL
+
+
+@pytest.mark.parametrize("prec", PRECS)
+def test_edge_mlp_per_type_c3_shape(prec):
+    """EDGE_MLP per_type (TypeAwareEdgeUpdate: node_ept_kernel + the EPT edge pass), C3-shaped batch."""
+    g = graph(8, 17, 160, 160, 9, "fully")
+    cfg = pcfg.published_mpn_config(17, 3, "attn")
+    cfg.EDGE_MLP = "per_type"
+    model, sd = make_model(cfg, 6.5, prec)
+    x, ea, ei, types = g[0], g[1], g[2], g[7][:, 2]
+    pe, pn, pc, _ = run(model, x, ea, ei, types)
+    rpe, rpn, rpc, _ = restate.mpn_forward(sd, cfg, x, ea, ei, types)
+    for a, b in zip(pe + pn + pc, rpe + rpn + rpc):
+        assert a.shape == b.shape
+        assert max_err(a, b) < TOL
