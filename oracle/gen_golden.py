@@ -102,6 +102,9 @@ def mpn_cfg(meta):
         c.UPDATE_TYPE = meta["update_type"]
     if meta.get("edge_mlp"):
         c.EDGE_MLP = meta["edge_mlp"]
+    if meta.get("late_fusion"):
+        c.LATE_FUSION_POS = True
+        c.EDGE_EMB.BN = True
     return c
 
 
@@ -185,6 +188,8 @@ MPN_CASES = {
     "mpn_attn_ept_t2": (dict(J=17, steps=2, variant="attn", salt=15.5, edge_mlp="per_type"), "gc_realistic_knn"),
     "mpn_attn_ept_pt_t3": (dict(J=17, steps=3, variant="attn", salt=16.5, edge_mlp="per_type",
                                 aggr_sub="node_edge_attn_per_type", aggr="add", attn_gain=16.0), "gc_small_fully"),
+    "mpn_max_latefusion_t3": (dict(J=17, steps=3, variant="max", salt=17.5, late_fusion=True), "gc_realistic_knn"),
+    "mpn_attn_latefusion_t2": (dict(J=17, steps=2, variant="attn", salt=18.5, late_fusion=True), "gc_small_fully"),
     "mpn_attn_pertype_t2": (dict(J=17, steps=2, variant="attn", salt=10.5, aggr_sub="node_edge_attn_per_type",
                                  aggr="add", attn_gain=16.0), "gc_realistic_knn"),
 }

@@ -384,7 +384,13 @@ def mpn_forward(sd, cfg, x, edge_attr, edge_index, node_types):
     """NodeClassificationMPNSimple.forward (NodeClassificationMPNSimple.py:62-97)."""
     types = _type_map(cfg.NODE_TYPE_SUMMARY, node_types)
     nf = _mlp(sd, "node_embedding", x, cfg.NODE_EMB.OUTPUT_SIZES, cfg.NODE_EMB.BN, cfg.NODE_EMB.END_WITH_RELU)
-    ef = _mlp(sd, "edge_embedding", edge_attr, cfg.EDGE_EMB.OUTPUT_SIZES, cfg.EDGE_EMB.BN, cfg.EDGE_EMB.END_WITH_RELU)
+    if getattr(cfg, "LATE_FUSION_POS", False):   # LateFusionEdgeMLP.forward (NodeClassificationMPNSimple.py:18-21)
+        single = [size // 2 for size in cfg.EDGE_EMB.OUTPUT_SIZES[:-1]]
+        pos = _mlp(sd, "edge_embedding.pos_mlp", edge_attr[:, :2], single, cfg.EDGE_EMB.BN, cfg.EDGE_EMB.END_WITH_RELU)
+        edg = _mlp(sd, "edge_embedding.edge_mlp", edge_attr[:, 2:], single, cfg.EDGE_EMB.BN, cfg.EDGE_EMB.END_WITH_RELU)
+        ef = F.linear(F.relu(torch.cat([pos, edg], 1)), sd["edge_embedding.out.weight"], sd["edge_embedding.out.bias"])
+    else:
+        ef = _mlp(sd, "edge_embedding", edge_attr, cfg.EDGE_EMB.OUTPUT_SIZES, cfg.EDGE_EMB.BN, cfg.EDGE_EMB.END_WITH_RELU)
     nf0, ef0 = nf, ef
     pe, pn, pc = [], [], []
 

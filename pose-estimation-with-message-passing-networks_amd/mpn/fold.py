@@ -117,14 +117,38 @@ class Folded:
         return d
 
     def mlp(self, seq, device):
+        return self.mlp_from_layers(mlp_layers(seq), device)
+
+    def mlp_from_layers(self, layers, device):
         m = _lib.PempMlp()
-        layers = mlp_layers(seq)
+        if len(layers) > 4:
+            raise NotImplementedError("MLPs deeper than 4 Linear layers")
         m.n_layers = len(layers)
         for i, (W, b, relu) in enumerate(layers):
             Wp, bp = _padded(W, b)
             wd, bd = self.dev(Wp, device), self.dev(bp, device)
             m.layer[i] = _lib.PempLayer(wd.data_ptr(), bd.data_ptr(), W.shape[1], W.shape[0], int(relu), 0)
         return m
+
+
+def edge_embedding_layers(emb):
+    """Folded layers of the edge embedding: the plain ``_make_mlp`` Sequential, or LATE_FUSION_POS's
+    two branch MLPs (NodeClassificationMPNSimple.py:7-21) as block-diagonal layers over
+    [dx, dy | 17 one-hot columns] followed by out(ReLU(cat)) -- exact, the off-diagonal blocks are 0."""
+    if isinstance(emb, nn.Sequential):
+        return mlp_layers(emb)
+    pos, edg = mlp_layers(emb.pos_mlp), mlp_layers(emb.edge_mlp)
+    if len(pos) != len(edg) or [r for _, _, r in pos] != [r for _, _, r in edg]:
+        raise NotImplementedError("LATE_FUSION_POS branches of different structure")
+    layers = []
+    for (Wp, bp, relu), (We, be, _) in zip(pos, edg):
+        W = torch.zeros(Wp.shape[0] + We.shape[0], Wp.shape[1] + We.shape[1], dtype=torch.float64)
+        W[:Wp.shape[0], :Wp.shape[1]] = Wp
+        W[Wp.shape[0]:, Wp.shape[1]:] = We
+        layers.append([W, torch.cat([bp, be]), relu])
+    layers[-1][2] = True                                  # ReLU(cat([pos, edge]))
+    layers.append([emb.out.weight.detach().double().cpu(), emb.out.bias.detach().double().cpu(), False])
+    return layers
 
 
 def hierarch_dense_layers(upd, T):
@@ -190,7 +214,8 @@ def fold_weights(model, device) -> Folded:
     skip = layer.skip
     T = model.num_types
     s.node_emb = f.mlp(model.node_embedding, device)
-    s.edge_emb = f.mlp(model.edge_embedding, device)
+    emb = edge_embedding_layers(model.edge_embedding)
+    s.edge_emb = f.mlp_from_layers(emb, device)
     s.edge_head = f.mlp(model.edge_classification, device)
     s.node_head = f.mlp(model.node_classification, device)
     s.class_head = f.mlp(model.classification, device)
@@ -260,7 +285,6 @@ def fold_weights(model, device) -> Folded:
             and head[0][2] and head[1][2] and not head[2][2] and head[2][0].shape[0] == 1):
         s.head_bf = f.dev_raw(torch.cat([bf16_pack(head[0][0]).reshape(-1), bf16_pack(head[1][0]).reshape(-1)]),
                               device).data_ptr()
-    emb = mlp_layers(model.edge_embedding)
     if all(W.shape[0] <= 64 and W.shape[1] <= 64 for W, _, _ in emb):
         packs = [bf16_pack(W).reshape(-1) for W, _, _ in emb] + [bf16_pack(q0).reshape(-1)]
         s.emb_bf = f.dev_raw(torch.cat(packs), device).data_ptr()

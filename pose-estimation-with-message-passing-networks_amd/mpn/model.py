@@ -59,6 +59,18 @@ def _make_mlp(input_dim, hidden_dims, bn=False, end_with_relu=False):
     return nn.Sequential(*mods)
 
 
+class LateFusionEdgeMLP(nn.Module):
+    """``NodeClassificationMPNSimple.py:7-21`` (LATE_FUSION_POS): separate MLPs on [dx, dy] and on the
+    17 connection columns, then out(ReLU(cat)). Parameters only; folded block-diagonally by fold.py."""
+
+    def __init__(self, config):
+        super().__init__()
+        single = [size // 2 for size in config.EDGE_EMB.OUTPUT_SIZES[:-1]]
+        self.pos_mlp = _make_mlp(2, single, bn=config.EDGE_EMB.BN, end_with_relu=config.EDGE_EMB.END_WITH_RELU)
+        self.edge_mlp = _make_mlp(17, single, bn=config.EDGE_EMB.BN, end_with_relu=config.EDGE_EMB.END_WITH_RELU)
+        self.out = nn.Linear(single[-1] * 2, config.EDGE_EMB.OUTPUT_SIZES[-1])
+
+
 class TypeAwareNodeUpdate(nn.Module):
     """``layers.py:260-274``: 17 Linear+ReLU message MLPs selected by the source node type."""
 
@@ -134,8 +146,6 @@ class NodeClassificationMPNSimple(nn.Module):
         for k, v in (("NODE_FEATURE_DIM", 64), ("EDGE_FEATURE_DIM", 64), ("EDGE_FEATURE_HIDDEN", 64)):
             if config[k] != v:
                 raise NotImplementedError(f"{k}={config[k]}: the HIP kernels are built for width 64")
-        if config.get("LATE_FUSION_POS", False):
-            raise NotImplementedError("LATE_FUSION_POS")
         if config.AGGR_TYPE == "agnostic":
             self.mpn_node_cls = MPLayer(64, 64, 64, aggr=config.AGGR, skip=config.SKIP,
                                         use_node_update_mlp=config.USE_NODE_UPDATE_MLP, edge_mlp=config.EDGE_MLP)
@@ -147,8 +157,13 @@ class NodeClassificationMPNSimple(nn.Module):
                                                   aggr_sub=config.AGGR_SUB, update_type=config.UPDATE_TYPE)
         else:
             raise NotImplementedError(f"AGGR_TYPE={config.AGGR_TYPE}")
-        self.edge_embedding = _make_mlp(config.EDGE_INPUT_DIM, config.EDGE_EMB.OUTPUT_SIZES, bn=config.EDGE_EMB.BN,
-                                        end_with_relu=config.EDGE_EMB.END_WITH_RELU)
+        if config.get("LATE_FUSION_POS", False):
+            if config.EDGE_INPUT_DIM != 19:   # LateFusionEdgeMLP slices [dx, dy | 17 one-hot columns]
+                raise NotImplementedError(f"LATE_FUSION_POS needs EDGE_INPUT_DIM 19 (got {config.EDGE_INPUT_DIM})")
+            self.edge_embedding = LateFusionEdgeMLP(config)
+        else:
+            self.edge_embedding = _make_mlp(config.EDGE_INPUT_DIM, config.EDGE_EMB.OUTPUT_SIZES, bn=config.EDGE_EMB.BN,
+                                            end_with_relu=config.EDGE_EMB.END_WITH_RELU)
         self.node_embedding = _make_mlp(config.NODE_INPUT_DIM, config.NODE_EMB.OUTPUT_SIZES, bn=config.NODE_EMB.BN,
                                         end_with_relu=config.NODE_EMB.END_WITH_RELU)
         self.edge_classification = _make_mlp(64, config.EDGE_CLASS.OUTPUT_SIZES, bn=config.BN)

@@ -57,4 +57,7 @@ def mpn_config(meta):
         c.UPDATE_TYPE = meta["update_type"]
     if meta.get("edge_mlp"):
         c.EDGE_MLP = meta["edge_mlp"]
+    if meta.get("late_fusion"):
+        c.LATE_FUSION_POS = True
+        c.EDGE_EMB.BN = True
     return c
