@@ -947,8 +947,19 @@ enum { STAGE_FIRST = 0, STAGE_MID = 1, STAGE_LAST = 2, STAGE_EPT = 4 };
 // STAGE_FIRST: the first pass with the edge embedding fused (reads edge_attr, writes Q0 and r_next);
 // STAGE_MID reads r_cur and Q0 and writes r_next; STAGE_LAST reads r_cur only.
 // waves per workgroup: 16 (<= 128 VGPRs); the embedding-fused first pass needs more registers: 8
+// PEMP_EDGE_PIPE (build flag, default off): the middle / last passes prefetch the next tile's rows
+// while the current tile computes. 1: r, Q0 and the three node-table gathers (80 VGPRs, 8 waves per
+// CU): 47.3 us vs 41.8 us per C3 pass; 2: r and Q0 only (12 waves): 43.4 us. Occupancy (16 waves)
+// hides more latency than the prefetch does, so both stay off.
+#ifndef PEMP_EDGE_PIPE
+#define PEMP_EDGE_PIPE 0
+#endif
 template <int STAGE>
-constexpr int edge_waves() { return STAGE == STAGE_FIRST ? 8 : EDGE_WAVES; }
+constexpr bool edge_pipe() { return PEMP_EDGE_PIPE && (STAGE & 3) != STAGE_FIRST; }
+template <int STAGE>
+constexpr int edge_waves() {
+  return (STAGE & 3) == STAGE_FIRST ? 8 : edge_pipe<STAGE>() ? (PEMP_EDGE_PIPE == 2 ? 12 : 8) : EDGE_WAVES;
+}
 
 template <int AGG, int HEAD, int PREC, int UPD, int STAGE>
 __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(EdgeStepArgs a) {
@@ -1042,6 +1053,31 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
 
   int dst_n = a.s_dst[min(first + c, end - 1)];
   int src_n = a.s_src[min(first + c, end - 1)];
+  constexpr bool PIPE = edge_pipe<STAGE>();
+  // PIPE: rows of the next tile in flight during the current tile's compute; indices two tiles ahead
+  float4 nr[4], na[4], nb[4], np4[4], nq[4];
+  int dst_nn = dst_n, src_nn = src_n;
+  auto load_rows = [&](int b0, int d, int s_) {
+    const int qq = min(b0 + c, end - 1);
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob) {
+      const int f = 16 * ob + 4 * g;
+      nr[ob] = ld4(a.r_cur + (int64_t)qq * D + f);
+      if (PEMP_EDGE_PIPE != 2) {
+        na[ob] = ld4(a.NT + (int64_t)d * a.t_nt_ld + f);
+        nb[ob] = ld4(a.NT + (int64_t)s_ * a.t_nt_ld + 64 + f);
+        np4[ob] = ld4(ntP + (int64_t)d * a.t_nt_ld + f);
+      }
+      if ((STAGE & 3) == STAGE_MID) nq[ob] = ld4(a.Q0 + (int64_t)qq * D + f);
+    }
+  };
+  if (PIPE) {
+    load_rows(first, dst_n, src_n);
+    if (first + 16 < end) {
+      dst_nn = a.s_dst[min(first + 16 + c, end - 1)];
+      src_nn = a.s_src[min(first + 16 + c, end - 1)];
+    }
+  }
   for (int base = first; base < end; base += 16) {
     // opaque zero: keeps the compiler from hoisting the LDS weight fragments out of the loop
     // (192+ VGPRs of loop-invariant loads would spill)
@@ -1056,7 +1092,21 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
     const int q = min(p, end - 1);
     const int dst = dst_n, src = src_n;
     const bool more = base + 16 < end;
-    if (more) {                                   // next tile's indices
+    float4 cr[4], ca[4], cb[4], cp[4], cq[4];     // PIPE: this tile's rows (loaded one tile ago)
+    if (PIPE) {
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob) { cr[ob] = nr[ob]; ca[ob] = na[ob]; cb[ob] = nb[ob]; cp[ob] = np4[ob]; cq[ob] = nq[ob]; }
+      dst_n = dst_nn;
+      src_n = src_nn;
+      if (more) {
+        load_rows(base + 16, dst_n, src_n);
+        if (base + 32 < end) {
+          const int qn = min(base + 32 + c, end - 1);
+          dst_nn = a.s_dst[qn];
+          src_nn = a.s_src[qn];
+        }
+      }
+    } else if (more) {                            // next tile's indices
       const int qn = min(base + 16 + c, end - 1);
       dst_n = a.s_dst[qn];
       src_n = a.s_src[qn];
@@ -1092,12 +1142,13 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob) {
         const int f = 16 * ob + 4 * g;
-        const float4 rr = ld4(a.r_cur + (int64_t)q * D + f);
-        const float4 xa = ld4(a.NT + (int64_t)dst * a.t_nt_ld + f);
-        const float4 xb = ld4(a.NT + (int64_t)src * a.t_nt_ld + 64 + f);
-        const float4 xp = ld4(ntP + (int64_t)dst * a.t_nt_ld + f);
+        const float4 rr = PIPE ? cr[ob] : ld4(a.r_cur + (int64_t)q * D + f);
+        constexpr bool PG = PIPE && PEMP_EDGE_PIPE != 2;   // node-table rows prefetched too
+        const float4 xa = PG ? ca[ob] : ld4(a.NT + (int64_t)dst * a.t_nt_ld + f);
+        const float4 xb = PG ? cb[ob] : ld4(a.NT + (int64_t)src * a.t_nt_ld + 64 + f);
+        const float4 xp = PG ? cp[ob] : ld4(ntP + (int64_t)dst * a.t_nt_ld + f);
         if ((STAGE & 3) == STAGE_MID) {
-          const float4 qq = ld4(a.Q0 + (int64_t)q * D + f);
+          const float4 qq = PIPE ? cq[ob] : ld4(a.Q0 + (int64_t)q * D + f);
           q0r[ob][0] = qq.x; q0r[ob][1] = qq.y; q0r[ob][2] = qq.z; q0r[ob][3] = qq.w;
         }
         if (EPT) {
