@@ -276,7 +276,9 @@ int pemp_mpn_status(const pemp_mpn_desc* desc, int64_t N, int64_t E, const void*
  * whose label contains `filter` ("*" = all, NULL or "" = off). pemp_prof_report synchronises those
  * events and writes "label count total_ms" lines into buf (returns the full length), then resets.
  * Labels: detect_nms, detect_top, detect_emit, pack_nodes, fully_graph, edge_features, knn_adj, knn_emit, score_graph,
- * mpn_prepare, node_embed, edge_embed, node_table, edge_step, edge_step_head, node_update, heads. */
+ * mpn_prepare, node_embed, edge_embed, node_table, edge_step, edge_step_head, node_update, heads.
+ * "label@R": launch sites that are idempotent (the edge passes) issue their launch R times between
+ * one event pair, so the per-launch average excludes the event-record overhead (count += R). */
 int pemp_prof_enable(const char* filter);
 int pemp_prof_report(char* buf, size_t len);
 

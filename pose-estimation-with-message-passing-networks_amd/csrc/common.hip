@@ -33,9 +33,11 @@ namespace {
 struct Pending {
   std::string label;
   hipEvent_t a, b;
+  int reps;
 };
 std::mutex g_prof_mu;
 std::string g_prof_filter;
+int g_prof_repeat = 1;     // "label@R": matching launch sites issue their launch R times per event pair
 std::vector<Pending> g_pending;
 std::vector<hipEvent_t> g_pool;
 struct Agg {
@@ -60,7 +62,7 @@ ProfScope::ProfScope(const char* label, hipStream_t st) : st_(st), slot_(-1) {
   std::lock_guard<std::mutex> lk(g_prof_mu);
   if (g_prof_filter.empty()) return;
   if (g_prof_filter != "*" && std::string(label).find(g_prof_filter) == std::string::npos) return;
-  Pending p{label, take_event(), take_event()};
+  Pending p{label, take_event(), take_event(), g_prof_repeat};
   if (!p.a || !p.b) return;
   (void)hipEventRecord(p.a, st);
   g_pending.push_back(p);
@@ -73,6 +75,13 @@ ProfScope::~ProfScope() {
   (void)hipEventRecord(g_pending[slot_].b, st_);
 }
 
+int prof_repeat(const char* label) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  if (g_prof_filter.empty() || g_prof_repeat <= 1) return 1;
+  if (g_prof_filter != "*" && std::string(label).find(g_prof_filter) == std::string::npos) return 1;
+  return g_prof_repeat;
+}
+
 bool prof_active() {
   std::lock_guard<std::mutex> lk(g_prof_mu);
   return !g_prof_filter.empty();
@@ -82,7 +91,15 @@ bool prof_active() {
 
 extern "C" int pemp_prof_enable(const char* filter) {
   std::lock_guard<std::mutex> lk(pemp::g_prof_mu);
-  pemp::g_prof_filter = filter ? filter : "";
+  std::string f = filter ? filter : "";
+  int reps = 1;
+  const size_t at = f.find('@');
+  if (at != std::string::npos) {
+    reps = atoi(f.c_str() + at + 1);
+    f = f.substr(0, at);
+  }
+  pemp::g_prof_filter = f;
+  pemp::g_prof_repeat = reps > 1 ? reps : 1;
   return PEMP_OK;
 }
 
@@ -93,7 +110,7 @@ extern "C" int pemp_prof_report(char* buf, size_t len) {
     PEMP_HIP(hipEventSynchronize(p.b));
     PEMP_HIP(hipEventElapsedTime(&ms, p.a, p.b));
     auto& a = pemp::g_agg[p.label];
-    a.count += 1;
+    a.count += p.reps;
     a.ms += ms;
     pemp::g_pool.push_back(p.a);
     pemp::g_pool.push_back(p.b);

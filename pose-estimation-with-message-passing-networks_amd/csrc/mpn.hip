@@ -2304,14 +2304,19 @@ extern "C" int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weight
       ea.upd_w = w->upd_w; ea.upd_bf = w->upd_bf;
       ea.edge_logits = record ? edge_logits + (int64_t)rec * E : nullptr;
       ea.write_next = !last;
-      ProfScope prof(record ? "edge_step_head" : "edge_step", st);
-      switch (desc->aggr) {
-        case PEMP_AGGR_ATTN: launch_edge_step<PEMP_AGGR_ATTN>(ea, record, edge_grid, desc->precision, upd_fused, stage, st); break;
-        case PEMP_AGGR_SUM: launch_edge_step<PEMP_AGGR_SUM>(ea, record, edge_grid, desc->precision, upd_fused, stage, st); break;
-        case PEMP_AGGR_MEAN: launch_edge_step<PEMP_AGGR_MEAN>(ea, record, edge_grid, desc->precision, upd_fused, stage, st); break;
-        default: launch_edge_step<PEMP_AGGR_MAX>(ea, record, edge_grid, desc->precision, false, stage, st); break;
+      const char* label = record ? "edge_step_head" : "edge_step";
+      ProfScope prof(label, st);
+      // a pass is idempotent (reads r_cur / NT / Q0, rewrites r_next / agg / logits), so the profiler
+      // may repeat it between one event pair ("edge_step@R")
+      for (int rep = prof_repeat(label); rep > 0; --rep) {
+        switch (desc->aggr) {
+          case PEMP_AGGR_ATTN: launch_edge_step<PEMP_AGGR_ATTN>(ea, record, edge_grid, desc->precision, upd_fused, stage, st); break;
+          case PEMP_AGGR_SUM: launch_edge_step<PEMP_AGGR_SUM>(ea, record, edge_grid, desc->precision, upd_fused, stage, st); break;
+          case PEMP_AGGR_MEAN: launch_edge_step<PEMP_AGGR_MEAN>(ea, record, edge_grid, desc->precision, upd_fused, stage, st); break;
+          default: launch_edge_step<PEMP_AGGR_MAX>(ea, record, edge_grid, desc->precision, false, stage, st); break;
+        }
+        PEMP_LAUNCH_CHECK();
       }
-      PEMP_LAUNCH_CHECK();
     }
     // node update + next node table; heads when recorded (the last iteration's heads also fill
     // the post-loop slot: NODE_STEPS = 0 leaves x unchanged, NodeClassificationMPNSimple.py:93-94)

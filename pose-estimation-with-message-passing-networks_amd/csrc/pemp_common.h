@@ -35,6 +35,9 @@ bool debug_sync();
 
 // true while the opt-in event profiler records (its hipEvent calls must not be graph-captured)
 bool prof_active();
+// launches a site should issue per event pair: R for a "label@R" profiler filter matching `label`
+// (launch sites that are idempotent may repeat to amortise the event overhead), else 1
+int prof_repeat(const char* label);
 
 #define PEMP_LAUNCH_CHECK()                                                        \
   do {                                                                             \
