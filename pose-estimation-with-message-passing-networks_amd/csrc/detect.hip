@@ -17,6 +17,8 @@
 //   emits detections in the reference's order.
 #include <math.h>
 
+#include <type_traits>
+
 #include "pemp_common.h"
 
 namespace pemp {
@@ -29,7 +31,9 @@ namespace {
 #define NMS_PREFETCH 1
 #endif
 constexpr int SR = NMS_SR;  // rows per unit (= band height of the threshold bitmask)
-static_assert(SR <= 16, "column masks are 16-bit");
+static_assert(SR <= 32, "column masks are at most 32-bit");
+// a lane's threshold bits over the SR rows of its unit column
+using cmask_t = typename std::conditional<(SR > 16), uint32_t, uint16_t>::type;
 constexpr int MAXR = 4;   // max pool radius (POOL_KERNEL_SIZE <= 9)
 constexpr int MAXJ = 32;
 constexpr int MAXB = 256;   // max bands per plane (H <= 4096)
@@ -62,7 +66,7 @@ constexpr int KCAP = 32;   // max top-k (pemp_detect checks topk <= 32)
 
 struct DetectWs {
   float *cand_v, *neg_v; int *cand_i, *neg_i, *tile_count, *tile_nonneg;
-  uint16_t* cbits;   // threshold bits per (unit, lane): bit j <-> row y0 + j of the lane's column
+  cmask_t* cbits;    // threshold bits per (unit, lane): bit j <-> row y0 + j of the lane's column
   // per plane (image, type): sorted top-k list, threshold-set counts per band and in-plane offsets
   float* ptop_sc; int *ptop_i, *ptop_bit, *pn_top, *pn_thr, *pstrip, *pstrip_off;
 };
@@ -77,7 +81,7 @@ static DetectWs carve(void* base, const DetectGeom& g, size_t* bytes) {
   w.neg_i = c.take<int>(nu * g.K);
   w.tile_count = c.take<int>(nu);
   w.tile_nonneg = c.take<int>(nu);
-  w.cbits = c.take<uint16_t>(nu * 64);
+  w.cbits = c.take<cmask_t>(nu * 64);
   const size_t np = (size_t)g.B * g.J;
   w.ptop_sc = c.take<float>(np * KCAP);
   w.ptop_i = c.take<int>(np * KCAP);
@@ -210,7 +214,7 @@ template <int P, int MODE, bool MASKED>
 __global__ __launch_bounds__(NT1) void nms_strips_kernel(
     const float* __restrict__ s, const float* __restrict__ masks, DetectGeom g, float thr, int use_thr,
     float* __restrict__ cand_v, int* __restrict__ cand_i, float* __restrict__ neg_v, int* __restrict__ neg_i,
-    int* __restrict__ tile_count, int* __restrict__ tile_nonneg, uint16_t* __restrict__ cbits) {
+    int* __restrict__ tile_count, int* __restrict__ tile_nonneg, cmask_t* __restrict__ cbits) {
   const int lane = threadIdx.x & 63;
   const int total = g.B * g.J * g.units, stride_u = gridDim.x * (NT1 / 64);
   const int H = g.H, W = g.W, K = g.K;
@@ -262,7 +266,7 @@ __global__ __launch_bounds__(NT1) void nms_strips_kernel(
       vmax_l = fmaxf(vmax_l, v[j]);                     // NaN (invalid) is ignored by fmaxf
     }
     if (!use_thr) tbits = 0;
-    cbits[(size_t)u * 64 + lane] = (uint16_t)tbits;
+    cbits[(size_t)u * 64 + lane] = (cmask_t)tbits;
     int cnt = __popc(tbits), nonneg = __popc(nnbits);
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
@@ -476,7 +480,7 @@ __global__ __launch_bounds__(256) void plane_top_kernel(DetectGeom g, float thr,
 // Stage 2b: one workgroup per plane. The plane's output offsets follow from the per-plane counts
 // of its image: [top-k dets of types 0..J-1] ++ [threshold dets, type-major, strip order].
 __global__ __launch_bounds__(256) void emit_kernel(const float* __restrict__ s, const float* __restrict__ masks,
-                                                   DetectGeom g, const uint16_t* __restrict__ cbits,
+                                                   DetectGeom g, const cmask_t* __restrict__ cbits,
                                                    DetectWs w, int64_t* __restrict__ det,
                                                    float* __restrict__ scores, int* __restrict__ n_det, int cap,
                                                    int* __restrict__ n_host) {
@@ -555,7 +559,7 @@ __global__ __launch_bounds__(256) void emit_kernel(const float* __restrict__ s, 
   // found from their counts; their column masks go to LDS; row words are rebuilt with one ballot
   // per (row, non-empty strip), visited in (y, x) order; a lane's output slot is the running base
   // plus the set bits below it (mbcnt).
-  __shared__ uint16_t cm_sh[4][64][64];
+  __shared__ cmask_t cm_sh[4][64][64];
   __shared__ int nz_sh[4][64];
   // non-empty bands, round-robin over the waves (the wave's k-th band is the (4k + wave)-th one)
   int kb = 0;
@@ -582,7 +586,7 @@ __global__ __launch_bounds__(256) void emit_kernel(const float* __restrict__ s, 
     for (unsigned long long m = nzm; m; m &= m - 1) {
       const int sx = __builtin_ctzll(m);
       const unsigned cm = nnz < 4 ? cms[nnz & 3] : cbits[(u0 + sx) * 64 + lane];
-      cm_sh[wave][nnz][lane] = (uint16_t)cm;
+      cm_sh[wave][nnz][lane] = (cmask_t)cm;
       if (lane == 0) nz_sh[wave][nnz] = sx;
       unsigned ra = cm;
 #pragma unroll
@@ -593,7 +597,7 @@ __global__ __launch_bounds__(256) void emit_kernel(const float* __restrict__ s, 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (unsigned rm = rows_any & ((1u << rows) - 1u); rm; rm &= rm - 1) {
+    for (unsigned rm = rows_any & (rows >= 32 ? ~0u : (1u << rows) - 1u); rm; rm &= rm - 1) {
       const int j = __builtin_ctz(rm), yy = ry0 + j;
       for (int k = 0; k < nnz; ++k) {
         const int sx = nz_sh[wave][k];
@@ -632,7 +636,10 @@ static void launch_nms(const float* s, const float* masks, const DetectGeom& g, 
                        const DetectWs& w, hipStream_t st) {
   const int total = g.B * g.J * g.units;
   const int want = (total + NT1 / 64 - 1) / (NT1 / 64);
-  const int grid = want < 4 * num_cus() ? want : 4 * num_cus();   // 4 waves/SIMD resident (<= 128 VGPRs)
+  // resident workgroups per CU: 4 (one wave per SIMD each) while the kernel fits 128 VGPRs (SR 16);
+  // the 32-row units need ~190 VGPRs: 2
+  constexpr int per_cu = SR > 16 ? 2 : 4;
+  const int grid = want < per_cu * num_cus() ? want : per_cu * num_cus();
   if (masks)
     hipLaunchKernelGGL((nms_strips_kernel<P, MODE, true>), dim3(grid), dim3(NT1), 0, st, s, masks, g, thr, use_thr,
                        w.cand_v, w.cand_i, w.neg_v, w.neg_i, w.tile_count, w.tile_nonneg, w.cbits);
