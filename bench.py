@@ -194,6 +194,35 @@ def _cpu_model():
     return None
 
 
+def frontend_projection(wl, gc, model, hm, tags, dev, out):
+    """SURVEY 8f row 1, informational: the reference projects the gathered features of every image to
+    the image size (interpolate bilinear, PoseEstimation.py:426-452) before construct_graph reads N
+    rows of it. Times that dense projection (torch on the GPU, [B, 128, H/2, W/2] -> [B, 128, H, W])
+    against pemp_gather_projected sampling only the detections (features=ProjectedMaps)."""
+    B, H, W = wl["B"], wl["H"], wl["W"]
+    low = torch.randn(B, 128, H // 2, W // 2, device=dev)
+    reps = 5
+    torch.nn.functional.interpolate(low, size=(H, W), mode="bilinear", align_corners=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        torch.nn.functional.interpolate(low, size=(H, W), mode="bilinear", align_corners=False)
+    torch.cuda.synchronize()
+    dense_ms = (time.perf_counter() - t0) / reps * 1e3
+    pm = pemp_amd.ProjectedMaps([low], (H, W))
+    _lib.prof_enable("gather_projected")
+    for _ in range(reps):
+        pemp_amd.get_graph_constructor(gc, scoremaps=hm, features=pm, tagmaps=tags, joints_gt=None, factor_list=None,
+                                       masks=None, device=dev, testing=True, heatmaps=None,
+                                       num_joints=wl["J"]).construct_graph()
+    torch.cuda.synchronize()
+    st = _lib.prof_report()
+    _lib.prof_enable(None)
+    n, ms = st.get("gather_projected", (1, float("nan")))
+    return {"dense_interpolate_ms": round(dense_ms, 3), "on_demand_gather_us": round(ms / n * 1e3, 2),
+            "dense_bytes_written": B * 128 * H * W * 4, "nodes": int(out[0].shape[0])}
+
+
 def main():
     args = parse()
     rank, world, dev = setup_dist(args.gpus)
@@ -264,6 +293,8 @@ def main():
     dt_mpn = max_over_ranks(time.perf_counter() - t1, world, dev)
     mpn_eups = E_all * wl["steps"] * args.steps / dt_mpn
 
+    front = frontend_projection(wl, gc, model, hm, tags, dev, out) if not args.no_roofline else None
+
     upd = wl["variant"] in ("attn", "mean")      # update block pre-applied in the edge pass (mpn.hip UPD)
     roof = roofline_for(dominant, stats_timed, E, wl, model.precision, upd) if dominant else None
     cpu = None
@@ -290,6 +321,7 @@ def main():
             "roofline": roof,
             "kernel_avg_us": breakdown if not args.no_roofline else None,
             "cpu_baseline": cpu,
+            "frontend_projection": front,
         }
         if cpu:
             rec["speedup_vs_cpu"] = round(value / cpu["value"], 1)

@@ -20,6 +20,7 @@
  *                        PyG to_undirected, remove_self_loops)
  *   pemp_score_graph     ConstructGraph.py:405-422 score_based_graph (k = 75 roots)
  *   pemp_edge_features   ConstructGraph.py:289-359 (edge_attr)
+ *   pemp_gather_projected  PoseEstimation.py:426-452 feature projection, sampled at the detections only
  *   pemp_mpn_forward     Models/MessagePassingNetwork/NodeClassificationMPNSimple.py:62-97 with
  *                        layers.py:32-86 (MPLayer) / :157-274 (TypeAwareMPNLayer)
  */
@@ -129,6 +130,16 @@ int pemp_knn_graph_count(const int64_t* joint_det, const int64_t* node_off, cons
 int pemp_knn_graph_emit(const int64_t* node_off, const int64_t* node_off_host, int B,
                         const int64_t* edge_off, int64_t e_total, void* workspace,
                         size_t workspace_bytes, int64_t* edge_index, void* stream);
+
+/* Node features from maps projected to the image size on demand (the test front-end's bilinear
+ * projection, PoseEstimation.py:426-452, summed over scales and divided, multi_scales_testing.py:182-190
+ * / PoseEstimation.py:244): x[n][c] = sum_s bilinear(maps[s][b_n][c], (y_n, x_n); H x W) / divisor,
+ * align_corners = False, torch's source-index rule. maps: host array of S (<= 8) device pointers to
+ * [B][C][map_h[s]][map_w[s]] fp32. Pairs with pemp_fully_graph_build / pemp_pack_nodes called with
+ * features = NULL (they then leave x to this call). */
+int pemp_gather_projected(const float* const* maps, const int* map_h, const int* map_w, int S, int C, int H, int W,
+                          float divisor, const int64_t* joint_det, const int64_t* batch_index, int64_t N, float* x,
+                          void* stream);
 
 /* score_based graph per image (ConstructGraph.py:405-422 score_based_graph, k = 75 there): the k
  * highest-scoring nodes are roots (ties: lower node index; torch.topk leaves them unspecified);

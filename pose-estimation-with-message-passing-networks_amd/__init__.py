@@ -19,3 +19,9 @@ def get_graph_constructor(config, **kwargs):
 def get_mpn_model(config, **kwargs):
     from .mpn import get_mpn_model as _m
     return _m(config, **kwargs)
+
+
+def ProjectedMaps(maps, size, divisor=None):
+    """Lazy image-size projection of per-scale feature maps for ``features=`` (frontend.py)."""
+    from .frontend import ProjectedMaps as _p
+    return _p(maps, size, divisor)

@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256) void pack_nodes_kernel(
     const int64_t i = g - node_off[b];
     const int64_t* d = det + ((size_t)b * cap + i) * 3;
     const int64_t px = d[0], py = d[1], pt = d[2];
-    x[idx] = feat[(((size_t)b * C + c) * H + py) * W + px];
+    if (feat) x[idx] = feat[(((size_t)b * C + c) * H + py) * W + px];   // NULL: pemp_gather_projected fills x
     if (c == 0) {
       jdet[g * 3 + 0] = px; jdet[g * 3 + 1] = py; jdet[g * 3 + 2] = pt;
       jsc[g] = det_sc[(size_t)b * cap + i];
@@ -354,7 +354,7 @@ extern "C" int pemp_pack_nodes(const float* features, int C, const float* tagmap
                                const int64_t* det_xyt, const float* det_scores, int cap, const int64_t* node_off,
                                int64_t n_total, float* x, int64_t* joint_det, float* joint_scores,
                                int64_t* batch_index, float* joint_tags, void* stream) {
-  PEMP_CHECK_ARG(features && det_xyt && det_scores && node_off && x && joint_det && joint_scores && batch_index,
+  PEMP_CHECK_ARG(det_xyt && det_scores && node_off && x && joint_det && joint_scores && batch_index,
                  "pemp_pack_nodes: null pointer");
   PEMP_CHECK_ARG(C > 0 && B > 0 && J > 0 && H > 0 && W > 0 && n_total >= 0, "pemp_pack_nodes: bad shape");
   PEMP_CHECK_ARG(!tagmaps || (joint_tags && F > 0 && F <= C), "pemp_pack_nodes: tags need F in [1, C]");
@@ -435,7 +435,7 @@ __global__ __launch_bounds__(256) void fused_fully_graph_kernel(FusedGraphArgs a
       const int64_t i = g - noff[b];
       const int64_t* d = a.det + ((size_t)b * a.cap + i) * 3;
       const int64_t px = d[0], py = d[1], pt = d[2];
-      a.x[idx] = a.feat[(((size_t)b * a.C + c) * a.H + py) * a.W + px];
+      if (a.feat) a.x[idx] = a.feat[(((size_t)b * a.C + c) * a.H + py) * a.W + px];
       if (c == 0) {
         a.jdet[g * 3 + 0] = px; a.jdet[g * 3 + 1] = py; a.jdet[g * 3 + 2] = pt;
         a.jsc[g] = a.det_sc[(size_t)b * a.cap + i];
@@ -544,7 +544,7 @@ static int fully_graph_build(const int32_t* n_det, int B, const int64_t* det_xyt
                              int64_t n_total, int64_t e_total, float norm_factor, int mode, float* x,
                              int64_t* joint_det, float* joint_scores, int64_t* batch_index, float* joint_tags,
                              int64_t* edge_index, float* edge_attr, int capacity, void* stream) {
-  PEMP_CHECK_ARG(n_det && det_xyt && det_scores && features && x && joint_det && joint_scores && batch_index,
+  PEMP_CHECK_ARG(n_det && det_xyt && det_scores && x && joint_det && joint_scores && batch_index,
                  "pemp_fully_graph_build: null pointer");
   PEMP_CHECK_ARG(B > 0 && B <= FUSED_MAXB && C > 0 && J > 0 && H > 0 && W > 0 && n_total >= 0 && e_total >= 0,
                  "pemp_fully_graph_build: bad shape (B must be in [1, %d])", FUSED_MAXB);
@@ -597,6 +597,57 @@ __global__ __launch_bounds__(64) void graph_offsets_kernel(const int32_t* __rest
     if (edge_off) edge_off[B] = ce;
   }
 }
+// ---- node features sampled from projected maps -----------------------------
+// The test front-end projects every scale's gathered features to the image size
+// (PoseEstimation.py:426-452: interpolate(bilinear, align_corners=False)), sums the scales and
+// divides by their count (multi_scales_testing.py:182-190, PoseEstimation.py:244), then
+// construct_graph reads x = features[:, y, x].T. Here only the N detections are interpolated:
+// nothing of size [C, H, W] is materialised. Source index as torch's area_pixel_compute_source_index:
+// s = (h / H) * (y + 0.5) - 0.5 clamped at 0, y1 = y0 + (y0 < h - 1), weights 1 - l, l.
+constexpr int PROJ_MAXS = 8;
+struct ProjMaps {
+  const float* p[PROJ_MAXS];   // [B][C][h_s][w_s]
+  int h[PROJ_MAXS], w[PROJ_MAXS];
+  int S;
+};
+
+__device__ __forceinline__ void proj_src(int dst, int out_size, int in_size, int& i0, int& i1, float& l0, float& l1) {
+  const float scale = (float)in_size / (float)out_size;
+  float src = __fsub_rn(__fmul_rn(scale, __fadd_rn((float)dst, 0.5f)), 0.5f);
+  if (src < 0.f) src = 0.f;
+  i0 = (int)src;
+  i1 = i0 + (i0 < in_size - 1 ? 1 : 0);
+  l1 = fminf(fmaxf(__fsub_rn(src, (float)i0), 0.f), 1.f);
+  l0 = __fsub_rn(1.f, l1);
+}
+
+__global__ __launch_bounds__(256) void gather_projected_kernel(ProjMaps m, int C, int H, int W, float divisor,
+                                                               const int64_t* __restrict__ jdet,
+                                                               const int64_t* __restrict__ bidx, int64_t N,
+                                                               float* __restrict__ x) {
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < N * C;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t n = idx / C;
+    const int c = (int)(idx - n * C);
+    const int px = (int)jdet[n * 3 + 0], py = (int)jdet[n * 3 + 1];
+    const int64_t b = bidx[n];
+    float acc = 0.f;
+    for (int s = 0; s < m.S; ++s) {
+      const int h = m.h[s], w = m.w[s];
+      int y0, y1, x0, x1;
+      float ly0, ly1, lx0, lx1;
+      proj_src(py, H, h, y0, y1, ly0, ly1);
+      proj_src(px, W, w, x0, x1, lx0, lx1);
+      const float* pl = m.p[s] + ((size_t)b * C + c) * h * w;
+      const float t0 = __fadd_rn(__fmul_rn(pl[y0 * w + x0], lx0), __fmul_rn(pl[y0 * w + x1], lx1));
+      const float t1 = __fadd_rn(__fmul_rn(pl[y1 * w + x0], lx0), __fmul_rn(pl[y1 * w + x1], lx1));
+      const float v = __fadd_rn(__fmul_rn(t0, ly0), __fmul_rn(t1, ly1));
+      acc = s == 0 ? v : __fadd_rn(acc, v);
+    }
+    x[idx] = __fdiv_rn(acc, divisor);
+  }
+}
+
 // ---- score_based_graph (ConstructGraph.py:405-422) -------------------------------------------
 // Roots are the k best-scoring nodes of an image (ties: lower node index). Edge (a, b), a != b,
 // exists iff a or b is a root, sorted by (a, b): a root row lists every other node, a non-root row
@@ -830,6 +881,29 @@ extern "C" int pemp_score_graph(const float* joint_scores, const int64_t* node_o
   const int64_t blocks = std::min<int64_t>((n_total + 3) / 4, 4096);
   hipLaunchKernelGGL(score_emit_kernel, dim3((unsigned)blocks), dim3(256), 0, st, node_off, B, k, w, n_total,
                      e_total, edge_index);
+  PEMP_LAUNCH_CHECK();
+  return PEMP_OK;
+}
+
+extern "C" int pemp_gather_projected(const float* const* maps, const int* map_h, const int* map_w, int S, int C,
+                                     int H, int W, float divisor, const int64_t* joint_det,
+                                     const int64_t* batch_index, int64_t N, float* x, void* stream) {
+  PEMP_CHECK_ARG(maps && map_h && map_w && S >= 1 && S <= PROJ_MAXS && C > 0 && H > 0 && W > 0 && N >= 0 &&
+                     divisor > 0.f,
+                 "pemp_gather_projected: bad args (S in [1, %d])", PROJ_MAXS);
+  PEMP_CHECK_ARG(N == 0 || (joint_det && batch_index && x), "pemp_gather_projected: null node arrays");
+  ProjMaps m{};
+  m.S = S;
+  for (int s = 0; s < S; ++s) {
+    PEMP_CHECK_ARG(maps[s] && map_h[s] > 0 && map_w[s] > 0, "pemp_gather_projected: bad map %d", s);
+    m.p[s] = maps[s];
+    m.h[s] = map_h[s];
+    m.w[s] = map_w[s];
+  }
+  if (N == 0) return PEMP_OK;
+  ProfScope prof("gather_projected", as_stream(stream));
+  hipLaunchKernelGGL(gather_projected_kernel, dim3(grid_for(N * C, 256, 4096)), dim3(256), 0, as_stream(stream), m, C,
+                     H, W, divisor, joint_det, batch_index, N, x);
   PEMP_LAUNCH_CHECK();
   return PEMP_OK;
 }

@@ -13,6 +13,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from .frontend import ProjectedMaps
 
 _SCORE_BASED_K = 75        # ConstructGraph.py:280 (score_based_graph roots)
 _EF_MODES = {
@@ -132,10 +133,18 @@ class NaiveGraphConstructor:
                                  cap, counts_h.ctypes.data, st))
         # host-side preparation of the graph stage, while the detection kernels run
         feats = self.features
-        if feats.dtype != torch.float32:
-            feats = feats.float()
-        feats = feats.contiguous()
-        C = feats.shape[1]
+        projected = isinstance(feats, ProjectedMaps)
+        if projected:      # x sampled from the projected maps after the graph build (pemp_gather_projected)
+            if feats.size != (H, W):
+                raise ValueError(f"ProjectedMaps size {feats.size} != scoremap size {(H, W)}")
+            pmaps = [m.float().contiguous() for m in feats.maps]
+            C = pmaps[0].shape[1]
+            feats = None
+        else:
+            if feats.dtype != torch.float32:
+                feats = feats.float()
+            feats = feats.contiguous()
+            C = feats.shape[1]
         tags = self.tagmaps
         if tags is not None:
             tags = tags.float().contiguous()
@@ -195,6 +204,8 @@ class NaiveGraphConstructor:
             joint_tags = built[4][:N] if tags is not None else None
             edge_index = built[5][:2 * E_fully].view(2, E_fully)
             edge_attr = built[6][:E_fully]
+            if projected:
+                self._gather_projected(L, st, pmaps, H, W, joint_det, batch_index, x)
             if tags is not None:
                 joint_tags = joint_tags.view((N,) + tuple(tags.shape[4:])) if tags.dim() > 4 else joint_tags.view(N)
             return (x, edge_attr, edge_index, None, None, None, None, joint_det, None, None, None, joint_scores,
@@ -231,10 +242,22 @@ class NaiveGraphConstructor:
             _lib.check(L.pemp_edge_features(_lib.ptr(joint_det), _lib.ptr(joint_tags), F, _lib.ptr(joint_scores),
                                             _lib.ptr(edge_index), E, J, norm, mode,
                                             _lib.ptr(edge_attr), st))
+        if projected:
+            self._gather_projected(L, st, pmaps, H, W, joint_det, batch_index, x)
         if tags is not None:
             joint_tags = joint_tags.view((N,) + tuple(tags.shape[4:])) if tags.dim() > 4 else joint_tags.view(N)
         return (x, edge_attr, edge_index, None, None, None, None, joint_det, None, None, None, joint_scores,
                 batch_index, None, joint_tags)
+
+    def _gather_projected(self, L, st, pmaps, H, W, joint_det, batch_index, x):
+        S = len(pmaps)
+        ptrs = (ctypes.c_void_p * S)(*[m.data_ptr() for m in pmaps])
+        hs = (ctypes.c_int32 * S)(*[m.shape[2] for m in pmaps])
+        ws = (ctypes.c_int32 * S)(*[m.shape[3] for m in pmaps])
+        vp = ctypes.c_void_p
+        _lib.check(L.pemp_gather_projected(ctypes.cast(ptrs, vp), ctypes.cast(hs, vp), ctypes.cast(ws, vp), S,
+                                           x.shape[1], H, W, self.features.divisor,
+                                           _lib.ptr(joint_det), _lib.ptr(batch_index), x.shape[0], _lib.ptr(x), st))
 
     def _edges(self, L, st, joint_det, joint_scores, node_off, fully_off, node_off_h, B, dev):
         counts = np.diff(node_off_h)

@@ -111,3 +111,27 @@ def test_score_based_needs_k_detections():
         run_gc(gc, J, hm, feats, None, None)
     with pytest.raises(RuntimeError, match="out of range"):
         restate.construct_graph(hm, feats, torch.zeros(1, J, H, W), None, gc, J)
+
+
+@pytest.mark.parametrize("graph_type,scales", [("fully", [(80, 80)]), ("knn", [(80, 80), (40, 40)]),
+                                               ("fully", [(53, 67), (160, 160), (27, 33)])])
+def test_projected_features(graph_type, scales):
+    """features=ProjectedMaps: x sampled at the detections from low-resolution maps
+    equals the reference's materialised bilinear projection (interpolate, align_corners=False, summed
+    over scales / their count) gathered at the same detections. Tolerance 2e-6 absolute (fp32 bilinear
+    weights; torch's CPU kernel may contract the products into FMAs); every other output bit-exact."""
+    from pemp_amd.frontend import ProjectedMaps
+    B, J, H, W = 2, 17, 160, 160
+    hm = torch.from_numpy(syn.make_heatmaps(31, B, J, H, W, 4, margin=4))
+    maps = [torch.from_numpy(syn.closed_form((B, 128, h, w), 0.25 + 0.1 * k)) for k, (h, w) in enumerate(scales)]
+    pm = ProjectedMaps(maps, (H, W))
+    dense = pm.materialize()                                   # torch CPU, the reference's tensors
+    gc = pcfg.inference_gc_config(graph_type, 5, False)
+    tags = torch.from_numpy(syn.closed_form((B, J, H, W, 1), 0.75))
+    for _ in range(2):                                          # second call takes the capacity build
+        out = run_gc(gc, J, hm, pm, tags, None)
+        ref = restate.construct_graph(hm, dense, tags, None, gc, J)
+        for i in (1, 2, 7, 11, 12, 14):
+            assert torch.equal(out[i].cpu(), ref[i]), i
+        assert out[0].shape == ref[0].shape
+        assert (out[0].cpu() - ref[0]).abs().max().item() <= 2e-6
