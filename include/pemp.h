@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PEMP_ABI_VERSION 6
+#define PEMP_ABI_VERSION 7
 
 enum {
   PEMP_OK = 0,
@@ -99,7 +99,8 @@ int pemp_fully_graph_build(const int32_t* n_det, int B, const int64_t* det_xyt, 
                            const float* features, int C, const float* tagmaps, int F, int J, int H, int W,
                            int64_t n_total, int64_t e_total, float norm_factor, int mode, float* x,
                            int64_t* joint_det, float* joint_scores, int64_t* batch_index, float* joint_tags,
-                           int64_t* edge_index, float* edge_attr, void* stream);
+                           int64_t* edge_index, float* edge_attr, int64_t* node_off /*[B+1] or NULL*/,
+                           void* stream);
 
 /* Capacity mode of pemp_fully_graph_build, launched BEFORE the host reads the counts back (the
  * reference's nonzero/cat syncs, ConstructGraph.py:1170-1196, become one host read that overlaps
@@ -111,7 +112,8 @@ int pemp_fully_graph_build_cap(const int32_t* n_det, int B, const int64_t* det_x
                                const float* features, int C, const float* tagmaps, int F, int J, int H, int W,
                                int64_t n_cap, int64_t e_cap, float norm_factor, int mode, float* x,
                                int64_t* joint_det, float* joint_scores, int64_t* batch_index, float* joint_tags,
-                               int64_t* edge_index, float* edge_attr, void* stream);
+                               int64_t* edge_index, float* edge_attr, int64_t* node_off /*[B+1] or NULL*/,
+                               void* stream);
 
 /* Fully connected graph per image: all (i,j), i != j, sorted by (src,dst), node-offset per image.
  * node_off / edge_off: device [B+1] int64 with edge_off[b+1]-edge_off[b] = n_b (n_b - 1). */
@@ -265,6 +267,17 @@ int pemp_mpn_forward(const pemp_mpn_desc* desc, const pemp_mpn_weights* weights,
                      const float* edge_attr, const int64_t* edge_index, const int64_t* node_types,
                      int64_t N, int64_t E, float* edge_logits, float* node_logits, float* class_logits,
                      void* workspace, size_t workspace_bytes, void* stream);
+
+/* pemp_mpn_forward for a batch whose edge_index is the fully-connected graph of
+ * pemp_fully_graph_build (ConstructGraph.py:376-381) with per-image node offsets node_off (device,
+ * [B+1], as written by the build) / node_off_host: the type-major edge order is produced in closed
+ * form by one kernel instead of the sorting prepare; results are identical. E must equal
+ * sum n_b (n_b - 1) (checked); images above 2048 nodes fall back to the sorting prepare. */
+int pemp_mpn_forward_fully(const pemp_mpn_desc* desc, const pemp_mpn_weights* weights, const float* x,
+                           const float* edge_attr, const int64_t* edge_index, const int64_t* node_types,
+                           int64_t N, int64_t E, const int64_t* node_off, const int64_t* node_off_host, int B,
+                           float* edge_logits, float* node_logits, float* class_logits,
+                           void* workspace, size_t workspace_bytes, void* stream);
 
 /* The edge-ordering part of pemp_mpn_forward (type-major counting sort of edge_index by (source type,
  * target)), callable ahead of it: it needs no weights, so a caller can queue it as soon as the graph

@@ -8,7 +8,7 @@ import os
 
 LIB_PATH = os.environ.get("PEMP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc",
                                                      "libpemp.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 ERR_INVALID_ARG, ERR_HIP, ERR_WORKSPACE, ERR_UNSUPPORTED = -1, -2, -3, -4
 
@@ -56,9 +56,9 @@ SIGNATURES = {
                                 c_p, c_p, c_p, c_p, c_p, c_p]),
     "pemp_graph_offsets": (c_i32, [c_p, c_i32, c_p, c_p, c_p]),
     "pemp_fully_graph_build": (c_i32, [c_p, c_i32, c_p, c_p, c_i32, c_p, c_i32, c_p, c_i32, c_i32, c_i32, c_i32,
-                                       c_i64, c_i64, c_f32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+                                       c_i64, c_i64, c_f32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "pemp_fully_graph_build_cap": (c_i32, [c_p, c_i32, c_p, c_p, c_i32, c_p, c_i32, c_p, c_i32, c_i32, c_i32, c_i32,
-                                           c_i64, c_i64, c_f32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+                                           c_i64, c_i64, c_f32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "pemp_fully_graph": (c_i32, [c_p, c_p, c_i32, c_i64, c_p, c_p]),
     "pemp_knn_workspace_size": (c_sz, [c_p, c_i32]),
     "pemp_knn_graph_count": (c_i32, [c_p, c_p, c_p, c_i32, c_i32, c_p, c_sz, c_p, c_p]),
@@ -70,6 +70,8 @@ SIGNATURES = {
     "pemp_mpn_workspace_size": (c_sz, [ctypes.POINTER(PempMpnDesc), c_i64, c_i64]),
     "pemp_mpn_forward": (c_i32, [ctypes.POINTER(PempMpnDesc), ctypes.POINTER(PempMpnWeights), c_p, c_p, c_p, c_p,
                                  c_i64, c_i64, c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "pemp_mpn_forward_fully": (c_i32, [ctypes.POINTER(PempMpnDesc), ctypes.POINTER(PempMpnWeights), c_p, c_p, c_p,
+                                       c_p, c_i64, c_i64, c_p, c_p, c_i32, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "pemp_mpn_prepare": (c_i32, [ctypes.POINTER(PempMpnDesc), c_p, c_p, c_i64, c_i64, c_p, c_sz, c_p]),
     "pemp_mpn_node_image_floats": (c_sz, [ctypes.POINTER(PempMpnWeights)]),
     "pemp_mpn_node_image": (c_i32, [ctypes.POINTER(PempMpnWeights), c_p, c_sz, c_p]),

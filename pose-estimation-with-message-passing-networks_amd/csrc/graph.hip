@@ -382,6 +382,7 @@ struct FusedGraphArgs {
   int node_blocks;
   float *x, *jsc, *jtag, *edge_attr;
   int64_t *jdet, *bidx, *ei;
+  int64_t* node_off_out;      // [B + 1] or NULL
 };
 
 // One launch for the whole fully-connected graph after the count read-back: every block derives
@@ -418,6 +419,8 @@ __global__ __launch_bounds__(256) void fused_fully_graph_kernel(FusedGraphArgs a
   const int64_t n_total = a.capacity ? (int64_t)noff[B] : a.n_total;
   const int64_t e_total = a.capacity ? (int64_t)eoff[B] : a.e_total;
   if (a.capacity && (n_total > a.n_total || e_total > a.e_total)) return;
+  if (a.node_off_out && blockIdx.x == 0)   // per-image node offsets for pemp_mpn_forward_fully
+    for (int i = threadIdx.x; i <= B; i += blockDim.x) a.node_off_out[i] = noff[i];
   auto seg = [&](const long long* off, long long v) {
     int lo = 0, hi = B - 1;
     while (lo < hi) {
@@ -517,33 +520,36 @@ static int fully_graph_build(const int32_t* n_det, int B, const int64_t* det_xyt
                              const float* features, int C, const float* tagmaps, int F, int J, int H, int W,
                              int64_t n_total, int64_t e_total, float norm_factor, int mode, float* x,
                              int64_t* joint_det, float* joint_scores, int64_t* batch_index, float* joint_tags,
-                             int64_t* edge_index, float* edge_attr, int capacity, void* stream);
+                             int64_t* edge_index, float* edge_attr, int64_t* node_off_out, int capacity, void* stream);
 
 extern "C" int pemp_fully_graph_build(const int32_t* n_det, int B, const int64_t* det_xyt, const float* det_scores,
                                       int cap, const float* features, int C, const float* tagmaps, int F, int J,
                                       int H, int W, int64_t n_total, int64_t e_total, float norm_factor, int mode,
                                       float* x, int64_t* joint_det, float* joint_scores, int64_t* batch_index,
-                                      float* joint_tags, int64_t* edge_index, float* edge_attr, void* stream) {
+                                      float* joint_tags, int64_t* edge_index, float* edge_attr, int64_t* node_off,
+                                      void* stream) {
   return fully_graph_build(n_det, B, det_xyt, det_scores, cap, features, C, tagmaps, F, J, H, W, n_total, e_total,
                            norm_factor, mode, x, joint_det, joint_scores, batch_index, joint_tags, edge_index,
-                           edge_attr, 0, stream);
+                           edge_attr, node_off, 0, stream);
 }
 
 extern "C" int pemp_fully_graph_build_cap(const int32_t* n_det, int B, const int64_t* det_xyt, const float* det_scores,
                                           int cap, const float* features, int C, const float* tagmaps, int F, int J,
                                           int H, int W, int64_t n_cap, int64_t e_cap, float norm_factor, int mode,
                                           float* x, int64_t* joint_det, float* joint_scores, int64_t* batch_index,
-                                          float* joint_tags, int64_t* edge_index, float* edge_attr, void* stream) {
+                                          float* joint_tags, int64_t* edge_index, float* edge_attr,
+                                          int64_t* node_off, void* stream) {
   return fully_graph_build(n_det, B, det_xyt, det_scores, cap, features, C, tagmaps, F, J, H, W, n_cap, e_cap,
                            norm_factor, mode, x, joint_det, joint_scores, batch_index, joint_tags, edge_index,
-                           edge_attr, 1, stream);
+                           edge_attr, node_off, 1, stream);
 }
 
 static int fully_graph_build(const int32_t* n_det, int B, const int64_t* det_xyt, const float* det_scores, int cap,
                              const float* features, int C, const float* tagmaps, int F, int J, int H, int W,
                              int64_t n_total, int64_t e_total, float norm_factor, int mode, float* x,
                              int64_t* joint_det, float* joint_scores, int64_t* batch_index, float* joint_tags,
-                             int64_t* edge_index, float* edge_attr, int capacity, void* stream) {
+                             int64_t* edge_index, float* edge_attr, int64_t* node_off_out, int capacity,
+                             void* stream) {
   PEMP_CHECK_ARG(n_det && det_xyt && det_scores && x && joint_det && joint_scores && batch_index,
                  "pemp_fully_graph_build: null pointer");
   PEMP_CHECK_ARG(B > 0 && B <= FUSED_MAXB && C > 0 && J > 0 && H > 0 && W > 0 && n_total >= 0 && e_total >= 0,
@@ -561,7 +567,7 @@ static int fully_graph_build(const int32_t* n_det, int B, const int64_t* det_xyt
   a.node_blocks = grid_for(n_total * C, 256, 4096);
   const int edge_blocks = e_total > 0 ? grid_for(e_total, 256, 8192) : 0;
   a.x = x; a.jsc = joint_scores; a.jtag = joint_tags; a.edge_attr = edge_attr;
-  a.jdet = joint_det; a.bidx = batch_index; a.ei = edge_index;
+  a.jdet = joint_det; a.bidx = batch_index; a.ei = edge_index; a.node_off_out = node_off_out;
   ProfScope prof("graph_build", as_stream(stream));
   hipLaunchKernelGGL(fused_fully_graph_kernel, dim3(a.node_blocks + edge_blocks), dim3(256), 0, as_stream(stream), a);
   PEMP_LAUNCH_CHECK();

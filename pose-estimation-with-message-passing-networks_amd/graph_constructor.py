@@ -30,6 +30,12 @@ _EF_MODES = {
 _EF_TAG_MODES = (5, 6, 7, 8)
 
 
+def _tag_fully(edge_index, node_off, counts, joint_det):
+    """Mark edge_index as this batch's fully graph (per-image node offsets on the device, counts on
+    the host) so that the MPN can take pemp_mpn_forward_fully; the versions detect in-place edits."""
+    edge_index._pemp_fully = (node_off, tuple(counts), joint_det, joint_det._version, edge_index._version)
+
+
 def get_graph_constructor(config, **kwargs):
     """``src/graph_constructor/__init__.py:4-5``."""
     return NaiveGraphConstructor(config=config, **kwargs)
@@ -173,7 +179,8 @@ class NaiveGraphConstructor:
                     torch.empty(n_cap, dtype=torch.int64, device=dev),
                     torch.empty(n_cap, F, dtype=torch.float32, device=dev) if tags is not None else None,
                     torch.empty(2 * e_cap, dtype=torch.int64, device=dev),
-                    torch.empty(e_cap, A, dtype=torch.float32, device=dev))
+                    torch.empty(e_cap, A, dtype=torch.float32, device=dev),
+                    torch.empty(B + 1, dtype=torch.int64, device=dev))          # node offsets (MPN fast path)
             _lib.check(L.pemp_fully_graph_build_cap(
                 _lib.ptr(n_det), B, _lib.ptr(det), _lib.ptr(dsc), cap, _lib.ptr(feats), C, _lib.ptr(tags), F, J, H, W,
                 n_cap, e_cap, norm, mode, *[_lib.ptr(t) for t in bufs], st))
@@ -208,6 +215,7 @@ class NaiveGraphConstructor:
                 self._gather_projected(L, st, pmaps, H, W, joint_det, batch_index, x)
             if tags is not None:
                 joint_tags = joint_tags.view((N,) + tuple(tags.shape[4:])) if tags.dim() > 4 else joint_tags.view(N)
+            _tag_fully(edge_index, built[7], counts_l, joint_det)
             return (x, edge_attr, edge_index, None, None, None, None, joint_det, None, None, None, joint_scores,
                     batch_index, None, joint_tags)
         x = torch.empty(N, C, dtype=torch.float32, device=dev)
@@ -221,10 +229,13 @@ class NaiveGraphConstructor:
             E = sum(c * (c - 1) for c in counts_l if c > 1)
             edge_index = torch.empty(2, E, dtype=torch.int64, device=dev)
             edge_attr = torch.empty(E, A, dtype=torch.float32, device=dev)
+            node_off = torch.empty(B + 1, dtype=torch.int64, device=dev)
             _lib.check(L.pemp_fully_graph_build(
                 _lib.ptr(n_det), B, _lib.ptr(det), _lib.ptr(dsc), cap, _lib.ptr(feats), C, _lib.ptr(tags), F, J, H, W,
                 N, E, norm, mode, _lib.ptr(x), _lib.ptr(joint_det), _lib.ptr(joint_scores), _lib.ptr(batch_index),
-                _lib.ptr(joint_tags), _lib.ptr(edge_index), _lib.ptr(edge_attr), st))
+                _lib.ptr(joint_tags), _lib.ptr(edge_index), _lib.ptr(edge_attr), _lib.ptr(node_off), st))
+            if N > 0:
+                _tag_fully(edge_index, node_off, counts_l, joint_det)
         else:
             node_off_h = np.zeros(B + 1, np.int64)
             node_off_h[1:] = np.cumsum(np.asarray(counts_l, np.int64))

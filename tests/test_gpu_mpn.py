@@ -200,3 +200,34 @@ def test_edge_mlp_per_type_c3_shape(prec):
     for a, b in zip(pe + pn + pc, rpe + rpn + rpc):
         assert a.shape == b.shape
         assert max_err(a, b) < TOL
+
+
+@pytest.mark.parametrize("prec", PRECS)
+def test_fully_graph_fast_prepare_is_identical(prec, monkeypatch):
+    """pemp_mpn_forward_fully (closed-form type-major order for the constructor's fully graph) must
+    give bit-identical logits to the sorting prepare, on the exact and the capacity build, and must
+    not be taken once edge_index was edited in place."""
+    from pemp_amd.mpn import model as mm
+    B, J, H, W = 4, 17, 160, 160
+    hm = torch.from_numpy(syn.make_heatmaps(11, B, J, H, W, 5))
+    hm[2] = 0.0                                                 # an empty image in the batch
+    feats = torch.from_numpy(syn.closed_form((B, 128, H, W), 0.25))
+    gc = pcfg.inference_gc_config("fully", 5, False)
+    cfg = pcfg.published_mpn_config(J, 3, "attn")
+    model, _ = make_model(cfg, 2.25, prec)
+    for _ in range(2):                                          # exact build, then the capacity build
+        out = pemp_amd.get_graph_constructor(gc, scoremaps=hm.to(DEV), features=feats.to(DEV), tagmaps=None,
+                                             joints_gt=None, factor_list=None, masks=None, device=DEV,
+                                             testing=True, heatmaps=None, num_joints=J).construct_graph()
+        x, ea, ei, types = out[0], out[1], out[2], out[7][:, 2]
+        assert mm._fully_graph(ei, types, x.shape[0]) is not None
+        fast = run(model, x, ea, ei, types)
+        monkeypatch.setattr(mm, "_FULLY_OFF", True)
+        slow = run(model, x, ea, ei, types)
+        monkeypatch.setattr(mm, "_FULLY_OFF", False)
+        for a, b in zip(fast[0] + fast[1] + fast[2], slow[0] + slow[1] + slow[2]):
+            assert torch.equal(a, b)
+    ei2 = ei.clone()
+    ei.add_(0)                                                  # in-place edit bumps the version
+    assert mm._fully_graph(ei, types, x.shape[0]) is None
+    assert mm._fully_graph(ei2, types, x.shape[0]) is None      # a copy carries no tag
