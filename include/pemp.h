@@ -21,6 +21,8 @@
  *   pemp_score_graph     ConstructGraph.py:405-422 score_based_graph (k = 75 roots)
  *   pemp_edge_features   ConstructGraph.py:289-359 (edge_attr)
  *   pemp_gather_projected  PoseEstimation.py:426-452 feature projection, sampled at the detections only
+ *   pemp_pose_*          Utils.py:499-514,672-743,1445-1455 pose grouping (pred_to_ann prefix, pred_to_person,
+ *                        GAEC of correlation_clustering_utils.py:187-245, graph_cluster_to_persons)
  *   pemp_mpn_forward     Models/MessagePassingNetwork/NodeClassificationMPNSimple.py:62-97 with
  *                        layers.py:32-86 (MPLayer) / :157-274 (TypeAwareMPNLayer)
  */
@@ -34,7 +36,7 @@
 extern "C" {
 #endif
 
-#define PEMP_ABI_VERSION 7
+#define PEMP_ABI_VERSION 8
 
 enum {
   PEMP_OK = 0,
@@ -170,6 +172,36 @@ enum {
 int pemp_edge_features(const int64_t* joint_det /*[N,3]*/, const float* joint_tags, int F, const float* joint_scores,
                        const int64_t* edge_index /*[2,E]*/, int64_t e_total, int J, float norm_factor, int mode,
                        float* edge_attr, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Pose grouping: Utils.py:1445-1455 (pred_to_ann: node threshold + subgraph),
+ * Utils.py:499-514 (pred_to_person), correlation_clustering_utils.py:99-151,187-245 (edge matrix
+ * symmetrisation, cluster_andres_graph with GAEC), Utils.py:672-743 (graph_cluster_to_persons).
+ *
+ * 1. pemp_pose_edge_weights (GPU, stream-ordered): edge_index [2,E] int64 must be strictly sorted by
+ *    (src, dst) (construct_graph's output is). An edge survives iff use_th == 0 or both
+ *    node_scores[end] > th. method 0 (GAEC): w[e] = fl32(pred[e] + pred[reverse(e)]) (0 if the reverse
+ *    is absent) for surviving edges with src < dst; method 1 (threshold): w[e] = pred[e] for every
+ *    surviving edge; NaN elsewhere. flags[B + 1] (device int32): flags[b] bit 0 = image b has a
+ *    surviving src > dst edge with pred != 0 (the reference then averages, else adds), bit 1 = image b
+ *    keeps an edge; flags[B] bit 0 = edge_index not sorted.
+ * 2. pemp_pose_cluster (HOST arrays, copies of the above): per image, greedy additive edge contraction
+ *    (andres graph greedyAdditiveEdgeContraction, weights (w/2 or w) - 0.5 in fp32, then double) or
+ *    threshold joins (w > 0.8f); labels[ΣN] = connected-component ids per image in order of each
+ *    component's lowest node (scipy connected_components), n_comp[B]. Images run on n_threads threads.
+ * 3. pemp_pose_persons (HOST): graph_cluster_to_persons per image from labels: persons[cap][J][3] f64
+ *    (x, y, score of the best-scoring joint per (re-)typed joint type; class_probs [ΣN,J] re-types by
+ *    first argmax when non-NULL; pose_scores replaces the score when non-NULL), person_count[B],
+ *    mutants[B] (a component larger than J). PEMP_ERR_WORKSPACE when more than cap persons. */
+int pemp_pose_edge_weights(const int64_t* edge_index, int64_t E, const float* pred, const float* node_scores,
+                           float th, int use_th, const int64_t* node_off /*[B+1] device*/, int B, int method,
+                           float* w, int* flags, void* stream);
+int pemp_pose_cluster(int B, const int64_t* node_off, const int64_t* edge_index, int64_t E, const float* w,
+                      const int* flags, int method, int n_threads, int32_t* labels, int32_t* n_comp);
+int pemp_pose_persons(int B, const int64_t* node_off, const int32_t* labels, const int32_t* n_comp,
+                      const int64_t* joint_det, const float* scores, const float* pose_scores,
+                      const float* class_probs, int J, int allow_single, int64_t cap, double* persons,
+                      int32_t* person_count, int32_t* mutants);
 
 /* ------------------------------------------------------------------------------------------
  * Message-passing network, inference (eval-mode BatchNorm folded into the next Linear by the

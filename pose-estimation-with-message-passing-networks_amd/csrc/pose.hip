@@ -1,0 +1,317 @@
+// Pose grouping — restates:
+//   Utils.py:1445-1455          pred_to_ann prefix: node threshold joint_scores > th, PyG subgraph
+//                               (an edge survives iff both ends survive; no relabelling)
+//   correlation_clustering_utils.py:99-151
+//                               extract_edge_matrix(update=True) + update_graph_with_edge_matrix: dense
+//                               adjacency of the surviving edges, averaged with its transpose in fp32
+//                               ((a + b) / 2), or a + transpose when its lower triangle sums to zero
+//   correlation_clustering_utils.py:187-245
+//                               cluster_andres_graph(complete=False): upper-triangle edges, weight
+//                               w - 0.5, andres GAEC, 1 = joined
+//   Utils.py:499-514            pred_to_person (GAEC / threshold branches)
+//   Utils.py:672-743            graph_cluster_to_persons: connected components (scipy labels: in order of
+//                               each component's lowest node), class re-typing, best-scoring joint per type
+//
+// The edge pass is a GPU kernel over the batched graph (one thread per edge, reverse edge found by binary
+// search in the (src, dst)-sorted edge list). Greedy additive edge contraction is inherently sequential: it
+// runs on the host, one image per thread, restating andres::graph::multicut::greedyAdditiveEdgeContraction
+// (andres graph, the library behind the reference's missing andres_graph_wrapper; not vendored): a max-heap of
+// (a, b, w, edition) entries ordered by w only (std::priority_queue, so ties resolve exactly as libstdc++'s
+// heap does), per-vertex std::map adjacency, contraction of the endpoint with fewer neighbours into the
+// other, stale entries skipped by edition, stop at the first entry with w < 0.
+#include <math.h>
+
+#include <algorithm>
+#include <map>
+#include <queue>
+#include <thread>
+#include <vector>
+
+#include "pemp_common.h"
+
+using namespace pemp;
+
+namespace {
+
+__device__ __forceinline__ int pose_find_image(const int64_t* off, int n, int64_t v) {
+  int lo = 0, hi = n;  // off[lo] <= v < off[hi]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (off[mid] <= v) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+// w[e] = fl32(pred[e] + pred[rev(e)]) for a surviving upper edge (src < dst) in mode 0 (GAEC), pred[e] for
+// every surviving edge in mode 1 (threshold), NaN otherwise. flags[b]: bit 0 = a surviving lower-triangle
+// edge of image b has pred != 0 (extract_edge_matrix then averages), bit 1 = image b keeps an edge.
+// flags[B] bit 0: edge_index is not strictly (src, dst)-sorted.
+__global__ __launch_bounds__(256) void pose_edge_weights_kernel(const int64_t* __restrict__ ei, int64_t E,
+                                                                const float* __restrict__ pred,
+                                                                const float* __restrict__ score, float th,
+                                                                int use_th, const int64_t* __restrict__ node_off,
+                                                                int B, int mode, float* __restrict__ w,
+                                                                int* __restrict__ flags) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = ei[e], d = ei[E + e];
+    if (e + 1 < E) {
+      const int64_t s1 = ei[e + 1], d1 = ei[E + e + 1];
+      if (s1 < s || (s1 == s && d1 <= d)) atomicOr(&flags[B], 1);
+    }
+    const bool keep = !use_th || (score[s] > th && score[d] > th);
+    float out = __int_as_float(0x7fc00000);
+    if (keep) {
+      const int b = pose_find_image(node_off, B, s);
+      const float p = pred[e];
+      if (s > d && p != 0.f && !(flags[b] & 1)) atomicOr(&flags[b], 1);
+      if (!(flags[b] & 2)) atomicOr(&flags[b], 2);
+      if (mode == 1) {
+        out = p;
+      } else if (s < d) {
+        int64_t lo = 0, hi = E;  // first edge with key >= (d, s)
+        while (lo < hi) {
+          const int64_t mid = (lo + hi) >> 1;
+          const int64_t ms = ei[mid], md = ei[E + mid];
+          if (ms < d || (ms == d && md < s)) lo = mid + 1; else hi = mid;
+        }
+        const float q = (lo < E && ei[lo] == d && ei[E + lo] == s) ? pred[lo] : 0.f;
+        out = p + q;
+      }
+    }
+    w[e] = out;
+  }
+}
+
+struct GaecEdge {
+  size_t a, b, edition;
+  double w;
+  GaecEdge(size_t a_, size_t b_, double w_) : a(a_ < b_ ? a_ : b_), b(a_ < b_ ? b_ : a_), edition(0), w(w_) {}
+  bool operator<(const GaecEdge& o) const { return w < o.w; }
+};
+
+// Greedy additive edge contraction over n vertices; root[v] = the cluster representative of v.
+void gaec(size_t n, const std::vector<size_t>& ea, const std::vector<size_t>& eb, const std::vector<double>& ew,
+          std::vector<size_t>& root) {
+  std::vector<std::map<size_t, double>> adj(n);
+  std::vector<std::map<size_t, size_t>> editions(n);
+  std::priority_queue<GaecEdge> q;
+  for (size_t i = 0; i < ea.size(); ++i) {
+    adj[ea[i]][eb[i]] += ew[i];
+    adj[eb[i]][ea[i]] += ew[i];
+    GaecEdge e(ea[i], eb[i], ew[i]);
+    e.edition = ++editions[e.a][e.b];
+    q.push(e);
+  }
+  std::vector<size_t> parent(n), rank(n, 0);
+  for (size_t v = 0; v < n; ++v) parent[v] = v;
+  auto find = [&](size_t v) {
+    while (parent[v] != v) {
+      parent[v] = parent[parent[v]];
+      v = parent[v];
+    }
+    return v;
+  };
+  while (!q.empty()) {
+    const GaecEdge e = q.top();
+    q.pop();
+    const auto& aa = adj[e.a];
+    if (aa.empty() || aa.find(e.b) == aa.end() || e.edition < editions[e.a][e.b]) continue;
+    if (e.w < 0.0) break;
+    size_t keep = e.a, merge = e.b;
+    if (adj[keep].size() < adj[merge].size()) std::swap(keep, merge);
+    {
+      size_t rk = find(keep), rm = find(merge);
+      if (rk != rm) {
+        if (rank[rk] < rank[rm]) std::swap(rk, rm);
+        parent[rm] = rk;
+        if (rank[rk] == rank[rm]) ++rank[rk];
+      }
+    }
+    for (const auto& p : adj[merge]) {
+      if (p.first == keep) continue;
+      adj[keep][p.first] += p.second;
+      adj[p.first][keep] += p.second;
+      GaecEdge ne(keep, p.first, adj[keep][p.first]);
+      ne.edition = ++editions[ne.a][ne.b];
+      q.push(ne);
+    }
+    for (const auto& p : adj[merge]) adj[p.first].erase(merge);
+    adj[merge].clear();
+  }
+  root.resize(n);
+  for (size_t v = 0; v < n; ++v) root[v] = find(v);
+}
+
+void union_join(std::vector<size_t>& parent, size_t a, size_t b) {
+  auto find = [&](size_t v) {
+    while (parent[v] != v) {
+      parent[v] = parent[parent[v]];
+      v = parent[v];
+    }
+    return v;
+  };
+  a = find(a);
+  b = find(b);
+  if (a != b) parent[std::max(a, b)] = std::min(a, b);
+}
+
+}  // namespace
+
+extern "C" int pemp_pose_edge_weights(const int64_t* edge_index, int64_t E, const float* pred,
+                                      const float* node_scores, float th, int use_th, const int64_t* node_off, int B,
+                                      int method, float* w, int* flags, void* stream) {
+  PEMP_CHECK_ARG(E >= 0 && B >= 1 && (method == 0 || method == 1), "pemp_pose_edge_weights: bad args");
+  PEMP_CHECK_ARG(node_off && flags && (E == 0 || (edge_index && pred && w)) && (!use_th || node_scores),
+                 "pemp_pose_edge_weights: null pointer");
+  PEMP_HIP(hipMemsetAsync(flags, 0, sizeof(int) * (B + 1), as_stream(stream)));
+  if (E == 0) return PEMP_OK;
+  ProfScope prof("pose_edge_weights", as_stream(stream));
+  const int64_t blocks = std::min<int64_t>((E + 255) / 256, 8192);
+  hipLaunchKernelGGL(pose_edge_weights_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), edge_index,
+                     E, pred, node_scores, th, use_th, node_off, B, method, w, flags);
+  PEMP_LAUNCH_CHECK();
+  return PEMP_OK;
+}
+
+extern "C" int pemp_pose_cluster(int B, const int64_t* node_off, const int64_t* edge_index, int64_t E, const float* w,
+                                 const int* flags, int method, int n_threads, int32_t* labels, int32_t* n_comp) {
+  PEMP_CHECK_ARG(B >= 1 && E >= 0 && node_off && flags && labels && n_comp && (method == 0 || method == 1),
+                 "pemp_pose_cluster: bad args");
+  PEMP_CHECK_ARG(E == 0 || (edge_index && w), "pemp_pose_cluster: null edge arrays");
+  if (flags[B] & 1) {
+    ::pemp::set_error("pemp_pose_cluster: edge_index is not sorted by (src, dst) without duplicates");
+    return PEMP_ERR_INVALID_ARG;
+  }
+  for (int b = 0; b < B; ++b)
+    PEMP_CHECK_ARG(node_off[b + 1] >= node_off[b], "pemp_pose_cluster: node_off not monotone");
+  // bucket the surviving edges per image, keeping edge_index order
+  std::vector<std::vector<size_t>> ua(B), ub(B);
+  std::vector<std::vector<double>> uw(B);
+  int b = 0;
+  for (int64_t e = 0; e < E; ++e) {
+    const float we = w[e];
+    if (std::isnan(we)) continue;
+    const int64_t s = edge_index[e], d = edge_index[E + e];
+    while (b + 1 < B && s >= node_off[b + 1]) ++b;
+    while (b > 0 && s < node_off[b]) --b;
+    if (s < node_off[b] || s >= node_off[b + 1] || d < node_off[b] || d >= node_off[b + 1]) {
+      ::pemp::set_error("pemp_pose_cluster: edge %lld crosses images", (long long)e);
+      return PEMP_ERR_INVALID_ARG;
+    }
+    double weight;
+    if (method == 0) {
+      const float m = (flags[b] & 1) ? we * 0.5f : we;  // extract_edge_matrix: average, or M + M^T
+      weight = (double)(m - 0.5f);                          // cluster_andres_graph: edge_attr - 0.5 (fp32)
+    } else {
+      if (!(we > 0.8f)) continue;                           // pred_to_person "threshold": pred > 0.8
+      weight = 1.0;
+    }
+    ua[b].push_back((size_t)(s - node_off[b]));
+    ub[b].push_back((size_t)(d - node_off[b]));
+    uw[b].push_back(weight);
+  }
+  auto run = [&](int img) {
+    const size_t n = (size_t)(node_off[img + 1] - node_off[img]);
+    std::vector<size_t> root;
+    if (method == 0) {
+      gaec(n, ua[img], ub[img], uw[img], root);
+    } else {
+      root.resize(n);
+      for (size_t v = 0; v < n; ++v) root[v] = v;
+      for (size_t i = 0; i < ua[img].size(); ++i) union_join(root, ua[img][i], ub[img][i]);
+      for (size_t v = 0; v < n; ++v) {
+        size_t r = v;
+        while (root[r] != r) r = root[r];
+        root[v] = r;
+      }
+    }
+    std::vector<int32_t> lab(n, -1);
+    int32_t next = 0;
+    int32_t* out = labels + node_off[img];
+    for (size_t v = 0; v < n; ++v) {  // scipy connected_components: labels in order of first vertex
+      if (lab[root[v]] < 0) lab[root[v]] = next++;
+      out[v] = lab[root[v]];
+    }
+    n_comp[img] = next;
+  };
+  const int nt = std::max(1, std::min(n_threads, B));
+  if (nt == 1) {
+    for (int img = 0; img < B; ++img) run(img);
+  } else {
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nt; ++t)
+      pool.emplace_back([&, t] {
+        for (int img = t; img < B; img += nt) run(img);
+      });
+    for (auto& th : pool) th.join();
+  }
+  return PEMP_OK;
+}
+
+extern "C" int pemp_pose_persons(int B, const int64_t* node_off, const int32_t* labels, const int32_t* n_comp,
+                                 const int64_t* joint_det, const float* scores, const float* pose_scores,
+                                 const float* class_probs, int J, int allow_single, int64_t cap, double* persons,
+                                 int32_t* person_count, int32_t* mutants) {
+  PEMP_CHECK_ARG(B >= 1 && J >= 1 && cap >= 0 && node_off && labels && n_comp && joint_det && scores &&
+                     person_count && mutants && (cap == 0 || persons),
+                 "pemp_pose_persons: bad args");
+  int64_t out = 0;
+  for (int b = 0; b < B; ++b) {
+    const int64_t o = node_off[b], n = node_off[b + 1] - o;
+    std::vector<std::vector<int64_t>> members(n_comp[b]);
+    for (int64_t v = 0; v < n; ++v) {
+      const int32_t l = labels[o + v];
+      PEMP_CHECK_ARG(l >= 0 && l < n_comp[b], "pemp_pose_persons: label out of range");
+      members[l].push_back(o + v);
+    }
+    int32_t count = 0;
+    mutants[b] = 0;
+    for (const auto& m : members) {
+      if ((int64_t)m.size() > J) mutants[b] = 1;
+      auto type_of = [&](int64_t g) -> int64_t {
+        if (!class_probs) return joint_det[g * 3 + 2];
+        const float* c = class_probs + g * J;
+        int best = 0;
+        for (int j = 1; j < J; ++j)
+          if (c[j] > c[best]) best = j;  // np.argmax: first maximum
+        return best;
+      };
+      double kp[64 * 3];
+      PEMP_CHECK_ARG(J <= 64, "pemp_pose_persons: J > 64");
+      std::fill(kp, kp + J * 3, 0.0);
+      bool emit = false;
+      if (m.size() > 1) {
+        for (int t = 0; t < J; ++t) {
+          int64_t best = -1;
+          for (int64_t g : m)
+            if (type_of(g) == t && (best < 0 || scores[g] > scores[best])) best = g;
+          if (best < 0) continue;
+          kp[t * 3 + 0] = (double)joint_det[best * 3 + 0];
+          kp[t * 3 + 1] = (double)joint_det[best * 3 + 1];
+          kp[t * 3 + 2] = pose_scores ? (double)pose_scores[best] : (double)scores[best];
+        }
+        for (int t = 0; t < J; ++t) emit |= kp[t * 3 + 2] > 0.0;
+      } else if (m.size() == 1 && allow_single) {
+        const int64_t g = m[0];
+        if (scores[g] < 0.1f) continue;
+        const int64_t t = type_of(g);
+        for (int j = 0; j < J; ++j) {
+          kp[j * 3 + 0] = (double)joint_det[g * 3 + 0];
+          kp[j * 3 + 1] = (double)joint_det[g * 3 + 1];
+        }
+        kp[t * 3 + 2] = (double)scores[g];
+        emit = true;
+      }
+      if (!emit) continue;
+      if (out >= cap) {
+        ::pemp::set_error("pemp_pose_persons: more than cap = %lld persons", (long long)cap);
+        return PEMP_ERR_WORKSPACE;
+      }
+      std::copy(kp, kp + J * 3, persons + out * J * 3);
+      ++out;
+      ++count;
+    }
+    person_count[b] = count;
+  }
+  return PEMP_OK;
+}

@@ -1,0 +1,146 @@
+"""Pose grouping after the MPN: MPN edge/node/class probabilities -> persons.
+
+Mirrors, with the same argument meaning and return values:
+  * ``pred_to_person`` (``src/Utils/Utils.py:499-514``; ``cc_method`` "GAEC" or "threshold") with the
+    GAEC path of ``cluster_graph`` (``src/Utils/correlation_clustering/correlation_clustering_utils.py:21-64,
+    99-151, 187-245``) and ``graph_cluster_to_persons`` (``Utils.py:672-743``);
+  * ``pred_to_ann``'s grouping prefix (``Utils.py:1445-1459``: detector-score check, node threshold +
+    ``subgraph``, the ``None`` returns), batched over every image of a ``construct_graph`` batch:
+    ``group_persons``.
+
+Work split (include/pemp.h, ``pemp_pose_*``): the per-edge pass (subgraph test, reverse-edge lookup,
+transpose averaging) is one HIP kernel over the whole batch; its output and the node arrays come back in
+one stream-ordered copy into pinned memory; greedy additive edge contraction (sequential by nature) and the
+person assembly run in C++ in the same library, one image per host thread. No numpy / scipy / Python loop
+sits on the path. ``greedy``, ``MUT`` and ``KL`` are not built (NotImplementedError, as the reference
+raises for unknown methods).
+"""
+import os
+
+import numpy as np
+import torch
+
+from . import _lib
+
+_METHODS = {"GAEC": 0, "threshold": 1}
+
+
+def _method(cc_method):
+    if cc_method not in _METHODS:
+        raise NotImplementedError(f"cc_method={cc_method!r}: pemp_amd builds GAEC and threshold")
+    return _METHODS[cc_method]
+
+
+def _host_threads():
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def _to_host(tensors):
+    """Stream-ordered copies of device tensors into pinned host tensors, one synchronisation."""
+    out = []
+    for t in tensors:
+        if t is None:
+            out.append(None)
+            continue
+        h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        h.copy_(t, non_blocking=True)
+        out.append(h)
+    torch.cuda.current_stream().synchronize()
+    return out
+
+
+def _run(joint_det, joint_scores, edge_index, pred, node_off, th, use_th, class_pred, cc_method, num_joints,
+         score_for_poses=None, allow_single=False):
+    """Shared path. node_off: host int64 [B+1]. Returns (persons list, mutants, labels, counts, flags)."""
+    L = _lib.lib()
+    method = _method(cc_method)
+    dev = edge_index.device
+    if dev.type != "cuda":
+        raise ValueError("pemp_amd.pose: expects device tensors (the HIP path has no CPU fallback)")
+    B = len(node_off) - 1
+    N = int(node_off[-1])
+    if joint_det.shape != (N, 3) or joint_scores.shape != (N,):
+        raise ValueError(f"pemp_amd.pose: joint_det {tuple(joint_det.shape)} / joint_scores "
+                         f"{tuple(joint_scores.shape)} do not match {N} nodes")
+    ei = edge_index.to(torch.int64).contiguous()
+    E = ei.shape[1]
+    pr = pred.reshape(-1).to(torch.float32).contiguous()
+    if pr.numel() != E:
+        raise ValueError(f"pemp_amd.pose: pred has {pr.numel()} values for {E} edges")
+    sc = joint_scores.to(torch.float32).contiguous()
+    off_d = torch.from_numpy(node_off).to(dev)
+    w = torch.empty(E, dtype=torch.float32, device=dev)
+    flags = torch.empty(B + 1, dtype=torch.int32, device=dev)
+    _lib.check(L.pemp_pose_edge_weights(_lib.ptr(ei), E, _lib.ptr(pr), _lib.ptr(sc), float(th), int(use_th),
+                                        _lib.ptr(off_d), B, method, _lib.ptr(w), _lib.ptr(flags), _lib.stream(dev)))
+    cls = class_pred.to(torch.float32).contiguous() if class_pred is not None else None
+    if cls is not None and cls.shape != (N, num_joints):
+        raise ValueError(f"pemp_amd.pose: class_pred {tuple(cls.shape)} != ({N}, {num_joints})")
+    ps = score_for_poses.to(torch.float32).contiguous() if score_for_poses is not None else None
+    h_ei, h_w, h_flags, h_det, h_sc, h_cls, h_ps = _to_host(
+        [ei, w, flags, joint_det.to(torch.int64).contiguous(), sc, cls, ps])
+    labels = np.empty(N, dtype=np.int32)
+    n_comp = np.empty(B, dtype=np.int32)
+    _lib.check(L.pemp_pose_cluster(B, node_off.ctypes.data, h_ei.data_ptr(), E, h_w.data_ptr(),
+                                   h_flags.data_ptr(), method, _host_threads(), labels.ctypes.data,
+                                   n_comp.ctypes.data), L)
+    cap = max(N, 1)
+    persons = np.empty((cap, num_joints, 3), dtype=np.float64)
+    counts = np.empty(B, dtype=np.int32)
+    mutants = np.empty(B, dtype=np.int32)
+    _lib.check(L.pemp_pose_persons(B, node_off.ctypes.data, labels.ctypes.data, n_comp.ctypes.data,
+                                   h_det.data_ptr(), h_sc.data_ptr(), None if h_ps is None else h_ps.data_ptr(),
+                                   None if h_cls is None else h_cls.data_ptr(), num_joints, int(allow_single), cap,
+                                   persons.ctypes.data, counts.ctypes.data, mutants.ctypes.data), L)
+    starts = np.concatenate([[0], np.cumsum(counts)])
+    per_image = [persons[starts[b]:starts[b + 1]].copy() for b in range(B)]
+    return per_image, mutants.astype(bool), labels, h_flags.numpy()
+
+
+def pred_to_person(joint_det, joint_scores, edge_index, pred, class_pred, cc_method, num_joints,
+                   score_for_poses=None, allow_single_joint_persons=False):
+    """``Utils.py:499-514`` for one image's (already thresholded) graph.
+
+    Returns ``(persons, mutant_detected, person_labels)``: persons float64 ``[P, num_joints, 3]`` (x, y,
+    score), or an empty ``np.array([])`` when no person is formed, as ``np.array(persons)`` gives there;
+    person_labels int32 ``[N]`` component ids in scipy ``connected_components`` order."""
+    node_off = np.array([0, joint_det.shape[0]], dtype=np.int64)
+    per_image, mutants, labels, _ = _run(joint_det, joint_scores, edge_index, pred, node_off, 0.0, False,
+                                         class_pred, cc_method, num_joints, score_for_poses,
+                                         allow_single_joint_persons)
+    persons = per_image[0] if len(per_image[0]) else np.array([])
+    return persons, bool(mutants[0]), labels
+
+
+def group_persons(joint_det, joint_scores, edge_index, pred, th, class_pred=None, cc_method="GAEC",
+                  num_joints=17, batch_index=None, score_map_scores=None):
+    """``pred_to_ann``'s grouping prefix (``Utils.py:1447-1459``) for every image of a batch.
+
+    joint_det [ΣN,3] int64, joint_scores [ΣN] (the node probabilities, ``preds_nodes`` in ``valid.py:109``),
+    edge_index [2,ΣE] int64 sorted by (src, dst) (``construct_graph``'s output), pred [ΣE] edge
+    probabilities, class_pred [ΣN,J] class probabilities or None, batch_index [ΣN] int64 (None: one image),
+    score_map_scores [ΣN] detector scores (None: skip that check). Returns one entry per image: persons
+    float64 [P, J, 3], or None where ``pred_to_ann`` returns None (no detector score > 0.1, no edge
+    surviving the node threshold, no person)."""
+    N = joint_det.shape[0]
+    if batch_index is None:
+        node_off = np.array([0, N], dtype=np.int64)
+    else:
+        bi = batch_index.cpu().numpy()
+        if len(bi) and np.any(bi[1:] < bi[:-1]):
+            raise ValueError("pemp_amd.pose: batch_index must be non-decreasing (construct_graph order)")
+        B = int(bi[-1]) + 1 if len(bi) else 1
+        node_off = np.searchsorted(bi, np.arange(B + 1)).astype(np.int64)
+    per_image, _, _, flags = _run(joint_det, joint_scores, edge_index, pred, node_off, th, True, class_pred,
+                                  cc_method, num_joints)
+    ok_det = None
+    if score_map_scores is not None:
+        s = (score_map_scores > 0.1).cpu().numpy()
+        ok_det = np.array([s[node_off[b]:node_off[b + 1]].any() for b in range(len(node_off) - 1)])
+    out = []
+    for b, persons in enumerate(per_image):
+        if (ok_det is not None and not ok_det[b]) or not (flags[b] & 2) or len(persons) == 0:
+            out.append(None)
+        else:
+            out.append(persons)
+    return out

@@ -1,0 +1,135 @@
+"""GPU parity of pose grouping: pemp_amd.pose (HIP edge pass + native GAEC and person
+assembly) against the golden vectors made by the reference's own functions and against the oracle on the
+same inputs. Bit-exact: persons are integer positions and copied fp32 scores; labels are integers."""
+import numpy as np
+import pytest
+import torch
+
+import pemp_amd
+from oracle import pose as opose, restate
+from pemp_amd import _lib, config as pcfg, pose as ppose, synthetic as syn
+from tests.test_pose_cpu import CASES, edge_pass, load
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_group_persons_golden(name):
+    g = load(name)
+    cls = dev(g["class_probs"]) if g["has_class"] else None
+    out = ppose.group_persons(dev(g["joint_det"]), dev(g["joint_scores"]), dev(g["edge_index"]), dev(g["pred"]),
+                              float(g["th"]), cls, str(g["method"]), int(g["num_joints"]),
+                              score_map_scores=dev(g["joint_scores"]))
+    assert len(out) == 1
+    if g["none"]:
+        assert out[0] is None
+    else:
+        np.testing.assert_array_equal(out[0], g["persons"])
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_pred_to_person_golden(name):
+    g = load(name)
+    J = int(g["num_joints"])
+    cls = dev(g["class_probs"]) if g["has_class"] else None
+    ei_s, p_s = opose.subgraph(g["joint_scores"] > g["th"], g["edge_index"], g["pred"])
+    persons, mutant, labels = ppose.pred_to_person(dev(g["joint_det"]), dev(g["joint_scores"]), dev(ei_s), dev(p_s),
+                                                   cls, "GAEC", J, score_for_poses=dev(g["pose_scores"]),
+                                                   allow_single_joint_persons=True)
+    np.testing.assert_array_equal(np.asarray(persons).reshape(-1, J, 3), g["single_persons"])
+    np.testing.assert_array_equal(labels, g["single_labels"])
+    assert mutant == bool(g["single_mutant"])
+
+
+@pytest.mark.parametrize("method", [0, 1])
+def test_edge_pass_kernel_bits(method):
+    """pemp_pose_edge_weights == its numpy statement, bit for bit (NaN positions included), on a batch of
+    three fixture graphs; flags per image."""
+    gs = [load(n) for n in CASES[:3]]
+    eis, prs, scs, offs = [], [], [], [0]
+    for g in gs:
+        eis.append(g["edge_index"] + offs[-1])
+        prs.append(g["pred"])
+        scs.append(g["joint_scores"])
+        offs.append(offs[-1] + len(g["joint_det"]))
+    ei, pr, sc, off = np.concatenate(eis, 1), np.concatenate(prs), np.concatenate(scs), np.array(offs, np.int64)
+    E, B = ei.shape[1], len(gs)
+    w = torch.empty(E, dtype=torch.float32, device=DEV)
+    flags = torch.empty(B + 1, dtype=torch.int32, device=DEV)
+    L = _lib.lib()
+    d_ei, d_pr, d_sc, d_off = dev(ei), dev(pr), dev(sc), dev(off)
+    _lib.check(L.pemp_pose_edge_weights(d_ei.data_ptr(), E, d_pr.data_ptr(), d_sc.data_ptr(), 0.3, 1,
+                                        d_off.data_ptr(), B, method, w.data_ptr(), flags.data_ptr(), _lib.stream(DEV)))
+    ref_w, ref_flags = edge_pass(ei, pr, sc, np.float32(0.3), True, off, method)
+    np.testing.assert_array_equal(w.cpu().numpy().view(np.int32), ref_w.view(np.int32))
+    np.testing.assert_array_equal(flags.cpu().numpy(), ref_flags)
+    # an unsorted edge list is flagged and refused by the grouping
+    bad = ei[:, ::-1].copy()
+    with pytest.raises(ValueError, match="sorted"):
+        ppose.group_persons(dev(np.zeros((off[-1], 3), np.int64)), dev(sc), dev(bad), dev(pr), 0.3,
+                            batch_index=dev(np.repeat(np.arange(B), np.diff(off))))
+
+
+def test_group_persons_batched():
+    gs = [load(n) for n in CASES if str(load(n)["method"]) == "GAEC" and int(load(n)["num_joints"]) == 17]
+    dets, scs, eis, prs, clss, bis = [], [], [], [], [], []
+    base = 0
+    for b, g in enumerate(gs):
+        n = len(g["joint_det"])
+        dets.append(g["joint_det"])
+        scs.append(g["joint_scores"])
+        eis.append(g["edge_index"] + base)
+        prs.append(g["pred"])
+        clss.append(g["class_probs"] if g["has_class"] else np.eye(17, dtype=np.float32)[g["joint_det"][:, 2]])
+        bis.append(np.full(n, b, np.int64))
+        base += n
+    out = ppose.group_persons(dev(np.concatenate(dets)), dev(np.concatenate(scs)), dev(np.concatenate(eis, 1)),
+                              dev(np.concatenate(prs)), 0.1, dev(np.concatenate(clss)), "GAEC", 17,
+                              batch_index=dev(np.concatenate(bis)))
+    assert len(out) == len(gs)
+    for b, g in enumerate(gs):
+        cls = g["class_probs"] if g["has_class"] else np.eye(17, dtype=np.float32)[g["joint_det"][:, 2]]
+        ref = opose.pred_to_ann_persons(g["joint_det"], g["joint_scores"], g["edge_index"], g["pred"],
+                                        np.float32(0.1), cls, "GAEC", 17)
+        if ref is None:
+            assert out[b] is None
+        else:
+            np.testing.assert_array_equal(out[b], ref)
+
+
+@pytest.mark.parametrize("method", ["GAEC", "threshold"])
+def test_end_to_end_after_mpn(method):
+    """construct_graph -> MPN -> sigmoid/softmax (valid.py:109-111) -> group_persons on the GPU, against
+    the oracle's pred_to_ann prefix on the SAME probabilities (copied to the host)."""
+    B, J, H, W = 2, 17, 128, 128
+    hm = torch.from_numpy(syn.make_heatmaps(5, B, J, H, W, persons=3))
+    feats = torch.from_numpy(syn.closed_form((B, 128, H, W), 0.25))
+    gc = pcfg.inference_gc_config("fully", 5, False)
+    out = pemp_amd.get_graph_constructor(gc, scoremaps=hm.to(DEV), features=feats.to(DEV), tagmaps=None,
+                                         joints_gt=None, factor_list=None, masks=None, device=DEV, testing=True,
+                                         heatmaps=None, num_joints=J).construct_graph()
+    x, ea, ei, det, sc, bi = out[0], out[1], out[2], out[7], out[11], out[12]
+    mcfg = pcfg.published_mpn_config(J, steps=3, variant="attn")
+    model = pemp_amd.get_mpn_model(mcfg)
+    model.load_state_dict(syn.closed_form_state_dict(model, 0.5))
+    model.eval().to(DEV)
+    with torch.no_grad():
+        pe, pn, pc, _ = model(x, ea, ei, node_types=det[:, 2])
+    pe, pn, pc = pe[-1].sigmoid().squeeze(), pn[-1].sigmoid(), pc[-1].softmax(dim=1)
+    got = ppose.group_persons(det, pn, ei, pe, 0.1, pc, method, J, batch_index=bi, score_map_scores=sc)
+    h = [t.cpu().numpy() for t in (det, pn, ei, pe, pc, bi, sc)]
+    for b in range(B):
+        nm = h[5] == b
+        lo = int(np.nonzero(nm)[0][0])
+        em = nm[h[2][0]]
+        ref = opose.pred_to_ann_persons(h[0][nm], h[1][nm], h[2][:, em] - lo, h[3][em], np.float32(0.1), h[4][nm],
+                                        method, J, h[6][nm])
+        if ref is None:
+            assert got[b] is None
+        else:
+            np.testing.assert_array_equal(got[b], ref)

@@ -1,0 +1,171 @@
+"""Pose grouping, CPU side.
+
+* the oracle (oracle/pose.py) against the golden vectors made by the reference's own functions;
+* the library's HOST entry points (pemp_pose_cluster: GAEC / threshold components; pemp_pose_persons:
+  graph_cluster_to_persons) against the oracle and the golden vectors. These two are plain C++ (no HIP
+  call), so they run here; the GPU edge pass that feeds them is restated below in numpy as test input
+  only and is checked against the real kernel by tests/test_gpu_pose.py.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from oracle import pose as opose
+from pemp_amd import _lib
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CASES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.startswith("pose_") and f.endswith(".npz"))
+
+
+def load(name):
+    z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+    return {k: z[k] for k in z.files}
+
+
+def edge_pass(ei, pred, scores, th, use_th, node_off, method):
+    """numpy statement of pemp_pose_edge_weights (test input only)."""
+    E = ei.shape[1]
+    B = len(node_off) - 1
+    w = np.full(E, np.nan, np.float32)
+    flags = np.zeros(B + 1, np.int32)
+    keep = np.ones(E, bool) if not use_th else (scores[ei[0]] > th) & (scores[ei[1]] > th)
+    img = np.searchsorted(node_off, ei[0], side="right") - 1
+    pos = {(int(s), int(d)): i for i, (s, d) in enumerate(ei.T)}
+    for e in np.nonzero(keep)[0]:
+        s, d = int(ei[0, e]), int(ei[1, e])
+        flags[img[e]] |= 2
+        if s > d and pred[e] != 0:
+            flags[img[e]] |= 1
+        if method == 1:
+            w[e] = pred[e]
+        elif s < d:
+            r = pos.get((d, s))
+            w[e] = np.float32(pred[e] + (pred[r] if r is not None else np.float32(0)))
+    return w, flags
+
+
+def host_group(det, scores, ei, pred, cls, J, node_off, th, use_th, method, pose_scores=None, allow_single=False):
+    L = _lib.load_cdll()
+    w, flags = edge_pass(ei, pred, scores, th, use_th, node_off, method)
+    B, N = len(node_off) - 1, len(det)
+    labels = np.empty(N, np.int32)
+    ncomp = np.empty(B, np.int32)
+    ei = np.ascontiguousarray(ei, np.int64)
+    rc = L.pemp_pose_cluster(B, node_off.ctypes.data, ei.ctypes.data, ei.shape[1], w.ctypes.data, flags.ctypes.data,
+                             method, 4, labels.ctypes.data, ncomp.ctypes.data)
+    _lib.check(rc, L)
+    cap = max(N, 1)
+    persons = np.empty((cap, J, 3))
+    counts = np.empty(B, np.int32)
+    mut = np.empty(B, np.int32)
+    det = np.ascontiguousarray(det, np.int64)
+    scores = np.ascontiguousarray(scores, np.float32)
+    cls_p = None if cls is None else np.ascontiguousarray(cls, np.float32).ctypes.data
+    ps_p = None if pose_scores is None else np.ascontiguousarray(pose_scores, np.float32).ctypes.data
+    rc = L.pemp_pose_persons(B, node_off.ctypes.data, labels.ctypes.data, ncomp.ctypes.data, det.ctypes.data,
+                             scores.ctypes.data, ps_p, cls_p, J, int(allow_single), cap, persons.ctypes.data,
+                             counts.ctypes.data, mut.ctypes.data)
+    _lib.check(rc, L)
+    st = np.concatenate([[0], np.cumsum(counts)])
+    return [persons[st[b]:st[b + 1]] for b in range(B)], labels, flags, mut
+
+
+def method_of(g):
+    return {"GAEC": 0, "threshold": 1}[str(g["method"])]
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_oracle_matches_reference_fixture(name):
+    g = load(name)
+    cls = g["class_probs"] if g["has_class"] else None
+    got = opose.pred_to_ann_persons(g["joint_det"], g["joint_scores"], g["edge_index"], g["pred"], g["th"], cls,
+                                    str(g["method"]), int(g["num_joints"]), g["joint_scores"])
+    assert (got is None) == bool(g["none"])
+    if got is not None:
+        np.testing.assert_array_equal(got, g["persons"])
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_host_grouping_matches_reference_fixture(name):
+    g = load(name)
+    J = int(g["num_joints"])
+    cls = g["class_probs"] if g["has_class"] else None
+    N = len(g["joint_det"])
+    off = np.array([0, N], np.int64)
+    persons, _, flags, _ = host_group(g["joint_det"], g["joint_scores"], g["edge_index"], g["pred"], cls, J, off,
+                                      float(g["th"]), True, method_of(g))
+    if g["none"]:
+        assert not (flags[0] & 2) or len(persons[0]) == 0
+    else:
+        np.testing.assert_array_equal(persons[0], g["persons"])
+    # graph_cluster_to_persons with single-joint persons and pose scores, on the unthresholded graph's
+    # GAEC solution restricted to the thresholded subgraph (as the generator built it)
+    ei_s, p_s = opose.subgraph(g["joint_scores"] > g["th"], g["edge_index"], g["pred"])
+    persons, labels, _, mut = host_group(g["joint_det"], g["joint_scores"], ei_s, p_s, cls, J, off, 0.0, False, 0,
+                                         pose_scores=g["pose_scores"], allow_single=True)
+    np.testing.assert_array_equal(persons[0].reshape(-1, J, 3), g["single_persons"])
+    np.testing.assert_array_equal(labels, g["single_labels"])
+    assert bool(mut[0]) == bool(g["single_mutant"])
+
+
+def test_host_grouping_batched_equals_per_image():
+    gs = [load(n) for n in CASES if str(load(n)["method"]) == "GAEC" and int(load(n)["num_joints"]) == 17]
+    dets, scs, eis, prs, clss, offs = [], [], [], [], [], [0]
+    for g in gs:
+        n = len(g["joint_det"])
+        dets.append(g["joint_det"])
+        scs.append(g["joint_scores"])
+        eis.append(g["edge_index"] + offs[-1])
+        prs.append(g["pred"])
+        clss.append(g["class_probs"] if g["has_class"] else np.eye(17, dtype=np.float32)[g["joint_det"][:, 2]])
+        offs.append(offs[-1] + n)
+    off = np.array(offs, np.int64)
+    persons, _, _, _ = host_group(np.concatenate(dets), np.concatenate(scs), np.concatenate(eis, 1),
+                                  np.concatenate(prs), np.concatenate(clss), 17, off, 0.1, True, 0)
+    for b, g in enumerate(gs):
+        cls = g["class_probs"] if g["has_class"] else np.eye(17, dtype=np.float32)[g["joint_det"][:, 2]]
+        ref = opose.pred_to_ann_persons(g["joint_det"], g["joint_scores"], g["edge_index"], g["pred"],
+                                        np.float32(0.1), cls, "GAEC", 17)
+        np.testing.assert_array_equal(persons[b], ref if ref is not None else np.zeros((0, 17, 3)))
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_gaec_matches_oracle_random_with_ties(seed):
+    """C++ GAEC == the libstdc++-heap restatement, incl. weight ties (quantised weights) and repeated
+    contractions; labels compared exactly."""
+    rng = np.random.default_rng(100 + seed)
+    n = int(rng.integers(2, 70))
+    dens = rng.uniform(0.1, 1.0)
+    up = np.triu(rng.random((n, n)) < dens, 1)
+    s, d = np.nonzero(up | up.T)
+    ei = np.stack([s, d]).astype(np.int64)
+    q = [0, 4, 16][seed % 3]
+    pred = rng.random(ei.shape[1]).astype(np.float32)
+    if q:
+        pred = (np.round(pred * q) / q).astype(np.float32)
+    det = np.stack([rng.integers(0, 640, n), rng.integers(0, 640, n), rng.integers(0, 17, n)], 1)
+    scores = rng.random(n).astype(np.float32)
+    off = np.array([0, n], np.int64)
+    _, labels, _, _ = host_group(det, scores, ei, pred, None, 17, off, 0.0, False, 0)
+    if ei.shape[1]:
+        sol = opose.cluster_gaec(n, ei, pred)
+    else:
+        sol = np.eye(n, dtype=np.int64)
+    _, _, ref_labels = opose.graph_cluster_to_persons(det, scores, np.stack(np.nonzero(sol)), None, 17)
+    np.testing.assert_array_equal(labels, ref_labels)
+
+
+def test_unsorted_edge_index_is_refused():
+    L = _lib.load_cdll()
+    flags = np.array([2, 1], np.int32)   # image 0 keeps edges; flags[B] bit 0: unsorted
+    off = np.array([0, 3], np.int64)
+    ei = np.array([[0, 1], [1, 0]], np.int64)
+    w = np.zeros(2, np.float32)
+    labels = np.empty(3, np.int32)
+    nc = np.empty(1, np.int32)
+    rc = L.pemp_pose_cluster(1, off.ctypes.data, ei.ctypes.data, 2, w.ctypes.data, flags.ctypes.data, 0, 1,
+                             labels.ctypes.data, nc.ctypes.data)
+    with pytest.raises(ValueError, match="sorted"):
+        _lib.check(rc, L)
