@@ -223,6 +223,60 @@ def frontend_projection(wl, gc, model, hm, tags, dev, out):
             "dense_bytes_written": B * 128 * H * W * 4, "nodes": int(out[0].shape[0])}
 
 
+def pose_grouping(wl, out, pe, pn, pc, cpu_ref):
+    """SURVEY 8f row 2, informational: the pred_to_ann grouping prefix (node threshold 0.1, GAEC,
+    graph_cluster_to_persons; Utils.py:1445-1459) for the whole step's batch, after the MPN and the
+    sigmoid / softmax of valid.py:109-111. GPU edge pass + native host GAEC (pemp_amd.pose), against
+    the oracle restatement (oracle/pose.py, numpy + pure-Python GAEC, one image at a time, 1 core)."""
+    from pemp_amd import pose as ppose
+    det, sc, ei, bi = out[7], out[11], out[2], out[12]
+    # The closed-form MPN weights give unstructured probabilities (no person would form), so the grouping
+    # input is synthetic and person-structured like a trained network's output: node i of an image
+    # belongs to person (local index mod persons_per_image); edge probabilities sigmoid(+-2.5 + N(0, 1.5))
+    # for same / different persons, drawn per direction; node probabilities sigmoid(2 + N(0, 1)); class
+    # probabilities are the MPN's own softmax.
+    N, E = det.shape[0], ei.shape[1]
+    node_off = torch.searchsorted(bi, torch.arange(wl["B"] + 1, device=bi.device))
+    pid = (torch.arange(N, device=bi.device) - node_off[bi]) % wl["persons"]
+    gen = torch.Generator(device=bi.device).manual_seed(7)
+    with torch.no_grad():
+        same = pid[ei[0]] == pid[ei[1]]
+        pe_p = torch.sigmoid(torch.where(same, 2.5, -2.5) + 1.5 * torch.randn(E, generator=gen, device=bi.device))
+        pn_p = torch.sigmoid(2.0 + torch.randn(N, generator=gen, device=bi.device))
+        pc_p = pc[-1].softmax(dim=1)
+    args = (det, pn_p, ei, pe_p, 0.1, pc_p, "GAEC", wl["J"])
+    ppose.group_persons(*args, batch_index=bi, score_map_scores=sc)
+    reps = 5
+    torch.cuda.synchronize()
+    _lib.prof_enable("pose_edge_weights")
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        res = ppose.group_persons(*args, batch_index=bi, score_map_scores=sc)
+    gpu_ms = (time.perf_counter() - t0) / reps * 1e3
+    st = _lib.prof_report()
+    _lib.prof_enable(None)
+    tm = {}
+    for _ in range(reps):
+        ppose.group_persons(*args, batch_index=bi, score_map_scores=sc, _timings=tm)
+    n, ms = st.get("pose_edge_weights", (1, float("nan")))
+    rec = {"ms_per_batch": round(gpu_ms, 3), "edge_pass_us": round(ms / n * 1e3, 2),
+           "stage_ms": {k: round(v / reps * 1e3, 3) for k, v in tm.items()},
+           "persons": int(sum(0 if r is None else len(r) for r in res)), "images": wl["B"],
+           "method": "GAEC", "node_threshold": 0.1}
+    if cpu_ref:
+        from oracle import pose as opose
+        h = [t.cpu().numpy() for t in (det, pn_p, ei, pe_p, pc_p, bi, sc)]
+        t0 = time.perf_counter()
+        for b in range(wl["B"]):
+            nm = h[5] == b
+            lo = int(np.nonzero(nm)[0][0])
+            em = nm[h[2][0]]
+            opose.pred_to_ann_persons(h[0][nm], h[1][nm], h[2][:, em] - lo, h[3][em], np.float32(0.1), h[4][nm],
+                                      "GAEC", wl["J"], h[6][nm])
+        rec["cpu_oracle_ms_per_batch"] = round((time.perf_counter() - t0) * 1e3, 1)
+    return rec
+
+
 def main():
     args = parse()
     rank, world, dev = setup_dist(args.gpus)
@@ -295,6 +349,9 @@ def main():
 
     front = frontend_projection(wl, gc, model, hm, tags, dev, out) if not args.no_roofline else None
 
+    grouping = pose_grouping(wl, out, pe, pn, pc, rank == 0 and world == 1 and not args.no_cpu_baseline) \
+        if not args.no_roofline else None
+
     upd = wl["variant"] in ("attn", "mean")      # update block pre-applied in the edge pass (mpn.hip UPD)
     roof = roofline_for(dominant, stats_timed, E, wl, model.precision, upd) if dominant else None
     cpu = None
@@ -322,6 +379,7 @@ def main():
             "kernel_avg_us": breakdown if not args.no_roofline else None,
             "cpu_baseline": cpu,
             "frontend_projection": front,
+            "pose_grouping": grouping,
         }
         if cpu:
             rec["speedup_vs_cpu"] = round(value / cpu["value"], 1)

@@ -20,6 +20,7 @@
 // heap does), per-vertex std::map adjacency, contraction of the endpoint with fewer neighbours into the
 // other, stale entries skipped by edition, stop at the first entry with w < 0.
 #include <math.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <map>
@@ -52,19 +53,30 @@ __global__ __launch_bounds__(256) void pose_edge_weights_kernel(const int64_t* _
                                                                 int use_th, const int64_t* __restrict__ node_off,
                                                                 int B, int mode, float* __restrict__ w,
                                                                 int* __restrict__ flags) {
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t s = ei[e], d = ei[E + e];
-    if (e + 1 < E) {
+  for (int64_t e0 = (int64_t)blockIdx.x * blockDim.x; e0 < E; e0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = e0 + threadIdx.x;
+    const bool live = e < E;
+    const int64_t s = live ? ei[e] : ei[E - 1], d = live ? ei[E + e] : ei[2 * E - 1];
+    if (live && e + 1 < E) {
       const int64_t s1 = ei[e + 1], d1 = ei[E + e + 1];
       if (s1 < s || (s1 == s && d1 <= d)) atomicOr(&flags[B], 1);
     }
-    const bool keep = !use_th || (score[s] > th && score[d] > th);
+    const bool keep = live && (!use_th || (score[s] > th && score[d] > th));
+    const int b = pose_find_image(node_off, B, s);
+    const float p = live ? pred[e] : 0.f;
+    // per-image flag bits, OR-reduced over the wave first (a wave's edges nearly always share an image):
+    // one atomic per wave instead of one per edge
+    const int bits = keep ? (2 | ((s > d && p != 0.f) ? 1 : 0)) : 0;
+    const int b0 = __shfl(b, 0);
+    if (__all(b == b0)) {
+      int r = bits;
+      for (int o = 32; o > 0; o >>= 1) r |= __shfl_xor(r, o);
+      if ((threadIdx.x & 63) == 0 && r) atomicOr(&flags[b0], r);
+    } else if (bits) {
+      atomicOr(&flags[b], bits);
+    }
     float out = __int_as_float(0x7fc00000);
     if (keep) {
-      const int b = pose_find_image(node_off, B, s);
-      const float p = pred[e];
-      if (s > d && p != 0.f && !(flags[b] & 1)) atomicOr(&flags[b], 1);
-      if (!(flags[b] & 2)) atomicOr(&flags[b], 2);
       if (mode == 1) {
         out = p;
       } else if (s < d) {
@@ -78,7 +90,7 @@ __global__ __launch_bounds__(256) void pose_edge_weights_kernel(const int64_t* _
         out = p + q;
       }
     }
-    w[e] = out;
+    if (live) w[e] = out;
   }
 }
 
@@ -137,6 +149,90 @@ void gaec(size_t n, const std::vector<size_t>& ea, const std::vector<size_t>& eb
     }
     for (const auto& p : adj[merge]) adj[p.first].erase(merge);
     adj[merge].clear();
+  }
+  root.resize(n);
+  for (size_t v = 0; v < n; ++v) root[v] = find(v);
+}
+
+// The same algorithm on dense n x n adjacency (weights, existence, edition counters, degrees): the
+// neighbours of a vertex are visited by a row scan in ascending vertex order, i.e. in std::map order, the
+// heap sees the identical push sequence, and every weight is the same sequence of double additions — so
+// the result is identical to gaec() above, ties included (tests compare both against the oracle).
+// 16-byte heap entry for the dense path (n <= 65535): the heap compares w only, so the entry layout does
+// not change the pop order.
+struct GaecEdge16 {
+  double w;
+  uint32_t edition;
+  uint16_t a, b;
+  GaecEdge16(size_t a_, size_t b_, double w_)
+      : w(w_), edition(0), a((uint16_t)(a_ < b_ ? a_ : b_)), b((uint16_t)(a_ < b_ ? b_ : a_)) {}
+  bool operator<(const GaecEdge16& o) const { return w < o.w; }
+};
+
+void gaec_dense(size_t n, const std::vector<size_t>& ea, const std::vector<size_t>& eb,
+                const std::vector<double>& ew, std::vector<size_t>& root) {
+  std::vector<double> wt(n * n, 0.0);
+  std::vector<uint32_t> ed(n * n, 0);
+  std::vector<uint8_t> ex(n * n, 0);
+  std::vector<uint32_t> deg(n, 0);
+  auto link = [&](size_t a, size_t b) {
+    if (!ex[a * n + b]) {
+      ex[a * n + b] = ex[b * n + a] = 1;
+      ++deg[a];
+      ++deg[b];
+    }
+  };
+  std::priority_queue<GaecEdge16> q;
+  for (size_t i = 0; i < ea.size(); ++i) {
+    link(ea[i], eb[i]);
+    wt[ea[i] * n + eb[i]] += ew[i];
+    wt[eb[i] * n + ea[i]] += ew[i];
+    GaecEdge16 e(ea[i], eb[i], ew[i]);
+    e.edition = ++ed[e.a * n + e.b];
+    q.push(e);
+  }
+  std::vector<size_t> parent(n), rank(n, 0);
+  for (size_t v = 0; v < n; ++v) parent[v] = v;
+  auto find = [&](size_t v) {
+    while (parent[v] != v) {
+      parent[v] = parent[parent[v]];
+      v = parent[v];
+    }
+    return v;
+  };
+  while (!q.empty()) {
+    const GaecEdge16 e = q.top();
+    q.pop();
+    if (!ex[e.a * n + e.b] || e.edition < ed[e.a * n + e.b]) continue;
+    if (e.w < 0.0) break;
+    size_t keep = e.a, merge = e.b;
+    if (deg[keep] < deg[merge]) std::swap(keep, merge);
+    {
+      size_t rk = find(keep), rm = find(merge);
+      if (rk != rm) {
+        if (rank[rk] < rank[rm]) std::swap(rk, rm);
+        parent[rm] = rk;
+        if (rank[rk] == rank[rm]) ++rank[rk];
+      }
+    }
+    const uint8_t* row = &ex[merge * n];
+    for (size_t p = 0; p < n; ++p) {
+      if (!row[p] || p == keep) continue;
+      const double pw = wt[merge * n + p];
+      link(keep, p);
+      wt[keep * n + p] += pw;
+      wt[p * n + keep] += pw;
+      GaecEdge16 ne(keep, p, wt[keep * n + p]);
+      ne.edition = ++ed[ne.a * n + ne.b];
+      q.push(ne);
+    }
+    for (size_t p = 0; p < n; ++p) {
+      if (!ex[merge * n + p]) continue;
+      ex[merge * n + p] = ex[p * n + merge] = 0;
+      wt[merge * n + p] = wt[p * n + merge] = 0.0;
+      --deg[p];
+    }
+    deg[merge] = 0;
   }
   root.resize(n);
   for (size_t v = 0; v < n; ++v) root[v] = find(v);
@@ -210,11 +306,15 @@ extern "C" int pemp_pose_cluster(int B, const int64_t* node_off, const int64_t* 
     ub[b].push_back((size_t)(d - node_off[b]));
     uw[b].push_back(weight);
   }
+  size_t dense_max = 2048;  // dense adjacency up to 2048 vertices (54 MB); PEMP_GAEC_DENSE_MAX overrides
+  if (const char* env = getenv("PEMP_GAEC_DENSE_MAX")) dense_max = (size_t)strtoull(env, nullptr, 10);
+  dense_max = std::min<size_t>(dense_max, 65535);
   auto run = [&](int img) {
     const size_t n = (size_t)(node_off[img + 1] - node_off[img]);
     std::vector<size_t> root;
     if (method == 0) {
-      gaec(n, ua[img], ub[img], uw[img], root);
+      if (n <= dense_max) gaec_dense(n, ua[img], ub[img], uw[img], root);
+      else gaec(n, ua[img], ub[img], uw[img], root);
     } else {
       root.resize(n);
       for (size_t v = 0; v < n; ++v) root[v] = v;

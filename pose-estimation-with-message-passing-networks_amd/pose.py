@@ -50,8 +50,11 @@ def _to_host(tensors):
 
 
 def _run(joint_det, joint_scores, edge_index, pred, node_off, th, use_th, class_pred, cc_method, num_joints,
-         score_for_poses=None, allow_single=False):
-    """Shared path. node_off: host int64 [B+1]. Returns (persons list, mutants, labels, counts, flags)."""
+         score_for_poses=None, allow_single=False, timings=None):
+    """Shared path. node_off: host int64 [B+1]. Returns (persons list, mutants, labels, flags).
+    timings: optional dict, filled with per-stage host wall times (s) -- measurement only."""
+    import time
+    t0 = time.perf_counter()
     L = _lib.lib()
     method = _method(cc_method)
     dev = edge_index.device
@@ -77,13 +80,26 @@ def _run(joint_det, joint_scores, edge_index, pred, node_off, th, use_th, class_
     if cls is not None and cls.shape != (N, num_joints):
         raise ValueError(f"pemp_amd.pose: class_pred {tuple(cls.shape)} != ({N}, {num_joints})")
     ps = score_for_poses.to(torch.float32).contiguous() if score_for_poses is not None else None
+    if timings is not None:
+        torch.cuda.current_stream().synchronize()
+        t1 = time.perf_counter()
+        timings["edge_pass"] = timings.get("edge_pass", 0.0) + t1 - t0
+        t0 = t1
     h_ei, h_w, h_flags, h_det, h_sc, h_cls, h_ps = _to_host(
         [ei, w, flags, joint_det.to(torch.int64).contiguous(), sc, cls, ps])
+    if timings is not None:
+        t1 = time.perf_counter()
+        timings["to_host"] = timings.get("to_host", 0.0) + t1 - t0
+        t0 = t1
     labels = np.empty(N, dtype=np.int32)
     n_comp = np.empty(B, dtype=np.int32)
     _lib.check(L.pemp_pose_cluster(B, node_off.ctypes.data, h_ei.data_ptr(), E, h_w.data_ptr(),
                                    h_flags.data_ptr(), method, _host_threads(), labels.ctypes.data,
                                    n_comp.ctypes.data), L)
+    if timings is not None:
+        t1 = time.perf_counter()
+        timings["cluster"] = timings.get("cluster", 0.0) + t1 - t0
+        t0 = t1
     cap = max(N, 1)
     persons = np.empty((cap, num_joints, 3), dtype=np.float64)
     counts = np.empty(B, dtype=np.int32)
@@ -92,6 +108,8 @@ def _run(joint_det, joint_scores, edge_index, pred, node_off, th, use_th, class_
                                    h_det.data_ptr(), h_sc.data_ptr(), None if h_ps is None else h_ps.data_ptr(),
                                    None if h_cls is None else h_cls.data_ptr(), num_joints, int(allow_single), cap,
                                    persons.ctypes.data, counts.ctypes.data, mutants.ctypes.data), L)
+    if timings is not None:
+        timings["persons"] = timings.get("persons", 0.0) + time.perf_counter() - t0
     starts = np.concatenate([[0], np.cumsum(counts)])
     per_image = [persons[starts[b]:starts[b + 1]].copy() for b in range(B)]
     return per_image, mutants.astype(bool), labels, h_flags.numpy()
@@ -113,7 +131,7 @@ def pred_to_person(joint_det, joint_scores, edge_index, pred, class_pred, cc_met
 
 
 def group_persons(joint_det, joint_scores, edge_index, pred, th, class_pred=None, cc_method="GAEC",
-                  num_joints=17, batch_index=None, score_map_scores=None):
+                  num_joints=17, batch_index=None, score_map_scores=None, _timings=None):
     """``pred_to_ann``'s grouping prefix (``Utils.py:1447-1459``) for every image of a batch.
 
     joint_det [ΣN,3] int64, joint_scores [ΣN] (the node probabilities, ``preds_nodes`` in ``valid.py:109``),
@@ -132,7 +150,7 @@ def group_persons(joint_det, joint_scores, edge_index, pred, th, class_pred=None
         B = int(bi[-1]) + 1 if len(bi) else 1
         node_off = np.searchsorted(bi, np.arange(B + 1)).astype(np.int64)
     per_image, _, _, flags = _run(joint_det, joint_scores, edge_index, pred, node_off, th, True, class_pred,
-                                  cc_method, num_joints)
+                                  cc_method, num_joints, timings=_timings)
     ok_det = None
     if score_map_scores is not None:
         s = (score_map_scores > 0.1).cpu().numpy()

@@ -131,12 +131,14 @@ def test_host_grouping_batched_equals_per_image():
         np.testing.assert_array_equal(persons[b], ref if ref is not None else np.zeros((0, 17, 3)))
 
 
+@pytest.mark.parametrize("dense", [True, False])
 @pytest.mark.parametrize("seed", range(12))
-def test_gaec_matches_oracle_random_with_ties(seed):
+def test_gaec_matches_oracle_random_with_ties(seed, dense, monkeypatch):
     """C++ GAEC == the libstdc++-heap restatement, incl. weight ties (quantised weights) and repeated
-    contractions; labels compared exactly."""
+    contractions; labels compared exactly. Both adjacency forms (dense rows and std::map)."""
+    monkeypatch.setenv("PEMP_GAEC_DENSE_MAX", "4096" if dense else "0")
     rng = np.random.default_rng(100 + seed)
-    n = int(rng.integers(2, 70))
+    n = int(rng.integers(2, 70)) if seed < 10 else 220
     dens = rng.uniform(0.1, 1.0)
     up = np.triu(rng.random((n, n)) < dens, 1)
     s, d = np.nonzero(up | up.T)
