@@ -166,7 +166,57 @@ CASES = {
 THRESHOLDS = {"pose_gaec_noclass": 0.5, "pose_gaec_many": 0.2}
 
 
+def make_refine_case(seed, J, H, W, F, P, quant=0):
+    """Scoremaps with person peaks over noise, tag maps that are piecewise per person plus noise, and
+    keypoints [P, J, 3] with some joints detected (integer x, y inside the map, score > 0)."""
+    rng = np.random.default_rng(seed)
+    s = (rng.random((J, H, W)) * 0.2).astype(np.float32)
+    tag = rng.normal(0, 0.3, size=(J, H, W, F)).astype(np.float32)
+    kp = np.zeros((P, J, 3))
+    for p in range(P):
+        cx, cy = rng.integers(8, W - 8), rng.integers(8, H - 8)
+        tv = rng.normal(p * 1.7, 0.2, size=F)
+        nd = rng.integers(2, J + 1)
+        for i in rng.choice(J, size=nd, replace=False):
+            x, y = int(np.clip(cx + rng.integers(-6, 7), 0, W - 1)), int(np.clip(cy + rng.integers(-6, 7), 0, H - 1))
+            s[i, y, x] = np.float32(0.5 + 0.5 * rng.random())
+            tag[i, max(0, y - 3):y + 4, max(0, x - 3):x + 4] = (tv + rng.normal(0, 0.05, size=F)).astype(np.float32)
+            kp[p, i] = (x, y, 0.2 + 0.8 * rng.random())
+        for i in range(J):  # undetected joints: a peak somewhere in the person's tag region
+            if kp[p, i, 2] == 0:
+                x, y = int(np.clip(cx + rng.integers(-8, 9), 0, W - 1)), int(np.clip(cy + rng.integers(-8, 9), 0, H - 1))
+                s[i, y, x] = np.float32(0.3 + 0.5 * rng.random())
+                tag[i, max(0, y - 2):y + 3, max(0, x - 2):x + 3] = tv.astype(np.float32)
+    if quant:
+        s = (np.round(s * quant) / quant).astype(np.float32)
+    return s, tag, kp
+
+
+REFINE_CASES = {
+    "pose_refine_f1": dict(seed=11, J=17, H=96, W=112, F=1, P=5),
+    "pose_refine_f2": dict(seed=12, J=17, H=80, W=80, F=2, P=9),
+    "pose_refine_ties_j14": dict(seed=13, J=14, H=64, W=72, F=1, P=12, quant=16),
+}
+
+
+def main_refine():
+    npc = _np_compat()
+    ns = _extract(os.path.join(REF_SRC, "Utils", "Utils.py"), ["refine", "adjust"], {"np": npc})
+    for name, spec in REFINE_CASES.items():
+        s, tag, kp = make_refine_case(**spec)
+        tg = tag[..., 0] if spec["F"] == 1 and spec["seed"] % 2 else tag   # also the 3-D tag form
+        filled = opose.fill_mean(kp.copy())
+        refined = ns["refine"](s, tg, filled.copy())
+        adjusted = ns["adjust"](refined.copy(), s)
+        assert np.array_equal(refined, opose.refine(s, tg, filled.copy())), name
+        assert np.array_equal(adjusted, opose.adjust(refined.copy(), s)), name
+        np.savez_compressed(os.path.join(OUT, name + ".npz"), scoremaps=s, tag=tg, keypoints=kp, filled=filled,
+                            refined=refined, adjusted=adjusted)
+        print(f"{name}: P={len(kp)} added={(refined[:, :, 2] == 0.001).sum()}")
+
+
 def main():
+    main_refine()
     ref = load_reference_pose()
     for name, spec in CASES.items():
         spec = dict(spec)

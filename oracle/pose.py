@@ -201,3 +201,58 @@ def pred_to_ann_persons(joint_det, joint_scores, edge_index, pred, th, class_pre
     if len(persons.shape) == 1:
         return None
     return persons
+
+
+# ----------------------------------------------------------------------------------------
+# Finishing: fill_mean (Utils.py:1468-1470), refine (:1026-1104), adjust (:917-936)
+# ----------------------------------------------------------------------------------------
+def fill_mean(persons):
+    for i in range(len(persons)):
+        persons[i, persons[i, :, 2] == 0, :2] = persons[i, persons[i, :, 2] != 0, :2].mean(axis=0)
+    return persons
+
+
+def refine(scoremaps, tag, keypoints):
+    if len(tag.shape) == 3:
+        tag = tag[:, :, :, None]
+    tags = []
+    for p in range(keypoints.shape[0]):
+        pt = []
+        for i in range(keypoints.shape[1]):
+            if keypoints[p, i, 2] > 0:
+                x, y = keypoints[p, i][:2].astype(np.int32)
+                pt.append(tag[i, y, x])
+        tags.append(np.array(pt))
+    for p in range(keypoints.shape[0]):
+        prev = np.mean(tags[p], axis=0)
+        ans = []
+        for i in range(keypoints.shape[1]):
+            tmp = scoremaps[i]
+            tt = (((tag[i] - prev[None, None, :]) ** 2).sum(axis=2) ** 0.5)
+            y, x = np.unravel_index(np.argmax(tmp - np.round(tt)), tmp.shape)
+            val = tmp[y, x]
+            xx, yy = x, y
+            x, y = x + 0.5, y + 0.5
+            x += 0.25 if tmp[yy, min(xx + 1, tmp.shape[1] - 1)] > tmp[yy, max(xx - 1, 0)] else -0.25
+            y += 0.25 if tmp[min(yy + 1, tmp.shape[0] - 1), xx] > tmp[max(0, yy - 1), xx] else -0.25
+            ans.append((x, y, val))
+        ans = np.array(ans)
+        for i in range(scoremaps.shape[0]):
+            if ans[i, 2] > 0 and keypoints[p, i, 2] == 0:
+                keypoints[p, i, :2] = ans[i, :2]
+                keypoints[p, i, 2] = 0.001
+    return keypoints
+
+
+def adjust(ans, det):
+    for pid, person in enumerate(ans):
+        for jid, joint in enumerate(person):
+            if joint[2] > 0:
+                y, x = joint[0], joint[1]
+                xx, yy = int(x), int(y)
+                tmp = det[jid]
+                y += 0.25 if tmp[xx, min(yy + 1, tmp.shape[1] - 1)] > tmp[xx, max(yy - 1, 0)] else -0.25
+                x += 0.25 if tmp[min(xx + 1, tmp.shape[0] - 1), yy] > tmp[max(0, xx - 1), yy] else -0.25
+                ans[pid, jid, 1] = x + 0.5
+                ans[pid, jid, 0] = y + 0.5
+    return ans

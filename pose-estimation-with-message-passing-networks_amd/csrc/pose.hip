@@ -415,3 +415,214 @@ extern "C" int pemp_pose_persons(int B, const int64_t* node_off, const int32_t* 
   }
   return PEMP_OK;
 }
+
+// ------------------------------------------------------------------------------------------------
+// refine (Utils.py:1026-1104) and adjust (Utils.py:917-936)
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+constexpr int REFINE_PC = 8;  // persons per thread (grid.z covers the rest)
+
+// numpy's float32 add.reduce of k values: pairwise_sum for a contiguous run (F = 1: n < 8 sequential,
+// else 8 strided partial sums combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) plus the tail); for F = 2 the
+// reduction axis is the outer one and numpy adds row by row (sequential).
+__device__ float np_sum_f32(const float* v, int n, bool pairwise) {
+  if (!pairwise || n < 8) {
+    float r = 0.f;
+    for (int i = 0; i < n; ++i) r += v[i];
+    return r;
+  }
+  float r[8];
+  for (int j = 0; j < 8; ++j) r[j] = v[j];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8)
+    for (int j = 0; j < 8; ++j) r[j] += v[i + j];
+  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res += v[i];
+  return res;
+}
+
+// prev_tag[p] = np.mean(tags at the detected joints of person p, axis=0) (float32)
+__global__ void refine_mean_tag_kernel(const double* __restrict__ kp, int P, int J, const float* __restrict__ tag,
+                                       int H, int W, int F, float* __restrict__ mean_tag) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  float vals[2][64];
+  int k = 0;
+  for (int i = 0; i < J; ++i) {
+    const double* q = kp + ((size_t)p * J + i) * 3;
+    if (!(q[2] > 0.0)) continue;
+    const int x = (int)q[0], y = (int)q[1];  // astype(np.int32): truncation
+    for (int f = 0; f < F; ++f) vals[f][k] = tag[(((size_t)i * H + y) * W + x) * F + f];
+    ++k;
+  }
+  for (int f = 0; f < F; ++f) mean_tag[p * F + f] = np_sum_f32(vals[f], k, F == 1) / (float)k;
+}
+
+__device__ __forceinline__ unsigned long long refine_key(float v, uint32_t idx) {
+  const uint32_t u = __float_as_uint(v);
+  const uint32_t o = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ((unsigned long long)o << 32) | (0xFFFFFFFFu - idx);  // max: larger v, then lower flat index
+}
+
+// keys[p][i] = max over pixels of key(s - rint(||tag - prev_tag[p]||), pixel): np.argmax(tmp2), first max.
+// grid: (pixel blocks, J, person chunks of REFINE_PC); each pixel is read once per chunk.
+__global__ __launch_bounds__(256) void refine_argmax_kernel(const float* __restrict__ s, const float* __restrict__ tag,
+                                                            int H, int W, int F, const float* __restrict__ mean_tag,
+                                                            int P, unsigned long long* __restrict__ keys, int J) {
+  const int i = blockIdx.y;
+  const int p0 = blockIdx.z * REFINE_PC;
+  const int np_ = min(REFINE_PC, P - p0);
+  float mt[REFINE_PC][2];
+  for (int q = 0; q < REFINE_PC; ++q)
+    for (int f = 0; f < 2; ++f) mt[q][f] = (q < np_ && f < F) ? mean_tag[(p0 + q) * F + f] : 0.f;
+  unsigned long long best[REFINE_PC];
+  for (int q = 0; q < REFINE_PC; ++q) best[q] = 0ull;
+  const size_t HW = (size_t)H * W;
+  const float* sp = s + (size_t)i * HW;
+  const float* tp = tag + (size_t)i * HW * F;
+  for (size_t px = (size_t)blockIdx.x * blockDim.x + threadIdx.x; px < HW; px += (size_t)gridDim.x * blockDim.x) {
+    const float sv = sp[px];
+    const float t0 = tp[px * F], t1 = F == 2 ? tp[px * F + 1] : 0.f;
+    for (int q = 0; q < REFINE_PC; ++q) {
+      if (q >= np_) break;
+      const float d0 = t0 - mt[q][0];
+      float ss = d0 * d0;
+      if (F == 2) {
+        const float d1 = t1 - mt[q][1];
+        ss = __fadd_rn(ss, __fmul_rn(d1, d1));
+      }
+      const float v = __fsub_rn(sv, rintf(__fsqrt_rn(ss)));
+      const unsigned long long k = refine_key(v, (uint32_t)px);
+      best[q] = k > best[q] ? k : best[q];
+    }
+  }
+  __shared__ unsigned long long red[4][REFINE_PC];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int q = 0; q < REFINE_PC; ++q) {
+    unsigned long long k = best[q];
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long other = __shfl_xor(k, o);
+      k = other > k ? other : k;
+    }
+    if (lane == 0) red[wv][q] = k;
+  }
+  __syncthreads();
+  if (threadIdx.x < np_) {
+    const int q = threadIdx.x;
+    unsigned long long k = red[0][q];
+    for (int w2 = 1; w2 < (int)(blockDim.x >> 6); ++w2) k = red[w2][q] > k ? red[w2][q] : k;
+    atomicMax(&keys[(size_t)(p0 + q) * J + i], k);
+  }
+}
+
+// ans[p][i] = (x + 0.5 +- 0.25, y + 0.5 +- 0.25, val) as Utils.py:1075-1092, then the fill rule of
+// :1096-1101: keypoints[p, i] = (ans x, ans y, 0.001) where ans val > 0 and keypoints[p, i, 2] == 0.
+__global__ void refine_finish_kernel(const float* __restrict__ s, int H, int W,
+                                     const unsigned long long* __restrict__ keys, int P, int J,
+                                     double* __restrict__ kp) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= P * J) return;
+  const int i = t % J;
+  const uint32_t idx = 0xFFFFFFFFu - (uint32_t)(keys[t] & 0xFFFFFFFFull);
+  const int yy = idx / W, xx = idx % W;
+  const float* tmp = s + (size_t)i * H * W;
+  const float val = tmp[(size_t)yy * W + xx];
+  double x = xx + 0.5, y = yy + 0.5;
+  x += tmp[(size_t)yy * W + min(xx + 1, W - 1)] > tmp[(size_t)yy * W + max(xx - 1, 0)] ? 0.25 : -0.25;
+  y += tmp[(size_t)min(yy + 1, H - 1) * W + xx] > tmp[(size_t)max(yy - 1, 0) * W + xx] ? 0.25 : -0.25;
+  double* q = kp + (size_t)t * 3;
+  if ((double)val > 0.0 && q[2] == 0.0) {
+    q[0] = x;
+    q[1] = y;
+    q[2] = 0.001;
+  }
+}
+
+// adjust (Utils.py:917-936): for joints with score > 0, quarter-pixel shift toward the larger neighbour of
+// det[joint_id] (indexed [int(kp[1]), int(kp[0])]), then + 0.5.
+__global__ void adjust_kernel(const float* __restrict__ det, int H, int W, int P, int J, double* __restrict__ kp) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= P * J) return;
+  double* q = kp + (size_t)t * 3;
+  if (!(q[2] > 0.0)) return;
+  const int j = t % J;
+  double y = q[0], x = q[1];
+  const int xx = (int)x, yy = (int)y;
+  const float* tmp = det + (size_t)j * H * W;
+  y += tmp[(size_t)xx * W + min(yy + 1, W - 1)] > tmp[(size_t)xx * W + max(yy - 1, 0)] ? 0.25 : -0.25;
+  x += tmp[(size_t)min(xx + 1, H - 1) * W + yy] > tmp[(size_t)max(0, xx - 1) * W + yy] ? 0.25 : -0.25;
+  q[1] = x + 0.5;
+  q[0] = y + 0.5;
+}
+
+}  // namespace
+
+extern "C" int pemp_pose_refine(const float* scoremaps, const float* tag, int J, int H, int W, int F, double* keypoints,
+                                int P, void* workspace, size_t workspace_bytes, void* stream) {
+  PEMP_CHECK_ARG(J >= 1 && J <= 64 && H >= 1 && W >= 1 && (F == 1 || F == 2) && P >= 0,
+                 "pemp_pose_refine: bad args (J <= 64, F in {1, 2})");
+  PEMP_CHECK_ARG((size_t)H * W < 0xFFFFFFFFull, "pemp_pose_refine: map too large");
+  if (P == 0) return PEMP_OK;
+  PEMP_CHECK_ARG(scoremaps && tag && keypoints, "pemp_pose_refine: null pointer");
+  const size_t need = align_up((size_t)P * F * sizeof(float), 256) + (size_t)P * J * 8;
+  PEMP_CHECK_ARG(workspace && workspace_bytes >= need, "pemp_pose_refine: workspace %zu < %zu", workspace_bytes,
+                 need);
+  float* mean_tag = reinterpret_cast<float*>(workspace);
+  unsigned long long* keys =
+      reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(workspace) + align_up((size_t)P * F * 4, 256));
+  hipStream_t st = as_stream(stream);
+  ProfScope prof("pose_refine", st);
+  PEMP_HIP(hipMemsetAsync(keys, 0, (size_t)P * J * 8, st));
+  hipLaunchKernelGGL(refine_mean_tag_kernel, dim3((P + 63) / 64), dim3(64), 0, st, keypoints, P, J, tag, H, W, F,
+                     mean_tag);
+  PEMP_LAUNCH_CHECK();
+  const size_t HW = (size_t)H * W;
+  const int bx = (int)std::min<size_t>((HW + 255) / 256, std::max(1, 2048 / J));
+  hipLaunchKernelGGL(refine_argmax_kernel, dim3(bx, J, (P + REFINE_PC - 1) / REFINE_PC), dim3(256), 0, st, scoremaps,
+                     tag, H, W, F, mean_tag, P, keys, J);
+  PEMP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(refine_finish_kernel, dim3((P * J + 255) / 256), dim3(256), 0, st, scoremaps, H, W, keys, P, J,
+                     keypoints);
+  PEMP_LAUNCH_CHECK();
+  return PEMP_OK;
+}
+
+extern "C" size_t pemp_pose_refine_workspace_size(int P, int J, int F) {
+  if (P <= 0) return 0;
+  return align_up((size_t)P * F * sizeof(float), 256) + (size_t)P * J * 8;
+}
+
+extern "C" int pemp_pose_adjust(const float* det, int J, int H, int W, double* keypoints, int P, void* stream) {
+  PEMP_CHECK_ARG(J >= 1 && H >= 1 && W >= 1 && P >= 0, "pemp_pose_adjust: bad args");
+  if (P == 0) return PEMP_OK;
+  PEMP_CHECK_ARG(det && keypoints, "pemp_pose_adjust: null pointer");
+  hipLaunchKernelGGL(adjust_kernel, dim3((P * J + 255) / 256), dim3(256), 0, as_stream(stream), det, H, W, P, J,
+                     keypoints);
+  PEMP_LAUNCH_CHECK();
+  return PEMP_OK;
+}
+
+// fill_mean (Utils.py:1468-1470), host: joints with score == 0 take the mean (x, y) of the person's joints
+// with score != 0 (float64, numpy's row-by-row axis-0 sum from 0, then / count; NaN when none).
+extern "C" int pemp_pose_fill_mean(double* keypoints, int P, int J) {
+  PEMP_CHECK_ARG(P >= 0 && J >= 1 && (P == 0 || keypoints), "pemp_pose_fill_mean: bad args");
+  for (int p = 0; p < P; ++p) {
+    double* kp = keypoints + (size_t)p * J * 3;
+    double sx = 0.0, sy = 0.0;
+    int k = 0;
+    for (int j = 0; j < J; ++j)
+      if (kp[j * 3 + 2] != 0.0) {
+        sx += kp[j * 3 + 0];
+        sy += kp[j * 3 + 1];
+        ++k;
+      }
+    const double mx = sx / (double)k, my = sy / (double)k;
+    for (int j = 0; j < J; ++j)
+      if (kp[j * 3 + 2] == 0.0) {
+        kp[j * 3 + 0] = mx;
+        kp[j * 3 + 1] = my;
+      }
+  }
+  return PEMP_OK;
+}

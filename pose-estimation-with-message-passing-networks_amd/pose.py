@@ -162,3 +162,94 @@ def group_persons(joint_det, joint_scores, edge_index, pred, th, class_pred=None
         else:
             out.append(persons)
     return out
+
+
+# ----------------------------------------------------------------------------------------------------
+# Finishing (pred_to_ann, Utils.py:1460-1478): filter, fill_mean, refine, adjust
+# ----------------------------------------------------------------------------------------------------
+def _kp_array(keypoints):
+    kp = np.ascontiguousarray(keypoints, dtype=np.float64)
+    if kp.ndim != 3 or kp.shape[2] != 3:
+        raise ValueError(f"pemp_amd.pose: keypoints must be [P, J, 3], got {kp.shape}")
+    return kp
+
+
+def fill_mean(persons):
+    """``Utils.py:1468-1470`` in place on a float64 [P, J, 3] array (host C++)."""
+    L = _lib.load_cdll() if _lib._LIB is None else _lib._LIB
+    kp = _kp_array(persons)
+    _lib.check(L.pemp_pose_fill_mean(kp.ctypes.data, kp.shape[0], kp.shape[1]), L)
+    if kp is not persons:
+        persons[...] = kp
+    return persons
+
+
+def _maps(t, name, ndim):
+    if not (isinstance(t, torch.Tensor) and t.device.type == "cuda"):
+        raise ValueError(f"pemp_amd.pose: {name} must be a device tensor (no CPU fallback)")
+    t = t.to(torch.float32).contiguous()
+    if t.dim() not in ndim:
+        raise ValueError(f"pemp_amd.pose: {name} has shape {tuple(t.shape)}")
+    return t
+
+
+def refine(scoremaps, tag, keypoints):
+    """``Utils.py:1026-1104``: scoremaps [J,H,W], tag [J,H,W] or [J,H,W,F] (F = 1, 2) device tensors,
+    keypoints float64 [P, J, 3] (numpy). Updates keypoints in place and returns it, like the reference."""
+    L = _lib.lib()
+    s = _maps(scoremaps, "scoremaps", (3,))
+    tg = _maps(tag, "tag", (3, 4))
+    if tg.dim() == 3:
+        tg = tg[..., None]
+    J, H, W = s.shape
+    F = tg.shape[3]
+    if tuple(tg.shape[:3]) != (J, H, W):
+        raise ValueError(f"pemp_amd.pose: tag {tuple(tg.shape)} does not match scoremaps {tuple(s.shape)}")
+    kp = _kp_array(keypoints)
+    if kp.shape[1] != J:
+        raise ValueError(f"pemp_amd.pose: keypoints have {kp.shape[1]} joints, scoremaps {J}")
+    P = kp.shape[0]
+    if P == 0:
+        return keypoints
+    d_kp = torch.from_numpy(kp).to(s.device)
+    ws = torch.empty(L.pemp_pose_refine_workspace_size(P, J, F), dtype=torch.uint8, device=s.device)
+    _lib.check(L.pemp_pose_refine(s.data_ptr(), tg.data_ptr(), J, H, W, F, d_kp.data_ptr(), P, ws.data_ptr(),
+                                  ws.numel(), _lib.stream(s.device)))
+    keypoints[...] = d_kp.cpu().numpy()
+    return keypoints
+
+
+def adjust(ans, det):
+    """``Utils.py:917-936``: ans float64 [P, J, 3] (numpy, updated in place and returned), det [J,H,W]
+    device tensor."""
+    L = _lib.lib()
+    d = _maps(det, "det", (3,))
+    kp = _kp_array(ans)
+    J, H, W = d.shape
+    if kp.shape[0] == 0:
+        return ans
+    d_kp = torch.from_numpy(kp).to(d.device)
+    _lib.check(L.pemp_pose_adjust(d.data_ptr(), J, H, W, d_kp.data_ptr(), kp.shape[0], _lib.stream(d.device)))
+    ans[...] = d_kp.cpu().numpy()
+    return ans
+
+
+def finish_persons(persons, scoremaps, tags, adjustment, with_refine, with_filter=False, fill_mean_=True):
+    """The middle of ``pred_to_ann`` (``Utils.py:1460-1478``) for one image's grouped persons: the
+    optional max-score filter (> 0.25), fill_mean, refine (only when the first person has a score), adjust.
+    Returns the float64 [P, J, 3] array, or None where the reference returns None (all filtered out)."""
+    if persons is None:
+        return None
+    if with_filter:
+        keep = persons[:, :, 2].max(axis=1) > 0.25
+        persons = persons[keep]
+        if persons.shape[0] == 0:
+            return None
+    persons = np.ascontiguousarray(persons, dtype=np.float64)
+    if fill_mean_:
+        fill_mean(persons)
+    if with_refine and persons[0, :, 2].sum() != 0:
+        refine(scoremaps, tags, persons)
+    if adjustment:
+        adjust(persons, scoremaps)
+    return persons

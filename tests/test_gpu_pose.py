@@ -8,7 +8,7 @@ import torch
 import pemp_amd
 from oracle import pose as opose, restate
 from pemp_amd import _lib, config as pcfg, pose as ppose, synthetic as syn
-from tests.test_pose_cpu import CASES, edge_pass, load
+from tests.test_pose_cpu import GROUP, REFINE, edge_pass, load
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
@@ -18,7 +18,7 @@ def dev(a):
     return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
 
 
-@pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("name", GROUP)
 def test_group_persons_golden(name):
     g = load(name)
     cls = dev(g["class_probs"]) if g["has_class"] else None
@@ -32,7 +32,7 @@ def test_group_persons_golden(name):
         np.testing.assert_array_equal(out[0], g["persons"])
 
 
-@pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("name", GROUP)
 def test_pred_to_person_golden(name):
     g = load(name)
     J = int(g["num_joints"])
@@ -50,7 +50,7 @@ def test_pred_to_person_golden(name):
 def test_edge_pass_kernel_bits(method):
     """pemp_pose_edge_weights == its numpy statement, bit for bit (NaN positions included), on a batch of
     three fixture graphs; flags per image."""
-    gs = [load(n) for n in CASES[:3]]
+    gs = [load(n) for n in GROUP[:3]]
     eis, prs, scs, offs = [], [], [], [0]
     for g in gs:
         eis.append(g["edge_index"] + offs[-1])
@@ -76,7 +76,7 @@ def test_edge_pass_kernel_bits(method):
 
 
 def test_group_persons_batched():
-    gs = [load(n) for n in CASES if str(load(n)["method"]) == "GAEC" and int(load(n)["num_joints"]) == 17]
+    gs = [load(n) for n in GROUP if str(load(n)["method"]) == "GAEC" and int(load(n)["num_joints"]) == 17]
     dets, scs, eis, prs, clss, bis = [], [], [], [], [], []
     base = 0
     for b, g in enumerate(gs):
@@ -133,3 +133,27 @@ def test_end_to_end_after_mpn(method):
             assert got[b] is None
         else:
             np.testing.assert_array_equal(got[b], ref)
+
+
+@pytest.mark.parametrize("name", REFINE)
+def test_refine_adjust_golden(name):
+    """pemp_pose_refine / pemp_pose_adjust against the reference's own refine / adjust (bit-exact float64
+    keypoints; the per-person float32 mean tag follows numpy's summation order)."""
+    g = load(name)
+    s, tag = dev(g["scoremaps"]), dev(g["tag"])
+    kp = g["filled"].copy()
+    out = ppose.refine(s, tag, kp)
+    assert out is kp
+    np.testing.assert_array_equal(kp, g["refined"])
+    ppose.adjust(kp, s)
+    np.testing.assert_array_equal(kp, g["adjusted"])
+
+
+def test_finish_persons_matches_oracle():
+    g = load(REFINE[0])
+    s, tag = dev(g["scoremaps"]), dev(g["tag"])
+    got = ppose.finish_persons(g["keypoints"].copy(), s, tag, adjustment=True, with_refine=True, with_filter=True)
+    ref = g["keypoints"].copy()
+    ref = ref[ref[:, :, 2].max(axis=1) > 0.25]
+    ref = opose.adjust(opose.refine(g["scoremaps"], g["tag"], opose.fill_mean(ref)), g["scoremaps"])
+    np.testing.assert_array_equal(got, ref)

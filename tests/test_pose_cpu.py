@@ -17,6 +17,8 @@ from pemp_amd import _lib
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CASES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.startswith("pose_") and f.endswith(".npz"))
+REFINE = [c for c in CASES if c.startswith("pose_refine")]
+GROUP = [c for c in CASES if not c.startswith("pose_refine")]
 
 
 def load(name):
@@ -76,7 +78,7 @@ def method_of(g):
     return {"GAEC": 0, "threshold": 1}[str(g["method"])]
 
 
-@pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("name", GROUP)
 def test_oracle_matches_reference_fixture(name):
     g = load(name)
     cls = g["class_probs"] if g["has_class"] else None
@@ -87,7 +89,7 @@ def test_oracle_matches_reference_fixture(name):
         np.testing.assert_array_equal(got, g["persons"])
 
 
-@pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("name", GROUP)
 def test_host_grouping_matches_reference_fixture(name):
     g = load(name)
     J = int(g["num_joints"])
@@ -111,7 +113,7 @@ def test_host_grouping_matches_reference_fixture(name):
 
 
 def test_host_grouping_batched_equals_per_image():
-    gs = [load(n) for n in CASES if str(load(n)["method"]) == "GAEC" and int(load(n)["num_joints"]) == 17]
+    gs = [load(n) for n in GROUP if str(load(n)["method"]) == "GAEC" and int(load(n)["num_joints"]) == 17]
     dets, scs, eis, prs, clss, offs = [], [], [], [], [], [0]
     for g in gs:
         n = len(g["joint_det"])
@@ -171,3 +173,22 @@ def test_unsorted_edge_index_is_refused():
                              labels.ctypes.data, nc.ctypes.data)
     with pytest.raises(ValueError, match="sorted"):
         _lib.check(rc, L)
+
+
+@pytest.mark.parametrize("name", REFINE)
+def test_oracle_refine_adjust_fixture(name):
+    g = load(name)
+    filled = opose.fill_mean(g["keypoints"].copy())
+    np.testing.assert_array_equal(filled, g["filled"])
+    refined = opose.refine(g["scoremaps"], g["tag"], filled.copy())
+    np.testing.assert_array_equal(refined, g["refined"])
+    np.testing.assert_array_equal(opose.adjust(refined.copy(), g["scoremaps"]), g["adjusted"])
+
+
+@pytest.mark.parametrize("name", REFINE)
+def test_host_fill_mean_fixture(name):
+    from pemp_amd import pose as ppose
+    g = load(name)
+    kp = g["keypoints"].copy()
+    ppose.fill_mean(kp)
+    np.testing.assert_array_equal(kp, g["filled"])
