@@ -87,6 +87,7 @@ def run_step(wl, gc, model, hm, feats, tags, dev):
     return out, pe, pn, pc
 
 
+_BENCH_MAPS = None
 ROOF_REPEAT = 8   # back-to-back launches per event pair in the roofline phase
 
 
@@ -274,6 +275,44 @@ def pose_grouping(wl, out, pe, pn, pc, cpu_ref):
             opose.pred_to_ann_persons(h[0][nm], h[1][nm], h[2][:, em] - lo, h[3][em], np.float32(0.1), h[4][nm],
                                       "GAEC", wl["J"], h[6][nm])
         rec["cpu_oracle_ms_per_batch"] = round((time.perf_counter() - t0) * 1e3, 1)
+    rec["refine"] = pose_refine(wl, res, cpu_ref)
+    return rec
+
+
+def pose_refine(wl, persons, cpu_ref):
+    """SURVEY 8f row 3, informational: refine (Utils.py:1026-1104) of image 0's grouped persons on its
+    full-size [J, H, W] scoremaps and [J, H, W, 1] tag maps (the pred_to_ann order: fill_mean, refine,
+    adjust). GPU kernels vs the oracle restatement (numpy, the reference's own ops)."""
+    from pemp_amd import pose as ppose
+    hm, tags = _BENCH_MAPS
+    kp0 = next((p for p in persons if p is not None), None)
+    if kp0 is None:
+        return None
+    kp0 = ppose.fill_mean(np.ascontiguousarray(kp0, dtype=np.float64).copy())
+    s, tg = hm[0], tags[0]
+    J, H, W = s.shape
+    P = kp0.shape[0]
+    ppose.refine(s, tg, kp0.copy())
+    reps = 5
+    torch.cuda.synchronize()
+    _lib.prof_enable("pose_refine")
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ppose.refine(s, tg, kp0.copy())
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    st = _lib.prof_report()
+    _lib.prof_enable(None)
+    n, kms = st.get("pose_refine", (1, float("nan")))
+    F = tg.shape[-1] if tg.dim() == 4 else 1
+    byts = J * H * W * (4 + 4 * F)
+    rec = {"persons": P, "map": [J, H, W, F], "ms_per_image": round(ms, 3), "kernels_us": round(kms / n * 1e3, 2),
+           "algorithmic_bytes": byts, "hbm_GBs_algorithmic": round(byts / (kms / n * 1e-3) / 1e9, 1)}
+    if cpu_ref:
+        from oracle import pose as opose
+        sh, th = s.cpu().numpy(), tg.cpu().numpy()
+        t0 = time.perf_counter()
+        opose.refine(sh, th, kp0.copy())
+        rec["cpu_oracle_ms_per_image"] = round((time.perf_counter() - t0) * 1e3, 1)
     return rec
 
 
@@ -349,6 +388,8 @@ def main():
 
     front = frontend_projection(wl, gc, model, hm, tags, dev, out) if not args.no_roofline else None
 
+    global _BENCH_MAPS
+    _BENCH_MAPS = (hm, tags)
     grouping = pose_grouping(wl, out, pe, pn, pc, rank == 0 and world == 1 and not args.no_cpu_baseline) \
         if not args.no_roofline else None
 

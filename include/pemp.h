@@ -209,10 +209,10 @@ int pemp_pose_persons(int B, const int64_t* node_off, const int32_t* labels, con
  *   person the float32 mean tag of its detected joints (numpy's summation order), per (person, joint) the
  *   first argmax over the map of s - rint(||tag - mean||) (one pass over the pixels per 8 persons), the
  *   quarter-pixel offset, and the fill of undetected joints with score 0.001. scoremaps [J][H][W] f32,
- *   tag [J][H][W][F] f32 (F = 1 or 2). Workspace: pemp_pose_refine_workspace_size(P, J, F) bytes.
+ *   tag [J][H][W][F] f32 (F = 1 or 2). Workspace: pemp_pose_refine_workspace_size(P, J, H, W, F) bytes.
  * pemp_pose_adjust (GPU, in place): adjust, Utils.py:917-936, det [J][H][W] f32. */
 int pemp_pose_fill_mean(double* keypoints, int P, int J);
-size_t pemp_pose_refine_workspace_size(int P, int J, int F);
+size_t pemp_pose_refine_workspace_size(int P, int J, int H, int W, int F);
 int pemp_pose_refine(const float* scoremaps, const float* tag, int J, int H, int W, int F, double* keypoints, int P,
                      void* workspace, size_t workspace_bytes, void* stream);
 int pemp_pose_adjust(const float* det, int J, int H, int W, double* keypoints, int P, void* stream);

@@ -80,7 +80,7 @@ SIGNATURES = {
     "pemp_pose_cluster": (c_i32, [c_i32, c_p, c_p, c_i64, c_p, c_p, c_i32, c_i32, c_p, c_p]),
     "pemp_pose_persons": (c_i32, [c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i32, c_i32, c_i64, c_p, c_p, c_p]),
     "pemp_pose_fill_mean": (c_i32, [c_p, c_i32, c_i32]),
-    "pemp_pose_refine_workspace_size": (c_sz, [c_i32, c_i32, c_i32]),
+    "pemp_pose_refine_workspace_size": (c_sz, [c_i32, c_i32, c_i32, c_i32, c_i32]),
     "pemp_pose_refine": (c_i32, [c_p, c_p, c_i32, c_i32, c_i32, c_i32, c_p, c_i32, c_p, c_sz, c_p]),
     "pemp_pose_adjust": (c_i32, [c_p, c_i32, c_i32, c_i32, c_p, c_i32, c_p]),
     "pemp_prof_enable": (c_i32, [ctypes.c_char_p]),

@@ -421,7 +421,6 @@ extern "C" int pemp_pose_persons(int B, const int64_t* node_off, const int32_t* 
 // ------------------------------------------------------------------------------------------------
 namespace {
 
-constexpr int REFINE_PC = 8;  // persons per thread (grid.z covers the rest)
 
 // numpy's float32 add.reduce of k values: pairwise_sum for a contiguous run (F = 1: n < 8 sequential,
 // else 8 strided partial sums combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) plus the tail); for F = 2 the
@@ -442,21 +441,41 @@ __device__ float np_sum_f32(const float* v, int n, bool pairwise) {
   return res;
 }
 
-// prev_tag[p] = np.mean(tags at the detected joints of person p, axis=0) (float32)
-__global__ void refine_mean_tag_kernel(const double* __restrict__ kp, int P, int J, const float* __restrict__ tag,
-                                       int H, int W, int F, float* __restrict__ mean_tag) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= P) return;
-  float vals[2][64];
-  int k = 0;
-  for (int i = 0; i < J; ++i) {
-    const double* q = kp + ((size_t)p * J + i) * 3;
-    if (!(q[2] > 0.0)) continue;
-    const int x = (int)q[0], y = (int)q[1];  // astype(np.int32): truncation
-    for (int f = 0; f < F; ++f) vals[f][k] = tag[(((size_t)i * H + y) * W + x) * F + f];
-    ++k;
+// prev_tag[p] = np.mean(tags at the detected joints of person p, axis=0) (float32). One wave per person:
+// lane j loads joint j's flag and tag values (all loads in flight together), lane 0 sums in numpy's order.
+__global__ __launch_bounds__(64) void refine_mean_tag_kernel(const double* __restrict__ kp, int P, int J,
+                                                             const float* __restrict__ tag, int H, int W, int F,
+                                                             float* __restrict__ mean_tag) {
+  const int p = blockIdx.x, j = threadIdx.x;
+  bool det = false;
+  float v0 = 0.f, v1 = 0.f;
+  if (j < J) {
+    const double* q = kp + ((size_t)p * J + j) * 3;
+    det = q[2] > 0.0;
+    if (det) {
+      const int x = (int)q[0], y = (int)q[1];  // astype(np.int32): truncation
+      const size_t o = (((size_t)j * H + y) * W + x) * F;
+      v0 = tag[o];
+      if (F == 2) v1 = tag[o + 1];
+    }
   }
-  for (int f = 0; f < F; ++f) mean_tag[p * F + f] = np_sum_f32(vals[f], k, F == 1) / (float)k;
+  __shared__ float vals[2][64];
+  __shared__ int flag[64];
+  vals[0][j] = v0;
+  vals[1][j] = v1;
+  flag[j] = det;
+  __syncthreads();
+  if (j == 0) {
+    float c[2][64];
+    int k = 0;
+    for (int i = 0; i < J; ++i)
+      if (flag[i]) {
+        c[0][k] = vals[0][i];
+        c[1][k] = vals[1][i];
+        ++k;
+      }
+    for (int f = 0; f < F; ++f) mean_tag[p * F + f] = np_sum_f32(c[f], k, F == 1) / (float)k;
+  }
 }
 
 __device__ __forceinline__ unsigned long long refine_key(float v, uint32_t idx) {
@@ -465,41 +484,69 @@ __device__ __forceinline__ unsigned long long refine_key(float v, uint32_t idx) 
   return ((unsigned long long)o << 32) | (0xFFFFFFFFu - idx);  // max: larger v, then lower flat index
 }
 
-// keys[p][i] = max over pixels of key(s - rint(||tag - prev_tag[p]||), pixel): np.argmax(tmp2), first max.
-// grid: (pixel blocks, J, person chunks of REFINE_PC); each pixel is read once per chunk.
+// ordered 64-bit key: larger value first, then the lower flat index
+// partial keys[i][block][p] = max over the block's pixels of key(s - rint(||tag - prev_tag[p]||), pixel):
+// np.argmax(tmp2), first max. grid: (pixel blocks, J, person chunks of PC). Straight-line code: persons
+// beyond P in the last chunk are computed on a copy of a real mean tag and never stored; pixels past the
+// end are clamped to the last pixel (a true candidate with its own index). A thread visits its pixels in
+// increasing order, so a strict > keeps the first maximum; (value, index) pairs become ordered 64-bit keys
+// only for the cross-thread reduction.
+template <int PC>
 __global__ __launch_bounds__(256) void refine_argmax_kernel(const float* __restrict__ s, const float* __restrict__ tag,
                                                             int H, int W, int F, const float* __restrict__ mean_tag,
                                                             int P, unsigned long long* __restrict__ keys, int J) {
   const int i = blockIdx.y;
-  const int p0 = blockIdx.z * REFINE_PC;
-  const int np_ = min(REFINE_PC, P - p0);
-  float mt[REFINE_PC][2];
-  for (int q = 0; q < REFINE_PC; ++q)
-    for (int f = 0; f < 2; ++f) mt[q][f] = (q < np_ && f < F) ? mean_tag[(p0 + q) * F + f] : 0.f;
-  unsigned long long best[REFINE_PC];
-  for (int q = 0; q < REFINE_PC; ++q) best[q] = 0ull;
+  const int p0 = blockIdx.z * PC;
+  const int np_ = min(PC, P - p0);
+  float mt0[PC], mt1[PC], bv[PC];
+  uint32_t bi[PC];
   const size_t HW = (size_t)H * W;
+  const size_t first = min((size_t)blockIdx.x * blockDim.x + threadIdx.x, HW - 1);
+#pragma unroll
+  for (int q = 0; q < PC; ++q) {
+    const int pq = p0 + min(q, np_ - 1);
+    mt0[q] = mean_tag[pq * F];
+    mt1[q] = F == 2 ? mean_tag[pq * F + 1] : 0.f;
+    bv[q] = -INFINITY;
+    bi[q] = (uint32_t)first;
+  }
   const float* sp = s + (size_t)i * HW;
   const float* tp = tag + (size_t)i * HW * F;
-  for (size_t px = (size_t)blockIdx.x * blockDim.x + threadIdx.x; px < HW; px += (size_t)gridDim.x * blockDim.x) {
-    const float sv = sp[px];
-    const float t0 = tp[px * F], t1 = F == 2 ? tp[px * F + 1] : 0.f;
-    for (int q = 0; q < REFINE_PC; ++q) {
-      if (q >= np_) break;
-      const float d0 = t0 - mt[q][0];
-      float ss = d0 * d0;
-      if (F == 2) {
-        const float d1 = t1 - mt[q][1];
-        ss = __fadd_rn(ss, __fmul_rn(d1, d1));
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t base = (size_t)blockIdx.x * blockDim.x + threadIdx.x; base < HW; base += 4 * stride) {
+    float sv[4], t0[4], t1[4];
+    uint32_t pxs[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const size_t px = min(base + u * stride, HW - 1);
+      pxs[u] = (uint32_t)px;
+      sv[u] = sp[px];
+      t0[u] = tp[px * F];
+      t1[u] = F == 2 ? tp[px * F + 1] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int q = 0; q < PC; ++q) {
+        const float d0 = __fsub_rn(t0[u], mt0[q]);
+        float ss = __fmul_rn(d0, d0);
+        if (F == 2) {
+          const float d1 = __fsub_rn(t1[u], mt1[q]);
+          ss = __fadd_rn(ss, __fmul_rn(d1, d1));
+        }
+        const float v = __fsub_rn(sv[u], rintf(__fsqrt_rn(ss)));
+        const bool better = v > bv[q];
+        bv[q] = better ? v : bv[q];
+        bi[q] = better ? pxs[u] : bi[q];
       }
-      const float v = __fsub_rn(sv, rintf(__fsqrt_rn(ss)));
-      const unsigned long long k = refine_key(v, (uint32_t)px);
-      best[q] = k > best[q] ? k : best[q];
     }
   }
-  __shared__ unsigned long long red[4][REFINE_PC];
+  unsigned long long best[PC];
+#pragma unroll
+  for (int q = 0; q < PC; ++q) best[q] = refine_key(bv[q], bi[q]);
+  __shared__ unsigned long long red[4][PC];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int q = 0; q < REFINE_PC; ++q) {
+  for (int q = 0; q < PC; ++q) {
     unsigned long long k = best[q];
     for (int o = 32; o > 0; o >>= 1) {
       const unsigned long long other = __shfl_xor(k, o);
@@ -508,23 +555,33 @@ __global__ __launch_bounds__(256) void refine_argmax_kernel(const float* __restr
     if (lane == 0) red[wv][q] = k;
   }
   __syncthreads();
-  if (threadIdx.x < np_) {
+  if (threadIdx.x < np_) {  // per-block partial: no cross-XCD atomics on the same few addresses
     const int q = threadIdx.x;
     unsigned long long k = red[0][q];
     for (int w2 = 1; w2 < (int)(blockDim.x >> 6); ++w2) k = red[w2][q] > k ? red[w2][q] : k;
-    atomicMax(&keys[(size_t)(p0 + q) * J + i], k);
+    keys[((size_t)i * gridDim.x + blockIdx.x) * P + p0 + q] = k;
   }
 }
 
 // ans[p][i] = (x + 0.5 +- 0.25, y + 0.5 +- 0.25, val) as Utils.py:1075-1092, then the fill rule of
 // :1096-1101: keypoints[p, i] = (ans x, ans y, 0.001) where ans val > 0 and keypoints[p, i, 2] == 0.
-__global__ void refine_finish_kernel(const float* __restrict__ s, int H, int W,
-                                     const unsigned long long* __restrict__ keys, int P, int J,
-                                     double* __restrict__ kp) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= P * J) return;
-  const int i = t % J;
-  const uint32_t idx = 0xFFFFFFFFu - (uint32_t)(keys[t] & 0xFFFFFFFFull);
+// One wave per (person, joint): the lanes reduce the per-block partial keys, lane 0 finishes.
+__global__ __launch_bounds__(64) void refine_finish_kernel(const float* __restrict__ s, int H, int W,
+                                                           const unsigned long long* __restrict__ keys, int nblk,
+                                                           int P, int J, double* __restrict__ kp) {
+  const int t = blockIdx.x;
+  const int i = t % J, p = t / J;
+  unsigned long long key = 0ull;
+  for (int b = threadIdx.x; b < nblk; b += 64) {
+    const unsigned long long k = keys[((size_t)i * nblk + b) * P + p];
+    key = k > key ? k : key;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long other = __shfl_xor(key, o);
+    key = other > key ? other : key;
+  }
+  if (threadIdx.x != 0) return;
+  const uint32_t idx = 0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull);
   const int yy = idx / W, xx = idx % W;
   const float* tmp = s + (size_t)i * H * W;
   const float val = tmp[(size_t)yy * W + xx];
@@ -558,6 +615,15 @@ __global__ void adjust_kernel(const float* __restrict__ det, int H, int W, int P
 
 }  // namespace
 
+static int refine_blocks(int J, int H, int W) {
+  return (int)std::min<size_t>(((size_t)H * W + 1023) / 1024, (size_t)std::max(1, 4096 / J));
+}
+
+extern "C" size_t pemp_pose_refine_workspace_size(int P, int J, int H, int W, int F) {
+  if (P <= 0 || J <= 0 || H <= 0 || W <= 0) return 0;
+  return align_up((size_t)P * F * sizeof(float), 256) + (size_t)J * refine_blocks(J, H, W) * P * 8;
+}
+
 extern "C" int pemp_pose_refine(const float* scoremaps, const float* tag, int J, int H, int W, int F, double* keypoints,
                                 int P, void* workspace, size_t workspace_bytes, void* stream) {
   PEMP_CHECK_ARG(J >= 1 && J <= 64 && H >= 1 && W >= 1 && (F == 1 || F == 2) && P >= 0,
@@ -565,7 +631,7 @@ extern "C" int pemp_pose_refine(const float* scoremaps, const float* tag, int J,
   PEMP_CHECK_ARG((size_t)H * W < 0xFFFFFFFFull, "pemp_pose_refine: map too large");
   if (P == 0) return PEMP_OK;
   PEMP_CHECK_ARG(scoremaps && tag && keypoints, "pemp_pose_refine: null pointer");
-  const size_t need = align_up((size_t)P * F * sizeof(float), 256) + (size_t)P * J * 8;
+  const size_t need = pemp_pose_refine_workspace_size(P, J, H, W, F);
   PEMP_CHECK_ARG(workspace && workspace_bytes >= need, "pemp_pose_refine: workspace %zu < %zu", workspace_bytes,
                  need);
   float* mean_tag = reinterpret_cast<float*>(workspace);
@@ -573,24 +639,33 @@ extern "C" int pemp_pose_refine(const float* scoremaps, const float* tag, int J,
       reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(workspace) + align_up((size_t)P * F * 4, 256));
   hipStream_t st = as_stream(stream);
   ProfScope prof("pose_refine", st);
-  PEMP_HIP(hipMemsetAsync(keys, 0, (size_t)P * J * 8, st));
-  hipLaunchKernelGGL(refine_mean_tag_kernel, dim3((P + 63) / 64), dim3(64), 0, st, keypoints, P, J, tag, H, W, F,
+  hipLaunchKernelGGL(refine_mean_tag_kernel, dim3(P), dim3(64), 0, st, keypoints, P, J, tag, H, W, F,
                      mean_tag);
   PEMP_LAUNCH_CHECK();
-  const size_t HW = (size_t)H * W;
-  const int bx = (int)std::min<size_t>((HW + 255) / 256, std::max(1, 2048 / J));
-  hipLaunchKernelGGL(refine_argmax_kernel, dim3(bx, J, (P + REFINE_PC - 1) / REFINE_PC), dim3(256), 0, st, scoremaps,
-                     tag, H, W, F, mean_tag, P, keys, J);
+  const int bx = refine_blocks(J, H, W);
+  // persons per thread: the smallest instantiated width covering an even split of P into <= 16-wide chunks
+  const int chunks = (P + 15) / 16, per = (P + chunks - 1) / chunks;
+  const int pc = per <= 2 ? 2 : per <= 4 ? 4 : per <= 6 ? 6 : per <= 8 ? 8 : per <= 10 ? 10 : per <= 12 ? 12 : 16;
+  const dim3 grid(bx, J, (P + pc - 1) / pc);
+#define PEMP_REFINE_LAUNCH(N)                                                                                    \
+  case N:                                                                                                        \
+    hipLaunchKernelGGL(refine_argmax_kernel<N>, grid, dim3(256), 0, st, scoremaps, tag, H, W, F, mean_tag, P, keys, \
+                       J);                                                                                       \
+    break;
+  switch (pc) {
+    PEMP_REFINE_LAUNCH(2)
+    PEMP_REFINE_LAUNCH(4)
+    PEMP_REFINE_LAUNCH(6)
+    PEMP_REFINE_LAUNCH(8)
+    PEMP_REFINE_LAUNCH(10)
+    PEMP_REFINE_LAUNCH(12)
+    PEMP_REFINE_LAUNCH(16)
+  }
+#undef PEMP_REFINE_LAUNCH
   PEMP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(refine_finish_kernel, dim3((P * J + 255) / 256), dim3(256), 0, st, scoremaps, H, W, keys, P, J,
-                     keypoints);
+  hipLaunchKernelGGL(refine_finish_kernel, dim3(P * J), dim3(64), 0, st, scoremaps, H, W, keys, bx, P, J, keypoints);
   PEMP_LAUNCH_CHECK();
   return PEMP_OK;
-}
-
-extern "C" size_t pemp_pose_refine_workspace_size(int P, int J, int F) {
-  if (P <= 0) return 0;
-  return align_up((size_t)P * F * sizeof(float), 256) + (size_t)P * J * 8;
 }
 
 extern "C" int pemp_pose_adjust(const float* det, int J, int H, int W, double* keypoints, int P, void* stream) {

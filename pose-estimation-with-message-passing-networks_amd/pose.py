@@ -212,7 +212,7 @@ def refine(scoremaps, tag, keypoints):
     if P == 0:
         return keypoints
     d_kp = torch.from_numpy(kp).to(s.device)
-    ws = torch.empty(L.pemp_pose_refine_workspace_size(P, J, F), dtype=torch.uint8, device=s.device)
+    ws = torch.empty(L.pemp_pose_refine_workspace_size(P, J, H, W, F), dtype=torch.uint8, device=s.device)
     _lib.check(L.pemp_pose_refine(s.data_ptr(), tg.data_ptr(), J, H, W, F, d_kp.data_ptr(), P, ws.data_ptr(),
                                   ws.numel(), _lib.stream(s.device)))
     keypoints[...] = d_kp.cpu().numpy()

@@ -157,3 +157,30 @@ def test_finish_persons_matches_oracle():
     ref = ref[ref[:, :, 2].max(axis=1) > 0.25]
     ref = opose.adjust(opose.refine(g["scoremaps"], g["tag"], opose.fill_mean(ref)), g["scoremaps"])
     np.testing.assert_array_equal(got, ref)
+
+
+@pytest.mark.parametrize("F", [1, 2])
+@pytest.mark.parametrize("seed", range(4))
+def test_refine_rounding_boundaries(F, seed):
+    """Tag distances placed within a few ulp of half-integers (where rint(sqrt) flips): the refined
+    position of an undetected joint must match numpy (oracle) exactly."""
+    rng = np.random.default_rng(seed)
+    J, H, W = 2, 8, 128
+    m = np.float32(rng.uniform(-1, 1))
+    tag = np.full((J, H, W, F), m, np.float32)
+    k = rng.integers(0, 4, size=(H, W)).astype(np.float32) + np.float32(0.5)
+    ulps = rng.integers(-4, 5, size=(H, W))
+    d = np.nextafter(k, np.where(ulps > 0, np.float32(np.inf), np.float32(-np.inf)))
+    d = np.where(ulps == 0, k, d).astype(np.float32)
+    if F == 2:
+        tag[1, :, :, 0] = m + d * np.float32(0.6)
+        tag[1, :, :, 1] = m + d * np.float32(0.8)
+    else:
+        tag[1, :, :, 0] = m + d
+    s = (rng.random((J, H, W)) * 0.01).astype(np.float32)
+    kp = np.zeros((1, J, 3))
+    kp[0, 0] = (3, 2, 0.9)
+    tg = tag if F == 2 else tag[..., 0]
+    ref = opose.refine(s, tg, kp.copy())
+    got = ppose.refine(dev(s), dev(tg), kp.copy())
+    np.testing.assert_array_equal(got, ref)
