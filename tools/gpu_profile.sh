@@ -13,3 +13,10 @@ timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$rx" --outp
 timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$rx" --output-format csv -d gpurun_out/${tag}_pmc_write -o pmc -- \
   python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-roofline > gpurun_out/${tag}_pmc_write.log 2>&1
 python tools/pmc_json.py gpurun_out/${tag}_pmc.json gpurun_out/${tag}_pmc_*/pmc_counter_collection.csv > /dev/null
+# refine (pose finishing): kernel stats and HBM passes of its own
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${tag}_refine_stats -o run -- \
+  python tools/refine_prof.py 9 > gpurun_out/${tag}_refine_stats.log 2>&1
+timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex refine_argmax --output-format csv -d gpurun_out/${tag}_refine_pmc_fetch -o pmc -- \
+  python tools/refine_prof.py 9 > gpurun_out/${tag}_refine_pmc_fetch.log 2>&1
+timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex refine_argmax --output-format csv -d gpurun_out/${tag}_refine_pmc_write -o pmc -- \
+  python tools/refine_prof.py 9 > gpurun_out/${tag}_refine_pmc_write.log 2>&1
