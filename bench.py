@@ -88,6 +88,7 @@ def run_step(wl, gc, model, hm, feats, tags, dev):
 
 
 _BENCH_MAPS = None
+_LAST_GROUPING = None
 ROOF_REPEAT = 8   # back-to-back launches per event pair in the roofline phase
 
 
@@ -254,6 +255,8 @@ def pose_grouping(wl, out, pe, pn, pc, cpu_ref):
     for _ in range(reps):
         res = ppose.group_persons(*args, batch_index=bi, score_map_scores=sc)
     gpu_ms = (time.perf_counter() - t0) / reps * 1e3
+    global _LAST_GROUPING
+    _LAST_GROUPING = res
     st = _lib.prof_report()
     _lib.prof_enable(None)
     tm = {}
@@ -392,6 +395,17 @@ def main():
     _BENCH_MAPS = (hm, tags)
     grouping = pose_grouping(wl, out, pe, pn, pc, rank == 0 and world == 1 and not args.no_cpu_baseline) \
         if not args.no_roofline else None
+    if grouping is not None and world > 1:
+        # the one data collective of the sharded path -- every rank's grouped poses to all ranks
+        try:
+            start, _ = pdist.image_block(wl["B"] * world, rank, world)
+            barrier(world)
+            t2 = time.perf_counter()
+            ids, poses = pdist.gather_poses(_LAST_GROUPING, list(range(start, start + wl["B"])), wl["J"], world, dev)
+            grouping["pose_all_gather_ms"] = round((time.perf_counter() - t2) * 1e3, 3)
+            grouping["gathered_images"] = len(ids)
+        except Exception as exc:  # informational field only: never lose the bench line over it
+            grouping["pose_all_gather_error"] = repr(exc)[:200]
 
     upd = wl["variant"] in ("attn", "mean")      # update block pre-applied in the edge pass (mpn.hip UPD)
     roof = roofline_for(dominant, stats_timed, E, wl, model.precision, upd) if dominant else None

@@ -2,8 +2,9 @@
 
 Images are independent units (the reference loops over them: ``ConstructGraph.py:58``,
 ``valid.py:95``), so a batch is split into contiguous image blocks per rank and every rank runs
-the whole path on its block with no data-path collective. The only collectives are the timing
-reductions of the benchmark (max of elapsed time, sum of work) and the barrier around it.
+the whole path on its block with no data-path collective. The collectives are the timing
+reductions of the benchmark (max of elapsed time, sum of work), the barrier around it, and after
+pose grouping the one pose all-gather of §8(e) (``gather_poses``).
 """
 import os
 
@@ -55,3 +56,47 @@ def max_over_ranks(v, world, dev):
 
 def sum_over_ranks(v, world, dev):
     return _reduce(v, world, dev, dist.ReduceOp.SUM)
+
+
+def gather_poses(per_image, image_ids, num_joints, world, dev):
+    """after each rank has grouped its own image block, one all_gather hands every rank the
+    poses of the whole batch, in global image order (rank order of the contiguous blocks).
+
+    per_image: this rank's list of float64 [P, J, 3] arrays or None (``pred_to_ann``'s "no poses");
+    image_ids: this rank's int image ids, same length. Returns (ids, poses) over all ranks. Records are
+    fixed-size ([cap, J, 3] f64 + person count + image id, cap = the largest P over all ranks, found by one
+    MAX all-reduce), blocks padded to the largest block; float64 keeps every value exact."""
+    n_local = len(per_image)
+    if len(image_ids) != n_local:
+        raise ValueError("gather_poses: per_image and image_ids differ in length")
+    if world == 1:
+        return list(image_ids), list(per_image)
+    p_local = max([0] + [0 if p is None else int(p.shape[0]) for p in per_image])
+    t = torch.tensor([p_local, n_local], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    cap, n_max = max(1, int(t[0])), max(1, int(t[1]))
+    rec = torch.zeros(n_max, cap, num_joints, 3, dtype=torch.float64)
+    meta = torch.full((n_max, 3), -1, dtype=torch.int64)   # (image id, person count or -1 for None, valid)
+    meta[:, 2] = 0
+    for k, (p, iid) in enumerate(zip(per_image, image_ids)):
+        meta[k, 0] = int(iid)
+        meta[k, 2] = 1
+        if p is not None:
+            rec[k, :p.shape[0]] = torch.from_numpy(p)
+            meta[k, 1] = p.shape[0]
+    rec, meta = rec.to(dev), meta.to(dev)
+    all_rec = torch.empty((world * n_max,) + tuple(rec.shape[1:]), dtype=rec.dtype, device=dev)
+    all_meta = torch.empty((world * n_max, 3), dtype=meta.dtype, device=dev)
+    dist.all_gather_into_tensor(all_rec, rec)
+    dist.all_gather_into_tensor(all_meta, meta)
+    all_rec = all_rec.cpu().numpy().reshape((world, n_max) + tuple(rec.shape[1:]))
+    all_meta = all_meta.cpu().numpy().reshape(world, n_max, 3)
+    ids, poses = [], []
+    for r in range(world):
+        for k in range(n_max):
+            iid, cnt, valid = all_meta[r, k]
+            if not valid:
+                continue
+            ids.append(int(iid))
+            poses.append(None if cnt < 0 else all_rec[r, k, :cnt].copy())
+    return ids, poses

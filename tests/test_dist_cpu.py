@@ -80,3 +80,43 @@ def test_gloo_world2_shards_reassemble(tmp_path):
     assert torch.equal(bi, full[12])
     assert all(p["t_max"] == world for p in parts)
     assert all(p["n_sum"] == full[0].shape[0] for p in parts)
+
+
+def _poses_for(img):
+    """Deterministic per-image pose arrays (None for some images, varying person counts)."""
+    rng = np.random.default_rng(img)
+    n = int(rng.integers(0, 5))
+    if n == 0:
+        return None
+    kp = rng.integers(0, 640, size=(n, J, 3)).astype(np.float64) + 0.25
+    kp[:, :, 2] = rng.random((n, J)).astype(np.float32)
+    kp[0, 0, 2] = 0.001
+    return kp
+
+
+def _pose_worker(rank, world, port, out_dir, total):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    r, w, dev = pdist.init_from_env("gloo")
+    s, e = pdist.image_block(total, r, w)
+    ids, poses = pdist.gather_poses([_poses_for(i) for i in range(s, e)], [1000 + i for i in range(s, e)], J, w, dev)
+    np.savez(os.path.join(out_dir, f"p{r}.npz"), ids=np.array(ids),
+             counts=np.array([-1 if p is None else len(p) for p in poses]),
+             flat=np.concatenate([p.reshape(-1) for p in poses if p is not None] or [np.zeros(0)]))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("total", [5, 4])
+def test_gloo_world2_gather_poses(tmp_path, total):
+    """The §8(e) pose all-gather: every rank ends with every image's poses, in global order, exact."""
+    world = 2
+    mp.start_processes(_pose_worker, args=(world, _free_port(), str(tmp_path), total), nprocs=world, join=True,
+                       start_method="spawn")
+    ref = [_poses_for(i) for i in range(total)]
+    for r in range(world):
+        z = np.load(tmp_path / f"p{r}.npz")
+        assert z["ids"].tolist() == [1000 + i for i in range(total)]
+        assert z["counts"].tolist() == [-1 if p is None else len(p) for p in ref]
+        flat = np.concatenate([p.reshape(-1) for p in ref if p is not None] or [np.zeros(0)])
+        np.testing.assert_array_equal(z["flat"], flat)
