@@ -203,6 +203,13 @@ int pemp_pose_persons(int B, const int64_t* node_off, const int32_t* labels, con
                       const float* class_probs, int J, int allow_single, int64_t cap, double* persons,
                       int32_t* person_count, int32_t* mutants);
 
+/* greedy_person_construction (Utils.py:517-626), HOST, per image over the surviving edges (w from
+ * pemp_pose_edge_weights method 1: pred, NaN = dropped; edge_index sorted by src): taken[ΣN] (image-local
+ * core node or -1), persons[cap][J][3] f64, person_count[B]. class_probs may be NULL. */
+int pemp_pose_greedy(int B, const int64_t* node_off, const int64_t* edge_index, int64_t E, const float* w,
+                     const int64_t* joint_det, const float* scores, const float* class_probs, int J, int32_t* taken,
+                     int64_t cap, double* persons, int32_t* person_count);
+
 /* Pose finishing, pred_to_ann (Utils.py:1468-1478) per image, keypoints [P][J][3] f64 (x, y, score):
  * pemp_pose_fill_mean (HOST): fill_mean, Utils.py:1468-1470.
  * pemp_pose_refine (GPU, keypoints in device memory, updated in place): refine, Utils.py:1026-1104 -- per

@@ -89,8 +89,8 @@ def load_reference_pose():
              ["cluster_graph", "extract_edge_matrix", "update_graph_with_edge_matrix", "cluster_andres_graph"], ns_cc)
     ns_u = {"np": npc, "torch": torch, "Graph": Graph, "cluster_graph": ns_cc["cluster_graph"],
             "dense_to_sparse": dense_to_sparse}
-    _extract(os.path.join(REF_SRC, "Utils", "Utils.py"), ["pred_to_person", "graph_cluster_to_persons", "to_numpy"],
-             ns_u)
+    _extract(os.path.join(REF_SRC, "Utils", "Utils.py"), ["pred_to_person", "graph_cluster_to_persons", "to_numpy",
+                                                         "greedy_person_construction"], ns_u)
     return ns_u
 
 
@@ -215,6 +215,30 @@ def main_refine():
         print(f"{name}: P={len(kp)} added={(refined[:, :, 2] == 0.001).sum()}")
 
 
+def main_greedy(ref):
+    """greedy_ fixtures: the pred_to_ann prefix with cc_method "greedy" (Utils.py:505-507, 517-626)."""
+    for name, spec in (("greedy_j17", dict(seed=21, J=17, persons=4, clutter=6)),
+                       ("greedy_noclass", dict(seed=22, J=17, persons=3, clutter=3, class_probs=False)),
+                       ("greedy_sparse_j14", dict(seed=23, J=14, persons=5, clutter=4, graph="sparse")),
+                       ("greedy_many", dict(seed=24, J=17, persons=9, clutter=12))):
+        J = spec["J"]
+        det, scores, ei, pred, cls = make_case(**spec)
+        th = 0.2
+        persons, taken = ref_pred_to_ann_persons(ref, det, scores, ei, pred, th, cls, "greedy", J, scores)
+        ei_s, p_s = subgraph(torch.from_numpy(scores > th), torch.from_numpy(ei), torch.from_numpy(pred))[:2]
+        mine, mine_taken = opose.greedy_person_construction(det, scores, p_s.numpy(), cls, ei_s.numpy(), J)
+        assert (persons is None) == (mine.ndim == 1), name
+        if persons is not None:
+            assert np.array_equal(persons, mine), name
+        assert np.array_equal(np.asarray(taken), mine_taken), name
+        np.savez_compressed(os.path.join(OUT, name + ".npz"), joint_det=det, joint_scores=scores, edge_index=ei,
+                            pred=pred, th=np.float32(th), num_joints=np.int64(J), has_class=np.bool_(cls is not None),
+                            class_probs=cls if cls is not None else np.zeros((0, J), np.float32),
+                            none=np.bool_(persons is None),
+                            persons=persons if persons is not None else np.zeros((0, J, 3)), taken=np.asarray(taken))
+        print(f"{name}: N={len(det)} persons={None if persons is None else len(persons)}")
+
+
 def main():
     main_refine()
     ref = load_reference_pose()
@@ -248,6 +272,7 @@ def main():
                    single_labels=single_labels, single_mutant=np.bool_(mutant), pose_scores=pose_sc)
         np.savez_compressed(os.path.join(OUT, name + ".npz"), **out)
         print(f"{name}: N={len(det)} E={ei.shape[1]} persons={None if persons is None else len(persons)}")
+    main_greedy(ref)
 
 
 if __name__ == "__main__":

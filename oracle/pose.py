@@ -256,3 +256,49 @@ def adjust(ans, det):
                 ans[pid, jid, 1] = x + 0.5
                 ans[pid, jid, 0] = y + 0.5
     return ans
+
+
+def greedy_person_construction(joint_det, preds_nodes, preds_edges, preds_classes, edge_index, num_joints):
+    """Utils.py:517-626 restated (numpy)."""
+    joint_det = joint_det.copy()
+    if preds_classes is not None:
+        joint_det[:, 2] = preds_classes.argmax(axis=1)
+    n = len(joint_det)
+    adj = np.zeros((n, n), dtype=np.float64)
+    adj[edge_index[0], edge_index[1]] = preds_edges
+    adj = (adj.T + adj) / 2.0
+    adj[np.diag_indices(n)] = 1.0
+    taken = np.zeros_like(preds_nodes, dtype=np.int32) - 1
+    for t in range(num_joints):
+        tj = joint_det[:, 2] == t
+        for i in range(n):
+            if not tj[i] or taken[i] != -1:
+                continue
+            if preds_nodes[i] < 0.5:
+                continue
+            taken[i] = i
+            for j in range(num_joints):
+                if j == t:
+                    continue
+                row = adj[i].copy()
+                row[joint_det[:, 2] != j] = 0.0
+                score, idx = np.max(row), np.argmax(row)
+                if score == 0.0 or idx == i:
+                    continue
+                if taken[idx] != -1 and adj[taken[idx], idx] > score:
+                    continue
+                taken[idx] = i
+    persons = []
+    for c in range(taken.max() + 1):
+        sel = taken == c
+        pj, ps = joint_det[sel], preds_nodes[sel]
+        if len(pj) > 1:
+            kp = np.zeros([num_joints, 3])
+            for t in range(num_joints):
+                s = pj[:, 2] == t
+                if s.sum():
+                    kp[t] = pj[s][np.argmax(ps[s])]
+                    kp[t, 2] = np.max(ps[s])
+            if (kp[:, 2] > 0).sum() > 0:
+                persons.append(kp)
+    return np.array(persons), taken

@@ -79,6 +79,7 @@ SIGNATURES = {
     "pemp_pose_edge_weights": (c_i32, [c_p, c_i64, c_p, c_p, c_f32, c_i32, c_p, c_i32, c_i32, c_p, c_p, c_p]),
     "pemp_pose_cluster": (c_i32, [c_i32, c_p, c_p, c_i64, c_p, c_p, c_i32, c_i32, c_p, c_p]),
     "pemp_pose_persons": (c_i32, [c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i32, c_i32, c_i64, c_p, c_p, c_p]),
+    "pemp_pose_greedy": (c_i32, [c_i32, c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_i32, c_p, c_i64, c_p, c_p]),
     "pemp_pose_fill_mean": (c_i32, [c_p, c_i32, c_i32]),
     "pemp_pose_refine_workspace_size": (c_sz, [c_i32, c_i32, c_i32, c_i32, c_i32]),
     "pemp_pose_refine": (c_i32, [c_p, c_p, c_i32, c_i32, c_i32, c_i32, c_p, c_i32, c_p, c_sz, c_p]),

@@ -701,3 +701,106 @@ extern "C" int pemp_pose_fill_mean(double* keypoints, int P, int J) {
   }
   return PEMP_OK;
 }
+
+// greedy_person_construction (Utils.py:517-626), host, per image: class re-typing (first argmax), the
+// float64 symmetric adjacency (adj + adj^T) / 2 of the surviving edges (w = pred, NaN = dropped; the
+// output of pemp_pose_edge_weights method 1), then type-major seeding: a free joint with node score >= 0.5
+// becomes a core and claims, per other type, its strongest neighbour (first maximum), taking it over from
+// an earlier core unless that core's edge is strictly stronger. Clusters are the joints claimed by one core
+// (cores in node order); persons as graph_cluster_to_persons without class re-typing of the keypoint rows.
+// taken[ΣN]: core node (image-local) or -1.
+extern "C" int pemp_pose_greedy(int B, const int64_t* node_off, const int64_t* edge_index, int64_t E, const float* w,
+                                const int64_t* joint_det, const float* scores, const float* class_probs, int J,
+                                int32_t* taken, int64_t cap, double* persons, int32_t* person_count) {
+  PEMP_CHECK_ARG(B >= 1 && J >= 1 && J <= 64 && E >= 0 && cap >= 0 && node_off && joint_det && scores && taken &&
+                     person_count && (E == 0 || (edge_index && w)) && (cap == 0 || persons),
+                 "pemp_pose_greedy: bad args");
+  int64_t out = 0;
+  int64_t e = 0;
+  for (int b = 0; b < B; ++b) {
+    const int64_t o = node_off[b], n = node_off[b + 1] - o;
+    std::vector<double> adj((size_t)(n * n), 0.0);
+    for (; e < E && edge_index[e] < node_off[b + 1]; ++e) {
+      if (std::isnan(w[e])) continue;
+      const int64_t s = edge_index[e] - o, d = edge_index[E + e] - o;
+      PEMP_CHECK_ARG(s >= 0 && d >= 0 && d < n, "pemp_pose_greedy: edge %lld crosses images", (long long)e);
+      adj[s * n + d] = (double)w[e];
+    }
+    std::vector<double> sym((size_t)(n * n));
+    for (int64_t i = 0; i < n; ++i)
+      for (int64_t k = 0; k < n; ++k) sym[i * n + k] = (adj[k * n + i] + adj[i * n + k]) / 2.0;
+    for (int64_t i = 0; i < n; ++i) sym[i * n + i] = 1.0;
+    std::vector<int> type(n);
+    for (int64_t i = 0; i < n; ++i) {
+      if (class_probs) {
+        const float* c = class_probs + (o + i) * J;
+        int best = 0;
+        for (int j = 1; j < J; ++j)
+          if (c[j] > c[best]) best = j;
+        type[i] = best;
+      } else {
+        type[i] = (int)joint_det[(o + i) * 3 + 2];
+      }
+    }
+    int32_t* tk = taken + o;
+    for (int64_t i = 0; i < n; ++i) tk[i] = -1;
+    for (int t = 0; t < J; ++t) {
+      for (int64_t i = 0; i < n; ++i) {
+        if (type[i] != t || tk[i] != -1) continue;
+        if (scores[o + i] < 0.5f) continue;
+        tk[i] = (int32_t)i;
+        for (int j = 0; j < J; ++j) {
+          if (j == t) continue;
+          double best = 0.0;  // np.max / np.argmax (first maximum) of the row with other types zeroed
+          int64_t idx = 0;
+          for (int64_t k = 0; k < n; ++k) {
+            const double v = type[k] == j ? sym[i * n + k] : 0.0;
+            if (k == 0 || v > best) {
+              best = v;
+              idx = k;
+            }
+          }
+          if (best == 0.0 || idx == i) continue;
+          if (tk[idx] != -1) {
+            if (sym[(int64_t)tk[idx] * n + idx] > best) continue;
+            tk[idx] = (int32_t)i;
+          } else {
+            tk[idx] = (int32_t)i;
+          }
+        }
+      }
+    }
+    int32_t mx = -1;
+    for (int64_t i = 0; i < n; ++i) mx = std::max(mx, tk[i]);
+    int32_t count = 0;
+    for (int32_t c = 0; c <= mx; ++c) {
+      std::vector<int64_t> m;
+      for (int64_t i = 0; i < n; ++i)
+        if (tk[i] == c) m.push_back(i);
+      if (m.size() <= 1) continue;
+      double kp[64 * 3];
+      std::fill(kp, kp + J * 3, 0.0);
+      for (int t = 0; t < J; ++t) {
+        int64_t bsel = -1;
+        for (int64_t i : m)
+          if (type[i] == t && (bsel < 0 || scores[o + i] > scores[o + bsel])) bsel = i;
+        if (bsel < 0) continue;
+        kp[t * 3 + 0] = (double)joint_det[(o + bsel) * 3 + 0];
+        kp[t * 3 + 1] = (double)joint_det[(o + bsel) * 3 + 1];
+        kp[t * 3 + 2] = (double)scores[o + bsel];
+      }
+      bool emit = false;
+      for (int t = 0; t < J; ++t) emit |= kp[t * 3 + 2] > 0.0;
+      if (!emit) continue;
+      if (out >= cap) {
+        ::pemp::set_error("pemp_pose_greedy: more than cap = %lld persons", (long long)cap);
+        return PEMP_ERR_WORKSPACE;
+      }
+      std::copy(kp, kp + J * 3, persons + out * J * 3);
+      ++out;
+      ++count;
+    }
+    person_count[b] = count;
+  }
+  return PEMP_OK;
+}

@@ -12,8 +12,8 @@ Work split (include/pemp.h, ``pemp_pose_*``): the per-edge pass (subgraph test, 
 transpose averaging) is one HIP kernel over the whole batch; its output and the node arrays come back in
 one stream-ordered copy into pinned memory; greedy additive edge contraction (sequential by nature) and the
 person assembly run in C++ in the same library, one image per host thread. No numpy / scipy / Python loop
-sits on the path. ``greedy``, ``MUT`` and ``KL`` are not built (NotImplementedError, as the reference
-raises for unknown methods).
+sits on the path. ``greedy`` (``Utils.py:517-626``) runs on the host after the same edge pass
+(``pemp_pose_greedy``). ``MUT`` and ``KL`` are not built (NotImplementedError).
 """
 import os
 
@@ -22,12 +22,12 @@ import torch
 
 from . import _lib
 
-_METHODS = {"GAEC": 0, "threshold": 1}
+_METHODS = {"GAEC": 0, "threshold": 1, "greedy": 1}   # greedy: the edge pass keeps raw preds, like threshold
 
 
 def _method(cc_method):
     if cc_method not in _METHODS:
-        raise NotImplementedError(f"cc_method={cc_method!r}: pemp_amd builds GAEC and threshold")
+        raise NotImplementedError(f"cc_method={cc_method!r}: pemp_amd builds GAEC, threshold and greedy")
     return _METHODS[cc_method]
 
 
@@ -91,6 +91,19 @@ def _run(joint_det, joint_scores, edge_index, pred, node_off, th, use_th, class_
         t1 = time.perf_counter()
         timings["to_host"] = timings.get("to_host", 0.0) + t1 - t0
         t0 = t1
+    if cc_method == "greedy":
+        if h_flags[B] & 1:
+            raise ValueError("pemp_amd.pose: edge_index is not sorted by (src, dst) without duplicates")
+        cap = max(N, 1)
+        taken = np.empty(N, dtype=np.int32)
+        persons = np.empty((cap, num_joints, 3), dtype=np.float64)
+        counts = np.empty(B, dtype=np.int32)
+        _lib.check(L.pemp_pose_greedy(B, node_off.ctypes.data, h_ei.data_ptr(), E, h_w.data_ptr(), h_det.data_ptr(),
+                                      h_sc.data_ptr(), None if h_cls is None else h_cls.data_ptr(), num_joints,
+                                      taken.ctypes.data, cap, persons.ctypes.data, counts.ctypes.data), L)
+        starts = np.concatenate([[0], np.cumsum(counts)])
+        per_image = [persons[starts[b]:starts[b + 1]].copy() for b in range(B)]
+        return per_image, np.zeros(B, dtype=bool), taken, h_flags.numpy()
     labels = np.empty(N, dtype=np.int32)
     n_comp = np.empty(B, dtype=np.int32)
     _lib.check(L.pemp_pose_cluster(B, node_off.ctypes.data, h_ei.data_ptr(), E, h_w.data_ptr(),

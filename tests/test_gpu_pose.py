@@ -184,3 +184,24 @@ def test_refine_rounding_boundaries(F, seed):
     ref = opose.refine(s, tg, kp.copy())
     got = ppose.refine(dev(s), dev(tg), kp.copy())
     np.testing.assert_array_equal(got, ref)
+
+
+from tests.test_pose_cpu import GREEDY  # noqa: E402
+
+
+@pytest.mark.parametrize("name", GREEDY)
+def test_greedy_golden(name):
+    g = load(name)
+    J = int(g["num_joints"])
+    cls = dev(g["class_probs"]) if g["has_class"] else None
+    out = ppose.group_persons(dev(g["joint_det"]), dev(g["joint_scores"]), dev(g["edge_index"]), dev(g["pred"]),
+                              float(g["th"]), cls, "greedy", J, score_map_scores=dev(g["joint_scores"]))
+    if g["none"]:
+        assert out[0] is None
+    else:
+        np.testing.assert_array_equal(out[0], g["persons"])
+    ei_s, p_s = opose.subgraph(g["joint_scores"] > g["th"], g["edge_index"], g["pred"])
+    persons, mutant, taken = ppose.pred_to_person(dev(g["joint_det"]), dev(g["joint_scores"]), dev(ei_s), dev(p_s),
+                                                  cls, "greedy", J)
+    np.testing.assert_array_equal(taken, g["taken"])
+    assert mutant is False

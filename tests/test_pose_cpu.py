@@ -192,3 +192,36 @@ def test_host_fill_mean_fixture(name):
     kp = g["keypoints"].copy()
     ppose.fill_mean(kp)
     np.testing.assert_array_equal(kp, g["filled"])
+
+
+GREEDY = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.startswith("greedy_") and f.endswith(".npz"))
+
+
+@pytest.mark.parametrize("name", GREEDY)
+def test_greedy_oracle_and_host_fixture(name):
+    """greedy_person_construction: oracle and pemp_pose_greedy (host C++) against the reference's own
+    function's output (pred_to_ann prefix with cc_method "greedy")."""
+    g = load(name)
+    J = int(g["num_joints"])
+    cls = g["class_probs"] if g["has_class"] else None
+    ei_s, p_s = opose.subgraph(g["joint_scores"] > g["th"], g["edge_index"], g["pred"])
+    persons, taken = opose.greedy_person_construction(g["joint_det"], g["joint_scores"], p_s, cls, ei_s, J)
+    np.testing.assert_array_equal(taken, g["taken"])
+    if not g["none"]:
+        np.testing.assert_array_equal(persons, g["persons"])
+    # host C++ on the edge pass (method 1: surviving preds, NaN elsewhere)
+    L = _lib.load_cdll()
+    N = len(g["joint_det"])
+    off = np.array([0, N], np.int64)
+    ei = np.ascontiguousarray(g["edge_index"], np.int64)
+    w, _ = edge_pass(ei, g["pred"], g["joint_scores"], g["th"], True, off, 1)
+    tk = np.empty(N, np.int32)
+    out = np.empty((N, J, 3))
+    cnt = np.empty(1, np.int32)
+    det = np.ascontiguousarray(g["joint_det"], np.int64)
+    sc = np.ascontiguousarray(g["joint_scores"], np.float32)
+    cls_p = None if cls is None else np.ascontiguousarray(cls, np.float32).ctypes.data
+    _lib.check(L.pemp_pose_greedy(1, off.ctypes.data, ei.ctypes.data, ei.shape[1], w.ctypes.data, det.ctypes.data,
+                                  sc.ctypes.data, cls_p, J, tk.ctypes.data, N, out.ctypes.data, cnt.ctypes.data), L)
+    np.testing.assert_array_equal(tk, g["taken"])
+    np.testing.assert_array_equal(out[:cnt[0]], g["persons"])
