@@ -182,7 +182,10 @@ void gaec_dense(size_t n, const std::vector<size_t>& ea, const std::vector<size_
       ++deg[b];
     }
   };
-  std::priority_queue<GaecEdge16> q;
+  // the queue's vector reserved up front (initial edges + one push per neighbour per contraction bound)
+  std::vector<GaecEdge16> qstore;
+  qstore.reserve(ea.size() + n * 8 + 64);
+  std::priority_queue<GaecEdge16> q(std::less<GaecEdge16>(), std::move(qstore));
   for (size_t i = 0; i < ea.size(); ++i) {
     link(ea[i], eb[i]);
     wt[ea[i] * n + eb[i]] += ew[i];
