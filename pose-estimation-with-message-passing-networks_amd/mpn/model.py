@@ -249,9 +249,16 @@ class NodeClassificationMPNSimple(nn.Module):
         ws = self._ws.get(L.pemp_mpn_workspace_size(desc, N, E), dev)
         st = _lib.stream(dev)
         fw = self._weights(dev)
-        edge_logits = torch.empty(max(n_rec, 1), E, dtype=torch.float32, device=dev)
-        node_logits = torch.empty(n_rec + 1, N, dtype=torch.float32, device=dev)
-        class_logits = torch.empty(n_rec + 1, N, self.num_joints, dtype=torch.float32, device=dev)
+        # the three logit arrays share one allocation (one caching-allocator call per forward instead of
+        # three); each segment starts on a 256-byte boundary
+        ne, nn_ = max(n_rec, 1) * E, (n_rec + 1) * N
+        nc = nn_ * self.num_joints
+        a1 = (ne + 63) // 64 * 64
+        a2 = a1 + (nn_ + 63) // 64 * 64
+        buf = torch.empty(a2 + nc, dtype=torch.float32, device=dev)
+        edge_logits = buf[:ne].view(max(n_rec, 1), E)
+        node_logits = buf[a1:a1 + nn_].view(n_rec + 1, N)
+        class_logits = buf[a2:a2 + nc].view(n_rec + 1, N, self.num_joints)
         if fully is not None:       # the graph constructor's fully graph: closed-form edge order
             noff, offs, B = fully
             _lib.check(L.pemp_mpn_forward_fully(desc, fw.struct_ref, x.data_ptr(), edge_attr.data_ptr(),
