@@ -102,14 +102,16 @@ def test_group_persons_batched():
             np.testing.assert_array_equal(out[b], ref)
 
 
-@pytest.mark.parametrize("method", ["GAEC", "threshold"])
-def test_end_to_end_after_mpn(method):
+@pytest.mark.parametrize("method,graph,persons", [("GAEC", "fully", 3), ("threshold", "fully", 3),
+                                                   ("GAEC", "knn", 5), ("greedy", "knn", 5)])
+def test_end_to_end_after_mpn(method, graph, persons):
     """construct_graph -> MPN -> sigmoid/softmax (valid.py:109-111) -> group_persons on the GPU, against
-    the oracle's pred_to_ann prefix on the SAME probabilities (copied to the host)."""
+    the oracle's pred_to_ann prefix on the SAME probabilities (copied to the host). The knn case (85
+    nodes per image, k = 50) exercises a graph that is not complete."""
     B, J, H, W = 2, 17, 128, 128
-    hm = torch.from_numpy(syn.make_heatmaps(5, B, J, H, W, persons=3))
+    hm = torch.from_numpy(syn.make_heatmaps(5, B, J, H, W, persons=persons))
     feats = torch.from_numpy(syn.closed_form((B, 128, H, W), 0.25))
-    gc = pcfg.inference_gc_config("fully", 5, False)
+    gc = pcfg.inference_gc_config(graph, 5, False)
     out = pemp_amd.get_graph_constructor(gc, scoremaps=hm.to(DEV), features=feats.to(DEV), tagmaps=None,
                                          joints_gt=None, factor_list=None, masks=None, device=DEV, testing=True,
                                          heatmaps=None, num_joints=J).construct_graph()
@@ -127,8 +129,13 @@ def test_end_to_end_after_mpn(method):
         nm = h[5] == b
         lo = int(np.nonzero(nm)[0][0])
         em = nm[h[2][0]]
-        ref = opose.pred_to_ann_persons(h[0][nm], h[1][nm], h[2][:, em] - lo, h[3][em], np.float32(0.1), h[4][nm],
-                                        method, J, h[6][nm])
+        if method == "greedy":
+            ei_s, p_s = opose.subgraph(h[1][nm] > np.float32(0.1), h[2][:, em] - lo, h[3][em])
+            ref, _ = opose.greedy_person_construction(h[0][nm], h[1][nm], p_s, h[4][nm], ei_s, J)
+            ref = None if ref.ndim == 1 or not (h[6][nm] > 0.1).any() or ei_s.shape[1] == 0 else ref
+        else:
+            ref = opose.pred_to_ann_persons(h[0][nm], h[1][nm], h[2][:, em] - lo, h[3][em], np.float32(0.1),
+                                            h[4][nm], method, J, h[6][nm])
         if ref is None:
             assert got[b] is None
         else:
