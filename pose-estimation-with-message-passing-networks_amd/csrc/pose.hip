@@ -494,9 +494,9 @@ __device__ __forceinline__ unsigned long long refine_key(float v, uint32_t idx) 
 // end are clamped to the last pixel (a true candidate with its own index). A thread visits its pixels in
 // increasing order, so a strict > keeps the first maximum; (value, index) pairs become ordered 64-bit keys
 // only for the cross-thread reduction.
-template <int PC>
+template <int PC, int F>
 __global__ __launch_bounds__(256) void refine_argmax_kernel(const float* __restrict__ s, const float* __restrict__ tag,
-                                                            int H, int W, int F, const float* __restrict__ mean_tag,
+                                                            int H, int W, const float* __restrict__ mean_tag,
                                                             int P, unsigned long long* __restrict__ keys, int J) {
   const int i = blockIdx.y;
   const int p0 = blockIdx.z * PC;
@@ -532,12 +532,17 @@ __global__ __launch_bounds__(256) void refine_argmax_kernel(const float* __restr
 #pragma unroll
       for (int q = 0; q < PC; ++q) {
         const float d0 = __fsub_rn(t0[u], mt0[q]);
-        float ss = __fmul_rn(d0, d0);
+        float k;
         if (F == 2) {
           const float d1 = __fsub_rn(t1[u], mt1[q]);
-          ss = __fadd_rn(ss, __fmul_rn(d1, d1));
+          k = rintf(__fsqrt_rn(__fadd_rn(__fmul_rn(d0, d0), __fmul_rn(d1, d1))));
+        } else {
+          // F = 1: in binary floating point with round-to-nearest, sqrt(RN(d * d)) == |d| whenever d * d
+          // neither overflows nor underflows (an underflow only happens for |d| < 2^-63, where both round
+          // to 0), so rint(sqrt(d^2)) = rint(|d|) with no square root; d^2 = inf gives inf as in numpy
+          k = isinf(__fmul_rn(d0, d0)) ? INFINITY : rintf(fabsf(d0));
         }
-        const float v = __fsub_rn(sv[u], rintf(__fsqrt_rn(ss)));
+        const float v = __fsub_rn(sv[u], k);
         const bool better = v > bv[q];
         bv[q] = better ? v : bv[q];
         bi[q] = better ? pxs[u] : bi[q];
@@ -650,10 +655,14 @@ extern "C" int pemp_pose_refine(const float* scoremaps, const float* tag, int J,
   const int chunks = (P + 15) / 16, per = (P + chunks - 1) / chunks;
   const int pc = per <= 2 ? 2 : per <= 4 ? 4 : per <= 6 ? 6 : per <= 8 ? 8 : per <= 10 ? 10 : per <= 12 ? 12 : 16;
   const dim3 grid(bx, J, (P + pc - 1) / pc);
-#define PEMP_REFINE_LAUNCH(N)                                                                                    \
-  case N:                                                                                                        \
-    hipLaunchKernelGGL(refine_argmax_kernel<N>, grid, dim3(256), 0, st, scoremaps, tag, H, W, F, mean_tag, P, keys, \
-                       J);                                                                                       \
+#define PEMP_REFINE_LAUNCH(N)                                                                                   \
+  case N:                                                                                                       \
+    if (F == 1)                                                                                                 \
+      hipLaunchKernelGGL((refine_argmax_kernel<N, 1>), grid, dim3(256), 0, st, scoremaps, tag, H, W, mean_tag, P,  \
+                         keys, J);                                                                              \
+    else                                                                                                        \
+      hipLaunchKernelGGL((refine_argmax_kernel<N, 2>), grid, dim3(256), 0, st, scoremaps, tag, H, W, mean_tag, P,  \
+                         keys, J);                                                                              \
     break;
   switch (pc) {
     PEMP_REFINE_LAUNCH(2)

@@ -212,3 +212,24 @@ def test_greedy_golden(name):
                                                   cls, "greedy", J)
     np.testing.assert_array_equal(taken, g["taken"])
     assert mutant is False
+
+
+@pytest.mark.parametrize("mode", ["some", "all"])
+def test_refine_tag_distance_overflow(mode):
+    """|tag - mean| so large that its square overflows (numpy: inf, so s - inf = -inf): those pixels never
+    win, and when every pixel overflows the first pixel is the argmax, as np.argmax of all -inf."""
+    rng = np.random.default_rng(3)
+    J, H, W = 2, 8, 96
+    tag = np.zeros((J, H, W), np.float32)
+    big = np.float32(3e19)
+    if mode == "all":
+        tag[1] = big
+    else:
+        tag[1] = np.where(rng.random((H, W)) < 0.5, big, rng.normal(0, 2, (H, W))).astype(np.float32)
+    s = rng.random((J, H, W)).astype(np.float32)
+    kp = np.zeros((1, J, 3))
+    kp[0, 0] = (5, 4, 0.9)
+    with np.errstate(over="ignore"):
+        ref = opose.refine(s, tag, kp.copy())
+    got = ppose.refine(dev(s), dev(tag), kp.copy())
+    np.testing.assert_array_equal(got, ref)
