@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define PEMP_ABI_VERSION 8
+#define PEMP_ABI_VERSION 9
 
 enum {
   PEMP_OK = 0,
@@ -194,8 +194,9 @@ int pemp_edge_features(const int64_t* joint_det /*[N,3]*/, const float* joint_ta
  *    first argmax when non-NULL; pose_scores replaces the score when non-NULL), person_count[B],
  *    mutants[B] (a component larger than J). PEMP_ERR_WORKSPACE when more than cap persons. */
 int pemp_pose_edge_weights(const int64_t* edge_index, int64_t E, const float* pred, const float* node_scores,
-                           float th, int use_th, const int64_t* node_off /*[B+1] device*/, int B, int method,
-                           float* w, int* flags, void* stream);
+                           float th, int use_th, const int64_t* node_off /*[B+1] device*/, int B, int64_t N,
+                           int method, int64_t* row_start /*[N+1] device scratch*/, float* w, int* flags,
+                           void* stream);
 int pemp_pose_cluster(int B, const int64_t* node_off, const int64_t* edge_index, int64_t E, const float* w,
                       const int* flags, int method, int n_threads, int32_t* labels, int32_t* n_comp);
 int pemp_pose_persons(int B, const int64_t* node_off, const int32_t* labels, const int32_t* n_comp,

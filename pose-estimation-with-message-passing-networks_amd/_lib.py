@@ -8,7 +8,7 @@ import os
 
 LIB_PATH = os.environ.get("PEMP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc",
                                                      "libpemp.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 ERR_INVALID_ARG, ERR_HIP, ERR_WORKSPACE, ERR_UNSUPPORTED = -1, -2, -3, -4
 
@@ -76,7 +76,8 @@ SIGNATURES = {
     "pemp_mpn_node_image_floats": (c_sz, [ctypes.POINTER(PempMpnWeights)]),
     "pemp_mpn_node_image": (c_i32, [ctypes.POINTER(PempMpnWeights), c_p, c_sz, c_p]),
     "pemp_mpn_status": (c_i32, [ctypes.POINTER(PempMpnDesc), c_i64, c_i64, c_p, c_p]),
-    "pemp_pose_edge_weights": (c_i32, [c_p, c_i64, c_p, c_p, c_f32, c_i32, c_p, c_i32, c_i32, c_p, c_p, c_p]),
+    "pemp_pose_edge_weights": (c_i32, [c_p, c_i64, c_p, c_p, c_f32, c_i32, c_p, c_i32, c_i64, c_i32, c_p, c_p, c_p,
+                                       c_p]),
     "pemp_pose_cluster": (c_i32, [c_i32, c_p, c_p, c_i64, c_p, c_p, c_i32, c_i32, c_p, c_p]),
     "pemp_pose_persons": (c_i32, [c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i32, c_i32, c_i64, c_p, c_p, c_p]),
     "pemp_pose_greedy": (c_i32, [c_i32, c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_i32, c_p, c_i64, c_p, c_p]),

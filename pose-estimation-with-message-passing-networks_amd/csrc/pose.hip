@@ -12,8 +12,8 @@
 //   Utils.py:672-743            graph_cluster_to_persons: connected components (scipy labels: in order of
 //                               each component's lowest node), class re-typing, best-scoring joint per type
 //
-// The edge pass is a GPU kernel over the batched graph (one thread per edge, reverse edge found by binary
-// search in the (src, dst)-sorted edge list). Greedy additive edge contraction is inherently sequential: it
+// The edge pass is a GPU kernel over the batched graph (one thread per edge; the reverse edge is found by a
+// binary search inside its CSR row of the (src, dst)-sorted edge list). Greedy additive edge contraction is inherently sequential: it
 // runs on the host, one image per thread, restating andres::graph::multicut::greedyAdditiveEdgeContraction
 // (andres graph, the library behind the reference's missing andres_graph_wrapper; not vendored): a max-heap of
 // (a, b, w, edition) entries ordered by w only (std::priority_queue, so ties resolve exactly as libstdc++'s
@@ -34,25 +34,29 @@ using namespace pemp;
 
 namespace {
 
-__device__ __forceinline__ int pose_find_image(const int64_t* off, int n, int64_t v) {
-  int lo = 0, hi = n;  // off[lo] <= v < off[hi]
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (off[mid] <= v) lo = mid; else hi = mid;
+// row_start[v] = first edge with src >= v (v = 0..N): the CSR rows of the (src, dst)-sorted edge list
+__global__ __launch_bounds__(256) void pose_row_start_kernel(const int64_t* __restrict__ ei, int64_t E, int64_t N,
+                                                             int64_t* __restrict__ row_start) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v > N) return;
+  int64_t lo = 0, hi = E;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (ei[mid] < v) lo = mid + 1; else hi = mid;
   }
-  return lo;
+  row_start[v] = lo;
 }
 
 // w[e] = fl32(pred[e] + pred[rev(e)]) for a surviving upper edge (src < dst) in mode 0 (GAEC), pred[e] for
-// every surviving edge in mode 1 (threshold), NaN otherwise. flags[b]: bit 0 = a surviving lower-triangle
-// edge of image b has pred != 0 (extract_edge_matrix then averages), bit 1 = image b keeps an edge.
-// flags[B] bit 0: edge_index is not strictly (src, dst)-sorted.
+// every surviving edge in mode 1 (threshold), NaN otherwise. flags[B] bit 0: edge_index is not strictly
+// (src, dst)-sorted (the per-image bits come from pose_image_flags_kernel).
 __global__ __launch_bounds__(256) void pose_edge_weights_kernel(const int64_t* __restrict__ ei, int64_t E,
                                                                 const float* __restrict__ pred,
                                                                 const float* __restrict__ score, float th,
                                                                 int use_th, const int64_t* __restrict__ node_off,
-                                                                int B, int mode, float* __restrict__ w,
-                                                                int* __restrict__ flags) {
+                                                                int B, int mode,
+                                                                const int64_t* __restrict__ row_start, int64_t N,
+                                                                float* __restrict__ w, int* __restrict__ flags) {
   for (int64_t e0 = (int64_t)blockIdx.x * blockDim.x; e0 < E; e0 += (int64_t)gridDim.x * blockDim.x) {
     const int64_t e = e0 + threadIdx.x;
     const bool live = e < E;
@@ -62,36 +66,51 @@ __global__ __launch_bounds__(256) void pose_edge_weights_kernel(const int64_t* _
       if (s1 < s || (s1 == s && d1 <= d)) atomicOr(&flags[B], 1);
     }
     const bool keep = live && (!use_th || (score[s] > th && score[d] > th));
-    const int b = pose_find_image(node_off, B, s);
     const float p = live ? pred[e] : 0.f;
-    // per-image flag bits, OR-reduced over the wave first (a wave's edges nearly always share an image):
-    // one atomic per wave instead of one per edge
-    const int bits = keep ? (2 | ((s > d && p != 0.f) ? 1 : 0)) : 0;
-    const int b0 = __shfl(b, 0);
-    if (__all(b == b0)) {
-      int r = bits;
-      for (int o = 32; o > 0; o >>= 1) r |= __shfl_xor(r, o);
-      if ((threadIdx.x & 63) == 0 && r) atomicOr(&flags[b0], r);
-    } else if (bits) {
-      atomicOr(&flags[b], bits);
-    }
     float out = __int_as_float(0x7fc00000);
     if (keep) {
       if (mode == 1) {
         out = p;
       } else if (s < d) {
-        int64_t lo = 0, hi = E;  // first edge with key >= (d, s)
+        // reverse edge (d, s): binary search for dst == s inside row d only (a few cached steps)
+        int64_t lo = 0, hi = 0;
+        if (d >= 0 && d < N) {
+          lo = row_start[d];
+          hi = row_start[d + 1];
+        }
         while (lo < hi) {
           const int64_t mid = (lo + hi) >> 1;
-          const int64_t ms = ei[mid], md = ei[E + mid];
-          if (ms < d || (ms == d && md < s)) lo = mid + 1; else hi = mid;
+          if (ei[E + mid] < s) lo = mid + 1; else hi = mid;
         }
-        const float q = (lo < E && ei[lo] == d && ei[E + lo] == s) ? pred[lo] : 0.f;
+        const float q = (lo < E && d >= 0 && d < N && lo < row_start[d + 1] && ei[E + lo] == s) ? pred[lo] : 0.f;
         out = p + q;
       }
     }
     if (live) w[e] = out;
   }
+}
+
+// flags[b] (bit 0: a surviving src > dst edge with pred != 0; bit 1: a surviving edge) over image b's edge
+// range [row_start[node_off[b]], row_start[node_off[b + 1]]): grid (chunks, B), a block-wide OR per chunk and
+// one atomic per block (a handful per image instead of one per wave on a few hot addresses).
+__global__ __launch_bounds__(256) void pose_image_flags_kernel(const int64_t* __restrict__ ei, int64_t E,
+                                                               const float* __restrict__ pred,
+                                                               const float* __restrict__ score, float th, int use_th,
+                                                               const int64_t* __restrict__ node_off,
+                                                               const int64_t* __restrict__ row_start,
+                                                               int* __restrict__ flags) {
+  const int b = blockIdx.y;
+  const int64_t lo = row_start[node_off[b]], hi = row_start[node_off[b + 1]];
+  const int64_t chunk = (hi - lo + gridDim.x - 1) / gridDim.x;
+  const int64_t c0 = lo + chunk * blockIdx.x, c1 = min(hi, c0 + chunk);
+  int bits = 0;
+  for (int64_t e = c0 + threadIdx.x; e < c1; e += blockDim.x) {
+    const int64_t s = ei[e], d = ei[E + e];
+    if (use_th && !(score[s] > th && score[d] > th)) continue;
+    bits |= 2 | ((s > d && pred[e] != 0.f) ? 1 : 0);
+  }
+  const int b1 = __syncthreads_or(bits & 1), b2 = __syncthreads_or(bits & 2);
+  if (threadIdx.x == 0 && (b1 | b2)) atomicOr(&flags[b], (b1 ? 1 : 0) | (b2 ? 2 : 0));
 }
 
 struct GaecEdge {
@@ -258,16 +277,22 @@ void union_join(std::vector<size_t>& parent, size_t a, size_t b) {
 
 extern "C" int pemp_pose_edge_weights(const int64_t* edge_index, int64_t E, const float* pred,
                                       const float* node_scores, float th, int use_th, const int64_t* node_off, int B,
-                                      int method, float* w, int* flags, void* stream) {
-  PEMP_CHECK_ARG(E >= 0 && B >= 1 && (method == 0 || method == 1), "pemp_pose_edge_weights: bad args");
-  PEMP_CHECK_ARG(node_off && flags && (E == 0 || (edge_index && pred && w)) && (!use_th || node_scores),
+                                      int64_t N, int method, int64_t* row_start, float* w, int* flags, void* stream) {
+  PEMP_CHECK_ARG(E >= 0 && B >= 1 && N >= 0 && (method == 0 || method == 1), "pemp_pose_edge_weights: bad args");
+  PEMP_CHECK_ARG(node_off && flags && (E == 0 || (edge_index && pred && w && row_start)) && (!use_th || node_scores),
                  "pemp_pose_edge_weights: null pointer");
   PEMP_HIP(hipMemsetAsync(flags, 0, sizeof(int) * (B + 1), as_stream(stream)));
   if (E == 0) return PEMP_OK;
   ProfScope prof("pose_edge_weights", as_stream(stream));
+  hipLaunchKernelGGL(pose_row_start_kernel, dim3((unsigned)((N + 1 + 255) / 256)), dim3(256), 0, as_stream(stream),
+                     edge_index, E, N, row_start);
+  PEMP_LAUNCH_CHECK();
   const int64_t blocks = std::min<int64_t>((E + 255) / 256, 8192);
   hipLaunchKernelGGL(pose_edge_weights_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), edge_index,
-                     E, pred, node_scores, th, use_th, node_off, B, method, w, flags);
+                     E, pred, node_scores, th, use_th, node_off, B, method, row_start, N, w, flags);
+  PEMP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(pose_image_flags_kernel, dim3(16, B), dim3(256), 0, as_stream(stream), edge_index, E, pred,
+                     node_scores, th, use_th, node_off, row_start, flags);
   PEMP_LAUNCH_CHECK();
   return PEMP_OK;
 }

@@ -74,8 +74,10 @@ def _run(joint_det, joint_scores, edge_index, pred, node_off, th, use_th, class_
     off_d = torch.from_numpy(node_off).to(dev)
     w = torch.empty(E, dtype=torch.float32, device=dev)
     flags = torch.empty(B + 1, dtype=torch.int32, device=dev)
+    row_start = torch.empty(N + 1, dtype=torch.int64, device=dev)
     _lib.check(L.pemp_pose_edge_weights(_lib.ptr(ei), E, _lib.ptr(pr), _lib.ptr(sc), float(th), int(use_th),
-                                        _lib.ptr(off_d), B, method, _lib.ptr(w), _lib.ptr(flags), _lib.stream(dev)))
+                                        _lib.ptr(off_d), B, N, method, _lib.ptr(row_start), _lib.ptr(w),
+                                        _lib.ptr(flags), _lib.stream(dev)))
     cls = class_pred.to(torch.float32).contiguous() if class_pred is not None else None
     if cls is not None and cls.shape != (N, num_joints):
         raise ValueError(f"pemp_amd.pose: class_pred {tuple(cls.shape)} != ({N}, {num_joints})")

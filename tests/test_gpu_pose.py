@@ -63,8 +63,10 @@ def test_edge_pass_kernel_bits(method):
     flags = torch.empty(B + 1, dtype=torch.int32, device=DEV)
     L = _lib.lib()
     d_ei, d_pr, d_sc, d_off = dev(ei), dev(pr), dev(sc), dev(off)
+    rs = torch.empty(int(off[-1]) + 1, dtype=torch.int64, device=DEV)
     _lib.check(L.pemp_pose_edge_weights(d_ei.data_ptr(), E, d_pr.data_ptr(), d_sc.data_ptr(), 0.3, 1,
-                                        d_off.data_ptr(), B, method, w.data_ptr(), flags.data_ptr(), _lib.stream(DEV)))
+                                        d_off.data_ptr(), B, int(off[-1]), method, rs.data_ptr(), w.data_ptr(),
+                                        flags.data_ptr(), _lib.stream(DEV)))
     ref_w, ref_flags = edge_pass(ei, pr, sc, np.float32(0.3), True, off, method)
     np.testing.assert_array_equal(w.cpu().numpy().view(np.int32), ref_w.view(np.int32))
     np.testing.assert_array_equal(flags.cpu().numpy(), ref_flags)
