@@ -279,7 +279,7 @@ extern "C" int pemp_pose_edge_weights(const int64_t* edge_index, int64_t E, cons
                                       const float* node_scores, float th, int use_th, const int64_t* node_off, int B,
                                       int64_t N, int method, int64_t* row_start, float* w, int* flags, void* stream) {
   PEMP_CHECK_ARG(E >= 0 && B >= 1 && N >= 0 && (method == 0 || method == 1), "pemp_pose_edge_weights: bad args");
-  PEMP_CHECK_ARG(node_off && flags && (E == 0 || (edge_index && pred && w && row_start)) && (!use_th || node_scores),
+  PEMP_CHECK_ARG(node_off && flags && (E == 0 || (edge_index && pred && w && row_start && (!use_th || node_scores))),
                  "pemp_pose_edge_weights: null pointer");
   PEMP_HIP(hipMemsetAsync(flags, 0, sizeof(int) * (B + 1), as_stream(stream)));
   if (E == 0) return PEMP_OK;
@@ -380,9 +380,10 @@ extern "C" int pemp_pose_persons(int B, const int64_t* node_off, const int32_t* 
                                  const int64_t* joint_det, const float* scores, const float* pose_scores,
                                  const float* class_probs, int J, int allow_single, int64_t cap, double* persons,
                                  int32_t* person_count, int32_t* mutants) {
-  PEMP_CHECK_ARG(B >= 1 && J >= 1 && cap >= 0 && node_off && labels && n_comp && joint_det && scores &&
-                     person_count && mutants && (cap == 0 || persons),
+  PEMP_CHECK_ARG(B >= 1 && J >= 1 && cap >= 0 && node_off && n_comp && person_count && mutants &&
+                     (cap == 0 || persons),
                  "pemp_pose_persons: bad args");
+  PEMP_CHECK_ARG(node_off[B] == 0 || (labels && joint_det && scores), "pemp_pose_persons: null node arrays");
   int64_t out = 0;
   for (int b = 0; b < B; ++b) {
     const int64_t o = node_off[b], n = node_off[b + 1] - o;
@@ -749,9 +750,10 @@ extern "C" int pemp_pose_fill_mean(double* keypoints, int P, int J) {
 extern "C" int pemp_pose_greedy(int B, const int64_t* node_off, const int64_t* edge_index, int64_t E, const float* w,
                                 const int64_t* joint_det, const float* scores, const float* class_probs, int J,
                                 int32_t* taken, int64_t cap, double* persons, int32_t* person_count) {
-  PEMP_CHECK_ARG(B >= 1 && J >= 1 && J <= 64 && E >= 0 && cap >= 0 && node_off && joint_det && scores && taken &&
-                     person_count && (E == 0 || (edge_index && w)) && (cap == 0 || persons),
+  PEMP_CHECK_ARG(B >= 1 && J >= 1 && J <= 64 && E >= 0 && cap >= 0 && node_off && person_count &&
+                     (E == 0 || (edge_index && w)) && (cap == 0 || persons),
                  "pemp_pose_greedy: bad args");
+  PEMP_CHECK_ARG(node_off[B] == 0 || (joint_det && scores && taken), "pemp_pose_greedy: null node arrays");
   int64_t out = 0;
   int64_t e = 0;
   for (int b = 0; b < B; ++b) {

@@ -235,3 +235,25 @@ def test_refine_tag_distance_overflow(mode):
         ref = opose.refine(s, tag, kp.copy())
     got = ppose.refine(dev(s), dev(tag), kp.copy())
     np.testing.assert_array_equal(got, ref)
+
+
+def test_group_persons_empty_cases():
+    """pred_to_ann's None returns: an image without detections, an image whose nodes all fall below the node
+    threshold, and an image without edges, next to a normal one in the same batch; also an empty batch."""
+    g = load(GROUP[0])
+    n = len(g["joint_det"])
+    det = np.concatenate([g["joint_det"], g["joint_det"][:1], g["joint_det"]])
+    sc = np.concatenate([g["joint_scores"], np.float32([0.9]), np.zeros(n, np.float32)])
+    ei = np.concatenate([g["edge_index"], g["edge_index"] + n + 1], 1)
+    pr = np.concatenate([g["pred"], g["pred"]])
+    bi = np.concatenate([np.zeros(n, np.int64), np.full(1, 2, np.int64), np.full(n, 3, np.int64)])
+    cls = np.concatenate([g["class_probs"], g["class_probs"][:1], g["class_probs"]])
+    # images: 0 normal, 1 no detections, 2 one node / no edges, 3 all nodes below threshold
+    out = ppose.group_persons(dev(det), dev(sc), dev(ei), dev(pr), float(g["th"]), dev(cls), "GAEC",
+                              int(g["num_joints"]), batch_index=dev(bi))
+    assert len(out) == 4
+    np.testing.assert_array_equal(out[0], g["persons"])
+    assert out[1] is None and out[2] is None and out[3] is None
+    empty = ppose.group_persons(dev(np.zeros((0, 3), np.int64)), dev(np.zeros(0, np.float32)),
+                                dev(np.zeros((2, 0), np.int64)), dev(np.zeros(0, np.float32)), 0.1)
+    assert empty == [None]
