@@ -561,7 +561,8 @@ __global__ __launch_bounds__(256) void refine_argmax_kernel(const float* __restr
         float k;
         if (F == 2) {
           const float d1 = __fsub_rn(t1[u], mt1[q]);
-          k = rintf(__fsqrt_rn(__fadd_rn(__fmul_rn(d0, d0), __fmul_rn(d1, d1))));
+          // sqrtf is the correctly rounded square root (numpy's); __fsqrt_rn lowers to the 1-ulp v_sqrt_f32
+          k = rintf(sqrtf(__fadd_rn(__fmul_rn(d0, d0), __fmul_rn(d1, d1))));
         } else {
           // F = 1: in binary floating point with round-to-nearest, sqrt(RN(d * d)) == |d| whenever d * d
           // neither overflows nor underflows (an underflow only happens for |d| < 2^-63, where both round

@@ -169,7 +169,7 @@ def test_finish_persons_matches_oracle():
 
 
 @pytest.mark.parametrize("F", [1, 2])
-@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("seed", range(12))
 def test_refine_rounding_boundaries(F, seed):
     """Tag distances placed within a few ulp of half-integers (where rint(sqrt) flips): the refined
     position of an undetected joint must match numpy (oracle) exactly."""
@@ -182,8 +182,14 @@ def test_refine_rounding_boundaries(F, seed):
     d = np.nextafter(k, np.where(ulps > 0, np.float32(np.inf), np.float32(-np.inf)))
     d = np.where(ulps == 0, k, d).astype(np.float32)
     if F == 2:
-        tag[1, :, :, 0] = m + d * np.float32(0.6)
-        tag[1, :, :, 1] = m + d * np.float32(0.8)
+        # the two components put ||.|| within a few ulp of the half-integer; the small second component
+        # moves the sum by sub-ulp amounts, so the correctly rounded sqrt lands on either side
+        if seed % 2:
+            tag[1, :, :, 0] = m + d
+            tag[1, :, :, 1] = m + (rng.integers(0, 64, size=(H, W)) * np.float32(2.0 ** -12)).astype(np.float32)
+        else:
+            tag[1, :, :, 0] = m + d * np.float32(0.6)
+            tag[1, :, :, 1] = m + d * np.float32(0.8)
     else:
         tag[1, :, :, 0] = m + d
     s = (rng.random((J, H, W)) * 0.01).astype(np.float32)
