@@ -225,3 +225,24 @@ def test_greedy_oracle_and_host_fixture(name):
                                   sc.ctypes.data, cls_p, J, tk.ctypes.data, N, out.ctypes.data, cnt.ctypes.data), L)
     np.testing.assert_array_equal(tk, g["taken"])
     np.testing.assert_array_equal(out[:cnt[0]], g["persons"])
+
+
+def test_pose_product_path_has_no_cpu_fallback():
+    """group_persons / pred_to_person / refine need the HIP device: on a host without one they raise instead
+    of computing on the CPU (the host C++ parts above are only reachable through the GPU edge pass)."""
+    import torch
+    from pemp_amd import pose as ppose
+    if torch.cuda.is_available():
+        pytest.skip("a HIP device is present")
+    g = load(GROUP[0])
+    T = torch.from_numpy
+    with pytest.raises((RuntimeError, ValueError)):
+        ppose.group_persons(T(g["joint_det"]), T(g["joint_scores"]), T(g["edge_index"]), T(g["pred"]), 0.1)
+    with pytest.raises((RuntimeError, ValueError)):
+        ppose.pred_to_person(T(g["joint_det"]), T(g["joint_scores"]), T(g["edge_index"]), T(g["pred"]), None,
+                             "GAEC", 17)
+    r = load(REFINE[0])
+    with pytest.raises((RuntimeError, ValueError)):
+        ppose.refine(T(r["scoremaps"]), T(r["tag"]), r["filled"].copy())
+    with pytest.raises(NotImplementedError):
+        ppose._method("MUT")
