@@ -40,6 +40,11 @@ REF_EDGE_FLOP = 82048              # the reference's FLOP per edge-
 GEMM64 = 2 * 64 * 64                            # one 64x64 GEMM per edge
 EDGE_HEAD_FLOP = 2 * (64 * 64 + 64 * 32 + 32)   # fused edge-classification head
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_latest.json")   # tools/gpu_profile.sh + tools/pmc_json.py
+PREC_NOTE = {
+    "f16x3": "f16x3: f16 MFMA on hi/lo split operands (22 bits each), fp32 accumulate; fp32-level logits",
+    "bf16x3": "bf16x3: bf16 MFMA on hi/lo split operands, fp32 accumulate (opt-in, ~2^-16 per product)",
+    "fp32": "fp32 MFMA (v_mfma_f32_16x16x4_f32)",
+}
 
 
 def parse():
@@ -119,9 +124,10 @@ def roofline_for(label, stats, E, wl, precision, upd):
     """Roofline of the dominant kernel from its measured average launch time.
 
     edge_step*: executed FLOP and ALGORITHMIC HBM bytes per edge from edge_pass_cost (node-table
-    gathers are L2-resident and not counted). fp32: bound = fp32 MFMA peak. bf16x3: the MFMA work
-    is 3 bf16 products per fp32 product, so the compute floor is 3 x FLOP / bf16 dense peak; the
-    bound reported is whichever floor (compute, HBM) is larger. `traffic` = measured HBM bytes per
+    gathers are L2-resident and not counted). fp32: bound = fp32 MFMA peak. f16x3 / bf16x3: the MFMA
+    work is 3 16-bit products per fp32 product (f16 and bf16 MFMA run at the same dense rate), so the
+    compute floor is 3 x FLOP / bf16 dense peak; the bound reported is whichever floor (compute, HBM)
+    is larger. `traffic` = measured HBM bytes per
     launch (PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_latest.json)."""
     if label not in stats:
         return None
@@ -418,14 +424,13 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt_max / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "bf16x3" if model.precision == "bf16x3" else "fp32",
+            "dtype": model.precision,
             "data": "synthetic (seeded planted-Gaussian heatmaps, random features; closed-form MPN weights)",
             "config": {"workload": f"{args.workload}: {wl['B']}x{wl['J']}x{wl['H']}x{wl['W']} heatmaps/GPU -> "
                                    f"{wl['graph']} graph -> MPN TypeAware-attn T={wl['steps']}",
                        "images_per_gpu": wl["B"], "global_batch": wl["B"] * world, "persons_per_image": wl["persons"],
                        "nodes_per_gpu": N, "edges_per_gpu": E, "parallelism": f"image-sharded x{world}",
-                       "mpn_edge_gemms": ("bf16x3: bf16 MFMA on hi/lo split operands, fp32 accumulate"
-                                          if model.precision == "bf16x3" else "fp32 MFMA"),
+                       "mpn_edge_gemms": PREC_NOTE[model.precision],
                        "detection_and_node_math": "fp32"},
             "mpn_edge_updates_per_sec": round(mpn_eups, 1),
             "mpn_ms_per_step": round(dt_mpn / args.steps * 1e3, 3),

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define PEMP_ABI_VERSION 9
+#define PEMP_ABI_VERSION 10
 
 enum {
   PEMP_OK = 0,
@@ -232,12 +232,17 @@ int pemp_pose_adjust(const float* det, int J, int H, int W, double* keypoints, i
  * ---------------------------------------------------------------------------------------- */
 enum { PEMP_AGGR_ATTN = 0, PEMP_AGGR_SUM = 1, PEMP_AGGR_MEAN = 2, PEMP_AGGR_MAX = 3 };
 
-/* Arithmetic of the per-edge GEMMs (edge MLP, message, edge head); node-side GEMMs are fp32.
+/* Arithmetic of the per-edge GEMMs (edge embedding, edge MLP, message, edge head) and of the node
+ * table; the other node-side GEMMs are fp32.
  *   PEMP_PREC_FP32   exact fp32 MFMA (v_mfma_f32_16x16x4_f32)
  *   PEMP_PREC_BF16X3 x·w ~= xh·wh + xl·wh + xh·wl with bf16 hi/lo parts and fp32 accumulation
- *                    (v_mfma_f32_16x16x32_bf16): ~2^-16 relative error per product. Needs the
- *                    *_bf weight packs. */
-enum { PEMP_PREC_FP32 = 0, PEMP_PREC_BF16X3 = 1 };
+ *                    (v_mfma_f32_16x16x32_bf16): ~2^-16 relative error per product.
+ *   PEMP_PREC_F16X3  x·w ~= xh·wh + 2^-11 (xh·wl + xl·wh) with f16 parts, the low parts scaled by 2^11
+ *                    (v_mfma_f32_16x16x32_f16, fp32 accumulation): ~2^-22 relative error per product,
+ *                    fp32-level logits; fragments reaching 2^14 are range-scaled by exact powers of two.
+ * Both split precisions need the *_bf weight packs, in the matching 16-bit format (the field names
+ * keep "bf" for either). */
+enum { PEMP_PREC_FP32 = 0, PEMP_PREC_BF16X3 = 1, PEMP_PREC_F16X3 = 2 };
 
 typedef struct pemp_layer {
   const float* w; /* [out_pad][in_pad] */
@@ -269,7 +274,8 @@ typedef struct pemp_mpn_weights {
   pemp_mlp class_head; /* 64 -> .. -> J */
   float attn_b;
   int32_t pad_;
-  /* PEMP_PREC_BF16X3 weight packs (bf16 bit patterns): per matrix [hi | lo][out][64] with the input
+  /* split-precision weight packs (16-bit patterns: bf16 hi / lo for PEMP_PREC_BF16X3, f16 hi / f16 lo
+   * scaled by 2^11 for PEMP_PREC_F16X3): per matrix [hi | lo][out][64] with the input
    * columns in MFMA slot order: slot 32 kb + 8 g + j holds input 32 kb + 16 (j >> 2) + 4 g + (j & 3). */
   const uint16_t* e1_bf;   /* [2][64][64]    */
   const uint16_t* e2_bf;   /* [2][64][64]    */

@@ -105,6 +105,8 @@ def mpn_cfg(meta):
     if meta.get("late_fusion"):
         c.LATE_FUSION_POS = True
         c.EDGE_EMB.BN = True
+    if meta.get("node_summary"):
+        c.NODE_TYPE_SUMMARY = meta["node_summary"]
     return c
 
 
@@ -112,7 +114,7 @@ def make_mpn_case(MPN, name, meta, graph):
     torch.manual_seed(0)
     cfg = mpn_cfg(meta)
     model = MPN(cfg)
-    sd = syn.closed_form_state_dict(model, meta["salt"], meta.get("attn_gain", 1.0))
+    sd = syn.closed_form_state_dict(model, meta["salt"], meta.get("attn_gain", 1.0), meta.get("weight_gain", 1.0))
     model.load_state_dict(sd)
     model.eval()
     x, ea, ei, det = graph[0], graph[1], graph[2], graph[7]
@@ -192,6 +194,16 @@ MPN_CASES = {
     "mpn_attn_latefusion_t2": (dict(J=17, steps=2, variant="attn", salt=18.5, late_fusion=True), "gc_small_fully"),
     "mpn_attn_pertype_t2": (dict(J=17, steps=2, variant="attn", salt=10.5, aggr_sub="node_edge_attn_per_type",
                                  aggr="add", attn_gain=16.0), "gc_realistic_knn"),
+    # NODE_TYPE_SUMMARY type LUTs (src/Models/MessagePassingNetwork/utils.py:11-19): 9 / 6 merged types
+    "mpn_attn_lr_t3": (dict(J=17, steps=3, variant="attn", salt=19.5, node_summary="left_right"), "gc_realistic_knn"),
+    "mpn_attn_pbp_t2": (dict(J=17, steps=2, variant="attn", salt=20.5, node_summary="per_body_part"),
+                        "gc_small_fully"),
+    "mpn_pertype_max_lr_t2": (dict(J=17, steps=2, variant="attn", salt=21.5, aggr_sub="None", aggr="max",
+                                   node_summary="left_right"), "gc_small_fully"),
+    "mpn_pertype_max_pbp_t3": (dict(J=17, steps=3, variant="attn", salt=22.5, aggr_sub="None", aggr="max",
+                                    node_summary="per_body_part"), "gc_realistic_knn"),
+    # trained-checkpoint logit magnitudes (every Linear weight x2: |logit| up to ~50)
+    "mpn_attn_gain2_t3": (dict(J=17, steps=3, variant="attn", salt=9.5, weight_gain=2.0), "gc_c2_like"),
 }
 
 

@@ -536,16 +536,85 @@ __device__ __forceinline__ void gemm_bf3(const __bf16* __restrict__ W, const bf1
   }
 }
 
+// ---- f16x3 split precision (PREC 2, the default): with w' = 2^11 w split into f16 parts
+// wh = f16(w'), wl = f16(w' - wh) (mpn/fold.py::split_pack "f16") and x split into xh = f16(x),
+// xl = f16(x - xh), one fp32 accumulator takes 2^11 x·w ~= wl·xh + wh·xl + wh·xh on
+// v_mfma_f32_16x16x32_f16 (the f16 products are exact in fp32). Each pair carries 22 bits of its
+// operand (bf16x3: 16), so the dropped wl·xl term leaves ~2^-22 relative error per product:
+// fp32-level logits at trained-checkpoint magnitudes, where bf16x3 misses the 1e-4 bar
+// (tests/test_gpu_mpn.py::test_trained_scale). The accumulator is entered scaled by 2^11 and left by
+// 2^-11 (exact powers of two). Range: f16 holds |x| < 65504, so a wave whose fragment reaches 2^14
+// splits x·2^-16 instead and rescales by 2^16 on the way out (f16_big); the host keeps |w| < 32.
+// Same fragment slot order and LDS row layout as bf16x3.
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+constexpr float F16_BIG = 16384.0f;
+
+// wave-uniform: some |x| of the fragment reaches 2^14 (or is NaN): take the range-scaled split
+__device__ __forceinline__ bool f16_big(const float (&x)[4][4]) {
+  float m = 0.0f;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) m = fmaxf(m, fmaxf(fmaxf(fabsf(x[b][0]), fabsf(x[b][1])), fmaxf(fabsf(x[b][2]), fabsf(x[b][3]))));
+  return __any(!(m < F16_BIG));
+}
+
+template <bool SCALED>
+__device__ __forceinline__ void split_f16(const float (&x)[4][4], f16x8_t (&hi)[2], f16x8_t (&lo)[2]) {
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float f = SCALED ? x[2 * kb + (j >> 2)][j & 3] * (1.0f / 65536.0f) : x[2 * kb + (j >> 2)][j & 3];
+      const _Float16 h = (_Float16)f;
+      hi[kb][j] = h;
+      lo[kb][j] = (_Float16)(f - (float)h);
+    }
+}
+
+// split of one fragment; returns the (accumulator-in, accumulator-out) scale factors
+__device__ __forceinline__ float2 split_f16_any(const float (&x)[4][4], f16x8_t (&hi)[2], f16x8_t (&lo)[2]) {
+  if (__builtin_expect(f16_big(x), 0)) {
+    split_f16<true>(x, hi, lo);
+    return make_float2(1.0f / 32.0f, 32.0f);       // 2^11 * 2^-16 in, back out
+  }
+  split_f16<false>(x, hi, lo);
+  return make_float2(2048.0f, 1.0f / 2048.0f);
+}
+
+// acc[ob] += W[16 ob + i][.] · x (K = 64), W = interleaved f16 rows [wh 64 | wl 64 | pad] (gemm_bf3 layout)
+template <int OB>
+__device__ __forceinline__ void gemm_h3(const _Float16* __restrict__ W, const f16x8_t (&hi)[2], const f16x8_t (&lo)[2],
+                                        float2 sc, float (&acc)[OB][4]) {
+  const int lane = __lane_id(), i = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int ob = 0; ob < OB; ++ob) {
+    f32x4 c = {acc[ob][0] * sc.x, acc[ob][1] * sc.x, acc[ob][2] * sc.x, acc[ob][3] * sc.x};
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const int o = (16 * ob + i) * 2 * LDW + 32 * kb + 8 * g;
+      const f16x8_t ah = *reinterpret_cast<const f16x8_t*>(W + o);
+      const f16x8_t al = *reinterpret_cast<const f16x8_t*>(W + o + 64);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, hi[kb], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, lo[kb], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, hi[kb], c, 0, 0, 0);
+    }
+    acc[ob][0] = c[0] * sc.y; acc[ob][1] = c[1] * sc.y; acc[ob][2] = c[2] * sc.y; acc[ob][3] = c[3] * sc.y;
+  }
+}
+
 // one layer on fragments in the chosen precision; W points at the LDS image of the matrix
-// (PREC 0: fp32 [out][LDW]; PREC 1: interleaved bf16 rows [out][hi 64 | lo 64 | pad], see gemm_bf3)
+// (PREC 0: fp32 [out][LDW]; PREC 1 / 2: interleaved 16-bit rows [out][hi 64 | lo 64 | pad], see gemm_bf3)
 template <int PREC, int OB>
 __device__ __forceinline__ void gemm_p(const void* W, const float (&x)[4][4], float (&acc)[OB][4]) {
   if (PREC == 0) {
     gemm_frag<4, OB>(static_cast<const float*>(W), LDW, x, acc);
-  } else {
+  } else if (PREC == 1) {
     bf16x8_t hi[2], lo[2];
     split_bf16(x, hi, lo);
     gemm_bf3<OB>(static_cast<const __bf16*>(W), hi, lo, acc);
+  } else {
+    f16x8_t hi[2], lo[2];
+    const float2 sc = split_f16_any(x, hi, lo);
+    gemm_h3<OB>(static_cast<const _Float16*>(W), hi, lo, sc, acc);
   }
 }
 
@@ -582,7 +651,7 @@ static EmbedLayout embed_layout(const pemp_mlp& m, int prec) {
     L.ob[l] = (out + 15) / 16;
     L.relu[l] = l < L.n ? m.layer[l].relu : 0;
     L.w_off[l] = off;
-    if (prec == PEMP_PREC_BF16X3) {
+    if (prec != PEMP_PREC_FP32) {
       L.kb[l] = (in + 31) / 32;
       L.stride[l] = lds_stride_bf(32 * L.kb[l]);
       off += 16 * L.ob[l] * L.stride[l] / 2;             // interleaved hi | lo rows, stride bf16 elements
@@ -630,32 +699,47 @@ __device__ __forceinline__ void layer_lds(const float* __restrict__ W, int ldw, 
   }
 }
 
-// bf16x3 variant: W = interleaved rows [16 OB][hi 32 KB32 | lo 32 KB32 | pad], stride ldw; KB32 (<= 2)
-// k-blocks of 32 inputs.
-__device__ __forceinline__ void layer_lds_bf(const __bf16* __restrict__ W, int ldw, const float* __restrict__ bias,
-                                             int KB32, int OB, int relu, const float (&in)[4][4], float (&out)[4][4]) {
+// split-precision variants (PREC 1 bf16x3, PREC 2 f16x3): W = interleaved rows
+// [16 OB][hi 32 KB32 | lo 32 KB32 | pad], stride ldw; KB32 (<= 2) k-blocks of 32 inputs.
+template <int PREC>
+__device__ __forceinline__ void layer_lds_p(const uint16_t* __restrict__ W, int ldw, const float* __restrict__ bias,
+                                            int KB32, int OB, int relu, const float (&in)[4][4], float (&out)[4][4]) {
   const int lane = __lane_id(), i = lane & 15, g = lane >> 4;
-  bf16x8_t hi[2], lo[2];
-  split_bf16(in, hi, lo);
+  bf16x8_t hb[2], lb[2];
+  f16x8_t hh[2], lh[2];
+  float2 sc = make_float2(1.0f, 1.0f);
+  if (PREC == 1) split_bf16(in, hb, lb);
+  else sc = split_f16_any(in, hh, lh);
   const int lo_off = 32 * KB32;                 // interleaved rows: [hi | lo | pad]
 #pragma unroll
   for (int ob = 0; ob < 4; ++ob) {
     if (ob < OB) {
       const float4 bb = ld4(bias + 16 * ob + 4 * g);
-      f32x4 c = {bb.x, bb.y, bb.z, bb.w};
+      f32x4 c = {bb.x * sc.x, bb.y * sc.x, bb.z * sc.x, bb.w * sc.x};
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         if (kb < KB32) {
           const int o = (16 * ob + i) * ldw + 32 * kb + 8 * g;
-          const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(W + o);
-          const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(W + o + lo_off);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, hi[kb], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, lo[kb], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, hi[kb], c, 0, 0, 0);
+          if (PREC == 1) {
+            const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(W + o);
+            const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(W + o + lo_off);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, hb[kb], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, lb[kb], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, hb[kb], c, 0, 0, 0);
+          } else {
+            const f16x8_t ah = *reinterpret_cast<const f16x8_t*>(W + o);
+            const f16x8_t al = *reinterpret_cast<const f16x8_t*>(W + o + lo_off);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, hh[kb], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, lh[kb], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, hh[kb], c, 0, 0, 0);
+          }
         }
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) out[ob][r] = relu ? fmaxf(c[r], 0.0f) : c[r];
+      for (int r = 0; r < 4; ++r) {
+        const float v = c[r] * sc.y;
+        out[ob][r] = relu ? fmaxf(v, 0.0f) : v;
+      }
     } else {
 #pragma unroll
       for (int r = 0; r < 4; ++r) out[ob][r] = 0.0f;
@@ -723,9 +807,9 @@ __device__ __forceinline__ void embed_tile(const float* smz, const EmbedLayout& 
       if (to_y) layer_lds(W, Lo.stride[l], bias, Lo.kb[l], Lo.ob[l], relu, x, y);
       else layer_lds(W, Lo.stride[l], bias, Lo.kb[l], Lo.ob[l], relu, y, x);
     } else {
-      const __bf16* Wb = reinterpret_cast<const __bf16*>(W);
-      if (to_y) layer_lds_bf(Wb, Lo.stride[l], bias, Lo.kb[l], Lo.ob[l], relu, x, y);
-      else layer_lds_bf(Wb, Lo.stride[l], bias, Lo.kb[l], Lo.ob[l], relu, y, x);
+      const uint16_t* Wb = reinterpret_cast<const uint16_t*>(W);
+      if (to_y) layer_lds_p<PREC>(Wb, Lo.stride[l], bias, Lo.kb[l], Lo.ob[l], relu, x, y);
+      else layer_lds_p<PREC>(Wb, Lo.stride[l], bias, Lo.kb[l], Lo.ob[l], relu, y, x);
     }
   }
 }
@@ -837,7 +921,25 @@ struct EdgeStepArgs {
   pemp_mlp head;
   float* edge_logits;
   int write_next;
+  unsigned long long* stamps;   // diagnostic builds (-DPEMP_STAMPS) only: per-wave phase timestamps
 };
+
+// Diagnostic phase timestamps (-DPEMP_STAMPS builds only; tools/edge_timeline.py): lane 0 of each
+// wave stores s_memrealtime (100 MHz) into stamps[16 * global_wave + k].
+#ifdef PEMP_STAMPS
+#define EDGE_STAMP(k)                                                                               \
+  do {                                                                                              \
+    if (a.stamps && lane == 0) {                                                                    \
+      unsigned long long t_;                                                                        \
+      asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                \
+      a.stamps[16 * ((int64_t)blockIdx.x * NW + wave) + (k)] = t_;                                  \
+    }                                                                                               \
+  } while (0)
+#else
+#define EDGE_STAMP(k) \
+  do {                \
+  } while (0)
+#endif
 
 // ---- in-row (16-lane) DPP primitives: lane c = lane & 15 of every row holds edge c of the tile ----
 constexpr int DPP_SHR1 = 0x111, DPP_SHR2 = 0x112, DPP_SHR4 = 0x114, DPP_SHR8 = 0x118;
@@ -980,6 +1082,7 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
   const int T = a.T;
   const int blk = blockIdx.x;
+  EDGE_STAMP(0);
   if (blk >= a.wg_start[T]) return;             // uniform for the block
   int t = 0;
   while (t + 1 < T && a.wg_start[t + 1] <= blk) ++t;
@@ -1026,10 +1129,11 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
       else if (threadIdx.x < D + 32) hb[threadIdx.x] = a.head.layer[1].b[threadIdx.x - D];
       else if (threadIdx.x < D + 64) hb[threadIdx.x] = a.head.layer[2].w[threadIdx.x - D - 32];
     }
-    if (UPD) stage_tile64<PREC>(uw, a.upd_w + 64 * t, 64 * T, PREC == 1 ? a.upd_bf + (int64_t)t * 2 * D * D : nullptr);
+    if (UPD) stage_tile64<PREC>(uw, a.upd_w + 64 * t, 64 * T, PREC != 0 ? a.upd_bf + (int64_t)t * 2 * D * D : nullptr);
     if ((STAGE & 3) == STAGE_FIRST) stage_embed<PREC>(sm + a.emb_off, a.emb, a.Lo, a.emb_bf, a.q0_w, a.q0_b);
   }
   __syncthreads();
+  EDGE_STAMP(1);
 
   // ---- this wave's range ----
   const int64_t N = a.N;
@@ -1045,7 +1149,8 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
   };
   const int first = snap(lo + (int)(n_b * wave / NW));
   const int end = snap(lo + (int)(n_b * (wave + 1) / NW));
-  if (first >= end) return;
+  EDGE_STAMP(2);
+  if (first >= end) { EDGE_STAMP(15); return; }
   const float* ntP = a.NT + 128 + 64 * t;
 
   // carry of the chunk continuing into the next tile: features in lane c == 0 of each row,
@@ -1081,7 +1186,9 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
       src_nn = a.s_src[min(first + 16 + c, end - 1)];
     }
   }
-  for (int base = first; base < end; base += 16) {
+  int tile_no = 0;
+  for (int base = first; base < end; base += 16, ++tile_no) {
+    if (tile_no < 4) EDGE_STAMP(3 + 3 * tile_no);
     // opaque zero: keeps the compiler from hoisting the LDS weight fragments out of the loop
     // (192+ VGPRs of loop-invariant loads would spill)
     int z = 0;
@@ -1165,6 +1272,10 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
       }
     }
     // edge MLP layer 1: h = ReLU(r + A[dst] + B[src]), r = Q0 + W1_e_cur · e_cur
+#ifdef PEMP_STAMPS
+    asm volatile("" ::"v"(h[0][0]), "v"(h[3][3]));
+    if (tile_no < 4) EDGE_STAMP(4 + 3 * tile_no);
+#endif
     relu_frag<4>(h);
     // layer 2: e' = ReLU(W2 · h + b2)
     float ep[4][4];
@@ -1311,8 +1422,12 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
           st4(o + 16 * ob, v[ob][0], v[ob][1], v[ob][2], v[ob][3]);
       }
     }
-
+#ifdef PEMP_STAMPS
+    asm volatile("" ::"v"(v[0][0]), "v"(v[3][3]));
+    if (tile_no < 4) EDGE_STAMP(5 + 3 * tile_no);
+#endif
   }
+  EDGE_STAMP(15);
 }
 
 // Node update (separate launch, the whole edge pass must have finished): one workgroup per
@@ -1869,16 +1984,23 @@ __global__ __launch_bounds__(256) void node_table_kernel(NodeTableArgs a) {
   // this wave's weight fragment (rows 16 ob + c), issued first
   float4 w[8];
   bf16x8_t wh[4], wlo[4];
+  f16x8_t fh[4], flo[4];
   if (PREC == 0) {
 #pragma unroll
     for (int mb = 0; mb < 8; ++mb) w[mb] = ld4(a.pre_w + (int64_t)(16 * obc + c) * 128 + 16 * mb + 4 * g);
   } else {
-    const __bf16* Wb = reinterpret_cast<const __bf16*>(a.pre_bf);
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
       const int64_t o = (int64_t)(16 * obc + c) * 128 + 32 * kb + 8 * g;
-      wh[kb] = *reinterpret_cast<const bf16x8_t*>(Wb + o);
-      wlo[kb] = *reinterpret_cast<const bf16x8_t*>(Wb + (int64_t)a.NO * 128 + o);
+      if (PREC == 1) {
+        const __bf16* Wb = reinterpret_cast<const __bf16*>(a.pre_bf);
+        wh[kb] = *reinterpret_cast<const bf16x8_t*>(Wb + o);
+        wlo[kb] = *reinterpret_cast<const bf16x8_t*>(Wb + (int64_t)a.NO * 128 + o);
+      } else {
+        const _Float16* Wh = reinterpret_cast<const _Float16*>(a.pre_bf);
+        fh[kb] = *reinterpret_cast<const f16x8_t*>(Wh + o);
+        flo[kb] = *reinterpret_cast<const f16x8_t*>(Wh + (int64_t)a.NO * 128 + o);
+      }
     }
   }
   const float4 bb = ld4(a.pre_b + 16 * obc + 4 * g);
@@ -1919,7 +2041,7 @@ __global__ __launch_bounds__(256) void node_table_kernel(NodeTableArgs a) {
         acc = mfma4(w[mb].z, x[mb][2], acc);
         acc = mfma4(w[mb].w, x[mb][3], acc);
       }
-    } else {
+    } else if (PREC == 1) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const float (&xh)[4][4] = *reinterpret_cast<const float (*)[4][4]>(&x[4 * h][0]);
@@ -1932,6 +2054,26 @@ __global__ __launch_bounds__(256) void node_table_kernel(NodeTableArgs a) {
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[2 * h + kb], hi[kb], acc, 0, 0, 0);
         }
       }
+    } else {
+      // f16x3 over K = 128 (two 64-input halves, one range check for both)
+      const float (&x0)[4][4] = *reinterpret_cast<const float (*)[4][4]>(&x[0][0]);
+      const float (&x1)[4][4] = *reinterpret_cast<const float (*)[4][4]>(&x[4][0]);
+      const bool big = f16_big(x0) || f16_big(x1);
+      const float s_in = big ? 1.0f / 32.0f : 2048.0f, s_out = big ? 32.0f : 1.0f / 2048.0f;
+      acc *= s_in;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f16x8_t hi[2], lo[2];
+        if (big) split_f16<true>(h ? x1 : x0, hi, lo);
+        else split_f16<false>(h ? x1 : x0, hi, lo);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(flo[2 * h + kb], hi[kb], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[2 * h + kb], lo[kb], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[2 * h + kb], hi[kb], acc, 0, 0, 0);
+        }
+      }
+      acc *= s_out;
     }
     if (nn < N) st4(a.NT + nn * a.NO + 16 * ob + 4 * g, acc[0], acc[1], acc[2], acc[3]);
   }
@@ -1989,7 +2131,10 @@ static void launch_edge_step_p(const EdgeStepArgs& a, bool head, int grid, int s
 template <int AGG>
 static void launch_edge_step(const EdgeStepArgs& a, bool head, int grid, int prec, bool upd, int stage, hipStream_t st) {
   constexpr int U = AGG == PEMP_AGGR_ATTN || AGG == PEMP_AGGR_MEAN ? 1 : 0;
-  if (prec == PEMP_PREC_BF16X3) {
+  if (prec == PEMP_PREC_F16X3) {
+    if (U && upd) launch_edge_step_p<AGG, 2, U>(a, head, grid, stage, st);
+    else launch_edge_step_p<AGG, 2, 0>(a, head, grid, stage, st);
+  } else if (prec == PEMP_PREC_BF16X3) {
     if (U && upd) launch_edge_step_p<AGG, 1, U>(a, head, grid, stage, st);
     else launch_edge_step_p<AGG, 1, 0>(a, head, grid, stage, st);
   } else {
@@ -2198,6 +2343,17 @@ extern "C" size_t pemp_mpn_workspace_size(const pemp_mpn_desc* desc, int64_t N, 
 // buffers. Forwards launch directly.)
 // fully_node_off != NULL: edge_index is the fully graph of the batch with these per-image node
 // offsets (device, [fully_B + 1]) -> the closed-form prepare (fully_prepare_kernel)
+#ifdef PEMP_STAMPS
+// diagnostic builds: the edge pass `g_diag_stamp_pass` of every forward records per-wave phase stamps
+static unsigned long long* g_diag_stamps = nullptr;
+static int g_diag_stamp_pass = 0;
+extern "C" int pemp_diag_stamps(void* buf, int pass) {
+  g_diag_stamps = static_cast<unsigned long long*>(buf);
+  g_diag_stamp_pass = pass;
+  return PEMP_OK;
+}
+#endif
+
 static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w, const float* x,
                             const float* edge_attr, const int64_t* edge_index, const int64_t* node_types,
                             int64_t N, int64_t E, float* edge_logits, float* node_logits, float* class_logits,
@@ -2246,10 +2402,11 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
                  "pemp_mpn_forward: node/class heads must start at 64 and end at 1 / num_joints");
   PEMP_CHECK_ARG(w->pre_w && w->pre_b && w->q0_w && w->q0_b && w->e1_w && w->e2_w && w->e2_b && w->msg_w,
                  "pemp_mpn_forward: null layer weights");
-  PEMP_CHECK_ARG(desc->precision == PEMP_PREC_FP32 || desc->precision == PEMP_PREC_BF16X3,
+  PEMP_CHECK_ARG(desc->precision == PEMP_PREC_FP32 || desc->precision == PEMP_PREC_BF16X3 ||
+                     desc->precision == PEMP_PREC_F16X3,
                  "pemp_mpn_forward: unknown precision %d", desc->precision);
-  PEMP_CHECK_ARG(desc->precision != PEMP_PREC_BF16X3 || (w->e1_bf && w->e2_bf && w->msg_bf),
-                 "pemp_mpn_forward: PEMP_PREC_BF16X3 needs the e1_bf / e2_bf / msg_bf weight packs");
+  PEMP_CHECK_ARG(desc->precision == PEMP_PREC_FP32 || (w->e1_bf && w->e2_bf && w->msg_bf),
+                 "pemp_mpn_forward: split precisions need the e1_bf / e2_bf / msg_bf weight packs");
   PEMP_CHECK_ARG(N == 0 || (x && node_logits && class_logits && node_types), "pemp_mpn_forward: null node tensors");
   PEMP_CHECK_ARG(E == 0 || (edge_attr && edge_index && edge_logits), "pemp_mpn_forward: null edge tensors");
   size_t need = 0;
@@ -2288,7 +2445,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   const bool upd_fused = (desc->aggr == PEMP_AGGR_ATTN || desc->aggr == PEMP_AGGR_MEAN) && w->upd_w &&
                          (desc->precision == PEMP_PREC_FP32 || w->upd_bf);
   const bool emb_lds = mlp_ok(w->edge_emb, 64, 64);
-  const int emb_prec = desc->precision == PEMP_PREC_BF16X3 && w->emb_bf ? PEMP_PREC_BF16X3 : PEMP_PREC_FP32;
+  const int emb_prec = desc->precision != PEMP_PREC_FP32 && w->emb_bf ? desc->precision : PEMP_PREC_FP32;
   const EmbedLayout emb_lo = embed_layout(w->edge_emb, emb_prec);
   // PEMP_FUSED_FIRST (build flag, default off): the fused first pass runs 8 waves per CU (register
   // budget of the embedding) and measured slower than embedding + a 16-wave pass (95 vs ~82 us at C3)
@@ -2319,7 +2476,11 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
     if (emb_lds) {
       const int grid = (int)std::min<int64_t>(num_cus(), (E + 16 * EDGE_WAVES - 1) / (16 * EDGE_WAVES));
       const size_t lds = (size_t)(emb_lo.total + D * LDW) * sizeof(float);
-      if (emb_prec == PEMP_PREC_BF16X3)
+      if (emb_prec == PEMP_PREC_F16X3)
+        hipLaunchKernelGGL(edge_embed_kernel<2>, dim3(grid), dim3(64 * EDGE_WAVES), lds, st, w->edge_emb, emb_lo,
+                           w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, w->e1_bf,
+                           ws.EA, ws.Q0);
+      else if (emb_prec == PEMP_PREC_BF16X3)
         hipLaunchKernelGGL(edge_embed_kernel<1>, dim3(grid), dim3(64 * EDGE_WAVES), lds, st, w->edge_emb, emb_lo,
                            w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, w->e1_bf,
                            ws.EA, ws.Q0);
@@ -2341,7 +2502,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   const int edge_grid = std::max(num_cus(), T);   // >= wg_start[T] (see mpn_scan_kernel)
   const bool fused_heads = mlp_ok(w->node_head, 64, 64) && mlp_ok(w->class_head, 64, 64);
   const unsigned node_grid = (unsigned)((N + 15) / 16);
-  const int table_prec = desc->precision == PEMP_PREC_BF16X3 && w->pre_bf ? PEMP_PREC_BF16X3 : PEMP_PREC_FP32;
+  const int table_prec = desc->precision != PEMP_PREC_FP32 && w->pre_bf ? desc->precision : PEMP_PREC_FP32;
   const int table_groups = (NO / 16 + 3) / 4;
   const unsigned table_grid = (unsigned)(((N + 16 * TBL_TILES - 1) / (16 * TBL_TILES)) * table_groups);
   // x for the next stage (mode) + heads when slot >= 0, then the node table when `table`
@@ -2392,7 +2553,9 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
     if (table) {
       NodeTableArgs ta{ws.X, N, w->pre_w, w->pre_b, w->pre_bf, NO, table_groups, ws.NT};
       ProfScope prof("node_table", st);
-      if (table_prec == PEMP_PREC_BF16X3)
+      if (table_prec == PEMP_PREC_F16X3)
+        hipLaunchKernelGGL(node_table_kernel<2>, dim3(table_grid), dim3(256), 0, st, ta);
+      else if (table_prec == PEMP_PREC_BF16X3)
         hipLaunchKernelGGL(node_table_kernel<1>, dim3(table_grid), dim3(256), 0, st, ta);
       else
         hipLaunchKernelGGL(node_table_kernel<0>, dim3(table_grid), dim3(256), 0, st, ta);
@@ -2438,6 +2601,9 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
       ea.upd_w = w->upd_w; ea.upd_bf = w->upd_bf;
       ea.edge_logits = record ? edge_logits + (int64_t)rec * E : nullptr;
       ea.write_next = !last;
+#ifdef PEMP_STAMPS
+      ea.stamps = it == g_diag_stamp_pass ? g_diag_stamps : nullptr;
+#endif
       const char* label = record ? "edge_step_head" : "edge_step";
       ProfScope prof(label, st);
       // a pass is idempotent (reads r_cur / NT / Q0, rewrites r_next / agg / logits), so the profiler

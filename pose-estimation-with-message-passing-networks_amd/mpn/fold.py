@@ -84,18 +84,39 @@ def bf16_slot_perm(n_kb=2):
     return torch.tensor(perm)
 
 
-def bf16_pack(W):
-    """[out, in] weights -> [2, out_pad16, in_pad32] bf16 bit patterns (hi, lo), zero padded, columns
-    in slot order. The split starts from the fp32 value the fp32 path uses: hi = bf16(w),
-    lo = bf16(w - hi) (RNE)."""
+F16_W_SCALE = 2048.0       # csrc/mpn.hip gemm_h3: the f16 parts split w' = 2^11 w
+F16_MAX_WEIGHT = 32.0       # |w'| = 2^11 |w| must stay inside f16 (65504)
+
+
+def split_pack(W, kind="bf16"):
+    """[out, in] weights -> [2, out_pad16, in_pad32] 16-bit patterns (hi, lo), zero padded, columns in
+    slot order. The split starts from the fp32 value the fp32 path uses.
+      kind "bf16" (PEMP_PREC_BF16X3): hi = bf16(w), lo = bf16(w - hi), RNE.
+      kind "f16"  (PEMP_PREC_F16X3):  w' = 2^11 w (exact), hi = f16(w'), lo = f16(w' - hi), RNE."""
     out, inn = W.shape
     n_kb = (inn + 31) // 32
     Wp = torch.zeros(_pad16(out), 32 * n_kb, dtype=torch.float64)
     Wp[:out, :inn] = W
     w = Wp.to(torch.float32)[:, bf16_slot_perm(n_kb)]
-    hi = w.to(torch.bfloat16)
-    lo = (w - hi.to(torch.float32)).to(torch.bfloat16)
+    if kind == "f16":
+        if not bool((w.abs() < F16_MAX_WEIGHT).all()):
+            raise F16RangeError("f16x3 precision needs |weights| < 32 after BatchNorm folding")
+        w = w * F16_W_SCALE
+        hi = w.to(torch.float16)
+        lo = (w - hi.to(torch.float32)).to(torch.float16)
+    else:
+        hi = w.to(torch.bfloat16)
+        lo = (w - hi.to(torch.float32)).to(torch.bfloat16)
     return torch.stack([hi, lo], 0).contiguous().view(torch.int16)
+
+
+class F16RangeError(ValueError):
+    """A folded weight is outside the f16x3 range: the model falls back to exact fp32."""
+
+
+def bf16_pack(W):
+    """bf16x3 pack (split_pack kind "bf16")."""
+    return split_pack(W, "bf16")
 
 
 class Folded:
@@ -207,7 +228,11 @@ def hierarch_dense_layers(upd, T):
     return [(W1, b1), (W2, b2), (W3, g(upd.final.bias))]
 
 
-def fold_weights(model, device) -> Folded:
+def fold_weights(model, device, precision="f16x3") -> Folded:
+    """Folded weights for `precision` (fp32 | bf16x3 | f16x3): the split precisions get their 16-bit
+    weight packs (split_pack), fp32 the bf16 ones (unused by its kernels)."""
+    kind = "f16" if precision == "f16x3" else "bf16"
+    pack = lambda W: split_pack(W, kind)
     f = Folded()
     s = f.struct
     layer = model.mpn_node_cls
@@ -267,7 +292,7 @@ def fold_weights(model, device) -> Folded:
     msg_w = [m.weight.detach().double().cpu()[:, nx:nx + 64] for m in msg_mods]
     pre_full = torch.cat(pre_w, 0)
     s.pre_w = f.dev(pre_full, device).data_ptr()
-    s.pre_bf = f.dev_raw(bf16_pack(pre_full), device).data_ptr()
+    s.pre_bf = f.dev_raw(pack(pre_full), device).data_ptr()
     s.pre_b = f.dev(torch.cat(pre_b, 0), device).data_ptr()
     s.q0_w = f.dev(q0, device).data_ptr()
     s.q0_b = f.dev(b1, device).data_ptr()
@@ -277,16 +302,16 @@ def fold_weights(model, device) -> Folded:
     s.msg_w = f.dev(torch.stack(msg_w, 0), device).data_ptr()
     # bf16x3 packs of the per-edge GEMMs (PEMP_PREC_BF16X3)
     e2 = e2_full
-    s.e1_bf = f.dev_raw(bf16_pack(e1), device).data_ptr()
-    s.e2_bf = f.dev_raw(bf16_pack(e2), device).data_ptr()
-    s.msg_bf = f.dev_raw(torch.stack([bf16_pack(w) for w in msg_w], 0), device).data_ptr()
+    s.e1_bf = f.dev_raw(pack(e1), device).data_ptr()
+    s.e2_bf = f.dev_raw(pack(e2), device).data_ptr()
+    s.msg_bf = f.dev_raw(torch.stack([pack(w) for w in msg_w], 0), device).data_ptr()
     head = mlp_layers(model.edge_classification)
     if (len(head) == 3 and head[0][0].shape == (64, 64) and head[1][0].shape == (32, 64)
             and head[0][2] and head[1][2] and not head[2][2] and head[2][0].shape[0] == 1):
-        s.head_bf = f.dev_raw(torch.cat([bf16_pack(head[0][0]).reshape(-1), bf16_pack(head[1][0]).reshape(-1)]),
+        s.head_bf = f.dev_raw(torch.cat([pack(head[0][0]).reshape(-1), pack(head[1][0]).reshape(-1)]),
                               device).data_ptr()
     if all(W.shape[0] <= 64 and W.shape[1] <= 64 for W, _, _ in emb):
-        packs = [bf16_pack(W).reshape(-1) for W, _, _ in emb] + [bf16_pack(q0).reshape(-1)]
+        packs = [pack(W).reshape(-1) for W, _, _ in emb] + [pack(q0).reshape(-1)]
         s.emb_bf = f.dev_raw(torch.cat(packs), device).data_ptr()
     attn = getattr(layer, "attn_net", None)
     if attn is not None and attn[0].out_features == 1:       # node_edge_attn: one shared row
@@ -309,7 +334,7 @@ def fold_weights(model, device) -> Folded:
         s.upd_b = f.dev(upd[0].bias.detach().double().cpu(), device).data_ptr()
         U = upd[0].weight.detach().double().cpu()
         if U.shape == (64, 64 * T):
-            s.upd_bf = f.dev_raw(torch.stack([bf16_pack(U[:, 64 * t:64 * t + 64]) for t in range(T)], 0),
+            s.upd_bf = f.dev_raw(torch.stack([pack(U[:, 64 * t:64 * t + 64]) for t in range(T)], 0),
                                  device).data_ptr()
     # node embedding / head weights in the node kernels' LDS layout, built once per weight set
     L = _lib.lib()

@@ -10,12 +10,13 @@ Linear) and runs the whole network in ``pemp_mpn_forward`` (libpemp.so). Inferen
 import ctypes
 import itertools
 import os
+import warnings
 
 import torch
 import torch.nn as nn
 
 from .. import _lib
-from .fold import fold_weights
+from .fold import F16RangeError, fold_weights
 from .edge_type import TypeAwareEdgeUpdate
 from .hierarch import HierarchUpdateCnn, HierarchUpdateMlp
 
@@ -23,19 +24,22 @@ _VALIDATE = os.environ.get("PEMP_VALIDATE", "0") not in ("", "0")   # read once 
 _FULLY_OFF = os.environ.get("PEMP_NO_FULLY_PREPARE", "0") not in ("", "0")   # force the sorting prepare
 
 AGGR_CODES = {"attn": 0, "add": 1, "sum": 1, "mean": 2, "max": 3}
-PRECISIONS = {"fp32": 0, "bf16x3": 1}
+PRECISIONS = {"fp32": 0, "bf16x3": 1, "f16x3": 2}
 
 
 def default_precision(aggr_code):
-    """Arithmetic of the per-edge GEMMs. ``PEMP_PRECISION`` (fp32 | bf16x3) overrides; otherwise the
-    attention variant (published model, bounded softmax-weighted messages) uses bf16x3 split
-    precision and the sum/mean/max variants exact fp32 (unnormalised sums grow with the in-degree)."""
+    """Arithmetic of the per-edge GEMMs and the node table. ``PEMP_PRECISION`` (fp32 | bf16x3 | f16x3)
+    overrides. The default is f16x3 for every aggregation: f16 hi / scaled-lo split operands on the f16
+    MFMA, ~2^-22 relative error per product, which holds the 1e-4 logit bar at trained-checkpoint
+    magnitudes (|logit| ~ 50, tests/test_gpu_mpn.py::test_trained_scale) where bf16x3 (~2^-16) does
+    not, at the MFMA cost of bf16x3 (exact fp32 MFMA takes ~5x the matrix time). bf16x3 stays an
+    opt-in for small-magnitude models."""
     env = os.environ.get("PEMP_PRECISION", "")
     if env:
         if env not in PRECISIONS:
             raise ValueError(f"PEMP_PRECISION={env!r}: expected one of {sorted(PRECISIONS)}")
         return env
-    return "bf16x3" if aggr_code == AGGR_CODES["attn"] else "fp32"
+    return "f16x3"
 TYPE_LUTS = {"left_right": [0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8],
              "per_body_part": [0, 0, 0, 0, 0, 1, 1, 2, 3, 2, 3, 4, 5, 4, 5, 4, 5]}
 
@@ -208,9 +212,15 @@ class NodeClassificationMPNSimple(nn.Module):
         # because walking the module tree costs ~0.3 ms per call.
         if self._tensors is None:
             self._tensors = list(self.parameters()) + list(self.buffers())
-        key = (device, [t._version for t in self._tensors])
+        key = (device, self.precision, [t._version for t in self._tensors])
         if self._folded is None or self._folded_key != key:
-            self._folded = fold_weights(self, device)
+            try:
+                self._folded = fold_weights(self, device, self.precision)
+            except F16RangeError as exc:      # folded weights outside the f16 split range: exact fp32
+                warnings.warn(f"{exc}; this model runs in precision 'fp32'")
+                self.precision = "fp32"
+                key = (device, self.precision, key[2])
+                self._folded = fold_weights(self, device, self.precision)
             self._folded_key = key
         return self._folded
 
@@ -236,6 +246,7 @@ class NodeClassificationMPNSimple(nn.Module):
         t_stride = node_types.stride(0) if N > 0 else 1       # joint_det[:, 2] is read in place
         if self.precision not in PRECISIONS:
             raise ValueError(f"precision={self.precision!r}: expected one of {sorted(PRECISIONS)}")
+        fw = self._weights(dev)                               # may fall back to fp32 (weight range)
         A = edge_attr.shape[1] if edge_attr.dim() == 2 else 1
         dkey = (A, x.shape[1], self.precision, t_stride)
         if self._desc_key != dkey:
@@ -248,7 +259,6 @@ class NodeClassificationMPNSimple(nn.Module):
         desc, n_rec = self._desc_ref, self._n_rec
         ws = self._ws.get(L.pemp_mpn_workspace_size(desc, N, E), dev)
         st = _lib.stream(dev)
-        fw = self._weights(dev)
         # the three logit arrays share one allocation (one caching-allocator call per forward instead of
         # three); each segment starts on a 256-byte boundary
         ne, nn_ = max(n_rec, 1) * E, (n_rec + 1) * N

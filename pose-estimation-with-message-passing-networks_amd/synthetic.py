@@ -90,10 +90,11 @@ def closed_form(shape, salt: float) -> np.ndarray:
     return ((v - np.floor(v)) * 2.0 - 1.0).astype(np.float32)
 
 
-def closed_form_state_dict(module_or_sd, salt: float = 0.0, attn_gain: float = 1.0):
+def closed_form_state_dict(module_or_sd, salt: float = 0.0, attn_gain: float = 1.0, weight_gain: float = 1.0):
     """Deterministic weights for every tensor of a state_dict (BN stats kept non-trivial).
     `attn_gain` scales the attention net so its softmax is far from uniform (a fixture then tells
-    which attention row was used)."""
+    which attention row was used). `weight_gain` scales every Linear weight: 2.0 gives the logit
+    magnitudes of a trained checkpoint (|logit| up to ~20-55 on a C2-shaped graph, vs ~0.1 at 1.0)."""
     import torch
     sd = module_or_sd.state_dict() if hasattr(module_or_sd, "state_dict") else module_or_sd
     out = {}
@@ -109,7 +110,7 @@ def closed_form_state_dict(module_or_sd, salt: float = 0.0, attn_gain: float = 1
         elif k.endswith(".weight") and v.dim() == 1:   # BN gamma
             t = 0.8 + 0.2 * h
         elif v.dim() == 2:
-            t = h * (1.6 / math.sqrt(v.shape[1]))
+            t = h * (1.6 / math.sqrt(v.shape[1])) * weight_gain
         else:
             t = 0.05 * h
         if ".attn_net." in k:

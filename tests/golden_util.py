@@ -60,4 +60,6 @@ def mpn_config(meta):
     if meta.get("late_fusion"):
         c.LATE_FUSION_POS = True
         c.EDGE_EMB.BN = True
+    if meta.get("node_summary"):
+        c.NODE_TYPE_SUMMARY = meta["node_summary"]
     return c

@@ -41,6 +41,7 @@ def test_golden(name):
 CASES = [
     # B, J, H, W, persons, variant, graph, pool, thr, mask
     (8, 17, 640, 640, 9, "clean", "fully", 5, 0.1, False),      # C3 shape
+    (8, 17, 640, 640, 9, "clean", "knn", 5, 0.1, False),        # C3 shape, published knn (N ~ 150 > k + 1)
     (1, 14, 640, 640, 36, "clean", "fully", 5, 0.1, False),     # C5 shape (CrowdPose-dense)
     (3, 17, 200, 328, 5, "noisy", "knn", 3, 0.1, True),         # ragged W, masks, knn
     (2, 17, 96, 136, 1, "realistic", "fully", 5, 0.1, False),   # bilinear plateaus (4 equal maxima)

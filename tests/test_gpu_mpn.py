@@ -1,6 +1,7 @@
 """GPU parity of pemp_mpn_forward (NodeClassificationMPNSimple drop-in) against the reference's own
 logits (tests/golden) and the CPU oracle. Tolerance (north_star): edge/node/class logits within
-1e-4 absolute in fp32."""
+1e-4 absolute in fp32. Precisions: f16x3 (the default), fp32, and the bf16x3 opt-in (held to the bar
+only at the small logit magnitudes it is offered for)."""
 import numpy as np
 import pytest
 import torch
@@ -18,17 +19,17 @@ TOL = 1e-4          # north_star: logits within 1e-4 (fp32)
 REL_SUM = 2e-6
 
 
-def make_model(cfg, salt, precision=None, attn_gain=1.0):
+def make_model(cfg, salt, precision=None, attn_gain=1.0, weight_gain=1.0):
     m = pemp_amd.get_mpn_model(cfg)
-    sd = syn.closed_form_state_dict(m, salt, attn_gain)
+    sd = syn.closed_form_state_dict(m, salt, attn_gain, weight_gain)
     m.load_state_dict(sd)
     if precision:
         m.precision = precision
     return m.eval().to(DEV), sd
 
 
-# per-edge GEMM arithmetic: exact fp32 MFMA and bf16x3 split precision (the attention default)
-PRECS = ["fp32", "bf16x3"]
+# per-edge GEMM arithmetic: f16x3 split precision (the default), exact fp32 MFMA, bf16x3 (opt-in)
+PRECS = ["f16x3", "fp32", "bf16x3"]
 
 
 def run(model, x, ea, ei, types):
@@ -52,7 +53,9 @@ def test_golden(name, prec):
     cfg = gu.mpn_config(meta)
     if prec == "bf16x3" and "attn" not in name:
         pytest.skip("bf16x3 is offered for the attention variant")
-    model, _ = make_model(cfg, meta["salt"], prec, meta.get("attn_gain", 1.0))
+    if prec == "bf16x3" and meta.get("weight_gain", 1.0) > 1.0:
+        pytest.skip("bf16x3 (~2^-16 per product) misses 1e-4 at trained-scale logits: test_trained_scale")
+    model, _ = make_model(cfg, meta["salt"], prec, meta.get("attn_gain", 1.0), meta.get("weight_gain", 1.0))
     pe, pn, pc, tag = run(model, *(torch.from_numpy(a[k]) for k in ("x", "edge_attr", "edge_index", "node_types")))
     assert tag == [None]
     assert len(pe) == int(a["n_edge_preds"]) and len(pn) == int(a["n_node_preds"]) and len(pc) == len(pn)
@@ -72,6 +75,7 @@ def graph(B, J, H, W, persons, gtype="fully", seed=7):
 CASES = [
     # J, B, H, W, persons, variant, steps, aux, graph
     (17, 8, 160, 160, 9, "attn", 3, 0, "fully"),     # C3-shaped batch (N ~ 150/img)
+    (17, 8, 160, 160, 9, "attn", 3, 0, "knn"),       # C3-shaped, published knn graph (k = 50 < N)
     (14, 1, 256, 256, 36, "attn", 3, 0, "fully"),    # C5-shaped (N ~ 500, E ~ 250k)
     (17, 2, 128, 128, 6, "attn", 10, 2, "knn"),      # published T=10 with aux heads, knn
     (17, 2, 128, 128, 5, "max", 3, 0, "fully"),
@@ -231,3 +235,40 @@ def test_fully_graph_fast_prepare_is_identical(prec, monkeypatch):
     ei.add_(0)                                                  # in-place edit bumps the version
     assert mm._fully_graph(ei, types, x.shape[0]) is None
     assert mm._fully_graph(ei2, types, x.shape[0]) is None      # a copy carries no tag
+
+
+@pytest.mark.parametrize("variant", ["attn", "max"])
+def test_trained_scale(variant):
+    """Logit magnitudes of a trained checkpoint (every Linear weight x2: |logit| up to ~20-55 on this
+    C2/C3-shaped graph). f16x3 (the default) and fp32 hold 1e-4 against the fp64 oracle; bf16x3 does
+    not (~5e-4 here), which is why it is only an opt-in. The fp32 oracle itself is ~3e-5 from fp64."""
+    g = graph(2, 17, 160, 160, 9, "fully")
+    cfg = pcfg.published_mpn_config(17, 3, variant)
+    x, ea, ei, types = g[0], g[1], g[2], g[7][:, 2]
+    errs = {}
+    for prec in ("f16x3", "fp32", "bf16x3"):
+        model, sd = make_model(cfg, 9.5, prec, weight_gain=2.0)
+        pe, pn, pc, _ = run(model, x, ea, ei, types)
+        if prec == "f16x3":
+            sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
+            ref = restate.mpn_forward(sd64, cfg, x.double(), ea.double(), ei, types)
+            assert max(b[-1].abs().max().item() for b in ref[:3]) > 10.0      # trained-scale logits
+        errs[prec] = max(max_err(a[-1], b[-1]) for a, b in zip((pe, pn, pc), ref[:3]))
+    assert errs["f16x3"] < TOL and errs["fp32"] < TOL, errs
+    assert errs["bf16x3"] > errs["f16x3"], errs
+
+
+def test_f16_range_scaling():
+    """Activations past the f16 range (x 1e5 inputs): the range-scaled split keeps f16x3 at fp32 accuracy
+    relative to the logit magnitude."""
+    g = graph(1, 17, 96, 96, 3)
+    cfg = pcfg.published_mpn_config(17, 2, "max")
+    x, ea, ei, types = g[0] * 1e5, g[1], g[2], g[7][:, 2]
+    model, sd = make_model(cfg, 4.25, "f16x3")
+    pe, pn, pc, _ = run(model, x, ea, ei, types)
+    sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
+    ref = restate.mpn_forward(sd64, cfg, x.double(), ea.double(), ei, types)
+    for a, b in zip(pe + pn + pc, ref[0] + ref[1] + ref[2]):
+        scale = max(b.abs().max().item(), 1.0)
+        assert torch.isfinite(a).all()
+        assert max_err(a, b) < 1e-5 * scale

@@ -29,7 +29,7 @@ def test_construct_graph_matches_reference(name):
 def test_mpn_matches_reference(name):
     meta, a = gu.load(name)
     cfg = gu.mpn_config(meta)
-    sd = _state_dict(cfg, meta["salt"], meta.get("attn_gain", 1.0))
+    sd = _state_dict(cfg, meta["salt"], meta.get("attn_gain", 1.0), meta.get("weight_gain", 1.0))
     pe, pn, pc, tag = restate.mpn_forward(sd, cfg, torch.from_numpy(a["x"]), torch.from_numpy(a["edge_attr"]),
                                          torch.from_numpy(a["edge_index"]), torch.from_numpy(a["node_types"]))
     assert len(pe) == int(a["n_edge_preds"]) and len(pn) == int(a["n_node_preds"]) and tag == [None]
@@ -38,11 +38,11 @@ def test_mpn_matches_reference(name):
     np.testing.assert_allclose(pc[-1].numpy(), a["class_logits"], atol=1e-5, rtol=0)
 
 
-def _state_dict(cfg, salt, attn_gain=1.0):
+def _state_dict(cfg, salt, attn_gain=1.0, weight_gain=1.0):
     from pemp_amd.mpn.model import NodeClassificationMPNSimple
     from pemp_amd import synthetic as syn
     m = NodeClassificationMPNSimple(cfg)
-    return syn.closed_form_state_dict(m, salt, attn_gain)
+    return syn.closed_form_state_dict(m, salt, attn_gain, weight_gain)
 
 
 def test_per_type_attention_golden_distinguishes_rows():
