@@ -298,6 +298,8 @@ typedef struct pemp_mpn_weights {
    * with q0_w / q0_b / e1_w = edge_layer (e_init / e_cur columns), e2_w / e2_b = the e-block of out.1 and
    * the A / B rows of pre_w zero. L1, L2: [T][64][128] on [x_init | x_cur]; c1, c2: [T][64]; O1, O2: [64][64]. */
   const float *ept_l1_w, *ept_l1_b, *ept_l2_w, *ept_l2_b, *ept_o1_w, *ept_o2_w;
+  const float* edge_img;   /* edge-pass weight image (pemp_mpn_edge_image for the same desc), or NULL: then every
+                              forward builds it in its workspace */
 } pemp_mpn_weights;
 
 typedef struct pemp_mpn_desc {
@@ -349,6 +351,13 @@ int pemp_mpn_prepare(const pemp_mpn_desc* desc, const int64_t* edge_index, const
 /* The node embedding / node head / class head weights in the node kernels' LDS layout, built once
  * per weight set (stream-ordered) instead of once per forward: image of
  * pemp_mpn_node_image_floats(weights) floats, then weights->node_img = image. */
+/* The edge passes' weight image (per type: the pass's 64x64 blocks in the kernels' LDS row layout, bias and
+ * attention rows, the published edge head), built once per weight set and precision for `desc`
+ * (precision, aggregation, num_types) into a caller buffer of pemp_mpn_edge_image_floats() floats;
+ * pass it as pemp_mpn_weights.edge_img. No reference counterpart (replaces per-pass weight staging). */
+size_t pemp_mpn_edge_image_floats(const pemp_mpn_desc* desc, const pemp_mpn_weights* w);
+int pemp_mpn_edge_image(const pemp_mpn_desc* desc, const pemp_mpn_weights* w, float* image, size_t floats,
+                        void* stream);
 size_t pemp_mpn_node_image_floats(const pemp_mpn_weights* weights);
 int pemp_mpn_node_image(const pemp_mpn_weights* weights, float* image, size_t floats, void* stream);
 

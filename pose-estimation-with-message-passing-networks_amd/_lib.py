@@ -33,7 +33,7 @@ class PempMpnWeights(ctypes.Structure):
                 ("upd_bf", c_p), ("pre_bf", c_p), ("node_img", c_p), ("attn_bv", c_p),
                 ("upd_mlp", PempMlp),
                 ("ept_l1_w", c_p), ("ept_l1_b", c_p), ("ept_l2_w", c_p), ("ept_l2_b", c_p), ("ept_o1_w", c_p),
-                ("ept_o2_w", c_p)]
+                ("ept_o2_w", c_p), ("edge_img", c_p)]
 
 
 class PempMpnDesc(ctypes.Structure):
@@ -73,6 +73,8 @@ SIGNATURES = {
     "pemp_mpn_forward_fully": (c_i32, [ctypes.POINTER(PempMpnDesc), ctypes.POINTER(PempMpnWeights), c_p, c_p, c_p,
                                        c_p, c_i64, c_i64, c_p, c_p, c_i32, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "pemp_mpn_prepare": (c_i32, [ctypes.POINTER(PempMpnDesc), c_p, c_p, c_i64, c_i64, c_p, c_sz, c_p]),
+    "pemp_mpn_edge_image_floats": (c_sz, [ctypes.POINTER(PempMpnDesc), ctypes.POINTER(PempMpnWeights)]),
+    "pemp_mpn_edge_image": (c_i32, [ctypes.POINTER(PempMpnDesc), ctypes.POINTER(PempMpnWeights), c_p, c_sz, c_p]),
     "pemp_mpn_node_image_floats": (c_sz, [ctypes.POINTER(PempMpnWeights)]),
     "pemp_mpn_node_image": (c_i32, [ctypes.POINTER(PempMpnWeights), c_p, c_sz, c_p]),
     "pemp_mpn_status": (c_i32, [ctypes.POINTER(PempMpnDesc), c_i64, c_i64, c_p, c_p]),

@@ -40,11 +40,14 @@ __device__ __forceinline__ void st4(float* p, float a, float b, float c, float d
 }
 
 // acc[ob] += W[16ob + i][.] · in   (W row-major, row stride ldw; KB input / OB output blocks of 16)
+// (The weight pointers of the GEMM helpers carry no __restrict__: the inliner's noalias scopes would
+// replace the per-variable LDS scopes, and hipcc would then wait for every in-flight LDS-DMA of the edge
+// pass before each weight read.)
 #ifndef PEMP_GEMM_ORDER
 #define PEMP_GEMM_ORDER 0
 #endif
 template <int KB, int OB>
-__device__ __forceinline__ void gemm_frag(const float* __restrict__ W, int ldw, const float (&in)[KB][4],
+__device__ __forceinline__ void gemm_frag(const float* W, int ldw, const float (&in)[KB][4],
                                           float (&acc)[OB][4]) {
   const int lane = __lane_id(), i = lane & 15, g = lane >> 4;
   if (PEMP_GEMM_ORDER == 1) {   // k-outer: OB independent accumulation chains interleaved
@@ -192,10 +195,12 @@ __device__ __forceinline__ float scan_max_bwd(float v, const SegMask& m) {
 // ---------------------------------------------------------------------------------------------
 struct MpnWs {
   int *cnt, *seg, *wg_start, *perm, *s_src, *s_dst, *s_orig, *err;
-  float *X, *NT, *agg, *Q0, *EA, *EB, *img;
+  float *X, *NT, *agg, *Q0, *EA, *EB, *img, *eimg;
+  int4* ranges;
 };
 
 constexpr int IMG_FLOATS = 112 * 1024;  // >= LDS image of a node embedding (<= 4 layers, <= 128 wide) + both heads (<= 64 wide)
+constexpr int EIMG_MAX_STRIDE = 4 * D * LDW + (2 * D + 4) + (D + 32) * LDW + D + 32 + 32 + 4;   // edge image floats per type (max)
 
 static MpnWs mpn_carve(void* base, int T, int64_t N, int64_t E, size_t* bytes) {
   Carver c(base);
@@ -217,6 +222,9 @@ static MpnWs mpn_carve(void* base, int T, int64_t N, int64_t E, size_t* bytes) {
   w.EA = c.take<float>(E * D);
   w.EB = c.take<float>(E * D);
   w.img = c.take<float>(IMG_FLOATS);
+  const int G = std::max(num_cus(), T);       // edge-pass grid
+  w.ranges = c.take<int4>((size_t)G * (EDGE_WAVES + 12));
+  w.eimg = c.take<float>((size_t)T * EIMG_MAX_STRIDE);   // edge-pass weight image when the caller has none
   if (bytes) *bytes = c.used;
   return w;
 }
@@ -458,7 +466,7 @@ __global__ __launch_bounds__(256) void edge_embed_wide_kernel(pemp_mlp emb, cons
                                                          const int* __restrict__ s_orig, int64_t E,
                                                          const float* __restrict__ q0_w,
                                                          const float* __restrict__ q0_b, const float* __restrict__ e1_w,
-                                                         float* __restrict__ r0, float* __restrict__ q0) {
+                                                         float* __restrict__ r0, float* __restrict__ q0, float out_scale) {
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int64_t p = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + c;
   const bool valid = p < E;
@@ -481,14 +489,15 @@ __global__ __launch_bounds__(256) void edge_embed_wide_kernel(pemp_mlp emb, cons
     for (int r = 0; r < 4; ++r) e[ob][r] = a[ob][r];
   }
   gemm_frag<4, 4>(q0_w, 64, e, acc);
+  const float s = out_scale;                       // the edge passes' domain (f16x3: 2^11)
   if (valid) {
 #pragma unroll
-    for (int ob = 0; ob < 4; ++ob) st4(q0 + p * D + 16 * ob + 4 * g, acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]);
+    for (int ob = 0; ob < 4; ++ob) st4(q0 + p * D + 16 * ob + 4 * g, acc[ob][0] * s, acc[ob][1] * s, acc[ob][2] * s, acc[ob][3] * s);
   }
   gemm_frag<4, 4>(e1_w, 64, e, acc);              // R0 = Q0 + W1_e_cur · e_init
   if (valid) {
 #pragma unroll
-    for (int ob = 0; ob < 4; ++ob) st4(r0 + p * D + 16 * ob + 4 * g, acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]);
+    for (int ob = 0; ob < 4; ++ob) st4(r0 + p * D + 16 * ob + 4 * g, acc[ob][0] * s, acc[ob][1] * s, acc[ob][2] * s, acc[ob][3] * s);
   }
 }
 
@@ -517,7 +526,7 @@ __device__ __forceinline__ void split_bf16(const float (&x)[4][4], bf16x8_t (&hi
 // [hi 64 | lo 64 | pad 16]. The row stride (LDW = 72 dwords, = 8 mod 64) keeps the fragment reads
 // (row = lane & 15, 16 B at 8 (lane >> 4)) bank-conflict free for both parts (ds_read_b128 lane groups).
 template <int OB>
-__device__ __forceinline__ void gemm_bf3(const __bf16* __restrict__ W, const bf16x8_t (&hi)[2], const bf16x8_t (&lo)[2],
+__device__ __forceinline__ void gemm_bf3(const __bf16* W, const bf16x8_t (&hi)[2], const bf16x8_t (&lo)[2],
                                          float (&acc)[OB][4]) {
   const int lane = __lane_id(), i = lane & 15, g = lane >> 4;
 #pragma unroll
@@ -542,52 +551,67 @@ __device__ __forceinline__ void gemm_bf3(const __bf16* __restrict__ W, const bf1
 // v_mfma_f32_16x16x32_f16 (the f16 products are exact in fp32). Each pair carries 22 bits of its
 // operand (bf16x3: 16), so the dropped wl·xl term leaves ~2^-22 relative error per product:
 // fp32-level logits at trained-checkpoint magnitudes, where bf16x3 misses the 1e-4 bar
-// (tests/test_gpu_mpn.py::test_trained_scale). The accumulator is entered scaled by 2^11 and left by
-// 2^-11 (exact powers of two). Range: f16 holds |x| < 65504, so a wave whose fragment reaches 2^14
-// splits x·2^-16 instead and rescales by 2^16 on the way out (f16_big); the host keeps |w| < 32.
-// Same fragment slot order and LDS row layout as bf16x3.
+// (tests/test_gpu_mpn.py::test_trained_scale).
+// Scale domain: the accumulators are never rescaled. Every GEMM output of the edge passes, and the
+// per-edge state r, Q0 and the node table that feed them, live in the 2^11 domain (dom<PREC>());
+// the split of a fragment folds the 2^-11 back in (v_fma_mix with a scale operand), biases and
+// attention rows come pre-scaled in the weight image, and results leave the domain once, where the
+// segments are normalised. Range: f16 holds |x| < 65504, so a wave whose (scaled) fragment reaches
+// 2^14 splits x·2^-16 instead and its GEMMs rescale by 2^16 (exact powers of two; rare, uniform
+// branch); the host keeps |w| < 32. Same fragment slot order and LDS row layout as bf16x3.
 typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
-constexpr float F16_BIG = 16384.0f;
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+constexpr float F16_BIG = 16384.0f, F16_DOWN = 1.0f / 65536.0f, F16_UP = 65536.0f;
+template <int PREC>
+__host__ __device__ constexpr float dom() { return PREC == 2 ? 2048.0f : 1.0f; }
+template <int PREC>
+__host__ __device__ constexpr float dom_inv() { return PREC == 2 ? 1.0f / 2048.0f : 1.0f; }
 
-// wave-uniform: some |x| of the fragment reaches 2^14 (or is NaN): take the range-scaled split
-__device__ __forceinline__ bool f16_big(const float (&x)[4][4]) {
+// f16 pair of (s x0, s x1): hi = f16(s x), lo = f16(s x - hi) -- v_fma_mix: exact fp32 fma, one rounding
+__device__ __forceinline__ void split_pair(float x0, float x1, float s, uint32_t& hi, uint32_t& lo) {
+  asm("v_fma_mixlo_f16 %0, %2, %4, 0\n\t"
+      "v_fma_mixhi_f16 %0, %3, %4, 0\n\t"
+      "v_fma_mixlo_f16 %1, %2, %4, -%0 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %3, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(hi), "=&v"(lo)
+      : "v"(x0), "v"(x1), "s"(s));
+}
+
+// wave-uniform: some |s x| of the fragment reaches 2^14 (or is NaN): take the range-scaled split
+__device__ __forceinline__ bool f16_big(const float (&x)[4][4], float s) {
   float m = 0.0f;
 #pragma unroll
   for (int b = 0; b < 4; ++b) m = fmaxf(m, fmaxf(fmaxf(fabsf(x[b][0]), fabsf(x[b][1])), fmaxf(fabsf(x[b][2]), fabsf(x[b][3]))));
-  return __any(!(m < F16_BIG));
+  return __any(!(m * s < F16_BIG));
 }
 
-template <bool SCALED>
-__device__ __forceinline__ void split_f16(const float (&x)[4][4], f16x8_t (&hi)[2], f16x8_t (&lo)[2]) {
+// split of the fragment s·x (s a power of two); returns the wave's range flag (then the parts hold s·x·2^-16)
+__device__ __forceinline__ bool split_f16(const float (&x)[4][4], float s, f16x8_t (&hi)[2], f16x8_t (&lo)[2]) {
+  const bool big = f16_big(x, s);
+  const float ss = big ? s * F16_DOWN : s;
 #pragma unroll
-  for (int kb = 0; kb < 2; ++kb)
+  for (int kb = 0; kb < 2; ++kb) {
+    uint32_t h[4], l[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float f = SCALED ? x[2 * kb + (j >> 2)][j & 3] * (1.0f / 65536.0f) : x[2 * kb + (j >> 2)][j & 3];
-      const _Float16 h = (_Float16)f;
-      hi[kb][j] = h;
-      lo[kb][j] = (_Float16)(f - (float)h);
-    }
-}
-
-// split of one fragment; returns the (accumulator-in, accumulator-out) scale factors
-__device__ __forceinline__ float2 split_f16_any(const float (&x)[4][4], f16x8_t (&hi)[2], f16x8_t (&lo)[2]) {
-  if (__builtin_expect(f16_big(x), 0)) {
-    split_f16<true>(x, hi, lo);
-    return make_float2(1.0f / 32.0f, 32.0f);       // 2^11 * 2^-16 in, back out
+    for (int d = 0; d < 4; ++d)
+      split_pair(x[2 * kb + (d >> 1)][2 * (d & 1)], x[2 * kb + (d >> 1)][2 * (d & 1) + 1], ss, h[d], l[d]);
+    const u32x4_t hv = {h[0], h[1], h[2], h[3]}, lv = {l[0], l[1], l[2], l[3]};
+    hi[kb] = __builtin_bit_cast(f16x8_t, hv);
+    lo[kb] = __builtin_bit_cast(f16x8_t, lv);
   }
-  split_f16<false>(x, hi, lo);
-  return make_float2(2048.0f, 1.0f / 2048.0f);
+  return big;
 }
 
-// acc[ob] += W[16 ob + i][.] · x (K = 64), W = interleaved f16 rows [wh 64 | wl 64 | pad] (gemm_bf3 layout)
-template <int OB>
-__device__ __forceinline__ void gemm_h3(const _Float16* __restrict__ W, const f16x8_t (&hi)[2], const f16x8_t (&lo)[2],
-                                        float2 sc, float (&acc)[OB][4]) {
+// acc[ob] += W'[16 ob + i][.] · x (K = 64) in the 2^11 domain: acc raw in, raw out. W = interleaved f16
+// rows [wh 64 | wl 64 | pad] (gemm_bf3 layout); BIG: the split carried an extra 2^-16
+template <int OB, bool BIG>
+__device__ __forceinline__ void gemm_h3_body(const _Float16* W, const f16x8_t (&hi)[2],
+                                             const f16x8_t (&lo)[2], float (&acc)[OB][4]) {
   const int lane = __lane_id(), i = lane & 15, g = lane >> 4;
 #pragma unroll
   for (int ob = 0; ob < OB; ++ob) {
-    f32x4 c = {acc[ob][0] * sc.x, acc[ob][1] * sc.x, acc[ob][2] * sc.x, acc[ob][3] * sc.x};
+    f32x4 c = {acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]};
+    if (BIG) c *= F16_DOWN;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
       const int o = (16 * ob + i) * 2 * LDW + 32 * kb + 8 * g;
@@ -597,25 +621,48 @@ __device__ __forceinline__ void gemm_h3(const _Float16* __restrict__ W, const f1
       c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, lo[kb], c, 0, 0, 0);
       c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, hi[kb], c, 0, 0, 0);
     }
-    acc[ob][0] = c[0] * sc.y; acc[ob][1] = c[1] * sc.y; acc[ob][2] = c[2] * sc.y; acc[ob][3] = c[3] * sc.y;
+    if (BIG) c *= F16_UP;
+    acc[ob][0] = c[0]; acc[ob][1] = c[1]; acc[ob][2] = c[2]; acc[ob][3] = c[3];
   }
 }
 
-// one layer on fragments in the chosen precision; W points at the LDS image of the matrix
-// (PREC 0: fp32 [out][LDW]; PREC 1 / 2: interleaved 16-bit rows [out][hi 64 | lo 64 | pad], see gemm_bf3)
+// the range flag picks one of two whole GEMM bodies (a uniform branch: the common body has no rescaling)
+template <int OB>
+__device__ __forceinline__ void gemm_h3(const _Float16* W, const f16x8_t (&hi)[2], const f16x8_t (&lo)[2],
+                                        bool big, float (&acc)[OB][4]) {
+  if (__builtin_expect(big, 0)) gemm_h3_body<OB, true>(W, hi, lo, acc);
+  else gemm_h3_body<OB, false>(W, hi, lo, acc);
+}
+
+// A GEMM input fragment prepared once for the precision (split parts), reusable by several GEMMs.
+template <int PREC>
+struct Frag {
+  bf16x8_t bh[2], bl[2];
+  f16x8_t hh[2], hl[2];
+  bool big;
+};
+
+// x in the precision's domain (dom<PREC>() x_true for f16x3): split for the GEMMs that read it
+template <int PREC>
+__device__ __forceinline__ void prep(const float (&x)[4][4], Frag<PREC>& f) {
+  if constexpr (PREC == 1) split_bf16(x, f.bh, f.bl);
+  else if constexpr (PREC == 2) f.big = split_f16(x, dom_inv<PREC>(), f.hh, f.hl);
+}
+
+// x in the true domain (f16x3: split with scale 1)
+template <int PREC>
+__device__ __forceinline__ void prep_true(const float (&x)[4][4], Frag<PREC>& f) {
+  if constexpr (PREC == 1) split_bf16(x, f.bh, f.bl);
+  else if constexpr (PREC == 2) f.big = split_f16(x, 1.0f, f.hh, f.hl);
+}
+
+// acc (domain) += W · x_true over one prepared fragment; W = the LDS image of the matrix
+// (PREC 0: fp32 [out][LDW]; PREC 1 / 2: interleaved 16-bit rows [out][hi 64 | lo 64 | pad])
 template <int PREC, int OB>
-__device__ __forceinline__ void gemm_p(const void* W, const float (&x)[4][4], float (&acc)[OB][4]) {
-  if (PREC == 0) {
-    gemm_frag<4, OB>(static_cast<const float*>(W), LDW, x, acc);
-  } else if (PREC == 1) {
-    bf16x8_t hi[2], lo[2];
-    split_bf16(x, hi, lo);
-    gemm_bf3<OB>(static_cast<const __bf16*>(W), hi, lo, acc);
-  } else {
-    f16x8_t hi[2], lo[2];
-    const float2 sc = split_f16_any(x, hi, lo);
-    gemm_h3<OB>(static_cast<const _Float16*>(W), hi, lo, sc, acc);
-  }
+__device__ __forceinline__ void gemm_f(const void* W, const float (&x)[4][4], const Frag<PREC>& f, float (&acc)[OB][4]) {
+  if constexpr (PREC == 0) gemm_frag<4, OB>(static_cast<const float*>(W), LDW, x, acc);
+  else if constexpr (PREC == 1) gemm_bf3<OB>(static_cast<const __bf16*>(W), f.bh, f.bl, acc);
+  else gemm_h3<OB>(static_cast<const _Float16*>(W), f.hh, f.hl, f.big, acc);
 }
 
 // global [hi rows][lo rows] bf16 pack row `row` (< 2 rows_per_part) -> its place in an interleaved
@@ -700,22 +747,28 @@ __device__ __forceinline__ void layer_lds(const float* __restrict__ W, int ldw, 
 }
 
 // split-precision variants (PREC 1 bf16x3, PREC 2 f16x3): W = interleaved rows
-// [16 OB][hi 32 KB32 | lo 32 KB32 | pad], stride ldw; KB32 (<= 2) k-blocks of 32 inputs.
+// [16 OB][hi 32 KB32 | lo 32 KB32 | pad], stride ldw; KB32 (<= 2) k-blocks of 32 inputs. True-domain
+// input and output (f16x3: the bias enters scaled by 2^11, the result leaves scaled by 2^-11).
 template <int PREC>
 __device__ __forceinline__ void layer_lds_p(const uint16_t* __restrict__ W, int ldw, const float* __restrict__ bias,
                                             int KB32, int OB, int relu, const float (&in)[4][4], float (&out)[4][4]) {
   const int lane = __lane_id(), i = lane & 15, g = lane >> 4;
   bf16x8_t hb[2], lb[2];
   f16x8_t hh[2], lh[2];
-  float2 sc = make_float2(1.0f, 1.0f);
-  if (PREC == 1) split_bf16(in, hb, lb);
-  else sc = split_f16_any(in, hh, lh);
+  float s_in = 1.0f, s_out = 1.0f;
+  if (PREC == 1) {
+    split_bf16(in, hb, lb);
+  } else {
+    const bool big = split_f16(in, 1.0f, hh, lh);
+    s_in = big ? 2048.0f * F16_DOWN : 2048.0f;
+    s_out = big ? F16_UP / 2048.0f : 1.0f / 2048.0f;
+  }
   const int lo_off = 32 * KB32;                 // interleaved rows: [hi | lo | pad]
 #pragma unroll
   for (int ob = 0; ob < 4; ++ob) {
     if (ob < OB) {
       const float4 bb = ld4(bias + 16 * ob + 4 * g);
-      f32x4 c = {bb.x * sc.x, bb.y * sc.x, bb.z * sc.x, bb.w * sc.x};
+      f32x4 c = {bb.x * s_in, bb.y * s_in, bb.z * s_in, bb.w * s_in};
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         if (kb < KB32) {
@@ -737,41 +790,13 @@ __device__ __forceinline__ void layer_lds_p(const uint16_t* __restrict__ W, int 
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float v = c[r] * sc.y;
+        const float v = c[r] * s_out;
         out[ob][r] = relu ? fmaxf(v, 0.0f) : v;
       }
     } else {
 #pragma unroll
       for (int r = 0; r < 4; ++r) out[ob][r] = 0.0f;
     }
-  }
-}
-
-// Stage the edge-embedding LDS image (layers, then the Q0 tile, then biases; EmbedLayout).
-template <int PREC>
-__device__ inline void stage_embed(float* sm, const pemp_mlp& emb, const EmbedLayout& Lo, const uint16_t* emb_bf,
-                                   const float* q0_w, const float* q0_b) {
-  for (int l = 0; l <= Lo.n; ++l) {
-    const float* bsrc = l < Lo.n ? emb.layer[l].b : q0_b;
-    const int rows = 16 * Lo.ob[l];
-    if (PREC == 0) {
-      const float* src = l < Lo.n ? emb.layer[l].w : q0_w;
-      const int ip = 16 * Lo.kb[l], q4 = ip / 4;
-      for (int idx = threadIdx.x; idx < rows * q4; idx += blockDim.x) {
-        const int row = idx / q4, c4 = (idx - row * q4) * 4;
-        *reinterpret_cast<float4*>(&sm[Lo.w_off[l] + row * Lo.stride[l] + c4]) = ld4(src + row * ip + c4);
-      }
-    } else {
-      const uint16_t* src = emb_bf + Lo.g_off[l];
-      const int ip = 32 * Lo.kb[l], q8 = ip / 8;
-      __bf16* dstb = reinterpret_cast<__bf16*>(sm + Lo.w_off[l]);
-      for (int idx = threadIdx.x; idx < 2 * rows * q8; idx += blockDim.x) {   // hi rows, then lo rows
-        const int row = idx / q8, c8 = (idx - row * q8) * 8;
-        *reinterpret_cast<uint4*>(&dstb[interleaved_slot(row, rows, Lo.stride[l], ip) + c8]) =
-            *reinterpret_cast<const uint4*>(src + row * ip + c8);
-      }
-    }
-    for (int idx = threadIdx.x; idx < rows; idx += blockDim.x) sm[Lo.b_off[l] + idx] = bsrc[idx];
   }
 }
 
@@ -883,12 +908,20 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp em
     const int64_t o = s_orig[valid ? p : end - 1];
     float x[4][4], y[4][4];
     load_edge_attr(ea, A, o, x);
-    embed_tile<PREC>(smz, Lo, x, y);
+    embed_tile<PREC>(smz, Lo, x, y);              // x = e_init, y = Q0 (true values)
+    if (PREC == 2) {                              // Q0 and R0 are kept in the f16x3 domain (x 2^11)
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) y[ob][r] *= dom<PREC>();
+    }
     if (valid) {
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob) st4(q0 + p * D + 16 * ob + 4 * g, y[ob][0], y[ob][1], y[ob][2], y[ob][3]);
     }
-    gemm_p<PREC, 4>(smz + Lo.total, x, y);        // R0 = Q0 + W1_e_cur · e_init
+    Frag<PREC> fx;
+    prep_true<PREC>(x, fx);
+    gemm_f<PREC, 4>(smz + Lo.total, x, fx, y);    // R0 = Q0 + W1_e_cur · e_init
     if (valid) {
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob) st4(r0 + p * D + 16 * ob + 4 * g, y[ob][0], y[ob][1], y[ob][2], y[ob][3]);
@@ -902,23 +935,14 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp em
 struct EdgeStepArgs {
   int64_t N, E;
   int T, t_nt_ld;   // node-table row length = 128 + 64 T
-  const int *seg, *wg_start, *s_src, *s_dst, *s_orig;
+  const int4* ranges;             // per (block, wave): first, end, source type (edge_ranges_fill)
+  const int *s_src, *s_dst, *s_orig;
   const float *NT, *Q0, *r_cur;   // r = Q0 + W1_e_cur · e_cur (layer-1 input without the node terms)
-  float *r_next, *q0_out;         // r_next = Q0 + W1_e_cur · e' (unless the last pass); FIRST: Q0 out
-  const float* ea;                // STAGE_FIRST: edge_attr [E][A] and the embedding (LDS image at emb_off)
-  int A, emb_off;
-  EmbedLayout Lo;
-  pemp_mlp emb;
-  const uint16_t* emb_bf;
-  const float *q0_w, *q0_b;
-  const float *e1_w, *e2_w, *e2_b, *msg_w, *attn_w;
-  const uint16_t *e1_bf, *e2_bf, *msg_bf, *head_bf;   // PREC 1: [hi | lo][out][64] k-permuted bf16
-  const float* upd_w;        // UPD 1: update_mlp.0.weight [64][64 T] (U_t = columns 64 t .. 64 t + 63)
-  const uint16_t* upd_bf;    // UPD 1, PREC 1: [T][hi | lo][64][64]
-  float attn_b;
-  const float* attn_bv;      // per-type attention (node_edge_attn_per_type): bias [17], attn_w [17][64]
+  float* r_next;                  // r_next = Q0 + W1_e_cur · e' (middle passes)
+  const float* img;               // edge-pass weight image, per type (edge_image_kernel)
+  int64_t img_stride;             // floats per type
   float* agg;
-  pemp_mlp head;
+  pemp_mlp head;                  // HEAD 2: generic edge head, weights in global memory
   float* edge_logits;
   int write_next;
   unsigned long long* stamps;   // diagnostic builds (-DPEMP_STAMPS) only: per-wave phase timestamps
@@ -1025,167 +1049,280 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
 }
 
 
-// LDS image of the edge pass (floats): three 64x64 weight tiles, e2_b | attn_w, and for the
-// fused published edge head (HEAD 1) its 64x64 and 32x64 tiles + biases + last row.
-constexpr int LDS_W = 3 * D * LDW;
-constexpr int LDS_VEC = 2 * D;
-constexpr int LDS_HEAD = (D + 32) * LDW + D + 32 + 32;
+// ---- edge-pass weight image --------------------------------------------------------------------
+// The LDS image of one edge pass, prepared once per weight set in global memory (one block per source
+// type t, edge_image_kernel / pemp_mpn_edge_image) and copied into LDS with 16-byte LDS-DMA loads:
+//   common [W1_e_cur | W2 | W_t (message) | U_t (UPD only)]   64 x LDW floats each (PREC 0: fp32 rows;
+//          PREC 1/2: interleaved 16-bit rows [hi 64 | lo 64 | pad], gemm_bf3)
+//          vec [e2_b 64 | attention row t 64 | attention bias t | pad 3]
+//   head   (published 64 -> 64 -> 32 -> 1 edge head) [L1 64 x LDW | L2 32 x LDW | b1 64 | b2 32 | w3 32 | b3 | pad 3]
+// Middle passes copy the common part, the recorded (head) pass both.
+constexpr int IMG_VEC = 2 * D + 4;
+constexpr int IMG_HEAD = (D + 32) * LDW + D + 32 + 32 + 4;
+__host__ __device__ constexpr int img_common(int upd) { return (3 + upd) * D * LDW + IMG_VEC; }
+__host__ __device__ constexpr int img_stride(int upd, int head) { return img_common(upd) + (head ? IMG_HEAD : 0); }
 
+struct EdgeImgArgs {
+  int T, prec, upd, head, aggr;
+  const float *e1_w, *e2_w, *e2_b, *msg_w, *attn_w, *attn_bv, *upd_w;
+  float attn_b;
+  const uint16_t *e1_bf, *e2_bf, *msg_bf, *upd_bf, *head_bf;
+  pemp_mlp head_mlp;
+  float* img;
+};
+
+// one 64-row matrix block of the image: float `f` of row `row` (< rows), stride LDW
+__device__ inline float img_matrix_elem(int prec, int row, int f, const float* w32, int64_t ld32, const uint16_t* w16,
+                                        int rows16) {
+  if (prec == PEMP_PREC_FP32) return f < D ? w32[row * ld32 + f] : 0.0f;
+  // interleaved 16-bit row: floats 0..31 = hi pairs, 32..63 = lo pairs, 64..71 pad
+  if (f >= 2 * (D / 2)) return 0.0f;
+  const int part = f >= D / 2, e = 2 * (f - part * (D / 2));
+  const uint16_t* src = w16 + (int64_t)part * rows16 * D + (int64_t)row * D + e;
+  return __uint_as_float((uint32_t)src[0] | ((uint32_t)src[1] << 16));
+}
+
+__global__ __launch_bounds__(256) void edge_image_kernel(EdgeImgArgs a) {
+  const int t = blockIdx.y, T = a.T;
+  const int common = img_common(a.upd), total = img_stride(a.upd, a.head);
+  // f16x3 keeps the pass's GEMM outputs x 2^11: biases enter scaled up, the rows that reduce e' or the
+  // head's last hidden layer to a scalar scaled down (dom<2>)
+  const float dm = a.prec == PEMP_PREC_F16X3 ? dom<2>() : 1.0f, di = 1.0f / dm;
+  float* out = a.img + (int64_t)t * total;
+  for (int idx = blockIdx.x * 256 + threadIdx.x; idx < total; idx += gridDim.x * 256) {
+    float v = 0.0f;
+    if (idx < (3 + a.upd) * D * LDW) {
+      const int m = idx / (D * LDW), r = idx - m * D * LDW, row = r / LDW, f = r - row * LDW;
+      if (m == 0) v = img_matrix_elem(a.prec, row, f, a.e1_w, D, a.e1_bf, D);
+      else if (m == 1) v = img_matrix_elem(a.prec, row, f, a.e2_w, D, a.e2_bf, D);
+      else if (m == 2) v = img_matrix_elem(a.prec, row, f, a.msg_w + (int64_t)t * D * D, D, a.msg_bf + (int64_t)t * 2 * D * D, D);
+      else v = img_matrix_elem(a.prec, row, f, a.upd_w + 64 * t, 64 * T, a.upd_bf ? a.upd_bf + (int64_t)t * 2 * D * D : nullptr, D);
+    } else if (idx < common) {
+      const int k = idx - (3 + a.upd) * D * LDW;
+      if (k < D) v = a.e2_b[k] * dm;
+      else if (k < 2 * D) v = a.aggr == PEMP_AGGR_ATTN ? a.attn_w[(a.attn_bv ? t * D : 0) + k - D] * di : 0.0f;
+      else if (k == 2 * D) v = a.aggr == PEMP_AGGR_ATTN ? (a.attn_bv ? a.attn_bv[t] : a.attn_b) : 0.0f;
+    } else {
+      const int k = idx - common;
+      const pemp_mlp& h = a.head_mlp;
+      if (k < (D + 32) * LDW) {
+        const int row = k / LDW, f = k - row * LDW;
+        if (row < D) v = img_matrix_elem(a.prec, row, f, h.layer[0].w, D, a.head_bf, D);
+        else v = img_matrix_elem(a.prec, row - D, f, h.layer[1].w, D, a.head_bf ? a.head_bf + 2 * D * D : nullptr, 32);
+      } else {
+        const int q = k - (D + 32) * LDW;
+        if (q < D) v = h.layer[0].b[q] * dm;
+        else if (q < D + 32) v = h.layer[1].b[q - D] * dm;
+        else if (q < D + 64) v = h.layer[2].w[q - D - 32] * di;
+        else if (q == D + 64) v = h.layer[2].b[0];
+      }
+    }
+    out[idx] = v;
+  }
+}
+
+// ---- one message-passing iteration over all edges -------------------------------------------------
 // HEAD: 0 = no edge head, 1 = published head 64 -> 64 -> 32 -> 1 (ReLU, ReLU), 2 = generic pemp_mlp
 // UPD 1 (linear aggregations with an update MLP): each message is multiplied by the type's update
 // block U_t before aggregation, so agg holds U_t · agg[n, t] (the per-type term of update_mlp.0,
-// layers.py:253-258) and the node update is a plain sum over types. The U_t tile sits after the
-// rest of the LDS image.
+// layers.py:253-258) and the node update is a plain sum over types.
 //
 // Work split (balanced, no atomics): the edges of source type t (contiguous in the type-major
-// order) are cut into wg_start[t+1]-wg_start[t] equal workgroup ranges, each cut into
-// EDGE_WAVES equal wave ranges; every range boundary is moved forward to the next segment
-// start, so each (target, type) segment is reduced by exactly one wave. A wave walks its range
-// in 16-edge tiles; a segment that crosses a tile boundary is carried in registers.
-// PREC: 0 = exact fp32 MFMA (v_mfma_f32_16x16x4_f32), 1 = bf16x3 split precision (see gemm_bf3).
-// The LDS image has the same size in both: a 64 x LDW fp32 tile = its bf16 hi and lo tiles.
-enum { STAGE_FIRST = 0, STAGE_MID = 1, STAGE_LAST = 2, STAGE_EPT = 4 };
-#ifndef PEMP_FUSED_FIRST
-#define PEMP_FUSED_FIRST 0
-#endif
+// order) are cut into equal workgroup ranges, each cut into NW equal wave ranges; every range
+// boundary is moved forward to the next segment start, so each (target, type) segment is reduced
+// by exactly one wave (edge_wave_range, computed once per forward into a table). A wave walks its
+// range in 16-edge tiles; a segment that crosses a tile boundary is carried in registers.
+// Memory pipeline per tile k: the r rows of tile k+1 (the only per-edge stream besides Q0) are in
+// flight as LDS-DMA loads into the wave's 4 KB buffer (XOR-swizzled by row: conflict-free reads)
+// while tile k computes; Q0 rows and the node-table gathers of tile k are issued before that DMA,
+// so waiting for them never waits for it; the indices run two tiles ahead.
+// PREC: 0 = exact fp32 MFMA (v_mfma_f32_16x16x4_f32), 1 = bf16x3, 2 = f16x3 (gemm_bf3 / gemm_h3).
+enum { STAGE_MID = 1, STAGE_LAST = 2, STAGE_EPT = 4 };
 
-// STAGE_FIRST: the first pass with the edge embedding fused (reads edge_attr, writes Q0 and r_next);
-// STAGE_MID reads r_cur and Q0 and writes r_next; STAGE_LAST reads r_cur only.
-// waves per workgroup: 16 (<= 128 VGPRs); the embedding-fused first pass needs more registers: 8
-// PEMP_EDGE_PIPE (build flag, default off): the middle / last passes prefetch the next tile's rows
-// while the current tile computes. 1: r, Q0 and the three node-table gathers (80 VGPRs, 8 waves per
-// CU): 47.3 us vs 41.8 us per C3 pass; 2: r and Q0 only (12 waves): 43.4 us. Occupancy (16 waves)
-// hides more latency than the prefetch does, so both stay off.
-#ifndef PEMP_EDGE_PIPE
-#define PEMP_EDGE_PIPE 0
-#endif
-template <int STAGE>
-constexpr bool edge_pipe() { return PEMP_EDGE_PIPE && (STAGE & 3) != STAGE_FIRST; }
-template <int STAGE>
-constexpr int edge_waves() {
-  return (STAGE & 3) == STAGE_FIRST ? 8 : edge_pipe<STAGE>() ? (PEMP_EDGE_PIPE == 2 ? 12 : 8) : EDGE_WAVES;
-}
+// waves per workgroup (one workgroup per CU): 16 (<= 128 VGPRs); a recorded pass carries the head
+// weights in LDS and needs more registers: 12
+template <int HEAD>
+constexpr int edge_waves() { return HEAD == 1 ? 12 : EDGE_WAVES; }
 
-template <int AGG, int HEAD, int PREC, int UPD, int STAGE>
-__global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(EdgeStepArgs a) {
-  constexpr int NW = edge_waves<STAGE>();
-  // STAGE bit 2 (STAGE_EPT): EDGE_MLP per_type (TypeAwareEdgeUpdate, layers.py:275-303). The node
-  // terms A'[dst] + B'[src] (already through their own ReLU and out-block, node_ept_kernel) join
-  // after the e-block GEMM instead of inside the first ReLU.
-  constexpr bool EPT = (STAGE & STAGE_EPT) != 0;
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* wl = sm;                               // [3][64][LDW]: e1_w (e_cur part), e2_w, msg_w[t]
-  float* vec = sm + LDS_W;                      // e2_b[64] | attn_w[64]
-  float* hw = vec + LDS_VEC;                    // HEAD 1: [64][LDW] L1.w, [32][LDW] L2.w, b1[64], b2[32], w3[32]
-  float* hb_l = hw + (D + 32) * LDW;
-  float* uw = hw + (HEAD == 1 ? LDS_HEAD : 0);  // UPD 1: [64][LDW] U_t (or its hi + lo bf16)
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
-  const int T = a.T;
-  const int blk = blockIdx.x;
-  EDGE_STAMP(0);
-  if (blk >= a.wg_start[T]) return;             // uniform for the block
+// wave range table entry: first, end (sorted positions), source type, unused
+__device__ inline int4 edge_wave_range(const int* __restrict__ seg, const int* __restrict__ wg_start,
+                                       const int* __restrict__ s_dst, int T, int64_t N, int blk, int wave, int NW) {
+  if (blk >= wg_start[T]) return make_int4(0, 0, 0, 0);
   int t = 0;
-  while (t + 1 < T && a.wg_start[t + 1] <= blk) ++t;
-  const float attn_b = a.attn_bv ? a.attn_bv[t] : a.attn_b;
-  {
-    if (PREC == 0) {
-      const float* srcs[3] = {a.e1_w, a.e2_w, a.msg_w + (int64_t)t * D * D};
-      for (int idx = threadIdx.x; idx < 3 * D * 16; idx += 64 * NW) {
-        const int mtx = idx / (D * 16), rem = idx - mtx * D * 16, row = rem >> 4, c4 = (rem & 15) * 4;
-        *reinterpret_cast<float4*>(&wl[(mtx * D + row) * LDW + c4]) = ld4(srcs[mtx] + row * D + c4);
-      }
-    } else {
-      // 3 matrices x (hi, lo) x 64 rows of 64 bf16 (8 x 16 B) -> bf16 rows of stride LDW
-      const uint16_t* srcs[3] = {a.e1_bf, a.e2_bf, a.msg_bf + (int64_t)t * 2 * D * D};
-      __bf16* wb = reinterpret_cast<__bf16*>(wl);
-      for (int idx = threadIdx.x; idx < 3 * 2 * D * 8; idx += 64 * NW) {
-        const int mtx = idx / (2 * D * 8), rem = idx - mtx * 2 * D * 8, row = rem >> 3, c8 = (rem & 7) * 8;
-        *reinterpret_cast<uint4*>(&wb[mtx * 2 * D * LDW + interleaved_slot(row, D, 2 * LDW, D) + c8]) =
-            *reinterpret_cast<const uint4*>(srcs[mtx] + row * D + c8);
-      }
-    }
-    if (threadIdx.x < D) vec[threadIdx.x] = a.e2_b[threadIdx.x];
-    else if (threadIdx.x < 2 * D)   // messages of source type t use attention row t when per-type
-      vec[threadIdx.x] = (AGG == PEMP_AGGR_ATTN) ? a.attn_w[(a.attn_bv ? t * D : 0) + threadIdx.x - D] : 0.0f;
-    if (HEAD == 1) {
-      if (PREC == 0) {
-        for (int idx = threadIdx.x; idx < (D + 32) * 16; idx += 64 * NW) {
-          const int row = idx >> 4, c4 = (idx & 15) * 4;
-          const float* src = row < D ? a.head.layer[0].w + row * D : a.head.layer[1].w + (row - D) * D;
-          *reinterpret_cast<float4*>(&hw[row * LDW + c4]) = ld4(src + c4);
-        }
-      } else {
-        // head_bf: L1 [hi|lo][64][64], then L2 [hi|lo][32][64] -> same row order in LDS
-        __bf16* hwb = reinterpret_cast<__bf16*>(hw);
-        for (int idx = threadIdx.x; idx < 2 * (D + 32) * 8; idx += 64 * NW) {
-          const int row = idx >> 3, c8 = (idx & 7) * 8;
-          const int slot = row < 2 * D ? interleaved_slot(row, D, 2 * LDW, D)
-                                       : 2 * D * LDW + interleaved_slot(row - 2 * D, 32, 2 * LDW, D);
-          *reinterpret_cast<uint4*>(&hwb[slot + c8]) = *reinterpret_cast<const uint4*>(a.head_bf + row * D + c8);
-        }
-      }
-      float* hb = hb_l;
-      if (threadIdx.x < D) hb[threadIdx.x] = a.head.layer[0].b[threadIdx.x];
-      else if (threadIdx.x < D + 32) hb[threadIdx.x] = a.head.layer[1].b[threadIdx.x - D];
-      else if (threadIdx.x < D + 64) hb[threadIdx.x] = a.head.layer[2].w[threadIdx.x - D - 32];
-    }
-    if (UPD) stage_tile64<PREC>(uw, a.upd_w + 64 * t, 64 * T, PREC != 0 ? a.upd_bf + (int64_t)t * 2 * D * D : nullptr);
-    if ((STAGE & 3) == STAGE_FIRST) stage_embed<PREC>(sm + a.emb_off, a.emb, a.Lo, a.emb_bf, a.q0_w, a.q0_b);
-  }
-  __syncthreads();
-  EDGE_STAMP(1);
-
-  // ---- this wave's range ----
-  const int64_t N = a.N;
-  const int ts = a.seg[t * N], te = a.seg[(t + 1) * N];
-  const int gt = a.wg_start[t + 1] - a.wg_start[t], j = blk - a.wg_start[t];
+  while (t + 1 < T && wg_start[t + 1] <= blk) ++t;
+  const int ts = seg[t * N], te = seg[(t + 1) * N];
+  const int gt = wg_start[t + 1] - wg_start[t], j = blk - wg_start[t];
   const int64_t n_t = te - ts;
   const int lo = ts + (int)(n_t * j / gt), hi = ts + (int)(n_t * (j + 1) / gt);
   const int64_t n_b = hi - lo;
   auto snap = [&](int p) -> int {               // first segment start at or after p
     if (p <= ts || p >= te) return p;
-    const int dp = a.s_dst[p];
-    return dp == a.s_dst[p - 1] ? a.seg[t * N + dp + 1] : p;
+    const int dp = s_dst[p];
+    return dp == s_dst[p - 1] ? seg[t * N + dp + 1] : p;
   };
-  const int first = snap(lo + (int)(n_b * wave / NW));
-  const int end = snap(lo + (int)(n_b * (wave + 1) / NW));
+  return make_int4(snap(lo + (int)(n_b * wave / NW)), snap(lo + (int)(n_b * (wave + 1) / NW)), t, 0);
+}
+
+// ranges for the middle passes (EDGE_WAVES waves) then the recorded passes (edge_waves<1>()), G blocks
+__device__ inline void edge_ranges_fill(const int* seg, const int* wg_start, const int* s_dst, int T, int64_t N, int G,
+                                        int4* __restrict__ ranges) {
+  const int n_mid = G * EDGE_WAVES, n_all = n_mid + G * edge_waves<1>();
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n_all; q += gridDim.x * blockDim.x) {
+    const int NW = q < n_mid ? EDGE_WAVES : edge_waves<1>(), r = q < n_mid ? q : q - n_mid;
+    ranges[q] = edge_wave_range(seg, wg_start, s_dst, T, N, r / NW, r % NW, NW);
+  }
+}
+
+__global__ __launch_bounds__(256) void edge_ranges_kernel(const int* seg, const int* wg_start, const int* s_dst, int T,
+                                                          int64_t N, int G, int4* ranges) {
+  edge_ranges_fill(seg, wg_start, s_dst, T, N, G, ranges);
+}
+
+// 16-byte LDS-DMA load per lane into the wave-contiguous LDS block at `l` (lane i -> l + 16 i bytes).
+// (A non-template function: hipcc drops the host stub of a kernel template that calls the builtin
+// directly.)
+__device__ __forceinline__ void dma16(const float* g, float* l) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
+// ---- buffer-resource memory ops of the edge pass: a per-array SGPR descriptor and 32-bit lane offsets
+// (no 64-bit per-lane pointers to keep live across the tile loop; reads past the array end return 0)
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+constexpr int RSRC_DW3 = 0x00020000;   // raw buffer, gfx950
+// (32-bit size: a 64-bit clamp here makes hipcc treat the descriptor as divergent and wrap every access
+// in a readfirstlane waterfall loop; the host keeps the arrays below 2^31 bytes)
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, RSRC_DW3);
+}
+__device__ __forceinline__ float4 bld4(rsrc_t rs, int voff, int soff = 0) {
+  const u32x4v v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+__device__ __forceinline__ int bld1(rsrc_t rs, int voff) { return (int)__builtin_amdgcn_raw_buffer_load_b32(rs, voff, 0, 0); }
+__device__ __forceinline__ void bst4(rsrc_t rs, int voff, float a, float b, float c, float d) {
+  const u32x4v v = {__float_as_uint(a), __float_as_uint(b), __float_as_uint(c), __float_as_uint(d)};
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, 0, 0);
+}
+
+// LDS-DMA of the r rows of one 16-edge tile (sorted positions base .. base + 15; rows past the array
+// read 0, rows past the wave's range are loaded and ignored) into a 4 KB buffer: instruction i moves
+// rows 4i .. 4i+3, LDS row rho holding global row base + rho with its 16-byte chunks XOR-permuted by
+// 4 (rho & 3) -- the fragment reads (row c, chunk (4 ob + g) ^ 4 (c & 3)) are at most 2-way bank
+// conflicted, and the four instructions share one lane offset (immediate 1 KB steps)
+__device__ __forceinline__ void dma_rows(rsrc_t rs, int base, float* buf, int lane) {
+  const int voff = (base + (lane >> 4)) * 256 + 16 * ((lane & 15) ^ (4 * (lane >> 4)));
+  auto* l = (__attribute__((address_space(3))) void*)buf;
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, l, 16, voff, 0, 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, l, 16, voff, 0, 1024, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, l, 16, voff, 0, 2048, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, l, 16, voff, 0, 3072, 0);
+}
+
+// The same DMA for the tile loop, issued from inline asm: hipcc's wait-count pass cannot tell these
+// LDS writes from the weight image (its LDS alias scopes stop a few address steps deep) and would
+// drain them before every weight read, serialising the prefetch with the tile's compute. Invisible to
+// the compiler, they are waited for by hand (dma_wait below) and the compiler's own counts only
+// over-wait. M0 is saved and restored; `s_nop 0` covers the M0-write -> LDS-DMA hazard, and the
+// lgkmcnt(0) keeps the DMA behind the buffer's outstanding fragment reads.
+typedef uint32_t u32x4v_s __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4v_s rsrc_words(const void* p, int bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  return u32x4v_s{(uint32_t)a, (uint32_t)(a >> 32) & 0xffffu, (uint32_t)bytes, (uint32_t)RSRC_DW3};
+}
+__device__ __forceinline__ void dma_rows_async(u32x4v_s rs, int base, float* buf, int lane) {
+  const int voff = (base + (lane >> 4)) * 256 + 16 * ((lane & 15) ^ (4 * (lane >> 4)));
+  const uint32_t m = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)buf);
+  uint32_t saved;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen offset:1024 lds\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen offset:2048 lds\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen offset:3072 lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(saved)
+      : "v"(voff), "s"(rs), "s"(m)
+      : "memory");
+}
+// Wait until at most N vector-memory operations are outstanding: with exactly N issued after the DMA
+// above (the tile's unconditional stores), its rows have landed.
+template <int N>
+__device__ __forceinline__ void dma_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+constexpr int OOB_VOFF = (int)0x80000000u;   // buffer offset past every descriptor's size: store dropped
+
+template <int AGG, int HEAD, int PREC, int UPD, int STAGE>
+__global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(EdgeStepArgs a) {
+  constexpr int NW = edge_waves<HEAD>();
+  // STAGE bit 2 (STAGE_EPT): EDGE_MLP per_type (TypeAwareEdgeUpdate, layers.py:275-303). The node
+  // terms A'[dst] + B'[src] (already through their own ReLU and out-block, node_ept_kernel) join
+  // after the e-block GEMM instead of inside the first ReLU.
+  constexpr bool EPT = (STAGE & STAGE_EPT) != 0;
+  constexpr bool MID = (STAGE & 3) == STAGE_MID;
+  constexpr int IMG_F = img_common(UPD) + (HEAD == 1 ? IMG_HEAD : 0);
+  __shared__ __attribute__((aligned(16))) float img[IMG_F];
+  __shared__ __attribute__((aligned(16))) float rbuf[NW * 1024];
+  float* vec = img + (3 + UPD) * D * LDW;          // e2_b[64] | attn_w[64] | attn_b
+  float* hw = img + img_common(UPD);               // HEAD 1: L1 [64][LDW], L2 [32][LDW], b1[64], b2[32], w3[32], b3
+  float* hb_l = hw + (D + 32) * LDW;
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int T = a.T;
+  EDGE_STAMP(0);
+  const int4 rg = a.ranges[blockIdx.x * NW + wave];
+  // wave-uniform by construction; readfirstlane tells hipcc (else the tile loop and every buffer access
+  // downstream are compiled as divergent)
+  const int first = __builtin_amdgcn_readfirstlane(rg.x), end = __builtin_amdgcn_readfirstlane(rg.y);
+  const int t = __builtin_amdgcn_readfirstlane(rg.z);
+  float* mybuf = rbuf + wave * 1024;
+  const int E = (int)a.E;
+  const rsrc_t rs_r = make_rsrc(a.r_cur, E * 256), rs_q = make_rsrc(a.Q0, E * 256);
+  const rsrc_t rs_dst = make_rsrc(a.s_dst, E * 4), rs_src = make_rsrc(a.s_src, E * 4);
+  const rsrc_t rs_nt = make_rsrc(a.NT, (int)a.N * a.t_nt_ld * 4);
+  // first two tiles' indices and the first tile's r rows in flight before the weight copy
+  int dst_n = 0, src_n = 0, dst_nn = 0, src_nn = 0;
+  if (first < end) {   // (uniform)
+    dst_n = bld1(rs_dst, 4 * min(first + c, end - 1));
+    src_n = bld1(rs_src, 4 * min(first + c, end - 1));
+    dst_nn = bld1(rs_dst, 4 * min(first + 16 + c, end - 1));
+    src_nn = bld1(rs_src, 4 * min(first + 16 + c, end - 1));
+    dma_rows(rs_r, first, mybuf, lane);
+  }
+  {
+    // the block's type image: IMG_F floats, 1 KB per wave instruction, waves interleaved
+    const float* src = a.img + (int64_t)t * a.img_stride;
+    constexpr int PIECES = IMG_F / 256, TAIL = IMG_F - PIECES * 256;
+    for (int k = wave; k < PIECES; k += NW)
+      dma16(src + 256 * k + 4 * lane, img + 256 * k);
+    if (TAIL && wave == NW - 1 && 4 * lane < TAIL)
+      *reinterpret_cast<float4*>(&img[256 * PIECES + 4 * lane]) = ld4(src + 256 * PIECES + 4 * lane);
+  }
+  __syncthreads();
+  EDGE_STAMP(1);
   EDGE_STAMP(2);
   if (first >= end) { EDGE_STAMP(15); return; }
-  const float* ntP = a.NT + 128 + 64 * t;
+  const float attn_b = vec[2 * D];
+  const int nt_row = a.t_nt_ld * 4;                  // bytes per node-table row
+  const int nt_p = (128 + 64 * t) * 4;               // byte offset of P_t in a row (SGPR soffset)
+  const rsrc_t rs_next = make_rsrc(a.r_next, E * 256);
+  const rsrc_t rs_agg = make_rsrc(a.agg, (int)a.N * T * 256);
+  const rsrc_t rs_orig = make_rsrc(a.s_orig, E * 4);
+  const u32x4v_s rw_r = rsrc_words(a.r_cur, E * 256);
+  // stores issued after a tile's DMA, all unconditional (masked lanes write past the buffer end): the
+  // r_next rows (middle passes that write them) and the aggregate rows
+  const bool store_next = MID && a.write_next;
 
   // carry of the chunk continuing into the next tile: features in lane c == 0 of each row,
   // running max / normaliser wave-uniform
   float cacc[4][4];
   float cM = 0.f, cl = 0.f;
   bool have_carry = false;
-
-  int dst_n = a.s_dst[min(first + c, end - 1)];
-  int src_n = a.s_src[min(first + c, end - 1)];
-  constexpr bool PIPE = edge_pipe<STAGE>();
-  // PIPE: rows of the next tile in flight during the current tile's compute; indices two tiles ahead
-  float4 nr[4], na[4], nb[4], np4[4], nq[4];
-  int dst_nn = dst_n, src_nn = src_n;
-  auto load_rows = [&](int b0, int d, int s_) {
-    const int qq = min(b0 + c, end - 1);
-#pragma unroll
-    for (int ob = 0; ob < 4; ++ob) {
-      const int f = 16 * ob + 4 * g;
-      nr[ob] = ld4(a.r_cur + (int64_t)qq * D + f);
-      if (PEMP_EDGE_PIPE != 2) {
-        na[ob] = ld4(a.NT + (int64_t)d * a.t_nt_ld + f);
-        nb[ob] = ld4(a.NT + (int64_t)s_ * a.t_nt_ld + 64 + f);
-        np4[ob] = ld4(ntP + (int64_t)d * a.t_nt_ld + f);
-      }
-      if ((STAGE & 3) == STAGE_MID) nq[ob] = ld4(a.Q0 + (int64_t)qq * D + f);
-    }
-  };
-  if (PIPE) {
-    load_rows(first, dst_n, src_n);
-    if (first + 16 < end) {
-      dst_nn = a.s_dst[min(first + 16 + c, end - 1)];
-      src_nn = a.s_src[min(first + 16 + c, end - 1)];
-    }
-  }
   int tile_no = 0;
   for (int base = first; base < end; base += 16, ++tile_no) {
     if (tile_no < 4) EDGE_STAMP(3 + 3 * tile_no);
@@ -1193,89 +1330,79 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
     // (192+ VGPRs of loop-invariant loads would spill)
     int z = 0;
     asm volatile("" : "+s"(z));
-    const float* W1 = wl + z;                     // each matrix: 64 x LDW floats (or its hi + lo bf16)
-    const float* W2 = wl + z + D * LDW;
-    const float* WM = wl + z + 2 * D * LDW;
+    const float* W1 = img + z;                    // each matrix: 64 x LDW floats (or its hi + lo 16-bit parts)
+    const float* W2 = img + z + D * LDW;
+    const float* WM = img + z + 2 * D * LDW;
+    const float* UW = img + z + 3 * D * LDW;
     const float* hwz = hw + z;
     const int p = base + c;
     const bool valid = p < end;
-    const int q = min(p, end - 1);
     const int dst = dst_n, src = src_n;
     const bool more = base + 16 < end;
-    float4 cr[4], ca[4], cb[4], cp[4], cq[4];     // PIPE: this tile's rows (loaded one tile ago)
-    if (PIPE) {
-#pragma unroll
-      for (int ob = 0; ob < 4; ++ob) { cr[ob] = nr[ob]; ca[ob] = na[ob]; cb[ob] = nb[ob]; cp[ob] = np4[ob]; cq[ob] = nq[ob]; }
-      dst_n = dst_nn;
-      src_n = src_nn;
-      if (more) {
-        load_rows(base + 16, dst_n, src_n);
-        if (base + 32 < end) {
-          const int qn = min(base + 32 + c, end - 1);
-          dst_nn = a.s_dst[qn];
-          src_nn = a.s_src[qn];
-        }
-      }
-    } else if (more) {                            // next tile's indices
-      const int qn = min(base + 16 + c, end - 1);
-      dst_n = a.s_dst[qn];
-      src_n = a.s_src[qn];
+    dst_n = dst_nn;
+    src_n = src_nn;
+    // this tile's rows (DMA issued one tile ago) have landed
+    if (tile_no > 0) {
+      if (store_next) dma_wait<8>();
+      else dma_wait<4>();
     }
-    // gathers: r (or edge_attr) and Q0 rows of the edge, node-table rows of target and source
+    // this tile's r rows from the DMA buffer (row c, chunk (4 ob + g) ^ 4 (c & 3)); the lane terms are
+    // re-derived from the opaque zero each tile (kept live across the loop they would be spilled)
     float h[4][4], m[4][4], q0r[4][4];
+    float4 rr[4];
+    {
+      const int cz = c + z, rowb = 64 * cz + 4 * g;
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob) rr[ob] = ld4(mybuf + (rowb ^ (16 * (ob ^ (cz & 3)))));
+    }
+    // gathers of this tile (issued before the next tile's DMA): node-table rows of target and source,
+    // Q0 rows; then the indices two tiles ahead
+    float4 xa[4], xb[4], xp[4], qq[4];
+    const int va = dst * nt_row + 16 * g, vb = src * nt_row + 256 + 16 * g, vq = p * 256 + 16 * g;
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob) {
+      xa[ob] = bld4(rs_nt, va + 64 * ob);
+      xb[ob] = bld4(rs_nt, vb + 64 * ob);
+      xp[ob] = bld4(rs_nt, va + 64 * ob, nt_p);
+      if (MID) qq[ob] = bld4(rs_q, vq + 64 * ob);
+    }
+    const int orig = HEAD == 1 ? bld1(rs_orig, 4 * min(p, end - 1)) : 0;
+    {
+      const int qn = min(base + 32 + c, end - 1);
+      dst_nn = bld1(rs_dst, 4 * qn);
+      src_nn = bld1(rs_src, 4 * qn);
+    }
     float ab[4][4];                               // EPT: A'[dst] + B'[src]
-    if ((STAGE & 3) == STAGE_FIRST) {
-      // embedding first (few live registers), then the node-table gathers
-      float x[4][4];
-      load_edge_attr(a.ea, a.A, a.s_orig[q], x);
-      embed_tile<PREC>(sm + a.emb_off + z, a.Lo, x, q0r);    // x = e_init, q0r = Q0
-      if (a.q0_out && valid) {
 #pragma unroll
-        for (int ob = 0; ob < 4; ++ob)
-          st4(a.q0_out + (int64_t)p * D + 16 * ob + 4 * g, q0r[ob][0], q0r[ob][1], q0r[ob][2], q0r[ob][3]);
-      }
-#pragma unroll
-      for (int ob = 0; ob < 4; ++ob)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) h[ob][k] = q0r[ob][k];
-      gemm_p<PREC, 4>(W1, x, h);                  // r = Q0 + W1_e_cur · e_init
-#pragma unroll
-      for (int ob = 0; ob < 4; ++ob) {
-        const int f = 16 * ob + 4 * g;
-        const float4 xa = ld4(a.NT + (int64_t)dst * a.t_nt_ld + f);
-        const float4 xb = ld4(a.NT + (int64_t)src * a.t_nt_ld + 64 + f);
-        const float4 xp = ld4(ntP + (int64_t)dst * a.t_nt_ld + f);
-        h[ob][0] += xa.x + xb.x; h[ob][1] += xa.y + xb.y; h[ob][2] += xa.z + xb.z; h[ob][3] += xa.w + xb.w;
-        m[ob][0] = xp.x; m[ob][1] = xp.y; m[ob][2] = xp.z; m[ob][3] = xp.w;
-      }
-    } else {
-#pragma unroll
-      for (int ob = 0; ob < 4; ++ob) {
-        const int f = 16 * ob + 4 * g;
-        const float4 rr = PIPE ? cr[ob] : ld4(a.r_cur + (int64_t)q * D + f);
-        constexpr bool PG = PIPE && PEMP_EDGE_PIPE != 2;   // node-table rows prefetched too
-        const float4 xa = PG ? ca[ob] : ld4(a.NT + (int64_t)dst * a.t_nt_ld + f);
-        const float4 xb = PG ? cb[ob] : ld4(a.NT + (int64_t)src * a.t_nt_ld + 64 + f);
-        const float4 xp = PG ? cp[ob] : ld4(ntP + (int64_t)dst * a.t_nt_ld + f);
-        if ((STAGE & 3) == STAGE_MID) {
-          const float4 qq = PIPE ? cq[ob] : ld4(a.Q0 + (int64_t)q * D + f);
-          q0r[ob][0] = qq.x; q0r[ob][1] = qq.y; q0r[ob][2] = qq.z; q0r[ob][3] = qq.w;
-        }
-        if (EPT) {
-          h[ob][0] = rr.x; h[ob][1] = rr.y; h[ob][2] = rr.z; h[ob][3] = rr.w;
-          ab[ob][0] = xa.x + xb.x; ab[ob][1] = xa.y + xb.y; ab[ob][2] = xa.z + xb.z; ab[ob][3] = xa.w + xb.w;
-        } else {
-          h[ob][0] = rr.x + xa.x + xb.x; h[ob][1] = rr.y + xa.y + xb.y;
-          h[ob][2] = rr.z + xa.z + xb.z; h[ob][3] = rr.w + xa.w + xb.w;
-        }
-        m[ob][0] = xp.x; m[ob][1] = xp.y; m[ob][2] = xp.z; m[ob][3] = xp.w;
+    for (int ob = 0; ob < 4; ++ob) {
+      if (EPT) {
+        h[ob][0] = rr[ob].x; h[ob][1] = rr[ob].y; h[ob][2] = rr[ob].z; h[ob][3] = rr[ob].w;
+        ab[ob][0] = xa[ob].x + xb[ob].x; ab[ob][1] = xa[ob].y + xb[ob].y;
+        ab[ob][2] = xa[ob].z + xb[ob].z; ab[ob][3] = xa[ob].w + xb[ob].w;
+      } else {
+        h[ob][0] = rr[ob].x + xa[ob].x + xb[ob].x; h[ob][1] = rr[ob].y + xa[ob].y + xb[ob].y;
+        h[ob][2] = rr[ob].z + xa[ob].z + xb[ob].z; h[ob][3] = rr[ob].w + xa[ob].w + xb[ob].w;
       }
     }
-    // edge MLP layer 1: h = ReLU(r + A[dst] + B[src]), r = Q0 + W1_e_cur · e_cur
+    // the r rows of tile k+1 into the buffer this tile's rows were read from, once every gather of
+    // this tile has returned (the compiler's waits on those would otherwise also wait on the DMA)
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob) {
+      asm volatile("" ::"v"(xa[ob].x), "v"(xb[ob].x), "v"(xp[ob].x));
+      if (MID) asm volatile("" ::"v"(qq[ob].x));
+    }
+    if (HEAD == 1) asm volatile("" ::"v"(orig));
+    if (more) dma_rows_async(rw_r, base + 16, mybuf, lane);
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob) {
+      if (MID) { q0r[ob][0] = qq[ob].x; q0r[ob][1] = qq[ob].y; q0r[ob][2] = qq[ob].z; q0r[ob][3] = qq[ob].w; }
+      m[ob][0] = xp[ob].x; m[ob][1] = xp[ob].y; m[ob][2] = xp[ob].z; m[ob][3] = xp[ob].w;
+    }
 #ifdef PEMP_STAMPS
     asm volatile("" ::"v"(h[0][0]), "v"(h[3][3]));
     if (tile_no < 4) EDGE_STAMP(4 + 3 * tile_no);
 #endif
+    // edge MLP layer 1: h = ReLU(r + A[dst] + B[src]), r = Q0 + W1_e_cur · e_cur
     relu_frag<4>(h);
     // layer 2: e' = ReLU(W2 · h + b2)
     float ep[4][4];
@@ -1285,18 +1412,14 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
       ep[ob][0] = b2.x; ep[ob][1] = b2.y; ep[ob][2] = b2.z; ep[ob][3] = b2.w;
       if (EPT) { ep[ob][0] += ab[ob][0]; ep[ob][1] += ab[ob][1]; ep[ob][2] += ab[ob][2]; ep[ob][3] += ab[ob][3]; }
     }
-    gemm_p<PREC, 4>(W2, h, ep);
-    relu_frag<4>(ep);
-    if ((STAGE & 3) != STAGE_LAST && a.write_next) {    // next pass's r = Q0 + W1_e_cur · e'
-      gemm_p<PREC, 4>(W1, ep, q0r);
-      if (valid) {
-#pragma unroll
-        for (int ob = 0; ob < 4; ++ob)
-          st4(a.r_next + (int64_t)p * D + 16 * ob + 4 * g, q0r[ob][0], q0r[ob][1], q0r[ob][2], q0r[ob][3]);
-      }
+    {
+      Frag<PREC> fh;
+      prep<PREC>(h, fh);
+      gemm_f<PREC, 4>(W2, h, fh, ep);
     }
+    relu_frag<4>(ep);
     float av = 0.f;
-    if (AGG == PEMP_AGGR_ATTN) {
+    if (AGG == PEMP_AGGR_ATTN) {                  // attention row pre-scaled by dom_inv in the image
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob) {
         const float4 w = ld4(vec + D + 16 * ob + 4 * g);
@@ -1307,7 +1430,24 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
       av += __shfl_xor(av, 32);
       av += attn_b;
     }
-    if (HEAD == 1) {   // fused edge-classification head on e'
+    if (HEAD == 2) {   // generic edge head (weights in global memory, true domain)
+      float h1[4][4], h2[4][4];
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h1[ob][r] = ep[ob][r] * dom_inv<PREC>();
+      mlp_frag<4>(a.head, h1, h2);
+      if (valid && g == 0) a.edge_logits[a.s_orig[p]] = h1[0][0];
+    }
+    Frag<PREC> fe;                                // e' split once for the r_next, head and message GEMMs
+    prep<PREC>(ep, fe);
+    if (MID && a.write_next) {                    // next pass's r = Q0 + W1_e_cur · e'
+      gemm_f<PREC, 4>(W1, ep, fe, q0r);
+      const int vn = valid ? vq : OOB_VOFF;
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob) bst4(rs_next, vn + 64 * ob, q0r[ob][0], q0r[ob][1], q0r[ob][2], q0r[ob][3]);
+    }
+    if (HEAD == 1) {   // fused edge-classification head on e' (image: b1, b2 x dom, w3 x dom_inv)
       const float* hb = hb_l + z;
       float h1[4][4], h2[2][4];
 #pragma unroll
@@ -1315,15 +1455,18 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
         const float4 bb = ld4(hb + 16 * ob + 4 * g);
         h1[ob][0] = bb.x; h1[ob][1] = bb.y; h1[ob][2] = bb.z; h1[ob][3] = bb.w;
       }
-      gemm_p<PREC, 4>(hwz, ep, h1);
+      gemm_f<PREC, 4>(hwz, ep, fe, h1);
       relu_frag<4>(h1);
 #pragma unroll
       for (int ob = 0; ob < 2; ++ob) {
         const float4 bb = ld4(hb + D + 16 * ob + 4 * g);
         h2[ob][0] = bb.x; h2[ob][1] = bb.y; h2[ob][2] = bb.z; h2[ob][3] = bb.w;
       }
-      gemm_p<PREC, 2>(PREC == 0 ? (const void*)(hwz + D * LDW) : (const void*)(reinterpret_cast<const __bf16*>(hwz) + 2 * D * LDW),
-                      h1, h2);
+      {
+        Frag<PREC> f1;
+        prep<PREC>(h1, f1);
+        gemm_f<PREC, 2>(hwz + D * LDW, h1, f1, h2);
+      }
       relu_frag<2>(h2);
       float lg = 0.f;
 #pragma unroll
@@ -1334,18 +1477,10 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
       }
       lg += __shfl_xor(lg, 16);
       lg += __shfl_xor(lg, 32);
-      if (valid && g == 0) a.edge_logits[a.s_orig[p]] = lg + a.head.layer[2].b[0];
-    } else if (HEAD == 2) {
-      float h1[4][4], h2[4][4];                  // mlp_frag overwrites its input: work on a copy of e'
-#pragma unroll
-      for (int ob = 0; ob < 4; ++ob)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) h1[ob][r] = ep[ob][r];
-      mlp_frag<4>(a.head, h1, h2);
-      if (valid && g == 0) a.edge_logits[a.s_orig[p]] = h1[0][0];
+      if (valid && g == 0) a.edge_logits[orig] = lg + hb[D + 64];
     }
     // message: m = ReLU(P_t[dst] + W_t_e · e')
-    gemm_p<PREC, 4>(WM, ep, m);
+    gemm_f<PREC, 4>(WM, ep, fe, m);
     relu_frag<4>(m);
     if (UPD) {                                    // m <- U_t · m (no bias: added once per node)
       float u[4][4];
@@ -1353,7 +1488,9 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
       for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
         for (int r = 0; r < 4; ++r) u[ob][r] = 0.0f;
-      gemm_p<PREC, 4>(uw + z, m, u);
+      Frag<PREC> fm;
+      prep<PREC>(m, fm);
+      gemm_f<PREC, 4>(UW, m, fm, u);
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
@@ -1411,16 +1548,14 @@ __global__ __launch_bounds__(64 * edge_waves<STAGE>()) void edge_step_kernel(Edg
         for (int r = 0; r < 4; ++r) cacc[ob][r] = dppf<DPP_SHL15>(v[ob][r], 0.0f);   // lane 15 -> lane 0
     }
     have_carry = carry_out;
-    if (valid && ck.tail && !(carry_out && c == 15)) {
-      const float inv = (AGG == PEMP_AGGR_ATTN) ? 1.0f / (l + 1e-12f) : (AGG == PEMP_AGGR_MEAN) ? 1.0f / l : 1.0f;
-      float* o = a.agg + ((int64_t)seg * T + t) * D + 4 * g;
+    {
+      // the aggregate leaves the f16x3 domain here (dom_inv)
+      const float inv = ((AGG == PEMP_AGGR_ATTN) ? 1.0f / (l + 1e-12f) : (AGG == PEMP_AGGR_MEAN) ? 1.0f / l : 1.0f) *
+                        dom_inv<PREC>();
+      const bool out = valid && ck.tail && !(carry_out && c == 15);
+      const int vo = out ? (seg * T + t) * 256 + 16 * g : OOB_VOFF;
 #pragma unroll
-      for (int ob = 0; ob < 4; ++ob) {
-        if (AGG == PEMP_AGGR_ATTN || AGG == PEMP_AGGR_MEAN)
-          st4(o + 16 * ob, v[ob][0] * inv, v[ob][1] * inv, v[ob][2] * inv, v[ob][3] * inv);
-        else
-          st4(o + 16 * ob, v[ob][0], v[ob][1], v[ob][2], v[ob][3]);
-      }
+      for (int ob = 0; ob < 4; ++ob) bst4(rs_agg, vo + 64 * ob, v[ob][0] * inv, v[ob][1] * inv, v[ob][2] * inv, v[ob][3] * inv);
     }
 #ifdef PEMP_STAMPS
     asm volatile("" ::"v"(v[0][0]), "v"(v[3][3]));
@@ -1516,6 +1651,7 @@ struct NodeEptArgs {
   const float *l1_w, *l1_b, *l2_w, *l2_b, *o1_w, *o2_w;
   float* NT;
   int ldnt;
+  float out_scale;            // the edge passes' domain (dom<PREC>())
 };
 
 __global__ __launch_bounds__(256) void node_ept_kernel(NodeEptArgs a) {
@@ -1579,7 +1715,7 @@ __global__ __launch_bounds__(256) void node_ept_kernel(NodeEptArgs a) {
     }
     if (n0 + c < N)
       *reinterpret_cast<float4*>(&a.NT[(n0 + c) * a.ldnt + 64 * part + 16 * jb + 4 * g]) =
-          make_float4(acc[0], acc[1], acc[2], acc[3]);
+          make_float4(acc[0] * a.out_scale, acc[1] * a.out_scale, acc[2] * a.out_scale, acc[3] * a.out_scale);
     __syncthreads();
   }
 }
@@ -2055,17 +2191,27 @@ __global__ __launch_bounds__(256) void node_table_kernel(NodeTableArgs a) {
         }
       }
     } else {
-      // f16x3 over K = 128 (two 64-input halves, one range check for both)
+      // f16x3 over K = 128 (two 64-input halves, one range check for both); the table stays in the
+      // 2^11 domain of the edge passes (the bias enters x 2^11, nothing is scaled on the way out)
       const float (&x0)[4][4] = *reinterpret_cast<const float (*)[4][4]>(&x[0][0]);
       const float (&x1)[4][4] = *reinterpret_cast<const float (*)[4][4]>(&x[4][0]);
-      const bool big = f16_big(x0) || f16_big(x1);
-      const float s_in = big ? 1.0f / 32.0f : 2048.0f, s_out = big ? 32.0f : 1.0f / 2048.0f;
-      acc *= s_in;
+      const bool big = f16_big(x0, 1.0f) || f16_big(x1, 1.0f);
+      const float ss = big ? F16_DOWN : 1.0f;
+      acc *= big ? 2048.0f * F16_DOWN : 2048.0f;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         f16x8_t hi[2], lo[2];
-        if (big) split_f16<true>(h ? x1 : x0, hi, lo);
-        else split_f16<false>(h ? x1 : x0, hi, lo);
+        const float (&xh)[4][4] = h ? x1 : x0;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          uint32_t hw[4], lw[4];
+#pragma unroll
+          for (int d = 0; d < 4; ++d)
+            split_pair(xh[2 * kb + (d >> 1)][2 * (d & 1)], xh[2 * kb + (d >> 1)][2 * (d & 1) + 1], ss, hw[d], lw[d]);
+          const u32x4_t hv = {hw[0], hw[1], hw[2], hw[3]}, lv = {lw[0], lw[1], lw[2], lw[3]};
+          hi[kb] = __builtin_bit_cast(f16x8_t, hv);
+          lo[kb] = __builtin_bit_cast(f16x8_t, lv);
+        }
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
           acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(flo[2 * h + kb], hi[kb], acc, 0, 0, 0);
@@ -2073,7 +2219,7 @@ __global__ __launch_bounds__(256) void node_table_kernel(NodeTableArgs a) {
           acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[2 * h + kb], hi[kb], acc, 0, 0, 0);
         }
       }
-      acc *= s_out;
+      if (big) acc *= F16_UP;
     }
     if (nn < N) st4(a.NT + nn * a.NO + 16 * ob + 4 * g, acc[0], acc[1], acc[2], acc[3]);
   }
@@ -2090,56 +2236,59 @@ static bool published_head(const pemp_mlp& m) {
          m.layer[2].out_dim == 1 && !m.layer[2].relu;
 }
 
-// LDS floats of the edge-pass image before the (STAGE_FIRST) embedding image
-static int edge_lds_base(bool pub_head, bool upd) {
-  return LDS_W + LDS_VEC + (pub_head ? LDS_HEAD : 0) + (upd ? D * LDW : 0);
-}
-
 template <int AGG, int PREC, int UPD, int STAGE>
-static void launch_edge_step_s(const EdgeStepArgs& a, bool head, int grid, hipStream_t st) {
-  const dim3 blk(64 * edge_waves<STAGE>());
-  if constexpr (STAGE == STAGE_FIRST) {          // never with a recorded head (host falls back)
-    const size_t lds = (size_t)(a.emb_off + a.Lo.total) * sizeof(float);
-    hipLaunchKernelGGL((edge_step_kernel<AGG, 0, PREC, UPD, STAGE_FIRST>), dim3(grid), blk, lds, st, a);
-    return;
-  }
-  const bool pub = head && published_head(a.head) && (PREC == 0 || a.head_bf);
-  const size_t lds = (size_t)edge_lds_base(pub, UPD) * sizeof(float);
+static void launch_edge_step_s(const EdgeStepArgs& a, bool head, bool pub, int grid, hipStream_t st) {
   if (!head)
-    hipLaunchKernelGGL((edge_step_kernel<AGG, 0, PREC, UPD, STAGE>), dim3(grid), blk, lds, st, a);
+    hipLaunchKernelGGL((edge_step_kernel<AGG, 0, PREC, UPD, STAGE>), dim3(grid), dim3(64 * edge_waves<0>()), 0, st, a);
   else if (pub)
-    hipLaunchKernelGGL((edge_step_kernel<AGG, 1, PREC, UPD, STAGE>), dim3(grid), blk, lds, st, a);
+    hipLaunchKernelGGL((edge_step_kernel<AGG, 1, PREC, UPD, STAGE>), dim3(grid), dim3(64 * edge_waves<1>()), 0, st, a);
   else
-    hipLaunchKernelGGL((edge_step_kernel<AGG, 2, PREC, UPD, STAGE>), dim3(grid), blk, lds, st, a);
+    hipLaunchKernelGGL((edge_step_kernel<AGG, 2, PREC, UPD, STAGE>), dim3(grid), dim3(64 * edge_waves<2>()), 0, st, a);
 }
 
 template <int AGG, int PREC, int UPD>
-static void launch_edge_step_p(const EdgeStepArgs& a, bool head, int grid, int stage, hipStream_t st) {
-#if PEMP_FUSED_FIRST
-  if (stage == STAGE_FIRST) launch_edge_step_s<AGG, PREC, UPD, STAGE_FIRST>(a, head, grid, st);
-  else
-#endif
+static void launch_edge_step_p(const EdgeStepArgs& a, bool head, bool pub, int grid, int stage, hipStream_t st) {
   if constexpr (AGG == PEMP_AGGR_ATTN) {          // EDGE_MLP per_type: the published configs use attention
-    if (stage == (STAGE_MID | STAGE_EPT)) { launch_edge_step_s<AGG, PREC, UPD, STAGE_MID | STAGE_EPT>(a, head, grid, st); return; }
-    if (stage == (STAGE_LAST | STAGE_EPT)) { launch_edge_step_s<AGG, PREC, UPD, STAGE_LAST | STAGE_EPT>(a, head, grid, st); return; }
+    if (stage == (STAGE_MID | STAGE_EPT)) { launch_edge_step_s<AGG, PREC, UPD, STAGE_MID | STAGE_EPT>(a, head, pub, grid, st); return; }
+    if (stage == (STAGE_LAST | STAGE_EPT)) { launch_edge_step_s<AGG, PREC, UPD, STAGE_LAST | STAGE_EPT>(a, head, pub, grid, st); return; }
   }
-  if (stage == STAGE_MID) launch_edge_step_s<AGG, PREC, UPD, STAGE_MID>(a, head, grid, st);
-  else launch_edge_step_s<AGG, PREC, UPD, STAGE_LAST>(a, head, grid, st);
+  if (stage == STAGE_MID) launch_edge_step_s<AGG, PREC, UPD, STAGE_MID>(a, head, pub, grid, st);
+  else launch_edge_step_s<AGG, PREC, UPD, STAGE_LAST>(a, head, pub, grid, st);
+}
+
+static EdgeImgArgs edge_image_args(const pemp_mpn_desc& d, const pemp_mpn_weights& w, bool upd, bool head, float* img) {
+  EdgeImgArgs a{};
+  a.T = d.num_types; a.prec = d.precision; a.upd = upd ? 1 : 0; a.head = head ? 1 : 0; a.aggr = d.aggr;
+  a.e1_w = w.e1_w; a.e2_w = w.e2_w; a.e2_b = w.e2_b; a.msg_w = w.msg_w; a.attn_w = w.attn_w; a.attn_bv = w.attn_bv;
+  a.upd_w = w.upd_w; a.attn_b = w.attn_b;
+  a.e1_bf = w.e1_bf; a.e2_bf = w.e2_bf; a.msg_bf = w.msg_bf; a.upd_bf = w.upd_bf; a.head_bf = w.head_bf;
+  a.head_mlp = w.edge_head;
+  a.img = img;
+  return a;
+}
+
+// whether the edge passes pre-apply the update block (UPD) and carry the published head (HEAD 1)
+static bool edge_upd_fused(const pemp_mpn_desc& d, const pemp_mpn_weights& w) {
+  return (d.aggr == PEMP_AGGR_ATTN || d.aggr == PEMP_AGGR_MEAN) && w.upd_w && (d.precision == PEMP_PREC_FP32 || w.upd_bf);
+}
+static bool edge_pub_head(const pemp_mpn_desc& d, const pemp_mpn_weights& w) {
+  return published_head(w.edge_head) && (d.precision == PEMP_PREC_FP32 || w.head_bf);
 }
 
 // UPD is instantiated for the linear aggregations only (U · max(m) != max(U · m))
 template <int AGG>
-static void launch_edge_step(const EdgeStepArgs& a, bool head, int grid, int prec, bool upd, int stage, hipStream_t st) {
+static void launch_edge_step(const EdgeStepArgs& a, bool head, bool pub, int grid, int prec, bool upd, int stage,
+                             hipStream_t st) {
   constexpr int U = AGG == PEMP_AGGR_ATTN || AGG == PEMP_AGGR_MEAN ? 1 : 0;
   if (prec == PEMP_PREC_F16X3) {
-    if (U && upd) launch_edge_step_p<AGG, 2, U>(a, head, grid, stage, st);
-    else launch_edge_step_p<AGG, 2, 0>(a, head, grid, stage, st);
+    if (U && upd) launch_edge_step_p<AGG, 2, U>(a, head, pub, grid, stage, st);
+    else launch_edge_step_p<AGG, 2, 0>(a, head, pub, grid, stage, st);
   } else if (prec == PEMP_PREC_BF16X3) {
-    if (U && upd) launch_edge_step_p<AGG, 1, U>(a, head, grid, stage, st);
-    else launch_edge_step_p<AGG, 1, 0>(a, head, grid, stage, st);
+    if (U && upd) launch_edge_step_p<AGG, 1, U>(a, head, pub, grid, stage, st);
+    else launch_edge_step_p<AGG, 1, 0>(a, head, pub, grid, stage, st);
   } else {
-    if (U && upd) launch_edge_step_p<AGG, 0, U>(a, head, grid, stage, st);
-    else launch_edge_step_p<AGG, 0, 0>(a, head, grid, stage, st);
+    if (U && upd) launch_edge_step_p<AGG, 0, U>(a, head, pub, grid, stage, st);
+    else launch_edge_step_p<AGG, 0, 0>(a, head, pub, grid, stage, st);
   }
 }
 
@@ -2363,7 +2512,8 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   const int T = desc->num_types, J = desc->num_joints;
   PEMP_CHECK_ARG(desc->hidden == 64, "pemp_mpn_forward: hidden width must be 64 (got %d)", desc->hidden);
   PEMP_CHECK_ARG(T >= 1 && T <= MAXT, "pemp_mpn_forward: num_types must be in [1, %d]", MAXT);
-  PEMP_CHECK_ARG(N >= 0 && E >= 0 && N < (1ll << 30) && E < (1ll << 31) - 64 && (int64_t)T * N < (1ll << 30),
+  // (the edge passes address r, Q0 and the aggregates with 32-bit byte offsets: E, T N < 2^23)
+  PEMP_CHECK_ARG(N >= 0 && E >= 0 && N < (1ll << 23) && E < (1ll << 23) && (int64_t)T * N < (1ll << 23),
                  "pemp_mpn_forward: N=%lld E=%lld out of range", (long long)N, (long long)E);
   PEMP_CHECK_ARG(desc->steps >= 0 && desc->aux_loss_steps >= 0, "pemp_mpn_forward: bad steps");
   PEMP_CHECK_ARG(desc->aggr >= PEMP_AGGR_ATTN && desc->aggr <= PEMP_AGGR_MAX, "pemp_mpn_forward: bad aggr");
@@ -2405,8 +2555,9 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   PEMP_CHECK_ARG(desc->precision == PEMP_PREC_FP32 || desc->precision == PEMP_PREC_BF16X3 ||
                      desc->precision == PEMP_PREC_F16X3,
                  "pemp_mpn_forward: unknown precision %d", desc->precision);
-  PEMP_CHECK_ARG(desc->precision == PEMP_PREC_FP32 || (w->e1_bf && w->e2_bf && w->msg_bf),
-                 "pemp_mpn_forward: split precisions need the e1_bf / e2_bf / msg_bf weight packs");
+  PEMP_CHECK_ARG(desc->precision == PEMP_PREC_FP32 ||
+                     (w->e1_bf && w->e2_bf && w->msg_bf && w->pre_bf && (w->emb_bf || !mlp_ok(w->edge_emb, 64, 64))),
+                 "pemp_mpn_forward: split precisions need the e1_bf / e2_bf / msg_bf / pre_bf / emb_bf weight packs");
   PEMP_CHECK_ARG(N == 0 || (x && node_logits && class_logits && node_types), "pemp_mpn_forward: null node tensors");
   PEMP_CHECK_ARG(E == 0 || (edge_attr && edge_index && edge_logits), "pemp_mpn_forward: null edge tensors");
   size_t need = 0;
@@ -2442,17 +2593,21 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   // U_t pre-applied in the edge pass (linear aggregations with an update MLP): the node update is a sum
   // (ATTN / MEAN only: for the unnormalised SUM the reordered fp32 rounding of sum_e U m_e vs
   // U sum_e m_e grows with the in-degree past the logit tolerance)
-  const bool upd_fused = (desc->aggr == PEMP_AGGR_ATTN || desc->aggr == PEMP_AGGR_MEAN) && w->upd_w &&
-                         (desc->precision == PEMP_PREC_FP32 || w->upd_bf);
+  const bool upd_fused = edge_upd_fused(*desc, *w);
   const bool emb_lds = mlp_ok(w->edge_emb, 64, 64);
   const int emb_prec = desc->precision != PEMP_PREC_FP32 && w->emb_bf ? desc->precision : PEMP_PREC_FP32;
   const EmbedLayout emb_lo = embed_layout(w->edge_emb, emb_prec);
-  // PEMP_FUSED_FIRST (build flag, default off): the fused first pass runs 8 waves per CU (register
-  // budget of the embedding) and measured slower than embedding + a 16-wave pass (95 vs ~82 us at C3)
   const bool ept = w->ept_l1_w != nullptr;
-  const bool first_fused = PEMP_FUSED_FIRST && !ept && E > 0 && steps >= 1 && steps > aux + 1 && emb_lds &&
-                           emb_prec == desc->precision &&
-                           (size_t)(edge_lds_base(false, upd_fused) + emb_lo.total) * sizeof(float) <= 160 * 1024;
+  const int edge_grid = std::max(num_cus(), T);   // >= wg_start[T] (see mpn_scan_kernel)
+  const bool pub_head = edge_pub_head(*desc, *w);
+  // the edge-pass weight image: the caller's (pemp_mpn_edge_image, built once per weight set) or built here
+  const float* eimg = w->edge_img;
+  if (!eimg && E > 0 && steps >= 1) {
+    EdgeImgArgs ia = edge_image_args(*desc, *w, upd_fused, pub_head, ws.eimg);
+    hipLaunchKernelGGL(edge_image_kernel, dim3(16, (unsigned)T), dim3(256), 0, st, ia);
+    PEMP_LAUNCH_CHECK();
+    eimg = ws.eimg;
+  }
   // launched after the node embedding + first node table (which need no edge order), so that the
   // host issues the short prepare kernels while the GPU runs those node kernels
   auto edge_prelude = [&]() -> int {
@@ -2471,7 +2626,12 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
       if (rc0) return rc0;
     }
   }
-  if (E > 0 && steps >= 1 && !first_fused) {
+  if (E > 0 && steps >= 1) {   // per-wave edge ranges of the passes (static across iterations)
+    hipLaunchKernelGGL(edge_ranges_kernel, dim3((unsigned)std::min(64, (edge_grid * (EDGE_WAVES + 12) + 255) / 256)),
+                       dim3(256), 0, st, ws.seg, ws.wg_start, ws.s_dst, T, N, edge_grid, ws.ranges);
+    PEMP_LAUNCH_CHECK();
+  }
+  if (E > 0 && steps >= 1) {
     ProfScope prof("edge_embed", st);
     if (emb_lds) {
       const int grid = (int)std::min<int64_t>(num_cus(), (E + 16 * EDGE_WAVES - 1) / (16 * EDGE_WAVES));
@@ -2490,7 +2650,8 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
                            ws.EA, ws.Q0);
     } else {
       hipLaunchKernelGGL(edge_embed_wide_kernel, dim3((unsigned)((E + 63) / 64)), dim3(256), 0, st, w->edge_emb,
-                         edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, ws.EA, ws.Q0);
+                         edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, ws.EA, ws.Q0,
+                         desc->precision == PEMP_PREC_F16X3 ? dom<2>() : 1.0f);
     }
     PEMP_LAUNCH_CHECK();
   }
@@ -2499,7 +2660,6 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
 
   // ---- iterations ----
   const int NO = 128 + 64 * T;
-  const int edge_grid = std::max(num_cus(), T);   // >= wg_start[T] (see mpn_scan_kernel)
   const bool fused_heads = mlp_ok(w->node_head, 64, 64) && mlp_ok(w->class_head, 64, 64);
   const unsigned node_grid = (unsigned)((N + 15) / 16);
   const int table_prec = desc->precision != PEMP_PREC_FP32 && w->pre_bf ? desc->precision : PEMP_PREC_FP32;
@@ -2562,7 +2722,8 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
       PEMP_LAUNCH_CHECK();
       if (ept) {   // columns 0..127 of the table: the per-type node terms (zero rows in pre_w)
         NodeEptArgs xa{ws.X, node_types, tstride, T, N, w->ept_l1_w, w->ept_l1_b, w->ept_l2_w, w->ept_l2_b,
-                       w->ept_o1_w, w->ept_o2_w, ws.NT, NO};
+                       w->ept_o1_w, w->ept_o2_w, ws.NT, NO,
+                       desc->precision == PEMP_PREC_F16X3 ? dom<2>() : 1.0f};
         hipLaunchKernelGGL(node_ept_kernel, dim3(node_grid), dim3(256), 0, st, xa);
         PEMP_LAUNCH_CHECK();
       }
@@ -2586,19 +2747,13 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
     if (E > 0) {
       EdgeStepArgs ea{};
       ea.N = N; ea.E = E; ea.T = T; ea.t_nt_ld = NO;
-      ea.seg = ws.seg; ea.wg_start = ws.wg_start; ea.s_src = ws.s_src; ea.s_dst = ws.s_dst; ea.s_orig = ws.s_orig;
-      const int stage = (it == 0 && first_fused ? STAGE_FIRST : last ? STAGE_LAST : STAGE_MID) | (ept ? STAGE_EPT : 0);
+      const bool pub = record && pub_head;         // the published head's weights ride in the LDS image
+      ea.ranges = ws.ranges + (pub ? (int64_t)edge_grid * EDGE_WAVES : 0);
+      ea.s_src = ws.s_src; ea.s_dst = ws.s_dst; ea.s_orig = ws.s_orig;
+      const int stage = (last ? STAGE_LAST : STAGE_MID) | (ept ? STAGE_EPT : 0);
       ea.NT = ws.NT; ea.Q0 = ws.Q0; ea.r_cur = e_cur; ea.r_next = e_nxt;
-      if (stage == STAGE_FIRST) {
-        ea.q0_out = steps > 1 ? ws.Q0 : nullptr;
-        ea.ea = edge_attr; ea.A = desc->edge_attr_dim; ea.Lo = emb_lo; ea.emb = w->edge_emb; ea.emb_bf = w->emb_bf;
-        ea.q0_w = w->q0_w; ea.q0_b = w->q0_b;
-        ea.emb_off = edge_lds_base(false, upd_fused);
-      }
-      ea.e1_w = w->e1_w; ea.e2_w = w->e2_w; ea.e2_b = w->e2_b; ea.msg_w = w->msg_w; ea.attn_w = w->attn_w;
-      ea.attn_b = w->attn_b; ea.attn_bv = w->attn_bv; ea.agg = ws.agg; ea.head = w->edge_head;
-      ea.e1_bf = w->e1_bf; ea.e2_bf = w->e2_bf; ea.msg_bf = w->msg_bf; ea.head_bf = w->head_bf;
-      ea.upd_w = w->upd_w; ea.upd_bf = w->upd_bf;
+      ea.img = eimg; ea.img_stride = img_stride(upd_fused, pub_head);
+      ea.agg = ws.agg; ea.head = w->edge_head;
       ea.edge_logits = record ? edge_logits + (int64_t)rec * E : nullptr;
       ea.write_next = !last;
 #ifdef PEMP_STAMPS
@@ -2610,10 +2765,10 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
       // may repeat it between one event pair ("edge_step@R")
       for (int rep = prof_repeat(label); rep > 0; --rep) {
         switch (desc->aggr) {
-          case PEMP_AGGR_ATTN: launch_edge_step<PEMP_AGGR_ATTN>(ea, record, edge_grid, desc->precision, upd_fused, stage, st); break;
-          case PEMP_AGGR_SUM: launch_edge_step<PEMP_AGGR_SUM>(ea, record, edge_grid, desc->precision, upd_fused, stage, st); break;
-          case PEMP_AGGR_MEAN: launch_edge_step<PEMP_AGGR_MEAN>(ea, record, edge_grid, desc->precision, upd_fused, stage, st); break;
-          default: launch_edge_step<PEMP_AGGR_MAX>(ea, record, edge_grid, desc->precision, false, stage, st); break;
+          case PEMP_AGGR_ATTN: launch_edge_step<PEMP_AGGR_ATTN>(ea, record, pub, edge_grid, desc->precision, upd_fused, stage, st); break;
+          case PEMP_AGGR_SUM: launch_edge_step<PEMP_AGGR_SUM>(ea, record, pub, edge_grid, desc->precision, upd_fused, stage, st); break;
+          case PEMP_AGGR_MEAN: launch_edge_step<PEMP_AGGR_MEAN>(ea, record, pub, edge_grid, desc->precision, upd_fused, stage, st); break;
+          default: launch_edge_step<PEMP_AGGR_MAX>(ea, record, pub, edge_grid, desc->precision, false, stage, st); break;
         }
         PEMP_LAUNCH_CHECK();
       }
@@ -2674,6 +2829,27 @@ extern "C" int pemp_mpn_prepare(const pemp_mpn_desc* desc, const int64_t* edge_i
   if (N == 0) return PEMP_OK;
   return launch_prepare(desc, edge_index, node_types, N, E, mpn_carve(workspace, desc->num_types, N, E, nullptr),
                         as_stream(stream));
+}
+
+extern "C" size_t pemp_mpn_edge_image_floats(const pemp_mpn_desc* desc, const pemp_mpn_weights* w) {
+  if (!desc || !w || desc->num_types < 1 || desc->num_types > MAXT) return 0;
+  return (size_t)desc->num_types * img_stride(edge_upd_fused(*desc, *w), edge_pub_head(*desc, *w));
+}
+
+extern "C" int pemp_mpn_edge_image(const pemp_mpn_desc* desc, const pemp_mpn_weights* w, float* image, size_t floats,
+                                   void* stream) {
+  PEMP_CHECK_ARG(desc && w && image, "pemp_mpn_edge_image: null pointer");
+  PEMP_CHECK_ARG(desc->num_types >= 1 && desc->num_types <= MAXT, "pemp_mpn_edge_image: bad num_types");
+  PEMP_CHECK_ARG(desc->precision == PEMP_PREC_FP32 || (w->e1_bf && w->e2_bf && w->msg_bf),
+                 "pemp_mpn_edge_image: split precisions need the *_bf packs");
+  PEMP_CHECK_ARG(w->e1_w && w->e2_w && w->e2_b && w->msg_w, "pemp_mpn_edge_image: null layer weights");
+  PEMP_CHECK_ARG(desc->aggr != PEMP_AGGR_ATTN || w->attn_w, "pemp_mpn_edge_image: attention needs attn_w");
+  const size_t need = pemp_mpn_edge_image_floats(desc, w);
+  PEMP_CHECK_ARG(floats >= need, "pemp_mpn_edge_image: image needs %zu floats", need);
+  EdgeImgArgs ia = edge_image_args(*desc, *w, edge_upd_fused(*desc, *w), edge_pub_head(*desc, *w), image);
+  hipLaunchKernelGGL(edge_image_kernel, dim3(16, (unsigned)desc->num_types), dim3(256), 0, as_stream(stream), ia);
+  PEMP_LAUNCH_CHECK();
+  return PEMP_OK;
 }
 
 extern "C" size_t pemp_mpn_node_image_floats(const pemp_mpn_weights* w) {

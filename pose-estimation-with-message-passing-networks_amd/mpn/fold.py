@@ -344,4 +344,13 @@ def fold_weights(model, device, precision="f16x3") -> Folded:
         _lib.check(L.pemp_mpn_node_image(f.struct_ref, img.data_ptr(), n, _lib.stream(device)))
         f.tensors.append(img)
         s.node_img = img.data_ptr()
+    # the edge passes' weight image (per type, in the kernels' LDS layout), once per weight set and precision
+    from .model import PRECISIONS
+    desc = _lib.PempMpnDesc(T, model.num_joints, 1, 0, model.aggr_code, 64, 1, 1, PRECISIONS[precision], 1, 0)
+    n = L.pemp_mpn_edge_image_floats(ctypes.byref(desc), f.struct_ref)
+    if n:
+        img = torch.empty(n, dtype=torch.float32, device=device)
+        _lib.check(L.pemp_mpn_edge_image(ctypes.byref(desc), f.struct_ref, img.data_ptr(), n, _lib.stream(device)))
+        f.tensors.append(img)
+        s.edge_img = img.data_ptr()
     return f
