@@ -253,13 +253,13 @@ def pose_grouping(wl, out, pe, pn, pc, cpu_ref):
         pn_p = torch.sigmoid(2.0 + torch.randn(N, generator=gen, device=bi.device))
         pc_p = pc[-1].softmax(dim=1)
     args = (det, pn_p, ei, pe_p, 0.1, pc_p, "GAEC", wl["J"])
-    ppose.group_persons(*args, batch_index=bi, score_map_scores=sc)
+    ppose.group_persons(*args, batch_index=bi, score_map_scores=sc, num_images=wl["B"])
     reps = 5
     torch.cuda.synchronize()
     _lib.prof_enable("pose_edge_weights")
     t0 = time.perf_counter()
     for _ in range(reps):
-        res = ppose.group_persons(*args, batch_index=bi, score_map_scores=sc)
+        res = ppose.group_persons(*args, batch_index=bi, score_map_scores=sc, num_images=wl["B"])
     gpu_ms = (time.perf_counter() - t0) / reps * 1e3
     global _LAST_GROUPING
     _LAST_GROUPING = res
@@ -267,7 +267,7 @@ def pose_grouping(wl, out, pe, pn, pc, cpu_ref):
     _lib.prof_enable(None)
     tm = {}
     for _ in range(reps):
-        ppose.group_persons(*args, batch_index=bi, score_map_scores=sc, _timings=tm)
+        ppose.group_persons(*args, batch_index=bi, score_map_scores=sc, num_images=wl["B"], _timings=tm)
     n, ms = st.get("pose_edge_weights", (1, float("nan")))
     rec = {"ms_per_batch": round(gpu_ms, 3), "edge_pass_us": round(ms / n * 1e3, 2),
            "stage_ms": {k: round(v / reps * 1e3, 3) for k, v in tm.items()},

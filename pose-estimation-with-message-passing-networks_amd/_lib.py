@@ -4,6 +4,7 @@ The product path has no CPU fallback: ``lib()`` raises if the library is missing
 another ABI, or no gfx950 device is present.
 """
 import ctypes
+import threading
 import os
 
 LIB_PATH = os.environ.get("PEMP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc",
@@ -151,17 +152,26 @@ def stream(device=None):
 
 
 class Workspace:
-    """Grow-only device scratch owned by the caller side (one per use site)."""
+    """Grow-only device scratch owned by the caller side (one per use site), one buffer per (device,
+    stream): calls queued on different streams never share scratch, calls on one stream are ordered by
+    it (a buffer replaced on a stream goes back to torch's stream-aware allocator). Thread-safe."""
 
     def __init__(self):
-        self.buf = None
+        self._bufs = {}
+        self._mu = threading.Lock()
 
     def get(self, nbytes: int, device):
         import torch
         nbytes = max(int(nbytes), 256)
-        if self.buf is None or self.buf.numel() < nbytes or self.buf.device != device:
-            self.buf = torch.empty(nbytes + (nbytes >> 3), dtype=torch.uint8, device=device)
-        return self.buf
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        key = (idx, stream(idx))
+        with self._mu:
+            buf = self._bufs.get(key)
+            if buf is None or buf.numel() < nbytes:
+                with torch.cuda.device(idx):
+                    buf = torch.empty(nbytes + (nbytes >> 3), dtype=torch.uint8, device=device)
+                self._bufs[key] = buf
+            return buf
 
 
 def prof_enable(filt):

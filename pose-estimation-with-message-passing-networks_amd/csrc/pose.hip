@@ -49,7 +49,8 @@ __global__ __launch_bounds__(256) void pose_row_start_kernel(const int64_t* __re
 
 // w[e] = fl32(pred[e] + pred[rev(e)]) for a surviving upper edge (src < dst) in mode 0 (GAEC), pred[e] for
 // every surviving edge in mode 1 (threshold), NaN otherwise. flags[B] bit 0: edge_index is not strictly
-// (src, dst)-sorted (the per-image bits come from pose_image_flags_kernel).
+// (src, dst)-sorted; bit 2: a node index outside [0, N), never dereferenced (the per-image bits come
+// from pose_image_flags_kernel).
 __global__ __launch_bounds__(256) void pose_edge_weights_kernel(const int64_t* __restrict__ ei, int64_t E,
                                                                 const float* __restrict__ pred,
                                                                 const float* __restrict__ score, float th,
@@ -65,7 +66,10 @@ __global__ __launch_bounds__(256) void pose_edge_weights_kernel(const int64_t* _
       const int64_t s1 = ei[e + 1], d1 = ei[E + e + 1];
       if (s1 < s || (s1 == s && d1 <= d)) atomicOr(&flags[B], 1);
     }
-    const bool keep = live && (!use_th || (score[s] > th && score[d] > th));
+    // node indices outside [0, N): flagged (bit 2, raised as an error by the caller), never dereferenced
+    const bool inr = s >= 0 && s < N && d >= 0 && d < N;
+    if (live && !inr) atomicOr(&flags[B], 4);
+    const bool keep = live && inr && (!use_th || (score[s] > th && score[d] > th));
     const float p = live ? pred[e] : 0.f;
     float out = __int_as_float(0x7fc00000);
     if (keep) {
@@ -97,7 +101,7 @@ __global__ __launch_bounds__(256) void pose_image_flags_kernel(const int64_t* __
                                                                const float* __restrict__ pred,
                                                                const float* __restrict__ score, float th, int use_th,
                                                                const int64_t* __restrict__ node_off,
-                                                               const int64_t* __restrict__ row_start,
+                                                               const int64_t* __restrict__ row_start, int64_t N,
                                                                int* __restrict__ flags) {
   const int b = blockIdx.y;
   const int64_t lo = row_start[node_off[b]], hi = row_start[node_off[b + 1]];
@@ -106,6 +110,7 @@ __global__ __launch_bounds__(256) void pose_image_flags_kernel(const int64_t* __
   int bits = 0;
   for (int64_t e = c0 + threadIdx.x; e < c1; e += blockDim.x) {
     const int64_t s = ei[e], d = ei[E + e];
+    if (!(s >= 0 && s < N && d >= 0 && d < N)) continue;   // flagged by pose_edge_weights_kernel
     if (use_th && !(score[s] > th && score[d] > th)) continue;
     bits |= 2 | ((s > d && pred[e] != 0.f) ? 1 : 0);
   }
@@ -292,7 +297,7 @@ extern "C" int pemp_pose_edge_weights(const int64_t* edge_index, int64_t E, cons
                      E, pred, node_scores, th, use_th, node_off, B, method, row_start, N, w, flags);
   PEMP_LAUNCH_CHECK();
   hipLaunchKernelGGL(pose_image_flags_kernel, dim3(16, B), dim3(256), 0, as_stream(stream), edge_index, E, pred,
-                     node_scores, th, use_th, node_off, row_start, flags);
+                     node_scores, th, use_th, node_off, row_start, N, flags);
   PEMP_LAUNCH_CHECK();
   return PEMP_OK;
 }
@@ -302,6 +307,10 @@ extern "C" int pemp_pose_cluster(int B, const int64_t* node_off, const int64_t* 
   PEMP_CHECK_ARG(B >= 1 && E >= 0 && node_off && flags && labels && n_comp && (method == 0 || method == 1),
                  "pemp_pose_cluster: bad args");
   PEMP_CHECK_ARG(E == 0 || (edge_index && w), "pemp_pose_cluster: null edge arrays");
+  if (flags[B] & 4) {
+    ::pemp::set_error("pemp_pose_cluster: edge_index holds a node index outside [0, N)");
+    return PEMP_ERR_INVALID_ARG;
+  }
   if (flags[B] & 1) {
     ::pemp::set_error("pemp_pose_cluster: edge_index is not sorted by (src, dst) without duplicates");
     return PEMP_ERR_INVALID_ARG;
@@ -481,8 +490,10 @@ __global__ __launch_bounds__(64) void refine_mean_tag_kernel(const double* __res
   if (j < J) {
     const double* q = kp + ((size_t)p * J + j) * 3;
     det = q[2] > 0.0;
+    const int x = (int)q[0], y = (int)q[1];  // astype(np.int32): truncation
+    // (the host wrapper rejects detected joints outside the map; here they are only kept from faulting)
+    det = det && x >= 0 && x < W && y >= 0 && y < H;
     if (det) {
-      const int x = (int)q[0], y = (int)q[1];  // astype(np.int32): truncation
       const size_t o = (((size_t)j * H + y) * W + x) * F;
       v0 = tag[o];
       if (F == 2) v1 = tag[o + 1];
@@ -507,9 +518,11 @@ __global__ __launch_bounds__(64) void refine_mean_tag_kernel(const double* __res
   }
 }
 
+// np.argmax order as a 64-bit key: NaN above everything (argmax returns the first NaN), -0.0 equal to
+// +0.0 (canonicalised), then the lower flat index among equal values
 __device__ __forceinline__ unsigned long long refine_key(float v, uint32_t idx) {
-  const uint32_t u = __float_as_uint(v);
-  const uint32_t o = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  const uint32_t u = __float_as_uint(v == 0.f ? 0.f : v);
+  const uint32_t o = v != v ? 0xFFFFFFFFu : (u & 0x80000000u) ? ~u : (u | 0x80000000u);
   return ((unsigned long long)o << 32) | (0xFFFFFFFFu - idx);  // max: larger v, then lower flat index
 }
 
@@ -570,7 +583,7 @@ __global__ __launch_bounds__(256) void refine_argmax_kernel(const float* __restr
           k = isinf(__fmul_rn(d0, d0)) ? INFINITY : rintf(fabsf(d0));
         }
         const float v = __fsub_rn(sv[u], k);
-        const bool better = v > bv[q];
+        const bool better = v > bv[q] || (v != v && bv[q] == bv[q]);   // first NaN wins, as np.argmax
         bv[q] = better ? v : bv[q];
         bi[q] = better ? pxs[u] : bi[q];
       }
@@ -641,6 +654,7 @@ __global__ void adjust_kernel(const float* __restrict__ det, int H, int W, int P
   const int j = t % J;
   double y = q[0], x = q[1];
   const int xx = (int)x, yy = (int)y;
+  if (xx < 0 || xx >= H || yy < 0 || yy >= W) return;   // rejected by the host wrapper; kept from faulting
   const float* tmp = det + (size_t)j * H * W;
   y += tmp[(size_t)xx * W + min(yy + 1, W - 1)] > tmp[(size_t)xx * W + max(yy - 1, 0)] ? 0.25 : -0.25;
   x += tmp[(size_t)min(xx + 1, H - 1) * W + yy] > tmp[(size_t)max(0, xx - 1) * W + yy] ? 0.25 : -0.25;

@@ -8,6 +8,7 @@ Host synchronisation: one count read-back after detection (the reference syncs a
 ``nonzero``), plus one more for knn graphs.
 """
 import ctypes
+import threading
 
 import numpy as np
 import torch
@@ -42,26 +43,36 @@ def get_graph_constructor(config, **kwargs):
 
 
 class NaiveGraphConstructor:
+    # Shared between instances, threads and streams (reentrant calls). Device scratch is per
+    # (device, stream) (_lib.Workspace); each call takes its own mapped host count buffer from a pool and
+    # returns it when the counts are read; the capacity hints are only read / raised under _mu (a stale
+    # hint costs a re-build, never a wrong result).
     _ws_detect = _lib.Workspace()
     _ws_knn = _lib.Workspace()
+    _mu = threading.Lock()
     _cap = 512   # detections per image kept between calls (grows on overflow)
     _graph_hint = {}   # (shape key) -> (node, edge) capacities of the fully-graph capacity build
-    _host_counts_buf = {}   # device index -> (capacity, address, int32 view) of mapped host memory
+    _host_counts_free = {}   # device index -> free (capacity, address, int32 view) mapped host buffers
 
     @classmethod
-    def _host_counts(cls, L, dev, B):
-        """[B] int32 view of mapped host memory that pemp_detect stores the per-image counts into."""
-        ent = cls._host_counts_buf.get(dev.index)
-        if ent is None or ent[0] < B:
-            cap = max(B, 64)
-            addr = L.pemp_host_alloc(4 * cap)
-            if not addr:
-                raise RuntimeError(f"libpemp: {L.pemp_last_error().decode()}")
-            if ent is not None:
-                L.pemp_host_free(ent[1])
-            ent = (cap, addr, np.ctypeslib.as_array((ctypes.c_int32 * cap).from_address(addr)))
-            cls._host_counts_buf[dev.index] = ent
-        return ent[2][:B]
+    def _host_counts_take(cls, L, dev, B):
+        """A (capacity, address, int32 view) mapped host buffer of >= B words that pemp_detect stores the
+        per-image counts into, owned by the calling construct_graph until _host_counts_give."""
+        with cls._mu:
+            free = cls._host_counts_free.setdefault(dev.index, [])
+            for i, ent in enumerate(free):
+                if ent[0] >= B:
+                    return free.pop(i)
+        cap = max(B, 64)
+        addr = L.pemp_host_alloc(4 * cap)
+        if not addr:
+            raise RuntimeError(f"libpemp: {L.pemp_last_error().decode()}")
+        return (cap, addr, np.ctypeslib.as_array((ctypes.c_int32 * cap).from_address(addr)))
+
+    @classmethod
+    def _host_counts_give(cls, dev, ent):
+        with cls._mu:
+            cls._host_counts_free.setdefault(dev.index, []).append(ent)
 
     @staticmethod
     def _wait_counts(counts, dev):
@@ -128,11 +139,24 @@ class NaiveGraphConstructor:
         # ---- detection (pemp_detect): one read-back of the per-image counts ----
         ws_bytes = L.pemp_detect_workspace_size(B, J, H, W, topk)
         ws = self._ws_detect.get(ws_bytes, dev)
-        cap = NaiveGraphConstructor._cap
+        with NaiveGraphConstructor._mu:
+            cap = NaiveGraphConstructor._cap
         det = torch.empty(B, cap, 3, dtype=torch.int64, device=dev)
         dsc = torch.empty(B, cap, dtype=torch.float32, device=dev)
         n_det = torch.empty(B, dtype=torch.int32, device=dev)
-        counts_h = self._host_counts(L, dev, B)
+        counts_ent = self._host_counts_take(L, dev, B)
+        try:
+            out = self._construct(L, st, sm, masks, B, J, H, W, use_thr, topk, thr, dev, ws, cap, det, dsc,
+                                  n_det, counts_ent[2][:B])
+        except BaseException:
+            torch.cuda.current_stream(dev).synchronize()   # queued kernels may still store counts into it
+            self._host_counts_give(dev, counts_ent)
+            raise
+        self._host_counts_give(dev, counts_ent)   # every count was read: the device is done with it
+        return out
+
+    def _construct(self, L, st, sm, masks, B, J, H, W, use_thr, topk, thr, dev, ws, cap, det, dsc, n_det,
+                   counts_h):
         counts_h.fill(-1)
         _lib.check(L.pemp_detect(_lib.ptr(sm), _lib.ptr(masks), B, J, H, W, self.pool_kernel_size, thr, int(use_thr),
                                  topk, 3, _lib.ptr(ws), ws.numel(), _lib.ptr(det), _lib.ptr(dsc), _lib.ptr(n_det),
@@ -167,7 +191,8 @@ class NaiveGraphConstructor:
 
         fully = self.mpn_graph_type == "fully" and B <= 1024
         gkey = (B, J, H, W, C, F, A, dev)
-        hint = NaiveGraphConstructor._graph_hint.get(gkey) if fully else None
+        with NaiveGraphConstructor._mu:
+            hint = NaiveGraphConstructor._graph_hint.get(gkey) if fully else None
         built = None
         if hint is not None:
             # capacity mode: the graph build is queued before the counts are read, so the GPU builds
@@ -192,7 +217,8 @@ class NaiveGraphConstructor:
         cap_used = cap                                      # the detections the capacity build read
         if mx > cap:
             cap = mx
-            NaiveGraphConstructor._cap = max(NaiveGraphConstructor._cap, cap)
+            with NaiveGraphConstructor._mu:
+                NaiveGraphConstructor._cap = max(NaiveGraphConstructor._cap, cap)
             det = torch.empty(B, cap, 3, dtype=torch.int64, device=dev)
             dsc = torch.empty(B, cap, dtype=torch.float32, device=dev)
             _lib.check(L.pemp_detect(_lib.ptr(sm), _lib.ptr(masks), B, J, H, W, self.pool_kernel_size, thr,
@@ -202,9 +228,10 @@ class NaiveGraphConstructor:
         E_fully = sum(c * (c - 1) for c in counts_l if c > 1)
         if fully:   # capacities for the next batch of this shape: 25 % headroom over this one
             n_hint = (N + N // 4 + 16, E_fully + E_fully // 4 + 256)
-            old = NaiveGraphConstructor._graph_hint.get(gkey)
-            NaiveGraphConstructor._graph_hint[gkey] = n_hint if old is None else (max(old[0], n_hint[0]),
-                                                                                 max(old[1], n_hint[1]))
+            with NaiveGraphConstructor._mu:
+                old = NaiveGraphConstructor._graph_hint.get(gkey)
+                NaiveGraphConstructor._graph_hint[gkey] = n_hint if old is None else (
+                    max(old[0], n_hint[0]), max(old[1], n_hint[1]))
         if built is not None and mx <= cap_used and N <= built[0].shape[0] and E_fully <= built[6].shape[0]:
             # the capacity build fit: the outputs are leading (contiguous) slices of its buffers
             x, joint_det, joint_scores, batch_index = built[0][:N], built[1][:N], built[2][:N], built[3][:N]

@@ -35,17 +35,19 @@ def _host_threads():
     return max(1, min(16, os.cpu_count() or 1))
 
 
-def _to_host(tensors):
-    """Stream-ordered copies of device tensors into pinned host tensors, one synchronisation."""
+def _to_host(tensors, dev):
+    """Stream-ordered copies of device tensors into pinned host tensors, one synchronisation (of the
+    current stream of `dev`, where the edge pass and the copies are queued)."""
     out = []
     for t in tensors:
         if t is None:
             out.append(None)
             continue
         h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
-        h.copy_(t, non_blocking=True)
+        with torch.cuda.device(dev):
+            h.copy_(t, non_blocking=True)
         out.append(h)
-    torch.cuda.current_stream().synchronize()
+    torch.cuda.current_stream(dev).synchronize()
     return out
 
 
@@ -83,16 +85,18 @@ def _run(joint_det, joint_scores, edge_index, pred, node_off, th, use_th, class_
         raise ValueError(f"pemp_amd.pose: class_pred {tuple(cls.shape)} != ({N}, {num_joints})")
     ps = score_for_poses.to(torch.float32).contiguous() if score_for_poses is not None else None
     if timings is not None:
-        torch.cuda.current_stream().synchronize()
+        torch.cuda.current_stream(dev).synchronize()
         t1 = time.perf_counter()
         timings["edge_pass"] = timings.get("edge_pass", 0.0) + t1 - t0
         t0 = t1
     h_ei, h_w, h_flags, h_det, h_sc, h_cls, h_ps = _to_host(
-        [ei, w, flags, joint_det.to(torch.int64).contiguous(), sc, cls, ps])
+        [ei, w, flags, joint_det.to(torch.int64).contiguous(), sc, cls, ps], dev)
     if timings is not None:
         t1 = time.perf_counter()
         timings["to_host"] = timings.get("to_host", 0.0) + t1 - t0
         t0 = t1
+    if h_flags[B] & 4:
+        raise ValueError("pemp_amd.pose: edge_index holds a node index outside [0, N)")
     if cc_method == "greedy":
         if h_flags[B] & 1:
             raise ValueError("pemp_amd.pose: edge_index is not sorted by (src, dst) without duplicates")
@@ -146,23 +150,30 @@ def pred_to_person(joint_det, joint_scores, edge_index, pred, class_pred, cc_met
 
 
 def group_persons(joint_det, joint_scores, edge_index, pred, th, class_pred=None, cc_method="GAEC",
-                  num_joints=17, batch_index=None, score_map_scores=None, _timings=None):
+                  num_joints=17, batch_index=None, score_map_scores=None, num_images=None, _timings=None):
     """``pred_to_ann``'s grouping prefix (``Utils.py:1447-1459``) for every image of a batch.
 
     joint_det [ΣN,3] int64, joint_scores [ΣN] (the node probabilities, ``preds_nodes`` in ``valid.py:109``),
     edge_index [2,ΣE] int64 sorted by (src, dst) (``construct_graph``'s output), pred [ΣE] edge
     probabilities, class_pred [ΣN,J] class probabilities or None, batch_index [ΣN] int64 (None: one image),
-    score_map_scores [ΣN] detector scores (None: skip that check). Returns one entry per image: persons
-    float64 [P, J, 3], or None where ``pred_to_ann`` returns None (no detector score > 0.1, no edge
-    surviving the node threshold, no person)."""
+    score_map_scores [ΣN] detector scores (None: skip that check), num_images the batch size (required
+    with batch_index: trailing images without detections have no batch_index entry). Returns one entry
+    per image: persons float64 [P, J, 3], or None where ``pred_to_ann`` returns None (no detector score >
+    0.1, no edge surviving the node threshold, no person)."""
     N = joint_det.shape[0]
     if batch_index is None:
+        if num_images not in (None, 1):
+            raise ValueError("pemp_amd.pose: num_images > 1 needs batch_index")
         node_off = np.array([0, N], dtype=np.int64)
     else:
+        if num_images is None:
+            raise ValueError("pemp_amd.pose: group_persons(batch_index=...) needs num_images (the batch size)")
+        B = int(num_images)
         bi = batch_index.cpu().numpy()
         if len(bi) and np.any(bi[1:] < bi[:-1]):
             raise ValueError("pemp_amd.pose: batch_index must be non-decreasing (construct_graph order)")
-        B = int(bi[-1]) + 1 if len(bi) else 1
+        if len(bi) and (bi[0] < 0 or bi[-1] >= B):
+            raise ValueError(f"pemp_amd.pose: batch_index outside [0, {B})")
         node_off = np.searchsorted(bi, np.arange(B + 1)).astype(np.int64)
     per_image, _, _, flags = _run(joint_det, joint_scores, edge_index, pred, node_off, th, True, class_pred,
                                   cc_method, num_joints, timings=_timings)
@@ -199,6 +210,20 @@ def fill_mean(persons):
     return persons
 
 
+def _check_coords(kp, H, W, name):
+    """Detected joints (score > 0) must index inside the [H, W] map: the reference indexes numpy arrays at
+    int(x), int(y) there (IndexError past the end; a negative index would wrap around, which pemp rejects
+    as well)."""
+    live = kp[:, :, 2] > 0
+    if not live.any():
+        return
+    with np.errstate(invalid="ignore"):
+        x = kp[:, :, 0][live].astype(np.int64)
+        y = kp[:, :, 1][live].astype(np.int64)
+    if (x < 0).any() or (x >= W).any() or (y < 0).any() or (y >= H).any():
+        raise IndexError(f"pemp_amd.pose.{name}: a detected keypoint lies outside the {H}x{W} map")
+
+
 def _maps(t, name, ndim):
     if not (isinstance(t, torch.Tensor) and t.device.type == "cuda"):
         raise ValueError(f"pemp_amd.pose: {name} must be a device tensor (no CPU fallback)")
@@ -226,6 +251,7 @@ def refine(scoremaps, tag, keypoints):
     P = kp.shape[0]
     if P == 0:
         return keypoints
+    _check_coords(kp, H, W, "refine")
     d_kp = torch.from_numpy(kp).to(s.device)
     ws = torch.empty(L.pemp_pose_refine_workspace_size(P, J, H, W, F), dtype=torch.uint8, device=s.device)
     _lib.check(L.pemp_pose_refine(s.data_ptr(), tg.data_ptr(), J, H, W, F, d_kp.data_ptr(), P, ws.data_ptr(),
@@ -243,6 +269,9 @@ def adjust(ans, det):
     J, H, W = d.shape
     if kp.shape[0] == 0:
         return ans
+    if kp.shape[1] != J:
+        raise ValueError(f"pemp_amd.pose: keypoints have {kp.shape[1]} joints, det {J}")
+    _check_coords(kp, H, W, "adjust")
     d_kp = torch.from_numpy(kp).to(d.device)
     _lib.check(L.pemp_pose_adjust(d.data_ptr(), J, H, W, d_kp.data_ptr(), kp.shape[0], _lib.stream(d.device)))
     ans[...] = d_kp.cpu().numpy()

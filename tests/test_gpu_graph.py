@@ -136,3 +136,51 @@ def test_projected_features(graph_type, scales):
             assert torch.equal(out[i].cpu(), ref[i]), i
         assert out[0].shape == ref[0].shape
         assert (out[0].cpu() - ref[0]).abs().max().item() <= 2e-6
+
+
+@pytest.mark.parametrize("graph", ["fully", "knn"])
+def test_reentrant_two_streams(graph):
+    """construct_graph is reentrant. Two constructors with different inputs and shapes are
+    interleaved on two streams (the second call of each queued while the first's kernels may still
+    run), then run again from two host threads at once; every output stays bit-exact with the oracle."""
+    import threading
+    J = 17
+    jobs = []
+    for k, (B, H, W, persons) in enumerate(((2, 128, 128, 4), (3, 96, 160, 6))):
+        hm = torch.from_numpy(syn.make_heatmaps(70 + k, B, J, H, W, persons, margin=4))
+        feats = torch.from_numpy(syn.closed_form((B, 128, H, W), 0.25 + 0.1 * k))
+        tags = torch.from_numpy(syn.closed_form((B, J, H, W, 1), 0.75))
+        gc = pcfg.inference_gc_config(graph, 5, False)
+        ref = restate.construct_graph(hm, feats, tags, None, gc, J)
+        jobs.append((gc, hm.to(DEV), feats.to(DEV), tags.to(DEV), ref))
+    streams = [torch.cuda.Stream(DEV) for _ in jobs]
+
+    def call(j):
+        gc, hm, feats, tags, _ = jobs[j]
+        with torch.cuda.stream(streams[j]):
+            out = run_gc(gc, J, hm, feats, tags, None)
+            streams[j].synchronize()
+        return out
+
+    def check(j, out):
+        for i in (0, 1, 2, 7, 11, 12, 14):
+            assert torch.equal(out[i].cpu(), jobs[j][4][i]), (j, i)
+
+    outs = [call(0), call(1), call(0), call(1)]          # interleaved, capacity builds on the repeats
+    for n, out in enumerate(outs):
+        check(n % 2, out)
+    results, errors = [None] * 4, []
+
+    def worker(slot):
+        try:
+            results[slot] = call(slot % 2)
+        except Exception as e:        # noqa: BLE001 -- reported below
+            errors.append(e)
+    threads = [threading.Thread(target=worker, args=(s,)) for s in range(4)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert not errors, errors
+    for s, out in enumerate(results):
+        check(s % 2, out)

@@ -74,7 +74,7 @@ def test_edge_pass_kernel_bits(method):
     bad = ei[:, ::-1].copy()
     with pytest.raises(ValueError, match="sorted"):
         ppose.group_persons(dev(np.zeros((off[-1], 3), np.int64)), dev(sc), dev(bad), dev(pr), 0.3,
-                            batch_index=dev(np.repeat(np.arange(B), np.diff(off))))
+                            batch_index=dev(np.repeat(np.arange(B), np.diff(off))), num_images=B)
 
 
 def test_group_persons_batched():
@@ -92,7 +92,7 @@ def test_group_persons_batched():
         base += n
     out = ppose.group_persons(dev(np.concatenate(dets)), dev(np.concatenate(scs)), dev(np.concatenate(eis, 1)),
                               dev(np.concatenate(prs)), 0.1, dev(np.concatenate(clss)), "GAEC", 17,
-                              batch_index=dev(np.concatenate(bis)))
+                              batch_index=dev(np.concatenate(bis)), num_images=len(gs))
     assert len(out) == len(gs)
     for b, g in enumerate(gs):
         cls = g["class_probs"] if g["has_class"] else np.eye(17, dtype=np.float32)[g["joint_det"][:, 2]]
@@ -125,7 +125,8 @@ def test_end_to_end_after_mpn(method, graph, persons):
     with torch.no_grad():
         pe, pn, pc, _ = model(x, ea, ei, node_types=det[:, 2])
     pe, pn, pc = pe[-1].sigmoid().squeeze(), pn[-1].sigmoid(), pc[-1].softmax(dim=1)
-    got = ppose.group_persons(det, pn, ei, pe, 0.1, pc, method, J, batch_index=bi, score_map_scores=sc)
+    got = ppose.group_persons(det, pn, ei, pe, 0.1, pc, method, J, batch_index=bi, score_map_scores=sc,
+                              num_images=B)
     h = [t.cpu().numpy() for t in (det, pn, ei, pe, pc, bi, sc)]
     for b in range(B):
         nm = h[5] == b
@@ -254,12 +255,82 @@ def test_group_persons_empty_cases():
     pr = np.concatenate([g["pred"], g["pred"]])
     bi = np.concatenate([np.zeros(n, np.int64), np.full(1, 2, np.int64), np.full(n, 3, np.int64)])
     cls = np.concatenate([g["class_probs"], g["class_probs"][:1], g["class_probs"]])
-    # images: 0 normal, 1 no detections, 2 one node / no edges, 3 all nodes below threshold
+    # images: 0 normal, 1 no detections, 2 one node / no edges, 3 all nodes below threshold, 4 and 5 no
+    # detections (trailing: no batch_index entry, counted only by num_images)
     out = ppose.group_persons(dev(det), dev(sc), dev(ei), dev(pr), float(g["th"]), dev(cls), "GAEC",
-                              int(g["num_joints"]), batch_index=dev(bi))
-    assert len(out) == 4
+                              int(g["num_joints"]), batch_index=dev(bi), num_images=6)
+    assert len(out) == 6
     np.testing.assert_array_equal(out[0], g["persons"])
-    assert out[1] is None and out[2] is None and out[3] is None
+    assert all(o is None for o in out[1:])
+    # the normal image last (index 3), after an empty image 0, a one-node image 1 and an empty image 2
+    out = ppose.group_persons(dev(np.concatenate([g["joint_det"][:1], g["joint_det"]])),
+                              dev(np.concatenate([np.float32([0.9]), g["joint_scores"]])), dev(g["edge_index"] + 1),
+                              dev(g["pred"]), float(g["th"]), dev(np.concatenate([g["class_probs"][:1], g["class_probs"]])),
+                              "GAEC", int(g["num_joints"]), batch_index=dev(np.array([1] + [3] * n, np.int64)),
+                              num_images=4)
+    np.testing.assert_array_equal(out[3], g["persons"])
+    assert len(out) == 4 and out[0] is None and out[1] is None and out[2] is None
+    with pytest.raises(ValueError, match="num_images"):
+        ppose.group_persons(dev(det), dev(sc), dev(ei), dev(pr), float(g["th"]), dev(cls), "GAEC",
+                            int(g["num_joints"]), batch_index=dev(bi))
     empty = ppose.group_persons(dev(np.zeros((0, 3), np.int64)), dev(np.zeros(0, np.float32)),
                                 dev(np.zeros((2, 0), np.int64)), dev(np.zeros(0, np.float32)), 0.1)
     assert empty == [None]
+
+
+def _refine_case(s, tag):
+    kp = np.zeros((1, s.shape[0], 3))
+    kp[0, 0] = (5, 4, 0.9)
+    with np.errstate(invalid="ignore"):
+        ref = opose.refine(s, tag, kp.copy())
+    got = ppose.refine(dev(s), dev(tag), kp.copy())
+    np.testing.assert_array_equal(got, ref)
+    return got
+
+
+def test_refine_signed_zero_tie():
+    """np.argmax treats -0.0 and +0.0 as equal (first index wins): a -0.0 at a low pixel beats a +0.0 held by
+    another thread and block far away -- and there the score is not > 0, so the joint is not filled."""
+    J, H, W = 2, 64, 128
+    m = np.float32(0.25)
+    tag = np.full((J, H, W), m + 1, np.float32)
+    tag[0] = m
+    tag[1, 0, 3] = m                       # k = 0 at the low pixel, k = 1 elsewhere
+    s = np.full((J, H, W), 0.5, np.float32)
+    s[1, 0, 3] = -0.0                      # s - k = -0.0
+    s[1, 60, 100] = 1.0                    # s - k = +0.0
+    got = _refine_case(s, tag)
+    assert got[0, 1, 2] == 0.0             # not filled: the tie went to the -0.0 pixel
+
+
+def test_refine_nan_first():
+    """A NaN in the scoremap is np.argmax's answer (the first NaN): its value is not > 0, the joint stays
+    unfilled even though a clear maximum exists elsewhere."""
+    rng = np.random.default_rng(9)
+    J, H, W = 2, 32, 96
+    tag = np.zeros((J, H, W), np.float32)
+    s = rng.random((J, H, W)).astype(np.float32)
+    s[1, 20, 50] = 5.0
+    s[1, 30, 90] = np.nan
+    s[1, 31, 2] = np.nan
+    got = _refine_case(s, tag)
+    assert got[0, 1, 2] == 0.0
+
+
+def test_bad_indices_raise():
+    """Out-of-range inputs raise instead of faulting: a node index >= N in edge_index, a detected keypoint
+    outside the map in refine / adjust."""
+    g = load(GROUP[0])
+    n = len(g["joint_det"])
+    ei = g["edge_index"].copy()
+    ei[1, -1] = n + 5
+    with pytest.raises(ValueError, match="outside"):
+        ppose.group_persons(dev(g["joint_det"]), dev(g["joint_scores"]), dev(ei), dev(g["pred"]), 0.0)
+    s = dev(np.ones((2, 8, 16), np.float32))
+    for x, y in ((16, 3), (3, 8), (-1, 2)):
+        kp = np.zeros((1, 2, 3))
+        kp[0, 0] = (x, y, 0.9)
+        with pytest.raises(IndexError):
+            ppose.refine(s, s, kp)
+        with pytest.raises(IndexError):
+            ppose.adjust(kp, s)
