@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define PEMP_ABI_VERSION 10
+#define PEMP_ABI_VERSION 11
 
 enum {
   PEMP_OK = 0,
@@ -134,6 +134,15 @@ int pemp_knn_graph_count(const int64_t* joint_det, const int64_t* node_off, cons
 int pemp_knn_graph_emit(const int64_t* node_off, const int64_t* node_off_host, int B,
                         const int64_t* edge_off, int64_t e_total, void* workspace,
                         size_t workspace_bytes, int64_t* edge_index, void* stream);
+/* Both stages in one call, no host round trip between them (replaces ConstructGraph.py:363-368 +
+ * the count read-back): adjacency, per-image counts, their device scan and the emit, back to back.
+ * edge_buf: device int64 [2 * e_cap], e_cap >= sum_b min(n_b (n_b - 1), 2 k n_b) (checked); the graph
+ * is its leading [2, E] block (sources at 0, destinations at E). e_total_host: mapped host int32
+ * (pemp_host_alloc), set to E by the device once the counts are scanned (the emit may still run);
+ * the host spins on it (initialise it to -1). */
+int pemp_knn_graph_build(const int64_t* joint_det, const int64_t* node_off, const int64_t* node_off_host,
+                         int B, int k, void* workspace, size_t workspace_bytes, int64_t e_cap,
+                         int64_t* edge_buf, int32_t* e_total_host, void* stream);
 
 /* Node features from maps projected to the image size on demand (the test front-end's bilinear
  * projection, PoseEstimation.py:426-452, summed over scales and divided, multi_scales_testing.py:182-190

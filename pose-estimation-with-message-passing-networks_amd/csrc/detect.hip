@@ -30,6 +30,12 @@ namespace {
 #ifndef NMS_PREFETCH
 #define NMS_PREFETCH 1
 #endif
+#ifndef NMS_XCD_MAP
+#define NMS_XCD_MAP 1
+#endif
+#ifndef NMS_PER_CU
+#define NMS_PER_CU 4
+#endif
 constexpr int SR = NMS_SR;  // rows per unit (= band height of the threshold bitmask)
 static_assert(SR <= 32, "column masks are at most 32-bit");
 // a lane's threshold bits over the SR rows of its unit column
@@ -216,13 +222,20 @@ __global__ __launch_bounds__(NT1) void nms_strips_kernel(
     float* __restrict__ cand_v, int* __restrict__ cand_i, float* __restrict__ neg_v, int* __restrict__ neg_i,
     int* __restrict__ tile_count, int* __restrict__ tile_nonneg, cmask_t* __restrict__ cbits) {
   const int lane = threadIdx.x & 63;
-  const int total = g.B * g.J * g.units, stride_u = gridDim.x * (NT1 / 64);
+  const int total = g.B * g.J * g.units;
   const int H = g.H, W = g.W, K = g.K;
+  // Grid-stride over windows of G x 4 consecutive units; inside a window the units are dealt by XCD
+  // (blocks b and b + 8 share one): XCD x takes the x-th eighth of the window, a contiguous run of bands
+  // whose halo rows and columns its neighbours fetch at the same time into the same L2, instead of every
+  // neighbour sitting on another XCD and reading its halo from HBM again.
+  const int G = gridDim.x;
+  const int slot = (NMS_XCD_MAP && (G & 7) == 0) ? ((int)(blockIdx.x & 7) * (G >> 3) + (int)(blockIdx.x >> 3)) : (int)blockIdx.x;
+  const int stride_u = G * (NT1 / 64), u_hi = total;
   // the unit index is wave-uniform: keep it (and all address math derived from it) scalar
-  int u = __builtin_amdgcn_readfirstlane(blockIdx.x * (NT1 / 64) + (threadIdx.x >> 6));
+  int u = __builtin_amdgcn_readfirstlane(slot * (NT1 / 64) + (threadIdx.x >> 6));
   float r[SR + 2 * P];
-  if (NMS_PREFETCH && u < total) load_unit<P>(s, g, u, r);
-  for (; u < total; u += stride_u) {
+  if (NMS_PREFETCH && u < u_hi) load_unit<P>(s, g, u, r);
+  for (; u < u_hi; u += stride_u) {
     if (!NMS_PREFETCH) load_unit<P>(s, g, u, r);
     const int plane = u / g.units, rem = u - plane * g.units, band = rem / g.nsx, strip = rem - band * g.nsx;
     const int b = plane / g.J;
@@ -231,7 +244,7 @@ __global__ __launch_bounds__(NT1) void nms_strips_kernel(
     float cur[SR + 2 * P];
 #pragma unroll
     for (int i = 0; i < SR + 2 * P; ++i) cur[i] = r[i];
-    if (NMS_PREFETCH && u + stride_u < total) load_unit<P>(s, g, u + stride_u, r);   // next unit's rows in flight
+    if (NMS_PREFETCH && u + stride_u < u_hi) load_unit<P>(s, g, u + stride_u, r);   // next unit's rows in flight
     float vm[SR], c[SR];
 #pragma unroll
     for (int j = 0; j < SR; ++j) {
@@ -638,7 +651,7 @@ static void launch_nms(const float* s, const float* masks, const DetectGeom& g, 
   const int want = (total + NT1 / 64 - 1) / (NT1 / 64);
   // resident workgroups per CU: 4 (one wave per SIMD each) while the kernel fits 128 VGPRs (SR 16);
   // the 32-row units need ~190 VGPRs: 2
-  constexpr int per_cu = SR > 16 ? 2 : 4;
+  constexpr int per_cu = SR > 16 ? 2 : NMS_PER_CU;
   const int grid = want < per_cu * num_cus() ? want : per_cu * num_cus();
   if (masks)
     hipLaunchKernelGGL((nms_strips_kernel<P, MODE, true>), dim3(grid), dim3(NT1), 0, st, s, masks, g, thr, use_thr,

@@ -156,6 +156,8 @@ struct KnnWs {
   unsigned long long* adj;   // per image: n_b rows x words_b  (A: j among i's nearest)
   unsigned long long* adjt;  // transpose                      (T[j][i] = A[i][j])
   int64_t* mat_off;          // [B+1] word offsets (device copy)
+  int64_t* ecount;           // [B] edges per image (pemp_knn_graph_build)
+  int64_t* edge_off;         // [B+1] exclusive scan of ecount; [B] = the batch's edge total
 };
 
 static size_t knn_words(const int64_t* node_off_host, int B, int64_t* mat_off_host) {
@@ -176,6 +178,8 @@ static KnnWs knn_carve(void* base, const int64_t* node_off_host, int B, size_t* 
   k.adj = c.take<unsigned long long>(w);
   k.adjt = c.take<unsigned long long>(w);
   k.mat_off = c.take<int64_t>(B + 1);
+  k.ecount = c.take<int64_t>(B);
+  k.edge_off = c.take<int64_t>(B + 1);
   if (bytes) *bytes = c.used;
   return k;
 }
@@ -289,7 +293,11 @@ __global__ __launch_bounds__(1024) void knn_emit_kernel(const int64_t* __restric
                                                         const unsigned long long* __restrict__ adj,
                                                         const unsigned long long* __restrict__ adjt,
                                                         const int64_t* __restrict__ edge_off, int64_t e_total,
-                                                        int64_t* __restrict__ ei) {
+                                                        int64_t e_cap, int64_t* __restrict__ ei) {
+  // e_total < 0: the total is edge_off[B], known only on the device (pemp_knn_graph_build); the
+  // destination row starts right after the source row, at ei + e_total (a contiguous [2, E] view)
+  if (e_total < 0) e_total = edge_off[B];
+  if (e_total > e_cap) return;   // reported by the host (the total exceeds the buffer)
   const int b = blockIdx.x;
   const int64_t base = node_off[b];
   const int n = (int)(node_off[b + 1] - base);
@@ -335,6 +343,31 @@ __global__ __launch_bounds__(1024) void knn_emit_kernel(const int64_t* __restric
       carry += s;
     }
     __syncthreads();
+  }
+}
+
+// edge_off = exclusive scan of ecount, edge_off[B] = total; the total also goes straight into the
+// caller's mapped host word (system-scope store), like pemp_detect's counts
+__global__ __launch_bounds__(64) void knn_offsets_kernel(const int64_t* __restrict__ ecount, int B,
+                                                         int64_t* __restrict__ edge_off, int* __restrict__ e_host) {
+  const int lane = threadIdx.x;
+  long long c = 0;
+  for (int c0 = 0; c0 < B; c0 += 64) {
+    const int b = c0 + lane;
+    const long long e = b < B ? ecount[b] : 0;
+    long long x = e;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const long long o = __shfl_up(x, off);
+      if (lane >= off) x += o;
+    }
+    if (b < B) edge_off[b] = c + x - e;
+    c += __shfl(x, 63);
+  }
+  if (lane == 0) {
+    edge_off[B] = c;
+    if (e_host) __hip_atomic_store(e_host, (int)(c < 0x7fffffffll ? c : 0x7fffffffll), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -847,8 +880,60 @@ extern "C" int pemp_knn_graph_emit(const int64_t* node_off, const int64_t* node_
   if (e_total == 0) return PEMP_OK;
   ProfScope prof("knn_emit", as_stream(stream));
   hipLaunchKernelGGL(knn_emit_kernel, dim3(B), dim3(1024), 0, as_stream(stream), node_off, B, w.mat_off, w.adj,
-                     w.adjt, edge_off, e_total, edge_index);
+                     w.adjt, edge_off, e_total, e_total, edge_index);
   PEMP_LAUNCH_CHECK();
+  return PEMP_OK;
+}
+
+// The whole knn graph without a host round trip in the middle: adjacency, per-image counts, their scan
+// and the emit are queued back to back; the edge total reaches the host through mapped memory
+// (e_total_host, written by the scan kernel while the emit runs). edge_buf holds 2 * e_cap int64: the
+// graph is its leading [2, E] block (source row at 0, destination row at E).
+extern "C" int pemp_knn_graph_build(const int64_t* joint_det, const int64_t* node_off, const int64_t* node_off_host,
+                                    int B, int k, void* workspace, size_t workspace_bytes, int64_t e_cap,
+                                    int64_t* edge_buf, int32_t* e_total_host, void* stream) {
+  PEMP_CHECK_ARG(joint_det && node_off && node_off_host && workspace && edge_buf && B > 0 && k >= 1 && e_cap >= 0,
+                 "pemp_knn_graph_build: bad args");
+  size_t need = 0;
+  knn_carve(nullptr, node_off_host, B, &need);
+  if (workspace_bytes < need) {
+    set_error("pemp_knn_graph_build: workspace %zu < %zu", workspace_bytes, need);
+    return PEMP_ERR_WORKSPACE;
+  }
+  int64_t bound = 0;   // every node keeps min(k, n - 1) nearest; the union with the reverse at most doubles it
+  for (int b = 0; b < B; ++b) {
+    const int64_t n = node_off_host[b + 1] - node_off_host[b];
+    PEMP_CHECK_ARG(n >= 0, "pemp_knn_graph_build: decreasing node offsets");
+    bound += std::min<int64_t>(n * (n > 0 ? n - 1 : 0), 2 * (int64_t)k * n);
+  }
+  PEMP_CHECK_ARG(e_cap >= bound, "pemp_knn_graph_build: e_cap %lld < bound %lld", (long long)e_cap, (long long)bound);
+  const KnnWs w = knn_carve(workspace, node_off_host, B, nullptr);
+  const hipStream_t st = as_stream(stream);
+  int* e_dev_host = nullptr;   // device address of the caller's mapped host word
+  if (e_total_host) PEMP_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&e_dev_host), e_total_host, 0));
+  const size_t words = knn_words(node_off_host, B, nullptr);
+  hipLaunchKernelGGL(knn_matoff_kernel, dim3(1), dim3(64), 0, st, node_off, B, w.mat_off);
+  PEMP_LAUNCH_CHECK();
+  if (words) {
+    PEMP_HIP(hipMemsetAsync(w.adj, 0, words * sizeof(unsigned long long), st));
+    PEMP_HIP(hipMemsetAsync(w.adjt, 0, words * sizeof(unsigned long long), st));
+  }
+  const int64_t n_total = node_off_host[B];
+  ProfScope prof("knn_build", st);
+  if (n_total > 0) {
+    hipLaunchKernelGGL(knn_adj_kernel, dim3((unsigned)((n_total + 3) / 4)), dim3(256), 0, st, joint_det, node_off, B,
+                       n_total, k + 1, w.mat_off, w.adj, w.adjt);
+    PEMP_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(knn_count_kernel, dim3(B), dim3(256), 0, st, node_off, B, w.mat_off, w.adj, w.adjt, w.ecount);
+  PEMP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(knn_offsets_kernel, dim3(1), dim3(64), 0, st, w.ecount, B, w.edge_off, e_dev_host);
+  PEMP_LAUNCH_CHECK();
+  if (bound > 0) {
+    hipLaunchKernelGGL(knn_emit_kernel, dim3(B), dim3(1024), 0, st, node_off, B, w.mat_off, w.adj, w.adjt,
+                       w.edge_off, (int64_t)-1, e_cap, edge_buf);
+    PEMP_LAUNCH_CHECK();
+  }
   return PEMP_OK;
 }
 

@@ -302,13 +302,7 @@ class NaiveGraphConstructor:
         if self.mpn_graph_type == "fully":
             per = counts * np.maximum(counts - 1, 0)
         elif self.mpn_graph_type == "knn":
-            nh = np.ascontiguousarray(node_off_h)
-            nh_p = nh.ctypes.data_as(ctypes.c_void_p)
-            ws = self._ws_knn.get(L.pemp_knn_workspace_size(nh_p, B), dev)
-            ecount = torch.empty(B, dtype=torch.int64, device=dev)
-            _lib.check(L.pemp_knn_graph_count(_lib.ptr(joint_det), _lib.ptr(node_off), nh_p, B, 50, _lib.ptr(ws),
-                                              ws.numel(), _lib.ptr(ecount), st))
-            per = ecount.cpu().numpy()
+            return self._knn_edges(L, st, joint_det, node_off, node_off_h, counts, B, dev)
         elif self.mpn_graph_type == "score_based":
             k = _SCORE_BASED_K
             if counts.size and counts.min() < k:   # the reference's joint_scores.topk(k) raises
@@ -327,10 +321,33 @@ class NaiveGraphConstructor:
             ws = self._ws_knn.get(L.pemp_score_graph_workspace_size(nh_p, B, _SCORE_BASED_K), dev)
             _lib.check(L.pemp_score_graph(_lib.ptr(joint_scores), _lib.ptr(node_off), nh_p, B, _SCORE_BASED_K, E,
                                           _lib.ptr(ws), ws.numel(), _lib.ptr(edge_index), st))
-        else:
-            edge_off_h = np.zeros(B + 1, np.int64)
-            edge_off_h[1:] = np.cumsum(per)
-            edge_off = torch.from_numpy(edge_off_h).to(dev)
-            _lib.check(L.pemp_knn_graph_emit(_lib.ptr(node_off), nh_p, B, _lib.ptr(edge_off), E, _lib.ptr(ws),
-                                             ws.numel(), _lib.ptr(edge_index), st))
         return edge_index
+
+    _KNN_K = 50   # ConstructGraph.py:365 (knn_graph(k=50))
+
+    def _knn_edges(self, L, st, joint_det, node_off, node_off_h, counts, B, dev):
+        """knn_mpn_graph (ConstructGraph.py:363-368) in one queued call (pemp_knn_graph_build): the
+        buffer is sized by the closed-form bound, the total comes back through mapped memory while the
+        emit still runs, and the graph is the buffer's leading contiguous [2, E] block."""
+        k = self._KNN_K
+        nh = np.ascontiguousarray(node_off_h)
+        nh_p = nh.ctypes.data_as(ctypes.c_void_p)
+        ws = self._ws_knn.get(L.pemp_knn_workspace_size(nh_p, B), dev)
+        n = counts.astype(np.int64)
+        e_cap = int(np.minimum(n * np.maximum(n - 1, 0), 2 * k * n).sum())
+        buf = torch.empty(2 * max(e_cap, 1), dtype=torch.int64, device=dev)
+        ent = self._host_counts_take(L, dev, 1)
+        try:
+            word = ent[2][:1]
+            word.fill(-1)
+            _lib.check(L.pemp_knn_graph_build(_lib.ptr(joint_det), _lib.ptr(node_off), nh_p, B, k, _lib.ptr(ws),
+                                              ws.numel(), e_cap, _lib.ptr(buf), ent[1], st))
+            E = self._wait_counts(word, dev)[0]
+        except BaseException:
+            torch.cuda.current_stream(dev).synchronize()
+            self._host_counts_give(dev, ent)
+            raise
+        self._host_counts_give(dev, ent)
+        if E > e_cap:
+            raise RuntimeError(f"pemp_knn_graph_build: {E} edges > bound {e_cap}")
+        return buf[:2 * E].view(2, E)

@@ -1,0 +1,19 @@
+#!/bin/bash
+# usage (here, CPU): tools/build_variant.sh <name> <src.hip> [hipcc flags...]
+# -> build_ab/libpemp_<name>.so: csrc/*.o with <src>'s object rebuilt under the extra flags
+# (A/B on the GPU box: PEMP_LIB=build_ab/libpemp_<name>.so, e.g. through tools/ab_env.sh).
+set -e
+name=$1; src=$2; shift 2
+root=$(cd "$(dirname "$0")/.." && pwd)
+csrc=$root/pose-estimation-with-message-passing-networks_amd/csrc
+mkdir -p "$root/build_ab"
+base=$(basename "$src" .hip)
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function -Wno-unused-variable \
+  -I"$root/include" "$@" -c "$csrc/$base.hip" -o "$root/build_ab/v_${name}_$base.o"
+objs=""
+for o in "$csrc"/*.o; do
+  [ "$(basename "$o")" = "$base.o" ] || objs="$objs $o"
+done
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$root/build_ab/libpemp_$name.so" $objs \
+  "$root/build_ab/v_${name}_$base.o"
+echo "build_ab/libpemp_$name.so"
