@@ -246,3 +246,16 @@ def test_pose_product_path_has_no_cpu_fallback():
         ppose.refine(T(r["scoremaps"]), T(r["tag"]), r["filled"].copy())
     with pytest.raises(NotImplementedError):
         ppose._method("MUT")
+
+
+def test_reverse_affine_map_golden():
+    """pemp_amd.pose.reverse_affine_map against the reference's own transformations.py functions
+    (oracle/gen_golden_affine.py; cv2.getAffineTransform stubbed by its 6x6 float64 solve)."""
+    from pemp_amd import pose as ppose
+    g = np.load(os.path.join(GOLDEN, "affine_maps.npz"))
+    for c, spec in enumerate(g["cases"]):
+        w, h, size, kind, ms = str(spec).split(",")
+        got = ppose.reverse_affine_map(g[f"in_{c}"].copy(), (int(w), int(h)), int(size), kind, float(ms))
+        np.testing.assert_array_equal(got, g[f"out_{c}"])
+    with pytest.raises(NotImplementedError):
+        ppose.reverse_affine_map(np.zeros((1, 17, 3)), (640, 480), 512, "short_mine")
