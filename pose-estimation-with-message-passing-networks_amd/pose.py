@@ -297,3 +297,103 @@ def finish_persons(persons, scoremaps, tags, adjustment, with_refine, with_filte
     if adjustment:
         adjust(persons, scoremaps)
     return persons
+
+
+# ----------------------------------------------------------------------------------------------------
+# Back to original image coordinates (pred_to_ann, Utils.py:1479; valid.py:175): reverse_affine_map
+# ----------------------------------------------------------------------------------------------------
+# Host numpy, like the reference: a few hundred points per image. The 2 x 3 affine of three point pairs
+# is cv2.getAffineTransform's (OpenCV is not in this image): the 6 x 6 system of the three
+# correspondences solved in float64 (LU with partial pivoting, as cv::getAffineTransform's DECOMP_LU);
+# equal to OpenCV's up to the last bits of that solve (parity pinned against the reference's own
+# functions with this solve, tests/golden/affine_*.npz; the solve itself unpinned).
+def affine_from_points(src, dst):
+    """[2, 3] float64 M with dst_i = M [src_i; 1] for the three (float32) point pairs."""
+    s = np.asarray(src, dtype=np.float32).astype(np.float64)
+    d = np.asarray(dst, dtype=np.float32).astype(np.float64)
+    a = np.zeros((6, 6))
+    a[0::2, 0:2] = s
+    a[0::2, 2] = 1.0
+    a[1::2, 3:5] = s
+    a[1::2, 5] = 1.0
+    return np.linalg.solve(a, d.reshape(6)).reshape(2, 3)
+
+
+def multi_scale_size(img_h, img_w, input_size, current_scale, min_scale):
+    """transformations.py:216-238: ((w, h) of the resized input, centre, scale / 200) -- the input side
+    rounded up to multiples of 64, the short side set by min_scale."""
+    center = np.array([int(img_w / 2.0 + 0.5), int(img_h / 2.0 + 0.5)])
+    side = int((min_scale * input_size + 63) // 64 * 64)
+    if img_w < img_h:
+        short, long_in, long_ = img_w, img_h, "h"
+    else:
+        short, long_in, long_ = img_h, img_w, "w"
+    s_res = int(side * current_scale / min_scale)
+    l_res = int(int((side / short * long_in + 63) // 64 * 64) * current_scale / min_scale)
+    if long_ == "h":
+        size, scale = (s_res, l_res), np.array([img_w / 200.0, l_res / s_res * img_w / 200.0])
+    else:
+        size, scale = (l_res, s_res), np.array([l_res / s_res * img_h / 200.0, img_h / 200.0])
+    return size, center, scale
+
+
+def crop_affine(center, scale, output_size, inv=False):
+    """transformations.py:170-213 at rotation 0: the map of the box of width 200 * scale[0] centred at
+    `center` onto an output_size (w, h) image, from three float32 point pairs (centre, top-centre and
+    the point a quarter turn from it)."""
+    scale = np.asarray(scale) if isinstance(scale, (np.ndarray, list)) else np.array([scale, scale])
+    half_src = (scale * 200.0)[0] * -0.5
+    ow, oh = output_size
+    src = np.zeros((3, 2), np.float32)
+    dst = np.zeros((3, 2), np.float32)
+    src[0] = center
+    src[1] = center + np.array([0.0 - half_src * 0.0, half_src])   # rotation 0: (0 cos - y sin, 0 sin + y cos)
+    dst[0] = [ow * 0.5, oh * 0.5]
+    dst[1] = np.array([ow * 0.5, oh * 0.5]) + np.array([0, ow * -0.5], np.float32)
+    for p in (src, dst):
+        v = p[0] - p[1]
+        p[2] = p[1] + np.array([-v[1], v[0]], np.float32)
+    return affine_from_points(dst, src) if inv else affine_from_points(src, dst)
+
+
+def box_transform(center, scale, res):
+    """transformations.py:142-167 at rotation 0: the 3 x 3 float64 map of the box (200 * scale) around
+    `center` onto a res = (h, w) grid."""
+    h = 200 * np.asarray(scale)
+    t = np.zeros((3, 3))
+    t[0, 0] = float(res[1]) / h[1]
+    t[1, 1] = float(res[0]) / h[0]
+    t[0, 2] = res[1] * (-float(center[0]) / h[0] + .5)
+    t[1, 2] = res[0] * (-float(center[1]) / h[1] + .5)
+    t[2, 2] = 1
+    return t
+
+
+def apply_affine(points, mat):
+    """transformations.py:131-135: [..., 2] points through a [2, 3] matrix (homogeneous, float64)."""
+    p = np.array(points)
+    flat = p.reshape(-1, 2)
+    return np.dot(np.concatenate((flat, flat[:, 0:1] * 0 + 1), axis=1), mat.T).reshape(p.shape)
+
+
+def reverse_affine_map(keypoints, img_size_orig, input_size, scaling_type, min_scale=1.0):
+    """``reverse_affine_map`` (src/Utils/transformations.py:7-77): keypoints [P, J, >=2] in network output
+    space -> original image coordinates, in place (returned), for scaling_type "short" (heatmaps at half
+    the input size), "short_with_resize" (PROJECT2IMAGE), "long" and "long_with_multiscale" (x4 output
+    stride, 512 input). img_size_orig = (width, height). Raises NotImplementedError otherwise, as the
+    reference ("short_mine" needs a helper missing from the reference itself)."""
+    w0, h0 = img_size_orig[0], img_size_orig[1]
+    if scaling_type in ("short", "short_with_resize"):
+        size, center, scale = multi_scale_size(h0, w0, input_size, 1.0, min_scale)
+        out = (int(size[0] / 2), int(size[1] / 2)) if scaling_type == "short" else (int(size[0]), int(size[1]))
+        keypoints[:, :, :2] = apply_affine(keypoints[:, :, :2], crop_affine(center, scale, out, inv=True))
+        return keypoints
+    if scaling_type in ("long", "long_with_multiscale"):
+        if input_size != 512:
+            raise AssertionError("reverse_affine_map: 'long' scaling needs input_size 512")
+        s = max(h0, w0) / 200
+        res = (512, 512) if scaling_type == "long" else (1024, 1024)
+        mat = box_transform(np.array((w0 / 2, h0 / 2)), np.array([s, s]), res)
+        keypoints[:, :, :2] = apply_affine(keypoints[:, :, :2] * 4, np.linalg.pinv(mat)[:2])
+        return keypoints
+    raise NotImplementedError(f"reverse_affine_map: scaling_type={scaling_type!r}")
