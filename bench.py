@@ -257,6 +257,56 @@ def frontend_projection(wl, gc, model, hm, tags, dev, out):
             "dense_bytes_written": B * 128 * H * W * 4, "nodes": int(out[0].shape[0])}
 
 
+def frontend_heatmaps(wl, gc, feats, dev, reps=5):
+    """SURVEY 8f row 1, informational: the test front-end (flip test + project2image, single scale:
+    PoseEstimation.py:329-452, multi_scales_testing.py:144-195) in front of construct_graph. With: the
+    reference's own torch ops materialise [B, J, H, W] heatmaps and [B, J, H, W, 2] tags from the
+    half-resolution network outputs of both passes (interpolate, flip, index, average), then
+    construct_graph reads them. Without: ProjectedHeatmaps -- the NMS loads sample the low-resolution
+    outputs directly (pemp_detect_projected) and the tags are sampled at the detections."""
+    from pemp_amd.frontend import ProjectedHeatmaps
+    B, J, H, W = wl["B"], wl["J"], wl["H"], wl["W"]
+    h, w = H // 2, W // 2
+    fi = [0, 2, 1, 4, 3, 6, 5, 8, 7, 10, 9, 12, 11, 14, 13, 16, 15] if J == 17 else list(range(J))   # COCO flip
+    hm = torch.from_numpy(syn.make_heatmaps(2000, B, J, h, w, wl["persons"], sigma=1.0, margin=4)).to(dev)
+    hm2 = torch.flip(hm, [3])[:, fi]      # the flipped pass sees the mirrored image with left / right swapped
+    g = torch.Generator(device=dev).manual_seed(99)
+    outs = torch.cat([hm, torch.rand(B, J, h, w, generator=g, device=dev)], 1)
+    flips = torch.cat([hm2, torch.rand(B, J, h, w, generator=g, device=dev)], 1)
+    ph = ProjectedHeatmaps([outs], (H, W), J, [flips], fi)
+
+    def graph(scoremaps, tagmaps):
+        return pemp_amd.get_graph_constructor(gc, scoremaps=scoremaps, features=feats, tagmaps=tagmaps, joints_gt=None,
+                                              factor_list=None, masks=None, device=dev, testing=True, heatmaps=None,
+                                              num_joints=J).construct_graph()
+
+    def dense():
+        s, t = ph.materialize()
+        return graph(s, t)
+
+    res = {}
+    for name, fn in (("reference_ops_then_construct_graph_ms", dense),
+                     ("projected_construct_graph_ms", lambda: graph(ph, ph))):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            out = fn()
+        torch.cuda.synchronize()
+        res[name] = round((time.perf_counter() - t0) / reps * 1e3, 3)
+        res["nodes"] = int(out[0].shape[0])
+    _lib.prof_enable("detect_nms_projected")
+    graph(ph, ph)
+    torch.cuda.synchronize()
+    st = _lib.prof_report()
+    _lib.prof_enable(None)
+    n, ms = st.get("detect_nms_projected", (1, float("nan")))
+    res["detect_nms_projected_us"] = round(ms / n * 1e3, 2)
+    res["inputs"] = f"2 passes x [{B}, {2 * J}, {h}, {w}] fp32 -> [{B}, {J}, {H}, {W}] scoremaps + [{B}, {J}, {H}, {W}, 2] tags"
+    res["dense_bytes_written_by_reference_ops"] = B * J * H * W * 4 * 3
+    return res
+
+
 def pose_grouping(wl, out, pe, pn, pc, cpu_ref):
     """SURVEY 8f row 2, informational: the pred_to_ann grouping prefix (node threshold 0.1, GAEC,
     graph_cluster_to_persons; Utils.py:1445-1459) for the whole step's batch, after the MPN and the
@@ -422,6 +472,7 @@ def main():
     mpn_eups = E_all * wl["steps"] * args.steps / dt_mpn
 
     front = frontend_projection(wl, gc, model, hm, tags, dev, out) if not args.no_roofline else None
+    front_hm = frontend_heatmaps(wl, gc, feats, dev) if not args.no_roofline else None
 
     global _BENCH_MAPS
     _BENCH_MAPS = (hm, tags)
@@ -465,6 +516,7 @@ def main():
             "kernel_avg_us": breakdown if not args.no_roofline else None,
             "cpu_baseline": cpu,
             "frontend_projection": front,
+            "frontend_heatmaps": front_hm,
             "pose_grouping": grouping,
         }
         if cpu:

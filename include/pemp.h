@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define PEMP_ABI_VERSION 11
+#define PEMP_ABI_VERSION 12
 
 enum {
   PEMP_OK = 0,
@@ -72,6 +72,46 @@ int pemp_detect(const float* scoremaps /*[B,J,H,W]*/, const float* masks /*[B,H,
                 int topk, int stages, void* workspace, size_t workspace_bytes,
                 int64_t* det_xyt /*[B,cap,3]*/, float* det_scores /*[B,cap]*/,
                 int32_t* n_det /*[B]*/, int cap, int32_t* n_det_host /*[B] or NULL*/, void* stream);
+/* The test-time front-end evaluated inside the detection instead of materialising [B,J,H,W] maps
+ * (PoseEstimation.py:329-452 _get_multi_stage_outputs with flip + project2image,
+ * multi_scales_testing.py:144-195 aggregate_results_mpn, PoseEstimation.py:227):
+ *   s[b,j,Y,X] = (sum_s avg_s[b,j,Y,X]) / divisor,
+ *   avg_s = flip_maps[s] ? (up(maps[s])[b,j] + up(flip(flip_maps[s]))[b,flip_index[j]]) / 2
+ *                        : up(maps[s])[b,j],
+ * up = bilinear to H x W, align_corners = False (torch's source-index rule), each product and sum rounded
+ * in fp32 in the order t0 = a lx0 + b lx1, t1 = c lx0 + d lx1, v = t0 ly0 + t1 ly1; flip mirrors the
+ * columns of the low-resolution map. maps[s] / flip_maps[s]: the network's outputs for scale s as it
+ * produced them ([B][channels][h][w]: heatmaps in channels 0..J-1, per-joint tags in J..2J-1; the
+ * flipped pass NOT un-flipped), flip_maps NULL without flip test. flip_index: device [J] int32 (the
+ * FLIP_CONFIG permutation) or NULL for the identity. Scales summed in the caller's order (the reference
+ * visits them in descending scale). */
+#define PEMP_PROJ_MAXS 4
+typedef struct pemp_proj_maps {
+  int num_scales;
+  int channels;
+  const float* maps[PEMP_PROJ_MAXS];
+  const float* flip_maps[PEMP_PROJ_MAXS];
+  int h[PEMP_PROJ_MAXS], w[PEMP_PROJ_MAXS];
+  const int32_t* flip_index;
+  float divisor;                        /* len(TEST.SCALE_FACTOR) */
+} pemp_proj_maps;
+/* pemp_detect on the projected maps (same outputs, workspace and stages; the values are sampled on
+ * demand in the NMS loads and at the emitted detections). */
+int pemp_detect_projected(const pemp_proj_maps* maps, const float* masks, int B, int J, int H, int W,
+                          int pool_kernel, float threshold, int use_threshold, int topk, int stages,
+                          void* workspace, size_t workspace_bytes, int64_t* det_xyt, float* det_scores,
+                          int32_t* n_det, int cap, int32_t* n_det_host, void* stream);
+/* The same maps materialised (refine / adjust need the image-size maps; checks): scoremaps [B,J,H,W]
+ * (or NULL) and tags (or NULL) as F planes [F][B,J,H,W] (f = 0 forward, 1 flipped pass), F = 2 with a
+ * flipped pass. Values identical to the ones the detection samples. */
+int pemp_project_maps(const pemp_proj_maps* maps, int B, int J, int H, int W, int tag_scale, float* scoremaps,
+                      float* tags, void* stream);
+/* joint_tags [N, F] of the detections from the tag channels (J + type) of scale tag_scale: F = 2
+ * (up(maps), up(flip(flip_maps)) at channel J + flip_index[type]) with a flipped pass, else F = 1
+ * (aggregate_results_mpn's tags_list of that scale, ConstructGraph.py:103). channels >= 2 J. */
+int pemp_gather_projected_tags(const pemp_proj_maps* maps, int tag_scale, int J, int H, int W,
+                               const int64_t* joint_det, const int64_t* batch_index, int64_t N,
+                               float* joint_tags, void* stream);
 /* Mapped, coherent host memory (hipHostMalloc) that kernels may store into; NULL on failure. */
 void* pemp_host_alloc(size_t bytes);
 int pemp_host_free(void* p);
@@ -139,10 +179,15 @@ int pemp_knn_graph_emit(const int64_t* node_off, const int64_t* node_off_host, i
  * edge_buf: device int64 [2 * e_cap], e_cap >= sum_b min(n_b (n_b - 1), 2 k n_b) (checked); the graph
  * is its leading [2, E] block (sources at 0, destinations at E). e_total_host: mapped host int32
  * (pemp_host_alloc), set to E by the device once the counts are scanned (the emit may still run);
- * the host spins on it (initialise it to -1). */
+ * the host spins on it (initialise it to -1). Batches whose images all have <= 512 nodes take the
+ * fast path (3 launches: selection, LDS transpose, emit with the edge features; node coordinates must
+ * fit int32), others the global-memory kernels above + the features kernel. */
 int pemp_knn_graph_build(const int64_t* joint_det, const int64_t* node_off, const int64_t* node_off_host,
                          int B, int k, void* workspace, size_t workspace_bytes, int64_t e_cap,
-                         int64_t* edge_buf, int32_t* e_total_host, void* stream);
+                         int64_t* edge_buf, int32_t* e_total_host, const float* joint_tags, int F,
+                         const float* joint_scores, int J, float norm_factor, int mode,
+                         float* edge_attr /*[e_cap, A] or NULL: pemp_edge_features' values, leading E rows*/,
+                         void* stream);
 
 /* Node features from maps projected to the image size on demand (the test front-end's bilinear
  * projection, PoseEstimation.py:426-452, summed over scales and divided, multi_scales_testing.py:182-190

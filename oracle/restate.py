@@ -19,6 +19,8 @@ Defined where the reference is unpinned:
 """
 import math
 
+import numpy as np
+
 import torch
 import torch.nn.functional as F
 
@@ -413,3 +415,58 @@ def mpn_forward(sd, cfg, x, edge_attr, edge_index, node_types):
     pn.append(_mlp(sd, "node_classification", nf, cfg.NODE_CLASS.OUTPUT_SIZES, cfg.BN).squeeze())
     pc.append(_mlp(sd, "classification", nf, cfg.CLASS.OUTPUT_SIZES, cfg.BN))
     return pe, pn, pc, [None]
+
+
+# ----------------------------------------------------------------------------------------
+# Test-time front-end (PoseEstimation.py:329-452, multi_scales_testing.py:144-195)
+# ----------------------------------------------------------------------------------------
+def _taps(out_size, in_size):
+    """torch's area_pixel_compute_source_index (align_corners=False) in fp32: i0, i1, l0, l1 per output."""
+    f32 = np.float32
+    scale = f32(in_size) / f32(out_size)
+    src = (scale * (np.arange(out_size, dtype=f32) + f32(0.5))) - f32(0.5)
+    src = np.maximum(src, f32(0))
+    i0 = src.astype(np.int64)
+    i1 = i0 + (i0 < in_size - 1)
+    l1 = np.clip(src - i0.astype(f32), f32(0), f32(1))
+    return i0, i1, (f32(1) - l1).astype(f32), l1.astype(f32)
+
+
+def upsample_bilinear(m, size):
+    """interpolate(m, size, bilinear, align_corners=False) on [..., h, w] float32, every product and sum
+    rounded in fp32 in the order t0 = a lx0 + b lx1, t1 = c lx0 + d lx1, v = t0 ly0 + t1 ly1 (torch's
+    CPU upsample evaluates the same expression, possibly contracting products into FMAs)."""
+    m = np.asarray(m, dtype=np.float32)
+    H, W = size
+    y0, y1, ly0, ly1 = _taps(H, m.shape[-2])
+    x0, x1, lx0, lx1 = _taps(W, m.shape[-1])
+    r0, r1 = m[..., y0, :], m[..., y1, :]
+    t0 = r0[..., x0] * lx0 + r0[..., x1] * lx1
+    t1 = r1[..., x0] * lx0 + r1[..., x1] * lx1
+    return (t0 * ly0[:, None] + t1 * ly1[:, None]).astype(np.float32)
+
+
+def project_frontend(outputs, flip_outputs, size, num_joints, flip_index=None, divisor=None, tag_scale=0):
+    """The front-end's image-size scoremaps [B, J, H, W] and tags [B, J, H, W, F] (F = 2 with a flipped
+    pass) from per-scale network outputs [B, C, h, w]: heatmaps_avg = (up(out) + up(flip(flip_out))
+    [:, flip_index]) / 2 per scale, summed in order and divided by `divisor`; tags of scale tag_scale
+    (channels J..2J-1), flipped ones re-indexed by flip_index (TAG_PER_JOINT). fp32 numpy."""
+    J = num_joints
+    fi = np.arange(J) if flip_index is None else np.asarray(flip_index)
+    outs = [np.asarray(o, dtype=np.float32) for o in outputs]
+    flips = None if flip_outputs is None else [np.asarray(o, dtype=np.float32) for o in flip_outputs]
+    acc = None
+    for s, o in enumerate(outs):
+        h = upsample_bilinear(o[:, :J], size)
+        if flips is not None:
+            hf = upsample_bilinear(flips[s][:, :J][:, fi][..., ::-1], size)
+            h = ((h + hf) / np.float32(2.0)).astype(np.float32)
+        acc = h if acc is None else (acc + h).astype(np.float32)
+    scoremaps = (acc / np.float32(len(outs) if divisor is None else divisor)).astype(np.float32)
+    tags = None
+    if outs[tag_scale].shape[1] >= 2 * J:
+        tl = [upsample_bilinear(outs[tag_scale][:, J:2 * J], size)[..., None]]
+        if flips is not None:
+            tl.append(upsample_bilinear(flips[tag_scale][:, J:2 * J][:, fi][..., ::-1], size)[..., None])
+        tags = np.concatenate(tl, axis=4)
+    return torch.from_numpy(scoremaps), None if tags is None else torch.from_numpy(tags)

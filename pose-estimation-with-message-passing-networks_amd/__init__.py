@@ -25,3 +25,10 @@ def ProjectedMaps(maps, size, divisor=None):
     """Lazy image-size projection of per-scale feature maps for ``features=`` (frontend.py)."""
     from .frontend import ProjectedMaps as _p
     return _p(maps, size, divisor)
+
+
+def ProjectedHeatmaps(outputs, size, num_joints, flip_outputs=None, flip_index=None, divisor=None, tag_scale=0):
+    """The test front-end's image-size heatmaps / tags evaluated on demand, for ``scoremaps=`` and
+    ``tagmaps=`` (frontend.py)."""
+    from .frontend import ProjectedHeatmaps as _p
+    return _p(outputs, size, num_joints, flip_outputs, flip_index, divisor, tag_scale)

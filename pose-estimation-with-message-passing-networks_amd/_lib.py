@@ -9,7 +9,7 @@ import os
 
 LIB_PATH = os.environ.get("PEMP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc",
                                                      "libpemp.so")
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 ERR_INVALID_ARG, ERR_HIP, ERR_WORKSPACE, ERR_UNSUPPORTED = -1, -2, -3, -4
 
@@ -35,6 +35,11 @@ class PempMpnWeights(ctypes.Structure):
                 ("upd_mlp", PempMlp),
                 ("ept_l1_w", c_p), ("ept_l1_b", c_p), ("ept_l2_w", c_p), ("ept_l2_b", c_p), ("ept_o1_w", c_p),
                 ("ept_o2_w", c_p), ("edge_img", c_p)]
+
+
+class PempProjMaps(ctypes.Structure):
+    _fields_ = [("num_scales", c_i32), ("channels", c_i32), ("maps", c_p * 4), ("flip_maps", c_p * 4),
+                ("h", c_i32 * 4), ("w", c_i32 * 4), ("flip_index", c_p), ("divisor", c_f32)]
 
 
 class PempMpnDesc(ctypes.Structure):
@@ -64,10 +69,15 @@ SIGNATURES = {
     "pemp_knn_workspace_size": (c_sz, [c_p, c_i32]),
     "pemp_knn_graph_count": (c_i32, [c_p, c_p, c_p, c_i32, c_i32, c_p, c_sz, c_p, c_p]),
     "pemp_knn_graph_emit": (c_i32, [c_p, c_p, c_i32, c_p, c_i64, c_p, c_sz, c_p, c_p]),
-    "pemp_knn_graph_build": (c_i32, [c_p, c_p, c_p, c_i32, c_i32, c_p, c_sz, c_i64, c_p, c_p, c_p]),
+    "pemp_knn_graph_build": (c_i32, [c_p, c_p, c_p, c_i32, c_i32, c_p, c_sz, c_i64, c_p, c_p, c_p, c_i32, c_p,
+                                     c_i32, c_f32, c_i32, c_p, c_p]),
     "pemp_score_graph_workspace_size": (c_sz, [c_p, c_i32, c_i32]),
     "pemp_score_graph": (c_i32, [c_p, c_p, c_p, c_i32, c_i32, c_i64, c_p, c_sz, c_p, c_p]),
     "pemp_gather_projected": (c_i32, [c_p, c_p, c_p, c_i32, c_i32, c_i32, c_i32, c_f32, c_p, c_p, c_i64, c_p, c_p]),
+    "pemp_detect_projected": (c_i32, [c_p, c_p, c_i32, c_i32, c_i32, c_i32, c_i32, c_f32, c_i32, c_i32, c_i32, c_p,
+                                      c_sz, c_p, c_p, c_p, c_i32, c_p, c_p]),
+    "pemp_gather_projected_tags": (c_i32, [c_p, c_i32, c_i32, c_i32, c_i32, c_p, c_p, c_i64, c_p, c_p]),
+    "pemp_project_maps": (c_i32, [c_p, c_i32, c_i32, c_i32, c_i32, c_i32, c_p, c_p, c_p]),
     "pemp_edge_features": (c_i32, [c_p, c_p, c_i32, c_p, c_p, c_i64, c_i32, c_f32, c_i32, c_p, c_p]),
     "pemp_mpn_workspace_size": (c_sz, [ctypes.POINTER(PempMpnDesc), c_i64, c_i64]),
     "pemp_mpn_forward": (c_i32, [ctypes.POINTER(PempMpnDesc), ctypes.POINTER(PempMpnWeights), c_p, c_p, c_p, c_p,

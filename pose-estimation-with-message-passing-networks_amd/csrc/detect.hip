@@ -182,6 +182,96 @@ __device__ __forceinline__ float wave_shl1(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xF, 0xF, true));
 }
 
+// ---- test-time front-end evaluated on demand (pemp_detect_projected) -------------
+// s[b, j, Y, X] = (sum_s avg_s) / divisor, avg_s = (up(maps_s)[b, j] + up(flip(flip_maps_s))[b, fi[j]]) / 2
+// (or up(maps_s)[b, j] without a flipped pass). up = bilinear to H x W, align_corners=False, torch's
+// source index (area_pixel_compute_source_index); every product and sum rounded in fp32 in the order
+// t0 = a lx0 + b lx1, t1 = c lx0 + d lx1, v = t0 ly0 + t1 ly1 (as pemp_gather_projected). flip mirrors
+// the columns of the low-resolution map (torch.flip(output, [3]) before the interpolation).
+struct ProjArgs {
+  int S, C;                            // scales; channels of every map
+  const float* m[PEMP_PROJ_MAXS];      // [B][C][h][w]
+  const float* f[PEMP_PROJ_MAXS];      // flipped pass, or NULL
+  int h[PEMP_PROJ_MAXS], w[PEMP_PROJ_MAXS];
+  const int* fi;                       // [J] or NULL
+  float divisor;
+  int ch0;                             // first channel read (0: heatmaps; J: tags)
+};
+
+struct ProjTaps {   // one axis of the bilinear source index
+  int i0, i1;
+  float l0, l1;
+};
+
+__device__ __forceinline__ ProjTaps proj_taps(int dst, int out_size, int in_size) {
+  ProjTaps t;
+  const float scale = (float)in_size / (float)out_size;
+  float src = __fsub_rn(__fmul_rn(scale, __fadd_rn((float)dst, 0.5f)), 0.5f);
+  if (src < 0.f) src = 0.f;
+  t.i0 = (int)src;
+  t.i1 = t.i0 + (t.i0 < in_size - 1 ? 1 : 0);
+  t.l1 = fminf(fmaxf(__fsub_rn(src, (float)t.i0), 0.f), 1.f);
+  t.l0 = __fsub_rn(1.f, t.l1);
+  return t;
+}
+
+__device__ __forceinline__ float bilerp(const float* pl, int w, const ProjTaps& ty, int x0, int x1, float lx0,
+                                        float lx1) {
+  const float a = pl[ty.i0 * w + x0], b = pl[ty.i0 * w + x1];
+  const float c = pl[ty.i1 * w + x0], d = pl[ty.i1 * w + x1];
+  const float t0 = __fadd_rn(__fmul_rn(a, lx0), __fmul_rn(b, lx1));
+  const float t1 = __fadd_rn(__fmul_rn(c, lx0), __fmul_rn(d, lx1));
+  return __fadd_rn(__fmul_rn(t0, ty.l0), __fmul_rn(t1, ty.l1));
+}
+
+// one scale's (flip-averaged) value at row taps ty and the column's taps tx (tx of the unflipped map)
+__device__ __forceinline__ float proj_scale(const ProjArgs& pj, int s, int b, int j, const ProjTaps& ty,
+                                            const ProjTaps& tx) {
+  const int h = pj.h[s], w = pj.w[s];
+  const float v0 = bilerp(pj.m[s] + ((size_t)b * pj.C + pj.ch0 + j) * h * w, w, ty, tx.i0, tx.i1, tx.l0, tx.l1);
+  if (!pj.f[s]) return v0;
+  const int jf = pj.fi ? pj.fi[j] : j;
+  const float v1 = bilerp(pj.f[s] + ((size_t)b * pj.C + pj.ch0 + jf) * h * w, w, ty, w - 1 - tx.i0, w - 1 - tx.i1,
+                          tx.l0, tx.l1);
+  return __fmul_rn(__fadd_rn(v0, v1), 0.5f);   // (a + b) / 2.0: the division by 2 is exact
+}
+
+__device__ float proj_pixel(const ProjArgs& pj, int b, int j, int Y, int X, int H, int W) {
+  float acc = 0.f;
+  for (int s = 0; s < pj.S; ++s) {
+    const float v = proj_scale(pj, s, b, j, proj_taps(Y, H, pj.h[s]), proj_taps(X, W, pj.w[s]));
+    acc = s == 0 ? v : __fadd_rn(acc, v);
+  }
+  return div_rn(acc, pj.divisor);
+}
+
+// rows y0 - P .. y0 + SR - 1 + P of the lane's column from the projected maps; -inf outside the plane
+template <int P>
+__device__ __forceinline__ void load_unit_proj(const ProjArgs& pj, const DetectGeom& g, int u, float (&r)[SR + 2 * P]) {
+  const int lane = threadIdx.x & 63;
+  const int plane = u / g.units, rem = u - plane * g.units, band = rem / g.nsx, strip = rem - band * g.nsx;
+  const int b = plane / g.J, j = plane - b * g.J;
+  const int y0 = band * SR, x = strip * g.sc - P + lane;
+  const bool xok = x >= 0 && x < g.W;
+  const int xc = min(max(x, 0), g.W - 1);
+#pragma unroll
+  for (int i = 0; i < SR + 2 * P; ++i) r[i] = 0.f;
+  for (int s = 0; s < pj.S; ++s) {
+    const ProjTaps tx = proj_taps(xc, g.W, pj.w[s]);
+#pragma unroll
+    for (int i = 0; i < SR + 2 * P; ++i) {
+      const int yc = min(max(y0 - P + i, 0), g.H - 1);
+      const float v = proj_scale(pj, s, b, j, proj_taps(yc, g.H, pj.h[s]), tx);
+      r[i] = s == 0 ? v : __fadd_rn(r[i], v);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < SR + 2 * P; ++i) {
+    const int y = y0 - P + i;
+    r[i] = (xok && y >= 0 && y < g.H) ? div_rn(r[i], pj.divisor) : -INFINITY;
+  }
+}
+
 // rows y0 - P .. y0 + SR - 1 + P of the lane's column; -inf outside the plane (MaxPool padding)
 template <int P>
 __device__ __forceinline__ void load_unit(const float* __restrict__ s, const DetectGeom& g, int u,
@@ -216,11 +306,11 @@ __device__ __forceinline__ void load_unit(const float* __restrict__ s, const Det
   }
 }
 
-template <int P, int MODE, bool MASKED>
+template <int P, int MODE, bool MASKED, bool PROJ>
 __global__ __launch_bounds__(NT1) void nms_strips_kernel(
     const float* __restrict__ s, const float* __restrict__ masks, DetectGeom g, float thr, int use_thr,
     float* __restrict__ cand_v, int* __restrict__ cand_i, float* __restrict__ neg_v, int* __restrict__ neg_i,
-    int* __restrict__ tile_count, int* __restrict__ tile_nonneg, cmask_t* __restrict__ cbits) {
+    int* __restrict__ tile_count, int* __restrict__ tile_nonneg, cmask_t* __restrict__ cbits, ProjArgs pj) {
   const int lane = threadIdx.x & 63;
   const int total = g.B * g.J * g.units;
   const int H = g.H, W = g.W, K = g.K;
@@ -234,9 +324,13 @@ __global__ __launch_bounds__(NT1) void nms_strips_kernel(
   // the unit index is wave-uniform: keep it (and all address math derived from it) scalar
   int u = __builtin_amdgcn_readfirstlane(slot * (NT1 / 64) + (threadIdx.x >> 6));
   float r[SR + 2 * P];
-  if (NMS_PREFETCH && u < u_hi) load_unit<P>(s, g, u, r);
+  auto load = [&](int uu) {
+    if constexpr (PROJ) load_unit_proj<P>(pj, g, uu, r);
+    else load_unit<P>(s, g, uu, r);
+  };
+  if (NMS_PREFETCH && u < u_hi) load(u);
   for (; u < u_hi; u += stride_u) {
-    if (!NMS_PREFETCH) load_unit<P>(s, g, u, r);
+    if (!NMS_PREFETCH) load(u);
     const int plane = u / g.units, rem = u - plane * g.units, band = rem / g.nsx, strip = rem - band * g.nsx;
     const int b = plane / g.J;
     const int y0 = band * SR, x = strip * g.sc - P + lane;
@@ -244,7 +338,7 @@ __global__ __launch_bounds__(NT1) void nms_strips_kernel(
     float cur[SR + 2 * P];
 #pragma unroll
     for (int i = 0; i < SR + 2 * P; ++i) cur[i] = r[i];
-    if (NMS_PREFETCH && u + stride_u < u_hi) load_unit<P>(s, g, u + stride_u, r);   // next unit's rows in flight
+    if (NMS_PREFETCH && u + stride_u < u_hi) load(u + stride_u);   // next unit's rows in flight
     float vm[SR], c[SR];
 #pragma unroll
     for (int j = 0; j < SR; ++j) {
@@ -496,7 +590,7 @@ __global__ __launch_bounds__(256) void emit_kernel(const float* __restrict__ s, 
                                                    DetectGeom g, const cmask_t* __restrict__ cbits,
                                                    DetectWs w, int64_t* __restrict__ det,
                                                    float* __restrict__ scores, int* __restrict__ n_det, int cap,
-                                                   int* __restrict__ n_host) {
+                                                   int* __restrict__ n_host, ProjArgs pj) {
   __shared__ int top_i[KCAP], top_bit[KCAP], sh[4];
   __shared__ int band_n[MAXB], band_off[MAXB];
   __shared__ unsigned band_nz[MAXB][2];      // non-empty strips of each band (bit = strip, nsx <= 64)
@@ -626,7 +720,7 @@ __global__ __launch_bounds__(256) void emit_kernel(const float* __restrict__ s, 
           const int o = pos + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(word >> 32),
                                                           __builtin_amdgcn_mbcnt_lo((unsigned)word, 0u));
           if (o < cap) {
-            const float sv = plane[(size_t)yy * W + xx];
+            const float sv = pj.S ? proj_pixel(pj, b, t, yy, xx, H, W) : plane[(size_t)yy * W + xx];
             float jm = 1.0f;
             if (masks) jm = jm * masks[((size_t)b * H + yy) * W + xx];
             dout[o * 3 + 0] = xx;
@@ -644,9 +738,9 @@ __global__ __launch_bounds__(256) void emit_kernel(const float* __restrict__ s, 
   }
 }
 
-template <int P, int MODE>
+template <int P, int MODE, bool PROJ>
 static void launch_nms(const float* s, const float* masks, const DetectGeom& g, float thr, int use_thr,
-                       const DetectWs& w, hipStream_t st) {
+                       const DetectWs& w, const ProjArgs& pj, hipStream_t st) {
   const int total = g.B * g.J * g.units;
   const int want = (total + NT1 / 64 - 1) / (NT1 / 64);
   // resident workgroups per CU: 4 (one wave per SIMD each) while the kernel fits 128 VGPRs (SR 16);
@@ -654,33 +748,38 @@ static void launch_nms(const float* s, const float* masks, const DetectGeom& g, 
   constexpr int per_cu = SR > 16 ? 2 : NMS_PER_CU;
   const int grid = want < per_cu * num_cus() ? want : per_cu * num_cus();
   if (masks)
-    hipLaunchKernelGGL((nms_strips_kernel<P, MODE, true>), dim3(grid), dim3(NT1), 0, st, s, masks, g, thr, use_thr,
-                       w.cand_v, w.cand_i, w.neg_v, w.neg_i, w.tile_count, w.tile_nonneg, w.cbits);
+    hipLaunchKernelGGL((nms_strips_kernel<P, MODE, true, PROJ>), dim3(grid), dim3(NT1), 0, st, s, masks, g, thr,
+                       use_thr, w.cand_v, w.cand_i, w.neg_v, w.neg_i, w.tile_count, w.tile_nonneg, w.cbits, pj);
   else
-    hipLaunchKernelGGL((nms_strips_kernel<P, MODE, false>), dim3(grid), dim3(NT1), 0, st, s, masks, g, thr, use_thr,
-                       w.cand_v, w.cand_i, w.neg_v, w.neg_i, w.tile_count, w.tile_nonneg, w.cbits);
+    hipLaunchKernelGGL((nms_strips_kernel<P, MODE, false, PROJ>), dim3(grid), dim3(NT1), 0, st, s, masks, g, thr,
+                       use_thr, w.cand_v, w.cand_i, w.neg_v, w.neg_i, w.tile_count, w.tile_nonneg, w.cbits, pj);
 }
 
-template <int MODE>
+template <int MODE, bool PROJ>
 static void dispatch_nms(const float* s, const float* masks, const DetectGeom& g, float thr, int use_thr,
-                         const DetectWs& w, hipStream_t st) {
+                         const DetectWs& w, const ProjArgs& pj, hipStream_t st) {
   switch (g.p) {
-    case 0: launch_nms<0, MODE>(s, masks, g, thr, use_thr, w, st); break;
-    case 1: launch_nms<1, MODE>(s, masks, g, thr, use_thr, w, st); break;
-    case 2: launch_nms<2, MODE>(s, masks, g, thr, use_thr, w, st); break;
-    case 3: launch_nms<3, MODE>(s, masks, g, thr, use_thr, w, st); break;
-    default: launch_nms<4, MODE>(s, masks, g, thr, use_thr, w, st); break;
+    case 0: launch_nms<0, MODE, PROJ>(s, masks, g, thr, use_thr, w, pj, st); break;
+    case 1: launch_nms<1, MODE, PROJ>(s, masks, g, thr, use_thr, w, pj, st); break;
+    case 2: launch_nms<2, MODE, PROJ>(s, masks, g, thr, use_thr, w, pj, st); break;
+    case 3: launch_nms<3, MODE, PROJ>(s, masks, g, thr, use_thr, w, pj, st); break;
+    default: launch_nms<4, MODE, PROJ>(s, masks, g, thr, use_thr, w, pj, st); break;
   }
 }
 
 template <int KMAX>
 static int launch_detect(const float* s, const float* masks, const DetectGeom& g, float thr, int use_thr,
                          int stages, const DetectWs& w, int64_t* det, float* scores, int32_t* n_det, int cap,
-                         int32_t* n_host, hipStream_t st) {
+                         int32_t* n_host, const ProjArgs& pj, hipStream_t st) {
   if (stages & PEMP_DETECT_NMS) {
-    ProfScope prof("detect_nms", st);
-    if (use_thr) dispatch_nms<MODE_POS>(s, masks, g, thr, use_thr, w, st);
-    else dispatch_nms<MODE_ALL>(s, masks, g, thr, use_thr, w, st);
+    ProfScope prof(pj.S ? "detect_nms_projected" : "detect_nms", st);
+    if (pj.S) {
+      if (use_thr) dispatch_nms<MODE_POS, true>(s, masks, g, thr, use_thr, w, pj, st);
+      else dispatch_nms<MODE_ALL, true>(s, masks, g, thr, use_thr, w, pj, st);
+    } else {
+      if (use_thr) dispatch_nms<MODE_POS, false>(s, masks, g, thr, use_thr, w, pj, st);
+      else dispatch_nms<MODE_ALL, false>(s, masks, g, thr, use_thr, w, pj, st);
+    }
     PEMP_LAUNCH_CHECK();
   }
   if (stages & PEMP_DETECT_SELECT) {
@@ -692,9 +791,78 @@ static int launch_detect(const float* s, const float* masks, const DetectGeom& g
     }
     ProfScope prof("detect_emit", st);
     hipLaunchKernelGGL(emit_kernel, dim3(g.B * g.J), dim3(256), 0, st, s, masks, g, w.cbits, w, det, scores,
-                       (int*)n_det, cap, (int*)n_host);
+                       (int*)n_det, cap, (int*)n_host, pj);
     PEMP_LAUNCH_CHECK();
   }
+  return PEMP_OK;
+}
+
+// tags of the detections from the projected maps (channels J + type): joint_tags[n] = [up(maps_s)(y, x),
+// up(flip(flip_maps_s))(y, x) at channel J + fi[type]] for the tag scale s (F = 1 without a flipped pass)
+__global__ __launch_bounds__(256) void gather_proj_tags_kernel(ProjArgs pj, int s, int H, int W,
+                                                               const int64_t* __restrict__ jdet,
+                                                               const int64_t* __restrict__ bidx, int64_t N,
+                                                               float* __restrict__ tags) {
+  const int F = pj.f[s] ? 2 : 1;
+  for (int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; n < N; n += (int64_t)gridDim.x * blockDim.x) {
+    const int x = (int)jdet[n * 3], y = (int)jdet[n * 3 + 1], j = (int)jdet[n * 3 + 2];
+    const int b = (int)bidx[n];
+    const int h = pj.h[s], w = pj.w[s];
+    const ProjTaps ty = proj_taps(y, H, h), tx = proj_taps(x, W, w);
+    tags[n * F] = bilerp(pj.m[s] + ((size_t)b * pj.C + pj.ch0 + j) * h * w, w, ty, tx.i0, tx.i1, tx.l0, tx.l1);
+    if (F == 2) {
+      const int jf = pj.fi ? pj.fi[j] : j;
+      tags[n * F + 1] = bilerp(pj.f[s] + ((size_t)b * pj.C + pj.ch0 + jf) * h * w, w, ty, w - 1 - tx.i0,
+                               w - 1 - tx.i1, tx.l0, tx.l1);
+    }
+  }
+}
+
+// the projected scoremaps (or, ch0 = J, one tag plane f of the tags) materialised at [B, J, H, W]
+__global__ __launch_bounds__(256) void proj_materialize_kernel(ProjArgs pj, int B, int J, int H, int W, int tags_f,
+                                                               float* __restrict__ out) {
+  const int64_t total = (int64_t)B * J * H * W;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int X = (int)(idx % W);
+    const int64_t r = idx / W;
+    const int Y = (int)(r % H), plane = (int)(r / H), b = plane / J, j = plane - b * J;
+    if (tags_f < 0) {
+      out[idx] = proj_pixel(pj, b, j, Y, X, H, W);
+    } else {   // tags of scale 0 of pj (the caller selects the scale): f = 0 forward, 1 flipped
+      const ProjTaps ty = proj_taps(Y, H, pj.h[0]), tx = proj_taps(X, W, pj.w[0]);
+      const int h = pj.h[0], w = pj.w[0];
+      float v;
+      if (tags_f == 0) {
+        v = bilerp(pj.m[0] + ((size_t)b * pj.C + pj.ch0 + j) * h * w, w, ty, tx.i0, tx.i1, tx.l0, tx.l1);
+      } else {
+        const int jf = pj.fi ? pj.fi[j] : j;
+        v = bilerp(pj.f[0] + ((size_t)b * pj.C + pj.ch0 + jf) * h * w, w, ty, w - 1 - tx.i0, w - 1 - tx.i1, tx.l0,
+                   tx.l1);
+      }
+      out[idx] = v;
+    }
+  }
+}
+
+static int proj_args(const pemp_proj_maps* m, int J, ProjArgs* pj, const char* fn) {
+  PEMP_CHECK_ARG(m && m->num_scales >= 1 && m->num_scales <= PEMP_PROJ_MAXS && m->channels >= J && m->divisor > 0.f,
+                 "%s: bad projected maps (1..%d scales, channels >= J, divisor > 0)", fn, PEMP_PROJ_MAXS);
+  ProjArgs a{};
+  a.S = m->num_scales;
+  a.C = m->channels;
+  for (int s = 0; s < a.S; ++s) {
+    PEMP_CHECK_ARG(m->maps[s] && m->h[s] > 0 && m->w[s] > 0, "%s: scale %d: null map or empty size", fn, s);
+    PEMP_CHECK_ARG((size_t)m->h[s] * m->w[s] < 0x7fffffffull, "%s: scale %d map too large", fn, s);
+    a.m[s] = m->maps[s];
+    a.f[s] = m->flip_maps[s];
+    a.h[s] = m->h[s];
+    a.w[s] = m->w[s];
+  }
+  a.fi = m->flip_index;
+  a.divisor = m->divisor;
+  a.ch0 = 0;
+  *pj = a;
   return PEMP_OK;
 }
 
@@ -711,11 +879,11 @@ extern "C" size_t pemp_detect_workspace_size(int B, int J, int H, int W, int top
   return bytes;
 }
 
-extern "C" int pemp_detect(const float* scoremaps, const float* masks, int B, int J, int H, int W, int pool_kernel,
-                           float threshold, int use_threshold, int topk, int stages, void* workspace,
-                           size_t workspace_bytes, int64_t* det_xyt, float* det_scores, int32_t* n_det, int cap,
-                           int32_t* n_det_host, void* stream) {
-  PEMP_CHECK_ARG(scoremaps && workspace && det_xyt && det_scores && n_det, "pemp_detect: null pointer");
+static int detect_impl(const float* scoremaps, const ProjArgs* proj, const float* masks, int B, int J, int H, int W,
+                       int pool_kernel, float threshold, int use_threshold, int topk, int stages, void* workspace,
+                       size_t workspace_bytes, int64_t* det_xyt, float* det_scores, int32_t* n_det, int cap,
+                       int32_t* n_det_host, void* stream) {
+  PEMP_CHECK_ARG(workspace && det_xyt && det_scores && n_det, "pemp_detect: null pointer");
   PEMP_CHECK_ARG(B > 0 && J > 0 && J <= MAXJ && H > 0 && W > 0, "pemp_detect: bad shape B=%d J=%d H=%d W=%d", B, J, H, W);
   PEMP_CHECK_ARG(pool_kernel % 2 == 1 && pool_kernel >= 1 && pool_kernel / 2 <= MAXR,
                  "pemp_detect: pool_kernel must be odd and <= %d (got %d)", 2 * MAXR + 1, pool_kernel);
@@ -738,11 +906,77 @@ extern "C" int pemp_detect(const float* scoremaps, const float* masks, int B, in
   if (n_det_host) {
     PEMP_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&n_host), n_det_host, 0));
   }
+  const ProjArgs pj = proj ? *proj : ProjArgs{};
   if (K <= 8)
     return launch_detect<8>(scoremaps, masks, g, threshold, use_threshold, stages, w, det_xyt, det_scores, n_det,
-                            cap, n_host, st);
+                            cap, n_host, pj, st);
   return launch_detect<32>(scoremaps, masks, g, threshold, use_threshold, stages, w, det_xyt, det_scores, n_det,
-                           cap, n_host, st);
+                           cap, n_host, pj, st);
+}
+
+extern "C" int pemp_detect(const float* scoremaps, const float* masks, int B, int J, int H, int W, int pool_kernel,
+                           float threshold, int use_threshold, int topk, int stages, void* workspace,
+                           size_t workspace_bytes, int64_t* det_xyt, float* det_scores, int32_t* n_det, int cap,
+                           int32_t* n_det_host, void* stream) {
+  PEMP_CHECK_ARG(scoremaps, "pemp_detect: null pointer");
+  return detect_impl(scoremaps, nullptr, masks, B, J, H, W, pool_kernel, threshold, use_threshold, topk, stages,
+                     workspace, workspace_bytes, det_xyt, det_scores, n_det, cap, n_det_host, stream);
+}
+
+extern "C" int pemp_detect_projected(const pemp_proj_maps* maps, const float* masks, int B, int J, int H, int W,
+                                     int pool_kernel, float threshold, int use_threshold, int topk, int stages,
+                                     void* workspace, size_t workspace_bytes, int64_t* det_xyt, float* det_scores,
+                                     int32_t* n_det, int cap, int32_t* n_det_host, void* stream) {
+  ProjArgs pj;
+  if (const int rc = proj_args(maps, J, &pj, "pemp_detect_projected")) return rc;
+  return detect_impl(nullptr, &pj, masks, B, J, H, W, pool_kernel, threshold, use_threshold, topk, stages, workspace,
+                     workspace_bytes, det_xyt, det_scores, n_det, cap, n_det_host, stream);
+}
+
+extern "C" int pemp_project_maps(const pemp_proj_maps* maps, int B, int J, int H, int W, int tag_scale,
+                                 float* scoremaps, float* tags, void* stream) {
+  ProjArgs pj;
+  if (const int rc = proj_args(maps, J, &pj, "pemp_project_maps")) return rc;
+  PEMP_CHECK_ARG(B > 0 && J > 0 && H > 0 && W > 0 && (scoremaps || tags), "pemp_project_maps: bad args");
+  const hipStream_t st = as_stream(stream);
+  const int64_t total = (int64_t)B * J * H * W;
+  const unsigned grid = (unsigned)std::min<int64_t>((total + 255) / 256, 8192);
+  ProfScope prof("project_maps", st);
+  if (scoremaps) {
+    hipLaunchKernelGGL(proj_materialize_kernel, dim3(grid), dim3(256), 0, st, pj, B, J, H, W, -1, scoremaps);
+    PEMP_LAUNCH_CHECK();
+  }
+  if (tags) {   // [B, J, H, W, F] interleaved: materialise each f plane, then interleave on the host side
+    PEMP_CHECK_ARG(tag_scale >= 0 && tag_scale < pj.S && maps->channels >= 2 * J, "pemp_project_maps: no tag channels");
+    ProjArgs pt = pj;
+    pt.S = 1;
+    pt.m[0] = pj.m[tag_scale]; pt.f[0] = pj.f[tag_scale]; pt.h[0] = pj.h[tag_scale]; pt.w[0] = pj.w[tag_scale];
+    pt.ch0 = J;
+    const int F = pt.f[0] ? 2 : 1;
+    for (int f = 0; f < F; ++f) {
+      hipLaunchKernelGGL(proj_materialize_kernel, dim3(grid), dim3(256), 0, st, pt, B, J, H, W, f, tags + f * total);
+      PEMP_LAUNCH_CHECK();
+    }
+  }
+  return PEMP_OK;
+}
+
+extern "C" int pemp_gather_projected_tags(const pemp_proj_maps* maps, int tag_scale, int J, int H, int W,
+                                          const int64_t* joint_det, const int64_t* batch_index, int64_t N,
+                                          float* joint_tags, void* stream) {
+  ProjArgs pj;
+  if (const int rc = proj_args(maps, 2 * J, &pj, "pemp_gather_projected_tags")) return rc;
+  PEMP_CHECK_ARG(tag_scale >= 0 && tag_scale < pj.S && H > 0 && W > 0 && N >= 0,
+                 "pemp_gather_projected_tags: bad args");
+  PEMP_CHECK_ARG(N == 0 || (joint_det && batch_index && joint_tags), "pemp_gather_projected_tags: null pointer");
+  if (N == 0) return PEMP_OK;
+  pj.ch0 = J;
+  const hipStream_t st = as_stream(stream);
+  ProfScope prof("gather_proj_tags", st);
+  hipLaunchKernelGGL(gather_proj_tags_kernel, dim3((unsigned)std::min<int64_t>((N + 255) / 256, 1024)), dim3(256), 0,
+                     st, pj, tag_scale, H, W, joint_det, batch_index, N, joint_tags);
+  PEMP_LAUNCH_CHECK();
+  return PEMP_OK;
 }
 
 // Mapped, coherent host memory for pemp_detect's n_det_host (the kernels store into it directly).

@@ -42,7 +42,7 @@ __device__ __forceinline__ float tag_distance(const float* ts, const float* td, 
 // ae_tracking_1 -> (t_a - dist) / t_a with t_a = 1.8425 (fp32 ops, no contraction)
 __device__ __forceinline__ float ae_term(int mode, float dist, float score_src) {
   if (mode == PEMP_EF_AE_NORMED) return __fsub_rn(__fmul_rn(rintf(dist), 100.0f), score_src);
-  if (mode == PEMP_EF_AE_TRACKING) return __fdiv_rn(__fsub_rn(1.8425f, dist), 1.8425f);
+  if (mode == PEMP_EF_AE_TRACKING) return div_rn(__fsub_rn(1.8425f, dist), 1.8425f);
   return dist;
 }
 
@@ -125,9 +125,15 @@ __global__ __launch_bounds__(256) void edge_features_kernel(const int64_t* __res
                                                             const float* __restrict__ jtag, int F,
                                                             const float* __restrict__ jsc,
                                                             const int64_t* __restrict__ ei, int64_t E, int J,
-                                                            float norm, int mode, int A, float* __restrict__ out) {
+                                                            float norm, int mode, int A, float* __restrict__ out,
+                                                            const int64_t* __restrict__ e_dev = nullptr) {
   __shared__ float dx_s[256], dy_s[256], aux_s[256];
   __shared__ int ts_s[256], td_s[256];
+  if (e_dev) {   // the edge total known only on the device (pemp_knn_graph_build); E = the capacity
+    const int64_t e = *e_dev;
+    if (e > E) return;
+    E = e;
+  }
   for (int64_t base = (int64_t)blockIdx.x * 256; base < E; base += (int64_t)gridDim.x * 256) {
     const int64_t e = base + threadIdx.x;
     if (e < E) {
@@ -158,6 +164,9 @@ struct KnnWs {
   int64_t* mat_off;          // [B+1] word offsets (device copy)
   int64_t* ecount;           // [B] edges per image (pemp_knn_graph_build)
   int64_t* edge_off;         // [B+1] exclusive scan of ecount; [B] = the batch's edge total
+  unsigned long long* arow;  // fast path: A (the k+1 nearest of each node), 8 words per node
+  unsigned long long* rows;  // fast path: R = A | A^T, 8 words per node
+  int* rowstart;             // LDS path: degree prefix of each row inside its image
 };
 
 static size_t knn_words(const int64_t* node_off_host, int B, int64_t* mat_off_host) {
@@ -180,6 +189,11 @@ static KnnWs knn_carve(void* base, const int64_t* node_off_host, int B, size_t* 
   k.mat_off = c.take<int64_t>(B + 1);
   k.ecount = c.take<int64_t>(B);
   k.edge_off = c.take<int64_t>(B + 1);
+  // LDS path (pemp_knn_graph_build, every n_b <= 512): rows at a fixed stride of 8 words per node
+  const int64_t nt = node_off_host[B];
+  k.arow = c.take<unsigned long long>((size_t)nt * 8);
+  k.rows = c.take<unsigned long long>((size_t)nt * 8);
+  k.rowstart = c.take<int>((size_t)nt);
   if (bytes) *bytes = c.used;
   return k;
 }
@@ -346,6 +360,228 @@ __global__ __launch_bounds__(1024) void knn_emit_kernel(const int64_t* __restric
   }
 }
 
+// ---- knn, fast path (every image with n <= KNN_LDS_MAXN nodes) ------------------------------
+// Three launches, no atomics in global memory and no memsets:
+//   knn_select_kernel: wave per query node i (all images at once), candidates j = lane + 64 r in
+//     registers, the k+1 nearest by squared integer distance with ties admitted lowest index first
+//     (the rule of knn_adj_kernel); the counts of the threshold search are ballots + popcounts (no
+//     cross-lane shuffles). Row i of A goes to global memory at a fixed stride of KNN_W words.
+//   knn_rows_kernel: one workgroup per image: A^T in LDS, R = A | A^T, each row's degree prefix inside
+//     its image, the image's edge count.
+//   knn_emit_rows_kernel: wave per row (below).
+constexpr int KNN_LDS_MAXN = 512, KNN_W = KNN_LDS_MAXN / 64;
+
+__device__ __forceinline__ int ballot_count(bool p) { return __popcll(__ballot(p)); }
+
+__global__ __launch_bounds__(1024) void knn_select_kernel(const int64_t* __restrict__ jdet,
+                                                          const int64_t* __restrict__ node_off, int B,
+                                                          int64_t n_total, int kq,
+                                                          unsigned long long* __restrict__ Arow) {
+  const int lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 6);
+  if (g >= n_total) return;
+  const int b = find_segment(node_off, B, g);
+  const int64_t base = node_off[b];
+  const int n = (int)(node_off[b + 1] - base), i = (int)(g - base);
+  const int wpr = (n + 63) / 64;
+  const int64_t xi = jdet[g * 3 + 0], yi = jdet[g * 3 + 1];
+  long long d[KNN_W];
+  long long dmax = 0;
+#pragma unroll
+  for (int r = 0; r < KNN_W; ++r) {
+    const int j = lane + 64 * r;
+    d[r] = 0x7fffffffffffffffll;
+    if (r < wpr && j < n) {
+      const long long dx = jdet[(base + j) * 3 + 0] - xi, dy = jdet[(base + j) * 3 + 1] - yi;
+      d[r] = dx * dx + dy * dy;
+      dmax = max(dmax, d[r]);
+    }
+  }
+  long long tau = 0x7fffffffffffffffll;
+  int need = 0;   // n <= kq: every node is among the k+1 nearest
+  if (n > kq) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) dmax = max(dmax, (long long)__shfl_xor(dmax, off));
+    long long lo = 0, hi = dmax;   // smallest tau with #{d <= tau} >= kq
+    while (lo < hi) {
+      const long long mid = lo + (hi - lo) / 2;
+      int c = 0;
+      for (int r = 0; r < wpr; ++r) c += ballot_count(d[r] <= mid);
+      if (c >= kq) hi = mid; else lo = mid + 1;
+    }
+    tau = lo;
+    int less = 0;
+    for (int r = 0; r < wpr; ++r) less += ballot_count(d[r] < tau);
+    need = kq - less;
+  }
+  int ties_before = 0;   // ties at lower indices (j = lane + 64 r: r-major, then lane)
+  for (int r = 0; r < wpr; ++r) {
+    const int j = lane + 64 * r;
+    bool take = j < n && d[r] <= tau;
+    if (n > kq) {
+      const unsigned long long tm = __ballot(d[r] == tau);
+      const int rank = ties_before + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(tm >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((unsigned)tm, 0u));
+      if (d[r] == tau) take = rank < need;
+      ties_before += __popcll(tm);
+    }
+    const unsigned long long word = __ballot(take && j != i);
+    if (lane == 0) Arow[g * KNN_W + r] = word;
+  }
+}
+
+__global__ __launch_bounds__(1024) void knn_rows_kernel(const int64_t* __restrict__ node_off,
+                                                        const unsigned long long* __restrict__ Arow,
+                                                        unsigned long long* __restrict__ R, int* __restrict__ rowstart,
+                                                        int64_t* __restrict__ ecount) {
+  __shared__ unsigned long long T[KNN_LDS_MAXN * KNN_W];
+  __shared__ int wsum[16];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t base = node_off[b];
+  const int n = (int)(node_off[b + 1] - base);
+  const int wpr = (n + 63) / 64;
+  for (int t = tid; t < n * KNN_W; t += 1024) T[t] = 0ull;
+  __syncthreads();
+  for (int t = tid; t < n * wpr; t += 1024) {   // T[j] |= bit i for every j in A[i]
+    const int i = t / wpr, w = t - i * wpr;
+    unsigned long long word = Arow[(base + i) * KNN_W + w];
+    while (word) {
+      const int j = 64 * w + __builtin_ctzll(word);
+      word &= word - 1;
+      atomicOr(&T[j * KNN_W + (i >> 6)], 1ull << (i & 63));
+    }
+  }
+  __syncthreads();
+  int deg = 0;
+  if (tid < n) {
+    for (int w = 0; w < wpr; ++w) {
+      const unsigned long long v = Arow[(base + tid) * KNN_W + w] | T[tid * KNN_W + w];
+      R[(base + tid) * KNN_W + w] = v;
+      deg += __popcll(v);
+    }
+  }
+  int x = deg;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(x, off);
+    if (lane >= off) x += o;
+  }
+  if (lane == 63) wsum[wave] = x;
+  __syncthreads();
+  int pre = 0;
+  for (int w = 0; w < wave; ++w) pre += wsum[w];
+  if (tid < n) rowstart[base + tid] = pre + x - deg;
+  if (tid == 1023) ecount[b] = pre + x;
+}
+
+// Wave per row: the row's edges (src = the row, dst ascending) at image base + row prefix; the
+// destination row of edge_index starts at the batch total. With edge_attr != NULL the wave also writes
+// the edges' features (edge_features_kernel's values), staged in LDS so that each word's edges leave
+// as one contiguous range. Block (0, 0) publishes the total (edge_off[B], the mapped host word).
+struct KnnEmitArgs {
+  const int64_t* node_off;
+  int B;
+  const unsigned long long* R;
+  const int* rowstart;
+  const int64_t* ecount;
+  int64_t e_cap;
+  int64_t* edge_off;
+  int* e_host;
+  int64_t* ei;
+  // edge features (ConstructGraph.py:289-357)
+  const int64_t* jdet;
+  const float* jtag;
+  int F;
+  const float* jsc;
+  int J, mode, A;
+  float norm;
+  float* edge_attr;
+};
+
+__global__ __launch_bounds__(1024) void knn_emit_rows_kernel(KnnEmitArgs k) {
+  __shared__ long long red[2][16];
+  __shared__ float fdx[16][64], fdy[16][64], faux[16][64];
+  __shared__ int fts[16][64], ftd[16][64];
+  __shared__ int nx[KNN_LDS_MAXN], ny[KNN_LDS_MAXN], nt[KNN_LDS_MAXN];   // the image's nodes (features)
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, B = k.B;
+  long long before = 0, all = 0;
+  for (int q = tid; q < B; q += 1024) {
+    const long long e = k.ecount[q];
+    all += e;
+    if (q < b) before += e;
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    before += __shfl_xor(before, off);
+    all += __shfl_xor(all, off);
+  }
+  if (lane == 0) { red[0][wave] = before; red[1][wave] = all; }
+  __syncthreads();
+  before = 0; all = 0;
+  for (int w = 0; w < 16; ++w) { before += red[0][w]; all += red[1][w]; }
+  if (b == 0 && blockIdx.y == 0 && tid == 0) {
+    k.edge_off[B] = all;
+    if (k.e_host) __hip_atomic_store(k.e_host, (int)(all < 0x7fffffffll ? all : 0x7fffffffll), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (all > k.e_cap) return;   // reported by the host
+  const int64_t base = k.node_off[b];
+  const int n = (int)(k.node_off[b + 1] - base);
+  if (k.edge_attr) {   // (uniform) node coordinates and types once per block
+    for (int t = tid; t < n; t += 1024) {
+      nx[t] = (int)k.jdet[(base + t) * 3];
+      ny[t] = (int)k.jdet[(base + t) * 3 + 1];
+      nt[t] = (int)k.jdet[(base + t) * 3 + 2];
+    }
+    __syncthreads();
+  }
+  const int a = blockIdx.y * 16 + wave;
+  if (a >= n) return;
+  const int wpr = (n + 63) / 64;
+  const int64_t src = base + a;
+  int64_t pos = before + k.rowstart[src];
+  int64_t sx = 0, sy = 0;
+  int ts = 0;
+  float tsrc = 0.f;
+  if (k.edge_attr) { sx = nx[a]; sy = ny[a]; ts = nt[a]; }
+  for (int w = 0; w < wpr; ++w) {
+    const unsigned long long word = k.R[src * KNN_W + w];
+    const int cnt = __popcll(word);
+    const int r = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(word >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)word, 0u));
+    const bool has = (word >> lane) & 1ull;
+    const int64_t dst = base + 64 * w + lane;
+    if (has) {
+      k.ei[pos + r] = src;
+      k.ei[all + pos + r] = dst;
+    }
+    if (k.edge_attr) {   // (uniform)
+      if (has) {
+        const int jl = 64 * w + lane;
+        const int64_t dx = nx[jl], dy = ny[jl];
+        fdx[wave][r] = (float)(dx - sx) / k.norm;             // ConstructGraph.py:311-317 (IEEE division)
+        fdy[wave][r] = (float)(dy - sy) / k.norm;
+        fts[wave][r] = ts;
+        ftd[wave][r] = nt[jl];
+        if (k.mode == PEMP_EF_POSITION_ANGLE_CONNECTION) faux[wave][r] = edge_theta(sx, sy, dx, dy);
+        else if (ef_uses_tags(k.mode))
+          faux[wave][r] = ae_term(k.mode, tag_distance(k.jtag + src * k.F, k.jtag + dst * k.F, k.F), k.jsc[src]);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      float* o = k.edge_attr + pos * k.A;
+      for (int q = lane; q < cnt * k.A; q += 64) {
+        const int el = q / k.A, f = q - el * k.A;
+        o[q] = ef_value(k.mode, f, k.J, fdx[wave][el], fdy[wave][el], faux[wave][el], fts[wave][el], ftd[wave][el]);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    pos += cnt;
+  }
+}
+
 // edge_off = exclusive scan of ecount, edge_off[B] = total; the total also goes straight into the
 // caller's mapped host word (system-scope store), like pemp_detect's counts
 __global__ __launch_bounds__(64) void knn_offsets_kernel(const int64_t* __restrict__ ecount, int B,
@@ -427,13 +663,16 @@ __global__ __launch_bounds__(256) void fused_fully_graph_kernel(FusedGraphArgs a
   __shared__ long long noff[FUSED_MAXB + 1], eoff[FUSED_MAXB + 1];
   __shared__ float dx_s[256], dy_s[256], aux_s[256];
   __shared__ int ts_s[256], td_s[256];
+  __shared__ int over_cap;
   const int B = a.B;
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     long long cn = 0, ce = 0;
+    int over = 0;
     for (int c0 = 0; c0 < B; c0 += 64) {
       const int b = c0 + lane;
       const long long n = b < B ? a.n_det[b] : 0, e = n * (n > 0 ? n - 1 : 0);
+      over |= n > a.cap;   // an image with more detections than the detection buffer holds
       long long xn = n, xe = e;
 #pragma unroll
       for (int off = 1; off < 64; off <<= 1) {
@@ -444,14 +683,16 @@ __global__ __launch_bounds__(256) void fused_fully_graph_kernel(FusedGraphArgs a
       cn += __shfl(xn, 63);
       ce += __shfl(xe, 63);
     }
-    if (lane == 0) { noff[B] = cn; eoff[B] = ce; }
+    over = __any(over);
+    if (lane == 0) { noff[B] = cn; eoff[B] = ce; over_cap = over; }
   }
   __syncthreads();
   // capacity mode (launched before the host has read the counts back): device totals; a batch that
-  // does not fit writes nothing and the host rebuilds it with exact sizes
+  // does not fit (totals over the capacities, or an image over the detection cap: its detections past
+  // the cap were never written) writes nothing and the host rebuilds it with exact sizes
   const int64_t n_total = a.capacity ? (int64_t)noff[B] : a.n_total;
   const int64_t e_total = a.capacity ? (int64_t)eoff[B] : a.e_total;
-  if (a.capacity && (n_total > a.n_total || e_total > a.e_total)) return;
+  if (a.capacity && (n_total > a.n_total || e_total > a.e_total || over_cap)) return;
   if (a.node_off_out && blockIdx.x == 0)   // per-image node offsets for pemp_mpn_forward_fully
     for (int i = threadIdx.x; i <= B; i += blockDim.x) a.node_off_out[i] = noff[i];
   auto seg = [&](const long long* off, long long v) {
@@ -683,7 +924,7 @@ __global__ __launch_bounds__(256) void gather_projected_kernel(ProjMaps m, int C
       const float v = __fadd_rn(__fmul_rn(t0, ly0), __fmul_rn(t1, ly1));
       acc = s == 0 ? v : __fadd_rn(acc, v);
     }
-    x[idx] = __fdiv_rn(acc, divisor);
+    x[idx] = div_rn(acc, divisor);
   }
 }
 
@@ -891,9 +1132,19 @@ extern "C" int pemp_knn_graph_emit(const int64_t* node_off, const int64_t* node_
 // graph is its leading [2, E] block (source row at 0, destination row at E).
 extern "C" int pemp_knn_graph_build(const int64_t* joint_det, const int64_t* node_off, const int64_t* node_off_host,
                                     int B, int k, void* workspace, size_t workspace_bytes, int64_t e_cap,
-                                    int64_t* edge_buf, int32_t* e_total_host, void* stream) {
+                                    int64_t* edge_buf, int32_t* e_total_host, const float* joint_tags, int F,
+                                    const float* joint_scores, int J, float norm_factor, int mode, float* edge_attr,
+                                    void* stream) {
   PEMP_CHECK_ARG(joint_det && node_off && node_off_host && workspace && edge_buf && B > 0 && k >= 1 && e_cap >= 0,
                  "pemp_knn_graph_build: bad args");
+  int A = 0;
+  if (edge_attr) {
+    PEMP_CHECK_ARG(J > 0, "pemp_knn_graph_build: J <= 0");
+    A = ef_width(mode, J);
+    if (A < 0) { set_error("pemp_knn_graph_build: unknown mode %d", mode); return PEMP_ERR_INVALID_ARG; }
+    if (const int rc = ef_tag_check(mode, joint_tags, F, "pemp_knn_graph_build")) return rc;
+    PEMP_CHECK_ARG(mode != PEMP_EF_AE_NORMED || joint_scores, "pemp_knn_graph_build: ae_normed needs joint_scores");
+  }
   size_t need = 0;
   knn_carve(nullptr, node_off_host, B, &need);
   if (workspace_bytes < need) {
@@ -911,6 +1162,25 @@ extern "C" int pemp_knn_graph_build(const int64_t* joint_det, const int64_t* nod
   const hipStream_t st = as_stream(stream);
   int* e_dev_host = nullptr;   // device address of the caller's mapped host word
   if (e_total_host) PEMP_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&e_dev_host), e_total_host, 0));
+  int64_t nmax = 0;
+  for (int b = 0; b < B; ++b) nmax = std::max<int64_t>(nmax, node_off_host[b + 1] - node_off_host[b]);
+  if (nmax <= KNN_LDS_MAXN) {   // three launches: selection, rows, emit
+    ProfScope prof("knn_build", st);
+    const int64_t n_all = node_off_host[B];
+    if (n_all > 0) {
+      hipLaunchKernelGGL(knn_select_kernel, dim3((unsigned)((n_all + 15) / 16)), dim3(1024), 0, st, joint_det, node_off,
+                         B, n_all, k + 1, w.arow);
+      PEMP_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(knn_rows_kernel, dim3(B), dim3(1024), 0, st, node_off, w.arow, w.rows, w.rowstart, w.ecount);
+    PEMP_LAUNCH_CHECK();
+    KnnEmitArgs ka{node_off, B, w.rows, w.rowstart, w.ecount, e_cap, w.edge_off, e_dev_host, edge_buf,
+                   joint_det, joint_tags, F, joint_scores, J, mode, A, norm_factor, edge_attr};
+    hipLaunchKernelGGL(knn_emit_rows_kernel, dim3(B, (unsigned)std::max<int64_t>(1, (nmax + 15) / 16)), dim3(1024), 0,
+                       st, ka);
+    PEMP_LAUNCH_CHECK();
+    return PEMP_OK;
+  }
   const size_t words = knn_words(node_off_host, B, nullptr);
   hipLaunchKernelGGL(knn_matoff_kernel, dim3(1), dim3(64), 0, st, node_off, B, w.mat_off);
   PEMP_LAUNCH_CHECK();
@@ -933,6 +1203,12 @@ extern "C" int pemp_knn_graph_build(const int64_t* joint_det, const int64_t* nod
     hipLaunchKernelGGL(knn_emit_kernel, dim3(B), dim3(1024), 0, st, node_off, B, w.mat_off, w.adj, w.adjt,
                        w.edge_off, (int64_t)-1, e_cap, edge_buf);
     PEMP_LAUNCH_CHECK();
+    if (edge_attr) {
+      // edge_index's destination row starts at the device-side total: the features kernel reads it too
+      hipLaunchKernelGGL(edge_features_kernel, dim3(grid_for(e_cap, 256)), dim3(256), 0, st, joint_det, joint_tags, F,
+                         joint_scores, edge_buf, e_cap, J, norm_factor, mode, A, edge_attr, w.edge_off + B);
+      PEMP_LAUNCH_CHECK();
+    }
   }
   return PEMP_OK;
 }

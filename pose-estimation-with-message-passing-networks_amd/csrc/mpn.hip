@@ -800,16 +800,42 @@ __device__ __forceinline__ void layer_lds_p(const uint16_t* __restrict__ W, int 
   }
 }
 
-// edge_attr row of the tile's edge (lane column c): features 16 mb + 4 g + r < A
-__device__ __forceinline__ void load_edge_attr(const float* __restrict__ ea, int A, int64_t o, float (&x)[4][4]) {
+// ---- buffer-resource memory ops of the edge pass: a per-array SGPR descriptor and 32-bit lane offsets
+// (no 64-bit per-lane pointers to keep live across the tile loop; reads past the array end return 0)
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+constexpr int RSRC_DW3 = 0x00020000;   // raw buffer, gfx950
+// (32-bit size: a 64-bit clamp here makes hipcc treat the descriptor as divergent and wrap every access
+// in a readfirstlane waterfall loop; the host keeps the arrays below 2^31 bytes)
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, RSRC_DW3);
+}
+__device__ __forceinline__ float4 bld4(rsrc_t rs, int voff, int soff = 0) {
+  const u32x4v v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+__device__ __forceinline__ int bld1(rsrc_t rs, int voff) { return (int)__builtin_amdgcn_raw_buffer_load_b32(rs, voff, 0, 0); }
+constexpr int OOB_VOFF = (int)0x80000000u;   // buffer offset past every descriptor's size: store dropped
+__device__ __forceinline__ void bst4(rsrc_t rs, int voff, float a, float b, float c, float d) {
+  const u32x4v v = {__float_as_uint(a), __float_as_uint(b), __float_as_uint(c), __float_as_uint(d)};
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, 0, 0);
+}
+
+// edge_attr row of the tile's edge (lane column c): features 16 mb + 4 g + r < A. Every load is
+// unconditional (clamped column; the value masked afterwards) so that all of them issue back to back
+// under one wait -- a guard per element (or per block) made the compiler wait for each one.
+__device__ __forceinline__ void load_edge_attr(rsrc_t rs_ea, int A, int o, float (&x)[4][4]) {
   const int g = __lane_id() >> 4;
+  const int row = o * A * 4;   // byte offset of the row (32-bit: the host keeps E * A * 4 < 2^31)
+  float v[4][4];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int f = 16 * mb + 4 * g + r;
-      x[mb][r] = f < A ? ea[o * A + f] : 0.0f;
-    }
+    for (int r = 0; r < 4; ++r) v[mb][r] = __int_as_float(bld1(rs_ea, row + 4 * min(16 * mb + 4 * g + r, A - 1)));
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) x[mb][r] = 16 * mb + 4 * g + r < A ? v[mb][r] : 0.0f;
 }
 
 // embedding MLP then the Q0 layer on one tile: in x = edge_attr; out x = e_init, y = Q0 (+ b1)
@@ -839,6 +865,80 @@ __device__ __forceinline__ void embed_tile(const float* smz, const EmbedLayout& 
   }
 }
 
+// The published edge embedding ([J+2 <= 32] -> 32 -> 64 -> 64 -> 64, then Q0 64 -> 64) with the block
+// counts known at compile time: straight-line layers (the runtime-shaped loop above keeps its loop state,
+// per-layer guards and LDS offsets live and spilled). Split precisions only.
+template <int PREC, int KB32, int OB>
+__device__ __forceinline__ void layer_fixed(const float* smz, const EmbedLayout& Lo, int l, const float (&in)[4][4],
+                                            float (&out)[4][4]) {
+  const uint16_t* W = reinterpret_cast<const uint16_t*>(smz + Lo.w_off[l]);
+  const float* bias = smz + Lo.b_off[l];
+  const int ldw = Lo.stride[l], relu = Lo.relu[l];
+  const int lane = __lane_id(), i = lane & 15, g = lane >> 4;
+  bf16x8_t hb[2], lb[2];
+  f16x8_t hh[2], lh[2];
+  float s_in = 1.0f, s_out = 1.0f;
+  if (PREC == 1) {
+    split_bf16(in, hb, lb);
+  } else {
+    const bool big = split_f16(in, 1.0f, hh, lh);
+    s_in = big ? 2048.0f * F16_DOWN : 2048.0f;
+    s_out = big ? F16_UP / 2048.0f : 1.0f / 2048.0f;
+  }
+  constexpr int lo_off = 32 * KB32;
+#pragma unroll
+  for (int ob = 0; ob < 4; ++ob) {
+    if (ob < OB) {
+      const float4 bb = ld4(bias + 16 * ob + 4 * g);
+      f32x4 c = {bb.x * s_in, bb.y * s_in, bb.z * s_in, bb.w * s_in};
+#pragma unroll
+      for (int kb = 0; kb < KB32; ++kb) {
+        const int o = (16 * ob + i) * ldw + 32 * kb + 8 * g;
+        if (PREC == 1) {
+          const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(W + o);
+          const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(W + o + lo_off);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, hb[kb], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, lb[kb], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, hb[kb], c, 0, 0, 0);
+        } else {
+          const f16x8_t ah = *reinterpret_cast<const f16x8_t*>(W + o);
+          const f16x8_t al = *reinterpret_cast<const f16x8_t*>(W + o + lo_off);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, hh[kb], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, lh[kb], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, hh[kb], c, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = c[r] * s_out;
+        out[ob][r] = relu ? fmaxf(v, 0.0f) : v;
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[ob][r] = 0.0f;
+    }
+  }
+}
+
+template <int PREC>
+__device__ __forceinline__ void embed_tile_fixed(const float* smz, const EmbedLayout& Lo, float (&x)[4][4],
+                                                 float (&y)[4][4]) {
+  layer_fixed<PREC, 1, 2>(smz, Lo, 0, x, y);   // A -> 32
+  layer_fixed<PREC, 1, 4>(smz, Lo, 1, y, x);   // 32 -> 64
+  layer_fixed<PREC, 2, 4>(smz, Lo, 2, x, y);   // 64 -> 64
+  layer_fixed<PREC, 2, 4>(smz, Lo, 3, y, x);   // 64 -> 64  (e_init in x)
+  layer_fixed<PREC, 2, 4>(smz, Lo, 4, x, y);   // Q0 = W1_e_init e_init + b1
+}
+
+// the layout embed_tile_fixed assumes
+static bool embed_fixed_shape(const EmbedLayout& L) {
+  static const int kb[5] = {1, 1, 2, 2, 2}, ob[5] = {2, 4, 4, 4, 4};
+  if (L.prec == PEMP_PREC_FP32 || L.n != 4) return false;
+  for (int l = 0; l < 5; ++l)
+    if (L.kb[l] != kb[l] || L.ob[l] != ob[l]) return false;
+  return true;
+}
+
 // Stage one 64x64 edge-pass matrix into LDS (PREC 0: fp32 rows of LDW; PREC 1: interleaved bf16)
 template <int PREC>
 __device__ __forceinline__ void stage_tile64(float* dst, const float* w32, int64_t ld32, const uint16_t* wbf) {
@@ -861,7 +961,7 @@ __device__ __forceinline__ void stage_tile64(float* dst, const float* w32, int64
 // Q0 = W1_e_init·e_init + b1 and R0 = Q0 + W1_e_cur·e_init (the first pass's layer-1 input).
 // One 16-wave workgroup per CU, weights staged once in LDS; a wave walks an equal share of the
 // sorted positions in 16-edge tiles.
-template <int PREC>
+template <int PREC, bool FIXED>
 __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp emb, EmbedLayout Lo,
                                                                      const uint16_t* __restrict__ emb_bf,
                                                                      const float* __restrict__ ea, int A,
@@ -898,34 +998,36 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp em
   }
   __syncthreads();
   const int64_t gw = (int64_t)blockIdx.x * EDGE_WAVES + wave, nw = (int64_t)gridDim.x * EDGE_WAVES;
-  const int64_t first = E * gw / nw, end = E * (gw + 1) / nw;
-  for (int64_t base = first; base < end; base += 16) {
+  const int first = __builtin_amdgcn_readfirstlane((int)(E * gw / nw));
+  const int end = __builtin_amdgcn_readfirstlane((int)(E * (gw + 1) / nw));
+  // buffer descriptors + 32-bit offsets: no 64-bit lane pointers live across the tile loop
+  const rsrc_t rs_ea = make_rsrc(ea, (int)E * A * 4), rs_orig = make_rsrc(s_orig, (int)E * 4);
+  const rsrc_t rs_q0 = make_rsrc(q0, (int)E * 256), rs_r0 = make_rsrc(r0, (int)E * 256);
+  for (int base = first; base < end; base += 16) {
     int z = 0;
     asm volatile("" : "+s"(z));                  // keep the LDS fragment reads inside the loop
     const float* smz = sm + z;
-    const int64_t p = base + c;
+    const int p = base + c;
     const bool valid = p < end;
-    const int64_t o = s_orig[valid ? p : end - 1];
+    const int o = bld1(rs_orig, 4 * (valid ? p : end - 1));
     float x[4][4], y[4][4];
-    load_edge_attr(ea, A, o, x);
-    embed_tile<PREC>(smz, Lo, x, y);              // x = e_init, y = Q0 (true values)
+    load_edge_attr(rs_ea, A, o, x);
+    if constexpr (FIXED) embed_tile_fixed<PREC>(smz, Lo, x, y);   // x = e_init, y = Q0 (true values)
+    else embed_tile<PREC>(smz, Lo, x, y);
     if (PREC == 2) {                              // Q0 and R0 are kept in the f16x3 domain (x 2^11)
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
         for (int r = 0; r < 4; ++r) y[ob][r] *= dom<PREC>();
     }
-    if (valid) {
+    const int vo = valid ? p * 256 + 16 * g : OOB_VOFF;   // masked lanes: stores dropped
 #pragma unroll
-      for (int ob = 0; ob < 4; ++ob) st4(q0 + p * D + 16 * ob + 4 * g, y[ob][0], y[ob][1], y[ob][2], y[ob][3]);
-    }
+    for (int ob = 0; ob < 4; ++ob) bst4(rs_q0, vo + 64 * ob, y[ob][0], y[ob][1], y[ob][2], y[ob][3]);
     Frag<PREC> fx;
     prep_true<PREC>(x, fx);
     gemm_f<PREC, 4>(smz + Lo.total, x, fx, y);    // R0 = Q0 + W1_e_cur · e_init
-    if (valid) {
 #pragma unroll
-      for (int ob = 0; ob < 4; ++ob) st4(r0 + p * D + 16 * ob + 4 * g, y[ob][0], y[ob][1], y[ob][2], y[ob][3]);
-    }
+    for (int ob = 0; ob < 4; ++ob) bst4(rs_r0, vo + 64 * ob, y[ob][0], y[ob][1], y[ob][2], y[ob][3]);
   }
 }
 
@@ -1185,26 +1287,6 @@ __device__ __forceinline__ void dma16(const float* g, float* l) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
 
-// ---- buffer-resource memory ops of the edge pass: a per-array SGPR descriptor and 32-bit lane offsets
-// (no 64-bit per-lane pointers to keep live across the tile loop; reads past the array end return 0)
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-constexpr int RSRC_DW3 = 0x00020000;   // raw buffer, gfx950
-// (32-bit size: a 64-bit clamp here makes hipcc treat the descriptor as divergent and wrap every access
-// in a readfirstlane waterfall loop; the host keeps the arrays below 2^31 bytes)
-__device__ __forceinline__ rsrc_t make_rsrc(const void* p, int bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, RSRC_DW3);
-}
-__device__ __forceinline__ float4 bld4(rsrc_t rs, int voff, int soff = 0) {
-  const u32x4v v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0);
-  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
-}
-__device__ __forceinline__ int bld1(rsrc_t rs, int voff) { return (int)__builtin_amdgcn_raw_buffer_load_b32(rs, voff, 0, 0); }
-__device__ __forceinline__ void bst4(rsrc_t rs, int voff, float a, float b, float c, float d) {
-  const u32x4v v = {__float_as_uint(a), __float_as_uint(b), __float_as_uint(c), __float_as_uint(d)};
-  __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, 0, 0);
-}
-
 // LDS-DMA of the r rows of one 16-edge tile (sorted positions base .. base + 15; rows past the array
 // read 0, rows past the wave's range are loaded and ignored) into a 4 KB buffer: instruction i moves
 // rows 4i .. 4i+3, LDS row rho holding global row base + rho with its 16-byte chunks XOR-permuted by
@@ -1255,7 +1337,6 @@ template <int N>
 __device__ __forceinline__ void dma_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
-constexpr int OOB_VOFF = (int)0x80000000u;   // buffer offset past every descriptor's size: store dropped
 
 template <int AGG, int HEAD, int PREC, int UPD, int STAGE>
 __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(EdgeStepArgs a) {
@@ -2636,18 +2717,22 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
     if (emb_lds) {
       const int grid = (int)std::min<int64_t>(num_cus(), (E + 16 * EDGE_WAVES - 1) / (16 * EDGE_WAVES));
       const size_t lds = (size_t)(emb_lo.total + D * LDW) * sizeof(float);
-      if (emb_prec == PEMP_PREC_F16X3)
-        hipLaunchKernelGGL(edge_embed_kernel<2>, dim3(grid), dim3(64 * EDGE_WAVES), lds, st, w->edge_emb, emb_lo,
+      const bool fixed = embed_fixed_shape(emb_lo);
+#define PEMP_EMBED_LAUNCH(P, FX)                                                                                   \
+  hipLaunchKernelGGL((edge_embed_kernel<P, FX>), dim3(grid), dim3(64 * EDGE_WAVES), lds, st, w->edge_emb, emb_lo,  \
+                     w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, w->e1_bf, \
+                     ws.EA, ws.Q0)
+      if (emb_prec == PEMP_PREC_F16X3) {
+        if (fixed) PEMP_EMBED_LAUNCH(2, true);
+        else PEMP_EMBED_LAUNCH(2, false);
+      } else if (emb_prec == PEMP_PREC_BF16X3) {
+        if (fixed) PEMP_EMBED_LAUNCH(1, true);
+        else PEMP_EMBED_LAUNCH(1, false);
+      } else
+        hipLaunchKernelGGL((edge_embed_kernel<0, false>), dim3(grid), dim3(64 * EDGE_WAVES), lds, st, w->edge_emb, emb_lo,
                            w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, w->e1_bf,
                            ws.EA, ws.Q0);
-      else if (emb_prec == PEMP_PREC_BF16X3)
-        hipLaunchKernelGGL(edge_embed_kernel<1>, dim3(grid), dim3(64 * EDGE_WAVES), lds, st, w->edge_emb, emb_lo,
-                           w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, w->e1_bf,
-                           ws.EA, ws.Q0);
-      else
-        hipLaunchKernelGGL(edge_embed_kernel<0>, dim3(grid), dim3(64 * EDGE_WAVES), lds, st, w->edge_emb, emb_lo,
-                           w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, w->e1_bf,
-                           ws.EA, ws.Q0);
+#undef PEMP_EMBED_LAUNCH
     } else {
       hipLaunchKernelGGL(edge_embed_wide_kernel, dim3((unsigned)((E + 63) / 64)), dim3(256), 0, st, w->edge_emb,
                          edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, ws.EA, ws.Q0,

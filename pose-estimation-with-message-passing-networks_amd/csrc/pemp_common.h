@@ -8,6 +8,11 @@
 
 namespace pemp {
 
+// Correctly rounded fp32 division (HIP's `/` is IEEE-correct by default and never contracted; ocml
+// has no __fdiv_rn under OCML_BASIC_ROUNDED_OPERATIONS, see the Makefile)
+__device__ __forceinline__ float div_rn(float a, float b) { return a / b; }
+
+
 // ---- error reporting (thread-local last error, returned through pemp_last_error) ----
 void set_error(const char* fmt, ...);
 

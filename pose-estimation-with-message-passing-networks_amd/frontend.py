@@ -41,3 +41,112 @@ class ProjectedMaps:
             p = torch.nn.functional.interpolate(m.float(), size=self.size, mode="bilinear", align_corners=False)
             acc = p if acc is None else acc + p
         return acc / self.divisor
+
+
+class ProjectedHeatmaps:
+    """The test front-end's heatmaps and tag maps at the image size, never materialised
+    (``PoseEstimation.py:329-452`` ``_get_multi_stage_outputs`` with ``FLIP_TEST`` and ``PROJECT2IMAGE``,
+    ``multi_scales_testing.py:144-195`` ``aggregate_results_mpn``, ``PoseEstimation.py:227-229``).
+
+    Pass it as BOTH ``scoremaps=`` and ``tagmaps=`` of ``get_graph_constructor``: detection then evaluates
+    ``s = (sum_s (up(out_s) + up(flip(flip_out_s))[flip_index]) / 2) / divisor`` inside its NMS loads
+    (``pemp_detect_projected``) and the joint tags are sampled at the detections
+    (``pemp_gather_projected_tags``): nothing of size [B, J, H, W] is written.
+
+    outputs: list over scales of [B, C, h_s, w_s] network outputs of the forward pass (heatmaps in channels
+    0..J-1, per-joint tags in J..2J-1 when tags are used); flip_outputs: the flipped-image pass as the
+    network produced it (same shapes, not un-flipped) or None; flip_index: the FLIP_CONFIG permutation;
+    size: (H, W); tag_scale: index of the scale whose tags are kept (the reference keeps scale 1.0).
+    Scales in the reference's order (descending scale factor)."""
+
+    def __init__(self, outputs, size, num_joints, flip_outputs=None, flip_index=None, divisor=None, tag_scale=0):
+        if isinstance(outputs, torch.Tensor):
+            outputs = [outputs]
+        outputs = [o.float().contiguous() for o in outputs]
+        if not outputs or len(outputs) > 4:
+            raise ValueError("ProjectedHeatmaps: 1 to 4 scales")
+        if flip_outputs is not None:
+            if isinstance(flip_outputs, torch.Tensor):
+                flip_outputs = [flip_outputs]
+            flip_outputs = [o.float().contiguous() for o in flip_outputs]
+            if len(flip_outputs) != len(outputs) or any(a.shape != b.shape for a, b in zip(outputs, flip_outputs)):
+                raise ValueError("ProjectedHeatmaps: flip_outputs must match outputs scale by scale")
+        B, C = outputs[0].shape[:2]
+        J = int(num_joints)
+        for o in outputs:
+            if o.dim() != 4 or o.shape[0] != B or o.shape[1] != C:
+                raise ValueError("ProjectedHeatmaps: every output is [B, C, h, w] with the same B and C")
+        if C < J:
+            raise ValueError(f"ProjectedHeatmaps: {C} channels < {J} joints")
+        self.outputs, self.flip_outputs = outputs, flip_outputs
+        self.num_joints = J
+        self.size = (int(size[0]), int(size[1]))
+        self.divisor = float(len(outputs) if divisor is None else divisor)
+        self.tag_scale = int(tag_scale)
+        self.device = outputs[0].device
+        fi = list(range(J)) if flip_index is None else [int(v) for v in flip_index]
+        if sorted(fi) != list(range(J)):
+            raise ValueError("ProjectedHeatmaps: flip_index must be a permutation of the joints")
+        self.flip_index = torch.tensor(fi, dtype=torch.int32, device=self.device)
+        self.shape = torch.Size([B, J, self.size[0], self.size[1]])
+        self.dtype = torch.float32
+        self.has_tags = C >= 2 * J
+        self.tag_dims = 2 if flip_outputs is not None else 1
+
+    def to(self, device):
+        return ProjectedHeatmaps([o.to(device) for o in self.outputs], self.size, self.num_joints,
+                                 None if self.flip_outputs is None else [o.to(device) for o in self.flip_outputs],
+                                 self.flip_index.tolist(), self.divisor, self.tag_scale)
+
+    def _interp(self, m):
+        return torch.nn.functional.interpolate(m, size=self.size, mode="bilinear", align_corners=False)
+
+    def materialize(self):
+        """The reference's dense tensors, computed by its own torch ops (for refine / adjust and checks):
+        (scoremaps [B, J, H, W], tags [B, J, H, W, F] or None)."""
+        J, fi = self.num_joints, self.flip_index.long()
+        acc = None
+        for s, o in enumerate(self.outputs):
+            h = self._interp(o[:, :J])
+            if self.flip_outputs is not None:
+                hf = self._interp(torch.flip(self.flip_outputs[s], [3])[:, :J][:, fi])
+                h = (h + hf) / 2.0
+            acc = h if acc is None else acc + h
+        scoremaps = acc / self.divisor
+        tags = None
+        if self.has_tags:
+            o = self.outputs[self.tag_scale]
+            tl = [self._interp(o[:, J:2 * J]).unsqueeze(4)]
+            if self.flip_outputs is not None:
+                f = torch.flip(self.flip_outputs[self.tag_scale], [3])[:, J:2 * J][:, fi]
+                tl.append(self._interp(f).unsqueeze(4))
+            tags = torch.cat(tl, dim=4)
+        return scoremaps, tags
+
+    def project(self):
+        """The image-size maps materialised on the device by the library (pemp_project_maps), with the
+        values the detection samples: (scoremaps [B, J, H, W], tags [B, J, H, W, F] or None)."""
+        from . import _lib
+        L = _lib.lib()
+        B, J, (H, W) = self.outputs[0].shape[0], self.num_joints, self.size
+        s = torch.empty(B, J, H, W, dtype=torch.float32, device=self.device)
+        t = torch.empty(self.tag_dims, B, J, H, W, dtype=torch.float32, device=self.device) if self.has_tags else None
+        c = self.c_struct()
+        import ctypes
+        _lib.check(L.pemp_project_maps(ctypes.addressof(c), B, J, H, W, self.tag_scale, s.data_ptr(),
+                                       None if t is None else t.data_ptr(), _lib.stream(self.device)))
+        return s, None if t is None else t.permute(1, 2, 3, 4, 0).contiguous()
+
+    def c_struct(self):
+        """pemp_proj_maps for the C-ABI (keeps the tensors alive through self)."""
+        from . import _lib
+        s = _lib.PempProjMaps()
+        s.num_scales = len(self.outputs)
+        s.channels = self.outputs[0].shape[1]
+        for i, o in enumerate(self.outputs):
+            s.maps[i] = o.data_ptr()
+            s.flip_maps[i] = self.flip_outputs[i].data_ptr() if self.flip_outputs is not None else None
+            s.h[i], s.w[i] = o.shape[2], o.shape[3]
+        s.flip_index = self.flip_index.data_ptr()
+        s.divisor = self.divisor
+        return s

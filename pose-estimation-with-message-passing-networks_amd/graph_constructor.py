@@ -14,7 +14,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .frontend import ProjectedMaps
+from .frontend import ProjectedHeatmaps, ProjectedMaps
 
 _SCORE_BASED_K = 75        # ConstructGraph.py:280 (score_based_graph roots)
 _EF_MODES = {
@@ -119,9 +119,14 @@ class NaiveGraphConstructor:
         L = _lib.lib()
         st = _lib.stream(self.device)
         sm = self.scoremaps
-        if sm.dtype != torch.float32:
-            sm = sm.float()
-        sm = sm.contiguous()
+        if isinstance(sm, ProjectedHeatmaps):   # the test front-end evaluated inside the detection
+            self._proj = sm
+            self._proj_c = sm.c_struct()
+        else:
+            self._proj = None
+            if sm.dtype != torch.float32:
+                sm = sm.float()
+            sm = sm.contiguous()
         B, J, H, W = sm.shape
         if J != self.num_joints:
             raise ValueError(f"scoremaps have {J} types, num_joints={self.num_joints}")
@@ -158,9 +163,9 @@ class NaiveGraphConstructor:
     def _construct(self, L, st, sm, masks, B, J, H, W, use_thr, topk, thr, dev, ws, cap, det, dsc, n_det,
                    counts_h):
         counts_h.fill(-1)
-        _lib.check(L.pemp_detect(_lib.ptr(sm), _lib.ptr(masks), B, J, H, W, self.pool_kernel_size, thr, int(use_thr),
-                                 topk, 3, _lib.ptr(ws), ws.numel(), _lib.ptr(det), _lib.ptr(dsc), _lib.ptr(n_det),
-                                 cap, counts_h.ctypes.data, st))
+        _lib.check(self._detect(L)(self._detect_src(sm), _lib.ptr(masks), B, J, H, W, self.pool_kernel_size, thr,
+                                   int(use_thr), topk, 3, _lib.ptr(ws), ws.numel(), _lib.ptr(det), _lib.ptr(dsc),
+                                   _lib.ptr(n_det), cap, counts_h.ctypes.data, st))
         # host-side preparation of the graph stage, while the detection kernels run
         feats = self.features
         projected = isinstance(feats, ProjectedMaps)
@@ -176,7 +181,13 @@ class NaiveGraphConstructor:
             feats = feats.contiguous()
             C = feats.shape[1]
         tags = self.tagmaps
-        if tags is not None:
+        proj_tags = None
+        if isinstance(tags, ProjectedHeatmaps):   # sampled at the detections after the build
+            if not tags.has_tags:
+                raise ValueError(f"ProjectedHeatmaps has {tags.outputs[0].shape[1]} channels: no tag channels")
+            proj_tags, tags = tags, None
+            F = proj_tags.tag_dims
+        elif tags is not None:
             tags = tags.float().contiguous()
             F = 1 if tags.dim() == 4 else int(np.prod(tags.shape[4:]))
         else:
@@ -184,12 +195,13 @@ class NaiveGraphConstructor:
         mode = _EF_MODES.get(frozenset(self.edge_features_to_use))
         if mode is None:
             raise NotImplementedError(f"EDGE_FEATURES_TO_USE={self.edge_features_to_use}")
-        if mode in _EF_TAG_MODES and tags is None:
+        if mode in _EF_TAG_MODES and tags is None and proj_tags is None:
             raise TypeError(f"EDGE_FEATURES_TO_USE={self.edge_features_to_use} needs tagmaps")
         A = {0: J + 2, 1: J, 2: 1, 3: 2, 4: J + 3, 5: J + 3, 6: 1, 7: 1, 8: 1}[mode]
         norm = float(max(W, H)) if self.normalize_node_distance else 1.0
 
-        fully = self.mpn_graph_type == "fully" and B <= 1024
+        # (projected tags feeding the edge features: the generic path, which samples them before the features)
+        fully = self.mpn_graph_type == "fully" and B <= 1024 and not (proj_tags is not None and mode in _EF_TAG_MODES)
         gkey = (B, J, H, W, C, F, A, dev)
         with NaiveGraphConstructor._mu:
             hint = NaiveGraphConstructor._graph_hint.get(gkey) if fully else None
@@ -221,9 +233,9 @@ class NaiveGraphConstructor:
                 NaiveGraphConstructor._cap = max(NaiveGraphConstructor._cap, cap)
             det = torch.empty(B, cap, 3, dtype=torch.int64, device=dev)
             dsc = torch.empty(B, cap, dtype=torch.float32, device=dev)
-            _lib.check(L.pemp_detect(_lib.ptr(sm), _lib.ptr(masks), B, J, H, W, self.pool_kernel_size, thr,
-                                     int(use_thr), topk, 2, _lib.ptr(ws), ws.numel(), _lib.ptr(det), _lib.ptr(dsc),
-                                     _lib.ptr(n_det), cap, None, st))
+            _lib.check(self._detect(L)(self._detect_src(sm), _lib.ptr(masks), B, J, H, W, self.pool_kernel_size, thr,
+                                       int(use_thr), topk, 2, _lib.ptr(ws), ws.numel(), _lib.ptr(det), _lib.ptr(dsc),
+                                       _lib.ptr(n_det), cap, None, st))
         N = sum(counts_l)
         E_fully = sum(c * (c - 1) for c in counts_l if c > 1)
         if fully:   # capacities for the next batch of this shape: 25 % headroom over this one
@@ -242,6 +254,8 @@ class NaiveGraphConstructor:
                 self._gather_projected(L, st, pmaps, H, W, joint_det, batch_index, x)
             if tags is not None:
                 joint_tags = joint_tags.view((N,) + tuple(tags.shape[4:])) if tags.dim() > 4 else joint_tags.view(N)
+            if proj_tags is not None:
+                joint_tags = self._gather_proj_tags(L, st, proj_tags, J, H, W, joint_det, batch_index, N, dev)
             _tag_fully(edge_index, built[7], counts_l, joint_det)
             return (x, edge_attr, edge_index, None, None, None, None, joint_det, None, None, None, joint_scores,
                     batch_index, None, joint_tags)
@@ -274,18 +288,42 @@ class NaiveGraphConstructor:
             _lib.check(L.pemp_pack_nodes(_lib.ptr(feats), C, _lib.ptr(tags), F, B, J, H, W, _lib.ptr(det),
                                          _lib.ptr(dsc), cap, _lib.ptr(node_off), N, _lib.ptr(x), _lib.ptr(joint_det),
                                          _lib.ptr(joint_scores), _lib.ptr(batch_index), _lib.ptr(joint_tags), st))
-            edge_index = self._edges(L, st, joint_det, joint_scores, node_off, fully_off, node_off_h, B, dev)
-            E = edge_index.shape[1]
-            edge_attr = torch.empty(E, A, dtype=torch.float32, device=dev)
-            _lib.check(L.pemp_edge_features(_lib.ptr(joint_det), _lib.ptr(joint_tags), F, _lib.ptr(joint_scores),
-                                            _lib.ptr(edge_index), E, J, norm, mode,
-                                            _lib.ptr(edge_attr), st))
+            if proj_tags is not None:   # before the edge features, which may read them
+                joint_tags = self._gather_proj_tags(L, st, proj_tags, J, H, W, joint_det, batch_index, N, dev)
+            if self.mpn_graph_type == "knn":   # edge features written by the knn emit itself
+                edge_index, edge_attr = self._knn_edges(L, st, joint_det, joint_tags, F, joint_scores, node_off,
+                                                        node_off_h, B, J, A, norm, mode, dev)
+            else:
+                edge_index = self._edges(L, st, joint_det, joint_scores, node_off, fully_off, node_off_h, B, dev)
+                E = edge_index.shape[1]
+                edge_attr = torch.empty(E, A, dtype=torch.float32, device=dev)
+                _lib.check(L.pemp_edge_features(_lib.ptr(joint_det), _lib.ptr(joint_tags), F, _lib.ptr(joint_scores),
+                                                _lib.ptr(edge_index), E, J, norm, mode,
+                                                _lib.ptr(edge_attr), st))
         if projected:
             self._gather_projected(L, st, pmaps, H, W, joint_det, batch_index, x)
         if tags is not None:
             joint_tags = joint_tags.view((N,) + tuple(tags.shape[4:])) if tags.dim() > 4 else joint_tags.view(N)
+        if proj_tags is not None and fully:
+            joint_tags = self._gather_proj_tags(L, st, proj_tags, J, H, W, joint_det, batch_index, N, dev)
         return (x, edge_attr, edge_index, None, None, None, None, joint_det, None, None, None, joint_scores,
                 batch_index, None, joint_tags)
+
+    def _detect(self, L):
+        return L.pemp_detect_projected if self._proj is not None else L.pemp_detect
+
+    def _detect_src(self, sm):
+        return ctypes.addressof(self._proj_c) if self._proj is not None else _lib.ptr(sm)
+
+    def _gather_proj_tags(self, L, st, pt, J, H, W, joint_det, batch_index, N, dev):
+        """joint_tags [N, F] from the projected tag channels (pemp_gather_projected_tags); the reference's
+        tagmaps there are [B, J, H, W, F] (torch.cat(tags_list, dim=4)), so F = 1 stays [N, 1]."""
+        F = pt.tag_dims
+        jt = torch.empty(N, F, dtype=torch.float32, device=dev)
+        c = pt.c_struct()
+        _lib.check(L.pemp_gather_projected_tags(ctypes.addressof(c), pt.tag_scale, J, H, W, _lib.ptr(joint_det),
+                                                _lib.ptr(batch_index), N, _lib.ptr(jt), st))
+        return jt
 
     def _gather_projected(self, L, st, pmaps, H, W, joint_det, batch_index, x):
         S = len(pmaps)
@@ -301,8 +339,6 @@ class NaiveGraphConstructor:
         counts = np.diff(node_off_h)
         if self.mpn_graph_type == "fully":
             per = counts * np.maximum(counts - 1, 0)
-        elif self.mpn_graph_type == "knn":
-            return self._knn_edges(L, st, joint_det, node_off, node_off_h, counts, B, dev)
         elif self.mpn_graph_type == "score_based":
             k = _SCORE_BASED_K
             if counts.size and counts.min() < k:   # the reference's joint_scores.topk(k) raises
@@ -325,23 +361,27 @@ class NaiveGraphConstructor:
 
     _KNN_K = 50   # ConstructGraph.py:365 (knn_graph(k=50))
 
-    def _knn_edges(self, L, st, joint_det, node_off, node_off_h, counts, B, dev):
-        """knn_mpn_graph (ConstructGraph.py:363-368) in one queued call (pemp_knn_graph_build): the
-        buffer is sized by the closed-form bound, the total comes back through mapped memory while the
-        emit still runs, and the graph is the buffer's leading contiguous [2, E] block."""
+    def _knn_edges(self, L, st, joint_det, joint_tags, F, joint_scores, node_off, node_off_h, B, J, A, norm, mode,
+                   dev):
+        """knn_mpn_graph (ConstructGraph.py:363-368) + the edge features in one queued call
+        (pemp_knn_graph_build): buffers sized by the closed-form edge bound, the total back through
+        mapped memory while the emit still runs; edge_index / edge_attr are the leading contiguous
+        [2, E] / [E, A] blocks of those buffers."""
         k = self._KNN_K
         nh = np.ascontiguousarray(node_off_h)
         nh_p = nh.ctypes.data_as(ctypes.c_void_p)
         ws = self._ws_knn.get(L.pemp_knn_workspace_size(nh_p, B), dev)
-        n = counts.astype(np.int64)
+        n = np.diff(nh)
         e_cap = int(np.minimum(n * np.maximum(n - 1, 0), 2 * k * n).sum())
         buf = torch.empty(2 * max(e_cap, 1), dtype=torch.int64, device=dev)
+        ea = torch.empty(max(e_cap, 1) * A, dtype=torch.float32, device=dev)
         ent = self._host_counts_take(L, dev, 1)
         try:
             word = ent[2][:1]
             word.fill(-1)
             _lib.check(L.pemp_knn_graph_build(_lib.ptr(joint_det), _lib.ptr(node_off), nh_p, B, k, _lib.ptr(ws),
-                                              ws.numel(), e_cap, _lib.ptr(buf), ent[1], st))
+                                              ws.numel(), e_cap, _lib.ptr(buf), ent[1], _lib.ptr(joint_tags), F,
+                                              _lib.ptr(joint_scores), J, norm, mode, _lib.ptr(ea), st))
             E = self._wait_counts(word, dev)[0]
         except BaseException:
             torch.cuda.current_stream(dev).synchronize()
@@ -350,4 +390,4 @@ class NaiveGraphConstructor:
         self._host_counts_give(dev, ent)
         if E > e_cap:
             raise RuntimeError(f"pemp_knn_graph_build: {E} edges > bound {e_cap}")
-        return buf[:2 * E].view(2, E)
+        return buf[:2 * E].view(2, E), ea[:E * A].view(E, A)

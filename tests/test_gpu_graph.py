@@ -44,6 +44,7 @@ CASES = [
     (8, 17, 640, 640, 9, "clean", "knn", 5, 0.1, False),        # C3 shape, published knn (N ~ 150 > k + 1)
     (1, 14, 640, 640, 36, "clean", "fully", 5, 0.1, False),     # C5 shape (CrowdPose-dense)
     (3, 17, 200, 328, 5, "noisy", "knn", 3, 0.1, True),         # ragged W, masks, knn
+    (2, 17, 320, 320, 40, "clean", "knn", 3, 0.1, False),       # knn with n > 512 (global-memory path)
     (2, 17, 96, 136, 1, "realistic", "fully", 5, 0.1, False),   # bilinear plateaus (4 equal maxima)
     (2, 17, 64, 64, 2, "noisy", "fully", 3, 2.0, False),        # DETECT_THRESHOLD > 1.5 branch
     (1, 17, 33, 17, 1, "clean", "fully", 7, 0.1, False),        # tiny, odd sizes
@@ -184,3 +185,81 @@ def test_reentrant_two_streams(graph):
     assert not errors, errors
     for s, out in enumerate(results):
         check(s % 2, out)
+
+
+@pytest.mark.parametrize("graph,persons", [("knn", 5), ("knn", 40)])
+@pytest.mark.parametrize("features", [["position", "angle", "connection_type"], ["ae_normed"],
+                                      ["position", "connection_type", "ae_normed"]])
+def test_knn_edge_feature_modes(graph, persons, features):
+    """The knn build writes edge_attr itself (LDS path, n <= 512) or through the device-total features
+    kernel (n > 512): every EDGE_FEATURES_TO_USE mode, tags with F = 2, bit-exact with the oracle --
+    except the angle column: theta = |acos(a_x * rsqrt(a_x^2 + a_y^2))| (ConstructGraph.py:319-321) goes
+    through the device acosf, within 2 ulp of torch CPU's (vectorised SLEEF u10 / libm) acos, which
+    itself differs between its vector and tail paths: parity at the last ulp is unpinned there."""
+    B, J, H, W = 2, 17, 192, 192
+    hm = torch.from_numpy(syn.make_heatmaps(11 + persons, B, J, H, W, persons, margin=4))
+    feats = torch.from_numpy(syn.closed_form((B, 128, H, W), 0.25))
+    tags = torch.from_numpy(syn.closed_form((B, J, H, W, 2), 0.75))
+    gc = pcfg.inference_gc_config(graph, 3, False)
+    gc.EDGE_FEATURES_TO_USE = features
+    out = run_gc(gc, J, hm, feats, tags, None)
+    ref = restate.construct_graph(hm, feats, tags, None, gc, J)
+    for i in (0, 2, 7, 11, 12, 14):
+        assert torch.equal(out[i].cpu(), ref[i]), i
+    ea, ra = out[1].cpu(), ref[1]
+    if "angle" in features:
+        np.testing.assert_array_max_ulp(ea[:, 2].numpy(), ra[:, 2].numpy(), maxulp=2)
+        ea, ra = torch.cat([ea[:, :2], ea[:, 3:]], 1), torch.cat([ra[:, :2], ra[:, 3:]], 1)
+    assert torch.equal(ea, ra)
+
+
+@pytest.mark.parametrize("sizes,size,flip", [([(80, 80)], (160, 160), True), ([(90, 70)], (160, 176), True),
+                                             ([(80, 80), (40, 40)], (160, 160), True), ([(80, 80)], (160, 160), False)])
+def test_projected_maps_materialize(sizes, size, flip):
+    """pemp_project_maps (the values the projected detection samples) against the oracle's fp32
+    restatement: bit-exact scoremaps and tags."""
+    from pemp_amd.frontend import ProjectedHeatmaps
+    from tests.test_frontend_cpu import COCO_FLIP, make_outputs
+    B, J = 2, 17
+    outs, flips = make_outputs(7, B, J, sizes, flip)
+    fi = COCO_FLIP if flip else None
+    ph = ProjectedHeatmaps([o.to(DEV) for o in outs], size, J, None if flips is None else [o.to(DEV) for o in flips],
+                           fi)
+    s, t = ph.project()
+    rs, rt = restate.project_frontend(outs, flips, size, J, fi)
+    bad = (s.cpu() != rs).nonzero()
+    assert bad.shape[0] == 0, (bad[:5].tolist(), s.cpu()[tuple(bad[0])].item(), rs[tuple(bad[0])].item())
+    assert torch.equal(t.cpu(), rt)
+
+
+@pytest.mark.parametrize("graph,sizes,size,flip,features", [
+    ("fully", [(80, 80)], (160, 160), True, ["position", "connection_type"]),
+    ("fully", [(90, 70)], (160, 176), True, ["position", "connection_type", "ae_normed"]),
+    ("knn", [(80, 80), (40, 40)], (160, 160), True, ["position", "connection_type"]),
+    ("fully", [(80, 80)], (160, 160), False, ["ae"]),
+])
+def test_projected_frontend(graph, sizes, size, flip, features):
+    """scoremaps = tagmaps = ProjectedHeatmaps: detection evaluates the flip-averaged,
+    upsampled (align_corners=False) and scale-averaged heatmaps inside its NMS loads and the tags are
+    sampled at the detections. Bit-exact with the oracle run on the maps its fp32 restatement
+    materialises (oracle/restate.project_frontend; that restatement is within 2e-6 of the reference's
+    torch ops, tests/test_frontend_cpu.py). Twice: the second call takes the capacity build."""
+    from pemp_amd.frontend import ProjectedHeatmaps
+    from tests.test_frontend_cpu import COCO_FLIP, make_outputs
+    B, J = 2, 17
+    outs, flips = make_outputs(7, B, J, sizes, flip)
+    fi = COCO_FLIP if flip else None
+    ph = ProjectedHeatmaps([o.to(DEV) for o in outs], size, J, None if flips is None else [o.to(DEV) for o in flips],
+                           fi)
+    s, t = restate.project_frontend(outs, flips, size, J, fi)
+    feats = torch.from_numpy(syn.closed_form((B, 128) + tuple(size), 0.25))
+    gc = pcfg.inference_gc_config(graph, 5, False)
+    gc.EDGE_FEATURES_TO_USE = features
+    ref = restate.construct_graph(s, feats, t, None, gc, J)
+    for _ in range(2):
+        out = pemp_amd.get_graph_constructor(gc, scoremaps=ph, features=feats.to(DEV), tagmaps=ph, joints_gt=None,
+                                             factor_list=None, masks=None, device=DEV, testing=True, heatmaps=None,
+                                             num_joints=J).construct_graph()
+        assert ref[7].shape[0] > 2 * J       # detections found
+        for i in (7, 11, 12, 14, 2, 0, 1):
+            assert torch.equal(out[i].cpu(), ref[i]), i

@@ -3,7 +3,7 @@
 # ("name:" alone = defaults). Prints value + per-kernel us. Extra bench args via $AB_ARGS.
 for spec in "$@"; do
   name=${spec%%:*}; envs=${spec#*:}
-  ( IFS=','; for kv in $envs; do [ -n "$kv" ] && export "$kv"; done
+  ( IFS=','; for kv in $envs; do [ -n "$kv" ] && export "$kv"; done; unset IFS
     timeout -k 10 150 python bench.py --no-cpu-baseline --steps 10 $AB_ARGS > gpurun_out/ab_$name.log 2>&1 ) \
     || { echo "$name failed"; tail -5 gpurun_out/ab_$name.log; exit 1; }
   python - "$name" <<'PY'
