@@ -31,10 +31,13 @@ namespace {
 #define NMS_PREFETCH 1
 #endif
 #ifndef NMS_XCD_MAP
-#define NMS_XCD_MAP 1
+#define NMS_XCD_MAP 1   // XCD-sliced unit windows (1.0x HBM fetch vs 1.5x without)
 #endif
 #ifndef NMS_PER_CU
 #define NMS_PER_CU 4
+#endif
+#ifndef NMS_CLAMPED_LOADS
+#define NMS_CLAMPED_LOADS 1
 #endif
 constexpr int SR = NMS_SR;  // rows per unit (= band height of the threshold bitmask)
 static_assert(SR <= 32, "column masks are at most 32-bit");
@@ -272,6 +275,27 @@ __device__ __forceinline__ void load_unit_proj(const ProjArgs& pj, const DetectG
   }
 }
 
+// rows y0 - P .. y0 + SR - 1 + P of the lane's column, rows and columns outside the plane CLAMPED to
+// the border: a window that reaches past the border always contains that border row / column, so the
+// duplicates leave every window maximum -- and with it MaxPool2d's -inf padding -- unchanged, and the
+// loads need no masks. One SGPR buffer descriptor per plane, the row offsets in SGPRs (soffset), the
+// lane's column as the only VGPR offset.
+template <int P>
+__device__ __forceinline__ void load_unit_clamped(const float* __restrict__ s, const DetectGeom& g, int u,
+                                                  float (&r)[SR + 2 * P]) {
+  const int lane = threadIdx.x & 63;
+  const int plane = u / g.units, rem = u - plane * g.units, band = rem / g.nsx, strip = rem - band * g.nsx;
+  const int y0 = band * SR, x = strip * g.sc - P + lane;
+  const int xo = min(max(x, 0), g.W - 1);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(s + (size_t)plane * g.H * g.W), 0, g.H * g.W * 4, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < SR + 2 * P; ++i) {
+    const int yc = min(max(y0 - P + i, 0), g.H - 1);
+    r[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, 4 * xo, yc * g.W * 4, 0));
+  }
+}
+
 // rows y0 - P .. y0 + SR - 1 + P of the lane's column; -inf outside the plane (MaxPool padding)
 template <int P>
 __device__ __forceinline__ void load_unit(const float* __restrict__ s, const DetectGeom& g, int u,
@@ -326,6 +350,7 @@ __global__ __launch_bounds__(NT1) void nms_strips_kernel(
   float r[SR + 2 * P];
   auto load = [&](int uu) {
     if constexpr (PROJ) load_unit_proj<P>(pj, g, uu, r);
+    else if constexpr (NMS_CLAMPED_LOADS) load_unit_clamped<P>(s, g, uu, r);
     else load_unit<P>(s, g, uu, r);
   };
   if (NMS_PREFETCH && u < u_hi) load(u);
@@ -356,10 +381,12 @@ __global__ __launch_bounds__(NT1) void nms_strips_kernel(
         const float t = fmaxf(vm[j], wave_shr1(vm[j]));
         vm[j] = fmaxf(t, wave_shl1(vm[j]));
       }
-    // per lane: threshold bits and non-negative bits over the unit's rows, the largest value
+    // per lane: threshold bits over the unit's rows (the column masks the emit reads); the unit's
+    // threshold / non-negative / positive counts from per-row ballots (scalar popcounts, no shuffles)
     float v[SR];
-    unsigned int tbits = 0, nnbits = 0;
-    float vmax_l = -INFINITY;
+    unsigned int tbits = 0;
+    int cnt = 0, nonneg = 0;
+    bool anypos = false;
     const int rows = min(SR, H - y0);
 #pragma unroll
     for (int j = 0; j < SR; ++j) {
@@ -368,19 +395,14 @@ __global__ __launch_bounds__(NT1) void nms_strips_kernel(
       const float vj = c[j] * jm;                       // ConstructGraph.py:1162-1165
       const bool ok = lane_ok && j < rows;
       v[j] = ok ? vj : NAN;
-      tbits |= (unsigned)(ok && !(vj < thr) && vj != 0.0f) << j;
-      nnbits |= (unsigned)(ok && vj >= 0.0f) << j;
-      vmax_l = fmaxf(vmax_l, v[j]);                     // NaN (invalid) is ignored by fmaxf
+      const bool tb = ok && !(vj < thr) && vj != 0.0f;
+      tbits |= (unsigned)tb << j;
+      cnt += __popcll(__ballot(tb));
+      nonneg += __popcll(__ballot(ok && vj >= 0.0f));
+      anypos = anypos || __ballot(ok && vj > 0.0f) != 0;
     }
-    if (!use_thr) tbits = 0;
+    if (!use_thr) { tbits = 0; cnt = 0; }
     cbits[(size_t)u * 64 + lane] = (cmask_t)tbits;
-    int cnt = __popc(tbits), nonneg = __popc(nnbits);
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      cnt += __shfl_xor(cnt, off);
-      nonneg += __shfl_xor(nonneg, off);
-    }
-    const bool anypos = __ballot(vmax_l > 0.0f) != 0;
     if (lane == 0) { tile_count[u] = cnt; tile_nonneg[u] = nonneg; }
     const int base_id = y0 * W + x;
     if (MODE == MODE_POS) {
@@ -889,7 +911,7 @@ static int detect_impl(const float* scoremaps, const ProjArgs* proj, const float
                  "pemp_detect: pool_kernel must be odd and <= %d (got %d)", 2 * MAXR + 1, pool_kernel);
   PEMP_CHECK_ARG(topk >= 1 && topk <= 32, "pemp_detect: topk must be in [1, 32] (got %d)", topk);
   PEMP_CHECK_ARG(cap >= 0, "pemp_detect: cap < 0");
-  PEMP_CHECK_ARG((size_t)H * W < 0x7fffffffull, "pemp_detect: plane too large");
+  PEMP_CHECK_ARG((size_t)H * W * 4 < 0x7fffffffull, "pemp_detect: plane too large (H * W * 4 >= 2^31)");
   const int K = topk < H * W ? topk : H * W;
   const DetectGeom g = geom(B, J, H, W, pool_kernel, K);
   PEMP_CHECK_ARG(g.nsx <= 64, "pemp_detect: W=%d too wide (max %d for pool_kernel %d)", W, 64 * g.sc, pool_kernel);

@@ -2666,9 +2666,8 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
     node_img = ws.img;
   }
 
-  // ---- edge embedding: fused into the first edge pass (STAGE_FIRST) when the first pass records
-  // no head and the embedding's LDS image fits next to the pass's weights; otherwise a separate
-  // launch writes Q0 and R0 = Q0 + W1_e_cur · e_init ----
+  // ---- edge embedding: its own launch writes Q0 and R0 = Q0 + W1_e_cur · e_init (edge_embed_kernel;
+  // the published shape takes the straight-line edge_embed_kernel<PREC, true>) ----
   int rc = 0;
   const int steps = desc->steps, aux = desc->aux_loss_steps;
   // U_t pre-applied in the edge pass (linear aggregations with an update MLP): the node update is a sum
