@@ -381,12 +381,11 @@ __global__ __launch_bounds__(NT1) void nms_strips_kernel(
         const float t = fmaxf(vm[j], wave_shr1(vm[j]));
         vm[j] = fmaxf(t, wave_shl1(vm[j]));
       }
-    // per lane: threshold bits over the unit's rows (the column masks the emit reads); the unit's
-    // threshold / non-negative / positive counts from per-row ballots (scalar popcounts, no shuffles)
+    // per lane: threshold bits and non-negative bits over the unit's rows, the largest value
+    // (per-row ballots + scalar popcounts for the counts measured slower: 91 vs 67 us)
     float v[SR];
-    unsigned int tbits = 0;
-    int cnt = 0, nonneg = 0;
-    bool anypos = false;
+    unsigned int tbits = 0, nnbits = 0;
+    float vmax_l = -INFINITY;
     const int rows = min(SR, H - y0);
 #pragma unroll
     for (int j = 0; j < SR; ++j) {
@@ -395,14 +394,19 @@ __global__ __launch_bounds__(NT1) void nms_strips_kernel(
       const float vj = c[j] * jm;                       // ConstructGraph.py:1162-1165
       const bool ok = lane_ok && j < rows;
       v[j] = ok ? vj : NAN;
-      const bool tb = ok && !(vj < thr) && vj != 0.0f;
-      tbits |= (unsigned)tb << j;
-      cnt += __popcll(__ballot(tb));
-      nonneg += __popcll(__ballot(ok && vj >= 0.0f));
-      anypos = anypos || __ballot(ok && vj > 0.0f) != 0;
+      tbits |= (unsigned)(ok && !(vj < thr) && vj != 0.0f) << j;
+      nnbits |= (unsigned)(ok && vj >= 0.0f) << j;
+      vmax_l = fmaxf(vmax_l, v[j]);                     // NaN (invalid) is ignored by fmaxf
     }
-    if (!use_thr) { tbits = 0; cnt = 0; }
+    if (!use_thr) tbits = 0;
     cbits[(size_t)u * 64 + lane] = (cmask_t)tbits;
+    int cnt = __popc(tbits), nonneg = __popc(nnbits);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      cnt += __shfl_xor(cnt, off);
+      nonneg += __shfl_xor(nonneg, off);
+    }
+    const bool anypos = __ballot(vmax_l > 0.0f) != 0;
     if (lane == 0) { tile_count[u] = cnt; tile_nonneg[u] = nonneg; }
     const int base_id = y0 * W + x;
     if (MODE == MODE_POS) {
