@@ -275,6 +275,94 @@ __device__ __forceinline__ void load_unit_proj(const ProjArgs& pj, const DetectG
   }
 }
 
+// The same rows, separably: per scale and map, the horizontal interpolation of every low-resolution row
+// the unit's output rows touch (at most PROJ_LR of them: upsampling) is computed once per lane -- its
+// loads issued in groups of 8 rows under one wait -- and staged in the wave's LDS rows; the vertical
+// interpolation of each output row then reads its two staged rows. The values are bitwise those of
+// proj_pixel (same operations on the same operands). Ratios needing more rows take load_unit_proj.
+constexpr int PROJ_LR = 16;
+
+// horizontal interpolation of rows lo .. lo + nr - 1 of both passes' maps (pl1 NULL: forward pass only)
+// into the wave's stage rows; 8 rows of both maps (32 loads) in flight per wait
+__device__ __forceinline__ void proj_rows_maps(const float* __restrict__ pl0, const float* __restrict__ pl1, int w,
+                                               int h, int lo, int nr, int x0, int x1, float lx0, float lx1,
+                                               float* __restrict__ st0, float* __restrict__ st1) {
+  const int lane = threadIdx.x & 63;
+  const int f0 = w - 1 - x0, f1 = w - 1 - x1;   // the flipped pass's mirrored columns
+#pragma unroll
+  for (int k0 = 0; k0 < PROJ_LR; k0 += 8) {
+    if (k0 < nr) {   // (uniform)
+      float a[8], b[8], c[8], d[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int row = min(lo + k0 + k, h - 1);   // rows past the range: loaded, never read
+        a[k] = pl0[row * w + x0];
+        b[k] = pl0[row * w + x1];
+        if (pl1) {
+          c[k] = pl1[row * w + f0];
+          d[k] = pl1[row * w + f1];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        st0[(k0 + k) * 64 + lane] = __fadd_rn(__fmul_rn(a[k], lx0), __fmul_rn(b[k], lx1));
+        if (pl1) st1[(k0 + k) * 64 + lane] = __fadd_rn(__fmul_rn(c[k], lx0), __fmul_rn(d[k], lx1));
+      }
+    }
+  }
+}
+
+// (the host checks that every unit's rows span at most PROJ_LR low-resolution rows: proj_sep_ok)
+template <int P>
+__device__ __forceinline__ void load_unit_proj_sep(const ProjArgs& pj, const DetectGeom& g, int u,
+                                                   float (&r)[SR + 2 * P], float* __restrict__ stage) {
+  const int lane = threadIdx.x & 63;
+  const int plane = u / g.units, rem = u - plane * g.units, band = rem / g.nsx, strip = rem - band * g.nsx;
+  const int b = plane / g.J, j = plane - b * g.J;
+  const int y0 = band * SR, x = strip * g.sc - P + lane;
+  const bool xok = x >= 0 && x < g.W;
+  const int xc = min(max(x, 0), g.W - 1);
+  const int ya = min(max(y0 - P, 0), g.H - 1), yb = min(max(y0 + SR + P - 1, 0), g.H - 1);
+  float* st0 = stage;                    // forward pass rows
+  float* st1 = stage + PROJ_LR * 64;     // flipped pass rows
+  for (int s = 0; s < pj.S; ++s) {
+    const int h = pj.h[s], w = pj.w[s];
+    const int lo = proj_taps(ya, g.H, h).i0, nr = proj_taps(yb, g.H, h).i1 - lo + 1;
+    const ProjTaps tx = proj_taps(xc, g.W, w);
+    const bool flip = pj.f[s] != nullptr;
+    __builtin_amdgcn_wave_barrier();   // the previous readers of the wave's rows are done
+    proj_rows_maps(pj.m[s] + ((size_t)b * pj.C + pj.ch0 + j) * h * w,
+                   flip ? pj.f[s] + ((size_t)b * pj.C + pj.ch0 + (pj.fi ? pj.fi[j] : j)) * h * w : nullptr, w, h, lo,
+                   nr, tx.i0, tx.i1, tx.l0, tx.l1, st0, st1);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // the rows' taps (uniform per row) computed once per unit by lanes 0 .. SR + 2P - 1 and read back as
+    // LDS broadcasts: (stage offsets of the two source rows, weights)
+    float4* tap = reinterpret_cast<float4*>(stage + 2 * PROJ_LR * 64);
+    if (lane < SR + 2 * P) {
+      const ProjTaps t = proj_taps(min(max(y0 - P + lane, 0), g.H - 1), g.H, h);
+      tap[lane] = make_float4(__int_as_float((t.i0 - lo) * 64), __int_as_float((t.i1 - lo) * 64), t.l0, t.l1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int i = 0; i < SR + 2 * P; ++i) {
+      const float4 t = tap[i];
+      const int o0 = __float_as_int(t.x) + lane, o1 = __float_as_int(t.y) + lane;
+      float v = __fadd_rn(__fmul_rn(st0[o0], t.z), __fmul_rn(st0[o1], t.w));
+      if (flip) v = __fmul_rn(__fadd_rn(v, __fadd_rn(__fmul_rn(st1[o0], t.z), __fmul_rn(st1[o1], t.w))), 0.5f);
+      r[i] = s == 0 ? v : __fadd_rn(r[i], v);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < SR + 2 * P; ++i) {
+    const int y = y0 - P + i;
+    r[i] = (xok && y >= 0 && y < g.H) ? div_rn(r[i], pj.divisor) : -INFINITY;
+  }
+}
+
 // rows y0 - P .. y0 + SR - 1 + P of the lane's column, rows and columns outside the plane CLAMPED to
 // the border: a window that reaches past the border always contains that border row / column, so the
 // duplicates leave every window maximum -- and with it MaxPool2d's -inf padding -- unchanged, and the
@@ -330,7 +418,7 @@ __device__ __forceinline__ void load_unit(const float* __restrict__ s, const Det
   }
 }
 
-template <int P, int MODE, bool MASKED, bool PROJ>
+template <int P, int MODE, bool MASKED, int PROJ>   // PROJ: 0 dense maps, 1 projected, 2 projected separable
 __global__ __launch_bounds__(NT1) void nms_strips_kernel(
     const float* __restrict__ s, const float* __restrict__ masks, DetectGeom g, float thr, int use_thr,
     float* __restrict__ cand_v, int* __restrict__ cand_i, float* __restrict__ neg_v, int* __restrict__ neg_i,
@@ -348,14 +436,21 @@ __global__ __launch_bounds__(NT1) void nms_strips_kernel(
   // the unit index is wave-uniform: keep it (and all address math derived from it) scalar
   int u = __builtin_amdgcn_readfirstlane(slot * (NT1 / 64) + (threadIdx.x >> 6));
   float r[SR + 2 * P];
+  __shared__ __attribute__((aligned(16))) float proj_stage[PROJ == 2 ? NT1 / 64 : 1]
+                                                          [PROJ == 2 ? 2 * PROJ_LR * 64 + 4 * (SR + 2 * MAXR) : 1];
   auto load = [&](int uu) {
-    if constexpr (PROJ) load_unit_proj<P>(pj, g, uu, r);
+    if constexpr (PROJ) {
+      if constexpr (PROJ == 2) load_unit_proj_sep<P>(pj, g, uu, r, proj_stage[threadIdx.x >> 6]);
+      else load_unit_proj<P>(pj, g, uu, r);
+    }
     else if constexpr (NMS_CLAMPED_LOADS) load_unit_clamped<P>(s, g, uu, r);
     else load_unit<P>(s, g, uu, r);
   };
-  if (NMS_PREFETCH && u < u_hi) load(u);
+  // (the projected loader computes its values as it loads: nothing to overlap, no prefetch)
+  constexpr bool PF = NMS_PREFETCH && PROJ == 0;
+  if (PF && u < u_hi) load(u);
   for (; u < u_hi; u += stride_u) {
-    if (!NMS_PREFETCH) load(u);
+    if (!PF) load(u);
     const int plane = u / g.units, rem = u - plane * g.units, band = rem / g.nsx, strip = rem - band * g.nsx;
     const int b = plane / g.J;
     const int y0 = band * SR, x = strip * g.sc - P + lane;
@@ -363,7 +458,7 @@ __global__ __launch_bounds__(NT1) void nms_strips_kernel(
     float cur[SR + 2 * P];
 #pragma unroll
     for (int i = 0; i < SR + 2 * P; ++i) cur[i] = r[i];
-    if (NMS_PREFETCH && u + stride_u < u_hi) load(u + stride_u);   // next unit's rows in flight
+    if (PF && u + stride_u < u_hi) load(u + stride_u);   // next unit's rows in flight
     float vm[SR], c[SR];
 #pragma unroll
     for (int j = 0; j < SR; ++j) {
@@ -764,24 +859,29 @@ __global__ __launch_bounds__(256) void emit_kernel(const float* __restrict__ s, 
   }
 }
 
-template <int P, int MODE, bool PROJ>
+template <int P, int MODE, int PROJ>
 static void launch_nms(const float* s, const float* masks, const DetectGeom& g, float thr, int use_thr,
                        const DetectWs& w, const ProjArgs& pj, hipStream_t st) {
   const int total = g.B * g.J * g.units;
   const int want = (total + NT1 / 64 - 1) / (NT1 / 64);
   // resident workgroups per CU: 4 (one wave per SIMD each) while the kernel fits 128 VGPRs (SR 16);
   // the 32-row units need ~190 VGPRs: 2
-  constexpr int per_cu = SR > 16 ? 2 : NMS_PER_CU;
-  const int grid = want < per_cu * num_cus() ? want : per_cu * num_cus();
-  if (masks)
-    hipLaunchKernelGGL((nms_strips_kernel<P, MODE, true, PROJ>), dim3(grid), dim3(NT1), 0, st, s, masks, g, thr,
-                       use_thr, w.cand_v, w.cand_i, w.neg_v, w.neg_i, w.tile_count, w.tile_nonneg, w.cbits, pj);
-  else
-    hipLaunchKernelGGL((nms_strips_kernel<P, MODE, false, PROJ>), dim3(grid), dim3(NT1), 0, st, s, masks, g, thr,
-                       use_thr, w.cand_v, w.cand_i, w.neg_v, w.neg_i, w.tile_count, w.tile_nonneg, w.cbits, pj);
+  // The grid-stride loop assumes every workgroup is resident: size the grid by the kernel's own occupancy
+  // (the projected loaders need ~140 VGPRs: 3 workgroups per CU, not 4; a fourth row of workgroups
+  // would only start once the first ones finish)
+  auto launch = [&](auto kern) {
+    int per_cu = SR > 16 ? 2 : NMS_PER_CU, occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, NT1, 0) == hipSuccess && occ > 0)
+      per_cu = std::min(per_cu, occ);
+    const int grid = want < per_cu * num_cus() ? want : per_cu * num_cus();
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NT1), 0, st, s, masks, g, thr, use_thr, w.cand_v, w.cand_i, w.neg_v,
+                       w.neg_i, w.tile_count, w.tile_nonneg, w.cbits, pj);
+  };
+  if (masks) launch(nms_strips_kernel<P, MODE, true, PROJ>);
+  else launch(nms_strips_kernel<P, MODE, false, PROJ>);
 }
 
-template <int MODE, bool PROJ>
+template <int MODE, int PROJ>
 static void dispatch_nms(const float* s, const float* masks, const DetectGeom& g, float thr, int use_thr,
                          const DetectWs& w, const ProjArgs& pj, hipStream_t st) {
   switch (g.p) {
@@ -793,18 +893,44 @@ static void dispatch_nms(const float* s, const float* masks, const DetectGeom& g
   }
 }
 
+// host restatement of proj_taps (same fp32 operations, round to nearest): does every unit's row span
+// fit the separable loader's PROJ_LR staged rows?
+static int proj_taps_host(int dst, int out_size, int in_size, bool upper) {
+  const float scale = (float)in_size / (float)out_size;
+  volatile float t = (float)dst + 0.5f;   // volatile: one rounded operation each, as on the device
+  volatile float m = scale * t;
+  float src = m - 0.5f;
+  if (src < 0.f) src = 0.f;
+  const int i0 = (int)src;
+  return upper ? i0 + (i0 < in_size - 1 ? 1 : 0) : i0;
+}
+
+static bool proj_sep_ok(const ProjArgs& pj, const DetectGeom& g) {
+  const int P = g.p;
+  for (int s = 0; s < pj.S; ++s)
+    for (int band = 0; band < g.nb; ++band) {
+      const int y0 = band * SR;
+      const int ya = std::min(std::max(y0 - P, 0), g.H - 1), yb = std::min(std::max(y0 + SR + P - 1, 0), g.H - 1);
+      if (proj_taps_host(yb, g.H, pj.h[s], true) - proj_taps_host(ya, g.H, pj.h[s], false) + 1 > PROJ_LR) return false;
+    }
+  return true;
+}
+
 template <int KMAX>
 static int launch_detect(const float* s, const float* masks, const DetectGeom& g, float thr, int use_thr,
                          int stages, const DetectWs& w, int64_t* det, float* scores, int32_t* n_det, int cap,
                          int32_t* n_host, const ProjArgs& pj, hipStream_t st) {
   if (stages & PEMP_DETECT_NMS) {
     ProfScope prof(pj.S ? "detect_nms_projected" : "detect_nms", st);
-    if (pj.S) {
-      if (use_thr) dispatch_nms<MODE_POS, true>(s, masks, g, thr, use_thr, w, pj, st);
-      else dispatch_nms<MODE_ALL, true>(s, masks, g, thr, use_thr, w, pj, st);
+    if (pj.S && proj_sep_ok(pj, g)) {
+      if (use_thr) dispatch_nms<MODE_POS, 2>(s, masks, g, thr, use_thr, w, pj, st);
+      else dispatch_nms<MODE_ALL, 2>(s, masks, g, thr, use_thr, w, pj, st);
+    } else if (pj.S) {
+      if (use_thr) dispatch_nms<MODE_POS, 1>(s, masks, g, thr, use_thr, w, pj, st);
+      else dispatch_nms<MODE_ALL, 1>(s, masks, g, thr, use_thr, w, pj, st);
     } else {
-      if (use_thr) dispatch_nms<MODE_POS, false>(s, masks, g, thr, use_thr, w, pj, st);
-      else dispatch_nms<MODE_ALL, false>(s, masks, g, thr, use_thr, w, pj, st);
+      if (use_thr) dispatch_nms<MODE_POS, 0>(s, masks, g, thr, use_thr, w, pj, st);
+      else dispatch_nms<MODE_ALL, 0>(s, masks, g, thr, use_thr, w, pj, st);
     }
     PEMP_LAUNCH_CHECK();
   }
