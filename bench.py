@@ -253,8 +253,33 @@ def frontend_projection(wl, gc, model, hm, tags, dev, out):
     st = _lib.prof_report()
     _lib.prof_enable(None)
     n, ms = st.get("gather_projected", (1, float("nan")))
+    # with the model's feature_gather Conv2d(32, 128, 3, 1, 1) in front (PoseEstimation.py:64-66, 341): the
+    # reference convolves the whole half-resolution backbone feature map, then projects it
+    raw = torch.randn(B, 32, H // 2, W // 2, device=dev)
+    conv = torch.nn.Conv2d(32, 128, 3, 1, 1, bias=True).to(dev).eval()
+    with torch.no_grad():
+        for it in range(reps + 1):
+            if it == 1:
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+            torch.nn.functional.interpolate(conv(raw), size=(H, W), mode="bilinear", align_corners=False)
+        torch.cuda.synchronize()
+    dense_conv_ms = (time.perf_counter() - t0) / reps * 1e3
+    pmc = pemp_amd.ProjectedMaps([raw], (H, W), gather=conv)
+    _lib.prof_enable("gather_projected_conv")
+    for _ in range(reps):
+        pemp_amd.get_graph_constructor(gc, scoremaps=hm, features=pmc, tagmaps=tags, joints_gt=None, factor_list=None,
+                                       masks=None, device=dev, testing=True, heatmaps=None,
+                                       num_joints=wl["J"]).construct_graph()
+    torch.cuda.synchronize()
+    st = _lib.prof_report()
+    _lib.prof_enable(None)
+    nc, msc = st.get("gather_projected_conv", (1, float("nan")))
     return {"dense_interpolate_ms": round(dense_ms, 3), "on_demand_gather_us": round(ms / n * 1e3, 2),
-            "dense_bytes_written": B * 128 * H * W * 4, "nodes": int(out[0].shape[0])}
+            "dense_bytes_written": B * 128 * H * W * 4, "nodes": int(out[0].shape[0]),
+            "feature_gather_conv": {"dense_conv_then_interpolate_ms": round(dense_conv_ms, 3),
+                                    "on_demand_conv_gather_us": round(msc / nc * 1e3, 2),
+                                    "conv": "Conv2d(32, 128, 3, 1, 1) on [B, 32, H/2, W/2]"}}
 
 
 def frontend_heatmaps(wl, gc, feats, dev, reps=5):

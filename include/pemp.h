@@ -21,6 +21,7 @@
  *   pemp_score_graph     ConstructGraph.py:405-422 score_based_graph (k = 75 roots)
  *   pemp_edge_features   ConstructGraph.py:289-359 (edge_attr)
  *   pemp_gather_projected  PoseEstimation.py:426-452 feature projection, sampled at the detections only
+ *   pemp_gather_projected_conv  the same with feature_gather (PoseEstimation.py:64-66, 341) at the taps only
  *   pemp_pose_*          Utils.py:499-514,672-743,1445-1455 pose grouping (pred_to_ann prefix, pred_to_person,
  *                        GAEC of correlation_clustering_utils.py:187-245, graph_cluster_to_persons)
  *   pemp_mpn_forward     Models/MessagePassingNetwork/NodeClassificationMPNSimple.py:62-97 with
@@ -36,7 +37,7 @@
 extern "C" {
 #endif
 
-#define PEMP_ABI_VERSION 12
+#define PEMP_ABI_VERSION 13
 
 enum {
   PEMP_OK = 0,
@@ -198,6 +199,17 @@ int pemp_knn_graph_build(const int64_t* joint_det, const int64_t* node_off, cons
 int pemp_gather_projected(const float* const* maps, const int* map_h, const int* map_w, int S, int C, int H, int W,
                           float divisor, const int64_t* joint_det, const int64_t* batch_index, int64_t N, float* x,
                           void* stream);
+/* The same with the model's feature_gather Conv2d applied before the projection (PoseEstimation.py:64-66
+ * nn.Conv2d(KP_OUTPUT_DIM, NODE_INPUT_DIM, FEATURE_GATHER_KERNEL, 1, FEATURE_GATHER_PADDING), applied per scale
+ * at :341 and projected at :426-452): x[n][co] = sum_s bilinear(conv_s[b_n][co], (y_n, x_n); H x W) / divisor,
+ * conv_s = bias + weight * maps[s] (stride 1, zero padding `pad`, output (h + 2 pad - k + 1) x (w + ...)),
+ * evaluated only at the 4 taps of each detection. maps: S device pointers to [B][Cin][h_s][w_s] fp32;
+ * weight_t: the Conv2d weight transposed to [Cin][k][k][Cout] (device fp32); bias: [Cout] or NULL.
+ * Cout <= 512, k <= 7, Cin (k+1)^2 floats <= 64 KB. */
+int pemp_gather_projected_conv(const float* const* maps, const int* map_h, const int* map_w, int S, int Cin,
+                               const float* weight_t, const float* bias, int Cout, int ksize, int pad, int H, int W,
+                               float divisor, const int64_t* joint_det, const int64_t* batch_index, int64_t N,
+                               float* x, void* stream);
 
 /* score_based graph per image (ConstructGraph.py:405-422 score_based_graph, k = 75 there): the k
  * highest-scoring nodes are roots (ties: lower node index; torch.topk leaves them unspecified);

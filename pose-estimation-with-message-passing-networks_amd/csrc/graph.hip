@@ -928,6 +928,68 @@ __global__ __launch_bounds__(256) void gather_projected_kernel(ProjMaps m, int C
   }
 }
 
+// The same projection with the model's feature_gather Conv2d in front of it (PoseEstimation.py:64-66, 341,
+// 426-452: interpolate(feature_gather(feat)) per scale): the conv output is needed only at the 4 bilinear taps
+// of each detection, so one workgroup per detection stages the (k+1) x (k+1) x Cin input patch under the taps
+// in LDS (zero padding outside the map) and each thread computes the 4 tap values of its output channels
+// (weights transposed on the host to [Cin][k][k][Cout]: one coalesced load per tap weight).
+constexpr int PCONV_THREADS = 128, PCONV_MAXQ = 4;   // Cout <= 512
+__global__ __launch_bounds__(PCONV_THREADS) void gather_projected_conv_kernel(
+    ProjMaps m, const float* __restrict__ wt, const float* __restrict__ bias, int Cin, int Cout, int k, int pad, int H,
+    int W, float divisor, const int64_t* __restrict__ jdet, const int64_t* __restrict__ bidx, float* __restrict__ x) {
+  extern __shared__ float patch[];   // [Cin][P][P]
+  const int P = k + 1, PP = P * P, tid = threadIdx.x;
+  const int64_t n = blockIdx.x;
+  const int px = (int)jdet[n * 3 + 0], py = (int)jdet[n * 3 + 1];
+  const int64_t b = bidx[n];
+  float acc[PCONV_MAXQ] = {0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < m.S; ++s) {
+    const int h = m.h[s], w = m.w[s], ho = h + 2 * pad - k + 1, wo = w + 2 * pad - k + 1;
+    int y0, y1, x0, x1;
+    float ly0, ly1, lx0, lx1;
+    proj_src(py, H, ho, y0, y1, ly0, ly1);
+    proj_src(px, W, wo, x0, x1, lx0, lx1);
+    const int dy1 = y1 - y0, dx1 = x1 - x0;
+    const float* f = m.p[s] + (size_t)b * Cin * h * w;
+    __syncthreads();   // the previous scale's patch is consumed
+    for (int i = tid; i < Cin * PP; i += PCONV_THREADS) {
+      const int ci = i / PP, r = (i - ci * PP) / P, q = i - ci * PP - r * P;
+      const int yy = y0 - pad + r, xx = x0 - pad + q;
+      patch[i] = (yy >= 0 && yy < h && xx >= 0 && xx < w) ? f[((size_t)ci * h + yy) * w + xx] : 0.0f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PCONV_MAXQ; ++q) {
+      const int co = tid + PCONV_THREADS * q;
+      if (co >= Cout) break;
+      float c00 = 0.f, c01 = 0.f, c10 = 0.f, c11 = 0.f;
+      const float* wp = wt + co;
+      for (int ci = 0; ci < Cin; ++ci)
+        for (int dy = 0; dy < k; ++dy) {
+          const float* pr = patch + ci * PP + dy * P;
+          for (int dx = 0; dx < k; ++dx, wp += Cout) {
+            const float wv = *wp;
+            c00 = fmaf(wv, pr[dx], c00);
+            c01 = fmaf(wv, pr[dx + dx1], c01);
+            c10 = fmaf(wv, pr[dx + dy1 * P], c10);
+            c11 = fmaf(wv, pr[dx + dy1 * P + dx1], c11);
+          }
+        }
+      const float bb = bias ? bias[co] : 0.0f;
+      c00 += bb; c01 += bb; c10 += bb; c11 += bb;
+      const float t0 = __fadd_rn(__fmul_rn(c00, lx0), __fmul_rn(c01, lx1));
+      const float t1 = __fadd_rn(__fmul_rn(c10, lx0), __fmul_rn(c11, lx1));
+      const float v = __fadd_rn(__fmul_rn(t0, ly0), __fmul_rn(t1, ly1));
+      acc[q] = s == 0 ? v : __fadd_rn(acc[q], v);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < PCONV_MAXQ; ++q) {
+    const int co = tid + PCONV_THREADS * q;
+    if (co < Cout) x[n * Cout + co] = div_rn(acc[q], divisor);
+  }
+}
+
 // ---- score_based_graph (ConstructGraph.py:405-422) -------------------------------------------
 // Roots are the k best-scoring nodes of an image (ties: lower node index). Edge (a, b), a != b,
 // exists iff a or b is a root, sorted by (a, b): a root row lists every other node, a non-root row
@@ -1271,6 +1333,37 @@ extern "C" int pemp_gather_projected(const float* const* maps, const int* map_h,
   ProfScope prof("gather_projected", as_stream(stream));
   hipLaunchKernelGGL(gather_projected_kernel, dim3(grid_for(N * C, 256, 4096)), dim3(256), 0, as_stream(stream), m, C,
                      H, W, divisor, joint_det, batch_index, N, x);
+  PEMP_LAUNCH_CHECK();
+  return PEMP_OK;
+}
+
+extern "C" int pemp_gather_projected_conv(const float* const* maps, const int* map_h, const int* map_w, int S, int Cin,
+                                          const float* weight_t, const float* bias, int Cout, int ksize, int pad, int H,
+                                          int W, float divisor, const int64_t* joint_det, const int64_t* batch_index,
+                                          int64_t N, float* x, void* stream) {
+  PEMP_CHECK_ARG(maps && map_h && map_w && S >= 1 && S <= PROJ_MAXS && Cin > 0 && H > 0 && W > 0 && N >= 0 &&
+                     divisor > 0.f && weight_t && Cout > 0 && Cout <= PCONV_THREADS * PCONV_MAXQ && ksize >= 1 &&
+                     ksize <= 7 && pad >= 0 && pad < ksize,
+                 "pemp_gather_projected_conv: bad args (S in [1, %d], Cout <= %d, k <= 7, 0 <= pad < k)", PROJ_MAXS,
+                 PCONV_THREADS * PCONV_MAXQ);
+  PEMP_CHECK_ARG((size_t)Cin * (ksize + 1) * (ksize + 1) * 4 <= 64 * 1024,
+                 "pemp_gather_projected_conv: Cin * (k+1)^2 patch exceeds 64 KB of LDS");
+  PEMP_CHECK_ARG(N == 0 || (joint_det && batch_index && x), "pemp_gather_projected_conv: null node arrays");
+  ProjMaps m{};
+  m.S = S;
+  for (int s = 0; s < S; ++s) {
+    PEMP_CHECK_ARG(maps[s] && map_h[s] + 2 * pad - ksize + 1 > 0 && map_w[s] + 2 * pad - ksize + 1 > 0,
+                   "pemp_gather_projected_conv: bad map %d (conv output empty)", s);
+    m.p[s] = maps[s];
+    m.h[s] = map_h[s];
+    m.w[s] = map_w[s];
+  }
+  if (N == 0) return PEMP_OK;
+  PEMP_CHECK_ARG(N < (1ll << 31), "pemp_gather_projected_conv: N exceeds the grid");
+  ProfScope prof("gather_projected_conv", as_stream(stream));
+  const size_t lds = (size_t)Cin * (ksize + 1) * (ksize + 1) * sizeof(float);
+  hipLaunchKernelGGL(gather_projected_conv_kernel, dim3((unsigned)N), dim3(PCONV_THREADS), lds, as_stream(stream), m,
+                     weight_t, bias, Cin, Cout, ksize, pad, H, W, divisor, joint_det, batch_index, x);
   PEMP_LAUNCH_CHECK();
   return PEMP_OK;
 }

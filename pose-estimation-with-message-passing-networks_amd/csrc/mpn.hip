@@ -1338,6 +1338,17 @@ __device__ __forceinline__ void dma_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+#ifndef PEMP_FAST_EXP
+#define PEMP_FAST_EXP 0
+#endif
+// softmax exponent: expf (correctly rounded to ~1 ulp) or the bare v_exp_f32 path (__expf)
+__device__ __forceinline__ float pemp_exp(float x) { return PEMP_FAST_EXP ? __expf(x) : expf(x); }
+#ifndef PEMP_XCD_MAP
+#define PEMP_XCD_MAP 1
+#endif
+#ifndef PEMP_EARLY_GATHER
+#define PEMP_EARLY_GATHER 1
+#endif
 template <int AGG, int HEAD, int PREC, int UPD, int STAGE>
 __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(EdgeStepArgs a) {
   constexpr int NW = edge_waves<HEAD>();
@@ -1356,7 +1367,12 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int T = a.T;
   EDGE_STAMP(0);
-  const int4 rg = a.ranges[blockIdx.x * NW + wave];
+  // XCD-aware placement: blocks b and b + 8 share an XCD (round-robin dispatch), so logical block
+  // (b % 8) * G/8 + b / 8 gives each XCD a contiguous run of logical blocks, i.e. few source types,
+  // and its L2 holds only those types' node-table columns
+  int lb = blockIdx.x;
+  if (PEMP_XCD_MAP && (gridDim.x & 7) == 0) lb = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  const int4 rg = a.ranges[lb * NW + wave];
   // wave-uniform by construction; readfirstlane tells hipcc (else the tile loop and every buffer access
   // downstream are compiled as divergent)
   const int first = __builtin_amdgcn_readfirstlane(rg.x), end = __builtin_amdgcn_readfirstlane(rg.y);
@@ -1366,7 +1382,30 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
   const rsrc_t rs_r = make_rsrc(a.r_cur, E * 256), rs_q = make_rsrc(a.Q0, E * 256);
   const rsrc_t rs_dst = make_rsrc(a.s_dst, E * 4), rs_src = make_rsrc(a.s_src, E * 4);
   const rsrc_t rs_nt = make_rsrc(a.NT, (int)a.N * a.t_nt_ld * 4);
-  // first two tiles' indices and the first tile's r rows in flight before the weight copy
+  const rsrc_t rs_orig = make_rsrc(a.s_orig, E * 4);
+  const int nt_row = a.t_nt_ld * 4;                  // bytes per node-table row
+  const int nt_p = (128 + 64 * t) * 4;               // byte offset of P_t in a row (SGPR soffset)
+  // a tile's gathers (PEMP_EARLY_GATHER: issued at the end of the previous tile, and for the first tile
+  // while the weight image is copied): node-table rows of target and source, Q0 rows, original ids
+  float4 xa[4], xb[4], xp[4], qq[4];
+  int orig_t = 0;
+  auto gather_nt = [&](int dstv, int srcv, bool on) {
+    const int va = on ? dstv * nt_row + 16 * g : OOB_VOFF, vb = on ? srcv * nt_row + 256 + 16 * g : OOB_VOFF;
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob) {
+      xa[ob] = bld4(rs_nt, va + 64 * ob);
+      xb[ob] = bld4(rs_nt, vb + 64 * ob);
+      xp[ob] = bld4(rs_nt, va + 64 * ob, nt_p);
+    }
+  };
+  auto gather_q = [&](int pbase, bool on) {
+    const int vq = on ? (pbase + c) * 256 + 16 * g : OOB_VOFF;
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob)
+      if (MID) qq[ob] = bld4(rs_q, vq + 64 * ob);
+  };
+  // first two tiles' indices, the first tile's r rows (and, early gathers, its Q0 rows) in flight before
+  // the weight copy
   int dst_n = 0, src_n = 0, dst_nn = 0, src_nn = 0;
   if (first < end) {   // (uniform)
     dst_n = bld1(rs_dst, 4 * min(first + c, end - 1));
@@ -1374,6 +1413,7 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
     dst_nn = bld1(rs_dst, 4 * min(first + 16 + c, end - 1));
     src_nn = bld1(rs_src, 4 * min(first + 16 + c, end - 1));
     dma_rows(rs_r, first, mybuf, lane);
+    if (PEMP_EARLY_GATHER) gather_q(first, true);
   }
   {
     // the block's type image: IMG_F floats, 1 KB per wave instruction, waves interleaved
@@ -1384,16 +1424,17 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
     if (TAIL && wave == NW - 1 && 4 * lane < TAIL)
       *reinterpret_cast<float4*>(&img[256 * PIECES + 4 * lane]) = ld4(src + 256 * PIECES + 4 * lane);
   }
+  if (PEMP_EARLY_GATHER && first < end) {
+    gather_nt(dst_n, src_n, true);
+    if (HEAD == 1) orig_t = bld1(rs_orig, 4 * min(first + c, end - 1));
+  }
   __syncthreads();
   EDGE_STAMP(1);
   EDGE_STAMP(2);
   if (first >= end) { EDGE_STAMP(15); return; }
   const float attn_b = vec[2 * D];
-  const int nt_row = a.t_nt_ld * 4;                  // bytes per node-table row
-  const int nt_p = (128 + 64 * t) * 4;               // byte offset of P_t in a row (SGPR soffset)
   const rsrc_t rs_next = make_rsrc(a.r_next, E * 256);
   const rsrc_t rs_agg = make_rsrc(a.agg, (int)a.N * T * 256);
-  const rsrc_t rs_orig = make_rsrc(a.s_orig, E * 4);
   const u32x4v_s rw_r = rsrc_words(a.r_cur, E * 256);
   // stores issued after a tile's DMA, all unconditional (masked lanes write past the buffer end): the
   // r_next rows (middle passes that write them) and the aggregate rows
@@ -1422,10 +1463,12 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
     const bool more = base + 16 < end;
     dst_n = dst_nn;
     src_n = src_nn;
-    // this tile's rows (DMA issued one tile ago) have landed
+    // this tile's rows (DMA issued one tile ago) have landed: the ops issued after that DMA are the
+    // tile's unconditional stores and (early gathers) this tile's gathers
+    constexpr int NG = PEMP_EARLY_GATHER ? 12 + (MID ? 4 : 0) + (HEAD == 1 ? 1 : 0) : 0;
     if (tile_no > 0) {
-      if (store_next) dma_wait<8>();
-      else dma_wait<4>();
+      if (store_next) dma_wait<8 + NG>();
+      else dma_wait<4 + NG>();
     }
     // this tile's r rows from the DMA buffer (row c, chunk (4 ob + g) ^ 4 (c & 3)); the lane terms are
     // re-derived from the opaque zero each tile (kept live across the loop they would be spilled)
@@ -1436,18 +1479,15 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob) rr[ob] = ld4(mybuf + (rowb ^ (16 * (ob ^ (cz & 3)))));
     }
-    // gathers of this tile (issued before the next tile's DMA): node-table rows of target and source,
-    // Q0 rows; then the indices two tiles ahead
-    float4 xa[4], xb[4], xp[4], qq[4];
-    const int va = dst * nt_row + 16 * g, vb = src * nt_row + 256 + 16 * g, vq = p * 256 + 16 * g;
-#pragma unroll
-    for (int ob = 0; ob < 4; ++ob) {
-      xa[ob] = bld4(rs_nt, va + 64 * ob);
-      xb[ob] = bld4(rs_nt, vb + 64 * ob);
-      xp[ob] = bld4(rs_nt, va + 64 * ob, nt_p);
-      if (MID) qq[ob] = bld4(rs_q, vq + 64 * ob);
+    // gathers of this tile (issued before the next tile's DMA, or already in flight); then the indices two
+    // tiles ahead
+    const int vq = p * 256 + 16 * g;
+    if (!PEMP_EARLY_GATHER) {
+      gather_nt(dst, src, true);
+      gather_q(base, true);
+      if (HEAD == 1) orig_t = bld1(rs_orig, 4 * min(p, end - 1));
     }
-    const int orig = HEAD == 1 ? bld1(rs_orig, 4 * min(p, end - 1)) : 0;
+    const int orig = orig_t;
     {
       const int qn = min(base + 32 + c, end - 1);
       dst_nn = bld1(rs_dst, 4 * qn);
@@ -1586,7 +1626,7 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
     if (AGG == PEMP_AGGR_ATTN) {
       M = seg_bcast_tail_max(seg_max(av, ck.d), ck.u);
       if (carry_in && ck.d == c) M = fmaxf(M, cM);   // head chunk continues the carried segment
-      pe = expf(av - M);
+      pe = pemp_exp(av - M);
       l = pe;
     }
     float v[4][4];
@@ -1596,7 +1636,7 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
       for (int r = 0; r < 4; ++r) v[ob][r] = (AGG == PEMP_AGGR_ATTN) ? pe * m[ob][r] : m[ob][r];
     if (carry_in && c == 0) {
       if (AGG == PEMP_AGGR_ATTN) {
-        const float f = expf(cM - M);
+        const float f = pemp_exp(cM - M);
         l += cl * f;
 #pragma unroll
         for (int ob = 0; ob < 4; ++ob)
@@ -1637,6 +1677,11 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
       const int vo = out ? (seg * T + t) * 256 + 16 * g : OOB_VOFF;
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob) bst4(rs_agg, vo + 64 * ob, v[ob][0] * inv, v[ob][1] * inv, v[ob][2] * inv, v[ob][3] * inv);
+    }
+    if (PEMP_EARLY_GATHER) {   // the next tile's gathers, unconditional (past the range: OOB offsets, no traffic)
+      gather_nt(dst_n, src_n, more);
+      gather_q(base + 16, more);
+      if (HEAD == 1) orig_t = bld1(rs_orig, 4 * min(p + 16, end - 1));
     }
 #ifdef PEMP_STAMPS
     asm volatile("" ::"v"(v[0][0]), "v"(v[3][3]));

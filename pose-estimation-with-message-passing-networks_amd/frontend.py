@@ -6,15 +6,19 @@ scale (``PoseEstimation.py:426-452``), summed over scales and divided by their c
 (``multi_scales_testing.py:182-190``, ``PoseEstimation.py:244``) -- and is accepted by
 ``get_graph_constructor(features=...)``. The graph constructor then interpolates the N detections
 only (``pemp_gather_projected``): at 640x640 that skips writing and re-reading a [128, H, W] fp32
-map (210 MB) per scale.
+map (210 MB) per scale. With ``gather=`` (the model's ``feature_gather`` Conv2d, ``PoseEstimation.py:64-66``,
+applied per scale at ``:341``) the maps are the raw backbone features and the conv is evaluated at the four
+bilinear taps of each detection only (``pemp_gather_projected_conv``) instead of over the whole map.
 """
 import torch
 
 
 class ProjectedMaps:
-    def __init__(self, maps, size, divisor=None):
+    def __init__(self, maps, size, divisor=None, gather=None):
         """maps: list of [B, C, h_s, w_s] tensors (one per scale); size: (H, W) of the projection;
-        divisor: the reference's float(len(TEST.SCALE_FACTOR)) (default: number of maps)."""
+        divisor: the reference's float(len(TEST.SCALE_FACTOR)) (default: number of maps);
+        gather: optional nn.Conv2d applied to each map before the projection (the model's feature_gather:
+        stride 1, dilation 1, groups 1, square kernel <= 7, symmetric zero padding < kernel)."""
         if isinstance(maps, torch.Tensor):
             maps = [maps]
         maps = list(maps)
@@ -27,18 +31,54 @@ class ProjectedMaps:
         self.maps = maps
         self.size = (int(size[0]), int(size[1]))
         self.divisor = float(len(maps) if divisor is None else divisor)
+        self.gather = gather
+        if gather is not None:
+            if not isinstance(gather, torch.nn.Conv2d):
+                raise TypeError("ProjectedMaps: gather must be an nn.Conv2d (the model's feature_gather)")
+            k = gather.kernel_size
+            pad = gather.padding
+            if (isinstance(pad, str) or k[0] != k[1] or pad[0] != pad[1] or tuple(gather.stride) != (1, 1)
+                    or tuple(gather.dilation) != (1, 1) or gather.groups != 1 or gather.padding_mode != "zeros"
+                    or not 1 <= k[0] <= 7 or not 0 <= pad[0] < k[0]):
+                raise NotImplementedError("ProjectedMaps: gather conv must be stride 1, dilation 1, groups 1, square "
+                                          "kernel <= 7 with symmetric zero padding < kernel")
+            if gather.in_channels != C:
+                raise ValueError(f"ProjectedMaps: gather expects {gather.in_channels} channels, maps have {C}")
+            if gather.out_channels > 512:
+                raise NotImplementedError("ProjectedMaps: gather conv with more than 512 output channels")
+            C = gather.out_channels
         self.shape = torch.Size([B, C, self.size[0], self.size[1]])
         self.dtype = torch.float32
         self.device = maps[0].device
 
     def to(self, device):
-        return ProjectedMaps([m.to(device) for m in self.maps], self.size, self.divisor)
+        return ProjectedMaps([m.to(device) for m in self.maps], self.size, self.divisor,
+                             None if self.gather is None else self.gather.to(device))
+
+    def conv_params(self):
+        """(weight transposed to [Cin, k, k, Cout] fp32 contiguous, bias fp32 or None, k, pad) for the C-ABI;
+        the transpose is cached against the weight's version counter."""
+        g = self.gather
+        w = g.weight
+        key = (w.data_ptr(), w._version, w.device)
+        cache = getattr(self, "_wt_cache", None)
+        if cache is None or cache[0] != key:
+            with torch.no_grad():
+                wt = w.detach().float().permute(1, 2, 3, 0).contiguous()
+                b = None if g.bias is None else g.bias.detach().float().contiguous()
+            self._wt_cache = cache = (key, wt, b)
+        return cache[1], cache[2], g.kernel_size[0], g.padding[0]
 
     def materialize(self):
-        """The reference's dense map (for checks): sum of the projections / divisor."""
+        """The reference's dense map (for checks): sum of the projections / divisor, computed with the
+        reference's own torch ops (feature_gather conv first when given)."""
         acc = None
         for m in self.maps:
-            p = torch.nn.functional.interpolate(m.float(), size=self.size, mode="bilinear", align_corners=False)
+            m = m.float()
+            if self.gather is not None:
+                with torch.no_grad():
+                    m = self.gather(m)
+            p = torch.nn.functional.interpolate(m, size=self.size, mode="bilinear", align_corners=False)
             acc = p if acc is None else acc + p
         return acc / self.divisor
 

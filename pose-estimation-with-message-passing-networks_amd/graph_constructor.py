@@ -173,7 +173,8 @@ class NaiveGraphConstructor:
             if feats.size != (H, W):
                 raise ValueError(f"ProjectedMaps size {feats.size} != scoremap size {(H, W)}")
             pmaps = [m.float().contiguous() for m in feats.maps]
-            C = pmaps[0].shape[1]
+            C = feats.shape[1]
+            pconv = feats.conv_params() if feats.gather is not None else None
             feats = None
         else:
             if feats.dtype != torch.float32:
@@ -251,7 +252,7 @@ class NaiveGraphConstructor:
             edge_index = built[5][:2 * E_fully].view(2, E_fully)
             edge_attr = built[6][:E_fully]
             if projected:
-                self._gather_projected(L, st, pmaps, H, W, joint_det, batch_index, x)
+                self._gather_projected(L, st, pmaps, pconv, H, W, joint_det, batch_index, x)
             if tags is not None:
                 joint_tags = joint_tags.view((N,) + tuple(tags.shape[4:])) if tags.dim() > 4 else joint_tags.view(N)
             if proj_tags is not None:
@@ -301,7 +302,7 @@ class NaiveGraphConstructor:
                                                 _lib.ptr(edge_index), E, J, norm, mode,
                                                 _lib.ptr(edge_attr), st))
         if projected:
-            self._gather_projected(L, st, pmaps, H, W, joint_det, batch_index, x)
+            self._gather_projected(L, st, pmaps, pconv, H, W, joint_det, batch_index, x)
         if tags is not None:
             joint_tags = joint_tags.view((N,) + tuple(tags.shape[4:])) if tags.dim() > 4 else joint_tags.view(N)
         if proj_tags is not None and fully:
@@ -325,12 +326,19 @@ class NaiveGraphConstructor:
                                                 _lib.ptr(batch_index), N, _lib.ptr(jt), st))
         return jt
 
-    def _gather_projected(self, L, st, pmaps, H, W, joint_det, batch_index, x):
+    def _gather_projected(self, L, st, pmaps, pconv, H, W, joint_det, batch_index, x):
         S = len(pmaps)
         ptrs = (ctypes.c_void_p * S)(*[m.data_ptr() for m in pmaps])
         hs = (ctypes.c_int32 * S)(*[m.shape[2] for m in pmaps])
         ws = (ctypes.c_int32 * S)(*[m.shape[3] for m in pmaps])
         vp = ctypes.c_void_p
+        if pconv is not None:   # feature_gather conv at the taps (pemp_gather_projected_conv)
+            wt, b, k, pad = pconv
+            _lib.check(L.pemp_gather_projected_conv(ctypes.cast(ptrs, vp), ctypes.cast(hs, vp), ctypes.cast(ws, vp), S,
+                                                    pmaps[0].shape[1], _lib.ptr(wt), _lib.ptr(b), x.shape[1], k, pad,
+                                                    H, W, self.features.divisor, _lib.ptr(joint_det),
+                                                    _lib.ptr(batch_index), x.shape[0], _lib.ptr(x), st))
+            return
         _lib.check(L.pemp_gather_projected(ctypes.cast(ptrs, vp), ctypes.cast(hs, vp), ctypes.cast(ws, vp), S,
                                            x.shape[1], H, W, self.features.divisor,
                                            _lib.ptr(joint_det), _lib.ptr(batch_index), x.shape[0], _lib.ptr(x), st))

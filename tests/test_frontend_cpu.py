@@ -45,3 +45,27 @@ def test_projected_heatmaps_validation():
         ProjectedHeatmaps(outs, (40, 40), 17, flips, [0] * 17)          # not a permutation
     with pytest.raises(ValueError):
         ProjectedHeatmaps(outs, (40, 40), 17, flips[:0] + [flips[0][:, :, :10]])
+
+
+def test_projected_maps_gather_conv_host():
+    """ProjectedMaps(gather=feature_gather): materialize() is the reference's conv + interpolate per scale
+    (PoseEstimation.py:341, 426-452); the C-ABI transpose is [Cin, k, k, Cout]; unsupported convs are
+    refused loudly."""
+    import pytest
+    from pemp_amd.frontend import ProjectedMaps
+    g = torch.Generator().manual_seed(3)
+    raw = [torch.randn(2, 8, 10, 12, generator=g), torch.randn(2, 8, 5, 6, generator=g)]
+    conv = torch.nn.Conv2d(8, 16, 3, 1, 1)
+    pm = ProjectedMaps(raw, (20, 24), gather=conv)
+    assert pm.shape == torch.Size([2, 16, 20, 24])
+    with torch.no_grad():
+        want = sum(torch.nn.functional.interpolate(conv(m), size=(20, 24), mode="bilinear", align_corners=False)
+                   for m in raw) / 2.0
+    assert torch.equal(pm.materialize(), want)
+    wt, b, k, pad = pm.conv_params()
+    assert (k, pad) == (3, 1) and torch.equal(wt, conv.weight.detach().permute(1, 2, 3, 0))
+    assert torch.equal(b, conv.bias.detach())
+    with pytest.raises(NotImplementedError):
+        ProjectedMaps(raw, (20, 24), gather=torch.nn.Conv2d(8, 16, 3, 2, 1))
+    with pytest.raises(ValueError):
+        ProjectedMaps(raw, (20, 24), gather=torch.nn.Conv2d(4, 16, 3, 1, 1))

@@ -263,3 +263,34 @@ def test_projected_frontend(graph, sizes, size, flip, features):
         assert ref[7].shape[0] > 2 * J       # detections found
         for i in (7, 11, 12, 14, 2, 0, 1):
             assert torch.equal(out[i].cpu(), ref[i]), i
+
+
+@pytest.mark.parametrize("ksize,pad,scales", [(3, 1, [(80, 80)]), (1, 0, [(53, 67), (40, 40)]), (3, 1, [(27, 33), (160, 160)])])
+def test_projected_features_gather_conv(ksize, pad, scales):
+    """features=ProjectedMaps(raw, gather=feature_gather) (PoseEstimation.py:64-66, 341,
+    426-452): the Conv2d evaluated at the bilinear taps of each detection only equals the reference's own
+    torch ops (conv over the whole map, interpolate, sum over scales / count) gathered at the detections.
+    Floating point with a different summation order: |dx| <= 2e-5 * max(1, max|x|); every other output
+    bit-exact."""
+    from pemp_amd.frontend import ProjectedMaps
+    B, J, H, W = 2, 17, 160, 160
+    hm = torch.from_numpy(syn.make_heatmaps(37, B, J, H, W, 4, margin=2))
+    g = torch.Generator().manual_seed(5)
+    raw = [torch.randn(B, 32, h, w, generator=g) for (h, w) in scales]
+    conv = torch.nn.Conv2d(32, 128, ksize, 1, pad, bias=True)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) * 0.1)
+        conv.bias.copy_(torch.randn(128, generator=g))
+    pm = ProjectedMaps(raw, (H, W), gather=conv)
+    dense = pm.materialize()
+    gc = pcfg.inference_gc_config("fully", 5, False)
+    tags = torch.from_numpy(syn.closed_form((B, J, H, W, 1), 0.75))
+    pmd = pm.to(DEV)
+    for _ in range(2):
+        out = run_gc(gc, J, hm, pmd, tags, None)
+        ref = restate.construct_graph(hm, dense, tags, None, gc, J)
+        for i in (1, 2, 7, 11, 12, 14):
+            assert torch.equal(out[i].cpu(), ref[i]), i
+        assert out[0].shape == ref[0].shape
+        tol = 2e-5 * max(1.0, ref[0].abs().max().item())
+        assert (out[0].cpu() - ref[0]).abs().max().item() <= tol

@@ -8,7 +8,7 @@ root=$(cd "$(dirname "$0")/.." && pwd)
 csrc=$root/pose-estimation-with-message-passing-networks_amd/csrc
 mkdir -p "$root/build_ab"
 base=$(basename "$src" .hip)
-/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function -Wno-unused-variable \
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -DOCML_BASIC_ROUNDED_OPERATIONS -Wno-unused-function -Wno-unused-variable \
   -I"$root/include" "$@" -c "$csrc/$base.hip" -o "$root/build_ab/v_${name}_$base.o"
 objs=""
 for o in "$csrc"/*.o; do
