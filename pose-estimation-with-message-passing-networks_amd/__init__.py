@@ -21,10 +21,11 @@ def get_mpn_model(config, **kwargs):
     return _m(config, **kwargs)
 
 
-def ProjectedMaps(maps, size, divisor=None):
-    """Lazy image-size projection of per-scale feature maps for ``features=`` (frontend.py)."""
+def ProjectedMaps(maps, size, divisor=None, gather=None):
+    """Lazy image-size projection of per-scale feature maps for ``features=`` (frontend.py); ``gather``: the
+    model's feature_gather Conv2d, evaluated at the detections only."""
     from .frontend import ProjectedMaps as _p
-    return _p(maps, size, divisor)
+    return _p(maps, size, divisor, gather)
 
 
 def ProjectedHeatmaps(outputs, size, num_joints, flip_outputs=None, flip_index=None, divisor=None, tag_scale=0):

@@ -86,12 +86,18 @@ __device__ __forceinline__ void gemm_frag(const float* W, int ldw, const float (
   }
 }
 
+// ReLU as one integer max on the bit pattern (non-negative floats order as non-negative ints, every
+// negative float is a negative int): fmaxf on an MFMA result compiles to a canonicalising max plus the
+// max, two VALU issues per value. (An inline-asm v_max_f32 is not an option: the hazard recognizer does
+// not pad an asm read of a fresh MFMA result.) -0.0 -> +0.0; NaN with a clear sign bit stays NaN.
+__device__ __forceinline__ float relu1(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
+
 template <int NB>
 __device__ __forceinline__ void relu_frag(float (&v)[NB][4]) {
 #pragma unroll
   for (int b = 0; b < NB; ++b)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[b][r] = fmaxf(v[b][r], 0.0f);
+    for (int r = 0; r < 4; ++r) v[b][r] = relu1(v[b][r]);
 }
 
 // One Linear (+ReLU) of a pemp_mlp with runtime dims <= 16*MAXB, weights from global memory.
@@ -117,7 +123,7 @@ __device__ __forceinline__ void layer_rt(const pemp_layer& L, const float (&in)[
       }
       if (L.relu) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) c[r] = fmaxf(c[r], 0.0f);
+        for (int r = 0; r < 4; ++r) c[r] = relu1(c[r]);
       }
     }
     out[ob][0] = c[0]; out[ob][1] = c[1]; out[ob][2] = c[2]; out[ob][3] = c[3];
@@ -440,7 +446,7 @@ __global__ __launch_bounds__(256) void rows_mlp_kernel(RowsMlpArgs a) {
       }
       if (L.relu) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) c[r] = fmaxf(c[r], 0.0f);
+        for (int r = 0; r < 4; ++r) c[r] = relu1(c[r]);
       }
       st4(&act[cur ^ 1][i * RS + 16 * ob + 4 * g], c[0], c[1], c[2], c[3]);
     }
@@ -738,7 +744,7 @@ __device__ __forceinline__ void layer_lds(const float* __restrict__ W, int ldw, 
         }
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) out[ob][r] = relu ? fmaxf(c[r], 0.0f) : c[r];
+      for (int r = 0; r < 4; ++r) out[ob][r] = relu ? relu1(c[r]) : c[r];
     } else {
 #pragma unroll
       for (int r = 0; r < 4; ++r) out[ob][r] = 0.0f;
@@ -1346,9 +1352,6 @@ __device__ __forceinline__ float pemp_exp(float x) { return PEMP_FAST_EXP ? __ex
 #ifndef PEMP_XCD_MAP
 #define PEMP_XCD_MAP 1
 #endif
-#ifndef PEMP_EARLY_GATHER
-#define PEMP_EARLY_GATHER 1
-#endif
 template <int AGG, int HEAD, int PREC, int UPD, int STAGE>
 __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(EdgeStepArgs a) {
   constexpr int NW = edge_waves<HEAD>();
@@ -1385,9 +1388,9 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
   const rsrc_t rs_orig = make_rsrc(a.s_orig, E * 4);
   const int nt_row = a.t_nt_ld * 4;                  // bytes per node-table row
   const int nt_p = (128 + 64 * t) * 4;               // byte offset of P_t in a row (SGPR soffset)
-  // a tile's gathers (PEMP_EARLY_GATHER: issued at the end of the previous tile, and for the first tile
-  // while the weight image is copied): node-table rows of target and source, Q0 rows, original ids
-  float4 xa[4], xb[4], xp[4], qq[4];
+  // a tile's gathers, issued at the end of the previous tile (the first tile's while the weight image is
+  // copied): node-table rows of target and source, original ids
+  float4 xa[4], xb[4], xp[4];
   int orig_t = 0;
   auto gather_nt = [&](int dstv, int srcv, bool on) {
     const int va = on ? dstv * nt_row + 16 * g : OOB_VOFF, vb = on ? srcv * nt_row + 256 + 16 * g : OOB_VOFF;
@@ -1398,14 +1401,7 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
       xp[ob] = bld4(rs_nt, va + 64 * ob, nt_p);
     }
   };
-  auto gather_q = [&](int pbase, bool on) {
-    const int vq = on ? (pbase + c) * 256 + 16 * g : OOB_VOFF;
-#pragma unroll
-    for (int ob = 0; ob < 4; ++ob)
-      if (MID) qq[ob] = bld4(rs_q, vq + 64 * ob);
-  };
-  // first two tiles' indices, the first tile's r rows (and, early gathers, its Q0 rows) in flight before
-  // the weight copy
+  // first two tiles' indices and the first tile's r rows in flight before the weight copy
   int dst_n = 0, src_n = 0, dst_nn = 0, src_nn = 0;
   if (first < end) {   // (uniform)
     dst_n = bld1(rs_dst, 4 * min(first + c, end - 1));
@@ -1413,7 +1409,6 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
     dst_nn = bld1(rs_dst, 4 * min(first + 16 + c, end - 1));
     src_nn = bld1(rs_src, 4 * min(first + 16 + c, end - 1));
     dma_rows(rs_r, first, mybuf, lane);
-    if (PEMP_EARLY_GATHER) gather_q(first, true);
   }
   {
     // the block's type image: IMG_F floats, 1 KB per wave instruction, waves interleaved
@@ -1424,7 +1419,7 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
     if (TAIL && wave == NW - 1 && 4 * lane < TAIL)
       *reinterpret_cast<float4*>(&img[256 * PIECES + 4 * lane]) = ld4(src + 256 * PIECES + 4 * lane);
   }
-  if (PEMP_EARLY_GATHER && first < end) {
+  if (first < end) {
     gather_nt(dst_n, src_n, true);
     if (HEAD == 1) orig_t = bld1(rs_orig, 4 * min(first + c, end - 1));
   }
@@ -1432,10 +1427,10 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
   EDGE_STAMP(1);
   EDGE_STAMP(2);
   if (first >= end) { EDGE_STAMP(15); return; }
-  const float attn_b = vec[2 * D];
   const rsrc_t rs_next = make_rsrc(a.r_next, E * 256);
   const rsrc_t rs_agg = make_rsrc(a.agg, (int)a.N * T * 256);
   const u32x4v_s rw_r = rsrc_words(a.r_cur, E * 256);
+  const u32x4v_s rw_q = rsrc_words(a.Q0, E * 256);
   // stores issued after a tile's DMA, all unconditional (masked lanes write past the buffer end): the
   // r_next rows (middle passes that write them) and the aggregate rows
   const bool store_next = MID && a.write_next;
@@ -1464,8 +1459,8 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
     dst_n = dst_nn;
     src_n = src_nn;
     // this tile's rows (DMA issued one tile ago) have landed: the ops issued after that DMA are the
-    // tile's unconditional stores and (early gathers) this tile's gathers
-    constexpr int NG = PEMP_EARLY_GATHER ? 12 + (MID ? 4 : 0) + (HEAD == 1 ? 1 : 0) : 0;
+    // previous tile's unconditional stores and this tile's gathers
+    constexpr int NG = 12 + (HEAD == 1 ? 1 : 0);
     if (tile_no > 0) {
       if (store_next) dma_wait<8 + NG>();
       else dma_wait<4 + NG>();
@@ -1479,15 +1474,16 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob) rr[ob] = ld4(mybuf + (rowb ^ (16 * (ob ^ (cz & 3)))));
     }
-    // gathers of this tile (issued before the next tile's DMA, or already in flight); then the indices two
-    // tiles ahead
+    // this tile's gathers were issued at the end of the previous tile. Middle passes that write the next r:
+    // once they have landed (waited for here, so that no later compiler wait can also wait on the DMA) the
+    // Q0 rows of this tile go by LDS-DMA into the buffer just read, overlapping the first half of the tile
     const int vq = p * 256 + 16 * g;
-    if (!PEMP_EARLY_GATHER) {
-      gather_nt(dst, src, true);
-      gather_q(base, true);
-      if (HEAD == 1) orig_t = bld1(rs_orig, 4 * min(p, end - 1));
-    }
     const int orig = orig_t;
+    if (MID) {
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob) asm volatile("" ::"v"(xa[ob].x), "v"(xb[ob].x), "v"(xp[ob].x));
+      if (store_next) dma_rows_async(rw_q, base, mybuf, lane);
+    }
     {
       const int qn = min(base + 32 + c, end - 1);
       dst_nn = bld1(rs_dst, 4 * qn);
@@ -1505,18 +1501,16 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
         h[ob][2] = rr[ob].z + xa[ob].z + xb[ob].z; h[ob][3] = rr[ob].w + xa[ob].w + xb[ob].w;
       }
     }
-    // the r rows of tile k+1 into the buffer this tile's rows were read from, once every gather of
-    // this tile has returned (the compiler's waits on those would otherwise also wait on the DMA)
+    // other passes: the r rows of tile k+1 into the buffer this tile's rows were read from, once every
+    // gather of this tile has returned (the compiler's waits on those would otherwise also wait on the DMA)
+    if (!MID) {
 #pragma unroll
-    for (int ob = 0; ob < 4; ++ob) {
-      asm volatile("" ::"v"(xa[ob].x), "v"(xb[ob].x), "v"(xp[ob].x));
-      if (MID) asm volatile("" ::"v"(qq[ob].x));
+      for (int ob = 0; ob < 4; ++ob) asm volatile("" ::"v"(xa[ob].x), "v"(xb[ob].x), "v"(xp[ob].x));
+      if (HEAD == 1) asm volatile("" ::"v"(orig));
+      if (more) dma_rows_async(rw_r, base + 16, mybuf, lane);
     }
-    if (HEAD == 1) asm volatile("" ::"v"(orig));
-    if (more) dma_rows_async(rw_r, base + 16, mybuf, lane);
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob) {
-      if (MID) { q0r[ob][0] = qq[ob].x; q0r[ob][1] = qq[ob].y; q0r[ob][2] = qq[ob].z; q0r[ob][3] = qq[ob].w; }
       m[ob][0] = xp[ob].x; m[ob][1] = xp[ob].y; m[ob][2] = xp[ob].z; m[ob][3] = xp[ob].w;
     }
 #ifdef PEMP_STAMPS
@@ -1549,7 +1543,7 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
       }
       av += __shfl_xor(av, 16);
       av += __shfl_xor(av, 32);
-      av += attn_b;
+      av += vec[z + 2 * D];                      // attention bias (re-read: a register copy spills)
     }
     if (HEAD == 2) {   // generic edge head (weights in global memory, true domain)
       float h1[4][4], h2[4][4];
@@ -1562,6 +1556,20 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
     }
     Frag<PREC> fe;                                // e' split once for the r_next, head and message GEMMs
     prep<PREC>(ep, fe);
+    if (MID) {
+      // this tile's Q0 rows have landed (only the two index loads were issued after their DMA): read them,
+      // then the r rows of tile k+1 into the same buffer
+      if (store_next) {
+        dma_wait<2>();
+        const int cz = c + z, rowb = 64 * cz + 4 * g;
+#pragma unroll
+        for (int ob = 0; ob < 4; ++ob) {
+          const float4 q = ld4(mybuf + (rowb ^ (16 * (ob ^ (cz & 3)))));
+          q0r[ob][0] = q.x; q0r[ob][1] = q.y; q0r[ob][2] = q.z; q0r[ob][3] = q.w;
+        }
+      }
+      if (more) dma_rows_async(rw_r, base + 16, mybuf, lane);
+    }
     if (MID && a.write_next) {                    // next pass's r = Q0 + W1_e_cur · e'
       gemm_f<PREC, 4>(W1, ep, fe, q0r);
       const int vn = valid ? vq : OOB_VOFF;
@@ -1678,9 +1686,8 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob) bst4(rs_agg, vo + 64 * ob, v[ob][0] * inv, v[ob][1] * inv, v[ob][2] * inv, v[ob][3] * inv);
     }
-    if (PEMP_EARLY_GATHER) {   // the next tile's gathers, unconditional (past the range: OOB offsets, no traffic)
+    {   // the next tile's gathers, unconditional (past the range: OOB offsets, no traffic)
       gather_nt(dst_n, src_n, more);
-      gather_q(base + 16, more);
       if (HEAD == 1) orig_t = bld1(rs_orig, 4 * min(p + 16, end - 1));
     }
 #ifdef PEMP_STAMPS
