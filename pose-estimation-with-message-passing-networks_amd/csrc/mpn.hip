@@ -20,6 +20,7 @@
 #include <limits.h>
 
 #include <algorithm>
+#include <map>
 #include <mutex>
 #include <string.h>
 #include <math.h>
@@ -837,7 +838,8 @@ __device__ __forceinline__ void load_edge_attr(rsrc_t rs_ea, int A, int o, float
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[mb][r] = __int_as_float(bld1(rs_ea, row + 4 * min(16 * mb + 4 * g + r, A - 1)));
+    for (int r = 0; r < 4; ++r)   // 16-feature blocks past A are not loaded (uniform; A = 19 reads 2 of 4)
+      v[mb][r] = 16 * mb < A ? __int_as_float(bld1(rs_ea, row + 4 * min(16 * mb + 4 * g + r, A - 1))) : 0.0f;
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
@@ -874,9 +876,11 @@ __device__ __forceinline__ void embed_tile(const float* smz, const EmbedLayout& 
 // The published edge embedding ([J+2 <= 32] -> 32 -> 64 -> 64 -> 64, then Q0 64 -> 64) with the block
 // counts known at compile time: straight-line layers (the runtime-shaped loop above keeps its loop state,
 // per-layer guards and LDS offsets live and spilled). Split precisions only.
-template <int PREC, int KB32, int OB>
+// DOM (the Q0 layer): the output stays in the f16x3 domain (x 2^11, as the edge passes keep Q0 and R0) and
+// the input's split is handed back for the R0 GEMM on the same e_init
+template <int PREC, int KB32, int OB, bool DOM = false>
 __device__ __forceinline__ void layer_fixed(const float* smz, const EmbedLayout& Lo, int l, const float (&in)[4][4],
-                                            float (&out)[4][4]) {
+                                            float (&out)[4][4], Frag<PREC>* split_out = nullptr) {
   const uint16_t* W = reinterpret_cast<const uint16_t*>(smz + Lo.w_off[l]);
   const float* bias = smz + Lo.b_off[l];
   const int ldw = Lo.stride[l], relu = Lo.relu[l];
@@ -889,7 +893,20 @@ __device__ __forceinline__ void layer_fixed(const float* smz, const EmbedLayout&
   } else {
     const bool big = split_f16(in, 1.0f, hh, lh);
     s_in = big ? 2048.0f * F16_DOWN : 2048.0f;
-    s_out = big ? F16_UP / 2048.0f : 1.0f / 2048.0f;
+    s_out = DOM ? (big ? F16_UP : 1.0f) : (big ? F16_UP / 2048.0f : 1.0f / 2048.0f);
+    if constexpr (PREC == 2) {
+      if (split_out) {
+        split_out->hh[0] = hh[0]; split_out->hh[1] = hh[1];
+        split_out->hl[0] = lh[0]; split_out->hl[1] = lh[1];
+        split_out->big = big;
+      }
+    }
+  }
+  if constexpr (PREC == 1) {
+    if (split_out) {
+      split_out->bh[0] = hb[0]; split_out->bh[1] = hb[1];
+      split_out->bl[0] = lb[0]; split_out->bl[1] = lb[1];
+    }
   }
   constexpr int lo_off = 32 * KB32;
 #pragma unroll
@@ -928,12 +945,12 @@ __device__ __forceinline__ void layer_fixed(const float* smz, const EmbedLayout&
 
 template <int PREC>
 __device__ __forceinline__ void embed_tile_fixed(const float* smz, const EmbedLayout& Lo, float (&x)[4][4],
-                                                 float (&y)[4][4]) {
+                                                 float (&y)[4][4], Frag<PREC>& fx) {
   layer_fixed<PREC, 1, 2>(smz, Lo, 0, x, y);   // A -> 32
   layer_fixed<PREC, 1, 4>(smz, Lo, 1, y, x);   // 32 -> 64
   layer_fixed<PREC, 2, 4>(smz, Lo, 2, x, y);   // 64 -> 64
   layer_fixed<PREC, 2, 4>(smz, Lo, 3, y, x);   // 64 -> 64  (e_init in x)
-  layer_fixed<PREC, 2, 4>(smz, Lo, 4, x, y);   // Q0 = W1_e_init e_init + b1
+  layer_fixed<PREC, 2, 4, true>(smz, Lo, 4, x, y, &fx);   // Q0 = W1_e_init e_init + b1 (domain), e_init's split
 }
 
 // the layout embed_tile_fixed assumes
@@ -1009,28 +1026,34 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp em
   // buffer descriptors + 32-bit offsets: no 64-bit lane pointers live across the tile loop
   const rsrc_t rs_ea = make_rsrc(ea, (int)E * A * 4), rs_orig = make_rsrc(s_orig, (int)E * 4);
   const rsrc_t rs_q0 = make_rsrc(q0, (int)E * 256), rs_r0 = make_rsrc(r0, (int)E * 256);
+  // original edge ids one tile ahead (the edge_attr gather of a tile then waits for one round trip, not two)
+  int o_next = first < end ? bld1(rs_orig, 4 * min(first + c, end - 1)) : 0;
   for (int base = first; base < end; base += 16) {
     int z = 0;
     asm volatile("" : "+s"(z));                  // keep the LDS fragment reads inside the loop
     const float* smz = sm + z;
     const int p = base + c;
     const bool valid = p < end;
-    const int o = bld1(rs_orig, 4 * (valid ? p : end - 1));
+    const int o = o_next;
+    o_next = bld1(rs_orig, 4 * min(base + 16 + c, end - 1));
     float x[4][4], y[4][4];
     load_edge_attr(rs_ea, A, o, x);
-    if constexpr (FIXED) embed_tile_fixed<PREC>(smz, Lo, x, y);   // x = e_init, y = Q0 (true values)
-    else embed_tile<PREC>(smz, Lo, x, y);
-    if (PREC == 2) {                              // Q0 and R0 are kept in the f16x3 domain (x 2^11)
+    Frag<PREC> fx;
+    if constexpr (FIXED) {
+      embed_tile_fixed<PREC>(smz, Lo, x, y, fx);   // x = e_init, y = Q0 in the domain, fx = e_init's split
+    } else {
+      embed_tile<PREC>(smz, Lo, x, y);             // x = e_init, y = Q0 (true values)
+      if (PREC == 2) {                             // Q0 and R0 are kept in the f16x3 domain (x 2^11)
 #pragma unroll
-      for (int ob = 0; ob < 4; ++ob)
+        for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) y[ob][r] *= dom<PREC>();
+          for (int r = 0; r < 4; ++r) y[ob][r] *= dom<PREC>();
+      }
+      prep_true<PREC>(x, fx);
     }
     const int vo = valid ? p * 256 + 16 * g : OOB_VOFF;   // masked lanes: stores dropped
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob) bst4(rs_q0, vo + 64 * ob, y[ob][0], y[ob][1], y[ob][2], y[ob][3]);
-    Frag<PREC> fx;
-    prep_true<PREC>(x, fx);
     gemm_f<PREC, 4>(smz + Lo.total, x, fx, y);    // R0 = Q0 + W1_e_cur · e_init
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob) bst4(rs_r0, vo + 64 * ob, y[ob][0], y[ob][1], y[ob][2], y[ob][3]);
@@ -2636,6 +2659,46 @@ extern "C" int pemp_diag_stamps(void* buf, int pass) {
 }
 #endif
 
+// ---- side stream of a launch stream (the concurrent edge prelude of mpn_forward_impl) ----------------
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  std::mutex mu;   // held from the fork to the join enqueue: calls sharing a launch stream pair up
+};
+
+static bool serial_prelude() {
+  static const bool v = getenv("PEMP_SERIAL_PRELUDE") != nullptr;
+  return v;
+}
+
+// one per (device, launch stream), created on first use and kept; nullptr if HIP refuses (serial then)
+static SideStream* side_stream_for(hipStream_t st) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, SideStream*> table;
+  int cur = 0;
+  if (hipGetDevice(&cur) != hipSuccess) return nullptr;
+  int dev = cur;
+  if (st) {
+    hipDevice_t d;
+    if (hipStreamGetDevice(st, &d) == hipSuccess) dev = (int)d;
+  }
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = table.find({dev, st});
+  if (it != table.end()) return it->second;
+  if (dev != cur && hipSetDevice(dev) != hipSuccess) return nullptr;
+  SideStream* ss = new SideStream();
+  const bool ok = hipStreamCreateWithFlags(&ss->s, hipStreamNonBlocking) == hipSuccess &&
+                  hipEventCreateWithFlags(&ss->fork, hipEventDisableTiming) == hipSuccess &&
+                  hipEventCreateWithFlags(&ss->join, hipEventDisableTiming) == hipSuccess;
+  if (dev != cur) (void)hipSetDevice(cur);
+  if (!ok) {
+    (void)hipGetLastError();
+    return nullptr;   // (the partial objects are leaked once; the forward runs serially)
+  }
+  table[{dev, st}] = ss;
+  return ss;
+}
+
 static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w, const float* x,
                             const float* edge_attr, const int64_t* edge_index, const int64_t* node_types,
                             int64_t N, int64_t E, float* edge_logits, float* node_logits, float* class_logits,
@@ -2742,6 +2805,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   }
   // launched after the node embedding + first node table (which need no edge order), so that the
   // host issues the short prepare kernels while the GPU runs those node kernels
+  hipStream_t pst = st;                           // stream of the edge prelude (a side stream, below)
   auto edge_prelude = [&]() -> int {
   if (!(desc->flags & PEMP_MPN_PREPARED)) {
     if (fully_node_off && N > 0) {
@@ -2750,27 +2814,27 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
       // one thread per (type, target) segment (a per-edge mapping with binary searches measured 41 us
       // vs 15 us at C3)
       const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(64, ((int64_t)T * fully_nmax + 511) / 512));
-      ProfScope prof("mpn_prepare", st);
-      hipLaunchKernelGGL(fully_prepare_kernel, dim3(gx, (unsigned)fully_B), dim3(256), 0, st, fa);
+      ProfScope prof("mpn_prepare", pst);
+      hipLaunchKernelGGL(fully_prepare_kernel, dim3(gx, (unsigned)fully_B), dim3(256), 0, pst, fa);
       PEMP_LAUNCH_CHECK();
     } else {
-      const int rc0 = launch_prepare(desc, edge_index, node_types, N, E, ws, st);
+      const int rc0 = launch_prepare(desc, edge_index, node_types, N, E, ws, pst);
       if (rc0) return rc0;
     }
   }
   if (E > 0 && steps >= 1) {   // per-wave edge ranges of the passes (static across iterations)
     hipLaunchKernelGGL(edge_ranges_kernel, dim3((unsigned)std::min(64, (edge_grid * (EDGE_WAVES + 12) + 255) / 256)),
-                       dim3(256), 0, st, ws.seg, ws.wg_start, ws.s_dst, T, N, edge_grid, ws.ranges);
+                       dim3(256), 0, pst, ws.seg, ws.wg_start, ws.s_dst, T, N, edge_grid, ws.ranges);
     PEMP_LAUNCH_CHECK();
   }
   if (E > 0 && steps >= 1) {
-    ProfScope prof("edge_embed", st);
+    ProfScope prof("edge_embed", pst);
     if (emb_lds) {
       const int grid = (int)std::min<int64_t>(num_cus(), (E + 16 * EDGE_WAVES - 1) / (16 * EDGE_WAVES));
       const size_t lds = (size_t)(emb_lo.total + D * LDW) * sizeof(float);
       const bool fixed = embed_fixed_shape(emb_lo);
 #define PEMP_EMBED_LAUNCH(P, FX)                                                                                   \
-  hipLaunchKernelGGL((edge_embed_kernel<P, FX>), dim3(grid), dim3(64 * EDGE_WAVES), lds, st, w->edge_emb, emb_lo,  \
+  hipLaunchKernelGGL((edge_embed_kernel<P, FX>), dim3(grid), dim3(64 * EDGE_WAVES), lds, pst, w->edge_emb, emb_lo,  \
                      w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, w->e1_bf, \
                      ws.EA, ws.Q0)
       if (emb_prec == PEMP_PREC_F16X3) {
@@ -2780,12 +2844,12 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
         if (fixed) PEMP_EMBED_LAUNCH(1, true);
         else PEMP_EMBED_LAUNCH(1, false);
       } else
-        hipLaunchKernelGGL((edge_embed_kernel<0, false>), dim3(grid), dim3(64 * EDGE_WAVES), lds, st, w->edge_emb, emb_lo,
+        hipLaunchKernelGGL((edge_embed_kernel<0, false>), dim3(grid), dim3(64 * EDGE_WAVES), lds, pst, w->edge_emb, emb_lo,
                            w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, w->e1_bf,
                            ws.EA, ws.Q0);
 #undef PEMP_EMBED_LAUNCH
     } else {
-      hipLaunchKernelGGL(edge_embed_wide_kernel, dim3((unsigned)((E + 63) / 64)), dim3(256), 0, st, w->edge_emb,
+      hipLaunchKernelGGL(edge_embed_wide_kernel, dim3((unsigned)((E + 63) / 64)), dim3(256), 0, pst, w->edge_emb,
                          edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, ws.EA, ws.Q0,
                          desc->precision == PEMP_PREC_F16X3 ? dom<2>() : 1.0f);
     }
@@ -2869,11 +2933,42 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   // node embedding + node table of the first iteration (or, without iterations, the heads on the
   // embedding); embedding widths > 128 would not fit the node step's LDS rows: separate launch
   const bool fused_embed = fused_embed_;
-  if (!fused_embed) {
-    if ((rc = rows_mlp("node_embed", w->node_emb, x, desc->node_in_dim, N, ws.X, 128, ws.X + 64, 128, st))) return rc;
+  // The edge prelude (prepare, wave ranges, edge embedding) needs nothing the node embedding and the first
+  // node table produce: it runs on a side stream (forked from and joined back into `st`) while they run
+  // here (their 16-row grids leave most CUs idle). Serial when the library profiler is on (per-kernel
+  // event timing on `st`) or with PEMP_SERIAL_PRELUDE set.
+  SideStream* ss = (E > 0 && steps >= 1 && !prof_active() && !serial_prelude()) ? side_stream_for(st) : nullptr;
+  std::unique_lock<std::mutex> side_lock;
+  if (ss) {
+    side_lock = std::unique_lock<std::mutex>(ss->mu);
+    if (hipEventRecord(ss->fork, st) != hipSuccess || hipStreamWaitEvent(ss->s, ss->fork, 0) != hipSuccess) {
+      side_lock.unlock();
+      ss = nullptr;
+    } else {
+      pst = ss->s;
+    }
   }
-  if ((rc = node_step(fused_embed ? ROWS_EMBED : ROWS_NONE, steps > 0, steps > 0 ? -1 : 0, false))) return rc;
-  if ((rc = edge_prelude())) return rc;
+  auto join_side = [&]() {
+    if (!ss) return;
+    // (a failed join is reported by the next launch check: both calls only enqueue)
+    (void)hipEventRecord(ss->join, ss->s);
+    (void)hipStreamWaitEvent(st, ss->join, 0);
+    side_lock.unlock();
+    ss = nullptr;
+  };
+  if (ss && (rc = edge_prelude())) { join_side(); return rc; }
+  if (!fused_embed) {
+    if ((rc = rows_mlp("node_embed", w->node_emb, x, desc->node_in_dim, N, ws.X, 128, ws.X + 64, 128, st))) {
+      join_side();
+      return rc;
+    }
+  }
+  if ((rc = node_step(fused_embed ? ROWS_EMBED : ROWS_NONE, steps > 0, steps > 0 ? -1 : 0, false))) {
+    join_side();
+    return rc;
+  }
+  if (ss) join_side();
+  else if ((rc = edge_prelude())) return rc;
   float* e_cur = ws.EA;                           // r of the pass (R0 from the separate embedding)
   float* e_nxt = ws.EB;
   int rec = 0;
