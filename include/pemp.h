@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define PEMP_ABI_VERSION 13
+#define PEMP_ABI_VERSION 14
 
 enum {
   PEMP_OK = 0,
@@ -189,6 +189,22 @@ int pemp_knn_graph_build(const int64_t* joint_det, const int64_t* node_off, cons
                          const float* joint_scores, int J, float norm_factor, int mode,
                          float* edge_attr /*[e_cap, A] or NULL: pemp_edge_features' values, leading E rows*/,
                          void* stream);
+
+/* feature_knn graph per image (replaces ConstructGraph.py:370-374 feature_knn_mpn_graph:
+ * knn_graph(x, k=50) over the node features -> to_undirected -> remove_self_loops), with the edge
+ * features, in one queued call. Same contract as pemp_knn_graph_build (edge_buf, e_cap bound, mapped
+ * e_total_host, fast path for images of <= 512 nodes), plus x: device [N, C] fp32 node features
+ * (construct_graph's x; 16-byte aligned when C % 4 == 0; C <= 8192). Candidates are ranked by the
+ * fp32 sum over c in order of (x_j[c] - x_i[c])^2 as one fma per channel (torch_cluster's CUDA knn
+ * as nvcc compiles it), ties by node index; a NaN distance ranks last. The workspace also holds the
+ * sum_b n_b^2 distance keys (pemp_feature_knn_workspace_size). */
+size_t pemp_feature_knn_workspace_size(const int64_t* node_off_host, int B);
+int pemp_feature_knn_graph_build(const float* x, int C, const int64_t* joint_det, const int64_t* node_off,
+                                 const int64_t* node_off_host, int B, int k, void* workspace,
+                                 size_t workspace_bytes, int64_t e_cap, int64_t* edge_buf,
+                                 int32_t* e_total_host, const float* joint_tags, int F,
+                                 const float* joint_scores, int J, float norm_factor, int mode,
+                                 float* edge_attr, void* stream);
 
 /* Node features from maps projected to the image size on demand (the test front-end's bilinear
  * projection, PoseEstimation.py:426-452, summed over scales and divided, multi_scales_testing.py:182-190

@@ -160,6 +160,12 @@ GC_CASES = {
                              graph="fully", pool=5, thr=0.1, mask_crowds=False, features=["ae_normed"]), False),
     "gc_ae_tracking_f2": (dict(seed=14, B=2, J=17, H=64, W=64, C=128, F=2, persons=2, variant="clean",
                                graph="fully", pool=5, thr=0.1, mask_crowds=False, features=["ae_tracking_1"]), False),
+    # feature_knn_mpn_graph (ConstructGraph.py:370-374): knn over the 128-d node features
+    "gc_feature_knn": (dict(seed=15, B=2, J=17, H=128, W=128, C=128, F=1, persons=6, variant="clean",
+                            graph="feature_knn", pool=5, thr=0.1, mask_crowds=False), False),
+    "gc_feature_knn_small": (dict(seed=16, B=2, J=14, H=64, W=80, C=32, F=2, persons=2, variant="noisy",
+                                  graph="feature_knn", pool=3, thr=0.1, mask_crowds=False,
+                                  features=["position", "angle", "connection_type"]), True),
     "gc_score_based": (dict(seed=8, B=2, J=17, H=128, W=128, C=128, F=1, persons=6, variant="clean",
                             graph="score_based", pool=5, thr=0.1, mask_crowds=False), False),
     "gc_score_based_nothr": (dict(seed=9, B=1, J=17, H=64, W=80, C=128, F=1, persons=2, variant="noisy",

@@ -15,6 +15,7 @@ which runs the reference's own files under ``oracle/ref_shims.py``).
 Defined where the reference is unpinned:
   * top-k ties: lower flat index wins (the CUDA radix-select order the reference ran on);
   * knn ties:   (squared integer distance, node index) — torch_cluster's order is unspecified;
+  * feature_knn: fp32 fma-chain distance (torch_cluster's CUDA kernel as nvcc compiles it), then index;
   * score_based root ties: (score descending, node index) — torch.topk's tie order is unspecified.
 """
 import math
@@ -112,6 +113,32 @@ def knn_edge_index(det: torch.Tensor, k: int = 50) -> torch.Tensor:
     return torch.stack([src, dst], 0)
 
 
+def feature_knn_edge_index(x: torch.Tensor, k: int = 50) -> torch.Tensor:
+    """feature_knn_mpn_graph (ConstructGraph.py:370-374): knn_graph(x, k) over the node features
+    (k+1 queried, self removed) -> to_undirected -> remove_self_loops. The distance is torch_cluster
+    1.5.4's CUDA one (knn_cuda.cu: tmp += (x_j - x_i) * (x_j - x_i) over the channels in order, fp32,
+    one fma per channel under nvcc's default contraction); each fma is evaluated as the exact f64
+    t*t + acc rounded to fp32 (t*t of an fp32 t is exact in f64; the f64 sum's own rounding can
+    double-round only on an fp32 midpoint). Ties: (distance, node index); NaN ranks last."""
+    n = x.shape[0]
+    if n == 0:
+        return torch.zeros(2, 0, dtype=torch.long)
+    xs = x.to(torch.float32).numpy()
+    acc = np.zeros((n, n), np.float32)
+    for c in range(xs.shape[1]):
+        t = (xs[None, :, c] - xs[:, None, c]).astype(np.float64)     # [i, j] = x_j - x_i, fp32-rounded
+        acc = (acc.astype(np.float64) + t * t).astype(np.float32)
+    key = torch.from_numpy(acc.view(np.int32).astype(np.int64))
+    key[torch.from_numpy(np.isnan(acc))] = 2 ** 32 - 1
+    order = torch.argsort(key * n + torch.arange(n)[None, :], dim=1)[:, :k + 1]
+    adj = torch.zeros(n, n, dtype=torch.bool)
+    adj.scatter_(1, order, True)
+    adj = adj | adj.t()
+    adj.fill_diagonal_(False)
+    src, dst = adj.nonzero(as_tuple=True)
+    return torch.stack([src, dst], 0)
+
+
 def score_based_edge_index(scores: torch.Tensor, k: int = 75) -> torch.Tensor:
     """score_based_graph (ConstructGraph.py:405-422): the k best-scoring nodes are roots; rows of
     roots in a dense adjacency -> to_undirected -> remove_self_loops. Edge (a, b), a != b, exists
@@ -188,6 +215,8 @@ def construct_graph(scoremaps, features, tagmaps, masks, gc, num_joints):
             ei = fully_edge_index(det.shape[0])
         elif gc.GRAPH_TYPE == "knn":
             ei = knn_edge_index(det)
+        elif gc.GRAPH_TYPE == "feature_knn":
+            ei = feature_knn_edge_index(x)
         elif gc.GRAPH_TYPE == "score_based":
             ei = score_based_edge_index(sc, 75)
         else:

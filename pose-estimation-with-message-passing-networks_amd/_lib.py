@@ -9,7 +9,7 @@ import os
 
 LIB_PATH = os.environ.get("PEMP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc",
                                                      "libpemp.so")
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 ERR_INVALID_ARG, ERR_HIP, ERR_WORKSPACE, ERR_UNSUPPORTED = -1, -2, -3, -4
 
@@ -71,6 +71,9 @@ SIGNATURES = {
     "pemp_knn_graph_emit": (c_i32, [c_p, c_p, c_i32, c_p, c_i64, c_p, c_sz, c_p, c_p]),
     "pemp_knn_graph_build": (c_i32, [c_p, c_p, c_p, c_i32, c_i32, c_p, c_sz, c_i64, c_p, c_p, c_p, c_i32, c_p,
                                      c_i32, c_f32, c_i32, c_p, c_p]),
+    "pemp_feature_knn_workspace_size": (c_sz, [c_p, c_i32]),
+    "pemp_feature_knn_graph_build": (c_i32, [c_p, c_i32, c_p, c_p, c_p, c_i32, c_i32, c_p, c_sz, c_i64, c_p, c_p,
+                                             c_p, c_i32, c_p, c_i32, c_f32, c_i32, c_p, c_p]),
     "pemp_score_graph_workspace_size": (c_sz, [c_p, c_i32, c_i32]),
     "pemp_score_graph": (c_i32, [c_p, c_p, c_p, c_i32, c_i32, c_i64, c_p, c_sz, c_p, c_p]),
     "pemp_gather_projected": (c_i32, [c_p, c_p, c_p, c_i32, c_i32, c_i32, c_i32, c_f32, c_p, c_p, c_i64, c_p, c_p]),

@@ -167,6 +167,8 @@ struct KnnWs {
   unsigned long long* arow;  // fast path: A (the k+1 nearest of each node), 8 words per node
   unsigned long long* rows;  // fast path: R = A | A^T, 8 words per node
   int* rowstart;             // LDS path: degree prefix of each row inside its image
+  int64_t* doff;             // feature_knn: [B+1] offsets of the per-image n_b x n_b key matrices
+  unsigned* dkey;            // feature_knn: squared feature distances as ordered fp32 bit patterns
 };
 
 static size_t knn_words(const int64_t* node_off_host, int B, int64_t* mat_off_host) {
@@ -180,7 +182,7 @@ static size_t knn_words(const int64_t* node_off_host, int B, int64_t* mat_off_ho
   return w;
 }
 
-static KnnWs knn_carve(void* base, const int64_t* node_off_host, int B, size_t* bytes) {
+static KnnWs knn_carve(void* base, const int64_t* node_off_host, int B, size_t* bytes, bool feat = false) {
   Carver c(base);
   const size_t w = knn_words(node_off_host, B, nullptr);
   KnnWs k;
@@ -194,12 +196,91 @@ static KnnWs knn_carve(void* base, const int64_t* node_off_host, int B, size_t* 
   k.arow = c.take<unsigned long long>((size_t)nt * 8);
   k.rows = c.take<unsigned long long>((size_t)nt * 8);
   k.rowstart = c.take<int>((size_t)nt);
+  k.doff = nullptr;
+  k.dkey = nullptr;
+  if (feat) {
+    size_t nn = 0;
+    for (int b = 0; b < B; ++b) {
+      const int64_t n = node_off_host[b + 1] - node_off_host[b];
+      nn += (size_t)n * (size_t)n;
+    }
+    k.doff = c.take<int64_t>(B + 1);
+    k.dkey = c.take<unsigned>(nn);
+  }
   if (bytes) *bytes = c.used;
   return k;
 }
 
-// One wave per query node i: the k+1 nearest (squared distance, then index), self dropped.
-__global__ __launch_bounds__(256) void knn_adj_kernel(const int64_t* __restrict__ jdet,
+// The distance a selection kernel ranks by. Positions (knn_mpn_graph, ConstructGraph.py:363-368):
+// the squared integer pixel distance. Features (feature_knn_mpn_graph, ConstructGraph.py:370-374):
+// the key matrix of fknn_dist_kernel, row i of image b at dkey + doff[b] + i n.
+struct KnnDist {
+  const int64_t* jdet;
+  const unsigned* dkey;   // null: positions
+  const int64_t* doff;
+  __device__ __forceinline__ long long operator()(int64_t base, int b, int n, int i, int j) const {
+    if (dkey) return (long long)dkey[doff[b] + (int64_t)i * n + j];
+    const long long dx = jdet[(base + j) * 3 + 0] - jdet[(base + i) * 3 + 0];
+    const long long dy = jdet[(base + j) * 3 + 1] - jdet[(base + i) * 3 + 1];
+    return dx * dx + dy * dy;
+  }
+};
+
+// feature_knn keys: torch_cluster 1.5.4's CUDA knn (the reference's knn_graph(features, k=50) on the
+// device) ranks candidates by tmp_dist += (x_j[c] - x_i[c]) * (x_j[c] - x_i[c]) over c in order, fp32,
+// which nvcc contracts to one fma per channel; restated here as that fma chain. A non-negative fp32
+// orders as its bit pattern; NaN (a NaN feature) becomes the largest key. Block per query node,
+// candidates across the threads, the query row broadcast from LDS.
+__global__ __launch_bounds__(256) void fknn_dist_kernel(const float* __restrict__ x, int C,
+                                                        const int64_t* __restrict__ node_off, int B,
+                                                        const int64_t* __restrict__ doff,
+                                                        unsigned* __restrict__ dkey) {
+  extern __shared__ float xq[];
+  const int64_t g = blockIdx.x;
+  const int b = find_segment(node_off, B, g);
+  const int64_t base = node_off[b];
+  const int n = (int)(node_off[b + 1] - base), i = (int)(g - base);
+  for (int c = threadIdx.x; c < C; c += blockDim.x) xq[c] = x[g * C + c];
+  __syncthreads();
+  unsigned* row = dkey + doff[b] + (int64_t)i * n;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    const float* xj = x + (base + j) * C;
+    float acc = 0.f;
+    int c = 0;
+    if ((C & 3) == 0) {
+      for (; c < C; c += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(xj + c);
+        float t = v.x - xq[c];
+        acc = __fmaf_rn(t, t, acc);
+        t = v.y - xq[c + 1];
+        acc = __fmaf_rn(t, t, acc);
+        t = v.z - xq[c + 2];
+        acc = __fmaf_rn(t, t, acc);
+        t = v.w - xq[c + 3];
+        acc = __fmaf_rn(t, t, acc);
+      }
+    }
+    for (; c < C; ++c) {
+      const float t = xj[c] - xq[c];
+      acc = __fmaf_rn(t, t, acc);
+    }
+    row[j] = acc != acc ? 0xffffffffu : __float_as_uint(acc);
+  }
+}
+
+__global__ void fknn_doff_kernel(const int64_t* __restrict__ node_off, int B, int64_t* __restrict__ doff) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int64_t w = 0;
+  for (int b = 0; b < B; ++b) {
+    doff[b] = w;
+    const int64_t n = node_off[b + 1] - node_off[b];
+    w += n * n;
+  }
+  doff[B] = w;
+}
+
+// One wave per query node i: the k+1 nearest (distance, then index), self dropped.
+__global__ __launch_bounds__(256) void knn_adj_kernel(KnnDist dist,
                                                       const int64_t* __restrict__ node_off, int B, int64_t n_total,
                                                       int kq, const int64_t* __restrict__ mat_off,
                                                       unsigned long long* __restrict__ adj,
@@ -214,11 +295,7 @@ __global__ __launch_bounds__(256) void knn_adj_kernel(const int64_t* __restrict_
   const int wpr = (n + 63) / 64;
   unsigned long long* A = adj + mat_off[b];
   unsigned long long* T = adjt + mat_off[b];
-  const int64_t xi = jdet[g * 3 + 0], yi = jdet[g * 3 + 1];
-  auto d2 = [&](int j) -> int64_t {
-    const int64_t dx = jdet[(base + j) * 3 + 0] - xi, dy = jdet[(base + j) * 3 + 1] - yi;
-    return dx * dx + dy * dy;
-  };
+  auto d2 = [&](int j) -> int64_t { return dist(base, b, n, i, j); };
   const int chunk = (n + 63) / 64;
   const int j0 = lane * chunk, j1 = min(n, j0 + chunk);
   if (n <= kq) {   // every node is among the k+1 nearest
@@ -229,7 +306,7 @@ __global__ __launch_bounds__(256) void knn_adj_kernel(const int64_t* __restrict_
     }
     return;
   }
-  // smallest tau with #{d2 <= tau} >= kq (binary search over the integer distance)
+  // smallest tau with #{d2 <= tau} >= kq (binary search over the integer distance / key)
   int64_t lo = 0, hi = 0;
   for (int j = j0; j < j1; ++j) hi = max(hi, d2(j));
 #pragma unroll
@@ -373,7 +450,7 @@ constexpr int KNN_LDS_MAXN = 512, KNN_W = KNN_LDS_MAXN / 64;
 
 __device__ __forceinline__ int ballot_count(bool p) { return __popcll(__ballot(p)); }
 
-__global__ __launch_bounds__(1024) void knn_select_kernel(const int64_t* __restrict__ jdet,
+__global__ __launch_bounds__(1024) void knn_select_kernel(KnnDist dist,
                                                           const int64_t* __restrict__ node_off, int B,
                                                           int64_t n_total, int kq,
                                                           unsigned long long* __restrict__ Arow) {
@@ -384,7 +461,6 @@ __global__ __launch_bounds__(1024) void knn_select_kernel(const int64_t* __restr
   const int64_t base = node_off[b];
   const int n = (int)(node_off[b + 1] - base), i = (int)(g - base);
   const int wpr = (n + 63) / 64;
-  const int64_t xi = jdet[g * 3 + 0], yi = jdet[g * 3 + 1];
   long long d[KNN_W];
   long long dmax = 0;
 #pragma unroll
@@ -392,8 +468,7 @@ __global__ __launch_bounds__(1024) void knn_select_kernel(const int64_t* __restr
     const int j = lane + 64 * r;
     d[r] = 0x7fffffffffffffffll;
     if (r < wpr && j < n) {
-      const long long dx = jdet[(base + j) * 3 + 0] - xi, dy = jdet[(base + j) * 3 + 1] - yi;
-      d[r] = dx * dx + dy * dy;
+      d[r] = dist(base, b, n, i, j);
       dmax = max(dmax, d[r]);
     }
   }
@@ -1159,8 +1234,8 @@ extern "C" int pemp_knn_graph_count(const int64_t* joint_det, const int64_t* nod
   const int64_t n_total = node_off_host[B];
   if (n_total > 0) {
     ProfScope prof("knn_adj", st);
-    hipLaunchKernelGGL(knn_adj_kernel, dim3((unsigned)((n_total + 3) / 4)), dim3(256), 0, st, joint_det, node_off, B,
-                       n_total, k + 1, w.mat_off, w.adj, w.adjt);
+    hipLaunchKernelGGL(knn_adj_kernel, dim3((unsigned)((n_total + 3) / 4)), dim3(256), 0, st,
+                       KnnDist{joint_det, nullptr, nullptr}, node_off, B, n_total, k + 1, w.mat_off, w.adj, w.adjt);
     PEMP_LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(knn_count_kernel, dim3(B), dim3(256), 0, st, node_off, B, w.mat_off, w.adj, w.adjt, edge_count);
@@ -1192,36 +1267,47 @@ extern "C" int pemp_knn_graph_emit(const int64_t* node_off, const int64_t* node_
 // and the emit are queued back to back; the edge total reaches the host through mapped memory
 // (e_total_host, written by the scan kernel while the emit runs). edge_buf holds 2 * e_cap int64: the
 // graph is its leading [2, E] block (source row at 0, destination row at E).
-extern "C" int pemp_knn_graph_build(const int64_t* joint_det, const int64_t* node_off, const int64_t* node_off_host,
-                                    int B, int k, void* workspace, size_t workspace_bytes, int64_t e_cap,
-                                    int64_t* edge_buf, int32_t* e_total_host, const float* joint_tags, int F,
-                                    const float* joint_scores, int J, float norm_factor, int mode, float* edge_attr,
-                                    void* stream) {
+static int knn_build(const char* who, const float* feat, int C, const int64_t* joint_det, const int64_t* node_off,
+                     const int64_t* node_off_host, int B, int k, void* workspace, size_t workspace_bytes,
+                     int64_t e_cap, int64_t* edge_buf, int32_t* e_total_host, const float* joint_tags, int F,
+                     const float* joint_scores, int J, float norm_factor, int mode, float* edge_attr,
+                     void* stream) {
   PEMP_CHECK_ARG(joint_det && node_off && node_off_host && workspace && edge_buf && B > 0 && k >= 1 && e_cap >= 0,
-                 "pemp_knn_graph_build: bad args");
+                 "%s: bad args", who);
   int A = 0;
   if (edge_attr) {
-    PEMP_CHECK_ARG(J > 0, "pemp_knn_graph_build: J <= 0");
+    PEMP_CHECK_ARG(J > 0, "%s: J <= 0", who);
     A = ef_width(mode, J);
-    if (A < 0) { set_error("pemp_knn_graph_build: unknown mode %d", mode); return PEMP_ERR_INVALID_ARG; }
-    if (const int rc = ef_tag_check(mode, joint_tags, F, "pemp_knn_graph_build")) return rc;
-    PEMP_CHECK_ARG(mode != PEMP_EF_AE_NORMED || joint_scores, "pemp_knn_graph_build: ae_normed needs joint_scores");
+    if (A < 0) { set_error("%s: unknown mode %d", who, mode); return PEMP_ERR_INVALID_ARG; }
+    if (const int rc = ef_tag_check(mode, joint_tags, F, who)) return rc;
+    PEMP_CHECK_ARG(mode != PEMP_EF_AE_NORMED || joint_scores, "%s: ae_normed needs joint_scores", who);
   }
+  const bool fk = feat != nullptr;
   size_t need = 0;
-  knn_carve(nullptr, node_off_host, B, &need);
+  knn_carve(nullptr, node_off_host, B, &need, fk);
   if (workspace_bytes < need) {
-    set_error("pemp_knn_graph_build: workspace %zu < %zu", workspace_bytes, need);
+    set_error("%s: workspace %zu < %zu", who, workspace_bytes, need);
     return PEMP_ERR_WORKSPACE;
   }
   int64_t bound = 0;   // every node keeps min(k, n - 1) nearest; the union with the reverse at most doubles it
   for (int b = 0; b < B; ++b) {
     const int64_t n = node_off_host[b + 1] - node_off_host[b];
-    PEMP_CHECK_ARG(n >= 0, "pemp_knn_graph_build: decreasing node offsets");
+    PEMP_CHECK_ARG(n >= 0, "%s: decreasing node offsets", who);
     bound += std::min<int64_t>(n * (n > 0 ? n - 1 : 0), 2 * (int64_t)k * n);
   }
-  PEMP_CHECK_ARG(e_cap >= bound, "pemp_knn_graph_build: e_cap %lld < bound %lld", (long long)e_cap, (long long)bound);
-  const KnnWs w = knn_carve(workspace, node_off_host, B, nullptr);
+  PEMP_CHECK_ARG(e_cap >= bound, "%s: e_cap %lld < bound %lld", who, (long long)e_cap, (long long)bound);
+  const KnnWs w = knn_carve(workspace, node_off_host, B, nullptr, fk);
   const hipStream_t st = as_stream(stream);
+  KnnDist dist{joint_det, nullptr, nullptr};
+  if (fk && node_off_host[B] > 0) {   // the n_b x n_b feature-distance keys of every image
+    ProfScope prof("fknn_dist", st);
+    hipLaunchKernelGGL(fknn_doff_kernel, dim3(1), dim3(64), 0, st, node_off, B, w.doff);
+    PEMP_LAUNCH_CHECK();
+    hipLaunchKernelGGL(fknn_dist_kernel, dim3((unsigned)node_off_host[B]), dim3(256), (size_t)C * sizeof(float), st,
+                       feat, C, node_off, B, w.doff, w.dkey);
+    PEMP_LAUNCH_CHECK();
+    dist = KnnDist{joint_det, w.dkey, w.doff};
+  }
   int* e_dev_host = nullptr;   // device address of the caller's mapped host word
   if (e_total_host) PEMP_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&e_dev_host), e_total_host, 0));
   int64_t nmax = 0;
@@ -1230,8 +1316,8 @@ extern "C" int pemp_knn_graph_build(const int64_t* joint_det, const int64_t* nod
     ProfScope prof("knn_build", st);
     const int64_t n_all = node_off_host[B];
     if (n_all > 0) {
-      hipLaunchKernelGGL(knn_select_kernel, dim3((unsigned)((n_all + 15) / 16)), dim3(1024), 0, st, joint_det, node_off,
-                         B, n_all, k + 1, w.arow);
+      hipLaunchKernelGGL(knn_select_kernel, dim3((unsigned)((n_all + 15) / 16)), dim3(1024), 0, st, dist, node_off, B,
+                         n_all, k + 1, w.arow);
       PEMP_LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(knn_rows_kernel, dim3(B), dim3(1024), 0, st, node_off, w.arow, w.rows, w.rowstart, w.ecount);
@@ -1253,7 +1339,7 @@ extern "C" int pemp_knn_graph_build(const int64_t* joint_det, const int64_t* nod
   const int64_t n_total = node_off_host[B];
   ProfScope prof("knn_build", st);
   if (n_total > 0) {
-    hipLaunchKernelGGL(knn_adj_kernel, dim3((unsigned)((n_total + 3) / 4)), dim3(256), 0, st, joint_det, node_off, B,
+    hipLaunchKernelGGL(knn_adj_kernel, dim3((unsigned)((n_total + 3) / 4)), dim3(256), 0, st, dist, node_off, B,
                        n_total, k + 1, w.mat_off, w.adj, w.adjt);
     PEMP_LAUNCH_CHECK();
   }
@@ -1273,6 +1359,37 @@ extern "C" int pemp_knn_graph_build(const int64_t* joint_det, const int64_t* nod
     }
   }
   return PEMP_OK;
+}
+
+extern "C" int pemp_knn_graph_build(const int64_t* joint_det, const int64_t* node_off, const int64_t* node_off_host,
+                                    int B, int k, void* workspace, size_t workspace_bytes, int64_t e_cap,
+                                    int64_t* edge_buf, int32_t* e_total_host, const float* joint_tags, int F,
+                                    const float* joint_scores, int J, float norm_factor, int mode, float* edge_attr,
+                                    void* stream) {
+  return knn_build("pemp_knn_graph_build", nullptr, 0, joint_det, node_off, node_off_host, B, k, workspace,
+                   workspace_bytes, e_cap, edge_buf, e_total_host, joint_tags, F, joint_scores, J, norm_factor, mode,
+                   edge_attr, stream);
+}
+
+extern "C" size_t pemp_feature_knn_workspace_size(const int64_t* node_off_host, int B) {
+  if (!node_off_host || B <= 0) return 0;
+  size_t bytes = 0;
+  knn_carve(nullptr, node_off_host, B, &bytes, true);
+  return bytes;
+}
+
+extern "C" int pemp_feature_knn_graph_build(const float* x, int C, const int64_t* joint_det, const int64_t* node_off,
+                                            const int64_t* node_off_host, int B, int k, void* workspace,
+                                            size_t workspace_bytes, int64_t e_cap, int64_t* edge_buf,
+                                            int32_t* e_total_host, const float* joint_tags, int F,
+                                            const float* joint_scores, int J, float norm_factor, int mode,
+                                            float* edge_attr, void* stream) {
+  PEMP_CHECK_ARG(x && C > 0 && C <= 8192, "pemp_feature_knn_graph_build: x null or C %d out of (0, 8192]", C);
+  PEMP_CHECK_ARG((reinterpret_cast<uintptr_t>(x) & 15) == 0 || (C & 3) != 0,
+                 "pemp_feature_knn_graph_build: x not 16-byte aligned");
+  return knn_build("pemp_feature_knn_graph_build", x, C, joint_det, node_off, node_off_host, B, k, workspace,
+                   workspace_bytes, e_cap, edge_buf, e_total_host, joint_tags, F, joint_scores, J, norm_factor, mode,
+                   edge_attr, stream);
 }
 
 extern "C" size_t pemp_score_graph_workspace_size(const int64_t* node_off_host, int B, int k) {

@@ -3,7 +3,7 @@
 Same constructor signature, same ``construct_graph()`` 15-tuple, same dtypes (int64 indices) and
 node/edge order as the reference; computed by ``libpemp.so`` (``pemp_detect``,
 ``pemp_pack_nodes``, ``pemp_fully_graph_build`` / ``pemp_knn_graph_*`` / ``pemp_score_graph``,
-``pemp_edge_features``). GRAPH_TYPE fully, knn and score_based (``ConstructGraph.py:272-283``).
+``pemp_edge_features``). GRAPH_TYPE fully, knn, feature_knn and score_based (``ConstructGraph.py:272-283``).
 Host synchronisation: one count read-back after detection (the reference syncs at every
 ``nonzero``), plus one more for knn graphs.
 """
@@ -291,9 +291,13 @@ class NaiveGraphConstructor:
                                          _lib.ptr(joint_scores), _lib.ptr(batch_index), _lib.ptr(joint_tags), st))
             if proj_tags is not None:   # before the edge features, which may read them
                 joint_tags = self._gather_proj_tags(L, st, proj_tags, J, H, W, joint_det, batch_index, N, dev)
-            if self.mpn_graph_type == "knn":   # edge features written by the knn emit itself
+            if self.mpn_graph_type in ("knn", "feature_knn"):   # edge features written by the knn emit itself
+                if self.mpn_graph_type == "feature_knn" and projected:   # the graph ranks by x: sample it first
+                    self._gather_projected(L, st, pmaps, pconv, H, W, joint_det, batch_index, x)
+                    projected = False
                 edge_index, edge_attr = self._knn_edges(L, st, joint_det, joint_tags, F, joint_scores, node_off,
-                                                        node_off_h, B, J, A, norm, mode, dev)
+                                                        node_off_h, B, J, A, norm, mode, dev,
+                                                        x if self.mpn_graph_type == "feature_knn" else None)
             else:
                 edge_index = self._edges(L, st, joint_det, joint_scores, node_off, fully_off, node_off_h, B, dev)
                 E = edge_index.shape[1]
@@ -370,15 +374,19 @@ class NaiveGraphConstructor:
     _KNN_K = 50   # ConstructGraph.py:365 (knn_graph(k=50))
 
     def _knn_edges(self, L, st, joint_det, joint_tags, F, joint_scores, node_off, node_off_h, B, J, A, norm, mode,
-                   dev):
+                   dev, x=None):
         """knn_mpn_graph (ConstructGraph.py:363-368) + the edge features in one queued call
         (pemp_knn_graph_build): buffers sized by the closed-form edge bound, the total back through
         mapped memory while the emit still runs; edge_index / edge_attr are the leading contiguous
-        [2, E] / [E, A] blocks of those buffers."""
+        [2, E] / [E, A] blocks of those buffers. With x: feature_knn_mpn_graph (ConstructGraph.py:370-374),
+        the same graph over the node features x [N, C] (pemp_feature_knn_graph_build)."""
         k = self._KNN_K
         nh = np.ascontiguousarray(node_off_h)
         nh_p = nh.ctypes.data_as(ctypes.c_void_p)
-        ws = self._ws_knn.get(L.pemp_knn_workspace_size(nh_p, B), dev)
+        if x is not None:
+            ws = self._ws_knn.get(L.pemp_feature_knn_workspace_size(nh_p, B), dev)
+        else:
+            ws = self._ws_knn.get(L.pemp_knn_workspace_size(nh_p, B), dev)
         n = np.diff(nh)
         e_cap = int(np.minimum(n * np.maximum(n - 1, 0), 2 * k * n).sum())
         buf = torch.empty(2 * max(e_cap, 1), dtype=torch.int64, device=dev)
@@ -387,9 +395,13 @@ class NaiveGraphConstructor:
         try:
             word = ent[2][:1]
             word.fill(-1)
-            _lib.check(L.pemp_knn_graph_build(_lib.ptr(joint_det), _lib.ptr(node_off), nh_p, B, k, _lib.ptr(ws),
-                                              ws.numel(), e_cap, _lib.ptr(buf), ent[1], _lib.ptr(joint_tags), F,
-                                              _lib.ptr(joint_scores), J, norm, mode, _lib.ptr(ea), st))
+            args = (_lib.ptr(joint_det), _lib.ptr(node_off), nh_p, B, k, _lib.ptr(ws), ws.numel(), e_cap,
+                    _lib.ptr(buf), ent[1], _lib.ptr(joint_tags), F, _lib.ptr(joint_scores), J, norm, mode,
+                    _lib.ptr(ea), st)
+            if x is not None:
+                _lib.check(L.pemp_feature_knn_graph_build(_lib.ptr(x), x.shape[1], *args))
+            else:
+                _lib.check(L.pemp_knn_graph_build(*args))
             E = self._wait_counts(word, dev)[0]
         except BaseException:
             torch.cuda.current_stream(dev).synchronize()

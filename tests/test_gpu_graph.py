@@ -50,6 +50,9 @@ CASES = [
     (1, 17, 33, 17, 1, "clean", "fully", 7, 0.1, False),        # tiny, odd sizes
     (8, 17, 640, 640, 9, "clean", "score_based", 5, 0.1, False),  # C3 shape, score_based (k = 75 roots)
     (1, 14, 640, 640, 36, "clean", "score_based", 5, 0.1, False), # C5 shape, score_based
+    (8, 17, 640, 640, 9, "clean", "feature_knn", 5, 0.1, False),  # C3 shape, feature_knn (N ~ 150 > k + 1)
+    (2, 17, 320, 320, 40, "clean", "feature_knn", 3, 0.1, False), # feature_knn with n > 512 (global path)
+    (1, 17, 64, 64, 1, "clean", "feature_knn", 5, 0.1, False),    # n <= k + 1: every pair
 ]
 
 
@@ -137,6 +140,31 @@ def test_projected_features(graph_type, scales):
             assert torch.equal(out[i].cpu(), ref[i]), i
         assert out[0].shape == ref[0].shape
         assert (out[0].cpu() - ref[0]).abs().max().item() <= 2e-6
+
+
+def test_feature_knn_projected_and_duplicates():
+    """feature_knn (ConstructGraph.py:370-374) ranks by x, so with features=ProjectedMaps the product
+    samples x before the graph build; the graph must equal the oracle's feature_knn over that same x.
+    Duplicate feature rows (equal distances at the 51st boundary) resolve by node index."""
+    from pemp_amd.frontend import ProjectedMaps
+    B, J, H, W = 2, 17, 160, 160
+    hm = torch.from_numpy(syn.make_heatmaps(33, B, J, H, W, 5, margin=4))
+    pm = ProjectedMaps([torch.from_numpy(syn.closed_form((B, 128, 80, 80), 0.35))], (H, W))
+    gc = pcfg.inference_gc_config("feature_knn", 5, False)
+    out = run_gc(gc, J, hm, pm, None, None)
+    x, ei, bi = out[0].cpu(), out[2].cpu(), out[12].cpu()
+    parts, off = [], 0
+    for b in range(B):
+        n = int((bi == b).sum())
+        parts.append(restate.feature_knn_edge_index(x[off:off + n]) + off)
+        off += n
+    assert torch.equal(ei, torch.cat(parts, 1))
+    # constant features: every distance ties at 0 -> the 51 lowest indices of each image, symmetrised
+    feats = torch.ones(B, 16, H, W)
+    out = run_gc(gc, J, hm, feats, None, None)
+    ref = restate.construct_graph(hm, feats, torch.zeros(B, J, H, W), None, gc, J)
+    for i in (0, 1, 2, 7, 12):
+        assert torch.equal(out[i].cpu(), ref[i]), i
 
 
 @pytest.mark.parametrize("graph", ["fully", "knn"])
