@@ -165,7 +165,7 @@ GC_CASES = {
                             graph="feature_knn", pool=5, thr=0.1, mask_crowds=False), False),
     "gc_feature_knn_small": (dict(seed=16, B=2, J=14, H=64, W=80, C=32, F=2, persons=2, variant="noisy",
                                   graph="feature_knn", pool=3, thr=0.1, mask_crowds=False,
-                                  features=["position", "angle", "connection_type"]), True),
+                                  features=["position", "connection_type", "ae_normed"]), True),
     "gc_score_based": (dict(seed=8, B=2, J=17, H=128, W=128, C=128, F=1, persons=6, variant="clean",
                             graph="score_based", pool=5, thr=0.1, mask_crowds=False), False),
     "gc_score_based_nothr": (dict(seed=9, B=1, J=17, H=64, W=80, C=128, F=1, persons=2, variant="noisy",
