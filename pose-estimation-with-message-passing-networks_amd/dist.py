@@ -14,12 +14,19 @@ import torch.distributed as dist
 
 def init_from_env(backend="nccl"):
     """(rank, world, device) from the torchrun environment; initialises the process group when
-    WORLD_SIZE > 1 (rendezvous on 127.0.0.1 unless MASTER_ADDR is set)."""
+    WORLD_SIZE > 1 (rendezvous on 127.0.0.1 unless MASTER_ADDR is set).
+
+    Rehearsal knobs (one-GPU boxes; never the production setting): PEMP_DIST_BACKEND=gloo runs the
+    collectives over gloo on host copies while every rank still computes on its GPU, and
+    PEMP_SHARE_DEVICE=1 puts every rank on cuda:0 (RCCL refuses two ranks on one device)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if backend == "nccl":
-        dev = torch.device("cuda", local if world > 1 else 0)
+    gpu = backend == "nccl"
+    backend = os.environ.get("PEMP_DIST_BACKEND", backend) if gpu else backend
+    if gpu:
+        shared = os.environ.get("PEMP_SHARE_DEVICE", "0") == "1"
+        dev = torch.device("cuda", local if world > 1 and not shared else 0)
         torch.cuda.set_device(dev)
     else:
         dev = torch.device("cpu")
@@ -28,6 +35,11 @@ def init_from_env(backend="nccl"):
         kw = {"device_id": dev} if backend == "nccl" else {}
         dist.init_process_group(backend, rank=rank, world_size=world, **kw)
     return rank, world, dev
+
+
+def _coll_dev(dev):
+    """Where collective buffers live: the rank's device under RCCL, host memory under gloo."""
+    return torch.device("cpu") if dist.is_initialized() and dist.get_backend() == "gloo" else dev
 
 
 def image_block(total, rank, world):
@@ -45,7 +57,7 @@ def barrier(world):
 def _reduce(v, world, dev, op):
     if world == 1:
         return v
-    t = torch.tensor([v], dtype=torch.float64, device=dev)
+    t = torch.tensor([v], dtype=torch.float64, device=_coll_dev(dev))
     dist.all_reduce(t, op=op)
     return float(t.item())
 
@@ -72,6 +84,7 @@ def gather_poses(per_image, image_ids, num_joints, world, dev):
     if world == 1:
         return list(image_ids), list(per_image)
     p_local = max([0] + [0 if p is None else int(p.shape[0]) for p in per_image])
+    dev = _coll_dev(dev)
     t = torch.tensor([p_local, n_local], dtype=torch.int64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     cap, n_max = max(1, int(t[0])), max(1, int(t[1]))

@@ -272,3 +272,38 @@ def test_f16_range_scaling():
         scale = max(b.abs().max().item(), 1.0)
         assert torch.isfinite(a).all()
         assert max_err(a, b) < 1e-5 * scale
+
+
+def test_batches_in_flight_on_two_streams():
+    """bench.py's serving-style loop: whole steps (construct_graph + MPN forward) issued round-robin on two
+    HIP streams, so one batch's detection overlaps the previous batch's MPN. Each stream has its own
+    library scratch and side stream; every step's outputs must equal the same batch run serially."""
+    B, J, H, W = 4, 17, 256, 256
+    gc = pcfg.inference_gc_config("fully", 5, False)
+    cfg = pcfg.published_mpn_config(J, steps=3, variant="attn")
+    model, _ = make_model(cfg, 0.5)
+    feats = torch.from_numpy(syn.closed_form((B, 128, H, W), 0.25)).to(DEV)
+    tags = torch.from_numpy(syn.closed_form((B, J, H, W, 1), 0.75)).to(DEV)
+    hms = [torch.from_numpy(syn.make_heatmaps(40 + k, B, J, H, W, persons=3 + k % 3, margin=4)).to(DEV)
+           for k in range(6)]
+
+    def step(hm):
+        out = pemp_amd.get_graph_constructor(gc, scoremaps=hm, features=feats, tagmaps=tags, joints_gt=None,
+                                             factor_list=None, masks=None, device=DEV, testing=True,
+                                             heatmaps=None, num_joints=J).construct_graph()
+        with torch.no_grad():
+            pe, pn, pc, _ = model(out[0], out[1], out[2], node_types=out[7][:, 2])
+        return out[2], pe[-1], pn[-1], pc[-1]
+
+    serial = [tuple(t.cpu() for t in step(hm)) for hm in hms]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.current_stream(DEV), torch.cuda.Stream(DEV)]
+    for _ in range(2):
+        got = []
+        for k, hm in enumerate(hms):
+            with torch.cuda.stream(streams[k % 2]):
+                got.append(step(hm))
+        torch.cuda.synchronize()
+        for k in range(len(hms)):
+            for a, b in zip(got[k], serial[k]):
+                assert torch.equal(a.cpu(), b), k
