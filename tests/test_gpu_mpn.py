@@ -307,3 +307,30 @@ def test_batches_in_flight_on_two_streams():
         for k in range(len(hms)):
             for a, b in zip(got[k], serial[k]):
                 assert torch.equal(a.cpu(), b), k
+
+
+def test_feature_knn_graph_end_to_end():
+    """feature_knn graph (ConstructGraph.py:370-374) built on the device and fed to the MPN (the general
+    sorting prepare: not a fully graph) matches the oracle's graph bit for bit and its logits within 1e-4."""
+    B, J, H, W = 2, 17, 192, 192
+    hm = torch.from_numpy(syn.make_heatmaps(71, B, J, H, W, persons=5, margin=4))
+    feats = torch.from_numpy(syn.closed_form((B, 128, H, W), 0.25))
+    tags = torch.from_numpy(syn.closed_form((B, J, H, W, 1), 0.75))
+    gc = pcfg.inference_gc_config("feature_knn", 5, False)
+    out = pemp_amd.get_graph_constructor(gc, scoremaps=hm.to(DEV), features=feats.to(DEV), tagmaps=tags.to(DEV),
+                                         joints_gt=None, factor_list=None, masks=None, device=DEV, testing=True,
+                                         heatmaps=None, num_joints=J).construct_graph()
+    ref = restate.construct_graph(hm, feats, tags, None, gc, J)
+    for i in (0, 1, 2, 7):
+        assert torch.equal(out[i].cpu(), ref[i]), i
+    n = out[0].shape[0]
+    assert out[2].shape[1] < n * (n - 1)                             # a real knn graph, not fully
+    cfg = pcfg.published_mpn_config(J, steps=3, variant="attn")
+    model, sd = make_model(cfg, 0.5)
+    with torch.no_grad():
+        pe, pn, pc, _ = model(out[0], out[1], out[2], node_types=out[7][:, 2])
+    torch.cuda.synchronize()
+    rpe, rpn, rpc, _ = restate.mpn_forward(sd, cfg, ref[0], ref[1], ref[2], ref[7][:, 2])
+    assert max_err(pe[-1], rpe[-1]) <= TOL
+    assert max_err(pn[-1], rpn[-1]) <= TOL
+    assert max_err(pc[-1], rpc[-1]) <= TOL

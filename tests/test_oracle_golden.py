@@ -56,3 +56,38 @@ def test_per_type_attention_golden_distinguishes_rows():
     pe, pn, pc, _ = restate.mpn_forward(sd, cfg, torch.from_numpy(a["x"]), torch.from_numpy(a["edge_attr"]),
                                         torch.from_numpy(a["edge_index"]), torch.from_numpy(a["node_types"]))
     assert np.abs(pc[-1].numpy() - a["class_logits"]).max() > 5e-4      # 5x the logit tolerance
+
+
+def test_feature_knn_restatement_properties():
+    """feature_knn_edge_index (ConstructGraph.py:370-374): symmetric, no self loops, sorted by (src, dst);
+    n <= k + 1 gives the fully graph; every node keeps its k nearest by the fp32 fma-chain distance
+    (exact f64 check on a draw without near-ties); duplicate feature rows tie by node index."""
+    g = torch.Generator().manual_seed(5)
+    for n in (0, 1, 2, 51, 52, 130):
+        x = torch.randn(n, 24, generator=g)
+        ei = restate.feature_knn_edge_index(x)
+        if n <= 51:
+            assert torch.equal(ei, restate.fully_edge_index(n))
+            continue
+        s, d = ei
+        assert bool((s != d).all())
+        key = s * n + d
+        assert bool((key[1:] > key[:-1]).all())                      # coalesced order, no duplicates
+        adj = torch.zeros(n, n, dtype=torch.bool)
+        adj[s, d] = True
+        assert torch.equal(adj, adj.t())
+        d64 = ((x[:, None, :].double() - x[None, :, :].double()) ** 2).sum(-1)
+        d64.fill_diagonal_(float("inf"))
+        nearest = torch.argsort(d64, dim=1)[:, :50]
+        assert bool(adj.gather(1, nearest).all())                    # each node's 50 nearest are neighbours
+        assert int(adj.sum(1).min()) >= 50
+    # all rows equal: every distance ties at 0 -> nodes 0..50 for every query, symmetrised
+    n = 80
+    ei = restate.feature_knn_edge_index(torch.ones(n, 8))
+    adj = torch.zeros(n, n, dtype=torch.bool)
+    adj[ei[0], ei[1]] = True
+    want = torch.zeros(n, n, dtype=torch.bool)
+    want[:, :51] = True
+    want = want | want.t()
+    want.fill_diagonal_(False)
+    assert torch.equal(adj, want)
