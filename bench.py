@@ -35,8 +35,13 @@ WORKLOADS = {
     "c2": dict(B=1, J=17, H=640, W=640, persons=9, steps=3, graph="fully", variant="attn"),
     # configs[4] (C5): CrowdPose-dense, ~500 detections / ~250k directed edges per image
     "c5": dict(B=1, J=14, H=640, W=640, persons=36, steps=3, graph="fully", variant="attn"),
+    # configs[1] at its stated arithmetic: every per-edge GEMM in exact fp32 MFMA
+    "c2fp32": dict(B=1, J=17, H=640, W=640, persons=9, steps=3, graph="fully", variant="attn", precision="fp32"),
     # C3 with the secondary graph type: k = 50 nearest neighbours, symmetrised
     "c3knn": dict(B=8, J=17, H=640, W=640, persons=9, steps=3, graph="knn", variant="attn"),
+    # the published model on C3 (experiments/hybrid_class_agnostic_end2end/model_58_4_4.yaml:97,155):
+    # GRAPH_TYPE knn, STEPS 10
+    "c3knn10": dict(B=8, J=17, H=640, W=640, persons=9, steps=10, graph="knn", variant="attn"),
 }
 FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: dense f32 MFMA (= f32 vector) peak
 HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
@@ -89,6 +94,8 @@ def make_model(wl, dev):
     cfg = pcfg.published_mpn_config(wl["J"], wl["steps"], wl["variant"])
     model = pemp_amd.get_mpn_model(cfg)
     model.load_state_dict(syn.closed_form_state_dict(model, 0.5))
+    if wl.get("precision"):
+        model.precision = wl["precision"]
     return model.eval().to(dev), cfg
 
 
@@ -117,18 +124,21 @@ def edge_pass_cost(head, upd):
     return flop, byts
 
 
-def pmc_traffic(kernel_prefix):
-    """HBM bytes per dispatch of the kernel from the committed PMC passes (profiles/pmc_latest.json),
-    or None when no pass covers it."""
+def pmc_traffic(kernel_prefix, workload, E):
+    """HBM bytes per dispatch of the kernel from the committed PMC passes (profiles/pmc_latest.json,
+    tools/pmc_json.py), for a pass over the same workload and edge count; None when no pass covers it."""
     try:
-        ks = json.load(open(PMC_FILE))["kernels"]
+        runs = json.load(open(PMC_FILE))["runs"]
     except (OSError, ValueError, KeyError):
         return None
-    hits = [v for k, v in ks.items() if k.startswith(kernel_prefix)]
-    return hits[0]["bytes"] if len(hits) == 1 else None
+    for run in runs:
+        if run.get("workload") == workload and run.get("edges") == E:
+            hits = [v for k, v in run["kernels"].items() if k.startswith(kernel_prefix)]
+            return hits[0]["bytes"] if len(hits) == 1 else None
+    return None
 
 
-def roofline_for(label, stats, E, wl, precision, upd):
+def roofline_for(label, stats, E, wl, precision, upd, workload):
     """Roofline of the dominant kernel from its measured average launch time.
 
     edge_step*: executed FLOP and ALGORITHMIC HBM bytes per edge from edge_pass_cost (node-table
@@ -147,9 +157,9 @@ def roofline_for(label, stats, E, wl, precision, upd):
         f1, b1 = edge_pass_cost(head, upd)
         flop, byts = E * f1, E * b1
         gbs = byts / avg_s / 1e9
-        traffic = pmc_traffic("pemp::edge_step_kernel<0," + ("1" if head else "0"))
+        traffic = pmc_traffic("pemp::edge_step_kernel<0," + ("1" if head else "0"), workload, E)
         common = {"kernel": label, "avg_launch_us": round(avg_s * 1e6, 2), "launches": n, "traffic": traffic,
-                  "traffic_source": "profiles/pmc_latest.json" if traffic else None,
+                  "traffic_source": f"profiles/pmc_latest.json ({workload}, E={E})" if traffic else None,
                   "algorithmic": f"{f1} FLOP and {b1} B HBM x E={E} edges per launch",
                   "tflops_executed": round(flop / avg_s / 1e12, 2), "hbm_GBs_algorithmic": round(gbs, 1),
                   "ref_equiv_tflops": round(E * REF_EDGE_FLOP / avg_s / 1e12, 2), "precision": precision}
@@ -168,10 +178,10 @@ def roofline_for(label, stats, E, wl, precision, upd):
     if label == "detect_nms":
         byts = B * J * H * W * 4
         ach = byts / avg_s / 1e9
-        traffic = pmc_traffic("pemp::nms_strips_kernel")
+        traffic = pmc_traffic("pemp::nms_strips_kernel", workload, E)
         return {"kernel": label, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "traffic_source": "profiles/pmc_latest.json" if traffic else None,
+                "traffic_source": f"profiles/pmc_latest.json ({workload}, E={E})" if traffic else None,
                 "avg_launch_us": round(avg_s * 1e6, 2), "launches": n,
                 "algorithmic": f"{byts} B per launch (heatmap read once)"}
     return {"kernel": label, "avg_launch_us": round(avg_s * 1e6, 2), "launches": n}
@@ -547,7 +557,7 @@ def main():
             grouping["pose_all_gather_error"] = repr(exc)[:200]
 
     upd = wl["variant"] in ("attn", "mean")      # update block pre-applied in the edge pass (mpn.hip UPD)
-    roof = roofline_for(dominant, stats_timed, E, wl, model.precision, upd) if dominant else None
+    roof = roofline_for(dominant, stats_timed, E, wl, model.precision, upd, args.workload) if dominant else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(wl, gc, model, hm, feats, tags, args.cpu_seconds)

@@ -28,8 +28,9 @@ def ProjectedMaps(maps, size, divisor=None, gather=None):
     return _p(maps, size, divisor, gather)
 
 
-def ProjectedHeatmaps(outputs, size, num_joints, flip_outputs=None, flip_index=None, divisor=None, tag_scale=0):
+def ProjectedHeatmaps(outputs, size, num_joints, flip_outputs=None, flip_index=None, divisor=None, tag_scale=0,
+                      tag_per_joint=True):
     """The test front-end's image-size heatmaps / tags evaluated on demand, for ``scoremaps=`` and
     ``tagmaps=`` (frontend.py)."""
     from .frontend import ProjectedHeatmaps as _p
-    return _p(outputs, size, num_joints, flip_outputs, flip_index, divisor, tag_scale)
+    return _p(outputs, size, num_joints, flip_outputs, flip_index, divisor, tag_scale, tag_per_joint)

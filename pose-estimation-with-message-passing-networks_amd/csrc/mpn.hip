@@ -201,7 +201,7 @@ __device__ __forceinline__ float scan_max_bwd(float v, const SegMask& m) {
 // Workspace
 // ---------------------------------------------------------------------------------------------
 struct MpnWs {
-  int *cnt, *seg, *wg_start, *perm, *s_src, *s_dst, *s_orig, *err;
+  int *cnt, *seg, *wg_start, *perm, *s_src, *s_dst, *s_orig, *err, *sym;
   float *X, *NT, *agg, *Q0, *EA, *EB, *img, *eimg;
   int4* ranges;
 };
@@ -232,6 +232,7 @@ static MpnWs mpn_carve(void* base, int T, int64_t N, int64_t E, size_t* bytes) {
   const int G = std::max(num_cus(), T);       // edge-pass grid
   w.ranges = c.take<int4>((size_t)G * (EDGE_WAVES + 12));
   w.eimg = c.take<float>((size_t)T * EIMG_MAX_STRIDE);   // edge-pass weight image when the caller has none
+  w.sym = c.take<int>(64 * (4 + MAXT));                  // symmetric prepare: per-image records (SYM_REC)
   if (bytes) *bytes = c.used;
   return w;
 }
@@ -563,9 +564,12 @@ __device__ __forceinline__ void gemm_bf3(const __bf16* W, const bf16x8_t (&hi)[2
 // per-edge state r, Q0 and the node table that feed them, live in the 2^11 domain (dom<PREC>());
 // the split of a fragment folds the 2^-11 back in (v_fma_mix with a scale operand), biases and
 // attention rows come pre-scaled in the weight image, and results leave the domain once, where the
-// segments are normalised. Range: f16 holds |x| < 65504, so a wave whose (scaled) fragment reaches
-// 2^14 splits x·2^-16 instead and its GEMMs rescale by 2^16 (exact powers of two; rare, uniform
-// branch); the host keeps |w| < 32. Same fragment slot order and LDS row layout as bf16x3.
+// segments are normalised. Range: f16 holds |x| < 65504, so an item (edge / node column) whose (scaled)
+// values reach 2^14 is split at x·2^-k, the smallest such power of two that brings it under 2^14, and the
+// GEMMs rescale that item's accumulator column by 2^k (exact; rare: a uniform branch selects the rescaling
+// body when any item of the wave needs it, and the other items keep factor 1, so their precision does not
+// depend on their neighbours); the host keeps |w'| <= 65504. Same fragment slot order and LDS row layout
+// as bf16x3.
 typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 constexpr float F16_BIG = 16384.0f, F16_DOWN = 1.0f / 65536.0f, F16_UP = 65536.0f;
@@ -574,28 +578,52 @@ __host__ __device__ constexpr float dom() { return PREC == 2 ? 2048.0f : 1.0f; }
 template <int PREC>
 __host__ __device__ constexpr float dom_inv() { return PREC == 2 ? 1.0f / 2048.0f : 1.0f; }
 
-// f16 pair of (s x0, s x1): hi = f16(s x), lo = f16(s x - hi) -- v_fma_mix: exact fp32 fma, one rounding
+// f16 pair of (s x0, s x1): hi = f16(s x), lo = f16(s x - hi) -- v_fma_mix: exact fp32 fma, one rounding.
+// s is a per-lane factor (a VGPR operand): the item's power-of-two range scale folded into the split.
 __device__ __forceinline__ void split_pair(float x0, float x1, float s, uint32_t& hi, uint32_t& lo) {
   asm("v_fma_mixlo_f16 %0, %2, %4, 0\n\t"
       "v_fma_mixhi_f16 %0, %3, %4, 0\n\t"
       "v_fma_mixlo_f16 %1, %2, %4, -%0 op_sel_hi:[0,0,1]\n\t"
       "v_fma_mixhi_f16 %1, %3, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
       : "=&v"(hi), "=&v"(lo)
-      : "v"(x0), "v"(x1), "s"(s));
+      : "v"(x0), "v"(x1), "v"(s));
+}
+
+__device__ __forceinline__ float frag_absmax(const float (&x)[4][4]) {
+  float m = 0.0f;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) m = fmaxf(m, fmaxf(fmaxf(fabsf(x[b][0]), fabsf(x[b][1])), fmaxf(fabsf(x[b][2]), fabsf(x[b][3]))));
+  return m;
 }
 
 // wave-uniform: some |s x| of the fragment reaches 2^14 (or is NaN): take the range-scaled split
 __device__ __forceinline__ bool f16_big(const float (&x)[4][4], float s) {
-  float m = 0.0f;
-#pragma unroll
-  for (int b = 0; b < 4; ++b) m = fmaxf(m, fmaxf(fmaxf(fabsf(x[b][0]), fabsf(x[b][1])), fmaxf(fabsf(x[b][2]), fabsf(x[b][3]))));
-  return __any(!(m * s < F16_BIG));
+  return __any(!(frag_absmax(x) * s < F16_BIG));
 }
 
-// split of the fragment s·x (s a power of two); returns the wave's range flag (then the parts hold s·x·2^-16)
-__device__ __forceinline__ bool split_f16(const float (&x)[4][4], float s, f16x8_t (&hi)[2], f16x8_t (&lo)[2]) {
-  const bool big = f16_big(x, s);
-  const float ss = big ? s * F16_DOWN : s;
+// Range scale of one item (the lane column c = lane & 15; its 64 features sit in lanes c, c+16, c+32, c+48):
+// the largest power of two 2^-k, k >= 0, that brings the item's max |s x| under 2^14 -- 1 for every item
+// already in range, so an item's precision never depends on the other items of the wave. m = item max
+// (partial: this lane's values; the cross-lane max is taken here).
+__device__ __forceinline__ float f16_item_scale(float m, float s) {
+  m = fmaxf(m, __shfl_xor(m, 16));
+  m = fmaxf(m, __shfl_xor(m, 32));
+  m *= s;
+  if (m < F16_BIG) return 1.0f;
+  if (!(m <= 3.4028235e38f)) return F16_DOWN;      // inf / NaN: any scale (the result is not finite anyway)
+  int e;
+  frexpf(m, &e);                                   // 2^(e-1) <= m < 2^e, e >= 15
+  return ldexpf(1.0f, 14 - e);                     // m 2^(14-e) < 2^14, and >= 2^13
+}
+
+// split of the fragment s·x (s a power of two); returns the wave's range flag. When it is set, `sc` is each
+// item's range factor (the parts hold s·x·sc and a GEMM over them rescales the item's column by 1/sc); else 1.
+__device__ __forceinline__ bool split_f16(const float (&x)[4][4], float s, f16x8_t (&hi)[2], f16x8_t (&lo)[2],
+                                          float& sc) {
+  const float m = frag_absmax(x);
+  const bool big = __any(!(m * s < F16_BIG));
+  sc = big ? f16_item_scale(m, s) : 1.0f;
+  const float ss = s * sc;
 #pragma unroll
   for (int kb = 0; kb < 2; ++kb) {
     uint32_t h[4], l[4];
@@ -610,15 +638,17 @@ __device__ __forceinline__ bool split_f16(const float (&x)[4][4], float s, f16x8
 }
 
 // acc[ob] += W'[16 ob + i][.] · x (K = 64) in the 2^11 domain: acc raw in, raw out. W = interleaved f16
-// rows [wh 64 | wl 64 | pad] (gemm_bf3 layout); BIG: the split carried an extra 2^-16
+// rows [wh 64 | wl 64 | pad] (gemm_bf3 layout); BIG: the split carried the item factor sc (a power of two:
+// the accumulator is scaled by sc on the way in and by 1/sc on the way out, both exact)
 template <int OB, bool BIG>
 __device__ __forceinline__ void gemm_h3_body(const _Float16* W, const f16x8_t (&hi)[2],
-                                             const f16x8_t (&lo)[2], float (&acc)[OB][4]) {
+                                             const f16x8_t (&lo)[2], float sc, float (&acc)[OB][4]) {
   const int lane = __lane_id(), i = lane & 15, g = lane >> 4;
+  const float isc = BIG ? 1.0f / sc : 1.0f;
 #pragma unroll
   for (int ob = 0; ob < OB; ++ob) {
     f32x4 c = {acc[ob][0], acc[ob][1], acc[ob][2], acc[ob][3]};
-    if (BIG) c *= F16_DOWN;
+    if (BIG) c *= sc;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
       const int o = (16 * ob + i) * 2 * LDW + 32 * kb + 8 * g;
@@ -628,7 +658,7 @@ __device__ __forceinline__ void gemm_h3_body(const _Float16* W, const f16x8_t (&
       c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, lo[kb], c, 0, 0, 0);
       c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, hi[kb], c, 0, 0, 0);
     }
-    if (BIG) c *= F16_UP;
+    if (BIG) c *= isc;
     acc[ob][0] = c[0]; acc[ob][1] = c[1]; acc[ob][2] = c[2]; acc[ob][3] = c[3];
   }
 }
@@ -636,9 +666,9 @@ __device__ __forceinline__ void gemm_h3_body(const _Float16* W, const f16x8_t (&
 // the range flag picks one of two whole GEMM bodies (a uniform branch: the common body has no rescaling)
 template <int OB>
 __device__ __forceinline__ void gemm_h3(const _Float16* W, const f16x8_t (&hi)[2], const f16x8_t (&lo)[2],
-                                        bool big, float (&acc)[OB][4]) {
-  if (__builtin_expect(big, 0)) gemm_h3_body<OB, true>(W, hi, lo, acc);
-  else gemm_h3_body<OB, false>(W, hi, lo, acc);
+                                        bool big, float sc, float (&acc)[OB][4]) {
+  if (__builtin_expect(big, 0)) gemm_h3_body<OB, true>(W, hi, lo, sc, acc);
+  else gemm_h3_body<OB, false>(W, hi, lo, 1.0f, acc);
 }
 
 // A GEMM input fragment prepared once for the precision (split parts), reusable by several GEMMs.
@@ -647,20 +677,21 @@ struct Frag {
   bf16x8_t bh[2], bl[2];
   f16x8_t hh[2], hl[2];
   bool big;
+  float sc;   // f16x3, big: the item's range factor (split_f16)
 };
 
 // x in the precision's domain (dom<PREC>() x_true for f16x3): split for the GEMMs that read it
 template <int PREC>
 __device__ __forceinline__ void prep(const float (&x)[4][4], Frag<PREC>& f) {
   if constexpr (PREC == 1) split_bf16(x, f.bh, f.bl);
-  else if constexpr (PREC == 2) f.big = split_f16(x, dom_inv<PREC>(), f.hh, f.hl);
+  else if constexpr (PREC == 2) f.big = split_f16(x, dom_inv<PREC>(), f.hh, f.hl, f.sc);
 }
 
 // x in the true domain (f16x3: split with scale 1)
 template <int PREC>
 __device__ __forceinline__ void prep_true(const float (&x)[4][4], Frag<PREC>& f) {
   if constexpr (PREC == 1) split_bf16(x, f.bh, f.bl);
-  else if constexpr (PREC == 2) f.big = split_f16(x, 1.0f, f.hh, f.hl);
+  else if constexpr (PREC == 2) f.big = split_f16(x, 1.0f, f.hh, f.hl, f.sc);
 }
 
 // acc (domain) += W · x_true over one prepared fragment; W = the LDS image of the matrix
@@ -669,7 +700,7 @@ template <int PREC, int OB>
 __device__ __forceinline__ void gemm_f(const void* W, const float (&x)[4][4], const Frag<PREC>& f, float (&acc)[OB][4]) {
   if constexpr (PREC == 0) gemm_frag<4, OB>(static_cast<const float*>(W), LDW, x, acc);
   else if constexpr (PREC == 1) gemm_bf3<OB>(static_cast<const __bf16*>(W), f.bh, f.bl, acc);
-  else gemm_h3<OB>(static_cast<const _Float16*>(W), f.hh, f.hl, f.big, acc);
+  else gemm_h3<OB>(static_cast<const _Float16*>(W), f.hh, f.hl, f.big, f.sc, acc);
 }
 
 // global [hi rows][lo rows] bf16 pack row `row` (< 2 rows_per_part) -> its place in an interleaved
@@ -766,9 +797,10 @@ __device__ __forceinline__ void layer_lds_p(const uint16_t* __restrict__ W, int 
   if (PREC == 1) {
     split_bf16(in, hb, lb);
   } else {
-    const bool big = split_f16(in, 1.0f, hh, lh);
-    s_in = big ? 2048.0f * F16_DOWN : 2048.0f;
-    s_out = big ? F16_UP / 2048.0f : 1.0f / 2048.0f;
+    float sc;
+    split_f16(in, 1.0f, hh, lh, sc);              // sc: the item's range factor (1 in range)
+    s_in = 2048.0f * sc;
+    s_out = (1.0f / 2048.0f) / sc;
   }
   const int lo_off = 32 * KB32;                 // interleaved rows: [hi | lo | pad]
 #pragma unroll
@@ -891,14 +923,16 @@ __device__ __forceinline__ void layer_fixed(const float* smz, const EmbedLayout&
   if (PREC == 1) {
     split_bf16(in, hb, lb);
   } else {
-    const bool big = split_f16(in, 1.0f, hh, lh);
-    s_in = big ? 2048.0f * F16_DOWN : 2048.0f;
-    s_out = DOM ? (big ? F16_UP : 1.0f) : (big ? F16_UP / 2048.0f : 1.0f / 2048.0f);
+    float sc;
+    const bool big = split_f16(in, 1.0f, hh, lh, sc);   // sc: the item's range factor (1 in range)
+    s_in = 2048.0f * sc;
+    s_out = (DOM ? 1.0f : 1.0f / 2048.0f) / sc;
     if constexpr (PREC == 2) {
       if (split_out) {
         split_out->hh[0] = hh[0]; split_out->hh[1] = hh[1];
         split_out->hl[0] = lh[0]; split_out->hl[1] = lh[1];
         split_out->big = big;
+        split_out->sc = sc;
       }
     }
   }
@@ -980,6 +1014,16 @@ __device__ __forceinline__ void stage_tile64(float* dst, const float* w32, int64
   }
 }
 
+struct EdgeRangesArgs {   // the edge passes' wave range table, filled by the edge embedding (edge_ranges_fill)
+  const int *seg, *wg_start, *s_dst;
+  int T;
+  int64_t N;
+  int G;
+  int4* ranges;
+};
+__device__ inline void edge_ranges_fill(const int* seg, const int* wg_start, const int* s_dst, int T, int64_t N, int G,
+                                        int4* __restrict__ ranges);
+
 // Edge embedding (sorted order), the fallback of the fused first pass: e_init = MLP(edge_attr[orig]),
 // Q0 = W1_e_init·e_init + b1 and R0 = Q0 + W1_e_cur·e_init (the first pass's layer-1 input).
 // One 16-wave workgroup per CU, weights staged once in LDS; a wave walks an equal share of the
@@ -993,9 +1037,12 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp em
                                                                      const float* __restrict__ q0_b,
                                                                      const float* __restrict__ e1_w,
                                                                      const uint16_t* __restrict__ e1_bf,
-                                                                     float* __restrict__ r0, float* __restrict__ q0) {
+                                                                     float* __restrict__ r0, float* __restrict__ q0,
+                                                                     EdgeRangesArgs rg) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
+  // the edge passes' per-wave range table (needs only the prepared order; one entry per thread, grid-stride)
+  if (rg.ranges) edge_ranges_fill(rg.seg, rg.wg_start, rg.s_dst, rg.T, rg.N, rg.G, rg.ranges);
   stage_tile64<PREC>(sm + Lo.total, e1_w, D, e1_bf);   // W1_e_cur after the embedding image
   for (int l = 0; l <= Lo.n; ++l) {
     const float* bsrc = l < Lo.n ? emb.layer[l].b : q0_b;
@@ -2351,9 +2398,10 @@ __global__ __launch_bounds__(256) void node_table_kernel(NodeTableArgs a) {
       // 2^11 domain of the edge passes (the bias enters x 2^11, nothing is scaled on the way out)
       const float (&x0)[4][4] = *reinterpret_cast<const float (*)[4][4]>(&x[0][0]);
       const float (&x1)[4][4] = *reinterpret_cast<const float (*)[4][4]>(&x[4][0]);
-      const bool big = f16_big(x0, 1.0f) || f16_big(x1, 1.0f);
-      const float ss = big ? F16_DOWN : 1.0f;
-      acc *= big ? 2048.0f * F16_DOWN : 2048.0f;
+      const float mx = fmaxf(frag_absmax(x0), frag_absmax(x1));
+      const bool big = __any(!(mx < F16_BIG));
+      const float ss = big ? f16_item_scale(mx, 1.0f) : 1.0f;   // the node's range factor (1 in range)
+      acc *= 2048.0f * ss;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         f16x8_t hi[2], lo[2];
@@ -2375,7 +2423,7 @@ __global__ __launch_bounds__(256) void node_table_kernel(NodeTableArgs a) {
           acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[2 * h + kb], hi[kb], acc, 0, 0, 0);
         }
       }
-      if (big) acc *= F16_UP;
+      if (big) acc *= 1.0f / ss;
     }
     if (nn < N) st4(a.NT + nn * a.NO + 16 * ob + 4 * g, acc[0], acc[1], acc[2], acc[3]);
   }
@@ -2603,6 +2651,202 @@ __global__ __launch_bounds__(256) void fully_prepare_kernel(FullyPrepArgs a) {
   }
 }
 
+// ---- Symmetric prepare: edge_index sorted by (src, dst) and symmetric inside every image (PyG to_undirected's
+// coalesced output: knn_mpn_graph, feature_knn_mpn_graph, score_based_graph, ConstructGraph.py:363-422).
+// Then the incoming edges of d are the outgoing ones reversed: segment (t, d) = the type-t entries of row d in
+// ascending source order, which is also the original edge-id order the sorting prepare produces, and the id of
+// edge (s -> d) = (start of row s) + (rank of d in row s). Per image one block holds the image's adjacency as
+// bit rows in LDS (<= 512 nodes), so the counts, the in-image offsets and every rank are popcounts; no sort,
+// no global atomics. Two launches: sym_count_kernel (per-image edge range and per-(image, type) edge totals),
+// sym_emit_kernel (offsets, segments, the three index arrays). Identical arrays to launch_prepare's.
+constexpr int SYM_MAXB = 64;        // images per batch
+constexpr int SYM_MAXN = 512;       // nodes per image (LDS bit rows)
+constexpr int SYM_W = SYM_MAXN / 32;
+constexpr int SYM_THREADS = 1024;
+// per image in the workspace (ws.sym): [0] first edge, [1] end edge, [2] validation bits, [3..3+T) type totals
+constexpr int SYM_REC = 4 + MAXT;
+
+// first position p in [0, n) with a[p] >= key (n if none), by all threads of the block: 1024-way probes per round
+__device__ int64_t block_lower_bound(const int64_t* __restrict__ a, int64_t n, int64_t key) {
+  int64_t lo = 0, hi = n;                          // a[< lo] < key <= a[>= hi]
+  while (lo < hi) {                                // (uniform)
+    const int64_t s = (hi - lo + SYM_THREADS - 1) / SYM_THREADS;
+    const int64_t q = lo + (int64_t)threadIdx.x * s;
+    const bool below = q < hi && a[q] < key;
+    const int c = __syncthreads_count(below);      // probes below key form a prefix
+    if (c == 0) { hi = lo; break; }
+    // the last probe below: a[lo + (c-1) s] < key; the next one (if any, < hi) is >= key
+    const int64_t nlo = lo + (int64_t)(c - 1) * s + 1, nhi = min(hi, lo + (int64_t)c * s);
+    lo = nlo;
+    hi = nhi;
+  }
+  return lo;
+}
+
+struct SymPrepArgs {
+  const int64_t* ei;                // [2, E]
+  int64_t E, N;
+  const int64_t* node_off;          // [B + 1] device
+  int B;
+  const int64_t* types;
+  int64_t ts;
+  int T, Gsplit;
+  int *sym, *seg, *wg_start, *s_src, *s_dst, *s_orig, *err;
+};
+
+__global__ __launch_bounds__(SYM_THREADS) void sym_count_kernel(SymPrepArgs a) {
+  __shared__ int tot[MAXT];
+  __shared__ int bad;
+  const int b = blockIdx.x, T = a.T;
+  const int64_t E = a.E, n0 = a.node_off[b], n1 = a.node_off[b + 1];
+  if (threadIdx.x < MAXT) tot[threadIdx.x] = 0;
+  if (threadIdx.x == 0) bad = 0;
+  if (b == 0 && threadIdx.x < 4) a.err[threadIdx.x] = 0;   // (sym_emit_kernel only ORs into it)
+  // unwritten slots (only for an input that breaks the symmetry contract) stay valid indices
+  for (int64_t i = (int64_t)b * SYM_THREADS + threadIdx.x; i < E; i += (int64_t)a.B * SYM_THREADS) {
+    a.s_src[i] = 0; a.s_dst[i] = 0; a.s_orig[i] = 0;
+  }
+  const int64_t e0 = block_lower_bound(a.ei, E, n0);
+  const int64_t e1 = block_lower_bound(a.ei, E, n1);
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += SYM_THREADS) {
+    const int64_t s = a.ei[e], d = a.ei[E + e];
+    if (d < n0 || d >= n1 || d == s || (e > e0 && (a.ei[e - 1] > s || (a.ei[e - 1] == s && a.ei[E + e - 1] >= d))))
+      atomicOr(&bad, 4);                           // not sorted / not inside the image / self loop
+    const int64_t t = a.types[s * a.ts];
+    if (t >= 0 && t < T) atomicAdd(&tot[t], 1);
+    else atomicOr(&bad, 2);                        // skipped as a source, like mpn_count_kernel
+  }
+  __syncthreads();
+  int* rec = a.sym + b * SYM_REC;
+  if (threadIdx.x == 0) { rec[0] = (int)e0; rec[1] = (int)e1; rec[2] = bad; }
+  if (threadIdx.x < T) rec[3 + threadIdx.x] = tot[threadIdx.x];
+}
+
+__global__ __launch_bounds__(SYM_THREADS) void sym_emit_kernel(SymPrepArgs a) {
+  __shared__ unsigned R[SYM_MAXN][SYM_W];          // adjacency bit rows of the image
+  __shared__ unsigned short pre[SYM_MAXN][SYM_W];  // per row: set bits in the words before w
+  __shared__ unsigned M[MAXT][SYM_W];              // type masks
+  __shared__ int rs[SYM_MAXN];                     // row start (relative to the image's first edge)
+  __shared__ int X[MAXT * SYM_MAXN];               // (t, d) counts, then their exclusive scan
+  __shared__ int base[MAXT + 1], wsum[SYM_THREADS / 64 + 1];
+  __shared__ int tstart_g[MAXT + 1], gt_sh[MAXT];
+  __shared__ int bad;
+  const int b = blockIdx.x, T = a.T;
+  const int64_t E = a.E, N = a.N, n0 = a.node_off[b];
+  const int nb = (int)(a.node_off[b + 1] - n0), W = (nb + 31) >> 5;
+  const int* rec = a.sym + b * SYM_REC;
+  const int e0 = rec[0], e1 = rec[1];
+  for (int i = threadIdx.x; i < SYM_MAXN * SYM_W; i += SYM_THREADS) (&R[0][0])[i] = 0;
+  for (int i = threadIdx.x; i < MAXT * SYM_W; i += SYM_THREADS) (&M[0][0])[i] = 0;
+  if (threadIdx.x == 0) bad = 0;
+  // type-major bases: all images' edges of types < t, then the type-t edges of images before b
+  if (threadIdx.x <= T) {
+    const int t = threadIdx.x;
+    int acc = 0;
+    for (int bb = 0; bb < a.B; ++bb)
+      for (int u = 0; u < T; ++u) {
+        const int v = a.sym[bb * SYM_REC + 3 + u];
+        if (u < t || (u == t && bb < b)) acc += v;
+      }
+    base[t] = acc;                                 // base[T] = every edge of a valid source type
+    if (b == 0) tstart_g[t] = acc;                 // (b = 0: the type starts)
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nb; i += SYM_THREADS) {
+    const int64_t t = a.types[(n0 + i) * a.ts];
+    if (t >= 0 && t < T) atomicOr(&M[t][i >> 5], 1u << (i & 31));
+  }
+  for (int e = e0 + threadIdx.x; e < e1; e += SYM_THREADS) {
+    const int s = (int)(a.ei[e] - n0), d = (int)(a.ei[E + e] - n0);
+    if (s < 0 || s >= nb || d < 0 || d >= nb) continue;   // (flagged by sym_count_kernel)
+    if (e == e0 || a.ei[e - 1] != a.ei[e]) rs[s] = e - e0;
+    atomicOr(&R[s][d >> 5], 1u << (d & 31));
+  }
+  __syncthreads();
+  for (int s = threadIdx.x; s < nb; s += SYM_THREADS) {
+    int acc = 0;
+    for (int w = 0; w < W; ++w) { pre[s][w] = (unsigned short)acc; acc += __popc(R[s][w]); }
+  }
+  // counts (t, d) = type-t entries of row d, type-major; 1 per thread-slot chunk of 9 for the scan
+  const int Q = T * nb;
+  constexpr int PER = (MAXT * SYM_MAXN + SYM_THREADS - 1) / SYM_THREADS;
+  int v[PER], local = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int q = threadIdx.x * PER + j;
+    int c = 0;
+    if (q < Q) {
+      const int t = q / nb, d = q - t * nb;
+      for (int w = 0; w < W; ++w) c += __popc(R[d][w] & M[t][w]);
+    }
+    v[j] = c;
+    local += c;
+  }
+  // block-wide exclusive scan of the thread sums
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int x = local;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(x, off);
+    if (lane >= off) x += o;
+  }
+  if (lane == 63) wsum[wave] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int w = 0; w < SYM_THREADS / 64; ++w) { const int t = wsum[w]; wsum[w] = acc; acc += t; }
+  }
+  __syncthreads();
+  {
+    int run = wsum[wave] + x - local;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int q = threadIdx.x * PER + j;
+      if (q < Q) X[q] = run;
+      run += v[j];
+    }
+  }
+  __syncthreads();
+  // segments and their entries: one thread per (t, d)
+  for (int q = threadIdx.x; q < Q; q += SYM_THREADS) {
+    const int t = q / nb, d = q - t * nb;
+    int pos = base[t] + X[q] - X[t * nb];
+    a.seg[(int64_t)t * N + n0 + d] = pos;
+    const int dw = d >> 5;
+    const unsigned dbit = 1u << (d & 31), below = dbit - 1u;
+    for (int w = 0; w < W; ++w) {
+      unsigned bits = R[d][w] & M[t][w];
+      while (bits) {
+        const int s = 32 * w + __builtin_ctz(bits);
+        bits &= bits - 1u;
+        const unsigned rw = R[s][dw];
+        if (!(rw & dbit)) bad = 1;                 // (s -> d) missing: not symmetric
+        if (pos < E) {                             // (holds for a symmetric input)
+          a.s_src[pos] = (int)(n0 + s);
+          a.s_dst[pos] = (int)(n0 + d);
+          a.s_orig[pos] = e0 + rs[s] + pre[s][dw] + __popc(rw & below);
+        } else {
+          bad = 1;
+        }
+        ++pos;
+      }
+    }
+  }
+  __syncthreads();
+  if (b == 0) {
+    // nodes of other images are not visited by this block: seg of image-less nodes cannot exist (every node
+    // belongs to an image); the end marker and the pass split over the whole batch
+    if (threadIdx.x == 0) {
+      a.seg[(int64_t)T * N] = tstart_g[T];
+      int any = 0;
+      for (int bb = 0; bb < a.B; ++bb) any |= a.sym[bb * SYM_REC + 2];
+      if (any) atomicOr(a.err, any);             // 4: not a sorted symmetric list, 2: bad node type (mpn_status)
+    }
+    type_split(tstart_g, tstart_g[T], T, a.Gsplit, gt_sh, a.wg_start);
+  }
+  if (bad && threadIdx.x == 0) atomicOr(a.err, 4);   // not symmetric
+}
+
 static int launch_prepare(const pemp_mpn_desc* desc, const int64_t* edge_index, const int64_t* node_types, int64_t N,
                           int64_t E, const MpnWs& ws, hipStream_t st) {
   const int T = desc->num_types;
@@ -2703,7 +2947,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
                             const float* edge_attr, const int64_t* edge_index, const int64_t* node_types,
                             int64_t N, int64_t E, float* edge_logits, float* node_logits, float* class_logits,
                             void* workspace, size_t workspace_bytes, void* stream, const int64_t* fully_node_off,
-                            int fully_B, int fully_nmax) {
+                            int fully_B, int fully_nmax, const int64_t* sym_node_off = nullptr, int sym_B = 0) {
   PEMP_CHECK_ARG(desc && w, "pemp_mpn_forward: null desc/weights");
   const int T = desc->num_types, J = desc->num_joints;
   PEMP_CHECK_ARG(desc->hidden == 64, "pemp_mpn_forward: hidden width must be 64 (got %d)", desc->hidden);
@@ -2803,10 +3047,9 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
     PEMP_LAUNCH_CHECK();
     eimg = ws.eimg;
   }
-  // launched after the node embedding + first node table (which need no edge order), so that the
-  // host issues the short prepare kernels while the GPU runs those node kernels
   hipStream_t pst = st;                           // stream of the edge prelude (a side stream, below)
-  auto edge_prelude = [&]() -> int {
+  // the edge prelude in two parts: the edge order (prepare), then the range table + edge embedding
+  auto edge_prepare = [&]() -> int {
   if (!(desc->flags & PEMP_MPN_PREPARED)) {
     if (fully_node_off && N > 0) {
       FullyPrepArgs fa{fully_node_off, fully_B, node_types, tstride, N, T, std::max(num_cus(), T),
@@ -2817,12 +3060,25 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
       ProfScope prof("mpn_prepare", pst);
       hipLaunchKernelGGL(fully_prepare_kernel, dim3(gx, (unsigned)fully_B), dim3(256), 0, pst, fa);
       PEMP_LAUNCH_CHECK();
+    } else if (sym_node_off && N > 0) {
+      SymPrepArgs sa{edge_index, E, N, sym_node_off, sym_B, node_types, tstride, T, std::max(num_cus(), T),
+                     ws.sym, ws.seg, ws.wg_start, ws.s_src, ws.s_dst, ws.s_orig, ws.err};
+      ProfScope prof("mpn_prepare", pst);
+      hipLaunchKernelGGL(sym_count_kernel, dim3((unsigned)sym_B), dim3(SYM_THREADS), 0, pst, sa);
+      PEMP_LAUNCH_CHECK();
+      hipLaunchKernelGGL(sym_emit_kernel, dim3((unsigned)sym_B), dim3(SYM_THREADS), 0, pst, sa);
+      PEMP_LAUNCH_CHECK();
     } else {
       const int rc0 = launch_prepare(desc, edge_index, node_types, N, E, ws, pst);
       if (rc0) return rc0;
     }
   }
-  if (E > 0 && steps >= 1) {   // per-wave edge ranges of the passes (static across iterations)
+  return PEMP_OK;
+  };
+  auto edge_embed = [&]() -> int {
+  // per-wave edge ranges of the passes (static across iterations): filled by the LDS edge embedding itself
+  const EdgeRangesArgs rga{ws.seg, ws.wg_start, ws.s_dst, T, N, edge_grid, ws.ranges};
+  if (E > 0 && steps >= 1 && !emb_lds) {
     hipLaunchKernelGGL(edge_ranges_kernel, dim3((unsigned)std::min(64, (edge_grid * (EDGE_WAVES + 12) + 255) / 256)),
                        dim3(256), 0, pst, ws.seg, ws.wg_start, ws.s_dst, T, N, edge_grid, ws.ranges);
     PEMP_LAUNCH_CHECK();
@@ -2836,7 +3092,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
 #define PEMP_EMBED_LAUNCH(P, FX)                                                                                   \
   hipLaunchKernelGGL((edge_embed_kernel<P, FX>), dim3(grid), dim3(64 * EDGE_WAVES), lds, pst, w->edge_emb, emb_lo,  \
                      w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, w->e1_bf, \
-                     ws.EA, ws.Q0)
+                     ws.EA, ws.Q0, rga)
       if (emb_prec == PEMP_PREC_F16X3) {
         if (fixed) PEMP_EMBED_LAUNCH(2, true);
         else PEMP_EMBED_LAUNCH(2, false);
@@ -2846,7 +3102,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
       } else
         hipLaunchKernelGGL((edge_embed_kernel<0, false>), dim3(grid), dim3(64 * EDGE_WAVES), lds, pst, w->edge_emb, emb_lo,
                            w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, w->e1_bf,
-                           ws.EA, ws.Q0);
+                           ws.EA, ws.Q0, rga);
 #undef PEMP_EMBED_LAUNCH
     } else {
       hipLaunchKernelGGL(edge_embed_wide_kernel, dim3((unsigned)((E + 63) / 64)), dim3(256), 0, pst, w->edge_emb,
@@ -2956,7 +3212,10 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
     side_lock.unlock();
     ss = nullptr;
   };
-  if (ss && (rc = edge_prelude())) { join_side(); return rc; }
+  // side stream: the edge order first; then the node embedding + first node table here (short kernels with
+  // 16-row grids) while the order is prepared; then the range table and the edge embedding on the side stream
+  // (every CU, all of its LDS: the node kernels are done or nearly so by then)
+  if (ss && (rc = edge_prepare())) { join_side(); return rc; }
   if (!fused_embed) {
     if ((rc = rows_mlp("node_embed", w->node_emb, x, desc->node_in_dim, N, ws.X, 128, ws.X + 64, 128, st))) {
       join_side();
@@ -2967,8 +3226,12 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
     join_side();
     return rc;
   }
-  if (ss) join_side();
-  else if ((rc = edge_prelude())) return rc;
+  if (ss) {
+    if ((rc = edge_embed())) { join_side(); return rc; }
+    join_side();
+  } else if ((rc = edge_prepare()) || (rc = edge_embed())) {
+    return rc;
+  }
   float* e_cur = ws.EA;                           // r of the pass (R0 from the separate embedding)
   float* e_nxt = ws.EB;
   int rec = 0;
@@ -3045,6 +3308,26 @@ extern "C" int pemp_mpn_forward_fully(const pemp_mpn_desc* desc, const pemp_mpn_
                           workspace, workspace_bytes, stream, node_off, B, (int)nmax);
 }
 
+extern "C" int pemp_mpn_forward_sym(const pemp_mpn_desc* desc, const pemp_mpn_weights* w, const float* x,
+                                    const float* edge_attr, const int64_t* edge_index, const int64_t* node_types,
+                                    int64_t N, int64_t E, const int64_t* node_off, const int64_t* node_off_host, int B,
+                                    float* edge_logits, float* node_logits, float* class_logits, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
+  PEMP_CHECK_ARG(node_off && node_off_host && B >= 1, "pemp_mpn_forward_sym: bad node offsets");
+  PEMP_CHECK_ARG(node_off_host[0] == 0 && node_off_host[B] == N, "pemp_mpn_forward_sym: offsets do not sum to N");
+  int64_t nmax = 0;
+  for (int b = 0; b < B; ++b) {
+    const int64_t n = node_off_host[b + 1] - node_off_host[b];
+    PEMP_CHECK_ARG(n >= 0, "pemp_mpn_forward_sym: decreasing offsets");
+    nmax = std::max(nmax, n);
+  }
+  if (B > SYM_MAXB || nmax > SYM_MAXN)   // the LDS bit rows hold <= 512 nodes: the sorting prepare above that
+    return mpn_forward_impl(desc, w, x, edge_attr, edge_index, node_types, N, E, edge_logits, node_logits,
+                            class_logits, workspace, workspace_bytes, stream, nullptr, 0, 0);
+  return mpn_forward_impl(desc, w, x, edge_attr, edge_index, node_types, N, E, edge_logits, node_logits, class_logits,
+                          workspace, workspace_bytes, stream, nullptr, 0, 0, node_off, B);
+}
+
 extern "C" int pemp_mpn_prepare(const pemp_mpn_desc* desc, const int64_t* edge_index, const int64_t* node_types,
                                 int64_t N, int64_t E, void* workspace, size_t workspace_bytes, void* stream) {
   PEMP_CHECK_ARG(desc && desc->num_types >= 1 && desc->num_types <= MAXT, "pemp_mpn_prepare: bad desc");
@@ -3109,5 +3392,9 @@ extern "C" int pemp_mpn_status(const pemp_mpn_desc* desc, int64_t N, int64_t E, 
   PEMP_HIP(hipStreamSynchronize(as_stream(stream)));
   if (err & 1) { set_error("edge_index has entries outside [0, N)"); return PEMP_ERR_INVALID_ARG; }
   if (err & 2) { set_error("node_types has entries outside [0, num_types)"); return PEMP_ERR_INVALID_ARG; }
+  if (err & 4) {
+    set_error("edge_index is not sorted by (src, dst) and symmetric inside every image (pemp_mpn_forward_sym)");
+    return PEMP_ERR_INVALID_ARG;
+  }
   return PEMP_OK;
 }

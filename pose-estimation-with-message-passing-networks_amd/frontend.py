@@ -96,10 +96,17 @@ class ProjectedHeatmaps:
     outputs: list over scales of [B, C, h_s, w_s] network outputs of the forward pass (heatmaps in channels
     0..J-1, per-joint tags in J..2J-1 when tags are used); flip_outputs: the flipped-image pass as the
     network produced it (same shapes, not un-flipped) or None; flip_index: the FLIP_CONFIG permutation;
-    size: (H, W); tag_scale: index of the scale whose tags are kept (the reference keeps scale 1.0).
-    Scales in the reference's order (descending scale factor)."""
+    size: (H, W); tag_scale: index of the scale whose tags are kept (the reference keeps scale 1.0);
+    tag_per_joint: MODEL.HRNET.TAG_PER_JOINT. Scales in the reference's order (descending scale factor).
 
-    def __init__(self, outputs, size, num_joints, flip_outputs=None, flip_index=None, divisor=None, tag_scale=0):
+    Tags: the reference keeps ``output[:, J:]`` and re-indexes the flipped pass by flip_index only when
+    TAG_PER_JOINT is set (``PoseEstimation.py:406-410``); ``construct_graph`` then reads channel ``type`` of
+    that map (``ConstructGraph.py:103``), which exists only with one tag channel per joint. So tags need
+    exactly J tag channels (C == 2J) and TAG_PER_JOINT; a shared tag channel is refused (with it the
+    reference's own joint-tag gather indexes past the map)."""
+
+    def __init__(self, outputs, size, num_joints, flip_outputs=None, flip_index=None, divisor=None, tag_scale=0,
+                 tag_per_joint=True):
         if isinstance(outputs, torch.Tensor):
             outputs = [outputs]
         outputs = [o.float().contiguous() for o in outputs]
@@ -118,11 +125,18 @@ class ProjectedHeatmaps:
                 raise ValueError("ProjectedHeatmaps: every output is [B, C, h, w] with the same B and C")
         if C < J:
             raise ValueError(f"ProjectedHeatmaps: {C} channels < {J} joints")
+        if C != J and C != 2 * J:
+            raise ValueError(f"ProjectedHeatmaps: {C} channels: expected J = {J} (heatmaps only) or 2J (heatmaps + "
+                             "one tag channel per joint)")
+        if C == 2 * J and not tag_per_joint:
+            raise NotImplementedError("ProjectedHeatmaps: TAG_PER_JOINT False (a shared tag channel; the reference's "
+                                      "joint-tag gather, ConstructGraph.py:103, indexes it by joint type)")
         self.outputs, self.flip_outputs = outputs, flip_outputs
         self.num_joints = J
         self.size = (int(size[0]), int(size[1]))
         self.divisor = float(len(outputs) if divisor is None else divisor)
         self.tag_scale = int(tag_scale)
+        self.tag_per_joint = bool(tag_per_joint)
         self.device = outputs[0].device
         fi = list(range(J)) if flip_index is None else [int(v) for v in flip_index]
         if sorted(fi) != list(range(J)):
@@ -130,13 +144,13 @@ class ProjectedHeatmaps:
         self.flip_index = torch.tensor(fi, dtype=torch.int32, device=self.device)
         self.shape = torch.Size([B, J, self.size[0], self.size[1]])
         self.dtype = torch.float32
-        self.has_tags = C >= 2 * J
+        self.has_tags = C == 2 * J
         self.tag_dims = 2 if flip_outputs is not None else 1
 
     def to(self, device):
         return ProjectedHeatmaps([o.to(device) for o in self.outputs], self.size, self.num_joints,
                                  None if self.flip_outputs is None else [o.to(device) for o in self.flip_outputs],
-                                 self.flip_index.tolist(), self.divisor, self.tag_scale)
+                                 self.flip_index.tolist(), self.divisor, self.tag_scale, self.tag_per_joint)
 
     def _interp(self, m):
         return torch.nn.functional.interpolate(m, size=self.size, mode="bilinear", align_corners=False)

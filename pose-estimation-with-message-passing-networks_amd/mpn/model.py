@@ -22,6 +22,7 @@ from .hierarch import HierarchUpdateCnn, HierarchUpdateMlp
 
 _VALIDATE = os.environ.get("PEMP_VALIDATE", "0") not in ("", "0")   # read once at import
 _FULLY_OFF = os.environ.get("PEMP_NO_FULLY_PREPARE", "0") not in ("", "0")   # force the sorting prepare
+_SYM_OFF = os.environ.get("PEMP_NO_SYM_PREPARE", "0") not in ("", "0")       # (for symmetric graphs too)
 
 AGGR_CODES = {"attn": 0, "add": 1, "sum": 1, "mean": 2, "max": 3}
 PRECISIONS = {"fp32": 0, "bf16x3": 1, "f16x3": 2}
@@ -188,7 +189,7 @@ class NodeClassificationMPNSimple(nn.Module):
         if aggr not in AGGR_CODES:
             raise NotImplementedError(f"AGGR={aggr}")
         self.aggr_code = AGGR_CODES[aggr]
-        self.precision = default_precision(self.aggr_code)   # "fp32" | "bf16x3", settable
+        self.precision = default_precision(self.aggr_code)   # "fp32" | "bf16x3" | "f16x3", settable
         self._folded = None
         self._folded_key = None
         self._tensors = None
@@ -236,6 +237,7 @@ class NodeClassificationMPNSimple(nn.Module):
             node_types = torch.tensor(TYPE_LUTS[self.node_summary], device=dev)[node_types]
         N, E = x.shape[0], edge_index.shape[1]
         fully = _fully_graph(edge_index, node_types, N) if self.node_summary == "not" else None
+        sym = _sym_graph(edge_index, N) if fully is None else None
         x = _as(x, torch.float32)
         edge_attr = _as(edge_attr, torch.float32)
         edge_index = _as(edge_index, torch.int64)
@@ -275,6 +277,12 @@ class NodeClassificationMPNSimple(nn.Module):
                                                 edge_index.data_ptr(), node_types.data_ptr(), N, E, noff.data_ptr(),
                                                 offs, B, edge_logits.data_ptr(), node_logits.data_ptr(),
                                                 class_logits.data_ptr(), ws.data_ptr(), ws.numel(), st))
+        elif sym is not None:       # a to_undirected graph of the constructor: order from its bit rows
+            noff, offs, B = sym
+            _lib.check(L.pemp_mpn_forward_sym(desc, fw.struct_ref, x.data_ptr(), edge_attr.data_ptr(),
+                                              edge_index.data_ptr(), node_types.data_ptr(), N, E, noff.data_ptr(),
+                                              offs, B, edge_logits.data_ptr(), node_logits.data_ptr(),
+                                              class_logits.data_ptr(), ws.data_ptr(), ws.numel(), st))
         else:
             _lib.check(L.pemp_mpn_forward(desc, fw.struct_ref, x.data_ptr(), edge_attr.data_ptr(),
                                           edge_index.data_ptr(), node_types.data_ptr(), N, E, edge_logits.data_ptr(),
@@ -299,6 +307,19 @@ def _fully_graph(edge_index, node_types, N):
     if (edge_index._version != ever or jdet._version != jver or node_types.dtype != torch.int64
             or node_types.data_ptr() != jdet.data_ptr() + 16 or node_types.stride(0) != 3
             or node_types.shape[0] != N or jdet.shape[0] != N or len(counts) > 64):
+        return None
+    B = len(counts)
+    return noff, (ctypes.c_int64 * (B + 1))(*itertools.accumulate(counts, initial=0)), B
+
+
+def _sym_graph(edge_index, N):
+    """(node_off, host offsets, B) when edge_index is an untouched (src, dst)-sorted symmetric graph of the
+    graph constructor (graph_constructor._tag_sym), else None."""
+    meta = getattr(edge_index, "_pemp_sym", None)
+    if meta is None or _SYM_OFF:
+        return None
+    noff, counts, ever = meta
+    if edge_index._version != ever or sum(counts) != N or not 1 <= len(counts) <= 64:
         return None
     B = len(counts)
     return noff, (ctypes.c_int64 * (B + 1))(*itertools.accumulate(counts, initial=0)), B

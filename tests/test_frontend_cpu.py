@@ -45,6 +45,11 @@ def test_projected_heatmaps_validation():
         ProjectedHeatmaps(outs, (40, 40), 17, flips, [0] * 17)          # not a permutation
     with pytest.raises(ValueError):
         ProjectedHeatmaps(outs, (40, 40), 17, flips[:0] + [flips[0][:, :, :10]])
+    with pytest.raises(ValueError):                                     # neither J nor 2J channels
+        ProjectedHeatmaps([o[:, :20] for o in outs], (40, 40), 17)
+    with pytest.raises(NotImplementedError):                            # shared tag channel (TAG_PER_JOINT False)
+        ProjectedHeatmaps(outs, (40, 40), 17, flips, COCO_FLIP, tag_per_joint=False)
+    assert not ProjectedHeatmaps([o[:, :17] for o in outs], (40, 40), 17).has_tags
 
 
 def test_projected_maps_gather_conv_host():

@@ -237,6 +237,47 @@ def test_fully_graph_fast_prepare_is_identical(prec, monkeypatch):
     assert mm._fully_graph(ei2, types, x.shape[0]) is None      # a copy carries no tag
 
 
+@pytest.mark.parametrize("graph_type,persons,H", [("knn", 9, 160), ("knn", 28, 320), ("score_based", 9, 160),
+                                                   ("feature_knn", 6, 128)])
+def test_symmetric_graph_fast_prepare_is_identical(graph_type, persons, H, monkeypatch):
+    """pemp_mpn_forward_sym (type-major order from the image's adjacency bit rows, for the constructor's
+    to_undirected graphs) must give bit-identical logits to the sorting prepare; an empty image in the batch;
+    an in-place edit of edge_index drops the tag; a list that is not symmetric is reported by pemp_mpn_status
+    (the call itself stays in bounds)."""
+    from pemp_amd import _lib
+    from pemp_amd.mpn import model as mm
+    B, J, W = 4, 17, H
+    hm = torch.from_numpy(syn.make_heatmaps(5, B, J, H, W, persons))
+    if graph_type != "score_based":                             # (score_based needs >= 75 detections per image)
+        hm[1] = 0.0                                             # an empty image in the batch
+    feats = torch.from_numpy(syn.closed_form((B, 128, H, W), 0.25))
+    gc = pcfg.inference_gc_config(graph_type, 5, False)
+    cfg = pcfg.published_mpn_config(J, 3, "attn")
+    model, _ = make_model(cfg, 3.75, "f16x3")
+    out = pemp_amd.get_graph_constructor(gc, scoremaps=hm.to(DEV), features=feats.to(DEV), tagmaps=None,
+                                         joints_gt=None, factor_list=None, masks=None, device=DEV,
+                                         testing=True, heatmaps=None, num_joints=J).construct_graph()
+    x, ea, ei, types = out[0], out[1], out[2], out[7][:, 2]
+    assert mm._sym_graph(ei, x.shape[0]) is not None
+    fast = run(model, x, ea, ei, types)
+    monkeypatch.setattr(mm, "_SYM_OFF", True)
+    slow = run(model, x, ea, ei, types)
+    monkeypatch.setattr(mm, "_SYM_OFF", False)
+    for a, b in zip(fast[0] + fast[1] + fast[2], slow[0] + slow[1] + slow[2]):
+        assert torch.equal(a, b)
+    ei2 = ei.clone()
+    ei.add_(0)
+    assert mm._sym_graph(ei, x.shape[0]) is None
+    assert mm._sym_graph(ei2, x.shape[0]) is None
+    # contract check: drop one direction of an edge (keep sorted order) -> status reports it
+    bad = torch.cat([ei2[:, :3], ei2[:, 4:]], 1).contiguous()
+    bad._pemp_sym = ei._pemp_sym[:2] + (bad._version,)
+    with pytest.raises(Exception, match="symmetric"):
+        with torch.no_grad():
+            model(x, ea[:bad.shape[1]].contiguous(), bad, node_types=types, validate=True)
+        torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("variant", ["attn", "max"])
 def test_trained_scale(variant):
     """Logit magnitudes of a trained checkpoint (every Linear weight x2: |logit| up to ~20-55 on this
@@ -272,6 +313,30 @@ def test_f16_range_scaling():
         scale = max(b.abs().max().item(), 1.0)
         assert torch.isfinite(a).all()
         assert max_err(a, b) < 1e-5 * scale
+
+
+@pytest.mark.parametrize("variant", ["max", "attn"])
+def test_f16_range_scaling_per_item(variant):
+    """One image's nodes past the f16 range (x 1e5) beside normal images in the same 16-node and 16-edge
+    tiles (small images: every tile straddles several): the range scale is per item, so the normal images
+    keep the absolute 1e-4 bar and the huge one fp32-level accuracy relative to its own magnitude."""
+    g = graph(8, 17, 64, 64, 1)
+    cfg = pcfg.published_mpn_config(17, 2, variant)
+    x, ea, ei, types, bidx = g[0].clone(), g[1], g[2], g[7][:, 2], g[12]
+    x[bidx == 0] *= 1e5
+    model, sd = make_model(cfg, 2.5, "f16x3")
+    pe, pn, pc, _ = run(model, x, ea, ei, types)
+    sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
+    ref = restate.mpn_forward(sd64, cfg, x.double(), ea.double(), ei, types)
+    ebidx = bidx[ei[0]]
+    for a, b, sel in [(p, r, ebidx) for p, r in zip(pe, ref[0])] + [(p, r, bidx) for p, r in zip(pn + pc, ref[1] + ref[2])]:
+        a = a.detach().cpu().double()
+        assert torch.isfinite(a).all()
+        huge, normal = sel == 0, sel != 0
+        assert normal.any() and huge.any()
+        assert (a[normal] - b[normal]).abs().max().item() < TOL
+        scale = max(b[huge].abs().max().item(), 1.0)
+        assert (a[huge] - b[huge]).abs().max().item() < 1e-5 * scale
 
 
 def test_batches_in_flight_on_two_streams():
