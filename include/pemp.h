@@ -423,17 +423,15 @@ int pemp_mpn_forward_fully(const pemp_mpn_desc* desc, const pemp_mpn_weights* we
                            float* edge_logits, float* node_logits, float* class_logits,
                            void* workspace, size_t workspace_bytes, void* stream);
 
-/* pemp_mpn_forward for a batch whose edge_index is sorted by (src, dst) and symmetric inside every image
- * (PyG to_undirected's coalesced output, as knn_mpn_graph / feature_knn_mpn_graph / score_based_graph return it,
- * ConstructGraph.py:363-422), images contiguous with per-image node offsets node_off (device, [B+1]) /
- * node_off_host: the type-major edge order comes from the image's adjacency bit rows (two launches, no sort)
- * instead of the sorting prepare; results are identical. B <= 64 and <= 512 nodes per image, else the
- * sorting prepare runs. A list that breaks the contract is reported by pemp_mpn_status (its logits are then
- * undefined, every index stays in range). */
+/* pemp_mpn_forward for an edge_index sorted by (src, dst) without duplicates and symmetric (every s -> d has
+ * its d -> s: PyG to_undirected's coalesced output, as knn_mpn_graph / feature_knn_mpn_graph / score_based_graph
+ * return it, ConstructGraph.py:363-422): the type-major edge order is read off the rows of the list (segment
+ * (t, d) = the type-t entries of row d) instead of the sorting prepare's scatter + segment sort; results are
+ * identical. N >= 2^24 falls back to the sorting prepare. A list that breaks the contract is reported by
+ * pemp_mpn_status (its logits are then undefined, every index stays in range). */
 int pemp_mpn_forward_sym(const pemp_mpn_desc* desc, const pemp_mpn_weights* weights, const float* x,
                          const float* edge_attr, const int64_t* edge_index, const int64_t* node_types,
-                         int64_t N, int64_t E, const int64_t* node_off, const int64_t* node_off_host, int B,
-                         float* edge_logits, float* node_logits, float* class_logits,
+                         int64_t N, int64_t E, float* edge_logits, float* node_logits, float* class_logits,
                          void* workspace, size_t workspace_bytes, void* stream);
 
 /* The edge-ordering part of pemp_mpn_forward (type-major counting sort of edge_index by (source type,

@@ -3,6 +3,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <map>
 #include <mutex>
 #include <string>
@@ -19,6 +20,21 @@ bool debug_sync() {
     return v && v[0] && v[0] != '0';
   }();
   return on;
+}
+
+bool g_host_trace = [] {
+  const char* v = getenv("PEMP_HOST_TRACE");
+  return v && v[0] && v[0] != '0';
+}();
+namespace {
+std::mutex g_ht_mu;
+std::vector<std::pair<int, long long>> g_ht;   // (source line of the launch check, steady-clock ns)
+}
+void host_mark(int line) {
+  const long long t = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                          std::chrono::steady_clock::now().time_since_epoch()).count();
+  std::lock_guard<std::mutex> lk(g_ht_mu);
+  if (g_ht.size() < (1u << 20)) g_ht.emplace_back(line, t);
 }
 
 void set_error(const char* fmt, ...) {
@@ -144,4 +160,14 @@ extern "C" int pemp_device_check(void) {
     return PEMP_ERR_UNSUPPORTED;
   }
   return PEMP_OK;
+}
+
+// diagnostics (PEMP_HOST_TRACE=1): prints the host time between consecutive launch checks (source lines) since
+// the last dump to stderr, then clears; returns the number of marks
+extern "C" int pemp_host_trace_dump(void) {
+  std::lock_guard<std::mutex> lk(pemp::g_ht_mu);
+  const int n = (int)pemp::g_ht.size();
+  for (int i = 0; i < n; ++i) fprintf(stderr, "[ht] %lld line %d\n", pemp::g_ht[i].second, pemp::g_ht[i].first);
+  pemp::g_ht.clear();
+  return n;
 }

@@ -20,6 +20,7 @@
 #include <limits.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <map>
 #include <mutex>
 #include <string.h>
@@ -232,7 +233,7 @@ static MpnWs mpn_carve(void* base, int T, int64_t N, int64_t E, size_t* bytes) {
   const int G = std::max(num_cus(), T);       // edge-pass grid
   w.ranges = c.take<int4>((size_t)G * (EDGE_WAVES + 12));
   w.eimg = c.take<float>((size_t)T * EIMG_MAX_STRIDE);   // edge-pass weight image when the caller has none
-  w.sym = c.take<int>(64 * (4 + MAXT));                  // symmetric prepare: per-image records (SYM_REC)
+  w.sym = c.take<int>(3 * N);                           // symmetric prepare: row bounds + check flags per node
   if (bytes) *bytes = c.used;
   return w;
 }
@@ -306,12 +307,17 @@ __device__ void type_split(const int* tstart, int64_t etot, int T, int G, int* g
 // (all loads of a pass in flight together), carry across passes. The per-type segment starts
 // seg[t*N] are captured from LDS on the way out (no read-back of seg).
 constexpr int SCAN_SPT = 16;
+// With `flags` (the symmetric prepare, which has no zeroing launch): err[0..3] are written here, err[0] = the OR of
+// flags[0..nflags) | 4 if the counts do not sum to E_all.
 __global__ __launch_bounds__(1024) void mpn_scan_kernel(const int* __restrict__ cnt, int64_t K, int64_t N, int T,
-                                                        int G, int* __restrict__ seg, int* __restrict__ wg_start) {
+                                                        int G, int* __restrict__ seg, int* __restrict__ wg_start,
+                                                        const int* __restrict__ flags = nullptr, int64_t nflags = 0,
+                                                        int64_t E_all = 0, int* __restrict__ err = nullptr) {
   __shared__ int sh[20 + 2 * (MAXT + 1)];
   __shared__ int out[1024 * SCAN_SPT];          // one pass of exclusive offsets, stored coalesced
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (threadIdx.x <= T) sh[20 + threadIdx.x] = 0;   // (K = 0: every segment start is 0)
+  if (threadIdx.x == 0) sh[17] = 0;
   __syncthreads();
   int carry = 0;
   for (int64_t base = 0; base < K; base += 1024 * SCAN_SPT) {
@@ -367,7 +373,13 @@ __global__ __launch_bounds__(1024) void mpn_scan_kernel(const int* __restrict__ 
     seg[K] = carry;
     sh[20 + T] = carry;
   }
+  if (flags) {
+    int f = 0;
+    for (int64_t i = threadIdx.x; i < nflags; i += 1024) f |= flags[i];
+    if (f) atomicOr(&sh[17], f);                             // (sh[17..19]: free after the scan)
+  }
   __syncthreads();
+  if (flags && threadIdx.x < 4) err[threadIdx.x] = threadIdx.x ? 0 : (sh[17] | (carry != E_all ? 4 : 0));
   type_split(sh + 20, carry, T, G, sh + 20 + MAXT + 1, wg_start);
 }
 
@@ -1335,7 +1347,7 @@ __device__ inline int4 edge_wave_range(const int* __restrict__ seg, const int* _
   const int64_t n_b = hi - lo;
   auto snap = [&](int p) -> int {               // first segment start at or after p
     if (p <= ts || p >= te) return p;
-    const int dp = s_dst[p];
+    const int dp = min(max(s_dst[p], 0), (int)N - 1);   // (clamped: in range for any prepared list)
     return dp == s_dst[p - 1] ? seg[t * N + dp + 1] : p;
   };
   return make_int4(snap(lo + (int)(n_b * wave / NW)), snap(lo + (int)(n_b * (wave + 1) / NW)), t, 0);
@@ -1622,7 +1634,9 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
 #pragma unroll
         for (int r = 0; r < 4; ++r) h1[ob][r] = ep[ob][r] * dom_inv<PREC>();
       mlp_frag<4>(a.head, h1, h2);
-      if (valid && g == 0) a.edge_logits[a.s_orig[p]] = h1[0][0];
+      if (valid && g == 0)   // (descriptor store: an out-of-range id from a contract-breaking list is dropped)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(h1[0][0]), make_rsrc(a.edge_logits, E * 4),
+                                              4 * a.s_orig[p], 0, 0);
     }
     Frag<PREC> fe;                                // e' split once for the r_next, head and message GEMMs
     prep<PREC>(ep, fe);
@@ -1676,7 +1690,9 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
       }
       lg += __shfl_xor(lg, 16);
       lg += __shfl_xor(lg, 32);
-      if (valid && g == 0) a.edge_logits[orig] = lg + hb[D + 64];
+      if (valid && g == 0)   // (descriptor store: an out-of-range id from a contract-breaking list is dropped)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lg + hb[D + 64]), make_rsrc(a.edge_logits, E * 4),
+                                              4 * orig, 0, 0);
     }
     // message: m = ReLU(P_t[dst] + W_t_e · e')
     gemm_f<PREC, 4>(WM, ep, fe, m);
@@ -2343,8 +2359,8 @@ __global__ __launch_bounds__(256) void node_table_kernel(NodeTableArgs a) {
     }
   }
   const float4 bb = ld4(a.pre_b + 16 * obc + 4 * g);
-  // X chunk -> LDS: 64 rows x 32 float4, 8 per thread
   {
+  // X chunk -> LDS: 64 rows x 32 float4, 8 per thread
     float4 t[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -2651,31 +2667,32 @@ __global__ __launch_bounds__(256) void fully_prepare_kernel(FullyPrepArgs a) {
   }
 }
 
-// ---- Symmetric prepare: edge_index sorted by (src, dst) and symmetric inside every image (PyG to_undirected's
+// ---- Symmetric prepare: edge_index sorted by (src, dst) without duplicates and symmetric (PyG to_undirected's
 // coalesced output: knn_mpn_graph, feature_knn_mpn_graph, score_based_graph, ConstructGraph.py:363-422).
-// Then the incoming edges of d are the outgoing ones reversed: segment (t, d) = the type-t entries of row d in
-// ascending source order, which is also the original edge-id order the sorting prepare produces, and the id of
-// edge (s -> d) = (start of row s) + (rank of d in row s). Per image one block holds the image's adjacency as
-// bit rows in LDS (<= 512 nodes), so the counts, the in-image offsets and every rank are popcounts; no sort,
-// no global atomics. Two launches: sym_count_kernel (per-image edge range and per-(image, type) edge totals),
-// sym_emit_kernel (offsets, segments, the three index arrays). Identical arrays to launch_prepare's.
-constexpr int SYM_MAXB = 64;        // images per batch
-constexpr int SYM_MAXN = 512;       // nodes per image (LDS bit rows)
-constexpr int SYM_W = SYM_MAXN / 32;
-constexpr int SYM_THREADS = 1024;
-// per image in the workspace (ws.sym): [0] first edge, [1] end edge, [2] validation bits, [3..3+T) type totals
-constexpr int SYM_REC = 4 + MAXT;
+// The incoming edges of d are then the entries of row d read backwards: segment (t, d) = the type-t entries of
+// row d in ascending source order (= edge-id order, the sorting prepare's tie order), and the id of the incoming
+// edge (x -> d) is the position of d in row x. Three launches, no zeroing, no atomics on the data path:
+//   sym_rows_kernel   one wave per node n: row n's bounds (64-way probes + one coalesced run), its entries packed
+//                     as (dst | type(dst) << 24), the (type, n) counts written directly (all T of them), checks;
+//   mpn_scan_kernel   (shared with the sorting prepare) + the reduction of the per-node check flags;
+//   sym_place_kernel  one wave per node d: each entry's rank among the same-type entries before it (ballots),
+//                     its segment slot, and the incoming edge's id by a binary search of d in row x.
+// Measured alternatives: per-image blocks over LDS adjacency bit rows (8 busy CUs) 31-35 us; a per-edge walk along
+// row d (knn rows hold ~60 entries) 25 us for the placement alone; the sorting prepare 25 us (C3 knn).
+constexpr int SYM_TBITS = 24;        // packed row entry: dst (< 2^24) | type << 24 (type 31: invalid, never matched)
+constexpr unsigned SYM_NMASK = (1u << SYM_TBITS) - 1u;
 
-// first position p in [0, n) with a[p] >= key (n if none), by all threads of the block: 1024-way probes per round
-__device__ int64_t block_lower_bound(const int64_t* __restrict__ a, int64_t n, int64_t key) {
+// first position p in [0, n) with a[p] >= key (n if none), by one wave: 64-way probes per round (E = 250k:
+// 3 rounds of one load per lane, no barriers); bounded on an unsorted list too
+__device__ int64_t wave_lower_bound(const int64_t* __restrict__ a, int64_t n, int64_t key) {
+  const int lane = threadIdx.x & 63;
   int64_t lo = 0, hi = n;                          // a[< lo] < key <= a[>= hi]
   while (lo < hi) {                                // (uniform)
-    const int64_t s = (hi - lo + SYM_THREADS - 1) / SYM_THREADS;
-    const int64_t q = lo + (int64_t)threadIdx.x * s;
-    const bool below = q < hi && a[q] < key;
-    const int c = __syncthreads_count(below);      // probes below key form a prefix
-    if (c == 0) { hi = lo; break; }
-    // the last probe below: a[lo + (c-1) s] < key; the next one (if any, < hi) is >= key
+    const int64_t s = (hi - lo + 63) / 64;
+    const int64_t q = lo + (int64_t)lane * s;
+    const unsigned long long m = __ballot(q < hi && a[q] < key);
+    const int c = __popcll(m);                     // probes below key form a prefix
+    if (c == 0) break;                             // a[lo] >= key
     const int64_t nlo = lo + (int64_t)(c - 1) * s + 1, nhi = min(hi, lo + (int64_t)c * s);
     lo = nlo;
     hi = nhi;
@@ -2683,168 +2700,98 @@ __device__ int64_t block_lower_bound(const int64_t* __restrict__ a, int64_t n, i
   return lo;
 }
 
-struct SymPrepArgs {
-  const int64_t* ei;                // [2, E]
-  int64_t E, N;
-  const int64_t* node_off;          // [B + 1] device
-  int B;
-  const int64_t* types;
-  int64_t ts;
-  int T, Gsplit;
-  int *sym, *seg, *wg_start, *s_src, *s_dst, *s_orig, *err;
-};
-
-__global__ __launch_bounds__(SYM_THREADS) void sym_count_kernel(SymPrepArgs a) {
-  __shared__ int tot[MAXT];
-  __shared__ int bad;
-  const int b = blockIdx.x, T = a.T;
-  const int64_t E = a.E, n0 = a.node_off[b], n1 = a.node_off[b + 1];
-  if (threadIdx.x < MAXT) tot[threadIdx.x] = 0;
-  if (threadIdx.x == 0) bad = 0;
-  if (b == 0 && threadIdx.x < 4) a.err[threadIdx.x] = 0;   // (sym_emit_kernel only ORs into it)
-  // unwritten slots (only for an input that breaks the symmetry contract) stay valid indices
-  for (int64_t i = (int64_t)b * SYM_THREADS + threadIdx.x; i < E; i += (int64_t)a.B * SYM_THREADS) {
-    a.s_src[i] = 0; a.s_dst[i] = 0; a.s_orig[i] = 0;
+__global__ __launch_bounds__(256) void sym_rows_kernel(const int64_t* __restrict__ ei, const int64_t* __restrict__ types,
+                                                       int64_t ts, int64_t N, int64_t E, int T, int* __restrict__ cnt,
+                                                       int2* __restrict__ rows, unsigned* __restrict__ packed,
+                                                       int* __restrict__ flags) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= N) return;                                         // (wave-uniform)
+  const int64_t r0 = wave_lower_bound(ei, E, n);              // row n starts here if the list is sorted
+  int f = 0, tcount = 0;                                      // lane t < T: type-t entries of row n
+  int64_t r = r0, prev = -1;
+  for (;;) {                                                  // the run of source n, 64 entries per round
+    const int64_t e = r + lane;
+    const bool in = e < E && ei[e] == n;
+    const unsigned long long out = __ballot(!in);
+    const int len = out ? __builtin_ctzll(out) : 64;          // (entries past a mismatch are not the row's)
+    const bool mine = lane < len;
+    const int64_t d = mine ? ei[E + e] : 0;
+    int t = 31;
+    if (mine) {
+      if (d < 0 || d >= N) f |= 1;
+      else {
+        const int64_t tt = T == 1 ? 0 : types[d * ts];
+        if (tt >= 0 && tt < T) t = (int)tt;
+        else f |= 2;                                          // (d is a source too: the list is symmetric)
+      }
+      packed[e] = (unsigned)d | ((unsigned)t << SYM_TBITS);
+    }
+    const int64_t dp = __shfl_up(d, 1);
+    if (mine && (lane ? dp : prev) >= d) f |= 4;              // targets of a row strictly ascending
+    unsigned long long rem = __ballot(mine && t < T);
+    while (rem) {                                             // one round per distinct type in the chunk
+      const int tu = __shfl(t, __builtin_ctzll(rem));
+      const unsigned long long m = __ballot(mine && t == tu);
+      if (lane == tu) tcount += __popcll(m);
+      rem &= ~m;
+    }
+    prev = __shfl(d, 63);
+    r += len;
+    if (len < 64) break;
   }
-  const int64_t e0 = block_lower_bound(a.ei, E, n0);
-  const int64_t e1 = block_lower_bound(a.ei, E, n1);
-  for (int64_t e = e0 + threadIdx.x; e < e1; e += SYM_THREADS) {
-    const int64_t s = a.ei[e], d = a.ei[E + e];
-    if (d < n0 || d >= n1 || d == s || (e > e0 && (a.ei[e - 1] > s || (a.ei[e - 1] == s && a.ei[E + e - 1] >= d))))
-      atomicOr(&bad, 4);                           // not sorted / not inside the image / self loop
-    const int64_t t = a.types[s * a.ts];
-    if (t >= 0 && t < T) atomicAdd(&tot[t], 1);
-    else atomicOr(&bad, 2);                        // skipped as a source, like mpn_count_kernel
+  if ((r0 > 0 && ei[r0 - 1] >= n) || (r < E && ei[r] < n)) f |= 4;   // neighbouring runs: ascending sources
+  if (lane < T) cnt[(int64_t)lane * N + n] = tcount;
+  for (int o = 32; o; o >>= 1) f |= __shfl_xor(f, o);
+  if (lane == 0) {
+    rows[n] = make_int2((int)r0, (int)r);
+    flags[n] = f;
   }
-  __syncthreads();
-  int* rec = a.sym + b * SYM_REC;
-  if (threadIdx.x == 0) { rec[0] = (int)e0; rec[1] = (int)e1; rec[2] = bad; }
-  if (threadIdx.x < T) rec[3 + threadIdx.x] = tot[threadIdx.x];
 }
 
-__global__ __launch_bounds__(SYM_THREADS) void sym_emit_kernel(SymPrepArgs a) {
-  __shared__ unsigned R[SYM_MAXN][SYM_W];          // adjacency bit rows of the image
-  __shared__ unsigned short pre[SYM_MAXN][SYM_W];  // per row: set bits in the words before w
-  __shared__ unsigned M[MAXT][SYM_W];              // type masks
-  __shared__ int rs[SYM_MAXN];                     // row start (relative to the image's first edge)
-  __shared__ int X[MAXT * SYM_MAXN];               // (t, d) counts, then their exclusive scan
-  __shared__ int base[MAXT + 1], wsum[SYM_THREADS / 64 + 1];
-  __shared__ int tstart_g[MAXT + 1], gt_sh[MAXT];
-  __shared__ int bad;
-  const int b = blockIdx.x, T = a.T;
-  const int64_t E = a.E, N = a.N, n0 = a.node_off[b];
-  const int nb = (int)(a.node_off[b + 1] - n0), W = (nb + 31) >> 5;
-  const int* rec = a.sym + b * SYM_REC;
-  const int e0 = rec[0], e1 = rec[1];
-  for (int i = threadIdx.x; i < SYM_MAXN * SYM_W; i += SYM_THREADS) (&R[0][0])[i] = 0;
-  for (int i = threadIdx.x; i < MAXT * SYM_W; i += SYM_THREADS) (&M[0][0])[i] = 0;
-  if (threadIdx.x == 0) bad = 0;
-  // type-major bases: all images' edges of types < t, then the type-t edges of images before b
-  if (threadIdx.x <= T) {
-    const int t = threadIdx.x;
-    int acc = 0;
-    for (int bb = 0; bb < a.B; ++bb)
-      for (int u = 0; u < T; ++u) {
-        const int v = a.sym[bb * SYM_REC + 3 + u];
-        if (u < t || (u == t && bb < b)) acc += v;
+__global__ __launch_bounds__(256) void sym_place_kernel(int64_t N, int T, const int* __restrict__ seg,
+                                                        const int2* __restrict__ rows,
+                                                        const unsigned* __restrict__ packed, int* __restrict__ s_src,
+                                                        int* __restrict__ s_dst, int* __restrict__ s_orig,
+                                                        int* __restrict__ err) {
+  const int lane = threadIdx.x & 63;
+  const int64_t d = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (d >= N) return;                                         // (wave-uniform)
+  const int2 rb = rows[d];
+  const unsigned long long below = (1ull << lane) - 1ull;
+  int carry = 0, bad = 0;                                     // lane t: type-t entries of row d in earlier chunks
+  for (int c = rb.x; c < rb.y; c += 64) {
+    const int e = c + lane;
+    const bool mine = e < rb.y;
+    const unsigned w = mine ? packed[e] : 0u;
+    const int x = (int)(w & SYM_NMASK), t = (int)(w >> SYM_TBITS);
+    const bool ok = mine && t < T;
+    int rank = 0;
+    unsigned long long rem = __ballot(ok);
+    while (rem) {
+      const int tu = __shfl(t, __builtin_ctzll(rem));
+      const unsigned long long m = __ballot(ok && t == tu);
+      const int cu = __shfl(carry, tu);
+      if (ok && t == tu) rank = cu + __popcll(m & below);
+      if (lane == tu) carry += __popcll(m);
+      rem &= ~m;
+    }
+    if (ok) {
+      const int pos = seg[(int64_t)t * N + d] + rank;
+      const int2 rx = rows[x];                                // row x holds d if the list is symmetric
+      int lo = rx.x, hi = rx.y;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((int)(packed[mid] & SYM_NMASK) < (int)d) lo = mid + 1; else hi = mid;
       }
-    base[t] = acc;                                 // base[T] = every edge of a valid source type
-    if (b == 0) tstart_g[t] = acc;                 // (b = 0: the type starts)
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < nb; i += SYM_THREADS) {
-    const int64_t t = a.types[(n0 + i) * a.ts];
-    if (t >= 0 && t < T) atomicOr(&M[t][i >> 5], 1u << (i & 31));
-  }
-  for (int e = e0 + threadIdx.x; e < e1; e += SYM_THREADS) {
-    const int s = (int)(a.ei[e] - n0), d = (int)(a.ei[E + e] - n0);
-    if (s < 0 || s >= nb || d < 0 || d >= nb) continue;   // (flagged by sym_count_kernel)
-    if (e == e0 || a.ei[e - 1] != a.ei[e]) rs[s] = e - e0;
-    atomicOr(&R[s][d >> 5], 1u << (d & 31));
-  }
-  __syncthreads();
-  for (int s = threadIdx.x; s < nb; s += SYM_THREADS) {
-    int acc = 0;
-    for (int w = 0; w < W; ++w) { pre[s][w] = (unsigned short)acc; acc += __popc(R[s][w]); }
-  }
-  // counts (t, d) = type-t entries of row d, type-major; 1 per thread-slot chunk of 9 for the scan
-  const int Q = T * nb;
-  constexpr int PER = (MAXT * SYM_MAXN + SYM_THREADS - 1) / SYM_THREADS;
-  int v[PER], local = 0;
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int q = threadIdx.x * PER + j;
-    int c = 0;
-    if (q < Q) {
-      const int t = q / nb, d = q - t * nb;
-      for (int w = 0; w < W; ++w) c += __popc(R[d][w] & M[t][w]);
-    }
-    v[j] = c;
-    local += c;
-  }
-  // block-wide exclusive scan of the thread sums
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int x = local;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int o = __shfl_up(x, off);
-    if (lane >= off) x += o;
-  }
-  if (lane == 63) wsum[wave] = x;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int acc = 0;
-    for (int w = 0; w < SYM_THREADS / 64; ++w) { const int t = wsum[w]; wsum[w] = acc; acc += t; }
-  }
-  __syncthreads();
-  {
-    int run = wsum[wave] + x - local;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int q = threadIdx.x * PER + j;
-      if (q < Q) X[q] = run;
-      run += v[j];
+      const bool found = lo < rx.y && (int)(packed[lo] & SYM_NMASK) == (int)d;
+      bad |= !found;
+      s_src[pos] = x;
+      s_dst[pos] = (int)d;
+      s_orig[pos] = found ? lo : 0;
     }
   }
-  __syncthreads();
-  // segments and their entries: one thread per (t, d)
-  for (int q = threadIdx.x; q < Q; q += SYM_THREADS) {
-    const int t = q / nb, d = q - t * nb;
-    int pos = base[t] + X[q] - X[t * nb];
-    a.seg[(int64_t)t * N + n0 + d] = pos;
-    const int dw = d >> 5;
-    const unsigned dbit = 1u << (d & 31), below = dbit - 1u;
-    for (int w = 0; w < W; ++w) {
-      unsigned bits = R[d][w] & M[t][w];
-      while (bits) {
-        const int s = 32 * w + __builtin_ctz(bits);
-        bits &= bits - 1u;
-        const unsigned rw = R[s][dw];
-        if (!(rw & dbit)) bad = 1;                 // (s -> d) missing: not symmetric
-        if (pos < E) {                             // (holds for a symmetric input)
-          a.s_src[pos] = (int)(n0 + s);
-          a.s_dst[pos] = (int)(n0 + d);
-          a.s_orig[pos] = e0 + rs[s] + pre[s][dw] + __popc(rw & below);
-        } else {
-          bad = 1;
-        }
-        ++pos;
-      }
-    }
-  }
-  __syncthreads();
-  if (b == 0) {
-    // nodes of other images are not visited by this block: seg of image-less nodes cannot exist (every node
-    // belongs to an image); the end marker and the pass split over the whole batch
-    if (threadIdx.x == 0) {
-      a.seg[(int64_t)T * N] = tstart_g[T];
-      int any = 0;
-      for (int bb = 0; bb < a.B; ++bb) any |= a.sym[bb * SYM_REC + 2];
-      if (any) atomicOr(a.err, any);             // 4: not a sorted symmetric list, 2: bad node type (mpn_status)
-    }
-    type_split(tstart_g, tstart_g[T], T, a.Gsplit, gt_sh, a.wg_start);
-  }
-  if (bad && threadIdx.x == 0) atomicOr(a.err, 4);   // not symmetric
+  if (__ballot(bad) && lane == 0) atomicOr(err, 8);          // (x -> d) missing: not symmetric
 }
 
 static int launch_prepare(const pemp_mpn_desc* desc, const int64_t* edge_index, const int64_t* node_types, int64_t N,
@@ -2872,6 +2819,28 @@ static int launch_prepare(const pemp_mpn_desc* desc, const int64_t* edge_index, 
                        ws.perm, ws.s_src, ws.s_dst, ws.s_orig);
     PEMP_LAUNCH_CHECK();
   }
+  return PEMP_OK;
+}
+
+static int launch_prepare_sym(const pemp_mpn_desc* desc, const int64_t* edge_index, const int64_t* node_types,
+                              int64_t N, int64_t E, const MpnWs& ws, hipStream_t st) {
+  const int T = desc->num_types;
+  const int64_t tstride = desc->types_stride > 0 ? desc->types_stride : 1;
+  const int64_t K = (int64_t)T * N;
+  ProfScope prof("mpn_prepare", st);
+  int2* rows = reinterpret_cast<int2*>(ws.sym);
+  int* flags = ws.sym + 2 * N;
+  unsigned* packed = reinterpret_cast<unsigned*>(ws.perm);
+  const unsigned g = (unsigned)((N + 3) / 4);                 // one wave per node
+  hipLaunchKernelGGL(sym_rows_kernel, dim3(g), dim3(256), 0, st, edge_index, node_types, tstride, N, E, T, ws.cnt, rows,
+                     packed, flags);
+  PEMP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(mpn_scan_kernel, dim3(1), dim3(1024), 0, st, ws.cnt, K, N, T, std::max(num_cus(), T), ws.seg,
+                     ws.wg_start, flags, N, E, ws.err);
+  PEMP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(sym_place_kernel, dim3(g), dim3(256), 0, st, N, T, ws.seg, rows, packed, ws.s_src, ws.s_dst,
+                     ws.s_orig, ws.err);
+  PEMP_LAUNCH_CHECK();
   return PEMP_OK;
 }
 
@@ -2947,7 +2916,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
                             const float* edge_attr, const int64_t* edge_index, const int64_t* node_types,
                             int64_t N, int64_t E, float* edge_logits, float* node_logits, float* class_logits,
                             void* workspace, size_t workspace_bytes, void* stream, const int64_t* fully_node_off,
-                            int fully_B, int fully_nmax, const int64_t* sym_node_off = nullptr, int sym_B = 0) {
+                            int fully_B, int fully_nmax, bool sym = false) {
   PEMP_CHECK_ARG(desc && w, "pemp_mpn_forward: null desc/weights");
   const int T = desc->num_types, J = desc->num_joints;
   PEMP_CHECK_ARG(desc->hidden == 64, "pemp_mpn_forward: hidden width must be 64 (got %d)", desc->hidden);
@@ -3060,14 +3029,9 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
       ProfScope prof("mpn_prepare", pst);
       hipLaunchKernelGGL(fully_prepare_kernel, dim3(gx, (unsigned)fully_B), dim3(256), 0, pst, fa);
       PEMP_LAUNCH_CHECK();
-    } else if (sym_node_off && N > 0) {
-      SymPrepArgs sa{edge_index, E, N, sym_node_off, sym_B, node_types, tstride, T, std::max(num_cus(), T),
-                     ws.sym, ws.seg, ws.wg_start, ws.s_src, ws.s_dst, ws.s_orig, ws.err};
-      ProfScope prof("mpn_prepare", pst);
-      hipLaunchKernelGGL(sym_count_kernel, dim3((unsigned)sym_B), dim3(SYM_THREADS), 0, pst, sa);
-      PEMP_LAUNCH_CHECK();
-      hipLaunchKernelGGL(sym_emit_kernel, dim3((unsigned)sym_B), dim3(SYM_THREADS), 0, pst, sa);
-      PEMP_LAUNCH_CHECK();
+    } else if (sym && N > 0) {
+      const int rc0 = launch_prepare_sym(desc, edge_index, node_types, N, E, ws, pst);
+      if (rc0) return rc0;
     } else {
       const int rc0 = launch_prepare(desc, edge_index, node_types, N, E, ws, pst);
       if (rc0) return rc0;
@@ -3151,7 +3115,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
     na.img = node_img;
     na.head_off = fused_embed_ ? mlp_lds_floats(w->node_emb) : 0;
     na.head_floats = mlp_lds_floats(w->node_head) + mlp_lds_floats(w->class_head);
-    if (mode != ROWS_NONE || na.node_out) {
+    if (na.mode != ROWS_NONE || na.node_out) {
       ProfScope prof(mode == ROWS_EMBED ? "node_embed" : "node_update", st);
       hipLaunchKernelGGL(node_rows_kernel, dim3(node_grid), dim3(256), node_rows_lds_bytes(na), st, na);
       PEMP_LAUNCH_CHECK();
@@ -3212,9 +3176,8 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
     side_lock.unlock();
     ss = nullptr;
   };
-  // side stream: the edge order first; then the node embedding + first node table here (short kernels with
-  // 16-row grids) while the order is prepared; then the range table and the edge embedding on the side stream
-  // (every CU, all of its LDS: the node kernels are done or nearly so by then)
+  // side stream: the edge order; meanwhile the node embedding + first node table here (short kernels with
+  // 16-row grids); then, joined, the range table and the edge embedding (every CU, all of its LDS)
   if (ss && (rc = edge_prepare())) { join_side(); return rc; }
   if (!fused_embed) {
     if ((rc = rows_mlp("node_embed", w->node_emb, x, desc->node_in_dim, N, ws.X, 128, ws.X + 64, 128, st))) {
@@ -3226,9 +3189,12 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
     join_side();
     return rc;
   }
+  // the edge embedding on the launch stream once the order is ready: the join's wait resolves behind the node
+  // kernels (a join after the embedding waited ~13 us for the cross-stream event, measured)
   if (ss) {
-    if ((rc = edge_embed())) { join_side(); return rc; }
+    pst = st;
     join_side();
+    if ((rc = edge_embed())) return rc;
   } else if ((rc = edge_prepare()) || (rc = edge_embed())) {
     return rc;
   }
@@ -3310,22 +3276,11 @@ extern "C" int pemp_mpn_forward_fully(const pemp_mpn_desc* desc, const pemp_mpn_
 
 extern "C" int pemp_mpn_forward_sym(const pemp_mpn_desc* desc, const pemp_mpn_weights* w, const float* x,
                                     const float* edge_attr, const int64_t* edge_index, const int64_t* node_types,
-                                    int64_t N, int64_t E, const int64_t* node_off, const int64_t* node_off_host, int B,
-                                    float* edge_logits, float* node_logits, float* class_logits, void* workspace,
-                                    size_t workspace_bytes, void* stream) {
-  PEMP_CHECK_ARG(node_off && node_off_host && B >= 1, "pemp_mpn_forward_sym: bad node offsets");
-  PEMP_CHECK_ARG(node_off_host[0] == 0 && node_off_host[B] == N, "pemp_mpn_forward_sym: offsets do not sum to N");
-  int64_t nmax = 0;
-  for (int b = 0; b < B; ++b) {
-    const int64_t n = node_off_host[b + 1] - node_off_host[b];
-    PEMP_CHECK_ARG(n >= 0, "pemp_mpn_forward_sym: decreasing offsets");
-    nmax = std::max(nmax, n);
-  }
-  if (B > SYM_MAXB || nmax > SYM_MAXN)   // the LDS bit rows hold <= 512 nodes: the sorting prepare above that
-    return mpn_forward_impl(desc, w, x, edge_attr, edge_index, node_types, N, E, edge_logits, node_logits,
-                            class_logits, workspace, workspace_bytes, stream, nullptr, 0, 0);
+                                    int64_t N, int64_t E, float* edge_logits, float* node_logits, float* class_logits,
+                                    void* workspace, size_t workspace_bytes, void* stream) {
+  // the packed row entries hold a node id in SYM_TBITS bits: larger graphs take the sorting prepare
   return mpn_forward_impl(desc, w, x, edge_attr, edge_index, node_types, N, E, edge_logits, node_logits, class_logits,
-                          workspace, workspace_bytes, stream, nullptr, 0, 0, node_off, B);
+                          workspace, workspace_bytes, stream, nullptr, 0, 0, N < (1ll << SYM_TBITS));
 }
 
 extern "C" int pemp_mpn_prepare(const pemp_mpn_desc* desc, const int64_t* edge_index, const int64_t* node_types,
@@ -3392,8 +3347,9 @@ extern "C" int pemp_mpn_status(const pemp_mpn_desc* desc, int64_t N, int64_t E, 
   PEMP_HIP(hipStreamSynchronize(as_stream(stream)));
   if (err & 1) { set_error("edge_index has entries outside [0, N)"); return PEMP_ERR_INVALID_ARG; }
   if (err & 2) { set_error("node_types has entries outside [0, num_types)"); return PEMP_ERR_INVALID_ARG; }
-  if (err & 4) {
-    set_error("edge_index is not sorted by (src, dst) and symmetric inside every image (pemp_mpn_forward_sym)");
+  if (err & 12) {
+    set_error("edge_index is not a symmetric edge list sorted by (src, dst) (pemp_mpn_forward_sym%s)",
+              (err & 4) ? ": order" : ": symmetry");
     return PEMP_ERR_INVALID_ARG;
   }
   return PEMP_OK;

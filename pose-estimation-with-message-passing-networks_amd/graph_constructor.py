@@ -37,11 +37,11 @@ def _tag_fully(edge_index, node_off, counts, joint_det):
     edge_index._pemp_fully = (node_off, tuple(counts), joint_det, joint_det._version, edge_index._version)
 
 
-def _tag_sym(edge_index, node_off, counts):
-    """Mark edge_index as a (src, dst)-sorted graph that is symmetric inside every image (PyG to_undirected's
-    output: knn, feature_knn, score_based), images contiguous with these node offsets (device) / counts (host),
-    so that the MPN can take pemp_mpn_forward_sym; the version detects in-place edits."""
-    edge_index._pemp_sym = (node_off, tuple(counts), edge_index._version)
+def _tag_sym(edge_index):
+    """Mark edge_index as a (src, dst)-sorted symmetric graph without duplicates (PyG to_undirected's output:
+    knn, feature_knn, score_based), so that the MPN can take pemp_mpn_forward_sym; the version detects in-place
+    edits."""
+    edge_index._pemp_sym = edge_index._version
 
 
 def get_graph_constructor(config, **kwargs):
@@ -305,11 +305,11 @@ class NaiveGraphConstructor:
                 edge_index, edge_attr = self._knn_edges(L, st, joint_det, joint_tags, F, joint_scores, node_off,
                                                         node_off_h, B, J, A, norm, mode, dev,
                                                         x if self.mpn_graph_type == "feature_knn" else None)
-                _tag_sym(edge_index, node_off, counts_l)
+                _tag_sym(edge_index)
             else:
                 edge_index = self._edges(L, st, joint_det, joint_scores, node_off, fully_off, node_off_h, B, dev)
                 if self.mpn_graph_type == "score_based":
-                    _tag_sym(edge_index, node_off, counts_l)
+                    _tag_sym(edge_index)
                 E = edge_index.shape[1]
                 edge_attr = torch.empty(E, A, dtype=torch.float32, device=dev)
                 _lib.check(L.pemp_edge_features(_lib.ptr(joint_det), _lib.ptr(joint_tags), F, _lib.ptr(joint_scores),

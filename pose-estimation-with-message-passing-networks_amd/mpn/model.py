@@ -237,7 +237,7 @@ class NodeClassificationMPNSimple(nn.Module):
             node_types = torch.tensor(TYPE_LUTS[self.node_summary], device=dev)[node_types]
         N, E = x.shape[0], edge_index.shape[1]
         fully = _fully_graph(edge_index, node_types, N) if self.node_summary == "not" else None
-        sym = _sym_graph(edge_index, N) if fully is None else None
+        sym = fully is None and _sym_graph(edge_index)
         x = _as(x, torch.float32)
         edge_attr = _as(edge_attr, torch.float32)
         edge_index = _as(edge_index, torch.int64)
@@ -277,11 +277,10 @@ class NodeClassificationMPNSimple(nn.Module):
                                                 edge_index.data_ptr(), node_types.data_ptr(), N, E, noff.data_ptr(),
                                                 offs, B, edge_logits.data_ptr(), node_logits.data_ptr(),
                                                 class_logits.data_ptr(), ws.data_ptr(), ws.numel(), st))
-        elif sym is not None:       # a to_undirected graph of the constructor: order from its bit rows
-            noff, offs, B = sym
+        elif sym:                   # a to_undirected graph of the constructor: order from its rows
             _lib.check(L.pemp_mpn_forward_sym(desc, fw.struct_ref, x.data_ptr(), edge_attr.data_ptr(),
-                                              edge_index.data_ptr(), node_types.data_ptr(), N, E, noff.data_ptr(),
-                                              offs, B, edge_logits.data_ptr(), node_logits.data_ptr(),
+                                              edge_index.data_ptr(), node_types.data_ptr(), N, E,
+                                              edge_logits.data_ptr(), node_logits.data_ptr(),
                                               class_logits.data_ptr(), ws.data_ptr(), ws.numel(), st))
         else:
             _lib.check(L.pemp_mpn_forward(desc, fw.struct_ref, x.data_ptr(), edge_attr.data_ptr(),
@@ -312,17 +311,11 @@ def _fully_graph(edge_index, node_types, N):
     return noff, (ctypes.c_int64 * (B + 1))(*itertools.accumulate(counts, initial=0)), B
 
 
-def _sym_graph(edge_index, N):
-    """(node_off, host offsets, B) when edge_index is an untouched (src, dst)-sorted symmetric graph of the
-    graph constructor (graph_constructor._tag_sym), else None."""
-    meta = getattr(edge_index, "_pemp_sym", None)
-    if meta is None or _SYM_OFF:
-        return None
-    noff, counts, ever = meta
-    if edge_index._version != ever or sum(counts) != N or not 1 <= len(counts) <= 64:
-        return None
-    B = len(counts)
-    return noff, (ctypes.c_int64 * (B + 1))(*itertools.accumulate(counts, initial=0)), B
+def _sym_graph(edge_index):
+    """True when edge_index is an untouched (src, dst)-sorted symmetric graph of the graph constructor
+    (graph_constructor._tag_sym)."""
+    ever = getattr(edge_index, "_pemp_sym", None)
+    return ever is not None and not _SYM_OFF and edge_index._version == ever
 
 
 def _as(t, dtype):

@@ -240,10 +240,10 @@ def test_fully_graph_fast_prepare_is_identical(prec, monkeypatch):
 @pytest.mark.parametrize("graph_type,persons,H", [("knn", 9, 160), ("knn", 28, 320), ("score_based", 9, 160),
                                                    ("feature_knn", 6, 128)])
 def test_symmetric_graph_fast_prepare_is_identical(graph_type, persons, H, monkeypatch):
-    """pemp_mpn_forward_sym (type-major order from the image's adjacency bit rows, for the constructor's
+    """pemp_mpn_forward_sym (type-major order read off the rows of the sorted list, for the constructor's
     to_undirected graphs) must give bit-identical logits to the sorting prepare; an empty image in the batch;
-    an in-place edit of edge_index drops the tag; a list that is not symmetric is reported by pemp_mpn_status
-    (the call itself stays in bounds)."""
+    an in-place edit of edge_index drops the tag; a list that is not symmetric, or not sorted, is reported by
+    pemp_mpn_status (the call itself stays in bounds)."""
     from pemp_amd import _lib
     from pemp_amd.mpn import model as mm
     B, J, W = 4, 17, H
@@ -258,7 +258,7 @@ def test_symmetric_graph_fast_prepare_is_identical(graph_type, persons, H, monke
                                          joints_gt=None, factor_list=None, masks=None, device=DEV,
                                          testing=True, heatmaps=None, num_joints=J).construct_graph()
     x, ea, ei, types = out[0], out[1], out[2], out[7][:, 2]
-    assert mm._sym_graph(ei, x.shape[0]) is not None
+    assert mm._sym_graph(ei)
     fast = run(model, x, ea, ei, types)
     monkeypatch.setattr(mm, "_SYM_OFF", True)
     slow = run(model, x, ea, ei, types)
@@ -267,15 +267,47 @@ def test_symmetric_graph_fast_prepare_is_identical(graph_type, persons, H, monke
         assert torch.equal(a, b)
     ei2 = ei.clone()
     ei.add_(0)
-    assert mm._sym_graph(ei, x.shape[0]) is None
-    assert mm._sym_graph(ei2, x.shape[0]) is None
-    # contract check: drop one direction of an edge (keep sorted order) -> status reports it
-    bad = torch.cat([ei2[:, :3], ei2[:, 4:]], 1).contiguous()
-    bad._pemp_sym = ei._pemp_sym[:2] + (bad._version,)
-    with pytest.raises(Exception, match="symmetric"):
-        with torch.no_grad():
-            model(x, ea[:bad.shape[1]].contiguous(), bad, node_types=types, validate=True)
-        torch.cuda.synchronize()
+    assert not mm._sym_graph(ei)
+    assert not mm._sym_graph(ei2)
+    # contract checks: drop one direction of an edge (sorted order kept), swap two edges (symmetric, unsorted)
+    drop = torch.cat([ei2[:, :3], ei2[:, 4:]], 1).contiguous()
+    swap = ei2.clone()
+    swap[:, [5, 9]] = swap[:, [9, 5]]
+    for bad, what in ((drop, "symmetry"), (swap, "order")):
+        bad._pemp_sym = bad._version
+        with pytest.raises(Exception, match="symmetric.*" + what):
+            with torch.no_grad():
+                model(x, ea[:bad.shape[1]].contiguous(), bad, node_types=types, validate=True)
+            torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("variant", ["attn", "max"])
+def test_symmetric_prepare_random_graph(variant, monkeypatch):
+    """pemp_mpn_forward_sym on a random symmetric list with self loops, nodes of unsorted types, isolated
+    nodes and one long row (a hub joined to every node), against the sorting prepare: bit-identical."""
+    from pemp_amd.mpn import model as mm
+    g = torch.Generator().manual_seed(11)
+    N = 700
+    m = torch.rand(N, N, generator=g) < 0.02
+    m[:, 3] = True                                              # hub node 3
+    m[np.arange(0, N, 7), np.arange(0, N, 7)] = True            # self loops
+    m[650:] = False                                             # isolated tail
+    m[:, 650:] = False
+    m = m | m.T
+    ei = m.nonzero().T.contiguous()                             # row-major: sorted by (src, dst)
+    E = ei.shape[1]
+    cfg = pcfg.published_mpn_config(17, 3, variant)             # (max: one message MLP, types ignored)
+    model, _ = make_model(cfg, 3.75, "f16x3")
+    types = torch.randint(0, 17, (N,), generator=g)
+    x = torch.randn(N, 128, generator=g)
+    ea = torch.randn(E, 19, generator=g)
+    eid = ei.to(DEV)
+    eid._pemp_sym = eid._version
+    fast = run(model, x.to(DEV), ea.to(DEV), eid, types.to(DEV))
+    monkeypatch.setattr(mm, "_SYM_OFF", True)
+    slow = run(model, x.to(DEV), ea.to(DEV), eid, types.to(DEV))
+    for a, b in zip(fast[0] + fast[1] + fast[2], slow[0] + slow[1] + slow[2]):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("variant", ["attn", "max"])
