@@ -255,54 +255,43 @@ __global__ __launch_bounds__(256) void mpn_count_kernel(const int64_t* __restric
 
 
 
-// Split G edge-pass workgroups (one per CU) over the types in proportion to their edge counts:
-// floor shares, >= 1 per non-empty type, leftovers by largest remainder (ties: lower type);
-// sum <= G. tstart[t] (LDS, t <= T) = first edge of type t, etot = all edges; gt = LDS scratch
-// [MAXT]. Thread t < T owns type t; block-wide (contains __syncthreads).
+// Split G edge-pass workgroups (one per CU) over the types so that the largest share, in 16-edge tiles per
+// workgroup, is as small as possible: L = the least tile load with sum_t ceil(tiles_t / L) <= G, then
+// gt = ceil(tiles_t / L) (>= 1 per non-empty type; sum <= G, spare workgroups get no range). The kernel's time is
+// its busiest CU's, so this, not proportional shares, is the balanced split. tstart[t] (LDS, t <= T) = first edge
+// of type t; gt = LDS scratch [MAXT]. Wave 0 does the search (T <= MAXT < 64); block-wide (contains
+// __syncthreads).
 __device__ void type_split(const int* tstart, int64_t etot, int T, int G, int* gt, int* wg_start) {
-  __shared__ long long rem_sh[MAXT];
-  if (threadIdx.x < T) {
-    const int t = threadIdx.x;
-    const int64_t et = tstart[t + 1] - tstart[t];
-    int share = et > 0 ? (int)(et * G / etot) : 0;
-    long long r = et > 0 ? (et * G) % etot : -1;
-    if (et > 0 && share == 0) { share = 1; r = -1; }
-    gt[t] = share;
-    rem_sh[t] = r;
+  (void)etot;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const int tiles = lane < T ? (tstart[lane + 1] - tstart[lane] + 15) / 16 : 0;
+    int hi = tiles;
+    for (int o = 32; o >= 1; o >>= 1) hi = max(hi, __shfl_xor(hi, o));
+    int lo = 1;
+    hi = max(hi, 1);
+    while (lo < hi) {   // (uniform)
+      const int mid = (lo + hi) >> 1;
+      int need = tiles > 0 ? (tiles + mid - 1) / mid : 0;
+      for (int o = 32; o >= 1; o >>= 1) need += __shfl_xor(need, o);
+      if (need <= G) hi = mid;
+      else lo = mid + 1;
+    }
+    const int share = tiles > 0 ? (tiles + lo - 1) / lo : 0;
+    int incl = share;   // inclusive prefix over the types
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o);
+      if (lane >= o) incl += v;
+    }
+    if (lane < T) {
+      gt[lane] = share;
+      wg_start[lane + 1] = incl;
+    }
+    if (lane == 0) wg_start[0] = 0;
   }
   __syncthreads();
-  int add = 0;
-  if (threadIdx.x < T) {
-    const int t = threadIdx.x;
-    int used = 0, rank = 0;
-    for (int u = 0; u < T; ++u) {
-      used += gt[u];
-      rank += rem_sh[u] > rem_sh[t] || (rem_sh[u] == rem_sh[t] && u < t);
-    }
-    add = rem_sh[t] >= 0 && rank < G - used;
-  }
-  __syncthreads();
-  if (threadIdx.x < T) gt[threadIdx.x] += add;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int used = 0;
-    for (int t = 0; t < T; ++t) used += gt[t];
-    for (; used > G; --used) {           // only when many tiny types were raised to 1
-      int big = 0;
-      for (int t = 1; t < T; ++t) if (gt[t] > gt[big]) big = t;
-      if (gt[big] <= 1) break;
-      --gt[big];
-    }
-    int acc = 0;
-    wg_start[0] = 0;
-    for (int t = 0; t < T; ++t) {
-      acc += gt[t];
-      wg_start[t + 1] = acc;
-    }
-  }
 }
 
-// Exclusive scan of the (type, target) counts -> seg[0..K]; then per-type first workgroup of
 // the edge-step grid (wg_start). One 1024-thread block, 16 contiguous counts per thread per pass
 // (all loads of a pass in flight together), carry across passes. The per-type segment starts
 // seg[t*N] are captured from LDS on the way out (no read-back of seg).
@@ -1334,7 +1323,15 @@ enum { STAGE_MID = 1, STAGE_LAST = 2, STAGE_EPT = 4 };
 template <int HEAD>
 constexpr int edge_waves() { return HEAD == 1 ? 12 : EDGE_WAVES; }
 
-// wave range table entry: first, end (sorted positions), source type, unused
+// wave range table entry: first, end (sorted positions), source type, flags. A workgroup's range is its type's
+// equal share of 16-edge tiles (type_split), moved forward to the next segment start, so that no (target, type)
+// segment spans two workgroups. Inside it the waves take whole tiles, q or q + 1 each (the older waves, which
+// the SIMD arbitration favours, the extra ones; waves w, w + 4, w + 8, w + 12 share a SIMD and their sums differ
+// by at most one tile). A segment may then run across a wave boundary: its pieces go to the waves' LDS records
+// and the wave holding its first piece combines them after the tile loop (edge_step_kernel).
+// flags: 1 = the range starts inside a segment begun by the previous wave, 2 = its last segment continues into
+// the next wave, 4 = the whole range is one segment
+enum { RANGE_CONT_IN = 1, RANGE_CONT_OUT = 2, RANGE_ONE_SEG = 4 };
 __device__ inline int4 edge_wave_range(const int* __restrict__ seg, const int* __restrict__ wg_start,
                                        const int* __restrict__ s_dst, int T, int64_t N, int blk, int wave, int NW) {
   if (blk >= wg_start[T]) return make_int4(0, 0, 0, 0);
@@ -1342,15 +1339,24 @@ __device__ inline int4 edge_wave_range(const int* __restrict__ seg, const int* _
   while (t + 1 < T && wg_start[t + 1] <= blk) ++t;
   const int ts = seg[t * N], te = seg[(t + 1) * N];
   const int gt = wg_start[t + 1] - wg_start[t], j = blk - wg_start[t];
-  const int64_t n_t = te - ts;
-  const int lo = ts + (int)(n_t * j / gt), hi = ts + (int)(n_t * (j + 1) / gt);
-  const int64_t n_b = hi - lo;
+  const int64_t tiles_t = (te - ts + 15) / 16;
   auto snap = [&](int p) -> int {               // first segment start at or after p
-    if (p <= ts || p >= te) return p;
+    if (p <= ts || p >= te) return min(p, te);
     const int dp = min(max(s_dst[p], 0), (int)N - 1);   // (clamped: in range for any prepared list)
     return dp == s_dst[p - 1] ? seg[t * N + dp + 1] : p;
   };
-  return make_int4(snap(lo + (int)(n_b * wave / NW)), snap(lo + (int)(n_b * (wave + 1) / NW)), t, 0);
+  const int lo = snap(ts + 16 * (int)(tiles_t * j / gt)), hi = snap(ts + 16 * (int)(tiles_t * (j + 1) / gt));
+  const int ntile = (hi - lo + 15) / 16;
+  const int q = ntile / NW, r = ntile % NW;
+  const int a0 = wave * q + min(wave, r), a1 = a0 + q + (wave < r ? 1 : 0);
+  const int first = min(hi, lo + 16 * a0), end = min(hi, lo + 16 * a1);
+  int flags = 0;
+  if (first < end) {
+    if (first > lo && s_dst[first - 1] == s_dst[first]) flags |= RANGE_CONT_IN;
+    if (end < hi && s_dst[end - 1] == s_dst[end]) flags |= RANGE_CONT_OUT;
+    if (s_dst[first] == s_dst[end - 1]) flags |= RANGE_ONE_SEG;
+  }
+  return make_int4(first, end, t, flags);
 }
 
 // ranges for the middle passes (EDGE_WAVES waves) then the recorded passes (edge_waves<1>()), G blocks
@@ -1445,6 +1451,10 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
   constexpr int IMG_F = img_common(UPD) + (HEAD == 1 ? IMG_HEAD : 0);
   __shared__ __attribute__((aligned(16))) float img[IMG_F];
   __shared__ __attribute__((aligned(16))) float rbuf[NW * 1024];
+  // per wave: the pieces of the segments cut by its range ends ([0] the first segment, begun by an earlier wave;
+  // [1] the last, continued by later waves): raw aggregate (64 floats), running max, normaliser
+  constexpr int PREC_F = 68;
+  __shared__ __attribute__((aligned(16))) float pieces[NW * 2 * PREC_F];
   float* vec = img + (3 + UPD) * D * LDW;          // e2_b[64] | attn_w[64] | attn_b
   float* hw = img + img_common(UPD);               // HEAD 1: L1 [64][LDW], L2 [32][LDW], b1[64], b2[32], w3[32], b3
   float* hb_l = hw + (D + 32) * LDW;
@@ -1462,9 +1472,12 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
   // downstream are compiled as divergent)
   const int first = __builtin_amdgcn_readfirstlane(rg.x), end = __builtin_amdgcn_readfirstlane(rg.y);
   const int t = __builtin_amdgcn_readfirstlane(rg.z);
+  const int rflags = __builtin_amdgcn_readfirstlane(rg.w);
   float* mybuf = rbuf + wave * 1024;
   const int E = (int)a.E;
-  const rsrc_t rs_r = make_rsrc(a.r_cur, E * 256), rs_q = make_rsrc(a.Q0, E * 256);
+  // r / Q0 rows past the wave's range end are out of the descriptor: the last tile's DMA moves no bytes
+  // for them (its masked lanes read 0)
+  const rsrc_t rs_r = make_rsrc(a.r_cur, end * 256);
   const rsrc_t rs_dst = make_rsrc(a.s_dst, E * 4), rs_src = make_rsrc(a.s_src, E * 4);
   const rsrc_t rs_nt = make_rsrc(a.NT, (int)a.N * a.t_nt_ld * 4);
   const rsrc_t rs_orig = make_rsrc(a.s_orig, E * 4);
@@ -1483,14 +1496,14 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
       xp[ob] = bld4(rs_nt, va + 64 * ob, nt_p);
     }
   };
-  // first two tiles' indices and the first tile's r rows in flight before the weight copy
+  // prologue order: the first two tiles' indices (the only loads the first gathers wait for: small, ahead of the
+  // kernel-start burst), the type image, the first tile's node-table gathers, then its r rows
   int dst_n = 0, src_n = 0, dst_nn = 0, src_nn = 0;
   if (first < end) {   // (uniform)
     dst_n = bld1(rs_dst, 4 * min(first + c, end - 1));
     src_n = bld1(rs_src, 4 * min(first + c, end - 1));
     dst_nn = bld1(rs_dst, 4 * min(first + 16 + c, end - 1));
     src_nn = bld1(rs_src, 4 * min(first + 16 + c, end - 1));
-    dma_rows(rs_r, first, mybuf, lane);
   }
   {
     // the block's type image: IMG_F floats, 1 KB per wave instruction, waves interleaved
@@ -1503,16 +1516,18 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
   }
   if (first < end) {
     gather_nt(dst_n, src_n, true);
+    dma_rows(rs_r, first, mybuf, lane);
     if (HEAD == 1) orig_t = bld1(rs_orig, 4 * min(first + c, end - 1));
   }
   __syncthreads();
   EDGE_STAMP(1);
   EDGE_STAMP(2);
-  if (first >= end) { EDGE_STAMP(15); return; }
+  // target of the segment begun by the previous wave (lane 0 of the first tile's indices; wave-uniform)
+  const int seg_first = (rflags & RANGE_CONT_IN) ? __builtin_amdgcn_readfirstlane(dst_n) : -1;
   const rsrc_t rs_next = make_rsrc(a.r_next, E * 256);
   const rsrc_t rs_agg = make_rsrc(a.agg, (int)a.N * T * 256);
-  const u32x4v_s rw_r = rsrc_words(a.r_cur, E * 256);
-  const u32x4v_s rw_q = rsrc_words(a.Q0, E * 256);
+  const u32x4v_s rw_r = rsrc_words(a.r_cur, end * 256);
+  const u32x4v_s rw_q = rsrc_words(a.Q0, end * 256);
   // stores issued after a tile's DMA, all unconditional (masked lanes write past the buffer end): the
   // r_next rows (middle passes that write them) and the aggregate rows
   const bool store_next = MID && a.write_next;
@@ -1768,9 +1783,21 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
       const float inv = ((AGG == PEMP_AGGR_ATTN) ? 1.0f / (l + 1e-12f) : (AGG == PEMP_AGGR_MEAN) ? 1.0f / l : 1.0f) *
                         dom_inv<PREC>();
       const bool out = valid && ck.tail && !(carry_out && c == 15);
-      const int vo = out ? (seg * T + t) * 256 + 16 * g : OOB_VOFF;
+      // a segment cut by a range end: its raw piece goes to this wave's record instead (at most two per wave; the
+      // last segment of the range ends at the last tile's last valid lane)
+      const bool pin = seg == seg_first;
+      const bool pout = (rflags & RANGE_CONT_OUT) && !more && seg == __builtin_amdgcn_readlane(seg, end - 1 - base);
+      const bool piece = out && (pin || pout);
+      const int vo = out && !piece ? (seg * T + t) * 256 + 16 * g : OOB_VOFF;
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob) bst4(rs_agg, vo + 64 * ob, v[ob][0] * inv, v[ob][1] * inv, v[ob][2] * inv, v[ob][3] * inv);
+      if (piece) {
+        float* rec = pieces + (2 * wave + (pin ? 0 : 1)) * PREC_F;
+#pragma unroll
+        for (int ob = 0; ob < 4; ++ob)
+          *reinterpret_cast<float4*>(rec + 16 * ob + 4 * g) = make_float4(v[ob][0], v[ob][1], v[ob][2], v[ob][3]);
+        if (g == 0) { rec[64] = M; rec[65] = l; }
+      }
     }
     {   // the next tile's gathers, unconditional (past the range: OOB offsets, no traffic)
       gather_nt(dst_n, src_n, more);
@@ -1780,6 +1807,35 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
     asm volatile("" ::"v"(v[0][0]), "v"(v[3][3]));
     if (tile_no < 4) EDGE_STAMP(5 + 3 * tile_no);
 #endif
+  }
+  // segments cut by wave boundaries: the wave holding the first piece combines the pieces in range order (the
+  // later waves' [0] records, while those are whole-range middle pieces) and writes the aggregate row
+  __syncthreads();
+  constexpr int MIDDLE = RANGE_CONT_IN | RANGE_CONT_OUT | RANGE_ONE_SEG;   // a whole range inside one segment
+  if ((rflags & RANGE_CONT_OUT) && (rflags & MIDDLE) != MIDDLE) {
+    const float* r0 = pieces + (2 * wave + 1) * PREC_F;
+    float M = r0[64], l = r0[65], v = r0[lane];
+    for (int k = wave + 1; k < NW; ++k) {
+      const float* rk = pieces + 2 * k * PREC_F;
+      const float Mk = rk[64], lk = rk[65], vk = rk[lane];
+      if (AGG == PEMP_AGGR_ATTN) {
+        const float Mn = fmaxf(M, Mk), fa = pemp_exp(M - Mn), fb = pemp_exp(Mk - Mn);
+        l = l * fa + lk * fb;
+        v = v * fa + vk * fb;
+        M = Mn;
+      } else if (AGG == PEMP_AGGR_MAX) {
+        v = fmaxf(v, vk);
+      } else {
+        l += lk;
+        v += vk;
+      }
+      const int fk = __builtin_amdgcn_readfirstlane(a.ranges[lb * NW + k].w);
+      if ((fk & MIDDLE) != MIDDLE) break;
+    }
+    const float inv = ((AGG == PEMP_AGGR_ATTN) ? 1.0f / (l + 1e-12f) : (AGG == PEMP_AGGR_MEAN) ? 1.0f / l : 1.0f) *
+                      dom_inv<PREC>();
+    const int seg_last = __builtin_amdgcn_readfirstlane(a.s_dst[end - 1]);
+    a.agg[((int64_t)seg_last * T + t) * 64 + lane] = v * inv;
   }
   EDGE_STAMP(15);
 }
@@ -2489,7 +2545,8 @@ static EdgeImgArgs edge_image_args(const pemp_mpn_desc& d, const pemp_mpn_weight
 
 // whether the edge passes pre-apply the update block (UPD) and carry the published head (HEAD 1)
 static bool edge_upd_fused(const pemp_mpn_desc& d, const pemp_mpn_weights& w) {
-  return (d.aggr == PEMP_AGGR_ATTN || d.aggr == PEMP_AGGR_MEAN) && w.upd_w && (d.precision == PEMP_PREC_FP32 || w.upd_bf);
+  static const bool off = getenv("PEMP_NO_UPD_FUSE") != nullptr;   // (A/B switch: update MLP on the nodes)
+  return !off && (d.aggr == PEMP_AGGR_ATTN || d.aggr == PEMP_AGGR_MEAN) && w.upd_w && (d.precision == PEMP_PREC_FP32 || w.upd_bf);
 }
 static bool edge_pub_head(const pemp_mpn_desc& d, const pemp_mpn_weights& w) {
   return published_head(w.edge_head) && (d.precision == PEMP_PREC_FP32 || w.head_bf);

@@ -38,6 +38,8 @@ for pas in [int(a) for a in (sys.argv[1:] or ["0", "2"])]:
     torch.cuda.synchronize()
     fn(None, -1)
     s = buf.view(nw, 16).cpu().numpy().astype(np.int64)
+    if os.environ.get("STAMP_OUT"):
+        np.save(f"{os.environ['STAMP_OUT']}_pass{pas}.npy", s)
     live = s[:, 0] > 0
     s = s[live]
     t0 = s[:, 0].min()

@@ -1,0 +1,6 @@
+set -o pipefail
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_mpn.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r03s4_mpn.log 2>&1 && \
+timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 > gpurun_out/r03s4_c3.json 2>/dev/null && \
+PEMP_LIB=build_ab/libpemp_base.so timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 > gpurun_out/r03s4_c3_base.json 2>/dev/null && \
+STAMP_OUT=gpurun_out/r03s4_st PEMP_LIB=build_ab/libpemp_stamps.so timeout -k 10 200 python tools/edge_timeline.py 0 2 > gpurun_out/r03s4_timeline.txt 2>&1
