@@ -58,7 +58,33 @@ __device__ __forceinline__ bool better(float v1, int i1, float v2, int i2) {
 // unit owns column x = strip * sc - p + c.
 struct DetectGeom {
   int B, J, H, W, p, K, sc, nsx, nb, units, S;
+  unsigned mu, mn;   // unsigned division by units / nsx: q = (umulhi(n, m) + n) >> l (n < 2^31)
+  int lu, ln;
 };
+
+// Granlund-Montgomery constants of an unsigned division by d >= 1 for dividends below 2^31
+static void fastdiv_consts(unsigned d, unsigned& m, int& l) {
+  l = 0;
+  while ((1ull << l) < d) ++l;
+  m = (unsigned)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+}
+
+__device__ __forceinline__ int fastdiv(int n, unsigned m, int l) {
+  return (int)((__umulhi((unsigned)n, m) + (unsigned)n) >> l);
+}
+
+// plane, band and strip of unit u (wave-uniform; a few scalar instructions instead of two divisions)
+struct UnitPos {
+  int plane, band, strip;
+};
+__device__ __forceinline__ UnitPos unit_pos(const DetectGeom& g, int u) {
+  UnitPos q;
+  q.plane = fastdiv(u, g.mu, g.lu);
+  const int rem = u - q.plane * g.units;
+  q.band = fastdiv(rem, g.mn, g.ln);
+  q.strip = rem - q.band * g.nsx;
+  return q;
+}
 
 static DetectGeom geom(int B, int J, int H, int W, int pool_k, int K) {
   DetectGeom g;
@@ -68,6 +94,8 @@ static DetectGeom geom(int B, int J, int H, int W, int pool_k, int K) {
   g.nb = (H + SR - 1) / SR;
   g.units = g.nb * g.nsx;
   g.S = g.nb;
+  fastdiv_consts((unsigned)g.units, g.mu, g.lu);
+  fastdiv_consts((unsigned)g.nsx, g.mn, g.ln);
   return g;
 }
 
@@ -372,15 +400,25 @@ template <int P>
 __device__ __forceinline__ void load_unit_clamped(const float* __restrict__ s, const DetectGeom& g, int u,
                                                   float (&r)[SR + 2 * P]) {
   const int lane = threadIdx.x & 63;
-  const int plane = u / g.units, rem = u - plane * g.units, band = rem / g.nsx, strip = rem - band * g.nsx;
-  const int y0 = band * SR, x = strip * g.sc - P + lane;
+  const UnitPos q = unit_pos(g, u);
+  const int y0 = q.band * SR, x = q.strip * g.sc - P + lane;
   const int xo = min(max(x, 0), g.W - 1);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(s + (size_t)plane * g.H * g.W), 0, g.H * g.W * 4, 0x00020000);
+      const_cast<float*>(s + (size_t)q.plane * g.H * g.W), 0, g.H * g.W * 4, 0x00020000);
+  const int rowb = g.W * 4;
+  if (y0 - P >= 0 && y0 + SR + P <= g.H) {   // interior band (uniform): one running row offset
+    int so = (y0 - P) * rowb;
 #pragma unroll
-  for (int i = 0; i < SR + 2 * P; ++i) {
-    const int yc = min(max(y0 - P + i, 0), g.H - 1);
-    r[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, 4 * xo, yc * g.W * 4, 0));
+    for (int i = 0; i < SR + 2 * P; ++i) {
+      r[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, 4 * xo, so, 0));
+      so += rowb;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < SR + 2 * P; ++i) {
+      const int yc = min(max(y0 - P + i, 0), g.H - 1);
+      r[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, 4 * xo, yc * rowb, 0));
+    }
   }
 }
 
@@ -451,7 +489,8 @@ __global__ __launch_bounds__(NT1) void nms_strips_kernel(
   if (PF && u < u_hi) load(u);
   for (; u < u_hi; u += stride_u) {
     if (!PF) load(u);
-    const int plane = u / g.units, rem = u - plane * g.units, band = rem / g.nsx, strip = rem - band * g.nsx;
+    const UnitPos up = unit_pos(g, u);
+    const int plane = up.plane, band = up.band, strip = up.strip;
     const int b = plane / g.J;
     const int y0 = band * SR, x = strip * g.sc - P + lane;
     const bool lane_ok = lane >= P && lane < 64 - P && x < W;
@@ -478,21 +517,24 @@ __global__ __launch_bounds__(NT1) void nms_strips_kernel(
       }
     // per lane: threshold bits and non-negative bits over the unit's rows, the largest value
     // (per-row ballots + scalar popcounts for the counts measured slower: 91 vs 67 us)
-    float v[SR];
-    unsigned int tbits = 0, nnbits = 0;
-    float vmax_l = -INFINITY;
+    // the row / lane validity applied once to the per-row bits (rows past the plane: last band only)
     const int rows = min(SR, H - y0);
+    const unsigned vmask = lane_ok ? (rows >= 32 ? 0xffffffffu : ((1u << rows) - 1u)) : 0u;
+    float v[SR];
+    unsigned int tbits = 0, nnbits = 0, posbits = 0;
 #pragma unroll
     for (int j = 0; j < SR; ++j) {
       float jm = (vm[j] == c[j]) ? 1.0f : 0.0f;
       if (MASKED) jm = jm * masks[((size_t)b * H + min(y0 + j, H - 1)) * W + min(max(x, 0), W - 1)];
       const float vj = c[j] * jm;                       // ConstructGraph.py:1162-1165
-      const bool ok = lane_ok && j < rows;
-      v[j] = ok ? vj : NAN;
-      tbits |= (unsigned)(ok && !(vj < thr) && vj != 0.0f) << j;
-      nnbits |= (unsigned)(ok && vj >= 0.0f) << j;
-      vmax_l = fmaxf(vmax_l, v[j]);                     // NaN (invalid) is ignored by fmaxf
+      v[j] = vj;
+      tbits |= (unsigned)(!(vj < thr) && vj != 0.0f) << j;
+      nnbits |= (unsigned)(vj >= 0.0f) << j;
+      posbits |= (unsigned)(vj > 0.0f) << j;
     }
+    tbits &= vmask;
+    nnbits &= vmask;
+    posbits &= vmask;
     if (!use_thr) tbits = 0;
     cbits[(size_t)u * 64 + lane] = (cmask_t)tbits;
     int cnt = __popc(tbits), nonneg = __popc(nnbits);
@@ -501,9 +543,14 @@ __global__ __launch_bounds__(NT1) void nms_strips_kernel(
       cnt += __shfl_xor(cnt, off);
       nonneg += __shfl_xor(nonneg, off);
     }
-    const bool anypos = __ballot(vmax_l > 0.0f) != 0;
+    const bool anypos = __ballot(posbits != 0) != 0;
     if (lane == 0) { tile_count[u] = cnt; tile_nonneg[u] = nonneg; }
     const int base_id = y0 * W + x;
+    if (MODE == MODE_ALL || anypos || nonneg < K) {   // (uniform; rare with MODE_POS) invalid rows -> NaN
+#pragma unroll
+      for (int j = 0; j < SR; ++j)
+        if (!((vmask >> j) & 1u)) v[j] = NAN;
+    }
     if (MODE == MODE_POS) {
       if (anypos) wave_topk(v, base_id, W, K, [](float a) { return a > 0.0f; }, cand_v + (size_t)u * K, cand_i + (size_t)u * K);
       else write_sentinels(cand_v + (size_t)u * K, cand_i + (size_t)u * K, K);
