@@ -1322,6 +1322,10 @@ enum { STAGE_MID = 1, STAGE_LAST = 2, STAGE_EPT = 4 };
 // weights in LDS and needs more registers: 12
 template <int HEAD>
 constexpr int edge_waves() { return HEAD == 1 ? 12 : EDGE_WAVES; }
+// the last pass (no next r, no W1 in its image) fits 16 waves with the head too: it shares the middle passes'
+// range table
+template <int HEAD, int STAGE>
+constexpr int edge_waves_s() { return (HEAD == 1 && (STAGE & 3) == STAGE_MID) ? 12 : EDGE_WAVES; }
 
 // wave range table entry: first, end (sorted positions), source type, flags. A workgroup's range is its type's
 // equal share of 16-edge tiles (type_split), moved forward to the next segment start, so that no (target, type)
@@ -1441,22 +1445,24 @@ __device__ __forceinline__ float pemp_exp(float x) { return PEMP_FAST_EXP ? __ex
 #define PEMP_XCD_MAP 1
 #endif
 template <int AGG, int HEAD, int PREC, int UPD, int STAGE>
-__global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(EdgeStepArgs a) {
-  constexpr int NW = edge_waves<HEAD>();
+__global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_kernel(EdgeStepArgs a) {
+  constexpr int NW = edge_waves_s<HEAD, STAGE>();
   // STAGE bit 2 (STAGE_EPT): EDGE_MLP per_type (TypeAwareEdgeUpdate, layers.py:275-303). The node
   // terms A'[dst] + B'[src] (already through their own ReLU and out-block, node_ept_kernel) join
   // after the e-block GEMM instead of inside the first ReLU.
   constexpr bool EPT = (STAGE & STAGE_EPT) != 0;
   constexpr bool MID = (STAGE & 3) == STAGE_MID;
-  constexpr int IMG_F = img_common(UPD) + (HEAD == 1 ? IMG_HEAD : 0);
+  // the last pass writes no next r: its copy of the image starts past W1 (SKIP floats)
+  constexpr int SKIP = MID ? 0 : D * LDW;
+  constexpr int IMG_F = img_common(UPD) + (HEAD == 1 ? IMG_HEAD : 0) - SKIP;
   __shared__ __attribute__((aligned(16))) float img[IMG_F];
   __shared__ __attribute__((aligned(16))) float rbuf[NW * 1024];
   // per wave: the pieces of the segments cut by its range ends ([0] the first segment, begun by an earlier wave;
   // [1] the last, continued by later waves): raw aggregate (64 floats), running max, normaliser
   constexpr int PREC_F = 68;
   __shared__ __attribute__((aligned(16))) float pieces[NW * 2 * PREC_F];
-  float* vec = img + (3 + UPD) * D * LDW;          // e2_b[64] | attn_w[64] | attn_b
-  float* hw = img + img_common(UPD);               // HEAD 1: L1 [64][LDW], L2 [32][LDW], b1[64], b2[32], w3[32], b3
+  float* vec = img + (3 + UPD) * D * LDW - SKIP;   // e2_b[64] | attn_w[64] | attn_b
+  float* hw = img + img_common(UPD) - SKIP;        // HEAD 1: L1 [64][LDW], L2 [32][LDW], b1[64], b2[32], w3[32], b3
   float* hb_l = hw + (D + 32) * LDW;
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1507,7 +1513,7 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
   }
   {
     // the block's type image: IMG_F floats, 1 KB per wave instruction, waves interleaved
-    const float* src = a.img + (int64_t)t * a.img_stride;
+    const float* src = a.img + (int64_t)t * a.img_stride + SKIP;
     constexpr int PIECES = IMG_F / 256, TAIL = IMG_F - PIECES * 256;
     for (int k = wave; k < PIECES; k += NW)
       dma16(src + 256 * k + 4 * lane, img + 256 * k);
@@ -1545,9 +1551,9 @@ __global__ __launch_bounds__(64 * edge_waves<HEAD>()) void edge_step_kernel(Edge
     int z = 0;
     asm volatile("" : "+s"(z));
     const float* W1 = img + z;                    // each matrix: 64 x LDW floats (or its hi + lo 16-bit parts)
-    const float* W2 = img + z + D * LDW;
-    const float* WM = img + z + 2 * D * LDW;
-    const float* UW = img + z + 3 * D * LDW;
+    const float* W2 = img + z + D * LDW - SKIP;   // (W1: middle passes only, SKIP = 0)
+    const float* WM = img + z + 2 * D * LDW - SKIP;
+    const float* UW = img + z + 3 * D * LDW - SKIP;
     const float* hwz = hw + z;
     const int p = base + c;
     const bool valid = p < end;
@@ -2517,7 +2523,8 @@ static void launch_edge_step_s(const EdgeStepArgs& a, bool head, bool pub, int g
   if (!head)
     hipLaunchKernelGGL((edge_step_kernel<AGG, 0, PREC, UPD, STAGE>), dim3(grid), dim3(64 * edge_waves<0>()), 0, st, a);
   else if (pub)
-    hipLaunchKernelGGL((edge_step_kernel<AGG, 1, PREC, UPD, STAGE>), dim3(grid), dim3(64 * edge_waves<1>()), 0, st, a);
+    hipLaunchKernelGGL((edge_step_kernel<AGG, 1, PREC, UPD, STAGE>), dim3(grid), dim3(64 * edge_waves_s<1, STAGE>()), 0,
+                       st, a);
   else
     hipLaunchKernelGGL((edge_step_kernel<AGG, 2, PREC, UPD, STAGE>), dim3(grid), dim3(64 * edge_waves<2>()), 0, st, a);
 }
@@ -3265,7 +3272,8 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
       EdgeStepArgs ea{};
       ea.N = N; ea.E = E; ea.T = T; ea.t_nt_ld = NO;
       const bool pub = record && pub_head;         // the published head's weights ride in the LDS image
-      ea.ranges = ws.ranges + (pub ? (int64_t)edge_grid * EDGE_WAVES : 0);
+      // (12-wave table: recorded middle passes with the published head; every other pass runs 16 waves)
+      ea.ranges = ws.ranges + (pub && !last ? (int64_t)edge_grid * EDGE_WAVES : 0);
       ea.s_src = ws.s_src; ea.s_dst = ws.s_dst; ea.s_orig = ws.s_orig;
       const int stage = (last ? STAGE_LAST : STAGE_MID) | (ept ? STAGE_EPT : 0);
       ea.NT = ws.NT; ea.Q0 = ws.Q0; ea.r_cur = e_cur; ea.r_next = e_nxt;
