@@ -879,6 +879,24 @@ __device__ __forceinline__ void load_edge_attr(rsrc_t rs_ea, int A, int o, float
     for (int r = 0; r < 4; ++r) x[mb][r] = 16 * mb + 4 * g + r < A ? v[mb][r] : 0.0f;
 }
 
+// the first 32 features of the tile's edge_attr rows (A <= 32: the fixed published shape), raw and unmasked,
+// issued one tile ahead of their use (ea_mask)
+__device__ __forceinline__ void load_edge_attr32(rsrc_t rs_ea, int A, int o, float (&v)[2][4]) {
+  const int g = __lane_id() >> 4;
+  const int row = o * A * 4;
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[mb][r] = __int_as_float(bld1(rs_ea, row + 4 * min(16 * mb + 4 * g + r, A - 1)));
+}
+__device__ __forceinline__ void ea_mask(int A, const float (&v)[2][4], float (&x)[4][4]) {
+  const int g = __lane_id() >> 4;
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) x[mb][r] = (mb < 2 && 16 * mb + 4 * g + r < A) ? v[mb < 2 ? mb : 0][r] : 0.0f;
+}
+
 // embedding MLP then the Q0 layer on one tile: in x = edge_attr; out x = e_init, y = Q0 (+ b1)
 template <int PREC>
 __device__ __forceinline__ void embed_tile(const float* smz, const EmbedLayout& Lo, float (&x)[4][4], float (&y)[4][4]) {
@@ -1074,18 +1092,30 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp em
   // buffer descriptors + 32-bit offsets: no 64-bit lane pointers live across the tile loop
   const rsrc_t rs_ea = make_rsrc(ea, (int)E * A * 4), rs_orig = make_rsrc(s_orig, (int)E * 4);
   const rsrc_t rs_q0 = make_rsrc(q0, (int)E * 256), rs_r0 = make_rsrc(r0, (int)E * 256);
-  // original edge ids one tile ahead (the edge_attr gather of a tile then waits for one round trip, not two)
+  // original edge ids one tile ahead (the edge_attr gather of a tile then waits for one round trip, not two);
+  // FIXED: ids two tiles ahead and the edge_attr rows themselves one tile ahead
   int o_next = first < end ? bld1(rs_orig, 4 * min(first + c, end - 1)) : 0;
+  float ea_n[2][4];
+  if (FIXED && first < end) {
+    load_edge_attr32(rs_ea, A, o_next, ea_n);
+    o_next = bld1(rs_orig, 4 * min(first + 16 + c, end - 1));
+  }
   for (int base = first; base < end; base += 16) {
     int z = 0;
     asm volatile("" : "+s"(z));                  // keep the LDS fragment reads inside the loop
     const float* smz = sm + z;
     const int p = base + c;
     const bool valid = p < end;
-    const int o = o_next;
-    o_next = bld1(rs_orig, 4 * min(base + 16 + c, end - 1));
     float x[4][4], y[4][4];
-    load_edge_attr(rs_ea, A, o, x);
+    if constexpr (FIXED) {
+      ea_mask(A, ea_n, x);
+      load_edge_attr32(rs_ea, A, o_next, ea_n);   // the next tile's rows (clamped ids past the range: harmless)
+      o_next = bld1(rs_orig, 4 * min(base + 32 + c, end - 1));
+    } else {
+      const int o = o_next;
+      o_next = bld1(rs_orig, 4 * min(base + 16 + c, end - 1));
+      load_edge_attr(rs_ea, A, o, x);
+    }
     Frag<PREC> fx;
     if constexpr (FIXED) {
       embed_tile_fixed<PREC>(smz, Lo, x, y, fx);   // x = e_init, y = Q0 in the domain, fx = e_init's split

@@ -113,6 +113,32 @@ def test_vs_oracle(case, prec):
         assert max_err(a, b, rel) < TOL
 
 
+@pytest.mark.parametrize("variant", ["attn", "max", "mean"])
+@pytest.mark.parametrize("shape", [(600, 4), (100, 1)], ids=["N600-T4", "N100-T1"])
+def test_segments_across_wave_ranges(shape, variant):
+    """Long (target, type) segments: a fully graph over few node types, so that one segment covers several
+    16-edge tiles and runs across wave (and whole-range) boundaries. The pieces each wave leaves in its LDS
+    record are combined after the tile loop (mpn.hip edge_step_kernel); checked against the oracle."""
+    N, nt = shape
+    J = 17
+    g = torch.Generator().manual_seed(N + nt)
+    src, dst = torch.meshgrid(torch.arange(N), torch.arange(N), indexing="ij")
+    keep = src != dst
+    ei = torch.stack([src[keep], dst[keep]])                      # sorted by (src, dst)
+    types = torch.randint(0, nt, (N,), generator=g)
+    x = torch.rand(N, 128, generator=g) * 2 - 1
+    ea = torch.rand(ei.shape[1], J + 2, generator=g) * 2 - 1
+    cfg = pcfg.published_mpn_config(J, 3, variant)
+    for prec in ("f16x3", "fp32"):
+        # sharpened attention and trained-scale weights (|logit| ~ 10-70): a lost or doubled piece moves the
+        # node logits by far more than the bar (1e-4 + 2e-6 relative, as for the in-degree-sized sums)
+        model, sd = make_model(cfg, 2.5, prec, 4.0, 1.5)
+        pe, pn, pc, _ = run(model, x, ea, ei, types)
+        rpe, rpn, rpc, _ = restate.mpn_forward(sd, cfg, x, ea, ei, types)
+        for a, b in zip(pe + pn + pc, rpe + rpn + rpc):
+            assert max_err(a, b, REL_SUM) < TOL, prec
+
+
 @pytest.mark.parametrize("prec", PRECS)
 def test_permuted_edges_and_isolated_nodes(prec):
     """Edge order is free (the kernels sort by (source type, target)); nodes with no incoming
