@@ -66,9 +66,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=30.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=0,
                     help="batches in flight: step i runs on HIP stream i %% S (serving-style overlap of one "
-                         "batch's detection with the previous batch's MPN); 1 = strictly serial steps")
+                         "batch's detection with the previous batch's MPN); 1 = strictly serial steps; 0 (default) "
+                         "= the faster of 2 and 1, chosen by timing both schedules outside the timed region")
     return ap.parse_args()
 
 
@@ -453,13 +454,31 @@ def main():
 
     # batches in flight: each stream has its own library scratch (construct_graph and the MPN are
     # reentrant per (device, stream)); inputs are read-only and resident before the timed region
-    S = max(1, args.streams)
+    S = max(1, args.streams) if args.streams > 0 else 2
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
     torch.cuda.synchronize()
     for w in range(S):    # per-stream scratch and side streams allocated outside the timed region
         with torch.cuda.stream(streams[w]):
             run_step(wl, gc, model, hm, feats, tags, dev)
     torch.cuda.synchronize()
+    schedule_probe = None
+    if args.streams == 0:
+        # two batches in flight overlap one batch's detection with the other's MPN, but on some boxes the
+        # interleaving of the two queues serialises worse than one stream: time both schedules here (outside
+        # the timed region, every rank the same choice) and run the faster one
+        probe = {}
+        for S_try in (2, 1, 2, 1):
+            barrier(world)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(max(args.warmup, 4)):
+                with torch.cuda.stream(streams[i % S_try]):
+                    run_step(wl, gc, model, hm, feats, tags, dev)
+            torch.cuda.synchronize()
+            dt = max_over_ranks(time.perf_counter() - t0, world, dev)
+            probe[S_try] = min(probe.get(S_try, dt), dt)
+        S = 2 if probe[2] < probe[1] else 1
+        schedule_probe = {f"streams_{k}_ms_per_step": round(v / max(args.warmup, 4) * 1e3, 3) for k, v in probe.items()}
 
     # warmup (also finds the dominant kernel with the profiler on for every kernel)
     dominant = dominant_overall = None
@@ -583,7 +602,8 @@ def main():
                        "batches_in_flight": S,
                        "mpn_edge_gemms": PREC_NOTE[model.precision],
                        "detection_and_node_math": "fp32"},
-            "value_serial_steps": round(value_serial, 2) if value_serial else None,
+            "value_serial_steps": round(value_serial if value_serial else value, 2) if (value_serial or S == 1) else None,
+            "schedule_probe": schedule_probe,
             "mpn_edge_updates_per_sec": round(mpn_eups, 1),
             "mpn_ms_per_step": round(dt_mpn / args.steps * 1e3, 3),
             "pipeline_edge_updates_per_sec": round(E_all * wl["steps"] * args.steps / dt_max, 1),
