@@ -3131,16 +3131,18 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
       if (rc0) return rc0;
     }
   }
-  return PEMP_OK;
-  };
-  auto edge_embed = [&]() -> int {
-  // per-wave edge ranges of the passes (static across iterations): filled by the LDS edge embedding itself
-  const EdgeRangesArgs rga{ws.seg, ws.wg_start, ws.s_dst, T, N, edge_grid, ws.ranges};
-  if (E > 0 && steps >= 1 && !emb_lds) {
+  // the passes' per-wave range table (static across iterations), right behind the order on the prelude stream:
+  // its chains of dependent small loads stay off the edge embedding's workgroups
+  if (E > 0 && steps >= 1) {
     hipLaunchKernelGGL(edge_ranges_kernel, dim3((unsigned)std::min(64, (edge_grid * (EDGE_WAVES + 12) + 255) / 256)),
                        dim3(256), 0, pst, ws.seg, ws.wg_start, ws.s_dst, T, N, edge_grid, ws.ranges);
     PEMP_LAUNCH_CHECK();
   }
+  return PEMP_OK;
+  };
+  auto edge_embed = [&]() -> int {
+  // (the range table was filled behind the edge order, edge_prepare: the embedding does not)
+  const EdgeRangesArgs rga{ws.seg, ws.wg_start, ws.s_dst, T, N, edge_grid, nullptr};
   if (E > 0 && steps >= 1) {
     ProfScope prof("edge_embed", pst);
     if (emb_lds) {
