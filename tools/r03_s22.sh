@@ -1,0 +1,3 @@
+set -o pipefail
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_dist.py -x -v --timeout 300 --timeout-method thread > gpurun_out/r03s22_dist.log 2>&1
