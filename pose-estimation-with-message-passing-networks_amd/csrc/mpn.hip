@@ -617,11 +617,24 @@ __device__ __forceinline__ float f16_item_scale(float m, float s) {
   return ldexpf(1.0f, 14 - e);                     // m 2^(14-e) < 2^14, and >= 2^13
 }
 
+// largest value of a fragment known to hold no negative value (after relu1): non-negative floats order
+// as their bit patterns, so one v_max3_i32 chain (no fabs, no canonicalising moves); a NaN with a clear
+// sign bit sorts above +inf and still reaches the range check as a NaN
+__device__ __forceinline__ float frag_max_nonneg(const float (&x)[4][4]) {
+  int m = 0;
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+    m = max(m, max(max(__float_as_int(x[b][0]), __float_as_int(x[b][1])), max(__float_as_int(x[b][2]), __float_as_int(x[b][3]))));
+  return __int_as_float(m);
+}
+
 // split of the fragment s·x (s a power of two); returns the wave's range flag. When it is set, `sc` is each
 // item's range factor (the parts hold s·x·sc and a GEMM over them rescales the item's column by 1/sc); else 1.
+// NONNEG: x holds no negative value (relu1 output)
+template <bool NONNEG = false>
 __device__ __forceinline__ bool split_f16(const float (&x)[4][4], float s, f16x8_t (&hi)[2], f16x8_t (&lo)[2],
                                           float& sc) {
-  const float m = frag_absmax(x);
+  const float m = NONNEG ? frag_max_nonneg(x) : frag_absmax(x);
   const bool big = __any(!(m * s < F16_BIG));
   sc = big ? f16_item_scale(m, s) : 1.0f;
   const float ss = s * sc;
@@ -682,10 +695,11 @@ struct Frag {
 };
 
 // x in the precision's domain (dom<PREC>() x_true for f16x3): split for the GEMMs that read it
-template <int PREC>
+// (NONNEG: x is a relu1 output)
+template <int PREC, bool NONNEG = false>
 __device__ __forceinline__ void prep(const float (&x)[4][4], Frag<PREC>& f) {
   if constexpr (PREC == 1) split_bf16(x, f.bh, f.bl);
-  else if constexpr (PREC == 2) f.big = split_f16(x, dom_inv<PREC>(), f.hh, f.hl, f.sc);
+  else if constexpr (PREC == 2) f.big = split_f16<NONNEG>(x, dom_inv<PREC>(), f.hh, f.hl, f.sc);
 }
 
 // x in the true domain (f16x3: split with scale 1)
@@ -1662,7 +1676,7 @@ __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_
     }
     {
       Frag<PREC> fh;
-      prep<PREC>(h, fh);
+      prep<PREC, true>(h, fh);                    // (h, e', the head's h1 and m are relu1 outputs)
       gemm_f<PREC, 4>(W2, h, fh, ep);
     }
     relu_frag<4>(ep);
@@ -1690,7 +1704,7 @@ __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_
                                               4 * a.s_orig[p], 0, 0);
     }
     Frag<PREC> fe;                                // e' split once for the r_next, head and message GEMMs
-    prep<PREC>(ep, fe);
+    prep<PREC, true>(ep, fe);
     if (MID) {
       // this tile's Q0 rows have landed (only the two index loads were issued after their DMA): read them,
       // then the r rows of tile k+1 into the same buffer
@@ -1728,7 +1742,7 @@ __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_
       }
       {
         Frag<PREC> f1;
-        prep<PREC>(h1, f1);
+        prep<PREC, true>(h1, f1);
         gemm_f<PREC, 2>(hwz + D * LDW, h1, f1, h2);
       }
       relu_frag<2>(h2);
@@ -1755,7 +1769,7 @@ __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_
 #pragma unroll
         for (int r = 0; r < 4; ++r) u[ob][r] = 0.0f;
       Frag<PREC> fm;
-      prep<PREC>(m, fm);
+      prep<PREC, true>(m, fm);
       gemm_f<PREC, 4>(UW, m, fm, u);
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob)
