@@ -2232,6 +2232,18 @@ __device__ inline void copy_to_lds(float* __restrict__ lds, const float* __restr
   }
 }
 
+// the same copy by LDS-DMA (n multiple of 4, both ends 16-byte aligned): 1 KB per wave instruction,
+// the block's waves interleaved, nothing held in registers and nothing waited for here, so the loads
+// that follow overlap it; lds_drain() before the barrier that publishes it
+__device__ inline void dma_to_lds(float* __restrict__ lds, const float* __restrict__ src, int n) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int pieces = n >> 8, tail = n - (pieces << 8);
+  for (int k = wave; k < pieces; k += nw) dma16(src + 256 * k + 4 * lane, lds + 256 * k);
+  if (tail && wave == nw - 1 && 4 * lane < tail)
+    *reinterpret_cast<float4*>(&lds[256 * pieces + 4 * lane]) = ld4(src + 256 * pieces + 4 * lane);
+}
+__device__ __forceinline__ void lds_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // whole staged MLP on one wave's fragments (widths <= 64); result in `a`
 __device__ inline void mlp_lds_frag(const float* lds, const pemp_mlp& m, float (&a)[4][4]) {
   float b[4][4];
@@ -2274,6 +2286,7 @@ struct NodeRowsArgs {
   float *node_out, *node_out2, *class_out, *class_out2;
   const float* img;      // LDS image [emb | node head | class head] built by zero_words_kernel
   int head_off, head_floats;   // heads block: offset (= embedding image size, or 0) and size
+  int emb_whole;         // ROWS_EMBED: the whole embedding image fits in LDS (one DMA up front)
 };
 
 static int max_layer_floats(const pemp_mlp& m) {
@@ -2285,9 +2298,15 @@ static int max_layer_floats(const pemp_mlp& m) {
   return mx;
 }
 
+constexpr int NODE_ROWS_LDS_MAX = 160 * 1024;
+
+static bool node_emb_whole(const pemp_mlp& emb) {
+  return (size_t)(3 * 16 * RS + mlp_lds_floats(emb)) * sizeof(float) <= (size_t)NODE_ROWS_LDS_MAX;
+}
+
 static size_t node_rows_lds_bytes(const NodeRowsArgs& a) {
   int region = 0;
-  if (a.mode == ROWS_EMBED) region = max_layer_floats(a.emb);
+  if (a.mode == ROWS_EMBED) region = a.emb_whole ? mlp_lds_floats(a.emb) : max_layer_floats(a.emb);
   if (a.node_out) region = std::max(region, a.head_floats);
   return (size_t)(3 * 16 * RS + region) * sizeof(float);
 }
@@ -2304,6 +2323,10 @@ __global__ __launch_bounds__(256) void node_rows_kernel(NodeRowsArgs a) {
   const int r = threadIdx.x >> 4, q = threadIdx.x & 15;   // row r of the tile, features 4 q .. 4 q + 3
   const int64_t n = n0 + r, nc = n < N ? n : N - 1;
   if (a.mode == ROWS_EMBED) {
+    // whole image: every layer's weights in one DMA, in flight with the input rows (one latency
+    // round instead of one per layer)
+    const bool whole = a.emb_whole != 0;
+    if (whole) dma_to_lds(wreg, a.img, mlp_lds_floats(a.emb));
     const int K0 = a.emb.layer[0].in_dim, KP = (K0 + 15) & ~15;
     for (int base = threadIdx.x; base < 16 * KP; base += 8 * 256) {   // 16 x K0 inputs, 8 loads in flight
       float v[8];
@@ -2323,11 +2346,15 @@ __global__ __launch_bounds__(256) void node_rows_kernel(NodeRowsArgs a) {
       const pemp_layer& L = a.emb.layer[l];
       const int KB = (L.in_dim + 15) >> 4, OB = (L.out_dim + 15) >> 4, ld = lds_stride(16 * KB);
       const int lf = 16 * OB * ld + 16 * OB;
-      if (l > 0) __syncthreads();                // the previous layer is done with wreg
-      copy_to_lds(wreg, a.img + off, lf);
+      if (whole) {
+        if (l == 0) lds_drain();
+      } else {
+        if (l > 0) __syncthreads();              // the previous layer is done with wreg
+        copy_to_lds(wreg, a.img + off, lf);
+      }
+      __syncthreads();                           // layer l - 1's activations (and the weights) visible
+      const float* Wl = whole ? wreg + off : wreg;
       off += lf;
-      __syncthreads();
-      const float* Wl = wreg;
       const float* bl = Wl + 16 * OB * ld;
       const float* src = cur ? act1 : act0;
       float* dst = cur ? act0 : act1;
@@ -2351,7 +2378,7 @@ __global__ __launch_bounds__(256) void node_rows_kernel(NodeRowsArgs a) {
       cur ^= 1;
     }
     __syncthreads();
-    if (heads) copy_to_lds(wreg, a.img + a.head_off, a.head_floats);
+    if (heads) dma_to_lds(wreg, a.img + a.head_off, a.head_floats);
     const float* res = cur ? act1 : act0;
     const float4 v = ld4(&res[r * RS + 4 * q]);
     *reinterpret_cast<float4*>(&xs[r * RS + 64 + 4 * q]) = v;
@@ -2360,7 +2387,7 @@ __global__ __launch_bounds__(256) void node_rows_kernel(NodeRowsArgs a) {
       *reinterpret_cast<float4*>(a.X + n * 128 + 64 + 4 * q) = v;
     }
   } else {
-    if (heads) copy_to_lds(wreg, a.img + a.head_off, a.head_floats);
+    if (heads) dma_to_lds(wreg, a.img + a.head_off, a.head_floats);   // in flight with the row loads
     float4 v;
     if (a.mode == ROWS_SUM) {
       // all T rows and segment bounds in flight together; fixed summation order t = 0 .. T-1
@@ -2390,6 +2417,7 @@ __global__ __launch_bounds__(256) void node_rows_kernel(NodeRowsArgs a) {
     if (a.mode != ROWS_NONE && n < N) *reinterpret_cast<float4*>(a.X + n * 128 + 64 + 4 * q) = v;
   }
   if (!heads) return;
+  lds_drain();
   __syncthreads();
   if (wave < 2) {   // wave 0: node head, wave 1: class head
     float in[4][4];
@@ -3225,6 +3253,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
     na.img = node_img;
     na.head_off = fused_embed_ ? mlp_lds_floats(w->node_emb) : 0;
     na.head_floats = mlp_lds_floats(w->node_head) + mlp_lds_floats(w->class_head);
+    na.emb_whole = mode == ROWS_EMBED && node_emb_whole(w->node_emb);
     if (na.mode != ROWS_NONE || na.node_out) {
       ProfScope prof(mode == ROWS_EMBED ? "node_embed" : "node_update", st);
       hipLaunchKernelGGL(node_rows_kernel, dim3(node_grid), dim3(256), node_rows_lds_bytes(na), st, na);
