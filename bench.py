@@ -42,7 +42,13 @@ WORKLOADS = {
     # the published model on C3 (experiments/hybrid_class_agnostic_end2end/model_58_4_4.yaml:97,155):
     # GRAPH_TYPE knn, STEPS 10
     "c3knn10": dict(B=8, J=17, H=640, W=640, persons=9, steps=10, graph="knn", variant="attn"),
+    # configs[4] (C5) as stated: multi-scale x3 ({2.0, 1.0, 0.5}, multi_scales_testing.py:144-195) with flip test;
+    # the timed step starts from the network outputs of every scale (heatmaps + tags, and the gathered feature
+    # maps) and projects them on demand (ProjectedHeatmaps / ProjectedMaps) inside construct_graph
+    "c5ms": dict(B=1, J=14, H=640, W=640, persons=36, steps=3, graph="fully", variant="attn", scales=(2.0, 1.0, 0.5)),
 }
+FLIP_INDEX = {17: [0, 2, 1, 4, 3, 6, 5, 8, 7, 10, 9, 12, 11, 14, 13, 16, 15],   # COCO FLIP_CONFIG
+              14: [1, 0, 3, 2, 5, 4, 7, 6, 9, 8, 11, 10, 12, 13]}               # CrowdPose
 FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: dense f32 MFMA (= f32 vector) peak
 HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 BF16_MFMA_PEAK_TFLOPS = 2500.0     # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
@@ -74,7 +80,37 @@ def parse():
 
 
 def setup_dist(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != n_gpus:   # checked before anything touches the GPU
+        raise SystemExit(f"bench.py: --gpus {n_gpus} but WORLD_SIZE={world}: launch one rank per GPU "
+                         f"(torchrun --nproc-per-node {n_gpus}) or let bench.py spawn them (WORLD_SIZE unset)")
     return pdist.init_from_env("nccl")
+
+
+def spawn_ranks(n_gpus):
+    """`python bench.py --gpus N` without a launcher: start N rank processes of this same command (one per GPU,
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment) before anything here touches the GPU, wait
+    for all of them and return the worst exit code. Rank 0 prints the JSON line; the timing contract (barrier,
+    synchronize, max over ranks) is inside the ranks."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    try:
+        for r in range(n_gpus):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n_gpus),
+                       LOCAL_WORLD_SIZE=str(n_gpus), MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                       MASTER_PORT=str(port))
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+        codes = [p.wait() for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
 
 
 barrier = pdist.barrier
@@ -83,12 +119,40 @@ sum_over_ranks = pdist.sum_over_ranks
 
 
 def make_inputs(wl, rank, dev):
+    """(scoremaps, features, tagmaps) as construct_graph takes them. Single-scale workloads: image-size tensors.
+    Multi-scale ("scales"): the network outputs of every scale and of the flipped pass ([B, 2J, 320 s, 320 s]:
+    heatmaps whose planted peaks sit at the same image positions at every scale, then per-joint tags) and the
+    gathered feature maps ([B, 128, 320 s, 320 s]), wrapped as ProjectedHeatmaps / ProjectedMaps."""
     B, J, H, W = wl["B"], wl["J"], wl["H"], wl["W"]
-    hm = torch.from_numpy(syn.make_heatmaps(1000 + rank, B, J, H, W, wl["persons"])).to(dev)
     g = torch.Generator(device=dev).manual_seed(77 + rank)
-    feats = torch.rand(B, 128, H, W, generator=g, device=dev) * 2 - 1
-    tags = torch.rand(B, J, H, W, 1, generator=g, device=dev)
-    return hm, feats, tags
+    if not wl.get("scales"):
+        hm = torch.from_numpy(syn.make_heatmaps(1000 + rank, B, J, H, W, wl["persons"])).to(dev)
+        feats = torch.rand(B, 128, H, W, generator=g, device=dev) * 2 - 1
+        tags = torch.rand(B, J, H, W, 1, generator=g, device=dev)
+        return hm, feats, tags
+    scales = wl["scales"]
+    top = max(scales)
+    h0, w0 = int(H * top / 2), int(W * top / 2)
+    base = torch.from_numpy(syn.make_heatmaps(1000 + rank, B, J, h0, w0, wl["persons"])).to(dev)
+    fi = FLIP_INDEX[J]
+    outs, flips, fmaps = [], [], []
+    for s in scales:
+        k = int(round(top / s))
+        heat = base if k == 1 else torch.nn.functional.avg_pool2d(base, k)
+        h, w = heat.shape[-2:]
+        outs.append(torch.cat([heat, torch.rand(B, J, h, w, generator=g, device=dev)], 1))
+        flips.append(torch.cat([torch.flip(heat, [3])[:, fi], torch.rand(B, J, h, w, generator=g, device=dev)], 1))
+        fmaps.append(torch.rand(B, 128, h, w, generator=g, device=dev) * 2 - 1)
+    ph = pemp_amd.ProjectedHeatmaps(outs, (H, W), J, flips, fi, tag_scale=list(scales).index(1.0))
+    return ph, pemp_amd.ProjectedMaps(fmaps, (H, W)), ph
+
+
+def dense_maps(hm, tags):
+    """Image-size (scoremaps, tagmaps) for the legs that read whole maps (refine): the workload's own tensors,
+    or, multi-scale, the library's projection of them (pemp_project_maps)."""
+    if isinstance(hm, torch.Tensor):
+        return hm, tags
+    return hm.project()
 
 
 def make_model(wl, dev):
@@ -118,7 +182,8 @@ def edge_pass_cost(head, upd):
     A middle pass (no head) computes e' = ReLU(W2 h + b2) from h = ReLU(r + A[dst] + B[src]), the
     message W_t e', the update block U_t m (upd), the next r = Q0 + W1_e e', and the attention dot;
     it reads r and Q0 (2 x 256 B) and writes the next r (256 B) plus 2 int32 indices. The last pass
-    (head) drops the next r and Q0 and runs the fused edge head, writing a 4 B logit."""
+    (head) drops the next r and Q0 and runs the fused edge head, writing a 4 B logit. Per launch, both also
+    write one 256 B aggregate row per non-empty (target, source type) segment (seg_rows_bytes)."""
     gemms = 2 + (1 if upd else 0) + (0 if head else 1)
     flop = gemms * GEMM64 + 2 * 64 + (EDGE_HEAD_FLOP if head else 0)
     byts = (256 + 8 + 4) if head else (2 * 256 + 256 + 8)
@@ -139,7 +204,13 @@ def pmc_traffic(kernel_prefix, workload, E):
     return None
 
 
-def roofline_for(label, stats, E, wl, precision, upd, workload):
+def seg_rows_bytes(ei, types):
+    """Aggregate-row bytes one edge pass writes: 64 fp32 per non-empty (target, source type) segment."""
+    T = int(types.max().item()) + 1 if types.numel() else 1
+    return 256 * int(torch.unique(ei[1] * T + types[ei[0]]).numel())
+
+
+def roofline_for(label, stats, E, wl, precision, upd, workload, agg_bytes=0):
     """Roofline of the dominant kernel from its measured average launch time.
 
     edge_step*: executed FLOP and ALGORITHMIC HBM bytes per edge from edge_pass_cost (node-table
@@ -156,12 +227,13 @@ def roofline_for(label, stats, E, wl, precision, upd, workload):
     if label.startswith("edge_step"):
         head = label == "edge_step_head"
         f1, b1 = edge_pass_cost(head, upd)
-        flop, byts = E * f1, E * b1
+        flop, byts = E * f1, E * b1 + agg_bytes
         gbs = byts / avg_s / 1e9
         traffic = pmc_traffic("pemp::edge_step_kernel<0," + ("1" if head else "0"), workload, E)
         common = {"kernel": label, "avg_launch_us": round(avg_s * 1e6, 2), "launches": n, "traffic": traffic,
                   "traffic_source": f"profiles/pmc_latest.json ({workload}, E={E})" if traffic else None,
-                  "algorithmic": f"{f1} FLOP and {b1} B HBM x E={E} edges per launch",
+                  "algorithmic": f"{f1} FLOP and {b1} B HBM x E={E} edges + {agg_bytes} B of aggregate rows "
+                                 f"per launch",
                   "tflops_executed": round(flop / avg_s / 1e12, 2), "hbm_GBs_algorithmic": round(gbs, 1),
                   "ref_equiv_tflops": round(E * REF_EDGE_FLOP / avg_s / 1e12, 2), "precision": precision}
         if precision == "fp32":
@@ -189,50 +261,82 @@ def roofline_for(label, stats, E, wl, precision, upd, workload):
 
 
 def cpu_baseline(wl, gc, model, hm, feats, tags, budget_s):
-    """The oracle restatement (torch CPU fp32, oracle/restate.py) timed per stage on image 0 of the same
-    workload: 3 warm-up runs, then the median of >= 10 timed runs of each stage (fewer only when one run
-    alone exceeds the budget share), with every host thread of the box's CPU share (16 per GPU)."""
+    """The oracle restatement (torch CPU fp32, oracle/restate.py) timed per stage on image 0 of the same workload,
+    with torch.set_num_threads(os.cpu_count()) as SURVEY 8(d) / BASELINE.md prescribe (`value`), and again with
+    16 threads (the GPU box's CPU share per GPU; `threads_16`). The stages run interleaved, one of each per round
+    (3 warm-up rounds), so host noise hits them alike; each stage's figure is the least of the medians of three
+    blocks of rounds (min-of-medians), so that a noisy block on a shared host does not decide it."""
     from oracle import restate
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
     mcfg = pcfg.published_mpn_config(wl["J"], wl["steps"], wl["variant"])
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
-    h, f, tg = hm[0:1].cpu(), feats[0:1].cpu(), tags[0:1].cpu()
     thr = gc.DETECT_THRESHOLD if gc.DETECT_THRESHOLD <= 1.5 else None
     holder = {}
+    if isinstance(hm, torch.Tensor):
+        holder["maps"] = hm[0:1].cpu(), feats[0:1].cpu(), tags[0:1].cpu()
+        front_stage = ()
+    else:
+        # multi-scale: the reference's own torch ops project image 0's per-scale outputs to the image size on
+        # the CPU (PoseEstimation.py:329-452, multi_scales_testing.py:144-195) before construct_graph reads them
+        ph_cpu = pemp_amd.ProjectedHeatmaps([o[0:1].cpu() for o in hm.outputs], hm.size, wl["J"],
+                                            [o[0:1].cpu() for o in hm.flip_outputs], hm.flip_index.tolist(),
+                                            tag_scale=hm.tag_scale)
+        pm_cpu = pemp_amd.ProjectedMaps([m[0:1].cpu() for m in feats.maps], feats.size)
+
+        def frontend():
+            s_, t_ = ph_cpu.materialize()
+            holder["maps"] = s_, pm_cpu.materialize(), t_
+
+        frontend()
+        front_stage = (("frontend", frontend),)
 
     def detect():
+        h = holder["maps"][0]
         holder["det"] = restate.joint_det_from_scoremap(h[0], wl["J"], threshold=thr, pool_kernel=gc.POOL_KERNEL_SIZE,
                                                         hybrid_k=gc.HYBRID_K)
 
     def graph():
-        holder["g"] = restate.construct_graph(h, f, tg, None, gc, wl["J"])
+        holder["g"] = restate.construct_graph(*holder["maps"][:2], holder["maps"][2], None, gc, wl["J"])
 
     def mpn():
         g = holder["g"]
         restate.mpn_forward(sd, mcfg, g[0], g[1], g[2], g[7][:, 2])
 
-    stages, runs_used, spent = {}, {}, 0.0
-    for name, fn in (("detect", detect), ("construct_graph", graph), ("mpn_forward", mpn)):
-        times = []
-        for r in range(3 + 10):
-            t0 = time.perf_counter()
-            fn()
-            dt = time.perf_counter() - t0
-            spent += dt
-            if r >= 3:
-                times.append(dt)
-            if r >= 3 and len(times) >= 3 and spent > budget_s:
+    # detect runs right after construct_graph (which contains it), on the same warm heatmap, as inside it
+    stage_fns = front_stage + (("construct_graph", graph), ("detect", detect), ("mpn_forward", mpn))
+
+    def timed(threads, budget):
+        torch.set_num_threads(threads)
+        times = {name: [] for name, _ in stage_fns}
+        spent, rounds = 0.0, 0
+        for r in range(3 + 15):
+            for name, fn in stage_fns:
+                t0 = time.perf_counter()
+                fn()
+                dt = time.perf_counter() - t0
+                spent += dt
+                if r >= 3:
+                    times[name].append(dt)
+            rounds += r >= 3
+            if rounds >= 6 and spent > budget:
                 break
-        stages[name] = round(float(np.median(times)) * 1e3, 3)
-        runs_used[name] = len(times)
-    per_image_ms = stages["construct_graph"] + stages["mpn_forward"]
-    return {"value": round(1e3 / per_image_ms, 3), "unit": "images/s", "cores": threads, "kind": "port",
-            "stage_median_ms": stages, "runs": runs_used,
-            "sample": f"image 0 of the {wl['B']}-image workload; per stage 3 warm-ups + median of "
-                      f"{min(runs_used.values())}-{max(runs_used.values())} runs (oracle/restate.py, torch CPU fp32); "
-                      f"value = 1 / (construct_graph + mpn_forward)",
-            "host_cpus": os.cpu_count(), "cpu_model": _cpu_model()}
+        stages = {}
+        for name, ts in times.items():
+            k = max(1, len(ts) // 3)
+            blocks = [ts[i:i + k] for i in range(0, 3 * k, k)]
+            stages[name] = round(min(float(np.median(b)) for b in blocks) * 1e3, 3)
+        per_image_ms = stages.get("frontend", 0.0) + stages["construct_graph"] + stages["mpn_forward"]
+        return {"value": round(1e3 / per_image_ms, 3), "cores": threads, "stage_ms": stages, "rounds": rounds}
+
+    all_cores = os.cpu_count() or 1
+    main_run = timed(all_cores, 0.65 * budget_s)
+    share = timed(min(16, all_cores), 0.35 * budget_s)
+    return {"value": main_run["value"], "unit": "images/s", "cores": all_cores, "kind": "port",
+            "stage_ms": main_run["stage_ms"], "rounds": main_run["rounds"], "threads_16": share,
+            "sample": f"image 0 of the {wl['B']}-image workload; detect / construct_graph / mpn_forward interleaved, "
+                      f"3 warm-up rounds, then {main_run['rounds']} rounds; per stage the least median of 3 blocks "
+                      f"(oracle/restate.py, torch CPU fp32, torch.set_num_threads(os.cpu_count())); "
+                      f"value = 1 / ({'frontend + ' if front_stage else ''}construct_graph + mpn_forward)",
+            "host_cpus": all_cores, "cpu_model": _cpu_model()}
 
 
 def _cpu_model():
@@ -445,6 +549,8 @@ def pose_refine(wl, persons, cpu_ref):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     rank, world, dev = setup_dist(args.gpus)
     wl = WORKLOADS[args.workload]
     gc = pcfg.inference_gc_config(wl["graph"], 5, False)
@@ -561,11 +667,13 @@ def main():
     dt_mpn = max_over_ranks(time.perf_counter() - t1, world, dev)
     mpn_eups = E_all * wl["steps"] * args.steps / dt_mpn
 
-    front = frontend_projection(wl, gc, model, hm, tags, dev, out) if not args.no_roofline else None
-    front_hm = frontend_heatmaps(wl, gc, feats, dev) if not args.no_roofline else None
+    # (single-scale workloads: the front-end legs beside the step; a multi-scale workload runs them inside it)
+    single = not wl.get("scales")
+    front = frontend_projection(wl, gc, model, hm, tags, dev, out) if single and not args.no_roofline else None
+    front_hm = frontend_heatmaps(wl, gc, feats, dev) if single and not args.no_roofline else None
 
     global _BENCH_MAPS
-    _BENCH_MAPS = (hm, tags)
+    _BENCH_MAPS = dense_maps(hm, tags)
     grouping = pose_grouping(wl, out, pe, pn, pc, rank == 0 and world == 1 and not args.no_cpu_baseline) \
         if not args.no_roofline else None
     if grouping is not None and world > 1:
@@ -581,7 +689,8 @@ def main():
             grouping["pose_all_gather_error"] = repr(exc)[:200]
 
     upd = wl["variant"] in ("attn", "mean")      # update block pre-applied in the edge pass (mpn.hip UPD)
-    roof = roofline_for(dominant, stats_timed, E, wl, model.precision, upd, args.workload) if dominant else None
+    roof = roofline_for(dominant, stats_timed, E, wl, model.precision, upd, args.workload,
+                        seg_rows_bytes(out[2], out[7][:, 2])) if dominant else None
     if roof is not None and dominant_overall != dominant:
         roof["largest_total_time_kernel"] = dominant_overall
     cpu = None
@@ -613,6 +722,8 @@ def main():
             "frontend_projection": front,
             "frontend_heatmaps": front_hm,
             "pose_grouping": grouping,
+            # the one collective of the sharded path (RCCL all_gather of every rank's grouped poses)
+            "pose_all_gather_ms": grouping.get("pose_all_gather_ms") if grouping else None,
         }
         if cpu:
             rec["speedup_vs_cpu"] = round(value / cpu["value"], 1)

@@ -428,7 +428,9 @@ int pemp_mpn_forward_fully(const pemp_mpn_desc* desc, const pemp_mpn_weights* we
  * return it, ConstructGraph.py:363-422): the type-major edge order is read off the rows of the list (segment
  * (t, d) = the type-t entries of row d) instead of the sorting prepare's scatter + segment sort; results are
  * identical. N >= 2^24 falls back to the sorting prepare. A list that breaks the contract is reported by
- * pemp_mpn_status (its logits are then undefined, every index stays in range). */
+ * pemp_mpn_status (its logits are then undefined, every index stays in range). The caller's knowledge that a
+ * list meets the contract is a hint the library does not verify on this call (the Python mirror tags
+ * construct_graph's output and drops the tag on a version-counter change; call pemp_mpn_status to check). */
 int pemp_mpn_forward_sym(const pemp_mpn_desc* desc, const pemp_mpn_weights* weights, const float* x,
                          const float* edge_attr, const int64_t* edge_index, const int64_t* node_types,
                          int64_t N, int64_t E, float* edge_logits, float* node_logits, float* class_logits,

@@ -22,6 +22,7 @@ bool debug_sync() {
   return on;
 }
 
+#ifdef PEMP_HOST_TRACE   // diagnostics build only (-DPEMP_HOST_TRACE, tools/host_trace.py)
 bool g_host_trace = [] {
   const char* v = getenv("PEMP_HOST_TRACE");
   return v && v[0] && v[0] != '0';
@@ -36,6 +37,7 @@ void host_mark(int line) {
   std::lock_guard<std::mutex> lk(g_ht_mu);
   if (g_ht.size() < (1u << 20)) g_ht.emplace_back(line, t);
 }
+#endif
 
 void set_error(const char* fmt, ...) {
   va_list ap;
@@ -162,8 +164,10 @@ extern "C" int pemp_device_check(void) {
   return PEMP_OK;
 }
 
-// diagnostics (PEMP_HOST_TRACE=1): prints the host time between consecutive launch checks (source lines) since
-// the last dump to stderr, then clears; returns the number of marks
+#ifdef PEMP_HOST_TRACE
+// diagnostics build (-DPEMP_HOST_TRACE, run with PEMP_HOST_TRACE=1; not part of the C-ABI of include/pemp.h):
+// prints the host time between consecutive launch checks (source lines) since the last dump to stderr, then
+// clears; returns the number of marks
 extern "C" int pemp_host_trace_dump(void) {
   std::lock_guard<std::mutex> lk(pemp::g_ht_mu);
   const int n = (int)pemp::g_ht.size();
@@ -171,3 +175,4 @@ extern "C" int pemp_host_trace_dump(void) {
   pemp::g_ht.clear();
   return n;
 }
+#endif

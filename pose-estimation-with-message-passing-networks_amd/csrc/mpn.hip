@@ -1047,16 +1047,6 @@ __device__ __forceinline__ void stage_tile64(float* dst, const float* w32, int64
   }
 }
 
-struct EdgeRangesArgs {   // the edge passes' wave range table, filled by the edge embedding (edge_ranges_fill)
-  const int *seg, *wg_start, *s_dst;
-  int T;
-  int64_t N;
-  int G;
-  int4* ranges;
-};
-__device__ inline void edge_ranges_fill(const int* seg, const int* wg_start, const int* s_dst, int T, int64_t N, int G,
-                                        int4* __restrict__ ranges);
-
 // Edge embedding (sorted order), the fallback of the fused first pass: e_init = MLP(edge_attr[orig]),
 // Q0 = W1_e_init·e_init + b1 and R0 = Q0 + W1_e_cur·e_init (the first pass's layer-1 input).
 // One 16-wave workgroup per CU, weights staged once in LDS; a wave walks an equal share of the
@@ -1070,12 +1060,9 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp em
                                                                      const float* __restrict__ q0_b,
                                                                      const float* __restrict__ e1_w,
                                                                      const uint16_t* __restrict__ e1_bf,
-                                                                     float* __restrict__ r0, float* __restrict__ q0,
-                                                                     EdgeRangesArgs rg) {
+                                                                     float* __restrict__ r0, float* __restrict__ q0) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
-  // the edge passes' per-wave range table (needs only the prepared order; one entry per thread, grid-stride)
-  if (rg.ranges) edge_ranges_fill(rg.seg, rg.wg_start, rg.s_dst, rg.T, rg.N, rg.G, rg.ranges);
   stage_tile64<PREC>(sm + Lo.total, e1_w, D, e1_bf);   // W1_e_cur after the embedding image
   for (int l = 0; l <= Lo.n; ++l) {
     const float* bsrc = l < Lo.n ? emb.layer[l].b : q0_b;
@@ -2624,8 +2611,10 @@ static EdgeImgArgs edge_image_args(const pemp_mpn_desc& d, const pemp_mpn_weight
 
 // whether the edge passes pre-apply the update block (UPD) and carry the published head (HEAD 1)
 static bool edge_upd_fused(const pemp_mpn_desc& d, const pemp_mpn_weights& w) {
-  static const bool off = getenv("PEMP_NO_UPD_FUSE") != nullptr;   // (A/B switch: update MLP on the nodes)
-  return !off && (d.aggr == PEMP_AGGR_ATTN || d.aggr == PEMP_AGGR_MEAN) && w.upd_w && (d.precision == PEMP_PREC_FP32 || w.upd_bf);
+#ifdef PEMP_NO_UPD_FUSE   // (experiment builds only, DESIGN §4: the update MLP on the nodes)
+  return false;
+#endif
+  return (d.aggr == PEMP_AGGR_ATTN || d.aggr == PEMP_AGGR_MEAN) && w.upd_w && (d.precision == PEMP_PREC_FP32 || w.upd_bf);
 }
 static bool edge_pub_head(const pemp_mpn_desc& d, const pemp_mpn_weights& w) {
   return published_head(w.edge_head) && (d.precision == PEMP_PREC_FP32 || w.head_bf);
@@ -3183,8 +3172,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   return PEMP_OK;
   };
   auto edge_embed = [&]() -> int {
-  // (the range table was filled behind the edge order, edge_prepare: the embedding does not)
-  const EdgeRangesArgs rga{ws.seg, ws.wg_start, ws.s_dst, T, N, edge_grid, nullptr};
+  // (the range table is filled behind the edge order on the side stream, edge_prepare)
   if (E > 0 && steps >= 1) {
     ProfScope prof("edge_embed", pst);
     if (emb_lds) {
@@ -3194,7 +3182,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
 #define PEMP_EMBED_LAUNCH(P, FX)                                                                                   \
   hipLaunchKernelGGL((edge_embed_kernel<P, FX>), dim3(grid), dim3(64 * EDGE_WAVES), lds, pst, w->edge_emb, emb_lo,  \
                      w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, w->e1_bf, \
-                     ws.EA, ws.Q0, rga)
+                     ws.EA, ws.Q0)
       if (emb_prec == PEMP_PREC_F16X3) {
         if (fixed) PEMP_EMBED_LAUNCH(2, true);
         else PEMP_EMBED_LAUNCH(2, false);
@@ -3204,7 +3192,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
       } else
         hipLaunchKernelGGL((edge_embed_kernel<0, false>), dim3(grid), dim3(64 * EDGE_WAVES), lds, pst, w->edge_emb, emb_lo,
                            w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, w->e1_bf,
-                           ws.EA, ws.Q0, rga);
+                           ws.EA, ws.Q0);
 #undef PEMP_EMBED_LAUNCH
     } else {
       hipLaunchKernelGGL(edge_embed_wide_kernel, dim3((unsigned)((E + 63) / 64)), dim3(256), 0, pst, w->edge_emb,
@@ -3315,8 +3303,8 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
     side_lock.unlock();
     ss = nullptr;
   };
-  // side stream: the edge order; meanwhile the node embedding + first node table here (short kernels with
-  // 16-row grids); then, joined, the range table and the edge embedding (every CU, all of its LDS)
+  // side stream: the edge order and the edge passes' range table behind it; meanwhile the node embedding + first
+  // node table here (short kernels with 16-row grids); then, joined, the edge embedding (every CU, all of its LDS)
   if (ss && (rc = edge_prepare())) { join_side(); return rc; }
   if (!fused_embed) {
     if ((rc = rows_mlp("node_embed", w->node_emb, x, desc->node_in_dim, N, ws.X, 128, ws.X + 64, 128, st))) {

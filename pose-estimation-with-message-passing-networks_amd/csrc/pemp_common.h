@@ -44,14 +44,24 @@ bool prof_active();
 // (launch sites that are idempotent may repeat to amortise the event overhead), else 1
 int prof_repeat(const char* label);
 
-// host-side launch timing (diagnostics, PEMP_HOST_TRACE=1): a timestamp per launch check, printed by
-// pemp_host_trace_dump()
+// host-side launch timing (diagnostics builds with -DPEMP_HOST_TRACE, run with PEMP_HOST_TRACE=1): a timestamp
+// per launch check, printed by pemp_host_trace_dump(); compiled out of the product library
+#ifdef PEMP_HOST_TRACE
 void host_mark(int line);
 extern bool g_host_trace;
+#define PEMP_HOST_MARK() \
+  do {                   \
+    if (::pemp::g_host_trace) ::pemp::host_mark(__LINE__); \
+  } while (0)
+#else
+#define PEMP_HOST_MARK() \
+  do {                   \
+  } while (0)
+#endif
 
 #define PEMP_LAUNCH_CHECK()                                                        \
   do {                                                                             \
-    if (::pemp::g_host_trace) ::pemp::host_mark(__LINE__);                         \
+    PEMP_HOST_MARK();                                                              \
     hipError_t e_ = hipGetLastError();                                             \
     if (e_ == hipSuccess && ::pemp::debug_sync()) e_ = hipDeviceSynchronize();     \
     if (e_ != hipSuccess) {                                                        \

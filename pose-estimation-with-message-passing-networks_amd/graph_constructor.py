@@ -40,7 +40,10 @@ def _tag_fully(edge_index, node_off, counts, joint_det):
 def _tag_sym(edge_index):
     """Mark edge_index as a (src, dst)-sorted symmetric graph without duplicates (PyG to_undirected's output:
     knn, feature_knn, score_based), so that the MPN can take pemp_mpn_forward_sym; the version detects in-place
-    edits."""
+    edits. The tag is only a hint: writes the version counter does not see (through .data, raw pointers from
+    ctypes / DLPack / another library) keep it, and such an edited list then breaks the contract of
+    pemp_mpn_forward_sym. The library flags a broken contract in its workspace; the MPN reads that flag whenever
+    it validates (validate=True, PEMP_VALIDATE=1) and also under PEMP_DEBUG_SYNC=1."""
     edge_index._pemp_sym = edge_index._version
 
 

@@ -12,6 +12,7 @@ import itertools
 import os
 import warnings
 
+import numpy as np
 import torch
 import torch.nn as nn
 
@@ -21,8 +22,11 @@ from .edge_type import TypeAwareEdgeUpdate
 from .hierarch import HierarchUpdateCnn, HierarchUpdateMlp
 
 _VALIDATE = os.environ.get("PEMP_VALIDATE", "0") not in ("", "0")   # read once at import
+# PEMP_DEBUG_SYNC=1 (the library's synchronising debug mode) also reads the contract flags of every call
+_DEBUG_SYNC = os.environ.get("PEMP_DEBUG_SYNC", "0") not in ("", "0")
 _FULLY_OFF = os.environ.get("PEMP_NO_FULLY_PREPARE", "0") not in ("", "0")   # force the sorting prepare
 _SYM_OFF = os.environ.get("PEMP_NO_SYM_PREPARE", "0") not in ("", "0")       # (for symmetric graphs too)
+_EDGE_LIMIT = (1 << 23) - 1    # pemp_mpn_forward: E < 2^23 and T N < 2^23 per call (32-bit byte offsets)
 
 AGGR_CODES = {"attn": 0, "add": 1, "sum": 1, "mean": 2, "max": 3}
 PRECISIONS = {"fp32": 0, "bf16x3": 1, "f16x3": 2}
@@ -195,6 +199,10 @@ class NodeClassificationMPNSimple(nn.Module):
         self._tensors = None
         self._ws = _lib.Workspace()
         self._desc_key = None
+        # one libpemp call addresses r, Q0 and the aggregates with 32-bit byte offsets (pemp_mpn_forward: E, T N
+        # < 2^23); larger calls are cut into node blocks no edge crosses (image blocks for construct_graph output)
+        self._edge_limit = _EDGE_LIMIT
+        self._node_rows_limit = _EDGE_LIMIT
 
     # --------------------------------------------------------------------------------------
     def _apply(self, fn, *args, **kwargs):
@@ -225,6 +233,36 @@ class NodeClassificationMPNSimple(nn.Module):
             self._folded_key = key
         return self._folded
 
+    def _forward_blocks(self, x, edge_attr, edge_index, node_types, kwargs):
+        """A call over the library's size limit: the nodes are cut into contiguous blocks that no edge crosses
+        (each image of a construct_graph batch is such a block; node ids are image-major, ConstructGraph.py:206-231),
+        packed greedily under the limit, and each block runs as its own forward; the logits go back to their
+        edges and nodes. Graphs are per-image independent, so the result is the whole call's up to the rounding
+        order of the edge passes' work split."""
+        dev = x.device
+        N, E = x.shape[0], edge_index.shape[1]
+        ei = edge_index.long()
+        lo = torch.minimum(ei[0], ei[1])
+        blocks = node_blocks(ei, N, self._edge_limit, self._node_rows_limit // self.num_types)
+        n_rec = sum(1 for i in range(self.edge_steps) if i >= self.edge_steps - self.aux_loss_steps - 1)
+        edge_logits = torch.empty(max(n_rec, 1), E, dtype=torch.float32, device=dev)
+        node_logits = torch.empty(n_rec + 1, N, dtype=torch.float32, device=dev)
+        class_logits = torch.empty(n_rec + 1, N, self.num_joints, dtype=torch.float32, device=dev)
+        sub_kw = {k: v for k, v in kwargs.items() if k == "validate"}
+        for n0, n1 in blocks:
+            ids = torch.nonzero((lo >= n0) & (lo < n1)).flatten()
+            pe, pn, pc, _ = self.forward(x[n0:n1], edge_attr[ids], ei[:, ids] - n0, node_types=node_types[n0:n1],
+                                         **sub_kw)
+            for r in range(n_rec):
+                edge_logits[r, ids] = pe[r].reshape(-1)
+            for r in range(n_rec + 1):
+                node_logits[r, n0:n1] = pn[r].reshape(-1)
+                class_logits[r, n0:n1] = pc[r]
+        preds_edge = [edge_logits[r].view(E, 1).squeeze() for r in range(n_rec)]
+        preds_node = [node_logits[r].view(N, 1).squeeze() for r in range(n_rec + 1)]
+        preds_class = [class_logits[r] for r in range(n_rec + 1)]
+        return preds_edge, preds_node, preds_class, [None]
+
     def forward(self, x, edge_attr, edge_index, **kwargs):
         if self.training:
             raise NotImplementedError("pemp_amd MPN is inference-only: call .eval() (BatchNorm uses running stats)")
@@ -233,9 +271,11 @@ class NodeClassificationMPNSimple(nn.Module):
         L = _lib.lib()
         dev = x.device
         node_types = kwargs["node_types"]
+        N, E = x.shape[0], edge_index.shape[1]
+        if E > self._edge_limit or self.num_types * N > self._node_rows_limit:
+            return self._forward_blocks(x, edge_attr, edge_index, node_types, kwargs)
         if self.node_summary != "not":
             node_types = torch.tensor(TYPE_LUTS[self.node_summary], device=dev)[node_types]
-        N, E = x.shape[0], edge_index.shape[1]
         fully = _fully_graph(edge_index, node_types, N) if self.node_summary == "not" else None
         sym = fully is None and _sym_graph(edge_index)
         x = _as(x, torch.float32)
@@ -287,13 +327,41 @@ class NodeClassificationMPNSimple(nn.Module):
                                           edge_index.data_ptr(), node_types.data_ptr(), N, E, edge_logits.data_ptr(),
                                           node_logits.data_ptr(), class_logits.data_ptr(), ws.data_ptr(), ws.numel(),
                                           st))
-        if kwargs.get("validate", _VALIDATE):
+        if kwargs.get("validate", _VALIDATE or (_DEBUG_SYNC and (sym or fully is not None))):
             _lib.check(L.pemp_mpn_status(desc, N, E, _lib.ptr(ws), _lib.stream(dev)))
         # list lengths and .squeeze() semantics of NodeClassificationMPNSimple.py:81-97
         preds_edge = [edge_logits[r].view(E, 1).squeeze() for r in range(n_rec)]
         preds_node = [node_logits[r].view(N, 1).squeeze() for r in range(n_rec + 1)]
         preds_class = [class_logits[r] for r in range(n_rec + 1)]
         return preds_edge, preds_node, preds_class, [None]
+
+
+def node_blocks(edge_index, N, edge_limit, node_limit):
+    """[(n0, n1), ...]: contiguous node blocks covering [0, N) such that no edge joins two blocks, each holding at
+    most edge_limit edges and node_limit nodes (greedy: every block ends at the last admissible cut). Raises
+    NotImplementedError when one indivisible block is over a limit."""
+    E = edge_index.shape[1]
+    lo, hi = torch.minimum(edge_index[0], edge_index[1]), torch.maximum(edge_index[0], edge_index[1])
+    if E and (int(lo.min()) < 0 or int(hi.max()) >= N):
+        raise ValueError(f"edge_index holds node ids outside [0, {N})")
+    diff = torch.zeros(N + 1, dtype=torch.int64, device=edge_index.device)
+    diff.index_add_(0, lo, torch.ones_like(lo))
+    diff.index_add_(0, hi, -torch.ones_like(hi))
+    cover = diff.cumsum(0)[:N].cpu().numpy()                           # edges spanning the cut after node p
+    cum_e = torch.bincount(lo, minlength=N).cumsum(0).cpu().numpy()    # edges inside nodes [0, p]
+    cuts = np.nonzero(cover == 0)[0] + 1                               # admissible block ends; N among them
+    blocks, n0, e0 = [], 0, 0
+    while n0 < N:
+        k = min(int(np.searchsorted(cum_e[cuts - 1], e0 + edge_limit, "right")),
+                int(np.searchsorted(cuts, n0 + node_limit, "right"))) - 1
+        if k < 0:
+            raise NotImplementedError(f"pemp_amd MPN: a connected block of the graph exceeds one call's limit "
+                                      f"({edge_limit} edges, {node_limit} nodes)")
+        n1 = int(cuts[k])
+        blocks.append((n0, n1))
+        n0, e0 = n1, int(cum_e[n1 - 1])
+        cuts = cuts[k + 1:]
+    return blocks
 
 
 def _fully_graph(edge_index, node_types, N):
@@ -313,7 +381,7 @@ def _fully_graph(edge_index, node_types, N):
 
 def _sym_graph(edge_index):
     """True when edge_index is an untouched (src, dst)-sorted symmetric graph of the graph constructor
-    (graph_constructor._tag_sym)."""
+    (graph_constructor._tag_sym). A hint only: see _tag_sym for the edits it cannot see."""
     ever = getattr(edge_index, "_pemp_sym", None)
     return ever is not None and not _SYM_OFF and edge_index._version == ever
 

@@ -112,3 +112,26 @@ def test_two_ranks_share_gpu_hip_path(tmp_path):
         s = p["start"]
         for k, loc in enumerate(p["local"]):
             assert _same(parts[0]["poses"][s + k], loc)
+
+
+@pytest.mark.timeout(420)
+def test_bench_spawns_ranks():
+    """`python bench.py --gpus 2` with no launcher starts its two rank processes itself (bench.spawn_ranks) and
+    prints one line for the 2-rank job: n_gpus 2, the global batch of both image blocks, and the timed pose
+    all-gather. One-GPU rehearsal: both ranks on cuda:0, collectives over gloo."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(PEMP_SHARE_DEVICE="1", PEMP_DIST_BACKEND="gloo")
+    res = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                          "--no-cpu-baseline", "--streams", "1"], cwd=root, env=env, capture_output=True, text=True,
+                         timeout=400)
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout[-2000:]
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 16 and rec["config"]["images_per_gpu"] == 8
+    assert rec["pose_all_gather_ms"] is not None and rec["pose_grouping"]["gathered_images"] == 16
+    assert rec["value"] > 0

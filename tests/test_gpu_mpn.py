@@ -457,3 +457,28 @@ def test_feature_knn_graph_end_to_end():
     assert max_err(pe[-1], rpe[-1]) <= TOL
     assert max_err(pn[-1], rpn[-1]) <= TOL
     assert max_err(pc[-1], rpc[-1]) <= TOL
+
+
+@pytest.mark.parametrize("aux", [0, 2])
+def test_node_block_split(aux):
+    """A call over the library's per-call limit (E < 2^23, T N < 2^23) is cut into image blocks
+    (mpn/model.py::node_blocks); with the limit lowered, a 4-image batch runs as 3 blocks and its logits
+    equal the oracle's within the bar and the one-call run's within the bar."""
+    g = graph(4, 17, 96, 96, 3, seed=31)
+    x, ea, ei, types = g[0], g[1], g[2], g[7][:, 2]
+    cfg = pcfg.published_mpn_config(17, 3, "attn")
+    cfg.AUX_LOSS_STEPS = aux
+    model, sd = make_model(cfg, 0.75)
+    whole = run(model, x, ea, ei, types)
+    per_image = torch.bincount(g[12]).tolist()
+    edges = [n * (n - 1) for n in per_image]
+    model._edge_limit = max(edges[0] + edges[1], max(edges))   # images 0+1 fit one block, 2 and 3 alone
+    from pemp_amd.mpn.model import node_blocks
+    assert len(node_blocks(ei, x.shape[0], model._edge_limit, 1 << 20)) == 3
+    split = run(model, x, ea, ei, types)
+    ref = restate.mpn_forward(sd, cfg, x, ea, ei, types)
+    for k in range(3):
+        assert len(split[k]) == len(whole[k]) == len(ref[k])
+        for a, b, r in zip(split[k], whole[k], ref[k]):
+            assert a.shape == b.shape
+            assert max_err(a, r) < TOL and max_err(a, b.cpu()) < TOL

@@ -1,5 +1,6 @@
 """Host time between consecutive kernel launches inside the library (GPU box), one bench step:
-PEMP_HOST_TRACE=1 python tools/host_trace.py [workload]. Python-side marks: construct_graph entry/exit,
+PEMP_HOST_TRACE=1 PEMP_LIB=build_ab/libpemp_ht.so python tools/host_trace.py [workload], on a diagnostics
+build of the library (tools/build_variant.sh ht common.hip -DPEMP_HOST_TRACE, and mpn.hip / graph.hip the same way). Python-side marks: construct_graph entry/exit,
 count wait, model.forward entry/exit."""
 import ctypes
 import os
