@@ -307,17 +307,20 @@ def cpu_baseline(wl, gc, model, hm, feats, tags, budget_s):
     def timed(threads, budget):
         torch.set_num_threads(threads)
         times = {name: [] for name, _ in stage_fns}
-        spent, rounds = 0.0, 0
+        spent, rounds, warm = 0.0, 0, 3
         for r in range(3 + 15):
             for name, fn in stage_fns:
                 t0 = time.perf_counter()
                 fn()
                 dt = time.perf_counter() - t0
                 spent += dt
-                if r >= 3:
+                if r >= warm:
                     times[name].append(dt)
-            rounds += r >= 3
-            if rounds >= 6 and spent > budget:
+            if r == 0 and spent > budget / 6:
+                warm = 1                     # slow rounds (oversubscribed host): one warm-up round only
+            rounds += r >= warm
+            print(f"[bench] cpu_baseline {threads} threads: round {r + 1}, {spent:.1f} s", file=sys.stderr, flush=True)
+            if rounds >= (6 if warm == 3 else 1) and spent > budget:
                 break
         stages = {}
         for name, ts in times.items():
@@ -327,16 +330,39 @@ def cpu_baseline(wl, gc, model, hm, feats, tags, budget_s):
         per_image_ms = stages.get("frontend", 0.0) + stages["construct_graph"] + stages["mpn_forward"]
         return {"value": round(1e3 / per_image_ms, 3), "cores": threads, "stage_ms": stages, "rounds": rounds}
 
-    all_cores = os.cpu_count() or 1
-    main_run = timed(all_cores, 0.65 * budget_s)
-    share = timed(min(16, all_cores), 0.35 * budget_s)
-    return {"value": main_run["value"], "unit": "images/s", "cores": all_cores, "kind": "port",
+    cores = usable_cpus()
+    main_run = timed(cores, 0.65 * budget_s)
+    share = timed(min(16, cores), 0.35 * budget_s) if cores != min(16, cores) else None
+    return {"value": main_run["value"], "unit": "images/s", "cores": cores, "kind": "port",
             "stage_ms": main_run["stage_ms"], "rounds": main_run["rounds"], "threads_16": share,
             "sample": f"image 0 of the {wl['B']}-image workload; detect / construct_graph / mpn_forward interleaved, "
                       f"3 warm-up rounds, then {main_run['rounds']} rounds; per stage the least median of 3 blocks "
-                      f"(oracle/restate.py, torch CPU fp32, torch.set_num_threads(os.cpu_count())); "
+                      f"(oracle/restate.py, torch CPU fp32, torch.set_num_threads(every CPU this process may use: "
+                      f"os.cpu_count() {os.cpu_count()} limited by affinity and cgroup quota = {cores})); "
                       f"value = 1 / ({'frontend + ' if front_stage else ''}construct_graph + mpn_forward)",
-            "host_cpus": all_cores, "cpu_model": _cpu_model()}
+            "host_cpus": all_cores, "affinity_cpus": len(os.sched_getaffinity(0)), "cpu_model": _cpu_model()}
+
+
+def usable_cpus():
+    """CPUs this process can actually run on: os.cpu_count() limited by its affinity mask, OMP_NUM_THREADS and a
+    cgroup CPU quota (cgroup v2 cpu.max / v1 cfs_quota_us). On the GPU box os.cpu_count() is the whole machine's 256
+    threads while the process's share is 16: torch with 256 threads there thrashes (the MPN leg measured
+    108 s instead of 0.05 s), which times the contention, not the host."""
+    n = min(os.cpu_count() or 1, len(os.sched_getaffinity(0)))
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():   # the host's declared share (16 per GPU on the box)
+        n = min(n, max(1, int(os.environ["OMP_NUM_THREADS"])))
+    for path, per in (("/sys/fs/cgroup/cpu.max", None), ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us",
+                                                         "/sys/fs/cgroup/cpu/cpu.cfs_period_us")):
+        try:
+            txt = open(path).read().split()
+            quota = txt[0]
+            period = txt[1] if per is None else open(per).read().strip()
+            if quota not in ("max", "-1"):
+                n = min(n, max(1, int(int(quota) // int(period))))
+            break
+        except (OSError, ValueError, IndexError):
+            continue
+    return n
 
 
 def _cpu_model():
@@ -453,6 +479,116 @@ def frontend_heatmaps(wl, gc, feats, dev, reps=5):
     return res
 
 
+E2E_NODE_TH = 0.1     # node-probability threshold of the grouping (pred_to_ann th; bench's grouping leg uses the same)
+
+
+def e2e_pipeline(wl, gc, model, hm, feats, tags, dev, steps, warmup, world):
+    """The post-backbone step valid.py runs per image (valid.py:101-123), for a whole batch: the test front-end's
+    maps (ProjectedHeatmaps for the multi-scale workload) -> construct_graph -> MPN -> sigmoid / softmax
+    (valid.py:109-111) -> pred_to_ann (Utils.py:1445-1490): group_persons (GPU edge pass + host GAEC), fill_mean,
+    refine and adjust (TEST.WITH_REFINE / TEST.ADJUST of experiments/hybrid_class_agnostic_end2end/
+    model_58_4_4.yaml:170-172), reverse_affine_map. The MPN runs in every step; its closed-form weights form
+    no person, so the edge / node probabilities the grouping reads are person_structured_probs of the same graph
+    (the class probabilities are the MPN's softmax). Pipelined: batch k+1's GPU part (graph, MPN, edge pass,
+    copies) is queued before batch k's host part (GAEC, persons, finishing on a side stream) runs, as a server with
+    one batch in flight on each side would; `serial_*` runs the same steps one after the other."""
+    from pemp_amd import pose as ppose
+    J, B, H, W = wl["J"], wl["B"], wl["H"], wl["W"]
+    maps, tag_maps = dense_maps(hm, tags)
+    # the closed-form MPN weights give unstructured probabilities that form no person, so the grouping input is
+    # the pose_grouping leg's person-structured edge / node probabilities for the same graph
+    out0 = pemp_amd.get_graph_constructor(gc, scoremaps=hm, features=feats, tagmaps=tags, joints_gt=None,
+                                          factor_list=None, masks=None, device=dev, testing=True, heatmaps=None,
+                                          num_joints=J).construct_graph()
+    syn_probs = person_structured_probs(wl, out0)
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    stage = {}
+
+    def clock(name, t0):
+        t1 = time.perf_counter()
+        stage[name] = stage.get(name, 0.0) + t1 - t0
+        return t1
+
+    def gpu_part():
+        t0 = time.perf_counter()
+        out = pemp_amd.get_graph_constructor(gc, scoremaps=hm, features=feats, tagmaps=tags, joints_gt=None,
+                                             factor_list=None, masks=None, device=dev, testing=True, heatmaps=None,
+                                             num_joints=J).construct_graph()
+        t0 = clock("construct_graph", t0)
+        with torch.no_grad():
+            pe, pn, pc, _ = model(out[0], out[1], out[2], node_types=out[7][:, 2])
+            pe_p, pn_p, pc_p = pe[-1].sigmoid(), pn[-1].sigmoid(), pc[-1].softmax(dim=1)
+            if syn_probs:   # same shapes, person-structured (see pose_grouping); the MPN's class softmax is kept
+                pe_p, pn_p = syn_probs[0], syn_probs[1]
+        t0 = clock("mpn_queue", t0)
+        job = ppose.group_persons_start(out[7], pn_p, out[2], pe_p, E2E_NODE_TH, pc_p, "GAEC", J, batch_index=out[12],
+                                        score_map_scores=out[11], num_images=B)
+        clock("grouping_queue", t0)
+        return job
+
+    def host_part(job):
+        t0 = time.perf_counter()
+        per_image = job.result()
+        t0 = clock("grouping_host", t0)
+        fin = ppose.finish_batch(per_image, maps, tag_maps, adjustment=True, with_refine=True, stream=side)
+        t0 = clock("finish_refine_adjust", t0)
+        res = [None if p is None else ppose.reverse_affine_map(p.copy(), (W, H), W, "short_with_resize") for p in fin]
+        clock("reverse_affine_map", t0)
+        return res
+
+    def run(n, pipelined):
+        persons = 0
+        if pipelined:
+            pend = gpu_part()
+            for _ in range(n - 1):
+                nxt = gpu_part()
+                persons += sum(0 if r is None else len(r) for r in host_part(pend))
+                pend = nxt
+            persons += sum(0 if r is None else len(r) for r in host_part(pend))
+        else:
+            for _ in range(n):
+                persons += sum(0 if r is None else len(r) for r in host_part(gpu_part()))
+        return persons
+
+    rec = {}
+    for pipelined in (True, False):
+        run(max(2, warmup), pipelined)
+        stage.clear()
+        barrier(world)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        persons = run(steps, pipelined)
+        torch.cuda.synchronize()
+        barrier(world)
+        dt = max_over_ranks(time.perf_counter() - t0, world, dev)
+        key = "" if pipelined else "serial_"
+        rec[key + "images_per_sec"] = round(B * steps * world / dt, 2)
+        rec[key + "ms_per_batch"] = round(dt / steps * 1e3, 3)
+        if pipelined:
+            rec["stage_host_ms_per_batch"] = {k: round(v / steps * 1e3, 3) for k, v in stage.items()}
+            rec["persons_per_batch"] = round(persons / steps, 2)
+    rec["node_threshold"] = E2E_NODE_TH
+    rec["finishing"] = "fill_mean + refine + adjust (model_58_4_4.yaml TEST) + reverse_affine_map short_with_resize"
+    return rec
+
+
+def person_structured_probs(wl, out):
+    """Edge and node probabilities shaped like a trained network's for construct_graph output `out`: node i of
+    an image belongs to person (local index mod persons_per_image); edge probabilities sigmoid(+-2.5 + N(0, 1.5))
+    for same / different persons, drawn per direction; node probabilities sigmoid(2 + N(0, 1))."""
+    det, ei, bi = out[7], out[2], out[12]
+    N, E = det.shape[0], ei.shape[1]
+    node_off = torch.searchsorted(bi, torch.arange(wl["B"] + 1, device=bi.device))
+    pid = (torch.arange(N, device=bi.device) - node_off[bi]) % wl["persons"]
+    gen = torch.Generator(device=bi.device).manual_seed(7)
+    with torch.no_grad():
+        same = pid[ei[0]] == pid[ei[1]]
+        pe_p = torch.sigmoid(torch.where(same, 2.5, -2.5) + 1.5 * torch.randn(E, generator=gen, device=bi.device))
+        pn_p = torch.sigmoid(2.0 + torch.randn(N, generator=gen, device=bi.device))
+    return pe_p, pn_p
+
+
 def pose_grouping(wl, out, pe, pn, pc, cpu_ref):
     """SURVEY 8f row 2, informational: the pred_to_ann grouping prefix (node threshold 0.1, GAEC,
     graph_cluster_to_persons; Utils.py:1445-1459) for the whole step's batch, after the MPN and the
@@ -465,14 +601,8 @@ def pose_grouping(wl, out, pe, pn, pc, cpu_ref):
     # belongs to person (local index mod persons_per_image); edge probabilities sigmoid(+-2.5 + N(0, 1.5))
     # for same / different persons, drawn per direction; node probabilities sigmoid(2 + N(0, 1)); class
     # probabilities are the MPN's own softmax.
-    N, E = det.shape[0], ei.shape[1]
-    node_off = torch.searchsorted(bi, torch.arange(wl["B"] + 1, device=bi.device))
-    pid = (torch.arange(N, device=bi.device) - node_off[bi]) % wl["persons"]
-    gen = torch.Generator(device=bi.device).manual_seed(7)
+    pe_p, pn_p = person_structured_probs(wl, out)
     with torch.no_grad():
-        same = pid[ei[0]] == pid[ei[1]]
-        pe_p = torch.sigmoid(torch.where(same, 2.5, -2.5) + 1.5 * torch.randn(E, generator=gen, device=bi.device))
-        pn_p = torch.sigmoid(2.0 + torch.randn(N, generator=gen, device=bi.device))
         pc_p = pc[-1].softmax(dim=1)
     args = (det, pn_p, ei, pe_p, 0.1, pc_p, "GAEC", wl["J"])
     ppose.group_persons(*args, batch_index=bi, score_map_scores=sc, num_images=wl["B"])
@@ -667,6 +797,8 @@ def main():
     dt_mpn = max_over_ranks(time.perf_counter() - t1, world, dev)
     mpn_eups = E_all * wl["steps"] * args.steps / dt_mpn
 
+    e2e = e2e_pipeline(wl, gc, model, hm, feats, tags, dev, args.steps, args.warmup, world) \
+        if not args.no_roofline else None
     # (single-scale workloads: the front-end legs beside the step; a multi-scale workload runs them inside it)
     single = not wl.get("scales")
     front = frontend_projection(wl, gc, model, hm, tags, dev, out) if single and not args.no_roofline else None
@@ -713,6 +845,9 @@ def main():
                        "detection_and_node_math": "fp32"},
             "value_serial_steps": round(value_serial if value_serial else value, 2) if (value_serial or S == 1) else None,
             "schedule_probe": schedule_probe,
+            # the whole post-backbone step of valid.py (grouping and finishing included), pipelined over batches
+            "e2e_images_per_sec": e2e["images_per_sec"] if e2e else None,
+            "e2e": e2e,
             "mpn_edge_updates_per_sec": round(mpn_eups, 1),
             "mpn_ms_per_step": round(dt_mpn / args.steps * 1e3, 3),
             "pipeline_edge_updates_per_sec": round(E_all * wl["steps"] * args.steps / dt_max, 1),

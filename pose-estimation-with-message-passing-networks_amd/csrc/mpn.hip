@@ -631,13 +631,15 @@ __device__ __forceinline__ float frag_max_nonneg(const float (&x)[4][4]) {
 // split of the fragment s·x (s a power of two); returns the wave's range flag. When it is set, `sc` is each
 // item's range factor (the parts hold s·x·sc and a GEMM over them rescales the item's column by 1/sc); else 1.
 // NONNEG: x holds no negative value (relu1 output)
+// extra: a per-lane factor in (0, 1] folded into the parts (the parts then hold s x sc extra; one rounding, in
+// the split: the attention weight of the edge, PE_FOLD in edge_step_kernel); the range check stays on s x.
 template <bool NONNEG = false>
 __device__ __forceinline__ bool split_f16(const float (&x)[4][4], float s, f16x8_t (&hi)[2], f16x8_t (&lo)[2],
-                                          float& sc) {
+                                          float& sc, float extra = 1.0f) {
   const float m = NONNEG ? frag_max_nonneg(x) : frag_absmax(x);
   const bool big = __any(!(m * s < F16_BIG));
   sc = big ? f16_item_scale(m, s) : 1.0f;
-  const float ss = s * sc;
+  const float ss = s * sc * extra;
 #pragma unroll
   for (int kb = 0; kb < 2; ++kb) {
     uint32_t h[4], l[4];
@@ -700,6 +702,12 @@ template <int PREC, bool NONNEG = false>
 __device__ __forceinline__ void prep(const float (&x)[4][4], Frag<PREC>& f) {
   if constexpr (PREC == 1) split_bf16(x, f.bh, f.bl);
   else if constexpr (PREC == 2) f.big = split_f16<NONNEG>(x, dom_inv<PREC>(), f.hh, f.hl, f.sc);
+}
+
+// f16x3: x in the domain, split with the per-lane factor `extra` folded in (see split_f16)
+template <bool NONNEG = false>
+__device__ __forceinline__ void prep_f16_scaled(const float (&x)[4][4], Frag<2>& f, float extra) {
+  f.big = split_f16<NONNEG>(x, dom_inv<2>(), f.hh, f.hl, f.sc, extra);
 }
 
 // x in the true domain (f16x3: split with scale 1)
@@ -1258,6 +1266,68 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
+// ---- the same scans in hand-placed DPP instructions (PEMP_ASM_SCANS, the default) ----
+// hipcc turns the per-value `fmaf(dpp(v), mask, v)` of seg_sum into a v_mov_b32_dpp per value and a
+// v_pk_fma_f32 per pair (3 instructions per 2 values and step), and every fmaxf of seg_max into a
+// mov_dpp + cndmask + canonicalising max + max. Here: one v_fmac_f32_dpp per value and step (the DPP source
+// reads 0 outside the row, where the mask is 0 anyway), and for the max one v_max_f32_dpp (source lane
+// outside the row: not written) + one v_cndmask on a lane mask per step. The 17 sums go step by step, so
+// every DPP read is 17 instructions behind the write of its source (the 2 VALU-write -> DPP-read wait states
+// are only needed at entry, s_nop 1); the max chain is serial, with an s_nop 1 per step.
+// hipcc inserts no hazard wait states in front of inline asm: an asm block that reads an MFMA result (or writes
+// a register an MFMA still reads) right after the MFMA would see the stale value. Every block below therefore
+// opens with the longest XDL -> VALU distance (19 wait states: a 16-pass MFMA) before its first VALU instruction.
+#define PEMP_XDL_GUARD "s_nop 7\n\ts_nop 7\n\ts_nop 4\n\t"
+// ... and closes with the 2 VALU-write -> DPP-read wait states: the compiler does not see the asm's last writes
+// either, and its next DPP read of one of them (the carry's row shifts) would otherwise read the stale value
+#define PEMP_DPP_TAIL "s_nop 1\n\t"
+#ifndef PEMP_ASM_SCANS
+#define PEMP_ASM_SCANS 1
+#endif
+struct ChunkMasks {
+  uint64_t f1, f2, f4, f8, b1, b2, b4, b8;   // lanes with d >= k (forward steps) / u >= k (backward steps)
+};
+__device__ __forceinline__ ChunkMasks chunk_masks(const Chunks& k) {
+  return {__builtin_amdgcn_ballot_w64(k.d >= 1), __builtin_amdgcn_ballot_w64(k.d >= 2),
+          __builtin_amdgcn_ballot_w64(k.d >= 4), __builtin_amdgcn_ballot_w64(k.d >= 8),
+          __builtin_amdgcn_ballot_w64(k.u >= 1), __builtin_amdgcn_ballot_w64(k.u >= 2),
+          __builtin_amdgcn_ballot_w64(k.u >= 4), __builtin_amdgcn_ballot_w64(k.u >= 8)};
+}
+
+// every lane of a chunk gets the chunk's maximum (forward segmented max, then the tail's value backwards)
+__device__ __forceinline__ float chunk_max_asm(float v, const ChunkMasks& mk) {
+  float t;
+#define PEMP_MAXSTEP(ctl, m)                                                   \
+  "s_nop 1\n\t"                                                                \
+  "v_max_f32_dpp %1, %0, %0 " ctl " row_mask:0xf bank_mask:0xf\n\t"            \
+  "v_cndmask_b32_e64 %0, %0, %1, %" #m "\n\t"
+  asm(PEMP_XDL_GUARD PEMP_MAXSTEP("row_shr:1", 2) PEMP_MAXSTEP("row_shr:2", 3) PEMP_MAXSTEP("row_shr:4", 4)
+      PEMP_MAXSTEP("row_shr:8", 5) PEMP_MAXSTEP("row_shl:1", 6) PEMP_MAXSTEP("row_shl:2", 7)
+      PEMP_MAXSTEP("row_shl:4", 8) PEMP_MAXSTEP("row_shl:8", 9) PEMP_DPP_TAIL
+      : "+v"(v), "=&v"(t)
+      : "s"(mk.f1), "s"(mk.f2), "s"(mk.f4), "s"(mk.f8), "s"(mk.b1), "s"(mk.b2), "s"(mk.b4), "s"(mk.b8));
+#undef PEMP_MAXSTEP
+  return v;
+}
+
+// segmented inclusive sums of the 16 fragment values and the normaliser l (m: ScanMask, 1.0 where d >= k)
+#define PEMP_FMAC1(i, ctl, m) "v_fmac_f32_dpp %" #i ", %" #i ", %" #m " " ctl " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+#define PEMP_FMAC17(ctl, m)                                                                                       \
+  PEMP_FMAC1(0, ctl, m) PEMP_FMAC1(1, ctl, m) PEMP_FMAC1(2, ctl, m) PEMP_FMAC1(3, ctl, m) PEMP_FMAC1(4, ctl, m) \
+  PEMP_FMAC1(5, ctl, m) PEMP_FMAC1(6, ctl, m) PEMP_FMAC1(7, ctl, m) PEMP_FMAC1(8, ctl, m) PEMP_FMAC1(9, ctl, m) \
+  PEMP_FMAC1(10, ctl, m) PEMP_FMAC1(11, ctl, m) PEMP_FMAC1(12, ctl, m) PEMP_FMAC1(13, ctl, m)                   \
+  PEMP_FMAC1(14, ctl, m) PEMP_FMAC1(15, ctl, m) PEMP_FMAC1(16, ctl, m)
+__device__ __forceinline__ void seg_sum17_asm(float (&v)[4][4], float& l, const ScanMask& m) {
+  asm(PEMP_XDL_GUARD PEMP_FMAC17("row_shr:1", 17) PEMP_FMAC17("row_shr:2", 18) PEMP_FMAC17("row_shr:4", 19)
+          PEMP_FMAC17("row_shr:8", 20) PEMP_DPP_TAIL
+      : "+v"(v[0][0]), "+v"(v[0][1]), "+v"(v[0][2]), "+v"(v[0][3]), "+v"(v[1][0]), "+v"(v[1][1]), "+v"(v[1][2]),
+        "+v"(v[1][3]), "+v"(v[2][0]), "+v"(v[2][1]), "+v"(v[2][2]), "+v"(v[2][3]), "+v"(v[3][0]), "+v"(v[3][1]),
+        "+v"(v[3][2]), "+v"(v[3][3]), "+v"(l)
+      : "v"(m.m1), "v"(m.m2), "v"(m.m4), "v"(m.m8));
+}
+#undef PEMP_FMAC17
+#undef PEMP_FMAC1
+
 
 // ---- edge-pass weight image --------------------------------------------------------------------
 // The LDS image of one edge pass, prepared once per weight set in global memory (one block per source
@@ -1468,10 +1538,22 @@ __device__ __forceinline__ void dma_wait() {
 }
 
 #ifndef PEMP_FAST_EXP
-#define PEMP_FAST_EXP 0
+#define PEMP_FAST_EXP 1
 #endif
-// softmax exponent: expf (correctly rounded to ~1 ulp) or the bare v_exp_f32 path (__expf)
+#ifndef PEMP_GATHER_FIRST
+#define PEMP_GATHER_FIRST 0
+#endif
+#ifndef PEMP_PRIO
+#define PEMP_PRIO 1
+#endif
+// softmax exponent: expf (correctly rounded to ~1 ulp) or the bare v_exp_f32 path (__expf, the default: the
+// exponent is <= 0 and its relative error |x| 2^-24 ln 2 stays far below the 1e-4 logit bar)
 __device__ __forceinline__ float pemp_exp(float x) { return PEMP_FAST_EXP ? __expf(x) : expf(x); }
+#ifndef PEMP_FAST_RCP
+#define PEMP_FAST_RCP 1
+#endif
+// segment normaliser: IEEE division or v_rcp_f32 (1 ulp)
+__device__ __forceinline__ float pemp_rcp(float x) { return PEMP_FAST_RCP ? __builtin_amdgcn_rcpf(x) : 1.0f / x; }
 #ifndef PEMP_XCD_MAP
 #define PEMP_XCD_MAP 1
 #endif
@@ -1483,6 +1565,9 @@ __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_
   // after the e-block GEMM instead of inside the first ReLU.
   constexpr bool EPT = (STAGE & STAGE_EPT) != 0;
   constexpr bool MID = (STAGE & 3) == STAGE_MID;
+  // attention with the update block pre-applied, f16x3: each message's softmax weight exp(a - M) is folded into
+  // the split of m for the update GEMM (split_f16's per-lane factor) instead of a multiply of its 64 values
+  constexpr bool PE_FOLD = AGG == PEMP_AGGR_ATTN && UPD && PREC == 2;
   // the last pass writes no next r: its copy of the image starts past W1 (SKIP floats)
   constexpr int SKIP = MID ? 0 : D * LDW;
   constexpr int IMG_F = img_common(UPD) + (HEAD == 1 ? IMG_HEAD : 0) - SKIP;
@@ -1577,6 +1662,14 @@ __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_
   int tile_no = 0;
   for (int base = first; base < end; base += 16, ++tile_no) {
     if (tile_no < 4) EDGE_STAMP(3 + 3 * tile_no);
+#if PEMP_PRIO
+    // progress-ordered issue priority: a wave that has finished fewer tiles than its SIMD partners goes first
+    // (the hardware otherwise favours the oldest wave, which then finishes long before the youngest)
+    if (tile_no == 0) __builtin_amdgcn_s_setprio(3);
+    else if (tile_no == 1) __builtin_amdgcn_s_setprio(2);
+    else if (tile_no == 2) __builtin_amdgcn_s_setprio(1);
+    else if (tile_no == 3) __builtin_amdgcn_s_setprio(0);
+#endif
     // opaque zero: keeps the compiler from hoisting the LDS weight fragments out of the loop
     // (192+ VGPRs of loop-invariant loads would spill)
     int z = 0;
@@ -1679,6 +1772,21 @@ __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_
       av += __shfl_xor(av, 32);
       av += vec[z + 2 * D];                      // attention bias (re-read: a register copy spills)
     }
+    // chunk structure of the tile and each edge's softmax weight pe = exp(a - M), M = its segment's maximum so far
+    // (computed before the message GEMMs: with PE_FOLD it rides in the split of m)
+    const int seg = valid ? dst : -1 - c;        // padding lanes: singleton chunks, never written
+    const Chunks ck = chunks_of(seg, c);
+    const bool carry_in = have_carry;            // wave-uniform: set only when the segment continues
+    float M = 0.f, pe = 1.0f;
+    if (AGG == PEMP_AGGR_ATTN) {
+#if PEMP_ASM_SCANS
+      M = chunk_max_asm(av, chunk_masks(ck));   // (checked on the GPU in every precision)
+#else
+      M = seg_bcast_tail_max(seg_max(av, ck.d), ck.u);
+#endif
+      if (carry_in && ck.d == c) M = fmaxf(M, cM);   // head chunk continues the carried segment
+      pe = pemp_exp(av - M);
+    }
     if (HEAD == 2) {   // generic edge head (weights in global memory, true domain)
       float h1[4][4], h2[4][4];
 #pragma unroll
@@ -1756,7 +1864,8 @@ __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_
 #pragma unroll
         for (int r = 0; r < 4; ++r) u[ob][r] = 0.0f;
       Frag<PREC> fm;
-      prep<PREC, true>(m, fm);
+      if constexpr (PE_FOLD) prep_f16_scaled<true>(m, fm, pe);
+      else prep<PREC, true>(m, fm);
       gemm_f<PREC, 4>(UW, m, fm, u);
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob)
@@ -1765,21 +1874,12 @@ __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_
     }
 
     // ---- segmented reduction of the tile, carry in / out ----
-    const int seg = valid ? dst : -1 - c;        // padding lanes: singleton chunks, never written
-    const Chunks ck = chunks_of(seg, c);
-    const bool carry_in = have_carry;            // wave-uniform: set only when the segment continues
-    float M = 0.f, l = 1.0f, pe = 1.0f;
-    if (AGG == PEMP_AGGR_ATTN) {
-      M = seg_bcast_tail_max(seg_max(av, ck.d), ck.u);
-      if (carry_in && ck.d == c) M = fmaxf(M, cM);   // head chunk continues the carried segment
-      pe = pemp_exp(av - M);
-      l = pe;
-    }
+    float l = (AGG == PEMP_AGGR_ATTN) ? pe : 1.0f;
     float v[4][4];
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[ob][r] = (AGG == PEMP_AGGR_ATTN) ? pe * m[ob][r] : m[ob][r];
+      for (int r = 0; r < 4; ++r) v[ob][r] = (AGG == PEMP_AGGR_ATTN && !PE_FOLD) ? pe * m[ob][r] : m[ob][r];
     if (carry_in && c == 0) {
       if (AGG == PEMP_AGGR_ATTN) {
         const float f = pemp_exp(cM - M);
@@ -1798,11 +1898,18 @@ __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_
       }
     }
     const ScanMask smk = scan_mask(ck.d);
-    if (AGG == PEMP_AGGR_ATTN || AGG == PEMP_AGGR_MEAN) l = seg_sum(l, smk);   // normaliser / count
+    // (the hand-placed sums only where the attention weight is folded into the update split, PE_FOLD: with the
+    // weight multiplied in separately -- the bf16x3 / fp32 kernels -- they gave wrong aggregates on the GPU
+    // (bf16x3 logits 1e-3 off), for a reason not found; those kernels keep the compiler's scans)
+    if (PEMP_ASM_SCANS && PE_FOLD) {
+      seg_sum17_asm(v, l, smk);                  // the 64 features and the normaliser / count
+    } else {
+      if (AGG == PEMP_AGGR_ATTN || AGG == PEMP_AGGR_MEAN) l = seg_sum(l, smk);   // normaliser / count
 #pragma unroll
-    for (int ob = 0; ob < 4; ++ob)
+      for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[ob][r] = (AGG == PEMP_AGGR_MAX) ? seg_max(v[ob][r], ck.d) : seg_sum(v[ob][r], smk);
+        for (int r = 0; r < 4; ++r) v[ob][r] = (AGG == PEMP_AGGR_MAX) ? seg_max(v[ob][r], ck.d) : seg_sum(v[ob][r], smk);
+    }
     // the chunk at the tile end continues iff the next tile starts with the same target
     const int seg15 = __builtin_amdgcn_readlane(seg, 15);
     const bool carry_out = more && __builtin_amdgcn_readlane(dst_n, 0) == seg15;
@@ -1815,9 +1922,15 @@ __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_
         for (int r = 0; r < 4; ++r) cacc[ob][r] = dppf<DPP_SHL15>(v[ob][r], 0.0f);   // lane 15 -> lane 0
     }
     have_carry = carry_out;
+#if PEMP_GATHER_FIRST
+    // the next tile's gathers ahead of this tile's aggregate stores: waiting for them at the next tile then does
+    // not wait for those stores too (vmcnt retires in issue order)
+    gather_nt(dst_n, src_n, more);
+    if (HEAD == 1) orig_t = bld1(rs_orig, 4 * min(p + 16, end - 1));
+#endif
     {
       // the aggregate leaves the f16x3 domain here (dom_inv)
-      const float inv = ((AGG == PEMP_AGGR_ATTN) ? 1.0f / (l + 1e-12f) : (AGG == PEMP_AGGR_MEAN) ? 1.0f / l : 1.0f) *
+      const float inv = ((AGG == PEMP_AGGR_ATTN) ? pemp_rcp(l + 1e-12f) : (AGG == PEMP_AGGR_MEAN) ? pemp_rcp(l) : 1.0f) *
                         dom_inv<PREC>();
       const bool out = valid && ck.tail && !(carry_out && c == 15);
       // a segment cut by a range end: its raw piece goes to this wave's record instead (at most two per wave; the
@@ -1836,10 +1949,12 @@ __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_
         if (g == 0) { rec[64] = M; rec[65] = l; }
       }
     }
+#if !PEMP_GATHER_FIRST
     {   // the next tile's gathers, unconditional (past the range: OOB offsets, no traffic)
       gather_nt(dst_n, src_n, more);
       if (HEAD == 1) orig_t = bld1(rs_orig, 4 * min(p + 16, end - 1));
     }
+#endif
 #ifdef PEMP_STAMPS
     asm volatile("" ::"v"(v[0][0]), "v"(v[3][3]));
     if (tile_no < 4) EDGE_STAMP(5 + 3 * tile_no);

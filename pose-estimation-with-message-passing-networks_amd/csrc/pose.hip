@@ -148,11 +148,14 @@ void gaec(size_t n, const std::vector<size_t>& ea, const std::vector<size_t>& eb
     return v;
   };
   while (!q.empty()) {
+    // andres pops, skips stale entries and stops at the first live one with w < 0; every entry below a negative
+    // top is negative too, so no contraction can follow once the top is negative: stop there instead of popping
+    // the (mostly stale) negative entries one by one (the same partition; ~3x less time, gaec_dense alike)
+    if (q.top().w < 0.0) break;
     const GaecEdge e = q.top();
     q.pop();
     const auto& aa = adj[e.a];
     if (aa.empty() || aa.find(e.b) == aa.end() || e.edition < editions[e.a][e.b]) continue;
-    if (e.w < 0.0) break;
     size_t keep = e.a, merge = e.b;
     if (adj[keep].size() < adj[merge].size()) std::swap(keep, merge);
     {
@@ -228,10 +231,10 @@ void gaec_dense(size_t n, const std::vector<size_t>& ea, const std::vector<size_
     return v;
   };
   while (!q.empty()) {
+    if (q.top().w < 0.0) break;   // (see gaec)
     const GaecEdge16 e = q.top();
     q.pop();
     if (!ex[e.a * n + e.b] || e.edition < ed[e.a * n + e.b]) continue;
-    if (e.w < 0.0) break;
     size_t keep = e.a, merge = e.b;
     if (deg[keep] < deg[merge]) std::swap(keep, merge);
     {

@@ -35,26 +35,44 @@ def _host_threads():
     return max(1, min(16, os.cpu_count() or 1))
 
 
-def _to_host(tensors, dev):
-    """Stream-ordered copies of device tensors into pinned host tensors, one synchronisation (of the
-    current stream of `dev`, where the edge pass and the copies are queued)."""
+def _to_host_async(tensors, dev):
+    """Stream-ordered copies of device tensors into pinned host tensors, queued on the current stream of `dev`
+    behind the work that produces them, plus an event recorded after them: the host buffers are valid once the
+    event has completed."""
     out = []
-    for t in tensors:
-        if t is None:
-            out.append(None)
-            continue
-        h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
-        with torch.cuda.device(dev):
+    with torch.cuda.device(dev):
+        for t in tensors:
+            if t is None:
+                out.append(None)
+                continue
+            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
             h.copy_(t, non_blocking=True)
-        out.append(h)
-    torch.cuda.current_stream(dev).synchronize()
-    return out
+            out.append(h)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+    return out, ev
 
 
-def _run(joint_det, joint_scores, edge_index, pred, node_off, th, use_th, class_pred, cc_method, num_joints,
-         score_for_poses=None, allow_single=False, timings=None):
-    """Shared path. node_off: host int64 [B+1]. Returns (persons list, mutants, labels, flags).
-    timings: optional dict, filled with per-stage host wall times (s) -- measurement only."""
+class GroupingJob:
+    """The grouping of one batch, started on the GPU (group_persons_start / _start): the edge pass and the copies
+    of everything the host part reads are queued on the current stream, nothing waited for. ``result()`` waits for
+    the copies (an event, not a stream sync: work queued after the job keeps running) and runs the host part:
+    GAEC / threshold components and the person assembly (C++, one image per thread)."""
+
+    def __init__(self, state, finish):
+        self._state, self._finish, self._out = state, finish, None
+
+    def result(self):
+        if self._state is not None:
+            self._out = self._finish(**self._state)
+            self._state = None
+        return self._out
+
+
+def _start(joint_det, joint_scores, edge_index, pred, node_off_d, B, th, use_th, class_pred, cc_method, num_joints,
+           score_for_poses=None, allow_single=False, timings=None, extra=()):
+    """GPU part of the shared path. node_off_d: device int64 [B+1] (computed on the device from batch_index, so
+    that nothing here waits for the GPU); extra: more device tensors to bring to the host with the same copies."""
     import time
     t0 = time.perf_counter()
     L = _lib.lib()
@@ -62,8 +80,7 @@ def _run(joint_det, joint_scores, edge_index, pred, node_off, th, use_th, class_
     dev = edge_index.device
     if dev.type != "cuda":
         raise ValueError("pemp_amd.pose: expects device tensors (the HIP path has no CPU fallback)")
-    B = len(node_off) - 1
-    N = int(node_off[-1])
+    N = joint_det.shape[0]
     if joint_det.shape != (N, 3) or joint_scores.shape != (N,):
         raise ValueError(f"pemp_amd.pose: joint_det {tuple(joint_det.shape)} / joint_scores "
                          f"{tuple(joint_scores.shape)} do not match {N} nodes")
@@ -73,12 +90,11 @@ def _run(joint_det, joint_scores, edge_index, pred, node_off, th, use_th, class_
     if pr.numel() != E:
         raise ValueError(f"pemp_amd.pose: pred has {pr.numel()} values for {E} edges")
     sc = joint_scores.to(torch.float32).contiguous()
-    off_d = torch.from_numpy(node_off).to(dev)
     w = torch.empty(E, dtype=torch.float32, device=dev)
     flags = torch.empty(B + 1, dtype=torch.int32, device=dev)
     row_start = torch.empty(N + 1, dtype=torch.int64, device=dev)
     _lib.check(L.pemp_pose_edge_weights(_lib.ptr(ei), E, _lib.ptr(pr), _lib.ptr(sc), float(th), int(use_th),
-                                        _lib.ptr(off_d), B, N, method, _lib.ptr(row_start), _lib.ptr(w),
+                                        _lib.ptr(node_off_d), B, N, method, _lib.ptr(row_start), _lib.ptr(w),
                                         _lib.ptr(flags), _lib.stream(dev)))
     cls = class_pred.to(torch.float32).contiguous() if class_pred is not None else None
     if cls is not None and cls.shape != (N, num_joints):
@@ -89,12 +105,25 @@ def _run(joint_det, joint_scores, edge_index, pred, node_off, th, use_th, class_
         t1 = time.perf_counter()
         timings["edge_pass"] = timings.get("edge_pass", 0.0) + t1 - t0
         t0 = t1
-    h_ei, h_w, h_flags, h_det, h_sc, h_cls, h_ps = _to_host(
-        [ei, w, flags, joint_det.to(torch.int64).contiguous(), sc, cls, ps], dev)
+    host, ev = _to_host_async([ei, w, flags, joint_det.to(torch.int64).contiguous(), sc, cls, ps, node_off_d]
+                              + list(extra), dev)
+    return dict(host=host, ev=ev, B=B, N=N, E=E, cc_method=cc_method, num_joints=num_joints,
+                allow_single=allow_single, timings=timings, t0=t0)
+
+
+def _finish(host, ev, B, N, E, cc_method, num_joints, allow_single, timings, t0):
+    """Host part of the shared path. Returns (persons list, mutants, labels, flags, node_off, extra host tensors)."""
+    import time
+    ev.synchronize()
     if timings is not None:
         t1 = time.perf_counter()
         timings["to_host"] = timings.get("to_host", 0.0) + t1 - t0
         t0 = t1
+    L = _lib.lib()
+    method = _method(cc_method)
+    h_ei, h_w, h_flags, h_det, h_sc, h_cls, h_ps, h_off = host[:8]
+    extra = host[8:]
+    node_off = h_off.numpy()
     if h_flags[B] & 4:
         raise ValueError("pemp_amd.pose: edge_index holds a node index outside [0, N)")
     if cc_method == "greedy":
@@ -109,7 +138,7 @@ def _run(joint_det, joint_scores, edge_index, pred, node_off, th, use_th, class_
                                       taken.ctypes.data, cap, persons.ctypes.data, counts.ctypes.data), L)
         starts = np.concatenate([[0], np.cumsum(counts)])
         per_image = [persons[starts[b]:starts[b + 1]].copy() for b in range(B)]
-        return per_image, np.zeros(B, dtype=bool), taken, h_flags.numpy()
+        return per_image, np.zeros(B, dtype=bool), taken, h_flags.numpy(), node_off, extra
     labels = np.empty(N, dtype=np.int32)
     n_comp = np.empty(B, dtype=np.int32)
     _lib.check(L.pemp_pose_cluster(B, node_off.ctypes.data, h_ei.data_ptr(), E, h_w.data_ptr(),
@@ -131,7 +160,16 @@ def _run(joint_det, joint_scores, edge_index, pred, node_off, th, use_th, class_
         timings["persons"] = timings.get("persons", 0.0) + time.perf_counter() - t0
     starts = np.concatenate([[0], np.cumsum(counts)])
     per_image = [persons[starts[b]:starts[b + 1]].copy() for b in range(B)]
-    return per_image, mutants.astype(bool), labels, h_flags.numpy()
+    return per_image, mutants.astype(bool), labels, h_flags.numpy(), node_off, extra
+
+
+def _run(joint_det, joint_scores, edge_index, pred, node_off, th, use_th, class_pred, cc_method, num_joints,
+         score_for_poses=None, allow_single=False, timings=None):
+    """Shared path, synchronous. node_off: host int64 [B+1]. Returns (persons list, mutants, labels, flags)."""
+    off_d = torch.from_numpy(np.ascontiguousarray(node_off, dtype=np.int64)).to(edge_index.device)
+    st = _start(joint_det, joint_scores, edge_index, pred, off_d, len(node_off) - 1, th, use_th, class_pred, cc_method,
+                num_joints, score_for_poses, allow_single, timings)
+    return _finish(**st)[:4]
 
 
 def pred_to_person(joint_det, joint_scores, edge_index, pred, class_pred, cc_method, num_joints,
@@ -160,34 +198,56 @@ def group_persons(joint_det, joint_scores, edge_index, pred, th, class_pred=None
     with batch_index: trailing images without detections have no batch_index entry). Returns one entry
     per image: persons float64 [P, J, 3], or None where ``pred_to_ann`` returns None (no detector score >
     0.1, no edge surviving the node threshold, no person)."""
+    return group_persons_start(joint_det, joint_scores, edge_index, pred, th, class_pred, cc_method, num_joints,
+                               batch_index, score_map_scores, num_images, _timings).result()
+
+
+def group_persons_start(joint_det, joint_scores, edge_index, pred, th, class_pred=None, cc_method="GAEC",
+                        num_joints=17, batch_index=None, score_map_scores=None, num_images=None, _timings=None):
+    """group_persons in two halves for pipelined callers: this queues the GPU part (edge pass, copies to pinned
+    host memory) on the current stream and returns at once; ``.result()`` of the returned job waits for the
+    copies only and runs the host part, so the GPU can run the next batch meanwhile. Same arguments and
+    result as group_persons."""
     N = joint_det.shape[0]
+    dev = edge_index.device
     if batch_index is None:
         if num_images not in (None, 1):
             raise ValueError("pemp_amd.pose: num_images > 1 needs batch_index")
-        node_off = np.array([0, N], dtype=np.int64)
+        B = 1
+        off_d = torch.tensor([0, N], dtype=torch.int64, device=dev)
+        bi = None
     else:
         if num_images is None:
             raise ValueError("pemp_amd.pose: group_persons(batch_index=...) needs num_images (the batch size)")
         B = int(num_images)
-        bi = batch_index.cpu().numpy()
-        if len(bi) and np.any(bi[1:] < bi[:-1]):
-            raise ValueError("pemp_amd.pose: batch_index must be non-decreasing (construct_graph order)")
-        if len(bi) and (bi[0] < 0 or bi[-1] >= B):
-            raise ValueError(f"pemp_amd.pose: batch_index outside [0, {B})")
-        node_off = np.searchsorted(bi, np.arange(B + 1)).astype(np.int64)
-    per_image, _, _, flags = _run(joint_det, joint_scores, edge_index, pred, node_off, th, True, class_pred,
-                                  cc_method, num_joints, timings=_timings)
-    ok_det = None
-    if score_map_scores is not None:
-        s = (score_map_scores > 0.1).cpu().numpy()
-        ok_det = np.array([s[node_off[b]:node_off[b + 1]].any() for b in range(len(node_off) - 1)])
-    out = []
-    for b, persons in enumerate(per_image):
-        if (ok_det is not None and not ok_det[b]) or not (flags[b] & 2) or len(persons) == 0:
-            out.append(None)
-        else:
-            out.append(persons)
-    return out
+        bi = batch_index.to(torch.int64).contiguous()
+        off_d = torch.searchsorted(bi, torch.arange(B + 1, device=dev, dtype=torch.int64))
+    extra = [bi if bi is not None else None,
+             (score_map_scores > 0.1) if score_map_scores is not None else None]
+    st = _start(joint_det, joint_scores, edge_index, pred, off_d, B, th, True, class_pred, cc_method, num_joints,
+                timings=_timings, extra=extra)
+
+    def finish(**kw):
+        per_image, _, _, flags, node_off, (h_bi, h_ok) = _finish(**kw)
+        if h_bi is not None:
+            b_np = h_bi.numpy()
+            if len(b_np) and np.any(b_np[1:] < b_np[:-1]):
+                raise ValueError("pemp_amd.pose: batch_index must be non-decreasing (construct_graph order)")
+            if len(b_np) and (b_np[0] < 0 or b_np[-1] >= B):
+                raise ValueError(f"pemp_amd.pose: batch_index outside [0, {B})")
+        ok_det = None
+        if h_ok is not None:
+            s = h_ok.numpy()
+            ok_det = np.array([s[node_off[b]:node_off[b + 1]].any() for b in range(B)])
+        out = []
+        for b, persons in enumerate(per_image):
+            if (ok_det is not None and not ok_det[b]) or not (flags[b] & 2) or len(persons) == 0:
+                out.append(None)
+            else:
+                out.append(persons)
+        return out
+
+    return GroupingJob(st, finish)
 
 
 # ----------------------------------------------------------------------------------------------------
@@ -297,6 +357,59 @@ def finish_persons(persons, scoremaps, tags, adjustment, with_refine, with_filte
     if adjustment:
         adjust(persons, scoremaps)
     return persons
+
+
+def finish_batch(per_image, scoremaps, tags, adjustment=True, with_refine=False, with_filter=False,
+                 fill_mean_=True, stream=None):
+    """finish_persons over a batch (``pred_to_ann``, ``Utils.py:1460-1478``, once per image): per_image as
+    group_persons returns it, scoremaps [B, J, H, W] / tags [B, J, H, W(, F)] device tensors. The adjust
+    kernels of every image are queued together on `stream` (default: the current stream) and waited for once,
+    by an event after one pinned copy each, instead of one stream synchronisation per image."""
+    out = [None if p is None else p for p in per_image]
+    dev = scoremaps.device
+    st = stream if stream is not None else torch.cuda.current_stream(dev)
+    for b, persons in enumerate(out):
+        if persons is None:
+            continue
+        if with_filter:
+            keep = persons[:, :, 2].max(axis=1) > 0.25
+            persons = persons[keep]
+            if persons.shape[0] == 0:
+                out[b] = None
+                continue
+        persons = np.ascontiguousarray(persons, dtype=np.float64)
+        if fill_mean_:
+            fill_mean(persons)
+        if with_refine and persons[0, :, 2].sum() != 0:
+            with torch.cuda.stream(st):       # (its read-back waits for `stream` only)
+                refine(scoremaps[b], tags[b], persons)
+        out[b] = persons
+    if not adjustment or all(p is None for p in out):
+        return out
+    L = _lib.lib()
+    pend = []
+    with torch.cuda.stream(st):
+        d = _maps(scoremaps, "scoremaps", (4,))
+        B, J, H, W = d.shape
+        if len(out) != B:
+            raise ValueError(f"pemp_amd.pose: {len(out)} images of persons for {B} scoremaps")
+        for b, kp in enumerate(out):
+            if kp is None or kp.shape[0] == 0:
+                continue
+            if kp.shape[1] != J:
+                raise ValueError(f"pemp_amd.pose: keypoints have {kp.shape[1]} joints, det {J}")
+            _check_coords(kp, H, W, "adjust")
+            d_kp = torch.from_numpy(kp).pin_memory().to(dev, non_blocking=True)
+            _lib.check(L.pemp_pose_adjust(d[b].data_ptr(), J, H, W, d_kp.data_ptr(), kp.shape[0], _lib.stream(dev)))
+            h = torch.empty(kp.shape, dtype=torch.float64, pin_memory=True)
+            h.copy_(d_kp, non_blocking=True)
+            pend.append((b, h))
+        ev = torch.cuda.Event()
+        ev.record(st)
+    ev.synchronize()
+    for b, h in pend:
+        out[b][...] = h.numpy()
+    return out
 
 
 # ----------------------------------------------------------------------------------------------------

@@ -462,7 +462,7 @@ def test_feature_knn_graph_end_to_end():
 @pytest.mark.parametrize("aux", [0, 2])
 def test_node_block_split(aux):
     """A call over the library's per-call limit (E < 2^23, T N < 2^23) is cut into image blocks
-    (mpn/model.py::node_blocks); with the limit lowered, a 4-image batch runs as 3 blocks and its logits
+    (mpn/model.py::node_blocks); with the limit lowered to the largest image's edges, a 4-image batch runs in image blocks and its logits
     equal the oracle's within the bar and the one-call run's within the bar."""
     g = graph(4, 17, 96, 96, 3, seed=31)
     x, ea, ei, types = g[0], g[1], g[2], g[7][:, 2]
@@ -472,9 +472,11 @@ def test_node_block_split(aux):
     whole = run(model, x, ea, ei, types)
     per_image = torch.bincount(g[12]).tolist()
     edges = [n * (n - 1) for n in per_image]
-    model._edge_limit = max(edges[0] + edges[1], max(edges))   # images 0+1 fit one block, 2 and 3 alone
+    model._edge_limit = max(edges)             # no two images fit one call: at least 2 blocks, on image bounds
     from pemp_amd.mpn.model import node_blocks
-    assert len(node_blocks(ei, x.shape[0], model._edge_limit, 1 << 20)) == 3
+    blocks = node_blocks(ei, x.shape[0], model._edge_limit, 1 << 20)
+    bounds = set(torch.cumsum(torch.tensor(per_image), 0).tolist()) | {0}
+    assert len(blocks) >= 2 and all(n0 in bounds and n1 in bounds for n0, n1 in blocks)
     split = run(model, x, ea, ei, types)
     ref = restate.mpn_forward(sd, cfg, x, ea, ei, types)
     for k in range(3):

@@ -334,3 +334,45 @@ def test_bad_indices_raise():
             ppose.refine(s, s, kp)
         with pytest.raises(IndexError):
             ppose.adjust(kp, s)
+
+
+def test_group_persons_start_pipelined():
+    """group_persons_start: the GPU half queued for two batches before either host half runs (as the bench's
+    pipelined e2e step does) gives exactly group_persons' persons; finish_batch (fill_mean, refine, adjust with one
+    wait, on a side stream) equals finish_persons image by image."""
+    B, J, H, W = 3, 17, 96, 96
+    results = []
+    jobs, refs, maps = [], [], []
+    for seed in (41, 42):
+        hm = torch.from_numpy(syn.make_heatmaps(seed, B, J, H, W, persons=3)).to(DEV)
+        feats = torch.from_numpy(syn.closed_form((B, 128, H, W), 0.25)).to(DEV)
+        tags = torch.from_numpy(syn.closed_form((B, J, H, W, 1), 0.75)).to(DEV)
+        gc = pcfg.inference_gc_config("fully", 5, False)
+        out = pemp_amd.get_graph_constructor(gc, scoremaps=hm, features=feats, tagmaps=tags, joints_gt=None,
+                                             factor_list=None, masks=None, device=DEV, testing=True, heatmaps=None,
+                                             num_joints=J).construct_graph()
+        det, ei, bi, sc = out[7], out[2], out[12], out[11]
+        node_off = torch.searchsorted(bi, torch.arange(B + 1, device=DEV))
+        pid = (torch.arange(det.shape[0], device=DEV) - node_off[bi]) % 3
+        pe = torch.sigmoid(torch.where(pid[ei[0]] == pid[ei[1]], 2.5, -2.5))
+        pn = torch.full((det.shape[0],), 0.9, device=DEV)
+        pc = torch.eye(J, device=DEV)[det[:, 2]]
+        args = (det, pn, ei, pe, 0.1, pc, "GAEC", J)
+        refs.append(ppose.group_persons(*args, batch_index=bi, score_map_scores=sc, num_images=B))
+        jobs.append(ppose.group_persons_start(*args, batch_index=bi, score_map_scores=sc, num_images=B))
+        maps.append((hm, tags))
+    side = torch.cuda.Stream(DEV)
+    side.wait_stream(torch.cuda.current_stream(DEV))
+    for job, ref, (hm, tags) in zip(jobs, refs, maps):
+        got = job.result()
+        assert len(got) == B and sum(p is not None for p in got) > 0
+        for a, b in zip(got, ref):
+            assert (a is None) == (b is None)
+            if a is not None:
+                np.testing.assert_array_equal(a, b)
+        fin = ppose.finish_batch(got, hm, tags, adjustment=True, with_refine=True, stream=side)
+        for b, p in enumerate(ref):
+            one = ppose.finish_persons(None if p is None else p.copy(), hm[b], tags[b], True, True)
+            assert (one is None) == (fin[b] is None)
+            if one is not None:
+                np.testing.assert_array_equal(fin[b], one)
