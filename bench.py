@@ -340,7 +340,7 @@ def cpu_baseline(wl, gc, model, hm, feats, tags, budget_s):
                       f"(oracle/restate.py, torch CPU fp32, torch.set_num_threads(every CPU this process may use: "
                       f"os.cpu_count() {os.cpu_count()} limited by affinity and cgroup quota = {cores})); "
                       f"value = 1 / ({'frontend + ' if front_stage else ''}construct_graph + mpn_forward)",
-            "host_cpus": all_cores, "affinity_cpus": len(os.sched_getaffinity(0)), "cpu_model": _cpu_model()}
+            "host_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)), "cpu_model": _cpu_model()}
 
 
 def usable_cpus():

@@ -23,7 +23,11 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <map>
+#include <mutex>
 #include <queue>
 #include <thread>
 #include <vector>
@@ -198,10 +202,17 @@ struct GaecEdge16 {
 
 void gaec_dense(size_t n, const std::vector<size_t>& ea, const std::vector<size_t>& eb,
                 const std::vector<double>& ew, std::vector<size_t>& root) {
-  std::vector<double> wt(n * n, 0.0);
-  std::vector<uint32_t> ed(n * n, 0);
-  std::vector<uint8_t> ex(n * n, 0);
-  std::vector<uint32_t> deg(n, 0);
+  // per-thread buffers, reused across images and calls (fresh multi-100 KB blocks are mmap'ed, and their page
+  // faults serialise threads that cluster in parallel)
+  static thread_local std::vector<double> wt;
+  static thread_local std::vector<uint32_t> ed;
+  static thread_local std::vector<uint8_t> ex;
+  static thread_local std::vector<uint32_t> deg;
+  static thread_local std::vector<GaecEdge16> qstore;
+  wt.assign(n * n, 0.0);
+  ed.assign(n * n, 0);
+  ex.assign(n * n, 0);
+  deg.assign(n, 0);
   auto link = [&](size_t a, size_t b) {
     if (!ex[a * n + b]) {
       ex[a * n + b] = ex[b * n + a] = 1;
@@ -210,7 +221,7 @@ void gaec_dense(size_t n, const std::vector<size_t>& ea, const std::vector<size_
     }
   };
   // the queue's vector reserved up front (initial edges + one push per neighbour per contraction bound)
-  std::vector<GaecEdge16> qstore;
+  qstore.clear();
   qstore.reserve(ea.size() + n * 8 + 64);
   std::priority_queue<GaecEdge16> q(std::less<GaecEdge16>(), std::move(qstore));
   for (size_t i = 0; i < ea.size(); ++i) {
@@ -266,6 +277,73 @@ void gaec_dense(size_t n, const std::vector<size_t>& ea, const std::vector<size_
   }
   root.resize(n);
   for (size_t v = 0; v < n; ++v) root[v] = find(v);
+  // keep the heap's capacity for the next image (priority_queue exposes its container only to derived classes)
+  struct Drain : std::priority_queue<GaecEdge16> {
+    static std::vector<GaecEdge16>& c_of(std::priority_queue<GaecEdge16>& pq) { return pq.*(&Drain::c); }
+  };
+  qstore = std::move(Drain::c_of(q));
+}
+
+// Persistent host workers for the per-image loops (one image per task): a call hands out tasks through an atomic
+// counter and the calling thread works too, so no thread is created per call (std::thread creation and the first
+// touch of each new thread's stack cost more than a 153-node GAEC). Calls are serialised by the pool's mutex.
+class HostPool {
+ public:
+  void run(int tasks, int threads, const std::function<void(int)>& fn) {
+    threads = std::max(1, std::min(threads, tasks));
+    if (threads == 1) {
+      for (int i = 0; i < tasks; ++i) fn(i);
+      return;
+    }
+    std::lock_guard<std::mutex> call(call_mu_);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      while ((int)workers_.size() < threads - 1) workers_.emplace_back([this, id = (int)workers_.size()] { loop(id); });
+      fn_ = &fn;
+      tasks_ = tasks;
+      next_.store(0);
+      active_ = threads - 1;
+      running_ = threads - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    drain(fn);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [this] { return running_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void drain(const std::function<void(int)>& fn) {
+    for (int i = next_.fetch_add(1); i < tasks_; i = next_.fetch_add(1)) fn(i);
+  }
+  void loop(int id) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int)>* fn;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen && id < active_; });
+        seen = gen_;
+        fn = fn_;
+      }
+      drain(*fn);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--running_ == 0) done_cv_.notify_one();
+    }
+  }
+  std::mutex call_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<std::thread> workers_;   // never joined: the pool lives as long as the process
+  const std::function<void(int)>* fn_ = nullptr;
+  std::atomic<int> next_{0};
+  int tasks_ = 0, active_ = 0, running_ = 0;
+  uint64_t gen_ = 0;
+};
+
+HostPool& host_pool() {
+  static HostPool* p = new HostPool();   // (leaked on purpose: no join at exit)
+  return *p;
 }
 
 void union_join(std::vector<size_t>& parent, size_t a, size_t b) {
@@ -374,17 +452,7 @@ extern "C" int pemp_pose_cluster(int B, const int64_t* node_off, const int64_t* 
     }
     n_comp[img] = next;
   };
-  const int nt = std::max(1, std::min(n_threads, B));
-  if (nt == 1) {
-    for (int img = 0; img < B; ++img) run(img);
-  } else {
-    std::vector<std::thread> pool;
-    for (int t = 0; t < nt; ++t)
-      pool.emplace_back([&, t] {
-        for (int img = t; img < B; img += nt) run(img);
-      });
-    for (auto& th : pool) th.join();
-  }
+  host_pool().run(B, n_threads, run);
   return PEMP_OK;
 }
 

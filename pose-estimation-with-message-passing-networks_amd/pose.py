@@ -362,12 +362,12 @@ def finish_persons(persons, scoremaps, tags, adjustment, with_refine, with_filte
 def finish_batch(per_image, scoremaps, tags, adjustment=True, with_refine=False, with_filter=False,
                  fill_mean_=True, stream=None):
     """finish_persons over a batch (``pred_to_ann``, ``Utils.py:1460-1478``, once per image): per_image as
-    group_persons returns it, scoremaps [B, J, H, W] / tags [B, J, H, W(, F)] device tensors. The adjust
-    kernels of every image are queued together on `stream` (default: the current stream) and waited for once,
-    by an event after one pinned copy each, instead of one stream synchronisation per image."""
+    group_persons returns it, scoremaps [B, J, H, W] / tags [B, J, H, W(, F)] device tensors. The filter and
+    fill_mean run on the host; then every image's keypoints go up in one pinned copy, the refine and adjust
+    kernels of all images are queued on `stream` (default: the current stream; one refine workspace, reused in
+    stream order), and one copy back plus one event wait replace the two synchronisations per image of
+    finish_persons. Same results as finish_persons image by image."""
     out = [None if p is None else p for p in per_image]
-    dev = scoremaps.device
-    st = stream if stream is not None else torch.cuda.current_stream(dev)
     for b, persons in enumerate(out):
         if persons is None:
             continue
@@ -380,35 +380,53 @@ def finish_batch(per_image, scoremaps, tags, adjustment=True, with_refine=False,
         persons = np.ascontiguousarray(persons, dtype=np.float64)
         if fill_mean_:
             fill_mean(persons)
-        if with_refine and persons[0, :, 2].sum() != 0:
-            with torch.cuda.stream(st):       # (its read-back waits for `stream` only)
-                refine(scoremaps[b], tags[b], persons)
         out[b] = persons
-    if not adjustment or all(p is None for p in out):
+    live = [b for b, kp in enumerate(out) if kp is not None and kp.shape[0] > 0]
+    do_ref = [with_refine and out[b][0, :, 2].sum() != 0 for b in live]
+    if not live or not (adjustment or any(do_ref)):
         return out
     L = _lib.lib()
-    pend = []
+    dev = scoremaps.device
+    st = stream if stream is not None else torch.cuda.current_stream(dev)
+    d = _maps(scoremaps, "scoremaps", (4,))
+    B, J, H, W = d.shape
+    if len(out) != B:
+        raise ValueError(f"pemp_amd.pose: {len(out)} images of persons for {B} scoremaps")
+    tg = None
+    if any(do_ref):
+        tg = _maps(tags, "tags", (4, 5))
+        if tg.dim() == 4:
+            tg = tg[..., None]
+        if tuple(tg.shape[:4]) != (B, J, H, W):
+            raise ValueError(f"pemp_amd.pose: tags {tuple(tg.shape)} do not match scoremaps {tuple(d.shape)}")
+    F = tg.shape[4] if tg is not None else 1
+    for b in live:
+        if out[b].shape[1] != J:
+            raise ValueError(f"pemp_amd.pose: keypoints have {out[b].shape[1]} joints, maps {J}")
+        _check_coords(out[b], H, W, "refine" if with_refine else "adjust")
+    starts = np.cumsum([0] + [out[b].shape[0] for b in live])
+    host = torch.from_numpy(np.concatenate([out[b] for b in live])).pin_memory()
     with torch.cuda.stream(st):
-        d = _maps(scoremaps, "scoremaps", (4,))
-        B, J, H, W = d.shape
-        if len(out) != B:
-            raise ValueError(f"pemp_amd.pose: {len(out)} images of persons for {B} scoremaps")
-        for b, kp in enumerate(out):
-            if kp is None or kp.shape[0] == 0:
-                continue
-            if kp.shape[1] != J:
-                raise ValueError(f"pemp_amd.pose: keypoints have {kp.shape[1]} joints, det {J}")
-            _check_coords(kp, H, W, "adjust")
-            d_kp = torch.from_numpy(kp).pin_memory().to(dev, non_blocking=True)
-            _lib.check(L.pemp_pose_adjust(d[b].data_ptr(), J, H, W, d_kp.data_ptr(), kp.shape[0], _lib.stream(dev)))
-            h = torch.empty(kp.shape, dtype=torch.float64, pin_memory=True)
-            h.copy_(d_kp, non_blocking=True)
-            pend.append((b, h))
+        kp = host.to(dev, non_blocking=True)
+        if any(do_ref):
+            pmax = max(out[b].shape[0] for b, r in zip(live, do_ref) if r)
+            ws = torch.empty(L.pemp_pose_refine_workspace_size(pmax, J, H, W, F), dtype=torch.uint8, device=dev)
+        for k, b in enumerate(live):
+            P = int(starts[k + 1] - starts[k])
+            kp_b = kp[starts[k]:starts[k + 1]]
+            if do_ref[k]:
+                _lib.check(L.pemp_pose_refine(d[b].data_ptr(), tg[b].data_ptr(), J, H, W, F, kp_b.data_ptr(), P,
+                                              ws.data_ptr(), ws.numel(), _lib.stream(dev)))
+            if adjustment:
+                _lib.check(L.pemp_pose_adjust(d[b].data_ptr(), J, H, W, kp_b.data_ptr(), P, _lib.stream(dev)))
+        back = torch.empty(host.shape, dtype=torch.float64, pin_memory=True)
+        back.copy_(kp, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(st)
     ev.synchronize()
-    for b, h in pend:
-        out[b][...] = h.numpy()
+    res = back.numpy()
+    for k, b in enumerate(live):
+        out[b][...] = res[starts[k]:starts[k + 1]]
     return out
 
 
