@@ -106,6 +106,7 @@ struct DetectWs {
   cmask_t* cbits;    // threshold bits per (unit, lane): bit j <-> row y0 + j of the lane's column
   // per plane (image, type): sorted top-k list, threshold-set counts per band and in-plane offsets
   float* ptop_sc; int *ptop_i, *ptop_bit, *pn_top, *pn_thr, *pstrip, *pstrip_off;
+  int* pflag;        // per plane: 1 once its counts are published (plane_emit_kernel; zeroed by stage 1)
 };
 
 static DetectWs carve(void* base, const DetectGeom& g, size_t* bytes) {
@@ -127,6 +128,7 @@ static DetectWs carve(void* base, const DetectGeom& g, size_t* bytes) {
   w.pn_thr = c.take<int>(np);
   w.pstrip = c.take<int>(np * g.S);
   w.pstrip_off = c.take<int>(np * g.S);
+  w.pflag = c.take<int>(np);
   if (bytes) *bytes = c.used;
   return w;
 }
@@ -460,9 +462,12 @@ template <int P, int MODE, bool MASKED, int PROJ>   // PROJ: 0 dense maps, 1 pro
 __global__ __launch_bounds__(NT1) void nms_strips_kernel(
     const float* __restrict__ s, const float* __restrict__ masks, DetectGeom g, float thr, int use_thr,
     float* __restrict__ cand_v, int* __restrict__ cand_i, float* __restrict__ neg_v, int* __restrict__ neg_i,
-    int* __restrict__ tile_count, int* __restrict__ tile_nonneg, cmask_t* __restrict__ cbits, ProjArgs pj) {
+    int* __restrict__ tile_count, int* __restrict__ tile_nonneg, cmask_t* __restrict__ cbits, ProjArgs pj,
+    int* __restrict__ pflag) {
   const int lane = threadIdx.x & 63;
   const int total = g.B * g.J * g.units;
+  if (blockIdx.x == 0)   // the fused select + emit stage's publish flags, for this detection
+    for (int i = threadIdx.x; i < g.B * g.J; i += NT1) pflag[i] = 0;
   const int H = g.H, W = g.W, K = g.K;
   // Grid-stride over windows of G x 4 consecutive units; inside a window the units are dealt by XCD
   // (blocks b and b + 8 share one): XCD x takes the x-th eighth of the window, a contiguous run of bands
@@ -906,6 +911,279 @@ __global__ __launch_bounds__(256) void emit_kernel(const float* __restrict__ s, 
   }
 }
 
+constexpr int SEL_GATHER = 2048;   // candidates of live units gathered into LDS by the fused stage
+
+// Stages 2a + 2b in one launch (PEMP_DETECT_FUSED, the default): one workgroup per plane runs plane_top_kernel's
+// selection, keeps its top-k list and band counts / offsets in LDS, publishes the plane's two counts (release store
+// of a per-plane flag, agent scope), waits until every plane of its image has published (acquire polls by wave 0;
+// the planes of an image are consecutive workgroups, dispatched together) and then emits as emit_kernel does. One
+// launch instead of two, and no re-read of the plane's own results.
+template <int KMAX>
+__global__ __launch_bounds__(256) void plane_emit_kernel(const float* __restrict__ s, const float* __restrict__ masks,
+                                                         DetectGeom g, float thr, int use_thr,
+                                                         const cmask_t* __restrict__ cbits, DetectWs w,
+                                                         int64_t* __restrict__ det, float* __restrict__ scores,
+                                                         int* __restrict__ n_det, int cap, int* __restrict__ n_host,
+                                                         ProjArgs pj) {
+  __shared__ float lv[4][KMAX];
+  __shared__ int li[4][KMAX];
+  __shared__ float top_v[2 * KMAX], top_sc[KMAX];
+  __shared__ int top_i[2 * KMAX], top_bit[KMAX], sh[8];
+  __shared__ int band_n[MAXB], band_off[MAXB];
+  __shared__ unsigned band_nz[MAXB][2];      // non-empty strips of each band (bit = strip, nsx <= 64)
+  const int pl = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int J = g.J, b = pl / J, t = pl - b * J;
+  const int K = g.K, H = g.H, W = g.W, S = g.S, nl = g.units;
+  const size_t pt = (size_t)pl * nl;
+  // ---- selection (plane_top_kernel) ----
+  constexpr int UPT = 4;
+  int tc[UPT], tn[UPT];
+#pragma unroll
+  for (int k = 0; k < UPT; ++k) {
+    const int c = min((int)threadIdx.x + 256 * k, nl - 1);
+    tc[k] = w.tile_count[pt + c];
+    tn[k] = w.tile_nonneg[pt + c];
+  }
+  // MODE_POS: most units of a plane hold no positive value and wrote sentinel lists (-inf first); only the live
+  // units' candidates are gathered into LDS and merged (a handful of units per plane instead of all of them)
+  __shared__ float gv[SEL_GATHER];
+  __shared__ int gi[SEL_GATHER], glive[4];
+  int n;
+  {
+    if (threadIdx.x < 4) glive[threadIdx.x] = 0;
+    __syncthreads();
+    int live_total = 0;
+    if (use_thr) {
+      // (live units are counted per 256-unit chunk; their lists are appended in unit order)
+      for (int c0 = 0; c0 < nl; c0 += 256) {
+        const int u = c0 + threadIdx.x;
+        const bool live = u < nl && w.cand_v[(pt + u) * K] != -INFINITY;
+        const unsigned long long bal = __ballot(live);
+        if (lane == 0) glive[wave] = __popcll(bal);
+        __syncthreads();
+        int before = live_total;
+        for (int w2 = 0; w2 < wave; ++w2) before += glive[w2];
+        const int chunk = glive[0] + glive[1] + glive[2] + glive[3];
+        if (live) {
+          const int slot = before + (int)__popcll(bal & ((1ull << lane) - 1ull));
+          if ((slot + 1) * K <= SEL_GATHER)
+            for (int k = 0; k < K; ++k) {
+              gv[slot * K + k] = w.cand_v[(pt + u) * K + k];
+              gi[slot * K + k] = w.cand_i[(pt + u) * K + k];
+            }
+        }
+        live_total += chunk;
+        __syncthreads();
+      }
+    }
+    if (use_thr && live_total * K <= SEL_GATHER)
+      n = block_topk<KMAX>(gv, gi, live_total * K, K, top_v, top_i, lv, li, &sh[0]);
+    else
+      n = block_topk<KMAX>(w.cand_v + pt * K, w.cand_i + pt * K, nl * K, K, top_v, top_i, lv, li, &sh[0]);
+  }
+  if (use_thr) {
+    int nn = 0;
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) nn += (int)threadIdx.x + 256 * k < nl ? tn[k] : 0;
+    for (int c = threadIdx.x + 256 * UPT; c < nl; c += 256) nn += w.tile_nonneg[pt + c];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) nn += __shfl_xor(nn, off);
+    if (lane == 0) sh[4 + wave] = nn;
+    __syncthreads();
+    nn = sh[4] + sh[5] + sh[6] + sh[7];
+    if (nn < K)
+      n += block_topk<KMAX>(w.neg_v + pt * K, w.neg_i + pt * K, nl * K, K - nn, top_v + n, top_i + n, lv, li, &sh[1]);
+  }
+  if (threadIdx.x == 0) {
+    int m = 0;
+    for (int q = 0; q < n; ++q) {
+      const float v = top_v[q];
+      const float sc = use_thr ? v : v + 1e-10f;
+      if (sc != 0.0f && top_i[q] != INV) { top_v[m] = v; top_sc[m] = sc; top_i[m] = top_i[q]; ++m; }
+    }
+    for (int a2 = 1; a2 < m; ++a2) {            // insertion sort by flat index
+      const float v = top_v[a2], sc = top_sc[a2];
+      const int i = top_i[a2];
+      int c = a2 - 1;
+      while (c >= 0 && top_i[c] > i) { top_v[c + 1] = top_v[c]; top_sc[c + 1] = top_sc[c]; top_i[c + 1] = top_i[c]; --c; }
+      top_v[c + 1] = v; top_sc[c + 1] = sc; top_i[c + 1] = i;
+    }
+    for (int q = 0; q < m; ++q) {
+      top_bit[q] = use_thr && !(top_v[q] < thr) && top_v[q] != 0.0f;
+      w.ptop_i[(size_t)pl * KCAP + q] = top_i[q];
+      w.ptop_sc[(size_t)pl * KCAP + q] = top_sc[q];
+      w.ptop_bit[(size_t)pl * KCAP + q] = top_bit[q];
+    }
+    w.pn_top[pl] = m;
+    sh[0] = m;
+  }
+  for (int st = threadIdx.x; st < S; st += 256) {
+    band_n[st] = 0;
+    band_nz[st][0] = 0u;
+    band_nz[st][1] = 0u;
+  }
+  __syncthreads();
+  const int ntop = sh[0];
+  if (use_thr) {                                // per-band threshold counts and non-empty strips
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+      const int idx = threadIdx.x + 256 * k;
+      if (idx < nl && tc[k]) {
+        const int band = idx / g.nsx, sx = idx - band * g.nsx;
+        atomicAdd(&band_n[band], tc[k]);
+        atomicOr(&band_nz[band][sx >> 5], 1u << (sx & 31));
+      }
+    }
+    for (int idx = threadIdx.x + 256 * UPT; idx < nl; idx += 256) {
+      const int v = w.tile_count[pt + idx];
+      if (v) {
+        const int band = idx / g.nsx, sx = idx - band * g.nsx;
+        atomicAdd(&band_n[band], v);
+        atomicOr(&band_nz[band][sx >> 5], 1u << (sx & 31));
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 0; q < ntop; ++q)
+      if (top_bit[q]) band_n[top_i[q] / W / SR] -= 1;
+  }
+  __syncthreads();
+  if (wave == 0) {                              // in-plane exclusive scan over bands
+    int carry = 0;
+    for (int c0 = 0; c0 < S; c0 += 64) {
+      const int st = c0 + lane;
+      const int v = st < S ? band_n[st] : 0;
+      int x = v;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(x, off);
+        if (lane >= off) x += o;
+      }
+      if (st < S) {
+        band_off[st] = carry + x - v;
+        w.pstrip[(size_t)pl * S + st] = v;
+        w.pstrip_off[(size_t)pl * S + st] = carry + x - v;
+      }
+      carry += __shfl(x, 63);
+    }
+    if (lane == 0) {
+      w.pn_thr[pl] = carry;
+      // publish: the two counts above, then the flag (release: they are visible to whoever acquires it)
+      __hip_atomic_store(&w.pflag[pl], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // ---- the image's per-type counts: wait for every plane of the image (acquire polls) ----
+    for (;;) {
+      const int f = lane < J ? __hip_atomic_load(&w.pflag[b * J + lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : 1;
+      if (__all(f == 1)) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    const int nt = lane < J ? __hip_atomic_load(&w.pn_top[b * J + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    const int nh = lane < J ? __hip_atomic_load(&w.pn_thr[b * J + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    int top_before = lane < t ? nt : 0, thr_before = lane < t ? nh : 0, top_all = nt, thr_all = nh;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      top_before += __shfl_xor(top_before, off); thr_before += __shfl_xor(thr_before, off);
+      top_all += __shfl_xor(top_all, off); thr_all += __shfl_xor(thr_all, off);
+    }
+    if (lane == 0) {
+      sh[1] = top_before; sh[2] = top_all + thr_before;
+      if (t == 0) {
+        n_det[b] = top_all + thr_all;
+        if (n_host) __hip_atomic_store(&n_host[b], top_all + thr_all, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+  __syncthreads();
+  // ---- emission (emit_kernel) ----
+  const int top_base = sh[1], thr_base = sh[2];
+  int64_t* dout = det + (size_t)b * cap * 3;
+  float* sout = scores + (size_t)b * cap;
+  if ((int)threadIdx.x < ntop) {
+    const int pos = top_base + threadIdx.x;
+    if (pos < cap) {
+      const int idx = top_i[threadIdx.x];
+      dout[pos * 3 + 0] = idx % W;
+      dout[pos * 3 + 1] = idx / W;
+      dout[pos * 3 + 2] = t;
+      sout[pos] = top_sc[threadIdx.x];
+    }
+  }
+  __shared__ cmask_t cm_sh[4][64][64];
+  __shared__ int nz_sh[4][64];
+  int kb = 0;
+  for (int st = 0; st < S; ++st) {
+    if (band_n[st] == 0) continue;                       // uniform
+    if ((kb++ & 3) != wave) continue;
+    const int ry0 = st * SR, rows = min(SR, H - ry0);
+    int pos = thr_base + band_off[st];
+    const float* plane = s + (size_t)pl * H * W;
+    const size_t u0 = ((size_t)pl * g.nb + st) * g.nsx;
+    const unsigned long long nzm = (unsigned long long)band_nz[st][0] | ((unsigned long long)band_nz[st][1] << 32);
+    int nnz = 0;
+    unsigned rows_any = 0;
+    unsigned cms[4];
+    {
+      unsigned long long m = nzm;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int sx = m ? __builtin_ctzll(m) : 0;
+        cms[k] = cbits[(u0 + sx) * 64 + lane];
+        if (m) m &= m - 1;
+      }
+    }
+    for (unsigned long long m = nzm; m; m &= m - 1) {
+      const int sx = __builtin_ctzll(m);
+      const unsigned cm = nnz < 4 ? cms[nnz & 3] : cbits[(u0 + sx) * 64 + lane];
+      cm_sh[wave][nnz][lane] = (cmask_t)cm;
+      if (lane == 0) nz_sh[wave][nnz] = sx;
+      unsigned ra = cm;
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) ra |= __shfl_xor(ra, off);
+      rows_any |= ra;
+      ++nnz;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (unsigned rm = rows_any & (rows >= 32 ? ~0u : (1u << rows) - 1u); rm; rm &= rm - 1) {
+      const int j = __builtin_ctz(rm), yy = ry0 + j;
+      for (int k = 0; k < nnz; ++k) {
+        const int sx = nz_sh[wave][k];
+        unsigned long long word = __ballot((cm_sh[wave][k][lane] >> j) & 1u);
+        if (!word) continue;
+        for (int q = 0; q < ntop; ++q) {               // already listed as a top-k detection
+          if (!top_bit[q]) continue;
+          const int idx = top_i[q], ty = idx / W, tx = idx - ty * W, tsx = tx / g.sc;
+          if (ty == yy && tsx == sx) word &= ~(1ull << (tx - tsx * g.sc + g.p));
+        }
+        if ((word >> lane) & 1ull) {
+          const int xx = sx * g.sc - g.p + lane;
+          const int o = pos + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(word >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((unsigned)word, 0u));
+          if (o < cap) {
+            const float sv = pj.S ? proj_pixel(pj, b, t, yy, xx, H, W) : plane[(size_t)yy * W + xx];
+            float jm = 1.0f;
+            if (masks) jm = jm * masks[((size_t)b * H + yy) * W + xx];
+            dout[o * 3 + 0] = xx;
+            dout[o * 3 + 1] = yy;
+            dout[o * 3 + 2] = t;
+            sout[o] = sv * jm;
+          }
+        }
+        pos += __popcll(word);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+#ifndef PEMP_DETECT_FUSED
+#define PEMP_DETECT_FUSED 1
+#endif
+
 template <int P, int MODE, int PROJ>
 static void launch_nms(const float* s, const float* masks, const DetectGeom& g, float thr, int use_thr,
                        const DetectWs& w, const ProjArgs& pj, hipStream_t st) {
@@ -922,7 +1200,7 @@ static void launch_nms(const float* s, const float* masks, const DetectGeom& g, 
       per_cu = std::min(per_cu, occ);
     const int grid = want < per_cu * num_cus() ? want : per_cu * num_cus();
     hipLaunchKernelGGL(kern, dim3(grid), dim3(NT1), 0, st, s, masks, g, thr, use_thr, w.cand_v, w.cand_i, w.neg_v,
-                       w.neg_i, w.tile_count, w.tile_nonneg, w.cbits, pj);
+                       w.neg_i, w.tile_count, w.tile_nonneg, w.cbits, pj, w.pflag);
   };
   if (masks) launch(nms_strips_kernel<P, MODE, true, PROJ>);
   else launch(nms_strips_kernel<P, MODE, false, PROJ>);
@@ -981,7 +1259,13 @@ static int launch_detect(const float* s, const float* masks, const DetectGeom& g
     }
     PEMP_LAUNCH_CHECK();
   }
-  if (stages & PEMP_DETECT_SELECT) {
+  if ((stages & PEMP_DETECT_SELECT) && PEMP_DETECT_FUSED) {
+    if (!(stages & PEMP_DETECT_NMS)) PEMP_HIP(hipMemsetAsync(w.pflag, 0, sizeof(int) * g.B * g.J, st));
+    ProfScope prof("detect_select_emit", st);
+    hipLaunchKernelGGL(plane_emit_kernel<KMAX>, dim3(g.B * g.J), dim3(256), 0, st, s, masks, g, thr, use_thr, w.cbits,
+                       w, det, scores, (int*)n_det, cap, (int*)n_host, pj);
+    PEMP_LAUNCH_CHECK();
+  } else if (stages & PEMP_DETECT_SELECT) {
     {
       ProfScope prof("detect_top", st);
       hipLaunchKernelGGL(plane_top_kernel<KMAX>, dim3(g.B * g.J), dim3(256), 0, st, g, thr, use_thr, w.cand_v,

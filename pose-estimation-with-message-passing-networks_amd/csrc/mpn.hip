@@ -2563,7 +2563,10 @@ struct NodeTableArgs {
   float* NT;
 };
 
-constexpr int TBL_TILES = 4;
+#ifndef PEMP_TBL_TILES
+#define PEMP_TBL_TILES 4
+#endif
+constexpr int TBL_TILES = PEMP_TBL_TILES;   // 16-node tiles per workgroup
 
 template <int PREC>
 __global__ __launch_bounds__(256) void node_table_kernel(NodeTableArgs a) {
@@ -2596,17 +2599,17 @@ __global__ __launch_bounds__(256) void node_table_kernel(NodeTableArgs a) {
   }
   const float4 bb = ld4(a.pre_b + 16 * obc + 4 * g);
   {
-  // X chunk -> LDS: 64 rows x 32 float4, 8 per thread
-    float4 t[8];
+  // X chunk -> LDS: 16 TBL_TILES rows x 32 float4, 2 TBL_TILES per thread
+    float4 t[2 * TBL_TILES];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < 2 * TBL_TILES; ++k) {
       const int idx = threadIdx.x + 256 * k, row = idx >> 5, c4 = (idx & 31) * 4;
       const int64_t nn = min(n0 + row, N - 1);
       t[k] = ld4(a.X + nn * 128 + c4);
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < 2 * TBL_TILES; ++k) {
       const int idx = threadIdx.x + 256 * k, row = idx >> 5, c4 = (idx & 31) * 4;
       *reinterpret_cast<float4*>(&xs[row * RS + c4]) = t[k];
     }
@@ -3034,6 +3037,88 @@ __global__ __launch_bounds__(256) void sym_place_kernel(int64_t N, int T, const 
   if (__ballot(bad) && lane == 0) atomicOr(err, 8);          // (x -> d) missing: not symmetric
 }
 
+// Symmetric prepare, step 2 (instead of the one-block mpn_scan): one 1024-thread block per source type t. The
+// segment starts are seg[t N + d] = base_t + sum_{d' < d} cnt[t, d'] with base_t = the edges of all types before
+// t: every block sums every type's counts (one wave per type, T N ints, L2-resident) and scans its own type's N
+// counts, so the T scans run side by side instead of one block walking all T N counts. The last block also writes
+// seg[T N], the edge passes' type split (wg_start) and the contract flags (err[0..3]), as mpn_scan does.
+__global__ __launch_bounds__(1024) void sym_scan_kernel(const int* __restrict__ cnt, int64_t N, int T, int G,
+                                                        int* __restrict__ seg, int* __restrict__ wg_start,
+                                                        const int* __restrict__ flags, int64_t E_all,
+                                                        int* __restrict__ err) {
+  __shared__ int tb[MAXT + 1], gt[MAXT + 1], wsum[16], sh[4];
+  __shared__ int out[1024 * SCAN_SPT];
+  const int t = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool last = t == T - 1;
+  if (threadIdx.x < 4) sh[threadIdx.x] = 0;
+  // every type's total, one wave per type (wave w: types w, w + 16), all of a wave's loads in flight together
+  for (int tt = wave; tt < T; tt += 16) {
+    int v = 0;
+    const int* ct = cnt + (int64_t)tt * N;
+#pragma unroll 8
+    for (int64_t n = lane; n < N; n += 64) v += ct[n];
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) tb[tt] = v;
+  }
+  if (last) {                                          // the contract flags of every node (sym_rows_kernel)
+    int f = 0;
+    for (int64_t i = threadIdx.x; i < N; i += 1024) f |= flags[i];
+    if (f) atomicOr(&sh[0], f);
+  }
+  __syncthreads();
+  int base = 0;
+  for (int tt = 0; tt < t; ++tt) base += tb[tt];
+  // this type's segment starts: passes of 1024 x SCAN_SPT counts, carry across passes
+  int carry = base;
+  const int* c = cnt + (int64_t)t * N;
+  for (int64_t b0 = 0; b0 < N; b0 += 1024 * SCAN_SPT) {
+    const int64_t k0 = b0 + (int64_t)threadIdx.x * SCAN_SPT;
+    int v[SCAN_SPT];
+#pragma unroll
+    for (int j = 0; j < SCAN_SPT; ++j) v[j] = k0 + j < N ? c[k0 + j] : 0;
+    int local = 0;
+#pragma unroll
+    for (int j = 0; j < SCAN_SPT; ++j) local += v[j];
+    int x = local;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int o = __shfl_up(x, off);
+      if (lane >= off) x += o;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    int before = 0, all = 0;
+#pragma unroll
+    for (int w2 = 0; w2 < 16; ++w2) {
+      before += w2 < wave ? wsum[w2] : 0;
+      all += wsum[w2];
+    }
+    int run = carry + before + x - local;
+#pragma unroll
+    for (int j = 0; j < SCAN_SPT; ++j) { out[threadIdx.x * SCAN_SPT + j] = run; run += v[j]; }
+    carry += all;
+    __syncthreads();
+    const int64_t lim = N - b0 < 1024 * SCAN_SPT ? N - b0 : 1024 * SCAN_SPT;
+    for (int64_t k = threadIdx.x; k < lim; k += 1024) seg[(int64_t)t * N + b0 + k] = out[k];
+    __syncthreads();
+  }
+  if (!last) return;                                   // (block-uniform)
+  if (threadIdx.x == 0) {                              // type starts for the split; the total closes seg
+    int acc = 0;
+    for (int tt = 0; tt < T; ++tt) {
+      const int v = tb[tt];
+      tb[tt] = acc;
+      acc += v;
+    }
+    tb[T] = acc;
+    seg[(int64_t)T * N] = acc;
+    sh[1] = acc;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) err[threadIdx.x] = threadIdx.x ? 0 : (sh[0] | (sh[1] != E_all ? 4 : 0));
+  type_split(tb, sh[1], T, G, gt, wg_start);
+}
+
 static int launch_prepare(const pemp_mpn_desc* desc, const int64_t* edge_index, const int64_t* node_types, int64_t N,
                           int64_t E, const MpnWs& ws, hipStream_t st) {
   const int T = desc->num_types;
@@ -3075,8 +3160,8 @@ static int launch_prepare_sym(const pemp_mpn_desc* desc, const int64_t* edge_ind
   hipLaunchKernelGGL(sym_rows_kernel, dim3(g), dim3(256), 0, st, edge_index, node_types, tstride, N, E, T, ws.cnt, rows,
                      packed, flags);
   PEMP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(mpn_scan_kernel, dim3(1), dim3(1024), 0, st, ws.cnt, K, N, T, std::max(num_cus(), T), ws.seg,
-                     ws.wg_start, flags, N, E, ws.err);
+  hipLaunchKernelGGL(sym_scan_kernel, dim3((unsigned)T), dim3(1024), 0, st, ws.cnt, N, T, std::max(num_cus(), T), ws.seg,
+                     ws.wg_start, flags, E, ws.err);
   PEMP_LAUNCH_CHECK();
   hipLaunchKernelGGL(sym_place_kernel, dim3(g), dim3(256), 0, st, N, T, ws.seg, rows, packed, ws.s_src, ws.s_dst,
                      ws.s_orig, ws.err);
