@@ -36,6 +36,9 @@ namespace {
 #ifndef NMS_PER_CU
 #define NMS_PER_CU 5
 #endif
+#ifndef PEMP_DETECT_CLOCKS
+#define PEMP_DETECT_CLOCKS 0
+#endif   // diagnostics: phase clocks of the fused select + emit stage (printf)
 #ifndef NMS_CLAMPED_LOADS
 #define NMS_CLAMPED_LOADS 1
 #endif
@@ -106,7 +109,9 @@ struct DetectWs {
   cmask_t* cbits;    // threshold bits per (unit, lane): bit j <-> row y0 + j of the lane's column
   // per plane (image, type): sorted top-k list, threshold-set counts per band and in-plane offsets
   float* ptop_sc; int *ptop_i, *ptop_bit, *pn_top, *pn_thr, *pstrip, *pstrip_off;
-  int* pflag;        // per plane: 1 once its counts are published (plane_emit_kernel; zeroed by stage 1)
+  // per plane, the fused stage's publication: bit 63 set once published, bits 32..47 the top-k count, bits 0..31
+  // the threshold count -- one 64-bit word, so one relaxed device-scope atomic carries all of it (zeroed by stage 1)
+  unsigned long long* pflag;
 };
 
 static DetectWs carve(void* base, const DetectGeom& g, size_t* bytes) {
@@ -128,7 +133,7 @@ static DetectWs carve(void* base, const DetectGeom& g, size_t* bytes) {
   w.pn_thr = c.take<int>(np);
   w.pstrip = c.take<int>(np * g.S);
   w.pstrip_off = c.take<int>(np * g.S);
-  w.pflag = c.take<int>(np);
+  w.pflag = c.take<unsigned long long>(np);
   if (bytes) *bytes = c.used;
   return w;
 }
@@ -463,11 +468,11 @@ __global__ __launch_bounds__(NT1) void nms_strips_kernel(
     const float* __restrict__ s, const float* __restrict__ masks, DetectGeom g, float thr, int use_thr,
     float* __restrict__ cand_v, int* __restrict__ cand_i, float* __restrict__ neg_v, int* __restrict__ neg_i,
     int* __restrict__ tile_count, int* __restrict__ tile_nonneg, cmask_t* __restrict__ cbits, ProjArgs pj,
-    int* __restrict__ pflag) {
+    unsigned long long* __restrict__ pflag) {
   const int lane = threadIdx.x & 63;
   const int total = g.B * g.J * g.units;
   if (blockIdx.x == 0)   // the fused select + emit stage's publish flags, for this detection
-    for (int i = threadIdx.x; i < g.B * g.J; i += NT1) pflag[i] = 0;
+    for (int i = threadIdx.x; i < g.B * g.J; i += NT1) pflag[i] = 0ull;
   const int H = g.H, W = g.W, K = g.K;
   // Grid-stride over windows of G x 4 consecutive units; inside a window the units are dealt by XCD
   // (blocks b and b + 8 share one): XCD x takes the x-th eighth of the window, a contiguous run of bands
@@ -912,12 +917,20 @@ __global__ __launch_bounds__(256) void emit_kernel(const float* __restrict__ s, 
 }
 
 constexpr int SEL_GATHER = 2048;   // candidates of live units gathered into LDS by the fused stage
+constexpr int SEL_UNITS = 1024;    // units per plane the fused stage handles (4 per thread); more: the two kernels
 
-// Stages 2a + 2b in one launch (PEMP_DETECT_FUSED, the default): one workgroup per plane runs plane_top_kernel's
-// selection, keeps its top-k list and band counts / offsets in LDS, publishes the plane's two counts (release store
-// of a per-plane flag, agent scope), waits until every plane of its image has published (acquire polls by wave 0;
-// the planes of an image are consecutive workgroups, dispatched together) and then emits as emit_kernel does. One
-// launch instead of two, and no re-read of the plane's own results.
+// Stages 2a + 2b in one launch (PEMP_DETECT_FUSED, the default; planes of at most SEL_UNITS units): one workgroup per
+// plane. Every phase is shaped for latency (136 workgroups at C3, each a chain of dependent steps):
+//   A  one round trip: the plane's unit counts and the first candidate of every unit list (live = not a sentinel);
+//   B  band counts (LDS atomics), the non-negative total, and the live lists' candidates gathered into LDS (a second
+//      round trip; MODE_POS: a handful of units per plane instead of all of them);
+//   C  exact top-k from LDS (block_topk; the degenerate negative lists from global memory when needed);
+//   D  wave 0, one lane per entry: drop zero / empty entries, order by flat index (ranks by readlane, no serial
+//      loop), threshold bits, the band counts minus the entries already listed, the entries' emission positions;
+//   E  in-plane band scan, publish (release store of the plane's flag, agent scope), wait for the image's other
+//      planes (acquire polls; they are consecutive workgroups, dispatched together), output bases;
+//   F  emission as emit_kernel, except that a wave queues its detections (position, output slot) in LDS and then
+//      reads all their scores in one batch of loads.
 template <int KMAX>
 __global__ __launch_bounds__(256) void plane_emit_kernel(const float* __restrict__ s, const float* __restrict__ masks,
                                                          DetectGeom g, float thr, int use_thr,
@@ -925,97 +938,37 @@ __global__ __launch_bounds__(256) void plane_emit_kernel(const float* __restrict
                                                          int64_t* __restrict__ det, float* __restrict__ scores,
                                                          int* __restrict__ n_det, int cap, int* __restrict__ n_host,
                                                          ProjArgs pj) {
+  static_assert(2 * KMAX <= 64, "phase D: one lane per candidate");
   __shared__ float lv[4][KMAX];
   __shared__ int li[4][KMAX];
   __shared__ float top_v[2 * KMAX], top_sc[KMAX];
-  __shared__ int top_i[2 * KMAX], top_bit[KMAX], sh[8];
+  __shared__ int top_i[2 * KMAX], sh[8];
+  __shared__ int ex_y[KMAX], ex_sx[KMAX], ex_lane[KMAX];   // listed threshold entries: row, strip, lane (y -1: none)
   __shared__ int band_n[MAXB], band_off[MAXB];
   __shared__ unsigned band_nz[MAXB][2];      // non-empty strips of each band (bit = strip, nsx <= 64)
+  __shared__ float gv[SEL_GATHER];
+  __shared__ int gi[SEL_GATHER], glive[4][4], gnn[4];
   const int pl = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int J = g.J, b = pl / J, t = pl - b * J;
   const int K = g.K, H = g.H, W = g.W, S = g.S, nl = g.units;
   const size_t pt = (size_t)pl * nl;
-  // ---- selection (plane_top_kernel) ----
-  constexpr int UPT = 4;
+#if PEMP_DETECT_CLOCKS   // diagnostics: per-phase wall clock (100 MHz) of one plane per image, printed
+  long long clk[6];
+  clk[0] = wall_clock64();
+#define PEMP_CLK(i) clk[i] = wall_clock64()
+#else
+#define PEMP_CLK(i) (void)0
+#endif
+  // ---- A: counts and list heads of the plane's units (4 per thread) ----
+  constexpr int UPT = SEL_UNITS / 256;
   int tc[UPT], tn[UPT];
+  bool live[UPT];
 #pragma unroll
   for (int k = 0; k < UPT; ++k) {
     const int c = min((int)threadIdx.x + 256 * k, nl - 1);
     tc[k] = w.tile_count[pt + c];
     tn[k] = w.tile_nonneg[pt + c];
-  }
-  // MODE_POS: most units of a plane hold no positive value and wrote sentinel lists (-inf first); only the live
-  // units' candidates are gathered into LDS and merged (a handful of units per plane instead of all of them)
-  __shared__ float gv[SEL_GATHER];
-  __shared__ int gi[SEL_GATHER], glive[4];
-  int n;
-  {
-    if (threadIdx.x < 4) glive[threadIdx.x] = 0;
-    __syncthreads();
-    int live_total = 0;
-    if (use_thr) {
-      // (live units are counted per 256-unit chunk; their lists are appended in unit order)
-      for (int c0 = 0; c0 < nl; c0 += 256) {
-        const int u = c0 + threadIdx.x;
-        const bool live = u < nl && w.cand_v[(pt + u) * K] != -INFINITY;
-        const unsigned long long bal = __ballot(live);
-        if (lane == 0) glive[wave] = __popcll(bal);
-        __syncthreads();
-        int before = live_total;
-        for (int w2 = 0; w2 < wave; ++w2) before += glive[w2];
-        const int chunk = glive[0] + glive[1] + glive[2] + glive[3];
-        if (live) {
-          const int slot = before + (int)__popcll(bal & ((1ull << lane) - 1ull));
-          if ((slot + 1) * K <= SEL_GATHER)
-            for (int k = 0; k < K; ++k) {
-              gv[slot * K + k] = w.cand_v[(pt + u) * K + k];
-              gi[slot * K + k] = w.cand_i[(pt + u) * K + k];
-            }
-        }
-        live_total += chunk;
-        __syncthreads();
-      }
-    }
-    if (use_thr && live_total * K <= SEL_GATHER)
-      n = block_topk<KMAX>(gv, gi, live_total * K, K, top_v, top_i, lv, li, &sh[0]);
-    else
-      n = block_topk<KMAX>(w.cand_v + pt * K, w.cand_i + pt * K, nl * K, K, top_v, top_i, lv, li, &sh[0]);
-  }
-  if (use_thr) {
-    int nn = 0;
-#pragma unroll
-    for (int k = 0; k < UPT; ++k) nn += (int)threadIdx.x + 256 * k < nl ? tn[k] : 0;
-    for (int c = threadIdx.x + 256 * UPT; c < nl; c += 256) nn += w.tile_nonneg[pt + c];
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) nn += __shfl_xor(nn, off);
-    if (lane == 0) sh[4 + wave] = nn;
-    __syncthreads();
-    nn = sh[4] + sh[5] + sh[6] + sh[7];
-    if (nn < K)
-      n += block_topk<KMAX>(w.neg_v + pt * K, w.neg_i + pt * K, nl * K, K - nn, top_v + n, top_i + n, lv, li, &sh[1]);
-  }
-  if (threadIdx.x == 0) {
-    int m = 0;
-    for (int q = 0; q < n; ++q) {
-      const float v = top_v[q];
-      const float sc = use_thr ? v : v + 1e-10f;
-      if (sc != 0.0f && top_i[q] != INV) { top_v[m] = v; top_sc[m] = sc; top_i[m] = top_i[q]; ++m; }
-    }
-    for (int a2 = 1; a2 < m; ++a2) {            // insertion sort by flat index
-      const float v = top_v[a2], sc = top_sc[a2];
-      const int i = top_i[a2];
-      int c = a2 - 1;
-      while (c >= 0 && top_i[c] > i) { top_v[c + 1] = top_v[c]; top_sc[c + 1] = top_sc[c]; top_i[c + 1] = top_i[c]; --c; }
-      top_v[c + 1] = v; top_sc[c + 1] = sc; top_i[c + 1] = i;
-    }
-    for (int q = 0; q < m; ++q) {
-      top_bit[q] = use_thr && !(top_v[q] < thr) && top_v[q] != 0.0f;
-      w.ptop_i[(size_t)pl * KCAP + q] = top_i[q];
-      w.ptop_sc[(size_t)pl * KCAP + q] = top_sc[q];
-      w.ptop_bit[(size_t)pl * KCAP + q] = top_bit[q];
-    }
-    w.pn_top[pl] = m;
-    sh[0] = m;
+    live[k] = w.cand_v[(pt + c) * K] != -INFINITY;
   }
   for (int st = threadIdx.x; st < S; st += 256) {
     band_n[st] = 0;
@@ -1023,33 +976,104 @@ __global__ __launch_bounds__(256) void plane_emit_kernel(const float* __restrict
     band_nz[st][1] = 0u;
   }
   __syncthreads();
-  const int ntop = sh[0];
-  if (use_thr) {                                // per-band threshold counts and non-empty strips
+  // ---- B: band counts, non-negative total, live lists ----
+  int nn = 0;
 #pragma unroll
-    for (int k = 0; k < UPT; ++k) {
-      const int idx = threadIdx.x + 256 * k;
-      if (idx < nl && tc[k]) {
-        const int band = idx / g.nsx, sx = idx - band * g.nsx;
-        atomicAdd(&band_n[band], tc[k]);
-        atomicOr(&band_nz[band][sx >> 5], 1u << (sx & 31));
-      }
+  for (int k = 0; k < UPT; ++k) {
+    const int idx = threadIdx.x + 256 * k;
+    const bool in = idx < nl;
+    live[k] = live[k] && in && use_thr;
+    nn += in ? tn[k] : 0;
+    if (in && tc[k] && use_thr) {
+      const int band = fastdiv(idx, g.mn, g.ln), sx = idx - band * g.nsx;
+      atomicAdd(&band_n[band], tc[k]);
+      atomicOr(&band_nz[band][sx >> 5], 1u << (sx & 31));
     }
-    for (int idx = threadIdx.x + 256 * UPT; idx < nl; idx += 256) {
-      const int v = w.tile_count[pt + idx];
-      if (v) {
-        const int band = idx / g.nsx, sx = idx - band * g.nsx;
-        atomicAdd(&band_n[band], v);
-        atomicOr(&band_nz[band][sx >> 5], 1u << (sx & 31));
-      }
+    const unsigned long long bal = __ballot(live[k]);
+    if (lane == 0) glive[k][wave] = __popcll(bal);
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) nn += __shfl_xor(nn, off);
+  if (lane == 0) gnn[wave] = nn;
+  __syncthreads();
+  nn = gnn[0] + gnn[1] + gnn[2] + gnn[3];
+  int live_total = 0;
+#pragma unroll
+  for (int k = 0; k < UPT; ++k) {
+    int before = live_total;
+    for (int w2 = 0; w2 < wave; ++w2) before += glive[k][w2];
+    live_total += glive[k][0] + glive[k][1] + glive[k][2] + glive[k][3];
+    if (live[k]) {
+      const unsigned long long bal = __ballot(true);   // (the live lanes of this wave: exec mask)
+      const int slot = before + (int)__popcll(bal & ((1ull << lane) - 1ull));
+      const size_t src = (pt + threadIdx.x + 256 * k) * K;
+      if ((slot + 1) * K <= SEL_GATHER)
+        for (int q = 0; q < K; ++q) {
+          gv[slot * K + q] = w.cand_v[src + q];
+          gi[slot * K + q] = w.cand_i[src + q];
+        }
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int q = 0; q < ntop; ++q)
-      if (top_bit[q]) band_n[top_i[q] / W / SR] -= 1;
+  PEMP_CLK(1);
+  // ---- C: exact top-k ----
+  int n;
+  if (use_thr && live_total * K <= 256) {
+    // one gathered candidate per thread: its rank = the candidates better than it (distinct flat indices), the K
+    // best go to their rank's slot
+    const int nc = live_total * K;
+    const bool mine = (int)threadIdx.x < nc;
+    const float v = mine ? gv[threadIdx.x] : -INFINITY;
+    const int i = mine ? gi[threadIdx.x] : INV;
+    int rank = 0, valid = 0;
+    for (int r = 0; r < nc; ++r) {                 // (LDS broadcast reads)
+      const float vr = gv[r];
+      const int ir = gi[r];
+      rank += better(vr, ir, v, i) && ir != INV ? 1 : 0;
+    }
+    if (mine && i != INV && rank < K) { top_v[rank] = v; top_i[rank] = i; }
+    const unsigned long long bal = __ballot(mine && i != INV);
+    if (lane == 0) glive[0][wave] = __popcll(bal);
+    __syncthreads();
+    valid = glive[0][0] + glive[0][1] + glive[0][2] + glive[0][3];
+    n = min(K, valid);
+  } else if (use_thr && live_total * K <= SEL_GATHER)
+    n = block_topk<KMAX>(gv, gi, live_total * K, K, top_v, top_i, lv, li, &sh[0]);
+  else
+    n = block_topk<KMAX>(w.cand_v + pt * K, w.cand_i + pt * K, nl * K, K, top_v, top_i, lv, li, &sh[0]);
+  if (use_thr && nn < K)   // degenerate plane (fewer than K non-negative pixels): its top-k also holds negatives
+    n += block_topk<KMAX>(w.neg_v + pt * K, w.neg_i + pt * K, nl * K, K - nn, top_v + n, top_i + n, lv, li, &sh[1]);
+  PEMP_CLK(2);
+  // ---- D: the listed entries (wave 0, one lane per entry) ----
+  if (wave == 0) {
+    const bool has = lane < n;
+    const float v = has ? top_v[lane] : 0.0f;
+    const int i = has ? top_i[lane] : INV;
+    const float sc = use_thr ? v : v + 1e-10f;
+    const bool keep = has && sc != 0.0f && i != INV;
+    const unsigned long long km = __ballot(keep);
+    int rank = 0;                                  // position in flat-index order among the kept entries
+    for (int r = 0; r < n; ++r) {                  // (n uniform)
+      const int ir = __builtin_amdgcn_readlane(i, r);
+      rank += ((km >> r) & 1ull) && ir < i ? 1 : 0;
+    }
+    if (keep) {
+      const bool bit = use_thr && !(v < thr) && v != 0.0f;
+      const int ty = i / W, tx = i - ty * W, tsx = tx / g.sc;
+      top_i[KMAX + rank] = i;                      // (upper half: the lower one may still be read by other lanes)
+      top_sc[rank] = sc;
+      ex_y[rank] = bit ? ty : -1;
+      ex_sx[rank] = tsx;
+      ex_lane[rank] = tx - tsx * g.sc + g.p;
+      if (bit) atomicSub(&band_n[ty / SR], 1);     // already listed as a top-k detection
+    }
+    if (lane == 0) sh[4] = __popcll(km);
   }
   __syncthreads();
-  if (wave == 0) {                              // in-plane exclusive scan over bands
+  const int ntop = sh[4];
+  PEMP_CLK(3);
+  // ---- E: band offsets, publish, the image's per-type counts ----
+  if (wave == 0) {
     int carry = 0;
     for (int c0 = 0; c0 < S; c0 += 64) {
       const int st = c0 + lane;
@@ -1060,26 +1084,22 @@ __global__ __launch_bounds__(256) void plane_emit_kernel(const float* __restrict
         const int o = __shfl_up(x, off);
         if (lane >= off) x += o;
       }
-      if (st < S) {
-        band_off[st] = carry + x - v;
-        w.pstrip[(size_t)pl * S + st] = v;
-        w.pstrip_off[(size_t)pl * S + st] = carry + x - v;
-      }
+      if (st < S) band_off[st] = carry + x - v;
       carry += __shfl(x, 63);
     }
-    if (lane == 0) {
-      w.pn_thr[pl] = carry;
-      // publish: the two counts above, then the flag (release: they are visible to whoever acquires it)
-      __hip_atomic_store(&w.pflag[pl], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // ---- the image's per-type counts: wait for every plane of the image (acquire polls) ----
+    // publish both counts and the flag as one word: a relaxed device-scope atomic, no release / acquire fences
+    // (which would write back / invalidate the whole L2 of this XCD)
+    if (lane == 0)
+      __hip_atomic_store(&w.pflag[pl], (1ull << 63) | ((unsigned long long)ntop << 32) | (unsigned)carry,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long word = 1ull << 63;
     for (;;) {
-      const int f = lane < J ? __hip_atomic_load(&w.pflag[b * J + lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : 1;
-      if (__all(f == 1)) break;
+      if (lane < J) word = __hip_atomic_load(&w.pflag[b * J + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__all(word >> 63)) break;
       __builtin_amdgcn_s_sleep(1);
     }
-    const int nt = lane < J ? __hip_atomic_load(&w.pn_top[b * J + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-    const int nh = lane < J ? __hip_atomic_load(&w.pn_thr[b * J + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    const int nt = lane < J ? (int)((word >> 32) & 0xffff) : 0;
+    const int nh = lane < J ? (int)(word & 0xffffffffu) : 0;
     int top_before = lane < t ? nt : 0, thr_before = lane < t ? nh : 0, top_all = nt, thr_all = nh;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
@@ -1087,7 +1107,7 @@ __global__ __launch_bounds__(256) void plane_emit_kernel(const float* __restrict
       top_all += __shfl_xor(top_all, off); thr_all += __shfl_xor(thr_all, off);
     }
     if (lane == 0) {
-      sh[1] = top_before; sh[2] = top_all + thr_before;
+      sh[5] = top_before; sh[6] = top_all + thr_before;
       if (t == 0) {
         n_det[b] = top_all + thr_all;
         if (n_host) __hip_atomic_store(&n_host[b], top_all + thr_all, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1095,14 +1115,15 @@ __global__ __launch_bounds__(256) void plane_emit_kernel(const float* __restrict
     }
   }
   __syncthreads();
-  // ---- emission (emit_kernel) ----
-  const int top_base = sh[1], thr_base = sh[2];
+  PEMP_CLK(4);
+  // ---- F: emission ----
+  const int top_base = sh[5], thr_base = sh[6];
   int64_t* dout = det + (size_t)b * cap * 3;
   float* sout = scores + (size_t)b * cap;
   if ((int)threadIdx.x < ntop) {
     const int pos = top_base + threadIdx.x;
     if (pos < cap) {
-      const int idx = top_i[threadIdx.x];
+      const int idx = top_i[KMAX + threadIdx.x];
       dout[pos * 3 + 0] = idx % W;
       dout[pos * 3 + 1] = idx / W;
       dout[pos * 3 + 2] = t;
@@ -1111,19 +1132,41 @@ __global__ __launch_bounds__(256) void plane_emit_kernel(const float* __restrict
   }
   __shared__ cmask_t cm_sh[4][64][64];
   __shared__ int nz_sh[4][64];
+  __shared__ int q_xy[4][64], q_o[4][64];          // a wave's queued detections: y * W + x, output slot
+  const float* plane = s + (size_t)pl * H * W;
+  int qn = 0;                                      // (wave-uniform)
+  auto flush = [&]() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane < qn && q_xy[wave][lane] >= 0) {
+      const int xy = q_xy[wave][lane], o = q_o[wave][lane];
+      const int yy = xy / W, xx = xy - yy * W;
+      const float sv = pj.S ? proj_pixel(pj, b, t, yy, xx, H, W) : plane[xy];
+      float jm = 1.0f;
+      if (masks) jm = jm * masks[((size_t)b * H + yy) * W + xx];
+      dout[o * 3 + 0] = xx;
+      dout[o * 3 + 1] = yy;
+      dout[o * 3 + 2] = t;
+      sout[o] = sv * jm;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    qn = 0;
+  };
   int kb = 0;
   for (int st = 0; st < S; ++st) {
     if (band_n[st] == 0) continue;                       // uniform
     if ((kb++ & 3) != wave) continue;
     const int ry0 = st * SR, rows = min(SR, H - ry0);
     int pos = thr_base + band_off[st];
-    const float* plane = s + (size_t)pl * H * W;
-    const size_t u0 = ((size_t)pl * g.nb + st) * g.nsx;
+    const size_t u0 = ((size_t)pl * g.nb + st) * g.nsx;   // first unit of the band (nsx <= 64)
     const unsigned long long nzm = (unsigned long long)band_nz[st][0] | ((unsigned long long)band_nz[st][1] << 32);
     int nnz = 0;
     unsigned rows_any = 0;
     unsigned cms[4];
-    {
+    {                                                    // the first 4 strips' column masks together
       unsigned long long m = nzm;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -1152,32 +1195,38 @@ __global__ __launch_bounds__(256) void plane_emit_kernel(const float* __restrict
         const int sx = nz_sh[wave][k];
         unsigned long long word = __ballot((cm_sh[wave][k][lane] >> j) & 1u);
         if (!word) continue;
-        for (int q = 0; q < ntop; ++q) {               // already listed as a top-k detection
-          if (!top_bit[q]) continue;
-          const int idx = top_i[q], ty = idx / W, tx = idx - ty * W, tsx = tx / g.sc;
-          if (ty == yy && tsx == sx) word &= ~(1ull << (tx - tsx * g.sc + g.p));
-        }
+        for (int q = 0; q < ntop; ++q)                   // already listed as a top-k detection
+          if (ex_y[q] == yy && ex_sx[q] == sx) word &= ~(1ull << ex_lane[q]);
+        const int cnt = __popcll(word);
+        if (qn + cnt > 64) flush();
         if ((word >> lane) & 1ull) {
-          const int xx = sx * g.sc - g.p + lane;
-          const int o = pos + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(word >> 32),
+          const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(word >> 32),
                                                           __builtin_amdgcn_mbcnt_lo((unsigned)word, 0u));
+          const int o = pos + below;
           if (o < cap) {
-            const float sv = pj.S ? proj_pixel(pj, b, t, yy, xx, H, W) : plane[(size_t)yy * W + xx];
-            float jm = 1.0f;
-            if (masks) jm = jm * masks[((size_t)b * H + yy) * W + xx];
-            dout[o * 3 + 0] = xx;
-            dout[o * 3 + 1] = yy;
-            dout[o * 3 + 2] = t;
-            sout[o] = sv * jm;
+            q_xy[wave][qn + below] = yy * W + sx * g.sc - g.p + lane;
+            q_o[wave][qn + below] = o;
+          } else {
+            q_xy[wave][qn + below] = -1;
           }
         }
-        pos += __popcll(word);
+        qn += cnt;
+        pos += cnt;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+  if (qn) flush();
+#if PEMP_DETECT_CLOCKS
+  __syncthreads();
+  PEMP_CLK(5);
+  if (threadIdx.x == 0 && t == 0)
+    printf("clk plane %d: start %lld gathered +%lld selected +%lld listed +%lld published +%lld emitted +%lld\n", pl,
+           clk[0], clk[1] - clk[0], clk[2] - clk[0], clk[3] - clk[0], clk[4] - clk[0], clk[5] - clk[0]);
+#endif
+#undef PEMP_CLK
 }
 
 #ifndef PEMP_DETECT_FUSED
@@ -1259,8 +1308,8 @@ static int launch_detect(const float* s, const float* masks, const DetectGeom& g
     }
     PEMP_LAUNCH_CHECK();
   }
-  if ((stages & PEMP_DETECT_SELECT) && PEMP_DETECT_FUSED) {
-    if (!(stages & PEMP_DETECT_NMS)) PEMP_HIP(hipMemsetAsync(w.pflag, 0, sizeof(int) * g.B * g.J, st));
+  if ((stages & PEMP_DETECT_SELECT) && PEMP_DETECT_FUSED && g.units <= SEL_UNITS) {
+    if (!(stages & PEMP_DETECT_NMS)) PEMP_HIP(hipMemsetAsync(w.pflag, 0, sizeof(unsigned long long) * g.B * g.J, st));
     ProfScope prof("detect_select_emit", st);
     hipLaunchKernelGGL(plane_emit_kernel<KMAX>, dim3(g.B * g.J), dim3(256), 0, st, s, masks, g, thr, use_thr, w.cbits,
                        w, det, scores, (int*)n_det, cap, (int*)n_host, pj);

@@ -71,6 +71,59 @@ def test_vs_oracle(case):
         assert torch.equal(out[i].cpu(), ref[i]), f"output {i}"
 
 
+def _edge_maps(B, J, H, W, seed):
+    """Heatmaps for the detection edge cases: image 0 planted peaks plus a plateau of equal positive maxima
+    touching the left border, image 1 negative everywhere but a few values (planes with fewer than top-k
+    non-negative pixels: their top-k takes negatives), image 2 zero but for isolated values on the right and
+    bottom borders."""
+    rng = np.random.default_rng(seed)
+    hm = np.zeros((B, J, H, W), np.float32)
+    hm[0] = syn.make_heatmaps(seed, 1, J, H, W, 2, margin=2)[0]
+    hm[0, :, 1:7, 0:9] = 0.5
+    if B > 1:
+        hm[1] = -rng.random((J, H, W)).astype(np.float32) - 0.01
+        hm[1, :2, H // 2, W // 3] = 0.0
+        hm[1, 1, 1, 1] = 0.7
+    if B > 2:
+        hm[2][:, H - 1, rng.integers(0, W, 3)] = 0.3 + rng.random((J, 3)).astype(np.float32)
+        hm[2][:, rng.integers(0, H, 3), W - 1] = 0.2 + rng.random((J, 3)).astype(np.float32)
+    return torch.from_numpy(hm)
+
+
+@pytest.mark.parametrize("H,W,pool,mask", [(50, 1000, 9, False), (37, 8, 1, False), (64, 248, 3, True),
+                                           (16, 252, 5, False), (70, 500, 7, True), (33, 17, 5, False)])
+def test_detection_edges(H, W, pool, mask):
+    """Detection on shapes and values at the edges of both stage-1 layouts (4 columns per lane when W % 4 == 0,
+    1 otherwise): strips that end past the plane, single-strip planes narrower than a wave, bands cut by H,
+    every pool radius, negative planes, plateaus of equal maxima, maxima on every border, masks."""
+    B, J = 3, 17
+    hm = _edge_maps(B, J, H, W, H * W + pool)
+    feats = torch.from_numpy(syn.closed_form((B, 128, H, W), 0.25))
+    tags = torch.from_numpy(syn.closed_form((B, J, H, W, 1), 0.75))
+    masks = torch.from_numpy((np.random.default_rng(W).random((B, H, W)) > 0.2).astype(np.float32)) if mask else None
+    gc = pcfg.inference_gc_config("fully", pool, mask)
+    out = run_gc(gc, J, hm, feats, tags, masks)
+    ref = restate.construct_graph(hm, feats, tags, masks, gc, J)
+    assert ref[7].shape[0] > 0
+    for i in (7, 11, 12, 14, 2):
+        assert torch.equal(out[i].cpu(), ref[i]), f"output {i}"
+
+
+def test_detection_large_plane():
+    """A plane of more units than the fused select + emit stage takes (1280 x 1296: 80 bands x 22 strips > 1024)
+    goes through the two-kernel selection and emission; noisy background, masks off."""
+    B, J, H, W = 1, 17, 1280, 1296
+    hm = torch.from_numpy(syn.make_heatmaps(7, B, J, H, W, 9, variant="noisy", margin=4))
+    feats = torch.from_numpy(syn.closed_form((B, 16, H, W), 0.25))
+    tags = torch.from_numpy(syn.closed_form((B, J, H, W, 1), 0.75))
+    gc = pcfg.inference_gc_config("fully", 5, False)
+    out = run_gc(gc, J, hm, feats, tags, None)
+    ref = restate.construct_graph(hm, feats, tags, None, gc, J)
+    assert ref[7].shape[0] > J
+    for i in (7, 11, 12, 14, 2, 0):
+        assert torch.equal(out[i].cpu(), ref[i]), f"output {i}"
+
+
 def test_empty_image_and_overflow_growth():
     """An all-zero image yields no detections (N=0 rows) and a crowded one grows the capacity."""
     J, H, W = 17, 64, 64
