@@ -686,6 +686,8 @@ def main():
     gc = pcfg.inference_gc_config(wl["graph"], 5, False)
     hm, feats, tags = make_inputs(wl, rank, dev)
     model, _ = make_model(wl, dev)
+    if wl["graph"] == "fully" and not os.environ.get("PEMP_NO_CAP_MPN"):
+        pemp_amd.bind_mpn(model)   # capacity mode: the MPN queued behind the graph build, ahead of the counts
     _lib.lib()
 
     # batches in flight: each stream has its own library scratch (construct_graph and the MPN are

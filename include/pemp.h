@@ -423,6 +423,21 @@ int pemp_mpn_forward_fully(const pemp_mpn_desc* desc, const pemp_mpn_weights* we
                            float* edge_logits, float* node_logits, float* class_logits,
                            void* workspace, size_t workspace_bytes, void* stream);
 
+/* Capacity mode of pemp_mpn_forward_fully: queued right behind pemp_fully_graph_build_cap, before the host has the
+ * detection counts (replaces the host read-back at ConstructGraph.py:1174,1178 ahead of the MPN). x / edge_attr /
+ * node_types (= joint_det + 2, stride 3) / node_off are that build's capacity buffers (n_cap rows, e_cap edges);
+ * n_det is the detection's device count array ([B], det_cap detections per image at most). The batch's N and E
+ * are derived on the device; the logits are written compactly for those (edge row r at r * E, node / class row r
+ * at r * N), inside arrays sized for the capacities. A batch past any capacity (the capacity build then wrote
+ * nothing) runs as an empty forward and writes no logits: the caller, which reads the counts back anyway, re-runs
+ * the exact path. PEMP_ERR_UNSUPPORTED for models whose node MLPs are not fused (node embedding, heads) or
+ * det_cap above the closed-form image limit (2048). Results equal pemp_mpn_forward_fully's. */
+int pemp_mpn_forward_fully_cap(const pemp_mpn_desc* desc, const pemp_mpn_weights* weights, const float* x,
+                               const float* edge_attr, const int64_t* node_types, int64_t n_cap, int64_t e_cap,
+                               const int32_t* n_det, int det_cap, const int64_t* node_off, int B,
+                               float* edge_logits, float* node_logits, float* class_logits,
+                               void* workspace, size_t workspace_bytes, void* stream);
+
 /* pemp_mpn_forward for an edge_index sorted by (src, dst) without duplicates and symmetric (every s -> d has
  * its d -> s: PyG to_undirected's coalesced output, as knn_mpn_graph / feature_knn_mpn_graph / score_based_graph
  * return it, ConstructGraph.py:363-422): the type-major edge order is read off the rows of the list (segment

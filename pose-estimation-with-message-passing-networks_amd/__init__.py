@@ -21,6 +21,13 @@ def get_mpn_model(config, **kwargs):
     return _m(config, **kwargs)
 
 
+def bind_mpn(model):
+    """Capacity mode: construct_graph queues ``model``'s forward behind its capacity graph build, before the
+    detection counts reach the host (graph_constructor.NaiveGraphConstructor.bind_mpn); ``None`` unbinds."""
+    from .graph_constructor import NaiveGraphConstructor as _n
+    _n.bind_mpn(model)
+
+
 def ProjectedMaps(maps, size, divisor=None, gather=None):
     """Lazy image-size projection of per-scale feature maps for ``features=`` (frontend.py); ``gather``: the
     model's feature_gather Conv2d, evaluated at the detections only."""

@@ -89,6 +89,8 @@ SIGNATURES = {
                                  c_i64, c_i64, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "pemp_mpn_forward_fully": (c_i32, [ctypes.POINTER(PempMpnDesc), ctypes.POINTER(PempMpnWeights), c_p, c_p, c_p,
                                        c_p, c_i64, c_i64, c_p, c_p, c_i32, c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "pemp_mpn_forward_fully_cap": (c_i32, [ctypes.POINTER(PempMpnDesc), ctypes.POINTER(PempMpnWeights), c_p, c_p,
+                                           c_p, c_i64, c_i64, c_p, c_i32, c_p, c_i32, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "pemp_mpn_forward_sym": (c_i32, [ctypes.POINTER(PempMpnDesc), ctypes.POINTER(PempMpnWeights), c_p, c_p, c_p,
                                      c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "pemp_mpn_prepare": (c_i32, [ctypes.POINTER(PempMpnDesc), c_p, c_p, c_i64, c_i64, c_p, c_sz, c_p]),

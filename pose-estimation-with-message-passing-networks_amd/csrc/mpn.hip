@@ -23,6 +23,8 @@
 #include <type_traits>
 #include <map>
 #include <mutex>
+#include <string>
+#include <vector>
 #include <string.h>
 #include <math.h>
 
@@ -1068,8 +1070,10 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp em
                                                                      const float* __restrict__ q0_b,
                                                                      const float* __restrict__ e1_w,
                                                                      const uint16_t* __restrict__ e1_bf,
-                                                                     float* __restrict__ r0, float* __restrict__ q0) {
+                                                                     float* __restrict__ r0, float* __restrict__ q0,
+                                                                     const int64_t* __restrict__ ne) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
+  if (ne) E = ne[1];   // capacity mode: the device-side edge count
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
   stage_tile64<PREC>(sm + Lo.total, e1_w, D, e1_bf);   // W1_e_cur after the embedding image
   for (int l = 0; l <= Lo.n; ++l) {
@@ -1164,6 +1168,8 @@ struct EdgeStepArgs {
   float* edge_logits;
   int write_next;
   unsigned long long* stamps;   // diagnostic builds (-DPEMP_STAMPS) only: per-wave phase timestamps
+  const int64_t* ne;            // capacity mode: device-side (N, E); N / E above are then the capacities
+  int rec;                      // capacity mode: edge_logits is the base, the pass writes row rec (of E)
 };
 
 // Diagnostic phase timestamps (-DPEMP_STAMPS builds only; tools/edge_timeline.py): lane 0 of each
@@ -1475,7 +1481,8 @@ __device__ inline void edge_ranges_fill(const int* seg, const int* wg_start, con
 }
 
 __global__ __launch_bounds__(256) void edge_ranges_kernel(const int* seg, const int* wg_start, const int* s_dst, int T,
-                                                          int64_t N, int G, int4* ranges) {
+                                                          int64_t N, int G, int4* ranges, const int64_t* ne) {
+  if (ne) N = ne[0];   // capacity mode: the device-side node count (N: the capacity)
   edge_ranges_fill(seg, wg_start, s_dst, T, N, G, ranges);
 }
 
@@ -1596,7 +1603,8 @@ __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_
   const int t = __builtin_amdgcn_readfirstlane(rg.z);
   const int rflags = __builtin_amdgcn_readfirstlane(rg.w);
   float* mybuf = rbuf + wave * 1024;
-  const int E = (int)a.E;
+  const int E = (int)(a.ne ? a.ne[1] : a.E);
+  float* const logits = a.edge_logits && a.ne ? a.edge_logits + (int64_t)a.rec * E : a.edge_logits;
   // r / Q0 rows past the wave's range end are out of the descriptor: the last tile's DMA moves no bytes
   // for them (its masked lanes read 0)
   const rsrc_t rs_r = make_rsrc(a.r_cur, end * 256);
@@ -1795,7 +1803,7 @@ __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_
         for (int r = 0; r < 4; ++r) h1[ob][r] = ep[ob][r] * dom_inv<PREC>();
       mlp_frag<4>(a.head, h1, h2);
       if (valid && g == 0)   // (descriptor store: an out-of-range id from a contract-breaking list is dropped)
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(h1[0][0]), make_rsrc(a.edge_logits, E * 4),
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(h1[0][0]), make_rsrc(logits, E * 4),
                                               4 * a.s_orig[p], 0, 0);
     }
     Frag<PREC> fe;                                // e' split once for the r_next, head and message GEMMs
@@ -1851,7 +1859,7 @@ __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_
       lg += __shfl_xor(lg, 16);
       lg += __shfl_xor(lg, 32);
       if (valid && g == 0)   // (descriptor store: an out-of-range id from a contract-breaking list is dropped)
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lg + hb[D + 64]), make_rsrc(a.edge_logits, E * 4),
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lg + hb[D + 64]), make_rsrc(logits, E * 4),
                                               4 * orig, 0, 0);
     }
     // message: m = ReLU(P_t[dst] + W_t_e · e')
@@ -2012,6 +2020,7 @@ struct NodeMlpArgs {
   pemp_mlp mlp;
   int max_out;      // widest layer output
   float* X;
+  const int64_t* ne;   // capacity mode: device-side node count (N: the capacity)
 };
 
 __host__ __device__ inline int nmlp_stride(int k) { return (k + 15) / 16 * 16 + 8; }   // 8 * odd mod 64 dwords
@@ -2019,7 +2028,8 @@ __host__ __device__ inline int nmlp_stride(int k) { return (k + 15) / 16 * 16 + 
 __global__ __launch_bounds__(256) void node_mlp_kernel(NodeMlpArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
-  const int64_t n0 = (int64_t)blockIdx.x * 16, N = a.N;
+  const int64_t n0 = (int64_t)blockIdx.x * 16, N = a.ne ? a.ne[0] : a.N;
+  if (n0 >= N) return;   // (capacity grids)
   const int T = a.T, K0 = 64 * T;
   const int S[2] = {nmlp_stride(K0 > a.max_out ? K0 : a.max_out), nmlp_stride(a.max_out)};
   float* buf[2] = {lds, lds + 16 * S[0]};
@@ -2079,6 +2089,7 @@ struct NodeEptArgs {
   float* NT;
   int ldnt;
   float out_scale;            // the edge passes' domain (dom<PREC>())
+  const int64_t* ne;          // capacity mode: device-side node count (N: the capacity)
 };
 
 __global__ __launch_bounds__(256) void node_ept_kernel(NodeEptArgs a) {
@@ -2087,7 +2098,8 @@ __global__ __launch_bounds__(256) void node_ept_kernel(NodeEptArgs a) {
   __shared__ int tys[16];
   __shared__ unsigned tmask;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
-  const int64_t n0 = (int64_t)blockIdx.x * 16, N = a.N;
+  const int64_t n0 = (int64_t)blockIdx.x * 16, N = a.ne ? a.ne[0] : a.N;
+  if (n0 >= N) return;   // (capacity grids)
   for (int idx = threadIdx.x; idx < 16 * 32; idx += 256) {
     const int r = idx >> 5, c4 = (idx & 31) * 4;
     const int64_t n = n0 + r;
@@ -2165,6 +2177,7 @@ struct NodeUpdateArgs {
   int64_t N;
   const float *upd_w, *upd_b;
   float* X;
+  const int64_t* ne;   // capacity mode: device-side node count (N: the capacity)
 };
 
 constexpr int UPD_WAVES = 16;
@@ -2172,7 +2185,8 @@ constexpr int UPD_WAVES = 16;
 __global__ __launch_bounds__(64 * UPD_WAVES) void node_update_kernel(NodeUpdateArgs a) {
   __shared__ __attribute__((aligned(16))) float red[UPD_WAVES][16 * 17];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
-  const int64_t n0 = (int64_t)blockIdx.x * 16, N = a.N;
+  const int64_t n0 = (int64_t)blockIdx.x * 16, N = a.ne ? a.ne[0] : a.N;
+  if (n0 >= N) return;   // (capacity grids)
   const int ob = blockIdx.y, T = a.T;
   if (!a.upd_w) {   // x_new = agg[n, 0] (T == 1), this block's 16 features
     if (threadIdx.x < 256) {
@@ -2388,6 +2402,8 @@ struct NodeRowsArgs {
   float *node_out, *node_out2, *class_out, *class_out2;
   const float* img;      // LDS image [emb | node head | class head] built by zero_words_kernel
   int head_off, head_floats;   // heads block: offset (= embedding image size, or 0) and size
+  const int64_t* ne;     // capacity mode: device-side node count (N: the capacity); node_out / class_out are then
+  int slot, dup;         // the bases of the logit arrays, the rows written are slot (and slot + 1 when dup) of N
   int emb_whole;         // ROWS_EMBED: the whole embedding image fits in LDS (one DMA up front)
 };
 
@@ -2420,8 +2436,16 @@ __global__ __launch_bounds__(256) void node_rows_kernel(NodeRowsArgs a) {
   float* act1 = act0 + 16 * RS;
   float* wreg = act1 + 16 * RS;                  // one embedding layer at a time, then the heads
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
-  const int64_t n0 = (int64_t)blockIdx.x * 16, N = a.N;
+  const int64_t n0 = (int64_t)blockIdx.x * 16, N = a.ne ? a.ne[0] : a.N;
+  if (n0 >= N) return;   // (capacity grids)
   const bool heads = a.node_out != nullptr;
+  float *node_out = a.node_out, *node_out2 = a.node_out2, *class_out = a.class_out, *class_out2 = a.class_out2;
+  if (a.ne && heads) {   // capacity mode: rows slot (and slot + 1) of the device-side N
+    node_out = a.node_out + (int64_t)a.slot * N;
+    class_out = a.class_out + (int64_t)a.slot * N * a.J;
+    node_out2 = a.dup ? node_out + N : nullptr;
+    class_out2 = a.dup ? class_out + N * a.J : nullptr;
+  }
   const int r = threadIdx.x >> 4, q = threadIdx.x & 15;   // row r of the tile, features 4 q .. 4 q + 3
   const int64_t n = n0 + r, nc = n < N ? n : N - 1;
   if (a.mode == ROWS_EMBED) {
@@ -2531,8 +2555,8 @@ __global__ __launch_bounds__(256) void node_rows_kernel(NodeRowsArgs a) {
     const pemp_mlp& m = wave == 0 ? a.node_head : a.class_head;
     mlp_lds_frag(wave == 0 ? wreg : wreg + mlp_lds_floats(a.node_head), m, in);
     const int od = wave == 0 ? 1 : a.J;
-    float* o1 = wave == 0 ? a.node_out : a.class_out;
-    float* o2 = wave == 0 ? a.node_out2 : a.class_out2;
+    float* o1 = wave == 0 ? node_out : class_out;
+    float* o2 = wave == 0 ? node_out2 : class_out2;
     const int64_t nn = n0 + c;
     if (nn < N) {
 #pragma unroll
@@ -2561,6 +2585,7 @@ struct NodeTableArgs {
   const uint16_t* pre_bf;
   int NO, groups;
   float* NT;
+  const int64_t* ne;   // capacity mode: device-side node count (N: the capacity)
 };
 
 #ifndef PEMP_TBL_TILES
@@ -2573,7 +2598,8 @@ __global__ __launch_bounds__(256) void node_table_kernel(NodeTableArgs a) {
   __shared__ __attribute__((aligned(16))) float xs[16 * TBL_TILES * RS];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
   const int chunk = blockIdx.x / a.groups, grp = blockIdx.x - chunk * a.groups;
-  const int64_t n0 = (int64_t)chunk * 16 * TBL_TILES, N = a.N;
+  const int64_t n0 = (int64_t)chunk * 16 * TBL_TILES, N = a.ne ? a.ne[0] : a.N;
+  if (n0 >= N) return;   // (capacity grids)
   const int nob = a.NO / 16, ob = grp * 4 + wave, obc = min(ob, nob - 1);
   // this wave's weight fragment (rows 16 ob + c), issued first
   float4 w[8];
@@ -2802,6 +2828,40 @@ static StagePlan node_image_plan(const pemp_mpn_weights& w) {
 // with E_t = sum_b n_{b,t} (n_b - 1). Identical arrays to launch_prepare's (tested bit for bit).
 constexpr int FULLY_MAXB = 64;      // images per batch
 constexpr int FULLY_MAXN = 2048;    // nodes per image (LDS lists)
+// Capacity mode (pemp_mpn_forward_fully_cap): the batch's N = sum n_b and E = sum n_b (n_b - 1) from the detection
+// counts on the device, before the host has them. ne = (N, E, overflow); a batch past any capacity (an image over
+// the detection capacity, N > n_cap or E > e_cap: the capacity graph build wrote nothing) gets (0, 0, 1), and every
+// kernel of the forward then runs empty.
+__global__ __launch_bounds__(256) void cap_counts_kernel(const int32_t* __restrict__ n_det, int B, int det_cap,
+                                                         int64_t n_cap, int64_t e_cap, int64_t* __restrict__ ne) {
+  __shared__ long long sn[4], se[4];
+  __shared__ int sb[4];
+  long long n = 0, e = 0;
+  int bad = 0;
+  for (int b = threadIdx.x; b < B; b += 256) {
+    const long long c = n_det[b];
+    bad |= c < 0 || c > det_cap;
+    n += c;
+    e += c * (c > 0 ? c - 1 : 0);
+  }
+  for (int off = 32; off >= 1; off >>= 1) {
+    n += __shfl_xor(n, off);
+    e += __shfl_xor(e, off);
+    bad |= __shfl_xor(bad, off);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) { sn[wave] = n; se[wave] = e; sb[wave] = bad; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    n = sn[0] + sn[1] + sn[2] + sn[3];
+    e = se[0] + se[1] + se[2] + se[3];
+    const bool over = (sb[0] | sb[1] | sb[2] | sb[3]) || n > n_cap || e > e_cap;
+    ne[0] = over ? 0 : n;
+    ne[1] = over ? 0 : e;
+    ne[2] = over ? 1 : 0;
+  }
+}
+
 struct FullyPrepArgs {
   const int64_t* node_off;          // [B + 1] device
   int B;
@@ -2809,6 +2869,7 @@ struct FullyPrepArgs {
   int64_t ts, N;
   int T, Gsplit;
   int *seg, *wg_start, *s_src, *s_dst, *s_orig, *err;
+  const int64_t* ne;   // capacity mode: device-side (N, E, overflow); an overflowed batch prepares as empty images
 };
 
 __global__ __launch_bounds__(256) void fully_prepare_kernel(FullyPrepArgs a) {
@@ -2821,8 +2882,9 @@ __global__ __launch_bounds__(256) void fully_prepare_kernel(FullyPrepArgs a) {
   __shared__ int bad_sh;
   __shared__ long long eoff_sh;
   const int b = blockIdx.y, T = a.T, B = a.B;
-  const int64_t N = a.N;
-  for (int i = threadIdx.x; i <= B; i += 256) noff[i] = (int)a.node_off[i];
+  const int64_t N = a.ne ? a.ne[0] : a.N;
+  const bool empty = a.ne && a.ne[2];   // capacity overflow: node_off was not written
+  for (int i = threadIdx.x; i <= B; i += 256) noff[i] = empty ? 0 : (int)a.node_off[i];
   for (int i = threadIdx.x; i < FULLY_MAXB * MAXT; i += 256) (&cnt_bt[0][0])[i] = 0;
   if (threadIdx.x == 0) bad_sh = 0;
   __syncthreads();
@@ -3241,7 +3303,8 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
                             const float* edge_attr, const int64_t* edge_index, const int64_t* node_types,
                             int64_t N, int64_t E, float* edge_logits, float* node_logits, float* class_logits,
                             void* workspace, size_t workspace_bytes, void* stream, const int64_t* fully_node_off,
-                            int fully_B, int fully_nmax, bool sym = false) {
+                            int fully_B, int fully_nmax, bool sym = false, const int32_t* cap_ndet = nullptr,
+                            int cap_det = 0) {
   PEMP_CHECK_ARG(desc && w, "pemp_mpn_forward: null desc/weights");
   const int T = desc->num_types, J = desc->num_joints;
   PEMP_CHECK_ARG(desc->hidden == 64, "pemp_mpn_forward: hidden width must be 64 (got %d)", desc->hidden);
@@ -3293,7 +3356,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
                      (w->e1_bf && w->e2_bf && w->msg_bf && w->pre_bf && (w->emb_bf || !mlp_ok(w->edge_emb, 64, 64))),
                  "pemp_mpn_forward: split precisions need the e1_bf / e2_bf / msg_bf / pre_bf / emb_bf weight packs");
   PEMP_CHECK_ARG(N == 0 || (x && node_logits && class_logits && node_types), "pemp_mpn_forward: null node tensors");
-  PEMP_CHECK_ARG(E == 0 || (edge_attr && edge_index && edge_logits), "pemp_mpn_forward: null edge tensors");
+  PEMP_CHECK_ARG(E == 0 || (edge_attr && (edge_index || fully_node_off) && edge_logits), "pemp_mpn_forward: null edge tensors");
   size_t need = 0;
   mpn_carve(nullptr, T, N, E, &need);
   if (workspace_bytes < need) {
@@ -3305,6 +3368,12 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   const MpnWs ws = mpn_carve(workspace, T, N, E, nullptr);
   const hipStream_t st = as_stream(stream);
   const int64_t tstride = desc->types_stride > 0 ? desc->types_stride : 1;   // node_types may be a strided view
+  // capacity mode (pemp_mpn_forward_fully_cap): N and E are capacities; the device-side counts come first
+  int64_t* const ne = cap_ndet ? reinterpret_cast<int64_t*>(ws.err + 8) : nullptr;
+  if (cap_ndet) {
+    hipLaunchKernelGGL(cap_counts_kernel, dim3(1), dim3(256), 0, st, cap_ndet, fully_B, cap_det, N, E, ne);
+    PEMP_LAUNCH_CHECK();
+  }
   const int64_t K = (int64_t)T * N;
 
   const bool fused_heads_ = node_heads_fused(*w);
@@ -3347,7 +3416,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   if (!(desc->flags & PEMP_MPN_PREPARED)) {
     if (fully_node_off && N > 0) {
       FullyPrepArgs fa{fully_node_off, fully_B, node_types, tstride, N, T, std::max(num_cus(), T),
-                       ws.seg, ws.wg_start, ws.s_src, ws.s_dst, ws.s_orig, ws.err};
+                       ws.seg, ws.wg_start, ws.s_src, ws.s_dst, ws.s_orig, ws.err, ne};
       // one thread per (type, target) segment (a per-edge mapping with binary searches measured 41 us
       // vs 15 us at C3)
       const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(64, ((int64_t)T * fully_nmax + 511) / 512));
@@ -3366,7 +3435,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   // its chains of dependent small loads stay off the edge embedding's workgroups
   if (E > 0 && steps >= 1) {
     hipLaunchKernelGGL(edge_ranges_kernel, dim3((unsigned)std::min(64, (edge_grid * (EDGE_WAVES + 12) + 255) / 256)),
-                       dim3(256), 0, pst, ws.seg, ws.wg_start, ws.s_dst, T, N, edge_grid, ws.ranges);
+                       dim3(256), 0, pst, ws.seg, ws.wg_start, ws.s_dst, T, N, edge_grid, ws.ranges, ne);
     PEMP_LAUNCH_CHECK();
   }
   return PEMP_OK;
@@ -3382,7 +3451,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
 #define PEMP_EMBED_LAUNCH(P, FX)                                                                                   \
   hipLaunchKernelGGL((edge_embed_kernel<P, FX>), dim3(grid), dim3(64 * EDGE_WAVES), lds, pst, w->edge_emb, emb_lo,  \
                      w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, w->e1_bf, \
-                     ws.EA, ws.Q0)
+                     ws.EA, ws.Q0, ne)
       if (emb_prec == PEMP_PREC_F16X3) {
         if (fixed) PEMP_EMBED_LAUNCH(2, true);
         else PEMP_EMBED_LAUNCH(2, false);
@@ -3392,7 +3461,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
       } else
         hipLaunchKernelGGL((edge_embed_kernel<0, false>), dim3(grid), dim3(64 * EDGE_WAVES), lds, pst, w->edge_emb, emb_lo,
                            w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, w->e1_bf,
-                           ws.EA, ws.Q0);
+                           ws.EA, ws.Q0, ne);
 #undef PEMP_EMBED_LAUNCH
     } else {
       hipLaunchKernelGGL(edge_embed_wide_kernel, dim3((unsigned)((E + 63) / 64)), dim3(256), 0, pst, w->edge_emb,
@@ -3414,13 +3483,13 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   // x for the next stage (mode) + heads when slot >= 0, then the node table when `table`
   auto node_step = [&](int mode, bool table, int slot, bool dup) -> int {
     if (mode == -1 && w->upd_mlp.n_layers > 0) {     // hierarchical update MLP (dense-folded)
-      NodeMlpArgs ma{ws.agg, ws.seg, T, N, w->upd_mlp, nmlp_max_out(w->upd_mlp), ws.X};
+      NodeMlpArgs ma{ws.agg, ws.seg, T, N, w->upd_mlp, nmlp_max_out(w->upd_mlp), ws.X, ne};
       ProfScope prof("node_update", st);
       hipLaunchKernelGGL(node_mlp_kernel, dim3(node_grid), dim3(256), nmlp_lds_bytes(T, w->upd_mlp), st, ma);
       PEMP_LAUNCH_CHECK();
       mode = ROWS_NONE;
     } else if (mode == -1) {                           // update MLP on non-linear aggregates
-      NodeUpdateArgs ua{ws.agg, ws.seg, T, N, w->upd_w, w->upd_b, ws.X};
+      NodeUpdateArgs ua{ws.agg, ws.seg, T, N, w->upd_w, w->upd_b, ws.X, ne};
       ProfScope prof("node_update", st);
       hipLaunchKernelGGL(node_update_kernel, dim3(node_grid, 4), dim3(64 * UPD_WAVES), 0, st, ua);
       PEMP_LAUNCH_CHECK();
@@ -3431,7 +3500,13 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
     if (mode == ROWS_EMBED) { na.x_in = x; na.in_ld = desc->node_in_dim; }
     na.agg = ws.agg; na.seg = ws.seg; na.T = T; na.upd_b = w->upd_b; na.N = N; na.X = ws.X;
     na.node_head = w->node_head; na.class_head = w->class_head; na.J = J;
-    if (slot >= 0 && fused_heads) {
+    na.ne = ne;
+    if (slot >= 0 && fused_heads && ne) {   // capacity mode: bases, the kernel places rows slot (+ 1) of its N
+      na.node_out = node_logits;
+      na.class_out = class_logits;
+      na.slot = slot;
+      na.dup = dup ? 1 : 0;
+    } else if (slot >= 0 && fused_heads) {
       na.node_out = node_logits + (int64_t)slot * N;
       na.class_out = class_logits + (int64_t)slot * N * J;
       na.node_out2 = dup ? na.node_out + N : nullptr;
@@ -3458,7 +3533,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
       }
     }
     if (table) {
-      NodeTableArgs ta{ws.X, N, w->pre_w, w->pre_b, w->pre_bf, NO, table_groups, ws.NT};
+      NodeTableArgs ta{ws.X, N, w->pre_w, w->pre_b, w->pre_bf, NO, table_groups, ws.NT, ne};
       ProfScope prof("node_table", st);
       if (table_prec == PEMP_PREC_F16X3)
         hipLaunchKernelGGL(node_table_kernel<2>, dim3(table_grid), dim3(256), 0, st, ta);
@@ -3470,7 +3545,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
       if (ept) {   // columns 0..127 of the table: the per-type node terms (zero rows in pre_w)
         NodeEptArgs xa{ws.X, node_types, tstride, T, N, w->ept_l1_w, w->ept_l1_b, w->ept_l2_w, w->ept_l2_b,
                        w->ept_o1_w, w->ept_o2_w, ws.NT, NO,
-                       desc->precision == PEMP_PREC_F16X3 ? dom<2>() : 1.0f};
+                       desc->precision == PEMP_PREC_F16X3 ? dom<2>() : 1.0f, ne};
         hipLaunchKernelGGL(node_ept_kernel, dim3(node_grid), dim3(256), 0, st, xa);
         PEMP_LAUNCH_CHECK();
       }
@@ -3542,7 +3617,9 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
       ea.NT = ws.NT; ea.Q0 = ws.Q0; ea.r_cur = e_cur; ea.r_next = e_nxt;
       ea.img = eimg; ea.img_stride = img_stride(upd_fused, pub_head);
       ea.agg = ws.agg; ea.head = w->edge_head;
-      ea.edge_logits = record ? edge_logits + (int64_t)rec * E : nullptr;
+      ea.edge_logits = record ? (ne ? edge_logits : edge_logits + (int64_t)rec * E) : nullptr;
+      ea.ne = ne;
+      ea.rec = rec;
       ea.write_next = !last;
 #ifdef PEMP_STAMPS
       ea.stamps = it == g_diag_stamp_pass ? g_diag_stamps : nullptr;
@@ -3600,6 +3677,126 @@ extern "C" int pemp_mpn_forward_fully(const pemp_mpn_desc* desc, const pemp_mpn_
                             class_logits, workspace, workspace_bytes, stream, nullptr, 0, 0);
   return mpn_forward_impl(desc, w, x, edge_attr, edge_index, node_types, N, E, edge_logits, node_logits, class_logits,
                           workspace, workspace_bytes, stream, node_off, B, (int)nmax);
+}
+
+// ---- HIP graphs of the capacity-mode forward ------------------------------------------------------------------
+// A capacity-mode forward's launches depend only on its arguments (pointers, capacities, descriptor, weight set),
+// never on the batch's counts, so the whole sequence (~15 launches, its side-stream fork and join included) is
+// captured into a HIP graph the second time the same arguments come (the first time they launch directly: one-off
+// argument sets never pay a capture) and replayed with one launch from then on -- a serving loop whose allocator
+// hands back the same buffers every step. Keyed by the bytes of every argument; a small LRU.
+// PEMP_NO_GRAPHS disables it; the library profiler (per-kernel events) runs the launches directly.
+struct CapGraph {
+  std::string key;
+  hipGraphExec_t exec = nullptr;
+  uint64_t used = 0;
+};
+
+static bool graphs_off() {
+  static const bool v = getenv("PEMP_NO_GRAPHS") != nullptr;
+  return v;
+}
+
+static int cap_forward_direct(const pemp_mpn_desc* desc, const pemp_mpn_weights* w, const float* x,
+                              const float* edge_attr, const int64_t* node_types, int64_t n_cap, int64_t e_cap,
+                              const int32_t* n_det, int det_cap, const int64_t* node_off, int B, float* edge_logits,
+                              float* node_logits, float* class_logits, void* workspace, size_t workspace_bytes,
+                              void* stream) {
+  return mpn_forward_impl(desc, w, x, edge_attr, nullptr, node_types, n_cap, e_cap, edge_logits, node_logits,
+                          class_logits, workspace, workspace_bytes, stream, node_off, B, det_cap, false, n_det,
+                          det_cap);
+}
+
+extern "C" int pemp_mpn_forward_fully_cap(const pemp_mpn_desc* desc, const pemp_mpn_weights* w, const float* x,
+                                          const float* edge_attr, const int64_t* node_types, int64_t n_cap,
+                                          int64_t e_cap, const int32_t* n_det, int det_cap, const int64_t* node_off,
+                                          int B, float* edge_logits, float* node_logits, float* class_logits,
+                                          void* workspace, size_t workspace_bytes, void* stream) {
+  PEMP_CHECK_ARG(desc && w && n_det && node_off && B >= 1 && B <= FULLY_MAXB, "pemp_mpn_forward_fully_cap: bad args");
+  PEMP_CHECK_ARG(n_cap >= 1 && e_cap >= 0 && det_cap >= 1, "pemp_mpn_forward_fully_cap: bad capacities");
+  if (det_cap > FULLY_MAXN || !node_heads_fused(*w) || !node_embed_fused(*w) || !mlp_ok(w->edge_emb, 64, 64) ||
+      !(mlp_ok(w->node_head, 64, 64) && mlp_ok(w->class_head, 64, 64))) {
+    set_error("pemp_mpn_forward_fully_cap: this model / capacity takes the exact forward");
+    return PEMP_ERR_UNSUPPORTED;
+  }
+  if (graphs_off() || prof_active())
+    return cap_forward_direct(desc, w, x, edge_attr, node_types, n_cap, e_cap, n_det, det_cap, node_off, B,
+                              edge_logits, node_logits, class_logits, workspace, workspace_bytes, stream);
+  int dev = 0;
+  PEMP_HIP(hipGetDevice(&dev));
+  std::string key;
+  auto put = [&key](const void* p, size_t n) { key.append(static_cast<const char*>(p), n); };
+  const void* ptrs[] = {x, edge_attr, node_types, n_det, node_off, edge_logits, node_logits, class_logits, workspace,
+                        stream};
+  const int64_t nums[] = {n_cap, e_cap, det_cap, B, (int64_t)workspace_bytes, dev};
+  put(desc, sizeof(*desc));
+  put(w, sizeof(*w));
+  put(ptrs, sizeof(ptrs));
+  put(nums, sizeof(nums));
+  static std::mutex mu;
+  static std::vector<CapGraph> cache;
+  static std::vector<std::string> seen;   // argument sets launched directly once (most recent last)
+  static uint64_t tick = 0;
+  const hipStream_t st = as_stream(stream);
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto& e : cache)
+      if (e.key == key) {
+        e.used = ++tick;
+        PEMP_HIP(hipGraphLaunch(e.exec, st));
+        return PEMP_OK;
+      }
+    auto it = std::find(seen.begin(), seen.end(), key);
+    if (it == seen.end()) {                 // first sight: direct launches
+      if (seen.size() >= 32) seen.erase(seen.begin());
+      seen.push_back(key);
+      it = seen.end();
+    } else {
+      seen.erase(it);
+      it = seen.begin();                    // (marker: capture below)
+    }
+    if (it == seen.end()) {
+      mu.unlock();
+      const int rc0 = cap_forward_direct(desc, w, x, edge_attr, node_types, n_cap, e_cap, n_det, det_cap, node_off,
+                                         B, edge_logits, node_logits, class_logits, workspace, workspace_bytes, stream);
+      mu.lock();
+      return rc0;
+    }
+  }
+  // capture (thread-local mode: other threads' launches on other streams are unaffected)
+  PEMP_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+  const int rc = cap_forward_direct(desc, w, x, edge_attr, node_types, n_cap, e_cap, n_det, det_cap, node_off, B,
+                                    edge_logits, node_logits, class_logits, workspace, workspace_bytes, stream);
+  hipGraph_t graph = nullptr;
+  const hipError_t ec = hipStreamEndCapture(st, &graph);
+  if (rc != PEMP_OK || ec != hipSuccess || !graph) {
+    if (graph) (void)hipGraphDestroy(graph);
+    (void)hipGetLastError();
+    if (rc != PEMP_OK) return rc;
+    // capture refused (e.g. a caller-side capture in progress): launch directly
+    return cap_forward_direct(desc, w, x, edge_attr, node_types, n_cap, e_cap, n_det, det_cap, node_off, B,
+                              edge_logits, node_logits, class_logits, workspace, workspace_bytes, stream);
+  }
+  hipGraphExec_t exec = nullptr;
+  const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(graph);
+  if (ei != hipSuccess || !exec) {
+    (void)hipGetLastError();
+    return cap_forward_direct(desc, w, x, edge_attr, node_types, n_cap, e_cap, n_det, det_cap, node_off, B,
+                              edge_logits, node_logits, class_logits, workspace, workspace_bytes, stream);
+  }
+  PEMP_HIP(hipGraphLaunch(exec, st));
+  std::lock_guard<std::mutex> lk(mu);
+  constexpr size_t CAP_GRAPHS = 16;
+  if (cache.size() >= CAP_GRAPHS) {
+    auto lru = std::min_element(cache.begin(), cache.end(),
+                                [](const CapGraph& a, const CapGraph& b) { return a.used < b.used; });
+    (void)hipDeviceSynchronize();           // (rare: a replay of the evicted graph may still be in flight)
+    (void)hipGraphExecDestroy(lru->exec);
+    cache.erase(lru);
+  }
+  cache.push_back(CapGraph{key, exec, ++tick});
+  return PEMP_OK;
 }
 
 extern "C" int pemp_mpn_forward_sym(const pemp_mpn_desc* desc, const pemp_mpn_weights* w, const float* x,

@@ -63,6 +63,17 @@ class NaiveGraphConstructor:
     _cap = 512   # detections per image kept between calls (grows on overflow)
     _graph_hint = {}   # (shape key) -> (node, edge) capacities of the fully-graph capacity build
     _host_counts_free = {}   # device index -> free (capacity, address, int32 view) mapped host buffers
+    _bound_mpn = None        # capacity mode: the MPN queued right behind the capacity graph build (bind_mpn)
+
+    @classmethod
+    def bind_mpn(cls, model):
+        """Capacity mode for the MPN (None unbinds): when construct_graph takes the capacity graph build
+        (pemp_fully_graph_build_cap, a repeated fully-graph batch shape), it also queues `model`'s forward on
+        those buffers (pemp_mpn_forward_fully_cap) before it reads the detection counts back, and tags its
+        output so that model(x, edge_attr, edge_index, node_types=joint_det[:, 2]) on that output returns the
+        queued logits instead of launching again. Any other call of the model -- another graph, an input or
+        weight edited in between, a batch that overflowed the capacities -- runs the exact forward."""
+        cls._bound_mpn = model
 
     @classmethod
     def _host_counts_take(cls, L, dev, B):
@@ -217,6 +228,7 @@ class NaiveGraphConstructor:
         with NaiveGraphConstructor._mu:
             hint = NaiveGraphConstructor._graph_hint.get(gkey) if fully else None
         built = None
+        pending = None
         if hint is not None:
             # capacity mode: the graph build is queued before the counts are read, so the GPU builds
             # the graph while the host waits for them (pemp_fully_graph_build_cap)
@@ -232,6 +244,11 @@ class NaiveGraphConstructor:
             _lib.check(L.pemp_fully_graph_build_cap(
                 _lib.ptr(n_det), B, _lib.ptr(det), _lib.ptr(dsc), cap, _lib.ptr(feats), C, _lib.ptr(tags), F, J, H, W,
                 n_cap, e_cap, norm, mode, *[_lib.ptr(t) for t in bufs], st))
+            mpn = NaiveGraphConstructor._bound_mpn
+            if mpn is not None and not projected and J == getattr(mpn, "num_types", None):
+                pending_mpn = mpn
+                # the MPN behind the build, before the counts come back (capacity mode)
+                pending = mpn._forward_cap(bufs[0], bufs[6], bufs[1], n_cap, e_cap, n_det, cap, bufs[7], B)
             counts_l = self._wait_counts(counts_h, dev)
             built = bufs
         else:
@@ -268,6 +285,8 @@ class NaiveGraphConstructor:
             if proj_tags is not None:
                 joint_tags = self._gather_proj_tags(L, st, proj_tags, J, H, W, joint_det, batch_index, N, dev)
             _tag_fully(edge_index, built[7], counts_l, joint_det)
+            if pending is not None:
+                pending_mpn._attach_cap(pending, x, edge_attr, edge_index, joint_det, N, E_fully)
             return (x, edge_attr, edge_index, None, None, None, None, joint_det, None, None, None, joint_scores,
                     batch_index, None, joint_tags)
         x = torch.empty(N, C, dtype=torch.float32, device=dev)

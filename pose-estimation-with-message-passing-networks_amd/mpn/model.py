@@ -276,6 +276,10 @@ class NodeClassificationMPNSimple(nn.Module):
             return self._forward_blocks(x, edge_attr, edge_index, node_types, kwargs)
         if self.node_summary != "not":
             node_types = torch.tensor(TYPE_LUTS[self.node_summary], device=dev)[node_types]
+        else:
+            done = self._take_cap(x, edge_attr, edge_index, node_types)
+            if done is not None:      # queued by construct_graph ahead of the counts (capacity mode)
+                return done
         fully = _fully_graph(edge_index, node_types, N) if self.node_summary == "not" else None
         sym = fully is None and _sym_graph(edge_index)
         x = _as(x, torch.float32)
@@ -330,6 +334,76 @@ class NodeClassificationMPNSimple(nn.Module):
         if kwargs.get("validate", _VALIDATE or (_DEBUG_SYNC and (sym or fully is not None))):
             _lib.check(L.pemp_mpn_status(desc, N, E, _lib.ptr(ws), _lib.stream(dev)))
         # list lengths and .squeeze() semantics of NodeClassificationMPNSimple.py:81-97
+        preds_edge = [edge_logits[r].view(E, 1).squeeze() for r in range(n_rec)]
+        preds_node = [node_logits[r].view(N, 1).squeeze() for r in range(n_rec + 1)]
+        preds_class = [class_logits[r] for r in range(n_rec + 1)]
+        return preds_edge, preds_node, preds_class, [None]
+
+
+    # ---- capacity mode (graph_constructor.bind_mpn): the forward queued before the detection counts are known ----
+    def _forward_cap(self, x, edge_attr, joint_det, n_cap, e_cap, n_det, det_cap, node_off, B):
+        """Queue pemp_mpn_forward_fully_cap on the capacity buffers of pemp_fully_graph_build_cap (x [n_cap, C],
+        edge_attr [e_cap, A], joint_det [n_cap, 3], node_off [B + 1]) with the detection's device counts n_det.
+        Returns the pending result (logit buffer + the key it was computed under) or None when this model / batch
+        takes the exact forward (training, type summaries, unfused node MLPs, a detection capacity past the
+        closed-form limit, over-size capacities)."""
+        if self.training or self.node_summary != "not" or _FULLY_OFF or x.device.type != "cuda":
+            return None
+        if e_cap > self._edge_limit or self.num_types * n_cap > self._node_rows_limit:
+            return None
+        L = _lib.lib()
+        dev = x.device
+        node_types = joint_det[:, 2]
+        fw = self._weights(dev)
+        A = edge_attr.shape[1]
+        dkey = (A, x.shape[1], self.precision, 3)
+        if self._desc_key != dkey:
+            steps, aux = self.edge_steps, self.aux_loss_steps
+            self._n_rec = sum(1 for i in range(steps) if i >= steps - aux - 1)
+            self._desc = _lib.PempMpnDesc(self.num_types, self.num_joints, steps, aux, self.aggr_code, 64, A,
+                                          x.shape[1], PRECISIONS[self.precision], 3, 0)
+            self._desc_ref = ctypes.byref(self._desc)
+            self._desc_key = dkey
+        desc, n_rec = self._desc_ref, self._n_rec
+        ws = self._ws.get(L.pemp_mpn_workspace_size(desc, n_cap, e_cap), dev)
+        ne, nn_ = max(n_rec, 1) * e_cap, (n_rec + 1) * n_cap
+        a1 = (ne + 63) // 64 * 64
+        a2 = a1 + (nn_ + 63) // 64 * 64
+        buf = torch.empty(a2 + nn_ * self.num_joints, dtype=torch.float32, device=dev)
+        rc = L.pemp_mpn_forward_fully_cap(desc, fw.struct_ref, x.data_ptr(), edge_attr.data_ptr(),
+                                          node_types.data_ptr(), n_cap, e_cap, n_det.data_ptr(), det_cap,
+                                          node_off.data_ptr(), B, buf.data_ptr(), buf[a1:].data_ptr(),
+                                          buf[a2:].data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream(dev))
+        if rc == _lib.ERR_UNSUPPORTED:
+            return None           # the exact forward runs instead
+        _lib.check(rc)
+        return dict(buf=buf, a1=a1, a2=a2, n_rec=n_rec, key=(dev, self.precision, self._folded_key))
+
+    def _attach_cap(self, pending, x, edge_attr, edge_index, joint_det, N, E):
+        """Tag construct_graph's output with the queued result (the capacity batch fit: N, E are its counts)."""
+        edge_index._pemp_mpn = (self, pending, N, E, x.data_ptr(), x._version, edge_attr.data_ptr(),
+                                edge_attr._version, edge_index._version, joint_det.data_ptr(), joint_det._version)
+
+    def _take_cap(self, x, edge_attr, edge_index, node_types):
+        """The queued result of this exact graph, as forward returns it (once), or None (no tag, another model, an
+        input or weight changed since it was queued, already taken)."""
+        tag = getattr(edge_index, "_pemp_mpn", None)
+        if tag is None:
+            return None
+        mdl, pending, N, E, xp, xv, ep, ev, iv, jp, jv = tag
+        if (mdl is not self or x.data_ptr() != xp or x._version != xv or edge_attr.data_ptr() != ep
+                or edge_attr._version != ev or edge_index._version != iv or x.shape[0] != N
+                or edge_index.shape[1] != E or node_types.data_ptr() != jp + 16 or node_types.stride(0) != 3
+                or node_types._version != jv):
+            return None
+        self._weights(x.device)
+        if pending["key"] != (x.device, self.precision, self._folded_key):
+            return None
+        edge_index._pemp_mpn = None                            # one use: a repeated call computes
+        buf, a1, a2, n_rec, J = pending["buf"], pending["a1"], pending["a2"], pending["n_rec"], self.num_joints
+        edge_logits = buf[:max(n_rec, 1) * E].view(max(n_rec, 1), E)
+        node_logits = buf[a1:a1 + (n_rec + 1) * N].view(n_rec + 1, N)
+        class_logits = buf[a2:a2 + (n_rec + 1) * N * J].view(n_rec + 1, N, J)
         preds_edge = [edge_logits[r].view(E, 1).squeeze() for r in range(n_rec)]
         preds_node = [node_logits[r].view(N, 1).squeeze() for r in range(n_rec + 1)]
         preds_class = [class_logits[r] for r in range(n_rec + 1)]

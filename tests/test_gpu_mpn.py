@@ -263,6 +263,72 @@ def test_fully_graph_fast_prepare_is_identical(prec, monkeypatch):
     assert mm._fully_graph(ei2, types, x.shape[0]) is None      # a copy carries no tag
 
 
+@pytest.mark.parametrize("prec", ["f16x3", "fp32"])
+def test_capacity_mode_mpn(prec, monkeypatch):
+    """bind_mpn (capacity mode): construct_graph queues the MPN on the capacity build's buffers before the
+    counts reach the host; model(...) on that output returns the queued logits. They must equal the exact forward
+    on copies of the same graph bit for bit when the batch fits; a batch past the capacities (persons 6 after 3)
+    must run the exact forward; an in-place edit of x between the two calls must make the model compute again."""
+    from pemp_amd.mpn import model as mm
+    from pemp_amd.graph_constructor import NaiveGraphConstructor
+    B, J, H, W = 2, 17, 96, 104
+    NaiveGraphConstructor._graph_hint.clear()               # capacities from earlier tests' batches of this shape
+    gc = pcfg.inference_gc_config("fully", 5, False)
+    cfg = pcfg.published_mpn_config(J, 3, "attn")
+    model, _ = make_model(cfg, 1.25, prec)
+    feats = torch.from_numpy(syn.closed_form((B, 128, H, W), 0.25))
+    taken = []
+    orig_take = mm.NodeClassificationMPNSimple._take_cap
+
+    def take(self, *a):
+        r = orig_take(self, *a)
+        taken.append(r is not None)
+        return r
+
+    monkeypatch.setattr(mm.NodeClassificationMPNSimple, "_take_cap", take)
+    pemp_amd.bind_mpn(model)
+    try:
+        used = []
+        # (seed, persons, edit x in place before the model call)
+        for seed, persons, edit in ((1, 3, False), (2, 2, False), (3, 3, False), (4, 6, False), (5, 1, True),
+                                    (6, 2, False)):
+            hm = torch.from_numpy(syn.make_heatmaps(seed, B, J, H, W, persons, margin=4))
+            out = pemp_amd.get_graph_constructor(gc, scoremaps=hm.to(DEV), features=feats.to(DEV), tagmaps=None,
+                                                 joints_gt=None, factor_list=None, masks=None, device=DEV,
+                                                 testing=True, heatmaps=None, num_joints=J).construct_graph()
+            x, ea, ei, types = out[0], out[1], out[2], out[7][:, 2]
+            if edit:
+                x.add_(0)                                      # the queued result is stale now
+            taken.clear()
+            got = run(model, x, ea, ei, types)
+            used.append(bool(taken and taken[0]))
+            taken.clear()
+            again = run(model, x, ea, ei, types)               # a second call on the same graph computes
+            assert taken == [False]
+            ref = run(model, x.clone(), ea.clone(), ei.clone(), types.clone())
+            assert len(got[0]) == len(ref[0]) and len(got[1]) == len(ref[1])
+            for a, b, c in zip(got[0] + got[1] + got[2], ref[0] + ref[1] + ref[2], again[0] + again[1] + again[2]):
+                assert a.shape == b.shape and torch.equal(a, b) and torch.equal(c, b), (seed, persons)
+        # the first call sets the capacities (exact build); 6 persons overflow them
+        assert used == [False, True, True, False, False, True], used
+        # the same batch again and again: once the allocator hands back the same buffers, the library replays its
+        # captured HIP graph of the forward (second sight of an argument set: capture; then replays)
+        hm = torch.from_numpy(syn.make_heatmaps(2, B, J, H, W, 2, margin=4))
+        first = None
+        for _ in range(5):
+            out = pemp_amd.get_graph_constructor(gc, scoremaps=hm.to(DEV), features=feats.to(DEV), tagmaps=None,
+                                                 joints_gt=None, factor_list=None, masks=None, device=DEV,
+                                                 testing=True, heatmaps=None, num_joints=J).construct_graph()
+            got = run(model, out[0], out[1], out[2], out[7][:, 2])
+            flat = [t.clone() for t in got[0] + got[1] + got[2]]
+            if first is None:
+                first = flat
+            assert all(torch.equal(a, b) for a, b in zip(flat, first))
+            del out, got
+    finally:
+        pemp_amd.bind_mpn(None)
+
+
 @pytest.mark.parametrize("graph_type,persons,H", [("knn", 9, 160), ("knn", 28, 320), ("score_based", 9, 160),
                                                    ("feature_knn", 6, 128)])
 def test_symmetric_graph_fast_prepare_is_identical(graph_type, persons, H, monkeypatch):

@@ -1,5 +1,7 @@
 """cProfile of the host side of the bench step (GPU box): which Python functions the graph constructor and
-the MPN forward spend their host time in. usage: python tools/host_cprofile.py [workload]"""
+the MPN forward spend their host time in. usage: python tools/host_cprofile.py [workload]
+(PEMP_CAP=1: the model bound to the graph constructor, capacity mode, as bench.py runs fully-graph workloads)"""
+import time
 import cProfile
 import os
 import pstats
@@ -15,6 +17,17 @@ dev = torch.device("cuda", 0)
 gc = bench.pcfg.inference_gc_config(wl["graph"], 5, False)
 hm, feats, tags = bench.make_inputs(wl, 0, dev)
 model, _ = bench.make_model(wl, dev)
+if os.environ.get("PEMP_CAP"):
+    bench.pemp_amd.bind_mpn(model)
+for _ in range(5):
+    bench.run_step(wl, gc, model, hm, feats, tags, dev)
+torch.cuda.synchronize()
+with torch.no_grad():
+    t0 = time.perf_counter()
+    for _ in range(200):
+        bench.run_step(wl, gc, model, hm, feats, tags, dev)
+    torch.cuda.synchronize()
+    print(f"wall per step (serial, no profiler): {(time.perf_counter() - t0) / 200 * 1e3:.4f} ms", flush=True)
 for _ in range(5):
     bench.run_step(wl, gc, model, hm, feats, tags, dev)
 torch.cuda.synchronize()
@@ -26,4 +39,5 @@ with torch.no_grad():
 pr.disable()
 torch.cuda.synchronize()
 st = pstats.Stats(pr)
-st.sort_stats("tottime").print_stats(30)
+st.sort_stats("tottime").print_stats(25)
+st.sort_stats("cumulative").print_stats(25)
