@@ -2586,19 +2586,31 @@ struct NodeTableArgs {
   int NO, groups;
   float* NT;
   const int64_t* ne;   // capacity mode: device-side node count (N: the capacity)
+  // SUM variant (node_table_kernel<PREC, 1, true>): the node update of the same step first, from the aggregates
+  const float* agg;
+  const int* seg;
+  int T;
+  const float* upd_b;
 };
 
+#ifndef NODE_SUM_TABLE
+#define NODE_SUM_TABLE 1   // the middle steps' node update fused into the node-table launch
+#endif
 #ifndef PEMP_TBL_TILES
 #define PEMP_TBL_TILES 4
 #endif
 constexpr int TBL_TILES = PEMP_TBL_TILES;   // 16-node tiles per workgroup
 
-template <int PREC>
+// SUM: the node update x = ReLU(b + sum_t agg[n, t]) (node_rows_kernel ROWS_SUM, same operations and order) is
+// computed here for the tile's 16 rows, by every column group of the tile (the aggregates are re-read from L2 by
+// each group instead of a separate launch writing x and this one reading it back); group 0 also stores x.
+template <int PREC, int TILES = TBL_TILES, bool SUM = false>
 __global__ __launch_bounds__(256) void node_table_kernel(NodeTableArgs a) {
-  __shared__ __attribute__((aligned(16))) float xs[16 * TBL_TILES * RS];
+  static_assert(!SUM || TILES == 1, "the summing variant takes one 16-node tile per workgroup");
+  __shared__ __attribute__((aligned(16))) float xs[16 * TILES * RS];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
   const int chunk = blockIdx.x / a.groups, grp = blockIdx.x - chunk * a.groups;
-  const int64_t n0 = (int64_t)chunk * 16 * TBL_TILES, N = a.ne ? a.ne[0] : a.N;
+  const int64_t n0 = (int64_t)chunk * 16 * TILES, N = a.ne ? a.ne[0] : a.N;
   if (n0 >= N) return;   // (capacity grids)
   const int nob = a.NO / 16, ob = grp * 4 + wave, obc = min(ob, nob - 1);
   // this wave's weight fragment (rows 16 ob + c), issued first
@@ -2624,18 +2636,42 @@ __global__ __launch_bounds__(256) void node_table_kernel(NodeTableArgs a) {
     }
   }
   const float4 bb = ld4(a.pre_b + 16 * obc + 4 * g);
-  {
-  // X chunk -> LDS: 16 TBL_TILES rows x 32 float4, 2 TBL_TILES per thread
-    float4 t[2 * TBL_TILES];
+  if constexpr (SUM) {
+    // row r of the tile, features 4 q .. 4 q + 3: x0 and every type's aggregate and segment bounds in flight together
+    const int r = threadIdx.x >> 4, q = threadIdx.x & 15;
+    const int64_t n = n0 + r, nc = n < N ? n : N - 1;
+    const int T = a.T;
+    const float4 x0 = ld4(a.X + nc * 128 + 4 * q);
+    float4 y[MAXT];
+    int s0[MAXT], s1[MAXT];
 #pragma unroll
-    for (int k = 0; k < 2 * TBL_TILES; ++k) {
+    for (int t = 0; t < MAXT; ++t) {
+      const int tc = min(t, T - 1);
+      y[t] = ld4(a.agg + (nc * T + tc) * D + 4 * q);
+      s0[t] = a.seg[tc * N + nc];
+      s1[t] = a.seg[tc * N + nc + 1];
+    }
+    float4 v = ld4(a.upd_b + 4 * q);
+#pragma unroll
+    for (int t = 0; t < MAXT; ++t) {
+      if (t < T && s1[t] > s0[t]) { v.x += y[t].x; v.y += y[t].y; v.z += y[t].z; v.w += y[t].w; }
+    }
+    v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+    *reinterpret_cast<float4*>(&xs[r * RS + 4 * q]) = x0;
+    *reinterpret_cast<float4*>(&xs[r * RS + 64 + 4 * q]) = v;
+    if (grp == 0 && n < N) *reinterpret_cast<float4*>(const_cast<float*>(a.X) + n * 128 + 64 + 4 * q) = v;
+  } else {
+  // X chunk -> LDS: 16 TILES rows x 32 float4, 2 TILES per thread
+    float4 t[2 * TILES];
+#pragma unroll
+    for (int k = 0; k < 2 * TILES; ++k) {
       const int idx = threadIdx.x + 256 * k, row = idx >> 5, c4 = (idx & 31) * 4;
       const int64_t nn = min(n0 + row, N - 1);
       t[k] = ld4(a.X + nn * 128 + c4);
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int k = 0; k < 2 * TBL_TILES; ++k) {
+    for (int k = 0; k < 2 * TILES; ++k) {
       const int idx = threadIdx.x + 256 * k, row = idx >> 5, c4 = (idx & 31) * 4;
       *reinterpret_cast<float4*>(&xs[row * RS + c4]) = t[k];
     }
@@ -2643,7 +2679,7 @@ __global__ __launch_bounds__(256) void node_table_kernel(NodeTableArgs a) {
   __syncthreads();
   if (ob >= nob) return;
 #pragma unroll
-  for (int tile = 0; tile < TBL_TILES; ++tile) {
+  for (int tile = 0; tile < TILES; ++tile) {
     const int64_t nn = n0 + 16 * tile + c;
     if (n0 + 16 * tile >= N) break;               // uniform
     float x[8][4];
@@ -3481,7 +3517,23 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   const int table_groups = (NO / 16 + 3) / 4;
   const unsigned table_grid = (unsigned)(((N + 16 * TBL_TILES - 1) / (16 * TBL_TILES)) * table_groups);
   // x for the next stage (mode) + heads when slot >= 0, then the node table when `table`
+  // middle steps of the attention model (update block in the edge pass, no heads): the node update runs inside the
+  // node-table launch (node_table_kernel<PREC, 1, true>) instead of a launch of its own
+  const unsigned table_grid1 = (unsigned)(((N + 15) / 16) * table_groups);
   auto node_step = [&](int mode, bool table, int slot, bool dup) -> int {
+    if (mode == ROWS_SUM && table && slot < 0 && !ept && NODE_SUM_TABLE) {
+      NodeTableArgs ta{ws.X, N, w->pre_w, w->pre_b, w->pre_bf, NO, table_groups, ws.NT, ne, ws.agg, ws.seg, T,
+                       w->upd_b};
+      ProfScope prof("node_update_table", st);
+      if (table_prec == PEMP_PREC_F16X3)
+        hipLaunchKernelGGL((node_table_kernel<2, 1, true>), dim3(table_grid1), dim3(256), 0, st, ta);
+      else if (table_prec == PEMP_PREC_BF16X3)
+        hipLaunchKernelGGL((node_table_kernel<1, 1, true>), dim3(table_grid1), dim3(256), 0, st, ta);
+      else
+        hipLaunchKernelGGL((node_table_kernel<0, 1, true>), dim3(table_grid1), dim3(256), 0, st, ta);
+      PEMP_LAUNCH_CHECK();
+      return PEMP_OK;
+    }
     if (mode == -1 && w->upd_mlp.n_layers > 0) {     // hierarchical update MLP (dense-folded)
       NodeMlpArgs ma{ws.agg, ws.seg, T, N, w->upd_mlp, nmlp_max_out(w->upd_mlp), ws.X, ne};
       ProfScope prof("node_update", st);
@@ -3697,6 +3749,30 @@ static bool graphs_off() {
   return v;
 }
 
+// The null (legacy) stream cannot be captured: a caller on it gets its graphs captured on and replayed from a
+// private stream of the device, joined to the null stream by events around each replay.
+struct GraphStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+
+static GraphStream* graph_stream(int dev) {
+  static std::mutex mu;
+  static std::map<int, GraphStream*> table;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = table.find(dev);
+  if (it != table.end()) return it->second;
+  GraphStream* g = new GraphStream();
+  if (hipStreamCreateWithFlags(&g->s, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&g->fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&g->join, hipEventDisableTiming) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;   // (leaked once; graphs are then not used on the null stream)
+  }
+  table[dev] = g;
+  return g;
+}
+
 static int cap_forward_direct(const pemp_mpn_desc* desc, const pemp_mpn_weights* w, const float* x,
                               const float* edge_attr, const int64_t* node_types, int64_t n_cap, int64_t e_cap,
                               const int32_t* n_det, int det_cap, const int64_t* node_off, int B, float* edge_logits,
@@ -3737,14 +3813,30 @@ extern "C" int pemp_mpn_forward_fully_cap(const pemp_mpn_desc* desc, const pemp_
   static std::vector<CapGraph> cache;
   static std::vector<std::string> seen;   // argument sets launched directly once (most recent last)
   static uint64_t tick = 0;
-  const hipStream_t st = as_stream(stream);
+  const hipStream_t ust = as_stream(stream);
+  GraphStream* gs = ust ? nullptr : graph_stream(dev);
+  if (!ust && !gs)
+    return cap_forward_direct(desc, w, x, edge_attr, node_types, n_cap, e_cap, n_det, det_cap, node_off, B,
+                              edge_logits, node_logits, class_logits, workspace, workspace_bytes, stream);
+  const hipStream_t st = ust ? ust : gs->s;   // capture / replay stream
+  auto launch = [&](hipGraphExec_t exec) -> int {
+    if (gs) {                                 // null-stream caller: fork to the private stream and back
+      PEMP_HIP(hipEventRecord(gs->fork, ust));
+      PEMP_HIP(hipStreamWaitEvent(gs->s, gs->fork, 0));
+    }
+    PEMP_HIP(hipGraphLaunch(exec, st));
+    if (gs) {
+      PEMP_HIP(hipEventRecord(gs->join, gs->s));
+      PEMP_HIP(hipStreamWaitEvent(ust, gs->join, 0));
+    }
+    return PEMP_OK;
+  };
   {
     std::lock_guard<std::mutex> lk(mu);
     for (auto& e : cache)
       if (e.key == key) {
         e.used = ++tick;
-        PEMP_HIP(hipGraphLaunch(e.exec, st));
-        return PEMP_OK;
+        return launch(e.exec);
       }
     auto it = std::find(seen.begin(), seen.end(), key);
     if (it == seen.end()) {                 // first sight: direct launches
@@ -3764,9 +3856,13 @@ extern "C" int pemp_mpn_forward_fully_cap(const pemp_mpn_desc* desc, const pemp_
     }
   }
   // capture (thread-local mode: other threads' launches on other streams are unaffected)
-  PEMP_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+  if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+    (void)hipGetLastError();
+    return cap_forward_direct(desc, w, x, edge_attr, node_types, n_cap, e_cap, n_det, det_cap, node_off, B,
+                              edge_logits, node_logits, class_logits, workspace, workspace_bytes, stream);
+  }
   const int rc = cap_forward_direct(desc, w, x, edge_attr, node_types, n_cap, e_cap, n_det, det_cap, node_off, B,
-                                    edge_logits, node_logits, class_logits, workspace, workspace_bytes, stream);
+                                    edge_logits, node_logits, class_logits, workspace, workspace_bytes, st);
   hipGraph_t graph = nullptr;
   const hipError_t ec = hipStreamEndCapture(st, &graph);
   if (rc != PEMP_OK || ec != hipSuccess || !graph) {
@@ -3785,7 +3881,11 @@ extern "C" int pemp_mpn_forward_fully_cap(const pemp_mpn_desc* desc, const pemp_
     return cap_forward_direct(desc, w, x, edge_attr, node_types, n_cap, e_cap, n_det, det_cap, node_off, B,
                               edge_logits, node_logits, class_logits, workspace, workspace_bytes, stream);
   }
-  PEMP_HIP(hipGraphLaunch(exec, st));
+  const int rl = launch(exec);
+  if (rl != PEMP_OK) {
+    (void)hipGraphExecDestroy(exec);
+    return rl;
+  }
   std::lock_guard<std::mutex> lk(mu);
   constexpr size_t CAP_GRAPHS = 16;
   if (cache.size() >= CAP_GRAPHS) {

@@ -3,7 +3,7 @@
 # (build_ab/libpemp_<v>.so; "default" = the in-tree library). Prints value + per-kernel us.
 for v in "$@"; do
   if [ "$v" = default ]; then unset PEMP_LIB; else export PEMP_LIB=$PWD/build_ab/libpemp_$v.so; fi
-  timeout -k 10 150 python bench.py --no-cpu-baseline --steps 10 > gpurun_out/ab_$v.log 2>&1 || { echo "$v failed"; exit 1; }
+  timeout -k 10 150 python bench.py --no-cpu-baseline --steps 10 $AB_ARGS > gpurun_out/ab_$v.log 2>&1 || { echo "$v failed"; exit 1; }
   python - "$v" <<'PY'
 import json, sys
 v = sys.argv[1]
