@@ -39,6 +39,9 @@ namespace {
 #ifndef PEMP_DETECT_CLOCKS
 #define PEMP_DETECT_CLOCKS 0
 #endif   // diagnostics: phase clocks of the fused select + emit stage (printf)
+#ifndef NMS_THR_POS
+#define NMS_THR_POS 1   // positive thresholds take the one-compare threshold test (nms_strips_kernel TP)
+#endif
 #ifndef NMS_CLAMPED_LOADS
 #define NMS_CLAMPED_LOADS 1
 #endif
@@ -463,7 +466,9 @@ __device__ __forceinline__ void load_unit(const float* __restrict__ s, const Det
   }
 }
 
-template <int P, int MODE, bool MASKED, int PROJ>   // PROJ: 0 dense maps, 1 projected, 2 projected separable
+// PROJ: 0 dense maps, 1 projected, 2 projected separable. TP: the threshold is positive, so !(v < thr) alone
+// decides a threshold pixel (v = 0 fails it; NaN passes both forms): one compare per pixel fewer.
+template <int P, int MODE, bool MASKED, int PROJ, bool TP = false>
 __global__ __launch_bounds__(NT1) void nms_strips_kernel(
     const float* __restrict__ s, const float* __restrict__ masks, DetectGeom g, float thr, int use_thr,
     float* __restrict__ cand_v, int* __restrict__ cand_i, float* __restrict__ neg_v, int* __restrict__ neg_i,
@@ -531,20 +536,24 @@ __global__ __launch_bounds__(NT1) void nms_strips_kernel(
     const int rows = min(SR, H - y0);
     const unsigned vmask = lane_ok ? (rows >= 32 ? 0xffffffffu : ((1u << rows) - 1u)) : 0u;
     float v[SR];
-    unsigned int tbits = 0, nnbits = 0, posbits = 0;
+    unsigned int tbits = 0, nnbits = 0;
+    // the lane's largest value (a positive one marks the unit for ranking): one max per pixel instead of a
+    // compare, a select and an or of a per-row bit. Rows past the plane (last band only) are included: a value
+    // there can only mark a unit whose ranking then finds nothing valid (it masks those rows) and writes the
+    // same sentinel list as an unmarked unit.
+    float pmax = -INFINITY;
 #pragma unroll
     for (int j = 0; j < SR; ++j) {
       float jm = (vm[j] == c[j]) ? 1.0f : 0.0f;
       if (MASKED) jm = jm * masks[((size_t)b * H + min(y0 + j, H - 1)) * W + min(max(x, 0), W - 1)];
       const float vj = c[j] * jm;                       // ConstructGraph.py:1162-1165
       v[j] = vj;
-      tbits |= (unsigned)(!(vj < thr) && vj != 0.0f) << j;
+      tbits |= (unsigned)(TP ? !(vj < thr) : (!(vj < thr) && vj != 0.0f)) << j;
       nnbits |= (unsigned)(vj >= 0.0f) << j;
-      posbits |= (unsigned)(vj > 0.0f) << j;
+      pmax = fmaxf(pmax, vj);                            // (fmaxf skips a NaN operand)
     }
     tbits &= vmask;
     nnbits &= vmask;
-    posbits &= vmask;
     if (!use_thr) tbits = 0;
     cbits[(size_t)u * 64 + lane] = (cmask_t)tbits;
     int cnt = __popc(tbits), nonneg = __popc(nnbits);
@@ -553,7 +562,7 @@ __global__ __launch_bounds__(NT1) void nms_strips_kernel(
       cnt += __shfl_xor(cnt, off);
       nonneg += __shfl_xor(nonneg, off);
     }
-    const bool anypos = __ballot(posbits != 0) != 0;
+    const bool anypos = __ballot(lane_ok && pmax > 0.0f) != 0;
     if (lane == 0) { tile_count[u] = cnt; tile_nonneg[u] = nonneg; }
     const int base_id = y0 * W + x;
     if (MODE == MODE_ALL || anypos || nonneg < K) {   // (uniform; rare with MODE_POS) invalid rows -> NaN
@@ -1251,8 +1260,14 @@ static void launch_nms(const float* s, const float* masks, const DetectGeom& g, 
     hipLaunchKernelGGL(kern, dim3(grid), dim3(NT1), 0, st, s, masks, g, thr, use_thr, w.cand_v, w.cand_i, w.neg_v,
                        w.neg_i, w.tile_count, w.tile_nonneg, w.cbits, pj, w.pflag);
   };
-  if (masks) launch(nms_strips_kernel<P, MODE, true, PROJ>);
-  else launch(nms_strips_kernel<P, MODE, false, PROJ>);
+  const bool tp = MODE == MODE_POS && thr > 0.0f && NMS_THR_POS;
+  if (masks) {
+    if (tp) launch(nms_strips_kernel<P, MODE, true, PROJ, MODE == MODE_POS>);
+    else launch(nms_strips_kernel<P, MODE, true, PROJ, false>);
+  } else {
+    if (tp) launch(nms_strips_kernel<P, MODE, false, PROJ, MODE == MODE_POS>);
+    else launch(nms_strips_kernel<P, MODE, false, PROJ, false>);
+  }
 }
 
 template <int MODE, int PROJ>
