@@ -2596,6 +2596,9 @@ struct NodeTableArgs {
 #ifndef NODE_SUM_TABLE
 #define NODE_SUM_TABLE 1   // the middle steps' node update fused into the node-table launch
 #endif
+#ifndef NODE_SUM_TABLE_MAX_MB
+#define NODE_SUM_TABLE_MAX_MB 16   // ... while its aggregate re-reads (N T 256 B x column groups) stay below this
+#endif
 #ifndef PEMP_TBL_TILES
 #define PEMP_TBL_TILES 4
 #endif
@@ -3521,7 +3524,10 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   // node-table launch (node_table_kernel<PREC, 1, true>) instead of a launch of its own
   const unsigned table_grid1 = (unsigned)(((N + 15) / 16) * table_groups);
   auto node_step = [&](int mode, bool table, int slot, bool dup) -> int {
-    if (mode == ROWS_SUM && table && slot < 0 && !ept && NODE_SUM_TABLE) {
+    // (every column group re-reads the tile's aggregates: worth it while those re-reads stay small -- C2 -- not at
+    // C3, where they are ~100 MB per call and the fused launch only ties the two it replaces)
+    if (mode == ROWS_SUM && table && slot < 0 && !ept && NODE_SUM_TABLE &&
+        N * T * 256 * (int64_t)table_groups <= (int64_t)NODE_SUM_TABLE_MAX_MB << 20) {
       NodeTableArgs ta{ws.X, N, w->pre_w, w->pre_b, w->pre_bf, NO, table_groups, ws.NT, ne, ws.agg, ws.seg, T,
                        w->upd_b};
       ProfScope prof("node_update_table", st);
