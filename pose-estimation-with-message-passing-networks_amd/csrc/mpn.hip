@@ -3282,9 +3282,10 @@ extern "C" size_t pemp_mpn_workspace_size(const pemp_mpn_desc* desc, int64_t N, 
   return bytes;
 }
 
-// (A HIP-graph replay of repeated identical forwards was measured slower on this stack: the
-// isolated forward 0.252 vs 0.242 ms, and re-captures whenever the caching allocator alternates
-// buffers. Forwards launch directly.)
+// (Exact forwards launch directly: a HIP-graph replay of repeated identical exact forwards measured slower (the
+// isolated forward 0.252 vs 0.242 ms, re-captured whenever N / E or the allocator's buffers change). The
+// capacity-mode forward, whose arguments repeat from step to step, is replayed from a graph:
+// pemp_mpn_forward_fully_cap.)
 // fully_node_off != NULL: edge_index is the fully graph of the batch with these per-image node
 // offsets (device, [fully_B + 1]) -> the closed-form prepare (fully_prepare_kernel)
 #ifdef PEMP_STAMPS
