@@ -2593,6 +2593,9 @@ struct NodeTableArgs {
   const float* upd_b;
 };
 
+#ifndef EMBED_ON_SIDE
+#define EMBED_ON_SIDE 1   // capacity mode: the edge embedding on the prelude side stream (see mpn_forward_impl)
+#endif
 #ifndef NODE_SUM_TABLE
 #define NODE_SUM_TABLE 1   // the middle steps' node update fused into the node-table launch
 #endif
@@ -3651,8 +3654,14 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
     return rc;
   }
   // the edge embedding on the launch stream once the order is ready: the join's wait resolves behind the node
-  // kernels (a join after the embedding waited ~13 us for the cross-stream event, measured)
-  if (ss) {
+  // kernels (a join after the embedding waited ~13 us for the cross-stream event, measured). Inside a captured
+  // capacity-mode forward the join is a graph edge, not an event wait: there the embedding stays on the side
+  // stream, right behind the order, concurrent with the node embedding and first table (EMBED_ON_SIDE)
+  if (ss && cap_ndet && EMBED_ON_SIDE) {
+    if ((rc = edge_embed())) { join_side(); return rc; }
+    join_side();
+    pst = st;
+  } else if (ss) {
     pst = st;
     join_side();
     if ((rc = edge_embed())) return rc;
