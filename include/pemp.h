@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define PEMP_ABI_VERSION 15
+#define PEMP_ABI_VERSION 16
 
 enum {
   PEMP_OK = 0,
@@ -199,6 +199,11 @@ int pemp_knn_graph_build(const int64_t* joint_det, const int64_t* node_off, cons
  * as nvcc compiles it), ties by node index; a NaN distance ranks last. The workspace also holds the
  * sum_b n_b^2 distance keys (pemp_feature_knn_workspace_size). */
 size_t pemp_feature_knn_workspace_size(const int64_t* node_off_host, int B);
+/* Byte offsets, inside a knn build's workspace, of the fast path's bit rows ([N][8] uint64), row starts ([N]
+ * int32) and per-image edge counts ([B] int64) (offs[0..2]), for pemp_mpn_forward_knn; feature != 0 for a
+ * pemp_feature_knn_graph_build workspace. Returns PEMP_ERR_UNSUPPORTED when the batch would not take the fast
+ * path (an image over 512 nodes). */
+int pemp_knn_rows_layout(const int64_t* node_off_host, int B, int feature, size_t* offs);
 int pemp_feature_knn_graph_build(const float* x, int C, const int64_t* joint_det, const int64_t* node_off,
                                  const int64_t* node_off_host, int B, int k, void* workspace,
                                  size_t workspace_bytes, int64_t e_cap, int64_t* edge_buf,
@@ -449,6 +454,21 @@ int pemp_mpn_forward_fully_cap(const pemp_mpn_desc* desc, const pemp_mpn_weights
 int pemp_mpn_forward_sym(const pemp_mpn_desc* desc, const pemp_mpn_weights* weights, const float* x,
                          const float* edge_attr, const int64_t* edge_index, const int64_t* node_types,
                          int64_t N, int64_t E, float* edge_logits, float* node_logits, float* class_logits,
+                         void* workspace, size_t workspace_bytes, void* stream);
+
+/* pemp_mpn_forward for the knn graph of pemp_knn_graph_build / pemp_feature_knn_graph_build's fast path (every
+ * image <= 512 nodes), handed over as the bit rows that build emitted the edges from (pemp_knn_rows_layout):
+ * knn_rows [N][8] uint64 (bit j of word w of row n: the edge n -> node 64 w + j of n's image), knn_rowstart [N]
+ * int32 (the row's first edge inside its image) and ecount [B] int64 (edges per image), all device, from the
+ * same build as edge_index. The edge order then comes from popcounts of the rows in one launch instead of the
+ * symmetric prepare's three; results are identical to pemp_mpn_forward_sym's. B <= 64, N <= 4096 and
+ * node_off_host[B] == N (checked); rows that do not belong to edge_index break the contract (reported by
+ * pemp_mpn_status through the edge total, logits undefined, every index in range). */
+int pemp_mpn_forward_knn(const pemp_mpn_desc* desc, const pemp_mpn_weights* weights, const float* x,
+                         const float* edge_attr, const int64_t* edge_index, const int64_t* node_types,
+                         int64_t N, int64_t E, const void* knn_rows, const int32_t* knn_rowstart,
+                         const int64_t* node_off, const int64_t* node_off_host, const int64_t* ecount, int B,
+                         float* edge_logits, float* node_logits, float* class_logits,
                          void* workspace, size_t workspace_bytes, void* stream);
 
 /* The edge-ordering part of pemp_mpn_forward (type-major counting sort of edge_index by (source type,

@@ -9,7 +9,7 @@ import os
 
 LIB_PATH = os.environ.get("PEMP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc",
                                                      "libpemp.so")
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 ERR_INVALID_ARG, ERR_HIP, ERR_WORKSPACE, ERR_UNSUPPORTED = -1, -2, -3, -4
 
@@ -72,6 +72,7 @@ SIGNATURES = {
     "pemp_knn_graph_build": (c_i32, [c_p, c_p, c_p, c_i32, c_i32, c_p, c_sz, c_i64, c_p, c_p, c_p, c_i32, c_p,
                                      c_i32, c_f32, c_i32, c_p, c_p]),
     "pemp_feature_knn_workspace_size": (c_sz, [c_p, c_i32]),
+    "pemp_knn_rows_layout": (c_i32, [c_p, c_i32, c_i32, c_p]),
     "pemp_feature_knn_graph_build": (c_i32, [c_p, c_i32, c_p, c_p, c_p, c_i32, c_i32, c_p, c_sz, c_i64, c_p, c_p,
                                              c_p, c_i32, c_p, c_i32, c_f32, c_i32, c_p, c_p]),
     "pemp_score_graph_workspace_size": (c_sz, [c_p, c_i32, c_i32]),
@@ -93,6 +94,9 @@ SIGNATURES = {
                                            c_p, c_i64, c_i64, c_p, c_i32, c_p, c_i32, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "pemp_mpn_forward_sym": (c_i32, [ctypes.POINTER(PempMpnDesc), ctypes.POINTER(PempMpnWeights), c_p, c_p, c_p,
                                      c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "pemp_mpn_forward_knn": (c_i32, [ctypes.POINTER(PempMpnDesc), ctypes.POINTER(PempMpnWeights), c_p, c_p, c_p,
+                                     c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_i32, c_p, c_p, c_p, c_p, c_sz,
+                                     c_p]),
     "pemp_mpn_prepare": (c_i32, [ctypes.POINTER(PempMpnDesc), c_p, c_p, c_i64, c_i64, c_p, c_sz, c_p]),
     "pemp_mpn_edge_image_floats": (c_sz, [ctypes.POINTER(PempMpnDesc), ctypes.POINTER(PempMpnWeights)]),
     "pemp_mpn_edge_image": (c_i32, [ctypes.POINTER(PempMpnDesc), ctypes.POINTER(PempMpnWeights), c_p, c_sz, c_p]),

@@ -1378,6 +1378,21 @@ extern "C" size_t pemp_feature_knn_workspace_size(const int64_t* node_off_host, 
   return bytes;
 }
 
+extern "C" int pemp_knn_rows_layout(const int64_t* node_off_host, int B, int feature, size_t* offs) {
+  PEMP_CHECK_ARG(node_off_host && B > 0 && offs, "pemp_knn_rows_layout: bad args");
+  for (int b = 0; b < B; ++b)
+    if (node_off_host[b + 1] - node_off_host[b] > KNN_LDS_MAXN) {
+      set_error("pemp_knn_rows_layout: image %d over %d nodes (no bit rows)", b, KNN_LDS_MAXN);
+      return PEMP_ERR_UNSUPPORTED;
+    }
+  char* const base = reinterpret_cast<char*>(4096);   // (any aligned base: offsets only)
+  const KnnWs w = knn_carve(base, node_off_host, B, nullptr, feature != 0);
+  offs[0] = (size_t)(reinterpret_cast<char*>(w.rows) - base);
+  offs[1] = (size_t)(reinterpret_cast<char*>(w.rowstart) - base);
+  offs[2] = (size_t)(reinterpret_cast<char*>(w.ecount) - base);
+  return PEMP_OK;
+}
+
 extern "C" int pemp_feature_knn_graph_build(const float* x, int C, const int64_t* joint_det, const int64_t* node_off,
                                             const int64_t* node_off_host, int B, int k, void* workspace,
                                             size_t workspace_bytes, int64_t e_cap, int64_t* edge_buf,

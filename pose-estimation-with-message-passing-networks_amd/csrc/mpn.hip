@@ -3223,6 +3223,283 @@ __global__ __launch_bounds__(1024) void sym_scan_kernel(const int* __restrict__ 
   type_split(tb, sh[1], T, G, gt, wg_start);
 }
 
+// ---- knn prepare (pemp_mpn_forward_knn): the graph constructor's knn graph (knn_mpn_graph / feature_knn_mpn_graph,
+// ConstructGraph.py:363-374) handed over as the bit rows its build emitted the edges from (graph.hip,
+// knn_rows_kernel / knn_emit_rows_kernel): row n = bit mask R[n][w] over the image-local nodes 64 w + j, the edge
+// (n -> m) has id ebase_b + rowstart[n] + #{bits of row n below m}, and R is symmetric (A | A^T). Then
+//   cnt(t, d)  = sum_w popcount(R[d][w] & M_t[b][w])     (M_t: the type-t nodes of d's image as bit words),
+//   E_t        = sum over type-t nodes x of popcount(R[x]) (symmetry: the type-t sources of every row),
+//   the (x -> d) id is a popcount of row x below d (no search),
+// so the three launches of the symmetric prepare (rows with their binary searches, the scan, the placement)
+// collapse into one: blocks (t, chunk of KP_CH rows) each count and scan all N rows for type t in LDS (one round
+// of row loads, the type masks from the rows' own types) and place their chunk's sources through an LDS list,
+// entry-parallel (a second round of loads: one word of each source row and its start). The same arrays as
+// launch_prepare_sym's (tested bit for bit).
+#ifndef PEMP_KP_CLOCKS
+#define PEMP_KP_CLOCKS 0
+#endif
+constexpr int KP_MAXB = 64, KP_MAXN = 4096, KP_W = 8;   // images, nodes per batch, bit words per row (512 nodes)
+constexpr int KP_LIST = 12288;                          // sources one block lists in LDS (else placed row by row)
+constexpr int KP_CH = 256;                              // rows placed per block (a divisor of 1024)
+
+struct KnnPrepArgs {
+  const unsigned long long* R;   // [N][KP_W]
+  const int* rowstart;           // [N] row start inside its image
+  const int64_t* node_off;       // [B + 1]
+  const int64_t* ecount;         // [B] edges per image
+  int B;
+  const int64_t* types;
+  int64_t ts, N, E;
+  int T, G;
+  int *seg, *wg_start, *s_src, *s_dst, *s_orig, *err;
+  int list_cap;                  // <= KP_LIST (PEMP_KNN_LIST_CAP: the row-by-row placement in tests)
+};
+
+__device__ __forceinline__ int kp_image(const int* noff, int B, int d) {
+  int lo = 0, hi = B - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (noff[mid] <= d) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(1024) void knn_prepare_kernel(KnnPrepArgs a) {
+  __shared__ unsigned long long M[KP_MAXB * KP_W];   // bit j of word (b, w): node 64 w + j of image b has type t
+  __shared__ int noff[KP_MAXB + 1], ebase[KP_MAXB + 1];
+  __shared__ int tot[MAXT + 1], tst[MAXT + 1], gt[MAXT], wsum[16];
+  __shared__ int bad_sh;
+  __shared__ int cs[KP_MAXN];                        // cnt(t, d), then the segment starts
+  __shared__ unsigned short pw[KP_MAXN][KP_W];       // entries of row n in its words before w
+  __shared__ int lst[KP_LIST];                       // the chunk's sources in segment order: x << 10 | (d - d0)
+  __shared__ int cend;
+  constexpr int SPT = KP_MAXN / 1024;
+  const int t = blockIdx.x, T = a.T, B = a.B, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int N = (int)a.N;
+#if PEMP_KP_CLOCKS   // diagnostics: per-phase wall clock (100 MHz) of two blocks, printed
+  long long clk[6];
+  clk[0] = wall_clock64();
+#define KP_CLK(i) clk[i] = wall_clock64()
+#else
+#define KP_CLK(i) (void)0
+#endif
+  // the words and types of this thread's first two rows, in flight with the offsets (words past a row's image
+  // are masked below: R is [N][KP_W])
+  unsigned long long rr[2][KP_W];
+  int64_t tr[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int d = tid + 1024 * i;
+#pragma unroll
+    for (int w = 0; w < KP_W; ++w) rr[i][w] = d < N ? a.R[(int64_t)d * KP_W + w] : 0ull;
+    tr[i] = d < N ? a.types[(int64_t)d * a.ts] : -1;
+  }
+  if (tid <= B) noff[tid] = (int)a.node_off[tid];
+  if (wave == 1) {                                   // edge id base of every image (B <= 64)
+    const int e = lane < B ? (int)a.ecount[lane] : 0;
+    int x = e;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(x, o);
+      if (lane >= o) x += v;
+    }
+    if (lane < B) ebase[lane] = x - e;
+    if (lane == B - 1) ebase[B] = x;
+  }
+  if (tid <= MAXT) tot[tid] = 0;
+  if (tid == 0) bad_sh = 0;
+  for (int q = tid; q < B * KP_W; q += 1024) M[q] = 0ull;
+  __syncthreads();
+  KP_CLK(1);
+  // type-t masks of every image word, from the rows' own types (no second round of loads)
+  bool bad = false;
+  auto mark = [&](int d, int64_t tt) {
+    if (tt < 0 || tt >= T) bad = true;               // skipped as a source, like mpn_count_kernel
+    if (tt == t) {
+      const int b = kp_image(noff, B, d), dl = d - noff[b];
+      atomicOr(&M[b * KP_W + (dl >> 6)], 1ull << (dl & 63));
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+    if (tid + 1024 * i < N) mark(tid + 1024 * i, tr[i]);
+  for (int d = tid + 2048; d < N; d += 1024) mark(d, a.types[(int64_t)d * a.ts]);
+  if (__ballot(bad) && lane == 0) bad_sh = 1;
+  __syncthreads();
+  KP_CLK(2);
+  // every row: cnt(t, d), its word prefix counts and its degree (the per-type edge totals)
+  auto row = [&](int d, const unsigned long long* v, int64_t tt) {
+    const int b = kp_image(noff, B, d), nb = noff[b + 1] - noff[b], wpr = (nb + 63) >> 6;
+    int c = 0, deg = 0;
+#pragma unroll
+    for (int w = 0; w < KP_W; ++w) {
+      pw[d][w] = (unsigned short)deg;
+      if (w < wpr) {
+        c += __popcll(v[w] & M[b * KP_W + w]);
+        deg += __popcll(v[w]);
+      }
+    }
+    cs[d] = c;
+    if (tt >= 0 && tt < T) atomicAdd(&tot[tt], deg);
+  };
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+    if (tid + 1024 * i < N) row(tid + 1024 * i, rr[i], tr[i]);
+  for (int d = tid + 2048; d < N; d += 1024) {
+    unsigned long long v[KP_W];
+#pragma unroll
+    for (int w = 0; w < KP_W; ++w) v[w] = a.R[(int64_t)d * KP_W + w];
+    row(d, v, a.types[(int64_t)d * a.ts]);
+  }
+  __syncthreads();
+  KP_CLK(3);
+  int base = 0;
+  for (int u = 0; u < t; ++u) base += tot[u];
+  const int d0 = blockIdx.y * KP_CH, d1 = min(N, d0 + KP_CH);   // this block's rows (placement, seg)
+  {                                                  // exclusive scan of cs in place (SPT counts per thread)
+    int v[SPT], local = 0;
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+      const int d = tid * SPT + j;
+      v[j] = d < N ? cs[d] : 0;
+      local += v[j];
+    }
+    int x = local;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    int run = base + x - local;
+    for (int w2 = 0; w2 < wave; ++w2) run += wsum[w2];
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+      const int d = tid * SPT + j;
+      if (d < N) cs[d] = run;
+      if (d >= d0 && d < d1) a.seg[(int64_t)t * N + d] = run;
+      run += v[j];
+    }
+    if (tid == 1023) cend = run;                     // the end of type t's segments
+  }
+  __syncthreads();
+  KP_CLK(4);
+  // placement: the type-t sources x of row d in ascending order; the (x -> d) id = the image's base + row x's
+  // start + its entries before d (word prefix from LDS + one word of row x). The chunk's positions are contiguous
+  // ([p0, p1)): each row lists its sources in LDS, then the list is placed entry-parallel (coalesced stores).
+  const int p0 = d0 < d1 ? cs[d0] : 0, p1 = d1 < N ? cs[d1] : cend;
+  if (p1 - p0 <= a.list_cap) {                       // (block-uniform)
+    // row d is listed by the thread that loaded it (d = tid + 1024 i, rr[i])
+    const int dr = (d0 & ~1023) + tid, ir = d0 >> 10;
+    if (dr >= d0 && dr < d1) {
+      const int b = kp_image(noff, B, dr), ob = noff[b], nb = noff[b + 1] - ob, wpr = (nb + 63) >> 6;
+      int q = cs[dr] - p0;
+#pragma unroll
+      for (int w = 0; w < KP_W; ++w) {               // (static word indices: rr stays in registers)
+        if (w >= wpr) break;
+        unsigned long long r = ir == 0 ? rr[0][w] : ir == 1 ? rr[1][w] : a.R[(int64_t)dr * KP_W + w];
+        r &= M[b * KP_W + w];
+        while (r) {
+          lst[q++] = (ob + 64 * w + __builtin_ctzll(r)) << 10 | (dr - d0);
+          r &= r - 1ull;
+        }
+      }
+    }
+    __syncthreads();
+    for (int i0 = 0; i0 < p1 - p0; i0 += 4096) {
+      int xs[4], ds[4], rs[4];
+      unsigned long long wd[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {                  // 4 entries per thread, all loads in flight together
+        const int i = i0 + k * 1024 + tid;
+        xs[k] = -1;
+        if (i < p1 - p0) {
+          const int v = lst[i];
+          xs[k] = v >> 10;
+          ds[k] = d0 + (v & 1023);
+          const int b = kp_image(noff, B, ds[k]);
+          wd[k] = a.R[(int64_t)xs[k] * KP_W + ((ds[k] - noff[b]) >> 6)];
+          rs[k] = a.rowstart[xs[k]] + ebase[b];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (xs[k] >= 0) {
+          const int i = i0 + k * 1024 + tid;
+          const int dl = ds[k] - noff[kp_image(noff, B, ds[k])];
+          a.s_src[p0 + i] = xs[k];
+          a.s_dst[p0 + i] = ds[k];
+          a.s_orig[p0 + i] = rs[k] + pw[xs[k]][dl >> 6] + __popcll(wd[k] & ((1ull << (dl & 63)) - 1ull));
+        }
+      }
+    }
+  } else if (d0 + tid < d1) {                        // row by row, 8 sources at a time
+    const int d = d0 + tid;
+    const int b = kp_image(noff, B, d), ob = noff[b], nb = noff[b + 1] - ob, wpr = (nb + 63) >> 6;
+    const int dl = d - ob, dw = dl >> 6;
+    const unsigned long long below = (1ull << (dl & 63)) - 1ull;
+    const int eb = ebase[b];
+    int pos = cs[d];
+    unsigned long long rw[KP_W];
+#pragma unroll
+    for (int w = 0; w < KP_W; ++w) rw[w] = w < wpr ? a.R[(int64_t)d * KP_W + w] & M[b * KP_W + w] : 0ull;
+    for (;;) {
+      int xs[8], n = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {                  // the next (up to) 8 sources, from the bits alone
+        xs[k] = -1;                                  // (static indices only: rw stays in registers)
+        bool got = false;
+#pragma unroll
+        for (int w = 0; w < KP_W; ++w) {
+          if (!got && rw[w] != 0ull) {
+            xs[k] = ob + 64 * w + __builtin_ctzll(rw[w]);
+            rw[w] &= rw[w] - 1ull;
+            got = true;
+          }
+        }
+        if (got) n = k + 1;
+      }
+      if (n == 0) break;
+      unsigned long long wd[8];
+      int rs[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {                  // all their loads in flight together
+        wd[k] = xs[k] >= 0 ? a.R[(int64_t)xs[k] * KP_W + dw] : 0ull;
+        rs[k] = xs[k] >= 0 ? a.rowstart[xs[k]] : 0;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (xs[k] >= 0) {
+          a.s_src[pos + k] = xs[k];
+          a.s_dst[pos + k] = d;
+          a.s_orig[pos + k] = eb + rs[k] + pw[xs[k]][dw] + __popcll(wd[k] & below);
+        }
+      }
+      pos += n;
+      if (n < 8) break;
+    }
+  }
+#if PEMP_KP_CLOCKS
+  __syncthreads();
+  KP_CLK(5);
+  if (tid == 0 && (t == 0 || t == T - 1))
+    printf("kp block %d,%d: start %lld init +%lld masks +%lld rows +%lld scan +%lld placed +%lld\n", t, blockIdx.y,
+           clk[0], clk[1] - clk[0], clk[2] - clk[0], clk[3] - clk[0], clk[4] - clk[0], clk[5] - clk[0]);
+#endif
+  if (t != T - 1 || blockIdx.y != 0) return;         // (block-uniform) one block closes seg and the split
+  if (tid == 0) {
+    int acc = 0;
+    for (int u = 0; u < T; ++u) { tst[u] = acc; acc += tot[u]; }
+    tst[T] = acc;
+    a.seg[(int64_t)T * N] = acc;
+    a.err[0] = (bad_sh ? 2 : 0) | (acc != a.E || ebase[B] != a.E ? 4 : 0);
+    a.err[1] = a.err[2] = a.err[3] = 0;
+  }
+  __syncthreads();
+  type_split(tst, tst[T], T, a.G, gt, a.wg_start);
+}
+
 static int launch_prepare(const pemp_mpn_desc* desc, const int64_t* edge_index, const int64_t* node_types, int64_t N,
                           int64_t E, const MpnWs& ws, hipStream_t st) {
   const int T = desc->num_types;
@@ -3347,7 +3624,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
                             int64_t N, int64_t E, float* edge_logits, float* node_logits, float* class_logits,
                             void* workspace, size_t workspace_bytes, void* stream, const int64_t* fully_node_off,
                             int fully_B, int fully_nmax, bool sym = false, const int32_t* cap_ndet = nullptr,
-                            int cap_det = 0) {
+                            int cap_det = 0, const KnnPrepArgs* knn = nullptr) {
   PEMP_CHECK_ARG(desc && w, "pemp_mpn_forward: null desc/weights");
   const int T = desc->num_types, J = desc->num_joints;
   PEMP_CHECK_ARG(desc->hidden == 64, "pemp_mpn_forward: hidden width must be 64 (got %d)", desc->hidden);
@@ -3465,6 +3742,24 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
       const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(64, ((int64_t)T * fully_nmax + 511) / 512));
       ProfScope prof("mpn_prepare", pst);
       hipLaunchKernelGGL(fully_prepare_kernel, dim3(gx, (unsigned)fully_B), dim3(256), 0, pst, fa);
+      PEMP_LAUNCH_CHECK();
+    } else if (knn && N > 0) {
+      KnnPrepArgs ka = *knn;
+      ka.types = node_types;
+      ka.ts = tstride;
+      ka.N = N;
+      ka.E = E;
+      ka.T = T;
+      ka.G = std::max(num_cus(), T);
+      ka.seg = ws.seg;
+      ka.wg_start = ws.wg_start;
+      ka.s_src = ws.s_src;
+      ka.s_dst = ws.s_dst;
+      ka.s_orig = ws.s_orig;
+      ka.err = ws.err;
+      ProfScope prof("mpn_prepare", pst);
+      hipLaunchKernelGGL(knn_prepare_kernel, dim3((unsigned)T, (unsigned)((N + KP_CH - 1) / KP_CH)), dim3(1024), 0, pst,
+                         ka);
       PEMP_LAUNCH_CHECK();
     } else if (sym && N > 0) {
       const int rc0 = launch_prepare_sym(desc, edge_index, node_types, N, E, ws, pst);
@@ -3922,6 +4217,31 @@ extern "C" int pemp_mpn_forward_sym(const pemp_mpn_desc* desc, const pemp_mpn_we
   // the packed row entries hold a node id in SYM_TBITS bits: larger graphs take the sorting prepare
   return mpn_forward_impl(desc, w, x, edge_attr, edge_index, node_types, N, E, edge_logits, node_logits, class_logits,
                           workspace, workspace_bytes, stream, nullptr, 0, 0, N < (1ll << SYM_TBITS));
+}
+
+extern "C" int pemp_mpn_forward_knn(const pemp_mpn_desc* desc, const pemp_mpn_weights* w, const float* x,
+                                    const float* edge_attr, const int64_t* edge_index, const int64_t* node_types,
+                                    int64_t N, int64_t E, const void* knn_rows, const int32_t* knn_rowstart,
+                                    const int64_t* node_off, const int64_t* node_off_host, const int64_t* ecount, int B,
+                                    float* edge_logits, float* node_logits, float* class_logits, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
+  PEMP_CHECK_ARG(B >= 1 && B <= KP_MAXB && node_off_host && node_off && ecount && (E == 0 || (knn_rows && knn_rowstart)),
+                 "pemp_mpn_forward_knn: bad rows / offsets (B=%d, at most %d images)", B, KP_MAXB);
+  PEMP_CHECK_ARG(N <= KP_MAXN && node_off_host[0] == 0 && node_off_host[B] == N,
+                 "pemp_mpn_forward_knn: N=%lld must equal node_off_host[B] and be <= %d", (long long)N, KP_MAXN);
+  for (int b = 0; b < B; ++b)
+    PEMP_CHECK_ARG(node_off_host[b + 1] >= node_off_host[b] && node_off_host[b + 1] - node_off_host[b] <= 64 * KP_W,
+                   "pemp_mpn_forward_knn: image %d holds more than %d nodes", b, 64 * KP_W);
+  KnnPrepArgs ka{};
+  ka.R = static_cast<const unsigned long long*>(knn_rows);
+  ka.rowstart = knn_rowstart;
+  ka.node_off = node_off;
+  ka.ecount = ecount;
+  ka.B = B;
+  const char* cap = getenv("PEMP_KNN_LIST_CAP");
+  ka.list_cap = cap ? std::max(0, std::min(KP_LIST, atoi(cap))) : KP_LIST;
+  return mpn_forward_impl(desc, w, x, edge_attr, edge_index, node_types, N, E, edge_logits, node_logits, class_logits,
+                          workspace, workspace_bytes, stream, nullptr, 0, 0, false, nullptr, 0, &ka);
 }
 
 extern "C" int pemp_mpn_prepare(const pemp_mpn_desc* desc, const int64_t* edge_index, const int64_t* node_types,

@@ -47,6 +47,13 @@ def _tag_sym(edge_index):
     edge_index._pemp_sym = edge_index._version
 
 
+def _tag_knn(edge_index, ws, offs, node_off, node_off_h):
+    """Hand the knn build's bit rows to the MPN (pemp_mpn_forward_knn): ws is that call's own workspace (kept
+    alive by the tag, never reused by a later build), offs the byte offsets of its rows / row starts / edge
+    counts (pemp_knn_rows_layout); the version detects in-place edits of edge_index."""
+    edge_index._pemp_knn = (ws, offs, node_off, node_off_h, edge_index._version)
+
+
 def get_graph_constructor(config, **kwargs):
     """``src/graph_constructor/__init__.py:4-5``."""
     return NaiveGraphConstructor(config=config, **kwargs)
@@ -415,11 +422,16 @@ class NaiveGraphConstructor:
         k = self._KNN_K
         nh = np.ascontiguousarray(node_off_h)
         nh_p = nh.ctypes.data_as(ctypes.c_void_p)
-        if x is not None:
-            ws = self._ws_knn.get(L.pemp_feature_knn_workspace_size(nh_p, B), dev)
-        else:
-            ws = self._ws_knn.get(L.pemp_knn_workspace_size(nh_p, B), dev)
         n = np.diff(nh)
+        size = (L.pemp_feature_knn_workspace_size if x is not None else L.pemp_knn_workspace_size)(nh_p, B)
+        # batches the MPN's knn prepare takes: a workspace of the call's own, whose bit rows go with edge_index
+        rows = None
+        if 1 <= B <= 64 and 0 < nh[B] <= 4096 and int(n.max()) <= 512:
+            rows = (ctypes.c_size_t * 3)()
+            _lib.check(L.pemp_knn_rows_layout(nh_p, B, int(x is not None), rows))
+            ws = torch.empty(max(int(size), 256), dtype=torch.uint8, device=dev)
+        else:
+            ws = self._ws_knn.get(size, dev)
         e_cap = int(np.minimum(n * np.maximum(n - 1, 0), 2 * k * n).sum())
         buf = torch.empty(2 * max(e_cap, 1), dtype=torch.int64, device=dev)
         ea = torch.empty(max(e_cap, 1) * A, dtype=torch.float32, device=dev)
@@ -442,4 +454,7 @@ class NaiveGraphConstructor:
         self._host_counts_give(dev, ent)
         if E > e_cap:
             raise RuntimeError(f"pemp_knn_graph_build: {E} edges > bound {e_cap}")
-        return buf[:2 * E].view(2, E), ea[:E * A].view(E, A)
+        edge_index = buf[:2 * E].view(2, E)
+        if rows is not None:
+            _tag_knn(edge_index, ws, tuple(rows), node_off, nh)
+        return edge_index, ea[:E * A].view(E, A)

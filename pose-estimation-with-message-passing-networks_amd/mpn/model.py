@@ -26,6 +26,7 @@ _VALIDATE = os.environ.get("PEMP_VALIDATE", "0") not in ("", "0")   # read once 
 _DEBUG_SYNC = os.environ.get("PEMP_DEBUG_SYNC", "0") not in ("", "0")
 _FULLY_OFF = os.environ.get("PEMP_NO_FULLY_PREPARE", "0") not in ("", "0")   # force the sorting prepare
 _SYM_OFF = os.environ.get("PEMP_NO_SYM_PREPARE", "0") not in ("", "0")       # (for symmetric graphs too)
+_KNN_OFF = os.environ.get("PEMP_NO_KNN_PREPARE", "0") not in ("", "0")      # knn graphs: the symmetric prepare
 _EDGE_LIMIT = (1 << 23) - 1    # pemp_mpn_forward: E < 2^23 and T N < 2^23 per call (32-bit byte offsets)
 
 AGGR_CODES = {"attn": 0, "add": 1, "sum": 1, "mean": 2, "max": 3}
@@ -281,7 +282,8 @@ class NodeClassificationMPNSimple(nn.Module):
             if done is not None:      # queued by construct_graph ahead of the counts (capacity mode)
                 return done
         fully = _fully_graph(edge_index, node_types, N) if self.node_summary == "not" else None
-        sym = fully is None and _sym_graph(edge_index)
+        knn = _knn_graph(edge_index, N) if fully is None else None
+        sym = fully is None and knn is None and _sym_graph(edge_index)
         x = _as(x, torch.float32)
         edge_attr = _as(edge_attr, torch.float32)
         edge_index = _as(edge_index, torch.int64)
@@ -321,6 +323,14 @@ class NodeClassificationMPNSimple(nn.Module):
                                                 edge_index.data_ptr(), node_types.data_ptr(), N, E, noff.data_ptr(),
                                                 offs, B, edge_logits.data_ptr(), node_logits.data_ptr(),
                                                 class_logits.data_ptr(), ws.data_ptr(), ws.numel(), st))
+        elif knn is not None:       # the constructor's knn graph: order from its build's bit rows
+            kws, offs, noff, nh = knn
+            base = kws.data_ptr()
+            _lib.check(L.pemp_mpn_forward_knn(desc, fw.struct_ref, x.data_ptr(), edge_attr.data_ptr(),
+                                              edge_index.data_ptr(), node_types.data_ptr(), N, E, base + offs[0],
+                                              base + offs[1], noff.data_ptr(), nh.ctypes.data, base + offs[2],
+                                              len(nh) - 1, edge_logits.data_ptr(), node_logits.data_ptr(),
+                                              class_logits.data_ptr(), ws.data_ptr(), ws.numel(), st))
         elif sym:                   # a to_undirected graph of the constructor: order from its rows
             _lib.check(L.pemp_mpn_forward_sym(desc, fw.struct_ref, x.data_ptr(), edge_attr.data_ptr(),
                                               edge_index.data_ptr(), node_types.data_ptr(), N, E,
@@ -331,7 +341,7 @@ class NodeClassificationMPNSimple(nn.Module):
                                           edge_index.data_ptr(), node_types.data_ptr(), N, E, edge_logits.data_ptr(),
                                           node_logits.data_ptr(), class_logits.data_ptr(), ws.data_ptr(), ws.numel(),
                                           st))
-        if kwargs.get("validate", _VALIDATE or (_DEBUG_SYNC and (sym or fully is not None))):
+        if kwargs.get("validate", _VALIDATE or (_DEBUG_SYNC and (sym or fully is not None or knn is not None))):
             _lib.check(L.pemp_mpn_status(desc, N, E, _lib.ptr(ws), _lib.stream(dev)))
         # list lengths and .squeeze() semantics of NodeClassificationMPNSimple.py:81-97
         preds_edge = [edge_logits[r].view(E, 1).squeeze() for r in range(n_rec)]
@@ -451,6 +461,18 @@ def _fully_graph(edge_index, node_types, N):
         return None
     B = len(counts)
     return noff, (ctypes.c_int64 * (B + 1))(*itertools.accumulate(counts, initial=0)), B
+
+
+def _knn_graph(edge_index, N):
+    """(workspace, offsets, node_off, host offsets) when edge_index is the untouched knn graph of the graph
+    constructor (graph_constructor._tag_knn) over these N nodes, else None. A hint like _tag_sym's."""
+    meta = getattr(edge_index, "_pemp_knn", None)
+    if meta is None or _KNN_OFF or _SYM_OFF:
+        return None
+    kws, offs, noff, nh, ever = meta
+    if edge_index._version != ever or int(nh[-1]) != N:
+        return None
+    return kws, offs, noff, nh
 
 
 def _sym_graph(edge_index):

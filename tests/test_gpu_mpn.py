@@ -373,6 +373,51 @@ def test_symmetric_graph_fast_prepare_is_identical(graph_type, persons, H, monke
             torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("graph_type,persons,H,B", [("knn", 9, 160, 4), ("knn", 28, 320, 4), ("feature_knn", 6, 128, 3),
+                                                     ("knn", 5, 96, 1), ("knn", 40, 320, 2)])
+def test_knn_rows_prepare_is_identical(graph_type, persons, H, B, monkeypatch):
+    """pemp_mpn_forward_knn (the edge order from the knn build's bit rows, one launch) against the symmetric
+    prepare and the sorting prepare on the constructor's knn / feature_knn graphs: bit-identical logits; an empty
+    image in the batch; an in-place edit drops the hand-over; images over 512 nodes (no bit rows) take the
+    symmetric prepare."""
+    from pemp_amd.mpn import model as mm
+    J, W = 17, H
+    hm = torch.from_numpy(syn.make_heatmaps(100 + H, B, J, H, W, persons, variant="clean", margin=4))
+    if B > 2:
+        hm[1] = 0.0                                             # an empty image in the batch
+    feats = torch.from_numpy(syn.closed_form((B, 128, H, W), 0.25))
+    gc = pcfg.inference_gc_config(graph_type, 3 if persons > 30 else 5, False)
+    cfg = pcfg.published_mpn_config(J, 3, "attn")
+    model, _ = make_model(cfg, 3.75, "f16x3")
+    out = pemp_amd.get_graph_constructor(gc, scoremaps=hm.to(DEV), features=feats.to(DEV), tagmaps=None,
+                                         joints_gt=None, factor_list=None, masks=None, device=DEV,
+                                         testing=True, heatmaps=None, num_joints=J).construct_graph()
+    x, ea, ei, types = out[0], out[1], out[2], out[7][:, 2]
+    N = x.shape[0]
+    big = int(torch.bincount(out[12]).max()) > 512
+    assert big == (persons > 30)
+    assert (mm._knn_graph(ei, N) is None) == big and mm._sym_graph(ei)
+    got = run(model, x, ea, ei, types)
+    monkeypatch.setattr(mm, "_KNN_OFF", True)
+    sym = run(model, x, ea, ei, types)
+    monkeypatch.setattr(mm, "_SYM_OFF", True)
+    srt = run(model, x, ea, ei, types)
+    for a, b, c in zip(got[0] + got[1] + got[2], sym[0] + sym[1] + sym[2], srt[0] + srt[1] + srt[2]):
+        assert torch.equal(a, b) and torch.equal(a, c)
+    monkeypatch.setattr(mm, "_KNN_OFF", False)
+    monkeypatch.setattr(mm, "_SYM_OFF", False)
+    monkeypatch.setenv("PEMP_KNN_LIST_CAP", "0")               # the row-by-row placement (chunks past the list)
+    rows = run(model, x, ea, ei, types)
+    monkeypatch.delenv("PEMP_KNN_LIST_CAP")
+    for a, b in zip(got[0] + got[1] + got[2], rows[0] + rows[1] + rows[2]):
+        assert torch.equal(a, b)
+    if not big:
+        with torch.no_grad():
+            model(x, ea, ei, node_types=types, validate=True)    # the contract flags stay clear
+        ei.add_(0)
+        assert mm._knn_graph(ei, N) is None
+
+
 @pytest.mark.parametrize("variant", ["attn", "max"])
 def test_symmetric_prepare_random_graph(variant, monkeypatch):
     """pemp_mpn_forward_sym on a random symmetric list with self loops, nodes of unsorted types, isolated
