@@ -3283,20 +3283,24 @@ __global__ __launch_bounds__(1024) void knn_prepare_kernel(KnnPrepArgs a) {
 #else
 #define KP_CLK(i) (void)0
 #endif
-  // the words and types of this thread's first two rows, in flight with the offsets (words past a row's image
-  // are masked below: R is [N][KP_W])
+  // the offsets first (the in-order load counter: the barrier below then waits for them, not for the rows), then
+  // the words and types of this thread's first two rows (words past a row's image are masked below: R is [N][KP_W])
+  // (clamped indices, no branches: straight-line loads let the barrier wait count exactly)
+  const int no = (int)a.node_off[min(tid, B)];
+  const int ec = (int)a.ecount[min(lane, B - 1)];
+  __builtin_amdgcn_sched_barrier(0);                 // (keeps the offsets' loads ahead of the rows')
   unsigned long long rr[2][KP_W];
   int64_t tr[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const int d = tid + 1024 * i;
+    const int d = min(tid + 1024 * i, N - 1);        // (rows past N are loaded but never used)
 #pragma unroll
-    for (int w = 0; w < KP_W; ++w) rr[i][w] = d < N ? a.R[(int64_t)d * KP_W + w] : 0ull;
-    tr[i] = d < N ? a.types[(int64_t)d * a.ts] : -1;
+    for (int w = 0; w < KP_W; ++w) rr[i][w] = a.R[(int64_t)d * KP_W + w];
+    tr[i] = a.types[(int64_t)d * a.ts];
   }
-  if (tid <= B) noff[tid] = (int)a.node_off[tid];
+  if (tid <= B) noff[tid] = no;
   if (wave == 1) {                                   // edge id base of every image (B <= 64)
-    const int e = lane < B ? (int)a.ecount[lane] : 0;
+    const int e = lane < B ? ec : 0;
     int x = e;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
