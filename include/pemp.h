@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define PEMP_ABI_VERSION 16
+#define PEMP_ABI_VERSION 17
 
 enum {
   PEMP_OK = 0,
@@ -442,6 +442,13 @@ int pemp_mpn_forward_fully_cap(const pemp_mpn_desc* desc, const pemp_mpn_weights
                                const int32_t* n_det, int det_cap, const int64_t* node_off, int B,
                                float* edge_logits, float* node_logits, float* class_logits,
                                void* workspace, size_t workspace_bytes, void* stream);
+
+/* Counters of pemp_mpn_forward_fully_cap's HIP graphs since the library loaded (no reference counterpart; for
+ * tests and servers): out3[0] captures made, out3[1] graph launches (first launch after a capture included),
+ * out3[2] captures refused (the forward then ran directly). A repeating argument set is launched directly the
+ * first time, captured the second, replayed from then on; PEMP_NO_GRAPHS, PEMP_DEBUG_SYNC and the library
+ * profiler run every call directly. */
+int pemp_mpn_graph_stats(uint64_t* out3);
 
 /* pemp_mpn_forward for an edge_index sorted by (src, dst) without duplicates and symmetric (every s -> d has
  * its d -> s: PyG to_undirected's coalesced output, as knn_mpn_graph / feature_knn_mpn_graph / score_based_graph

@@ -1323,7 +1323,25 @@ static int launch_detect(const float* s, const float* masks, const DetectGeom& g
     }
     PEMP_LAUNCH_CHECK();
   }
-  if ((stages & PEMP_DETECT_SELECT) && PEMP_DETECT_FUSED && g.units <= SEL_UNITS) {
+  // The fused stage's workgroups wait for their image's other J - 1 planes to publish: it needs at least J of its
+  // workgroups resident at once (workgroups are dispatched in order, so complete images drain and make room for the
+  // next). Checked once per device from the kernel's own occupancy; a device (partition) that cannot hold J takes
+  // the two-kernel path, which has no inter-workgroup wait.
+  auto fused_fits = [&]() {
+    static int cap_wg[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) { (void)hipGetLastError(); return false; }
+    if (!cap_wg[dev]) {
+      int occ = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, plane_emit_kernel<KMAX>, 256, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        occ = 0;
+      }
+      cap_wg[dev] = std::max(occ, 0) * num_cus() + 1;   // (+1: computed)
+    }
+    return cap_wg[dev] - 1 >= g.J;
+  };
+  if ((stages & PEMP_DETECT_SELECT) && PEMP_DETECT_FUSED && g.units <= SEL_UNITS && fused_fits()) {
     if (!(stages & PEMP_DETECT_NMS)) PEMP_HIP(hipMemsetAsync(w.pflag, 0, sizeof(unsigned long long) * g.B * g.J, st));
     ProfScope prof("detect_select_emit", st);
     hipLaunchKernelGGL(plane_emit_kernel<KMAX>, dim3(g.B * g.J), dim3(256), 0, st, s, masks, g, thr, use_thr, w.cbits,

@@ -20,6 +20,7 @@
 #include <limits.h>
 
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 #include <map>
 #include <mutex>
@@ -1290,6 +1291,12 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
 #ifndef PEMP_ASM_SCANS
 #define PEMP_ASM_SCANS 1
 #endif
+#ifndef PEMP_ASM_ALL   // diagnostics: the asm sums in every non-max instantiation
+#define PEMP_ASM_ALL 0
+#endif
+#ifdef PEMP_ASM_CHECK
+__device__ unsigned g_asm_check_count = 0;
+#endif
 struct ChunkMasks {
   uint64_t f1, f2, f4, f8, b1, b2, b4, b8;   // lanes with d >= k (forward steps) / u >= k (backward steps)
 };
@@ -1909,8 +1916,38 @@ __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_
     // (the hand-placed sums only where the attention weight is folded into the update split, PE_FOLD: with the
     // weight multiplied in separately -- the bf16x3 / fp32 kernels -- they gave wrong aggregates on the GPU
     // (bf16x3 logits 1e-3 off), for a reason not found; those kernels keep the compiler's scans)
-    if (PEMP_ASM_SCANS && PE_FOLD) {
+    if (PEMP_ASM_SCANS && (PE_FOLD || (PEMP_ASM_ALL && AGG != PEMP_AGGR_MAX))) {
+#ifdef PEMP_ASM_CHECK   // diagnostics: the asm sums against the compiler's on the same inputs, first mismatches printed
+      float vin[4][4], vc[4][4], lin = l, lc = l;
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) vin[ob][r] = vc[ob][r] = v[ob][r];
+#endif
       seg_sum17_asm(v, l, smk);                  // the 64 features and the normaliser / count
+#ifdef PEMP_ASM_CHECK
+      lc = seg_sum(lc, smk);
+      int bad = __float_as_uint(lc) != __float_as_uint(l) ? 16 : -1;
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          vc[ob][r] = seg_sum(vc[ob][r], smk);
+          if (bad < 0 && __float_as_uint(vc[ob][r]) != __float_as_uint(v[ob][r])) bad = 4 * ob + r;
+        }
+      if (bad >= 0) {
+        const unsigned k = atomicAdd(&g_asm_check_count, 1u);
+        if (k < 24) {
+          float a_ = l, c_ = lc, i_ = lin;
+#pragma unroll
+          for (int q = 0; q < 16; ++q)
+            if (q == bad) { a_ = v[q >> 2][q & 3]; c_ = vc[q >> 2][q & 3]; i_ = vin[q >> 2][q & 3]; }
+          printf("ASMCHK blk %d wave %d lane %d val %d d %d in %a asm %a cmp %a m %g %g %g %g exec %llx\n",
+                 (int)blockIdx.x, wave, lane, bad, ck.d, i_, a_, c_, smk.m1, smk.m2, smk.m4, smk.m8,
+                 (unsigned long long)__builtin_amdgcn_read_exec());
+        }
+      }
+#endif
     } else {
       if (AGG == PEMP_AGGR_ATTN || AGG == PEMP_AGGR_MEAN) l = seg_sum(l, smk);   // normaliser / count
 #pragma unroll
@@ -4065,10 +4102,13 @@ static bool graphs_off() {
 }
 
 // The null (legacy) stream cannot be captured: a caller on it gets its graphs captured on and replayed from a
-// private stream of the device, joined to the null stream by events around each replay.
+// private stream of the device, joined to the null stream by events around each replay. Every use of that stream
+// (capture, first launch, replays) holds its mutex: a replay queued on it while another thread captures would
+// invalidate the capture.
 struct GraphStream {
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
+  std::mutex mu;
 };
 
 static GraphStream* graph_stream(int dev) {
@@ -4098,6 +4138,17 @@ static int cap_forward_direct(const pemp_mpn_desc* desc, const pemp_mpn_weights*
                           det_cap);
 }
 
+// Graph statistics for the tests (pemp_mpn_graph_stats): captures made, replays launched, captures refused.
+static std::atomic<uint64_t> g_graph_captures{0}, g_graph_replays{0}, g_graph_refused{0};
+
+extern "C" int pemp_mpn_graph_stats(uint64_t* out3) {
+  PEMP_CHECK_ARG(out3, "pemp_mpn_graph_stats: null output");
+  out3[0] = g_graph_captures.load();
+  out3[1] = g_graph_replays.load();
+  out3[2] = g_graph_refused.load();
+  return PEMP_OK;
+}
+
 extern "C" int pemp_mpn_forward_fully_cap(const pemp_mpn_desc* desc, const pemp_mpn_weights* w, const float* x,
                                           const float* edge_attr, const int64_t* node_types, int64_t n_cap,
                                           int64_t e_cap, const int32_t* n_det, int det_cap, const int64_t* node_off,
@@ -4110,9 +4161,12 @@ extern "C" int pemp_mpn_forward_fully_cap(const pemp_mpn_desc* desc, const pemp_
     set_error("pemp_mpn_forward_fully_cap: this model / capacity takes the exact forward");
     return PEMP_ERR_UNSUPPORTED;
   }
-  if (graphs_off() || prof_active())
+  auto direct = [&](void* s) {
     return cap_forward_direct(desc, w, x, edge_attr, node_types, n_cap, e_cap, n_det, det_cap, node_off, B,
-                              edge_logits, node_logits, class_logits, workspace, workspace_bytes, stream);
+                              edge_logits, node_logits, class_logits, workspace, workspace_bytes, s);
+  };
+  // PEMP_DEBUG_SYNC synchronises the device after every launch, which a capturing stream does not allow
+  if (graphs_off() || prof_active() || debug_sync()) return direct(stream);
   int dev = 0;
   PEMP_HIP(hipGetDevice(&dev));
   std::string key;
@@ -4130,9 +4184,10 @@ extern "C" int pemp_mpn_forward_fully_cap(const pemp_mpn_desc* desc, const pemp_
   static uint64_t tick = 0;
   const hipStream_t ust = as_stream(stream);
   GraphStream* gs = ust ? nullptr : graph_stream(dev);
-  if (!ust && !gs)
-    return cap_forward_direct(desc, w, x, edge_attr, node_types, n_cap, e_cap, n_det, det_cap, node_off, B,
-                              edge_logits, node_logits, class_logits, workspace, workspace_bytes, stream);
+  if (!ust && !gs) return direct(stream);
+  // a null-stream caller holds the private stream for the whole call (replay, or capture + first launch)
+  std::unique_lock<std::mutex> gs_lock;
+  if (gs) gs_lock = std::unique_lock<std::mutex>(gs->mu);
   const hipStream_t st = ust ? ust : gs->s;   // capture / replay stream
   auto launch = [&](hipGraphExec_t exec) -> int {
     if (gs) {                                 // null-stream caller: fork to the private stream and back
@@ -4144,58 +4199,53 @@ extern "C" int pemp_mpn_forward_fully_cap(const pemp_mpn_desc* desc, const pemp_
       PEMP_HIP(hipEventRecord(gs->join, gs->s));
       PEMP_HIP(hipStreamWaitEvent(ust, gs->join, 0));
     }
+    g_graph_replays.fetch_add(1);
     return PEMP_OK;
   };
   {
-    std::lock_guard<std::mutex> lk(mu);
+    std::unique_lock<std::mutex> lk(mu);
     for (auto& e : cache)
       if (e.key == key) {
         e.used = ++tick;
         return launch(e.exec);
       }
     auto it = std::find(seen.begin(), seen.end(), key);
-    if (it == seen.end()) {                 // first sight: direct launches
+    const bool second_sight = it != seen.end();
+    if (second_sight) {
+      seen.erase(it);                       // captured below
+    } else {                                // first sight: direct launches
       if (seen.size() >= 32) seen.erase(seen.begin());
       seen.push_back(key);
-      it = seen.end();
-    } else {
-      seen.erase(it);
-      it = seen.begin();                    // (marker: capture below)
-    }
-    if (it == seen.end()) {
-      mu.unlock();
-      const int rc0 = cap_forward_direct(desc, w, x, edge_attr, node_types, n_cap, e_cap, n_det, det_cap, node_off,
-                                         B, edge_logits, node_logits, class_logits, workspace, workspace_bytes, stream);
-      mu.lock();
-      return rc0;
+      lk.unlock();
+      return direct(stream);
     }
   }
   // capture (thread-local mode: other threads' launches on other streams are unaffected)
   if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) != hipSuccess) {
     (void)hipGetLastError();
-    return cap_forward_direct(desc, w, x, edge_attr, node_types, n_cap, e_cap, n_det, det_cap, node_off, B,
-                              edge_logits, node_logits, class_logits, workspace, workspace_bytes, stream);
+    g_graph_refused.fetch_add(1);
+    return direct(stream);
   }
-  const int rc = cap_forward_direct(desc, w, x, edge_attr, node_types, n_cap, e_cap, n_det, det_cap, node_off, B,
-                                    edge_logits, node_logits, class_logits, workspace, workspace_bytes, st);
+  const int rc = direct(st);
   hipGraph_t graph = nullptr;
   const hipError_t ec = hipStreamEndCapture(st, &graph);
   if (rc != PEMP_OK || ec != hipSuccess || !graph) {
+    // a launch refused while capturing, or the capture itself invalidated: nothing was queued, so the forward
+    // runs directly on the caller's stream (an argument error repeats there and is returned from there)
     if (graph) (void)hipGraphDestroy(graph);
     (void)hipGetLastError();
-    if (rc != PEMP_OK) return rc;
-    // capture refused (e.g. a caller-side capture in progress): launch directly
-    return cap_forward_direct(desc, w, x, edge_attr, node_types, n_cap, e_cap, n_det, det_cap, node_off, B,
-                              edge_logits, node_logits, class_logits, workspace, workspace_bytes, stream);
+    g_graph_refused.fetch_add(1);
+    return direct(stream);
   }
   hipGraphExec_t exec = nullptr;
   const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
   (void)hipGraphDestroy(graph);
   if (ei != hipSuccess || !exec) {
     (void)hipGetLastError();
-    return cap_forward_direct(desc, w, x, edge_attr, node_types, n_cap, e_cap, n_det, det_cap, node_off, B,
-                              edge_logits, node_logits, class_logits, workspace, workspace_bytes, stream);
+    g_graph_refused.fetch_add(1);
+    return direct(stream);
   }
+  g_graph_captures.fetch_add(1);
   const int rl = launch(exec);
   if (rl != PEMP_OK) {
     (void)hipGraphExecDestroy(exec);
