@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <map>
@@ -284,6 +285,110 @@ void gaec_dense(size_t n, const std::vector<size_t>& ea, const std::vector<size_
   qstore = std::move(Drain::c_of(q));
 }
 
+// gaec_dense with a heap of the non-negative entries only. andres' loop stops at the first negative heap top and
+// never contracts a negative entry, so the negative entries matter only through the heap layout, i.e. through the
+// order in which EQUAL weights pop. When every live entry popped for a contraction is strictly larger than every
+// other entry in the heap at that moment, both heaps contract the same edges in the same order (a max-heap pops
+// the unique maximum whatever its layout; stale entries are skipped by both) and the partitions are identical.
+// So: the same adjacency, degrees, weights and edition counters as gaec_dense (every update counted, pushed or
+// not), a heap of the entries with w >= 0, and at each contraction a check that the next top does not equal the
+// popped weight. On such a tie it returns false and the caller runs gaec_dense (the exact libstdc++ heap order).
+// C3 / C5 shapes: 20-40x fewer heap entries (the fully graph's edges between persons are negative).
+bool gaec_fast(size_t n, const std::vector<size_t>& ea, const std::vector<size_t>& eb, const std::vector<double>& ew,
+               std::vector<size_t>& root) {
+  // One 16-byte cell (weight, edition, existence) per unordered pair, at (min, max) of an n x n array whose upper
+  // triangle alone is used (and cleared): an update of a pair touches one cache line, the initial edges (sorted by
+  // (src, dst), src < dst) fill the rows in order. A merged vertex is only marked dead (its cells are never read
+  // again: scans skip dead vertices, a popped entry with a dead end is stale). Within one contraction every pair is
+  // updated once, so the order of the row scan does not change any weight (the same double additions).
+  struct Cell {
+    double w;
+    uint32_t ed, ex;
+  };
+  static thread_local std::vector<Cell> cell;
+  static thread_local std::vector<uint32_t> deg;
+  static thread_local std::vector<uint8_t> alive;
+  static thread_local std::vector<GaecEdge16> qstore;
+  if (cell.size() < n * n) cell.resize(n * n);
+  for (size_t a = 0; a + 1 < n; ++a) std::fill(cell.begin() + a * n + a + 1, cell.begin() + (a + 1) * n, Cell{0.0, 0, 0});
+  deg.assign(n, 0);
+  alive.assign(n, 1);
+  auto at = [&](size_t a, size_t b) -> Cell& { return a < b ? cell[a * n + b] : cell[b * n + a]; };
+  qstore.clear();
+  std::priority_queue<GaecEdge16> q(std::less<GaecEdge16>(), std::move(qstore));
+  struct Drain : std::priority_queue<GaecEdge16> {
+    static std::vector<GaecEdge16>& c_of(std::priority_queue<GaecEdge16>& pq) { return pq.*(&Drain::c); }
+  };
+  for (size_t i = 0; i < ea.size(); ++i) {
+    const size_t a = ea[i], b = eb[i];
+    Cell& c = at(a, b);
+    if (!c.ex) {
+      c.ex = 1;
+      ++deg[a];
+      ++deg[b];
+    }
+    c.w += ew[i];
+    GaecEdge16 e(a, b, ew[i]);
+    e.edition = ++c.ed;
+    if (!(e.w < 0.0)) q.push(e);
+  }
+  std::vector<size_t> parent(n), rank(n, 0);
+  for (size_t v = 0; v < n; ++v) parent[v] = v;
+  auto find = [&](size_t v) {
+    while (parent[v] != v) {
+      parent[v] = parent[parent[v]];
+      v = parent[v];
+    }
+    return v;
+  };
+  bool exact = true;
+  while (!q.empty()) {
+    const GaecEdge16 e = q.top();
+    q.pop();
+    if (!alive[e.a] || !alive[e.b]) continue;
+    const Cell& ce = cell[(size_t)e.a * n + e.b];
+    if (!ce.ex || e.edition < ce.ed) continue;
+    if (!q.empty() && q.top().w == e.w) {   // an equal weight: its pop order is the full heap's to decide
+      exact = false;
+      break;
+    }
+    size_t keep = e.a, merge = e.b;
+    if (deg[keep] < deg[merge]) std::swap(keep, merge);
+    {
+      size_t rk = find(keep), rm = find(merge);
+      if (rk != rm) {
+        if (rank[rk] < rank[rm]) std::swap(rk, rm);
+        parent[rm] = rk;
+        if (rank[rk] == rank[rm]) ++rank[rk];
+      }
+    }
+    for (size_t p = 0; p < n; ++p) {
+      if (p == merge || !alive[p]) continue;
+      const Cell& mp = at(merge, p);
+      if (!mp.ex) continue;
+      --deg[p];                      // the edge (p, merge) goes with merge (p == keep included)
+      if (p == keep) continue;
+      Cell& kp = at(keep, p);
+      if (!kp.ex) {
+        kp.ex = 1;
+        ++deg[keep];
+        ++deg[p];
+      }
+      kp.w += mp.w;
+      GaecEdge16 ne(keep, p, kp.w);
+      ne.edition = ++kp.ed;
+      if (!(ne.w < 0.0)) q.push(ne);
+    }
+    alive[merge] = 0;
+    deg[merge] = 0;
+  }
+  qstore = std::move(Drain::c_of(q));
+  if (!exact) return false;
+  root.resize(n);
+  for (size_t v = 0; v < n; ++v) root[v] = find(v);
+  return true;
+}
+
 // Persistent host workers for the per-image loops (one image per task): a call hands out tasks through an atomic
 // counter and the calling thread works too, so no thread is created per call (std::thread creation and the first
 // touch of each new thread's stack cost more than a 153-node GAEC). Calls are serialised by the pool's mutex.
@@ -303,13 +408,21 @@ class HostPool {
       tasks_ = tasks;
       next_.store(0);
       active_ = threads - 1;
-      running_ = threads - 1;
-      ++gen_;
+      running_.store(threads - 1);
+      gen_.fetch_add(1, std::memory_order_release);
     }
     cv_.notify_all();
     drain(fn);
-    std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [this] { return running_ == 0; });
+    // the caller's share is done: wait for the workers' tasks (spinning first; they are short)
+    for (int spin = 0; running_.load(std::memory_order_acquire) != 0; ++spin) {
+      if (spin < 20000) {
+        __builtin_ia32_pause();
+      } else {
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [this] { return running_.load() == 0; });
+      }
+    }
+    std::lock_guard<std::mutex> lk(mu_);
     fn_ = nullptr;
   }
 
@@ -317,28 +430,49 @@ class HostPool {
   void drain(const std::function<void(int)>& fn) {
     for (int i = next_.fetch_add(1); i < tasks_; i = next_.fetch_add(1)) fn(i);
   }
+  // A worker spins on the generation counter for a while after its last task before it sleeps on the condition
+  // variable: a condition-variable wake-up measured 1-4 ms on some hosts (the per-image tasks are 0.1-1 ms), and a
+  // serving loop calls again within a few ms. PEMP_POOL_SPIN_US (default 2000) sets the window, 0 disables it.
+  static uint64_t spin_ns() {
+    static const uint64_t v = [] {
+      const char* e = getenv("PEMP_POOL_SPIN_US");
+      return (uint64_t)(e ? strtoull(e, nullptr, 10) : 2000) * 1000;
+    }();
+    return v;
+  }
   void loop(int id) {
     uint64_t seen = 0;
     for (;;) {
+      const uint64_t t_idle = now_ns();
+      while (gen_.load(std::memory_order_acquire) == seen && now_ns() - t_idle < spin_ns())
+        for (int k = 0; k < 64; ++k) __builtin_ia32_pause();
       const std::function<void(int)>* fn;
       {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return gen_ != seen && id < active_; });
-        seen = gen_;
+        cv_.wait(lk, [&] { return gen_.load() != seen; });
+        seen = gen_.load();
+        if (id >= active_) continue;   // not needed this call
         fn = fn_;
       }
       drain(*fn);
-      std::lock_guard<std::mutex> lk(mu_);
-      if (--running_ == 0) done_cv_.notify_one();
+      if (running_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+        std::lock_guard<std::mutex> lk(mu_);
+        done_cv_.notify_one();
+      }
     }
+  }
+  static uint64_t now_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
   }
   std::mutex call_mu_, mu_;
   std::condition_variable cv_, done_cv_;
   std::vector<std::thread> workers_;   // never joined: the pool lives as long as the process
   const std::function<void(int)>* fn_ = nullptr;
   std::atomic<int> next_{0};
-  int tasks_ = 0, active_ = 0, running_ = 0;
-  uint64_t gen_ = 0;
+  std::atomic<int> running_{0};
+  std::atomic<uint64_t> gen_{0};
+  int tasks_ = 0, active_ = 0;
 };
 
 HostPool& host_pool() {
@@ -398,45 +532,58 @@ extern "C" int pemp_pose_cluster(int B, const int64_t* node_off, const int64_t* 
   }
   for (int b = 0; b < B; ++b)
     PEMP_CHECK_ARG(node_off[b + 1] >= node_off[b], "pemp_pose_cluster: node_off not monotone");
-  // bucket the surviving edges per image, keeping edge_index order
-  std::vector<std::vector<size_t>> ua(B), ub(B);
-  std::vector<std::vector<double>> uw(B);
-  int b = 0;
-  for (int64_t e = 0; e < E; ++e) {
-    const float we = w[e];
-    if (std::isnan(we)) continue;
-    const int64_t s = edge_index[e], d = edge_index[E + e];
-    while (b + 1 < B && s >= node_off[b + 1]) ++b;
-    while (b > 0 && s < node_off[b]) --b;
-    if (s < node_off[b] || s >= node_off[b + 1] || d < node_off[b] || d >= node_off[b + 1]) {
-      ::pemp::set_error("pemp_pose_cluster: edge %lld crosses images", (long long)e);
-      return PEMP_ERR_INVALID_ARG;
-    }
-    double weight;
-    if (method == 0) {
-      const float m = (flags[b] & 1) ? we * 0.5f : we;  // extract_edge_matrix: average, or M + M^T
-      weight = (double)(m - 0.5f);                          // cluster_andres_graph: edge_attr - 0.5 (fp32)
-    } else {
-      if (!(we > 0.8f)) continue;                           // pred_to_person "threshold": pred > 0.8
-      weight = 1.0;
-    }
-    ua[b].push_back((size_t)(s - node_off[b]));
-    ub[b].push_back((size_t)(d - node_off[b]));
-    uw[b].push_back(weight);
-  }
   size_t dense_max = 2048;  // dense adjacency up to 2048 vertices (54 MB); PEMP_GAEC_DENSE_MAX overrides
   if (const char* env = getenv("PEMP_GAEC_DENSE_MAX")) dense_max = (size_t)strtoull(env, nullptr, 10);
   dense_max = std::min<size_t>(dense_max, 65535);
+  const bool exact_only = getenv("PEMP_GAEC_EXACT") != nullptr;   // diagnostics / tests: the full heap always
+  std::atomic<int64_t> bad_edge{-1};
+  // one task per image: its edges are the contiguous run of the (src, dst)-sorted list whose src lies in the image
+  // (found by binary search), bucketed in edge_index order, then clustered
   auto run = [&](int img) {
-    const size_t n = (size_t)(node_off[img + 1] - node_off[img]);
+    const int64_t o = node_off[img], n64 = node_off[img + 1] - o;
+    const size_t n = (size_t)n64;
+    const int64_t lo = std::lower_bound(edge_index, edge_index + E, o) - edge_index;
+    const int64_t hi = std::lower_bound(edge_index + lo, edge_index + E, o + n64) - edge_index;
+    static thread_local std::vector<size_t> ua, ub;
+    static thread_local std::vector<double> uw;
+    ua.clear();
+    ub.clear();
+    uw.clear();
+    ua.reserve((size_t)(hi - lo));
+    ub.reserve((size_t)(hi - lo));
+    uw.reserve((size_t)(hi - lo));
+    for (int64_t e = lo; e < hi; ++e) {
+      const float we = w[e];
+      if (std::isnan(we)) continue;
+      const int64_t d = edge_index[E + e];
+      if (d < o || d >= o + n64) {
+        int64_t none = -1;
+        bad_edge.compare_exchange_strong(none, e);
+        return;
+      }
+      double weight;
+      if (method == 0) {
+        const float m = (flags[img] & 1) ? we * 0.5f : we;  // extract_edge_matrix: average, or M + M^T
+        weight = (double)(m - 0.5f);                            // cluster_andres_graph: edge_attr - 0.5 (fp32)
+      } else {
+        if (!(we > 0.8f)) continue;                             // pred_to_person "threshold": pred > 0.8
+        weight = 1.0;
+      }
+      ua.push_back((size_t)(edge_index[e] - o));
+      ub.push_back((size_t)(d - o));
+      uw.push_back(weight);
+    }
     std::vector<size_t> root;
     if (method == 0) {
-      if (n <= dense_max) gaec_dense(n, ua[img], ub[img], uw[img], root);
-      else gaec(n, ua[img], ub[img], uw[img], root);
+      if (n <= dense_max) {
+        if (exact_only || !gaec_fast(n, ua, ub, uw, root)) gaec_dense(n, ua, ub, uw, root);
+      } else {
+        gaec(n, ua, ub, uw, root);
+      }
     } else {
       root.resize(n);
       for (size_t v = 0; v < n; ++v) root[v] = v;
-      for (size_t i = 0; i < ua[img].size(); ++i) union_join(root, ua[img][i], ub[img][i]);
+      for (size_t i = 0; i < ua.size(); ++i) union_join(root, ua[i], ub[i]);
       for (size_t v = 0; v < n; ++v) {
         size_t r = v;
         while (root[r] != r) r = root[r];
@@ -445,7 +592,7 @@ extern "C" int pemp_pose_cluster(int B, const int64_t* node_off, const int64_t* 
     }
     std::vector<int32_t> lab(n, -1);
     int32_t next = 0;
-    int32_t* out = labels + node_off[img];
+    int32_t* out = labels + o;
     for (size_t v = 0; v < n; ++v) {  // scipy connected_components: labels in order of first vertex
       if (lab[root[v]] < 0) lab[root[v]] = next++;
       out[v] = lab[root[v]];
@@ -453,6 +600,24 @@ extern "C" int pemp_pose_cluster(int B, const int64_t* node_off, const int64_t* 
     n_comp[img] = next;
   };
   host_pool().run(B, n_threads, run);
+  {   // surviving edges whose source lies in no image
+    const int64_t lo = std::lower_bound(edge_index, edge_index + E, node_off[0]) - edge_index;
+    const int64_t hi = std::lower_bound(edge_index, edge_index + E, node_off[B]) - edge_index;
+    auto scan = [&](int64_t a, int64_t b) {
+      for (int64_t e = a; e < b; ++e)
+        if (!std::isnan(w[e])) {
+          int64_t none = -1;
+          bad_edge.compare_exchange_strong(none, e);
+          return;
+        }
+    };
+    scan(0, lo);
+    scan(hi, E);
+  }
+  if (bad_edge.load() >= 0) {
+    ::pemp::set_error("pemp_pose_cluster: edge %lld crosses images", (long long)bad_edge.load());
+    return PEMP_ERR_INVALID_ARG;
+  }
   return PEMP_OK;
 }
 
@@ -475,16 +640,23 @@ extern "C" int pemp_pose_persons(int B, const int64_t* node_off, const int32_t* 
     }
     int32_t count = 0;
     mutants[b] = 0;
+    // each node's type once: its detection type, or the first argmax of its class probabilities (np.argmax)
+    std::vector<int64_t> types((size_t)n);
+    for (int64_t v = 0; v < n; ++v) {
+      const int64_t g = o + v;
+      if (!class_probs) {
+        types[v] = joint_det[g * 3 + 2];
+        continue;
+      }
+      const float* c = class_probs + g * J;
+      int best = 0;
+      for (int j = 1; j < J; ++j)
+        if (c[j] > c[best]) best = j;  // np.argmax: first maximum
+      types[v] = best;
+    }
     for (const auto& m : members) {
       if ((int64_t)m.size() > J) mutants[b] = 1;
-      auto type_of = [&](int64_t g) -> int64_t {
-        if (!class_probs) return joint_det[g * 3 + 2];
-        const float* c = class_probs + g * J;
-        int best = 0;
-        for (int j = 1; j < J; ++j)
-          if (c[j] > c[best]) best = j;  // np.argmax: first maximum
-        return best;
-      };
+      auto type_of = [&](int64_t g) -> int64_t { return types[g - o]; };
       double kp[64 * 3];
       PEMP_CHECK_ARG(J <= 64, "pemp_pose_persons: J > 64");
       std::fill(kp, kp + J * 3, 0.0);

@@ -161,6 +161,40 @@ def test_gaec_matches_oracle_random_with_ties(seed, dense, monkeypatch):
     np.testing.assert_array_equal(labels, ref_labels)
 
 
+@pytest.mark.parametrize("n,persons,quant", [(153, 9, 0), (60, 4, 0), (231, 13, 0), (90, 5, 64), (40, 3, 8)])
+def test_gaec_fast_path_equals_full_heap(n, persons, quant, monkeypatch):
+    """The non-negative-heap GAEC (gaec_fast) against the full libstdc++-heap GAEC (PEMP_GAEC_EXACT) on
+    person-structured fully graphs (bench.py's synthetic probabilities), batched; quantised probabilities make
+    equal weights, where the fast path hands over to the full heap. Labels must be identical, and equal to the
+    oracle's restatement of andres' GAEC."""
+    rng = np.random.default_rng(n + quant)
+    B = 3
+    dets, scs, eis, prs, offs = [], [], [], [], [0]
+    for b in range(B):
+        s, d = np.nonzero(~np.eye(n, dtype=bool))
+        same = (s % persons) == (d % persons)
+        p = (1 / (1 + np.exp(-(np.where(same, 2.5, -2.5) + 1.5 * rng.standard_normal(s.size))))).astype(np.float32)
+        if quant:
+            p = (np.round(p * quant) / quant).astype(np.float32)
+        dets.append(np.stack([rng.integers(0, 640, n), rng.integers(0, 640, n), np.arange(n) % 17], 1))
+        scs.append(rng.uniform(0.2, 1.0, n).astype(np.float32))
+        eis.append(np.stack([s, d]).astype(np.int64) + offs[-1])
+        prs.append(p)
+        offs.append(offs[-1] + n)
+    args = (np.concatenate(dets), np.concatenate(scs), np.concatenate(eis, 1), np.concatenate(prs), None, 17,
+            np.array(offs, np.int64), 0.0, False, 0)
+    _, fast, _, _ = host_group(*args)
+    monkeypatch.setenv("PEMP_GAEC_EXACT", "1")
+    _, full, _, _ = host_group(*args)
+    np.testing.assert_array_equal(fast, full)
+    for b in range(B):
+        sl = slice(offs[b], offs[b + 1])
+        ei = eis[b] - offs[b]
+        sol = opose.cluster_gaec(n, ei, prs[b])
+        _, _, ref = opose.graph_cluster_to_persons(dets[b], scs[b], np.stack(np.nonzero(sol)), None, 17)
+        np.testing.assert_array_equal(fast[sl], ref)
+
+
 def test_unsorted_edge_index_is_refused():
     L = _lib.load_cdll()
     flags = np.array([2, 1], np.int32)   # image 0 keeps edges; flags[B] bit 0: unsorted

@@ -7,3 +7,10 @@ echo "suite rc=$? $(tail -1 gpurun_out/r05a_gpu_tests.log)"
 PEMP_LIB=$PWD/build_ab/libpemp_asmchk.so timeout -k 10 120 python -u -m pytest tests/test_gpu_mpn.py -q -s -k "golden and attn and bf16x3" --timeout 100 --timeout-method thread > gpurun_out/r05a_asmchk.log 2>&1
 echo "asmchk rc=$? $(tail -1 gpurun_out/r05a_asmchk.log)"
 grep -c ASMCHK gpurun_out/r05a_asmchk.log || true
+# host GAEC on the box's cores (no GPU): thread counts and the pool's spin window
+for sp in 0 2000; do for t in 1 4 8 16; do
+  PEMP_POOL_SPIN_US=$sp timeout -k 5 60 python -u tools/gaec_bench.py 8 153 9 $t 50 | sed "s/^/spin=$sp /"
+done; done
+PEMP_GAEC_EXACT=1 timeout -k 5 60 python -u tools/gaec_bench.py 8 153 9 1 20 | sed "s/^/exact /"
+timeout -k 5 60 python -u tools/gaec_bench.py 1 502 36 1 20
+PEMP_GAEC_EXACT=1 timeout -k 5 60 python -u tools/gaec_bench.py 1 502 36 1 10 | sed "s/^/exact /"
