@@ -375,3 +375,49 @@ def test_projected_features_gather_conv(ksize, pad, scales):
         assert out[0].shape == ref[0].shape
         tol = 2e-5 * max(1.0, ref[0].abs().max().item())
         assert (out[0].cpu() - ref[0]).abs().max().item() <= tol
+
+
+CROWD_FLIP = [1, 0, 3, 2, 5, 4, 7, 6, 9, 8, 11, 10, 12, 13]   # FLIP_CONFIG['CROWDPOSE'] (multi_scales_testing.py:383)
+
+
+@pytest.mark.parametrize("graph,H,W", [("fully", 160, 160), ("knn", 160, 192)])
+def test_projected_frontend_three_scales_c5(graph, H, W):
+    """The C5 multi-scale front-end exactly as bench.py's c5ms builds it: CrowdPose J = 14, scale
+    factors {2, 1, 0.5} in the reference's descending order (PoseEstimation.py:193), network outputs at half the
+    scaled input (H s / 2), flipped passes re-indexed by FLIP_CONFIG['CROWDPOSE'], tags kept from the 1.0 scale
+    (tag_scale = 1, aggregate_results_mpn's scale_factor == 1 branch, multi_scales_testing.py:147-157), features
+    projected from three ProjectedMaps scales. construct_graph bit-exact with the oracle on its fp32 restatement of
+    the same projection; pemp_project_maps bit-exact with that restatement; the second call takes the capacity
+    build."""
+    from pemp_amd.frontend import ProjectedHeatmaps, ProjectedMaps
+    B, J = 2, 14
+    scales = [2.0, 1.0, 0.5]
+    outs, flips, fmaps = [], [], []
+    for k, sc in enumerate(scales):
+        h, w = int(H * sc / 2), int(W * sc / 2)
+        hm = syn.make_heatmaps(90 + k, B, J, h, w, 4, sigma=1.0, margin=2)
+        tg = syn.closed_form((B, J, h, w), 0.5 + 0.1 * k)
+        outs.append(torch.from_numpy(np.concatenate([hm, tg], 1)))
+        hm2 = syn.make_heatmaps(140 + k, B, J, h, w, 4, sigma=1.0, margin=2)
+        tg2 = syn.closed_form((B, J, h, w), 0.7 + 0.1 * k)
+        flips.append(torch.from_numpy(np.concatenate([hm2, tg2], 1)))
+        fmaps.append(torch.from_numpy(syn.closed_form((B, 128, h, w), 0.25 + 0.1 * k)))
+    tag_scale = scales.index(1.0)
+    ph = ProjectedHeatmaps([o.to(DEV) for o in outs], (H, W), J, [o.to(DEV) for o in flips], CROWD_FLIP,
+                           tag_scale=tag_scale)
+    s, t = restate.project_frontend(outs, flips, (H, W), J, CROWD_FLIP, tag_scale=tag_scale)
+    ps, pt = ph.project()
+    assert torch.equal(ps.cpu(), s) and torch.equal(pt.cpu(), t)
+    pm = ProjectedMaps(fmaps, (H, W))
+    dense_f = pm.materialize()
+    gc = pcfg.inference_gc_config(graph, 5, False)
+    ref = restate.construct_graph(s, dense_f, t, None, gc, J)
+    assert ref[7].shape[0] > 4 * J
+    for _ in range(2):
+        out = pemp_amd.get_graph_constructor(gc, scoremaps=ph, features=pm.to(DEV), tagmaps=ph, joints_gt=None,
+                                             factor_list=None, masks=None, device=DEV, testing=True, heatmaps=None,
+                                             num_joints=J).construct_graph()
+        for i in (1, 2, 7, 11, 12, 14):
+            assert torch.equal(out[i].cpu(), ref[i]), i
+        assert out[14].shape[1] == 2                               # F = 2: the flipped pass's tags too
+        assert (out[0].cpu() - ref[0]).abs().max().item() <= 2e-6
