@@ -107,6 +107,16 @@ int pemp_detect_projected(const pemp_proj_maps* maps, const float* masks, int B,
  * flipped pass. Values identical to the ones the detection samples. */
 int pemp_project_maps(const pemp_proj_maps* maps, int B, int J, int H, int W, int tag_scale, float* scoremaps,
                       float* tags, void* stream);
+
+/* HigherHRNet's multi-stage merge (_get_multi_stage_outputs, PoseEstimation.py:338-364 forward pass, :380-412 the
+ * flipped pass before its flip, with TEST.WITH_HEATMAPS [True, True] / TEST.WITH_AE [True, False] of the published
+ * configs): stage0 [B, C0, h0, w0] (heatmaps in channels 0..J-1, per-joint tags in J..C0-1), stage1 [B, C1, h1, w1]
+ * (heatmaps in 0..J-1) -> out [B, C0, h1, w1]: (up(stage0) + stage1) / 2 in channels 0..J-1, up(stage0) in J..C0-1,
+ * up = bilinear to h1 x w1 with align_corners=False (the rounding of pemp_project_maps). The merged maps of every
+ * scale and pass are what pemp_proj_maps takes (a flipped pass merged in the network's orientation: the projection
+ * applies the flip). Device pointers, stream-ordered. */
+int pemp_stage_merge(const float* stage0, int C0, int h0, int w0, const float* stage1, int C1, int h1, int w1, int B,
+                     int J, float* out, void* stream);
 /* joint_tags [N, F] of the detections from the tag channels (J + type) of scale tag_scale: F = 2
  * (up(maps), up(flip(flip_maps)) at channel J + flip_index[type]) with a flipped pass, else F = 1
  * (aggregate_results_mpn's tags_list of that scale, ConstructGraph.py:103). channels >= 2 J. */

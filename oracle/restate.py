@@ -499,3 +499,16 @@ def project_frontend(outputs, flip_outputs, size, num_joints, flip_index=None, d
             tl.append(upsample_bilinear(flips[tag_scale][:, J:2 * J][:, fi][..., ::-1], size)[..., None])
         tags = np.concatenate(tl, axis=4)
     return torch.from_numpy(scoremaps), None if tags is None else torch.from_numpy(tags)
+
+
+def stage_merge(stage0, stage1, num_joints):
+    """HigherHRNet's multi-stage merge of one pass at the last stage's resolution
+    (PoseEstimation.py:343-364, and :387-412 before the flipped pass's flip; TEST.WITH_HEATMAPS [True, True],
+    TEST.WITH_AE [True, False]): up = bilinear stage0 -> stage1's size (align_corners=False, fp32 in the
+    projection's order); heatmaps (up[:, :J] + stage1[:, :J]) / 2, tags up[:, J:]. fp32 numpy -> torch."""
+    J = num_joints
+    s0 = np.asarray(stage0, dtype=np.float32)
+    s1 = np.asarray(stage1, dtype=np.float32)
+    up = upsample_bilinear(s0, (s1.shape[2], s1.shape[3]))
+    heat = ((up[:, :J] + s1[:, :J]) / np.float32(2.0)).astype(np.float32)
+    return torch.from_numpy(np.ascontiguousarray(np.concatenate([heat, up[:, J:]], 1)))

@@ -84,6 +84,7 @@ SIGNATURES = {
                                       c_sz, c_p, c_p, c_p, c_i32, c_p, c_p]),
     "pemp_gather_projected_tags": (c_i32, [c_p, c_i32, c_i32, c_i32, c_i32, c_p, c_p, c_i64, c_p, c_p]),
     "pemp_project_maps": (c_i32, [c_p, c_i32, c_i32, c_i32, c_i32, c_i32, c_p, c_p, c_p]),
+    "pemp_stage_merge": (c_i32, [c_p, c_i32, c_i32, c_i32, c_p, c_i32, c_i32, c_i32, c_i32, c_i32, c_p, c_p]),
     "pemp_edge_features": (c_i32, [c_p, c_p, c_i32, c_p, c_p, c_i64, c_i32, c_f32, c_i32, c_p, c_p]),
     "pemp_mpn_workspace_size": (c_sz, [ctypes.POINTER(PempMpnDesc), c_i64, c_i64]),
     "pemp_mpn_forward": (c_i32, [ctypes.POINTER(PempMpnDesc), ctypes.POINTER(PempMpnWeights), c_p, c_p, c_p, c_p,

@@ -1410,6 +1410,32 @@ __global__ __launch_bounds__(256) void proj_materialize_kernel(ProjArgs pj, int 
   }
 }
 
+// HigherHRNet's multi-stage merge at the last stage's resolution (_get_multi_stage_outputs, PoseEstimation.py:338-364
+// for the forward pass, :380-412 for the flipped one, TEST.WITH_HEATMAPS [True, True] / WITH_AE [True, False]):
+// up = bilinear stage 0 (h0 x w0) -> stage 1's h1 x w1 (align_corners=False, the projection's taps and fp32 order);
+// out[b, c] = (up(s0)[b, c] + s1[b, c]) / 2 for c < J (heatmaps_avg = 0 + up(s0) + s1, / num_heatmaps = 2),
+// out[b, c] = up(s0)[b, c] for J <= c < C0 (the tags: stage 0 only). One thread per output pixel, the channels in a
+// loop (the taps are the pixel's): every row of every plane is read and written by consecutive lanes.
+__global__ __launch_bounds__(256) void stage_merge_kernel(const float* __restrict__ s0, int C0, int h0, int w0,
+                                                          const float* __restrict__ s1, int C1, int h1, int w1, int B,
+                                                          int J, float* __restrict__ out) {
+  const int64_t npix = (int64_t)B * h1 * w1, plane0 = (int64_t)h0 * w0, plane1 = (int64_t)h1 * w1;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < npix;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int x = (int)(idx % w1);
+    const int64_t r = idx / w1;
+    const int y = (int)(r % h1), b = (int)(r / h1);
+    const ProjTaps ty = proj_taps(y, h1, h0), tx = proj_taps(x, w1, w0);
+    const float* p0 = s0 + (size_t)b * C0 * plane0;
+    const float* p1 = s1 + (size_t)b * C1 * plane1 + (size_t)y * w1 + x;
+    float* po = out + (size_t)b * C0 * plane1 + (size_t)y * w1 + x;
+    for (int c = 0; c < C0; ++c) {
+      const float u = bilerp(p0 + c * plane0, w0, ty, tx.i0, tx.i1, tx.l0, tx.l1);
+      po[c * plane1] = c < J ? __fmul_rn(__fadd_rn(u, p1[c * plane1]), 0.5f) : u;
+    }
+  }
+}
+
 static int proj_args(const pemp_proj_maps* m, int J, ProjArgs* pj, const char* fn) {
   PEMP_CHECK_ARG(m && m->num_scales >= 1 && m->num_scales <= PEMP_PROJ_MAXS && m->channels >= J && m->divisor > 0.f,
                  "%s: bad projected maps (1..%d scales, channels >= J, divisor > 0)", fn, PEMP_PROJ_MAXS);
@@ -1523,6 +1549,21 @@ extern "C" int pemp_project_maps(const pemp_proj_maps* maps, int B, int J, int H
       PEMP_LAUNCH_CHECK();
     }
   }
+  return PEMP_OK;
+}
+
+extern "C" int pemp_stage_merge(const float* stage0, int C0, int h0, int w0, const float* stage1, int C1, int h1,
+                                int w1, int B, int J, float* out, void* stream) {
+  PEMP_CHECK_ARG(B > 0 && J > 0 && C0 >= J && C1 >= J && h0 > 0 && w0 > 0 && h1 > 0 && w1 > 0,
+                 "pemp_stage_merge: bad shapes (B=%d J=%d C0=%d C1=%d)", B, J, C0, C1);
+  PEMP_CHECK_ARG(stage0 && stage1 && out, "pemp_stage_merge: null pointer");
+  PEMP_CHECK_ARG((size_t)h0 * w0 < 0x7fffffffull && (size_t)h1 * w1 < 0x7fffffffull, "pemp_stage_merge: map too large");
+  const hipStream_t st = as_stream(stream);
+  const int64_t npix = (int64_t)B * h1 * w1;
+  ProfScope prof("stage_merge", st);
+  hipLaunchKernelGGL(stage_merge_kernel, dim3((unsigned)std::min<int64_t>((npix + 255) / 256, 16384)), dim3(256), 0, st,
+                     stage0, C0, h0, w0, stage1, C1, h1, w1, B, J, out);
+  PEMP_LAUNCH_CHECK();
   return PEMP_OK;
 }
 

@@ -147,6 +147,47 @@ class ProjectedHeatmaps:
         self.has_tags = C == 2 * J
         self.tag_dims = 2 if flip_outputs is not None else 1
 
+    @classmethod
+    def from_stages(cls, stage_outputs, size, num_joints, flip_stage_outputs=None, flip_index=None, divisor=None,
+                    tag_scale=0, tag_per_joint=True):
+        """The same from HigherHRNet's per-stage outputs (``_get_multi_stage_outputs``, ``PoseEstimation.py:338-412``,
+        with the published TEST.WITH_HEATMAPS [True, True] / TEST.WITH_AE [True, False]): stage_outputs is a list
+        over scales of (stage0 [B, C0, h/4-res], stage1 [B, C1, h/2-res]) pairs as the backbone returns them,
+        flip_stage_outputs the same for the flipped image (as the network produced it, not un-flipped). Each pair
+        is merged at the last stage's resolution -- (up(stage0) + stage1) / 2 for the heatmaps, up(stage0) for the
+        tags -- by ``pemp_stage_merge`` (one HBM pass, on the current stream); the image-size projection, the flip
+        average and the scale sum stay on demand in the detection's loads."""
+        from . import _lib
+        L = _lib.lib()
+        J = int(num_joints)
+
+        def merge(pair):
+            s0, s1 = (t.float().contiguous() for t in pair)
+            if s0.dim() != 4 or s1.dim() != 4 or s0.shape[0] != s1.shape[0]:
+                raise ValueError("ProjectedHeatmaps.from_stages: stages are [B, C, h, w] with the same B")
+            B, C0, h0, w0 = s0.shape
+            C1, h1, w1 = s1.shape[1:]
+            out = torch.empty(B, C0, h1, w1, dtype=torch.float32, device=s0.device)
+            _lib.check(L.pemp_stage_merge(s0.data_ptr(), C0, h0, w0, s1.data_ptr(), C1, h1, w1, B, J, out.data_ptr(),
+                                          _lib.stream(s0.device)))
+            return out
+
+        outs = [merge(p) for p in stage_outputs]
+        flips = None if flip_stage_outputs is None else [merge(p) for p in flip_stage_outputs]
+        return cls(outs, size, num_joints, flips, flip_index, divisor, tag_scale, tag_per_joint)
+
+    @staticmethod
+    def merge_stages_reference(stage0, stage1, num_joints):
+        """The reference's own torch ops for one pass of one scale (``PoseEstimation.py:343-364``): heatmaps
+        ``(0 + up(stage0)[:, :J] + stage1[:, :J]) / 2`` and tags ``up(stage0)[:, J:]``, concatenated (for checks)."""
+        J = int(num_joints)
+        up = torch.nn.functional.interpolate(stage0.float(), size=(stage1.size(2), stage1.size(3)), mode="bilinear",
+                                             align_corners=False)
+        heat = 0
+        heat += up[:, :J]
+        heat += stage1.float()[:, :J]
+        return torch.cat([heat / 2, up[:, J:]], 1)
+
     def to(self, device):
         return ProjectedHeatmaps([o.to(device) for o in self.outputs], self.size, self.num_joints,
                                  None if self.flip_outputs is None else [o.to(device) for o in self.flip_outputs],

@@ -74,3 +74,65 @@ def test_projected_maps_gather_conv_host():
         ProjectedMaps(raw, (20, 24), gather=torch.nn.Conv2d(8, 16, 3, 2, 1))
     with pytest.raises(ValueError):
         ProjectedMaps(raw, (20, 24), gather=torch.nn.Conv2d(4, 16, 3, 1, 1))
+
+
+def make_stages(seed, B, J, half_sizes, flip):
+    """HigherHRNet-shaped per-stage outputs per scale: stage 0 at 1/4 resolution with 2J channels (heatmaps + per-joint
+    tags), stage 1 at 1/2 resolution with J heatmap channels."""
+    g = torch.Generator().manual_seed(seed)
+
+    def pair(h, w):
+        s0 = torch.cat([torch.rand(B, J, h // 2, w // 2, generator=g), torch.randn(B, J, h // 2, w // 2, generator=g)], 1)
+        return s0, torch.rand(B, J, h, w, generator=g)
+
+    outs = [pair(h, w) for (h, w) in half_sizes]
+    flips = [pair(h, w) for (h, w) in half_sizes] if flip else None
+    return outs, flips
+
+
+def reference_multi_stage(stages, flip_stages, size, J, fi, tag_scale):
+    """_get_multi_stage_outputs + aggregate_results_mpn + the scale division (PoseEstimation.py:338-412, 187-229,
+    multi_scales_testing.py:144-195) restated with the reference's own torch ops, TEST.PROJECT2IMAGE."""
+    up = lambda t, hw: torch.nn.functional.interpolate(t, size=hw, mode="bilinear", align_corners=False)  # noqa: E731
+    final, tags_list = None, []
+    for k, (s0, s1) in enumerate(stages):
+        hw = (s1.size(2), s1.size(3))
+        heat, tags = 0, []
+        heat += up(s0, hw)[:, :J]
+        tags.append(up(s0, hw)[:, J:])
+        heat += s1[:, :J]
+        heatmaps = [heat / 2]
+        if flip_stages is not None:
+            f0, f1 = flip_stages[k]
+            hf = 0
+            o = torch.flip(up(f0, hw), [3])
+            hf += o[:, :J][:, fi]
+            tags.append(o[:, J:][:, fi])
+            hf += torch.flip(f1, [3])[:, :J][:, fi]
+            heatmaps.append(hf / 2)
+        heatmaps = [up(h, size) for h in heatmaps]
+        tags = [up(t, size) for t in tags]
+        if k == tag_scale:
+            tags_list += [t.unsqueeze(4) for t in tags]
+        avg = (heatmaps[0] + heatmaps[1]) / 2.0 if flip_stages is not None else heatmaps[0]
+        final = avg if final is None else final + avg
+    return final / float(len(stages)), torch.cat(tags_list, dim=4)
+
+
+@pytest.mark.parametrize("flip", [True, False])
+def test_stage_merge_restatement(flip):
+    """ProjectedHeatmaps.from_stages' merge (pemp_stage_merge; its oracle restate.stage_merge) + the projection equal
+    the reference's multi-stage, multi-scale test path run with its own torch ops: the oracle's fp32 merge within 2e-6
+    of the torch ops (FMA contraction in torch's CPU upsample); the torch-op merge fed to the projection equals the
+    reference path exactly (the flipped pass merged in the network's orientation, then flipped by the projection)."""
+    B, J, fi = 2, 17, COCO_FLIP
+    stages, flips = make_stages(4, B, J, [(40, 48), (20, 24)], flip)
+    size = (80, 96)
+    ref_s, ref_t = reference_multi_stage(stages, flips, size, J, fi, tag_scale=0)
+    merged = [ProjectedHeatmaps.merge_stages_reference(a, b, J) for a, b in stages]
+    mflip = None if flips is None else [ProjectedHeatmaps.merge_stages_reference(a, b, J) for a, b in flips]
+    for (a, b), m in zip(stages + (flips or []), merged + (mflip or [])):
+        assert (restate.stage_merge(a, b, J) - m).abs().max().item() <= 2e-6
+    ph = ProjectedHeatmaps(merged, size, J, mflip, fi if flip else None)
+    s, t = ph.materialize()
+    assert torch.equal(s, ref_s) and torch.equal(t, ref_t)

@@ -421,3 +421,37 @@ def test_projected_frontend_three_scales_c5(graph, H, W):
             assert torch.equal(out[i].cpu(), ref[i]), i
         assert out[14].shape[1] == 2                               # F = 2: the flipped pass's tags too
         assert (out[0].cpu() - ref[0]).abs().max().item() <= 2e-6
+
+
+@pytest.mark.parametrize("flip,half_sizes,size", [(True, [(80, 80), (40, 40)], (160, 160)),
+                                                  (False, [(90, 70)], (180, 140))])
+def test_projected_frontend_from_stages(flip, half_sizes, size):
+    """ProjectedHeatmaps.from_stages: HigherHRNet's per-stage outputs (1/4-res heatmaps + tags, 1/2-res heatmaps)
+    merged by pemp_stage_merge (_get_multi_stage_outputs, PoseEstimation.py:338-412) bit-exact with the oracle's
+    restate.stage_merge; construct_graph on the result bit-exact with the oracle on the projection of those maps."""
+    from pemp_amd.frontend import ProjectedHeatmaps
+    from tests.test_frontend_cpu import COCO_FLIP, make_stages
+    B, J = 2, 17
+    stages, flips = make_stages(12, B, J, half_sizes, flip)
+    # plant peaks in stage 1 so that detections exist (the random maps alone hold few maxima above 0.1)
+    for k, (h, w) in enumerate(half_sizes):
+        peaks = torch.from_numpy(syn.make_heatmaps(60 + k, B, J, h, w, 4, sigma=1.0, margin=2))
+        stages[k] = (stages[k][0] * 0.2, torch.maximum(stages[k][1] * 0.2, peaks))
+    fi = COCO_FLIP if flip else None
+    dev_stages = [(a.to(DEV), b.to(DEV)) for a, b in stages]
+    dev_flips = None if flips is None else [(a.to(DEV), b.to(DEV)) for a, b in flips]
+    ph = ProjectedHeatmaps.from_stages(dev_stages, size, J, dev_flips, fi)
+    merged = [restate.stage_merge(a, b, J) for a, b in stages]
+    mflip = None if flips is None else [restate.stage_merge(a, b, J) for a, b in flips]
+    for got, want in zip(ph.outputs + (ph.flip_outputs or []), merged + (mflip or [])):
+        assert torch.equal(got.cpu(), want)
+    s, t = restate.project_frontend(merged, mflip, size, J, fi)
+    feats = torch.from_numpy(syn.closed_form((B, 128) + tuple(size), 0.25))
+    gc = pcfg.inference_gc_config("fully", 5, False)
+    ref = restate.construct_graph(s, feats, t, None, gc, J)
+    assert ref[7].shape[0] > 2 * J
+    out = pemp_amd.get_graph_constructor(gc, scoremaps=ph, features=feats.to(DEV), tagmaps=ph, joints_gt=None,
+                                         factor_list=None, masks=None, device=DEV, testing=True, heatmaps=None,
+                                         num_joints=J).construct_graph()
+    for i in (7, 11, 12, 14, 2, 0, 1):
+        assert torch.equal(out[i].cpu(), ref[i]), i
