@@ -14,3 +14,7 @@ done; done
 PEMP_GAEC_EXACT=1 timeout -k 5 60 python -u tools/gaec_bench.py 8 153 9 1 20 | sed "s/^/exact /"
 timeout -k 5 60 python -u tools/gaec_bench.py 1 502 36 1 20
 PEMP_GAEC_EXACT=1 timeout -k 5 60 python -u tools/gaec_bench.py 1 502 36 1 10 | sed "s/^/exact /"
+# MFMA utilisation calibration: dense f16 MFMA on every SIMD, events, then the SQ / GRBM counters
+timeout -k 5 60 build_ab/mfma_peak 20000 1 | tee gpurun_out/r05a_mfma_peak.json
+timeout -s KILL 60 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_MFMA SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d gpurun_out/r05a_mfma_pmc -o pmc -- build_ab/mfma_peak 20000 1 > gpurun_out/r05a_mfma_pmc.log 2>&1
+echo "mfma pmc rc=$?"
