@@ -1287,7 +1287,16 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
 #define PEMP_XDL_GUARD "s_nop 7\n\ts_nop 7\n\ts_nop 4\n\t"
 // ... and closes with the 2 VALU-write -> DPP-read wait states: the compiler does not see the asm's last writes
 // either, and its next DPP read of one of them (the carry's row shifts) would otherwise read the stale value
+#ifdef PEMP_ASM_TAILPAD   // diagnostics: a long pad after the asm blocks
+#define PEMP_DPP_TAIL "s_nop 7\n\ts_nop 7\n\ts_nop 7\n\t"
+#else
 #define PEMP_DPP_TAIL "s_nop 1\n\t"
+#endif
+#ifdef PEMP_ASM_VOLATILE
+#define PEMP_SCAN_ASM asm volatile
+#else
+#define PEMP_SCAN_ASM asm
+#endif
 #ifndef PEMP_ASM_SCANS
 #define PEMP_ASM_SCANS 1
 #endif
@@ -1331,7 +1340,7 @@ __device__ __forceinline__ float chunk_max_asm(float v, const ChunkMasks& mk) {
   PEMP_FMAC1(10, ctl, m) PEMP_FMAC1(11, ctl, m) PEMP_FMAC1(12, ctl, m) PEMP_FMAC1(13, ctl, m)                   \
   PEMP_FMAC1(14, ctl, m) PEMP_FMAC1(15, ctl, m) PEMP_FMAC1(16, ctl, m)
 __device__ __forceinline__ void seg_sum17_asm(float (&v)[4][4], float& l, const ScanMask& m) {
-  asm(PEMP_XDL_GUARD PEMP_FMAC17("row_shr:1", 17) PEMP_FMAC17("row_shr:2", 18) PEMP_FMAC17("row_shr:4", 19)
+  PEMP_SCAN_ASM(PEMP_XDL_GUARD PEMP_FMAC17("row_shr:1", 17) PEMP_FMAC17("row_shr:2", 18) PEMP_FMAC17("row_shr:4", 19)
           PEMP_FMAC17("row_shr:8", 20) PEMP_DPP_TAIL
       : "+v"(v[0][0]), "+v"(v[0][1]), "+v"(v[0][2]), "+v"(v[0][3]), "+v"(v[1][0]), "+v"(v[1][1]), "+v"(v[1][2]),
         "+v"(v[1][3]), "+v"(v[2][0]), "+v"(v[2][1]), "+v"(v[2][2]), "+v"(v[2][3]), "+v"(v[3][0]), "+v"(v[3][1]),
@@ -1548,7 +1557,11 @@ __device__ __forceinline__ void dma_rows_async(u32x4v_s rs, int base, float* buf
 // above (the tile's unconditional stores), its rows have landed.
 template <int N>
 __device__ __forceinline__ void dma_wait() {
+#ifdef PEMP_DMA_DRAIN   // diagnostics: wait for every outstanding vector-memory op instead of the hand count
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+#endif
 }
 
 #ifndef PEMP_FAST_EXP
