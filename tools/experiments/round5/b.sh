@@ -10,3 +10,8 @@ for v in asmall asmall_drain asmall_vol asmall_tail; do
 done
 timeout -k 10 400 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/r05b_gpu_tests.log 2>&1
 echo "suite rc=$? $(tail -1 gpurun_out/r05b_gpu_tests.log)"; grep FAILED gpurun_out/r05b_gpu_tests.log | head
+timeout -k 5 60 build_ab/mfma_peak 20000 1 | tee gpurun_out/r05b_mfma_peak.json
+timeout -s KILL 60 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/r05b_mfma_pmc -o pmc -- build_ab/mfma_peak 20000 1 > gpurun_out/r05b_mfma_pmc.log 2>&1
+python tools/mfma_util.py gpurun_out/r05b_mfma_pmc/pmc_counter_collection.csv
+timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE --kernel-include-regex 'edge_step|edge_embed|node_' --output-format csv -d gpurun_out/r05b_mfma_c3 -o pmc -- python bench.py --workload c3 --steps 3 --warmup 1 --no-cpu-baseline --no-roofline > gpurun_out/r05b_mfma_c3.log 2>&1
+python tools/mfma_util.py gpurun_out/r05b_mfma_c3/pmc_counter_collection.csv

@@ -1,0 +1,53 @@
+"""MFMA utilisation per kernel from a rocprofv3 --pmc CSV holding SQ_VALU_MFMA_BUSY_CYCLES and GRBM_GUI_ACTIVE.
+
+util = SQ_VALU_MFMA_BUSY_CYCLES / (SIMDs x kernel cycles), kernel cycles = GRBM_GUI_ACTIVE / XCDs
+(rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs, MI355X_MICROARCH.md 'DVFS give-back'; SQ_VALU_MFMA_BUSY_CYCLES
+is summed over every SIMD and counts 16 cycles per v_mfma_f32_16x16x32_{f16,bf16}, calibrated with
+tools/ubench/mfma_peak.hip, where the counter figure equals the event-timed TFLOP/s over the peak at the clock
+the same counters give). 256 CUs x 4 SIMDs, 8 XCDs.
+usage: python tools/mfma_util.py pmc_counter_collection.csv [kernel-regex] [--json]"""
+import csv
+import json
+import re
+import sys
+from collections import defaultdict
+
+SIMDS, XCDS = 1024, 8
+
+
+def per_dispatch(path, rx=None):
+    d = defaultdict(dict)
+    names = {}
+    for r in csv.DictReader(open(path)):
+        if rx and not re.search(rx, r["Kernel_Name"]):
+            continue
+        k = (r["Dispatch_Id"])
+        d[k][r["Counter_Name"]] = d[k].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        names[k] = r["Kernel_Name"]
+    return d, names
+
+
+def summarize(path, rx=None):
+    d, names = per_dispatch(path, rx)
+    by = defaultdict(list)
+    for k, v in d.items():
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in v and v.get("GRBM_GUI_ACTIVE"):
+            cyc = v["GRBM_GUI_ACTIVE"] / XCDS
+            by[names[k]].append((v["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * cyc), cyc, v.get("SQ_INSTS_MFMA", 0.0)))
+    out = {}
+    for n, vals in by.items():
+        vals.sort()
+        med = vals[len(vals) // 2]
+        out[n] = {"mfma_busy": round(med[0], 4), "dispatches": len(vals), "kernel_cycles_median": round(med[1]),
+                  "mfma_insts_median": med[2]}
+    return out
+
+
+if __name__ == "__main__":
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    res = summarize(args[0], args[1] if len(args) > 1 else None)
+    if "--json" in sys.argv:
+        print(json.dumps(res, indent=1))
+    else:
+        for n, v in sorted(res.items(), key=lambda kv: -kv[1]["mfma_busy"]):
+            print(f"{v['mfma_busy']:7.4f}  n={v['dispatches']:<4d} cycles={v['kernel_cycles_median']:<9d} {n[:110]}")

@@ -22,10 +22,22 @@ __global__ __launch_bounds__(256) void k_mfma(int iters, float* out) {
   float4v c[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) c[k] = float4v{0.f, 0.f, 0.f, 0.f};
+  // eight accumulate chains in one asm statement per iteration (the compiler's allocation of the builtin's chains
+  // shuffled them through AGPR copies every iteration); the closing pad covers MFMA D -> compiler reader
   for (int it = 0; it < iters; ++it) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) c[k] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c[k], 0, 0, 0);
+    asm volatile(
+        "v_mfma_f32_16x16x32_f16 %0, %8, %9, %0\n\t"
+        "v_mfma_f32_16x16x32_f16 %1, %8, %9, %1\n\t"
+        "v_mfma_f32_16x16x32_f16 %2, %8, %9, %2\n\t"
+        "v_mfma_f32_16x16x32_f16 %3, %8, %9, %3\n\t"
+        "v_mfma_f32_16x16x32_f16 %4, %8, %9, %4\n\t"
+        "v_mfma_f32_16x16x32_f16 %5, %8, %9, %5\n\t"
+        "v_mfma_f32_16x16x32_f16 %6, %8, %9, %6\n\t"
+        "v_mfma_f32_16x16x32_f16 %7, %8, %9, %7"
+        : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7])
+        : "v"(a), "v"(b));
   }
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
   float s = 0.f;
 #pragma unroll
   for (int k = 0; k < 8; ++k) s += c[k][0] + c[k][1] + c[k][2] + c[k][3];
