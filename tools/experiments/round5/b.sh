@@ -2,7 +2,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 120 python -u tools/debug/cap_mode_debug.py > gpurun_out/r05b_capdbg.log 2>&1
+PYTHONPATH=$PWD timeout -k 10 120 python -u tools/debug/cap_mode_debug.py > gpurun_out/r05b_capdbg.log 2>&1
 echo "capdbg rc=$?"; cat gpurun_out/r05b_capdbg.log | tail -20
 for v in asmall asmall_drain asmall_vol asmall_tail; do
   PEMP_LIB=$PWD/build_ab/libpemp_$v.so timeout -k 10 120 python -u -m pytest tests/test_gpu_mpn.py -q -k "golden and attn and bf16x3" --timeout 100 --timeout-method thread > gpurun_out/r05b_$v.log 2>&1
