@@ -1623,6 +1623,12 @@ __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_
   const int t = __builtin_amdgcn_readfirstlane(rg.z);
   const int rflags = __builtin_amdgcn_readfirstlane(rg.w);
   float* mybuf = rbuf + wave * 1024;
+#ifdef PEMP_LDS_ZERO   // diagnostics: this wave's row buffer and piece records zeroed before first use
+#pragma unroll
+  for (int k = 0; k < 4; ++k) *reinterpret_cast<float4*>(mybuf + 256 * k + 4 * lane) = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int k = lane; k < 2 * PREC_F; k += 64) pieces[2 * wave * PREC_F + k] = 0.f;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
   const int E = (int)(a.ne ? a.ne[1] : a.E);
   float* const logits = a.edge_logits && a.ne ? a.edge_logits + (int64_t)a.rec * E : a.edge_logits;
   // r / Q0 rows past the wave's range end are out of the descriptor: the last tile's DMA moves no bytes
@@ -1930,6 +1936,12 @@ __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_
     // weight multiplied in separately -- the bf16x3 / fp32 kernels -- they gave wrong aggregates on the GPU
     // (bf16x3 logits 1e-3 off), for a reason not found; those kernels keep the compiler's scans)
     if (PEMP_ASM_SCANS && (PE_FOLD || (PEMP_ASM_ALL && AGG != PEMP_AGGR_MAX))) {
+#ifdef PEMP_ASM_OPAQUE_IN   // diagnostics: the scan inputs pinned in registers by an empty volatile statement
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+        asm volatile("" : "+v"(v[ob][0]), "+v"(v[ob][1]), "+v"(v[ob][2]), "+v"(v[ob][3]));
+      asm volatile("" : "+v"(l));
+#endif
 #ifdef PEMP_ASM_CHECK   // diagnostics: the asm sums against the compiler's on the same inputs, first mismatches printed
       float vin[4][4], vc[4][4], lin = l, lc = l;
 #pragma unroll

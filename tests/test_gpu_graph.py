@@ -436,7 +436,9 @@ def test_projected_frontend_from_stages(flip, half_sizes, size):
     # plant peaks in stage 1 so that detections exist (the random maps alone hold few maxima above 0.1)
     for k, (h, w) in enumerate(half_sizes):
         peaks = torch.from_numpy(syn.make_heatmaps(60 + k, B, J, h, w, 4, sigma=1.0, margin=2))
-        stages[k] = (stages[k][0] * 0.2, torch.maximum(stages[k][1] * 0.2, peaks))
+        stages[k] = (stages[k][0] * 0.05, torch.maximum(stages[k][1] * 0.05, peaks))
+        if flips is not None:
+            flips[k] = (flips[k][0] * 0.05, torch.maximum(flips[k][1] * 0.05, torch.flip(peaks, [3])))
     fi = COCO_FLIP if flip else None
     dev_stages = [(a.to(DEV), b.to(DEV)) for a, b in stages]
     dev_flips = None if flips is None else [(a.to(DEV), b.to(DEV)) for a, b in flips]

@@ -273,6 +273,7 @@ def test_capacity_mode_mpn(prec, monkeypatch):
     from pemp_amd.graph_constructor import NaiveGraphConstructor
     B, J, H, W = 2, 17, 96, 104
     NaiveGraphConstructor._graph_hint.clear()               # capacities from earlier tests' batches of this shape
+    NaiveGraphConstructor._cap = 512                          # (an earlier test's crowded maps grow it past 2048)
     gc = pcfg.inference_gc_config("fully", 5, False)
     cfg = pcfg.published_mpn_config(J, 3, "attn")
     model, _ = make_model(cfg, 1.25, prec)
@@ -326,10 +327,10 @@ def test_capacity_mode_mpn(prec, monkeypatch):
                 first = flat
             assert all(torch.equal(a, b) for a, b in zip(flat, first))
             del out, got
-        d = [b - a for a, b in zip(stats0, graph_stats())]
-        # a repeating argument set is captured on its second sight and replayed after that (a single repeating
-        # key included: the round-4 marker bug never captured it)
-        assert d[0] >= 1 and d[1] >= 2 and d[2] == 0, d
+        # (whether these five calls repeat an argument set -- and so capture / replay a graph -- depends on the
+        # caching allocator handing back the same buffers; test_capacity_graphs_single_key_and_debug_sync pins the
+        # capture logic with identical arguments)
+        assert graph_stats()[2] == stats0[2]                    # no capture was refused
     finally:
         pemp_amd.bind_mpn(None)
 
@@ -362,8 +363,10 @@ def test_capacity_graphs_single_key_and_debug_sync(tmp_path):
         assert r.returncode == 0, r.stderr[-3000:]
         outs[dbg] = json.loads(r.stdout.strip().splitlines()[-1])
     plain, dbg = outs["0"], outs["1"]
-    assert plain["stats"][0] == 1 and plain["stats"][1] >= 2 and plain["stats"][2] == 0, plain
-    assert dbg["stats"] == [0, 0, 0], dbg
+    # direct, capture (+ its first launch), replay, replay
+    assert plain["per_call"] == [[0, 0, 0], [1, 1, 0], [1, 2, 0], [1, 3, 0]], plain
+    assert dbg["per_call"] == [[0, 0, 0]] * 4, dbg
+    # the logits of the last call (a replay), of a fresh call and under debug sync are identical
     assert plain["sums"] == dbg["sums"] and len(set(map(tuple, plain["sums"]))) == 1, (plain, dbg)
 
 
@@ -392,10 +395,23 @@ def step():
         got = model(out[0], out[1], out[2], node_types=out[7][:, 2])
     torch.cuda.synchronize()
     return [float(t.double().sum()) for t in got[0] + got[1] + got[2]]
-step(); step()                      # sets the capacities (exact build), then the first capacity-mode call
-s0 = stats()
-sums = [step() for _ in range(4)]   # one repeating key: direct, capture, replay, replay (if the allocator repeats)
-print(json.dumps({"stats": [b - a for a, b in zip(s0, stats())], "sums": sums}))
+step()                              # sets the capacities (exact build)
+L = _lib.lib()
+real = L.pemp_mpn_forward_fully_cap
+calls = []
+def once(*args):                    # the same argument set four times in a row: direct, capture, replay, replay
+    s0 = stats()
+    for _ in range(4):
+        rc = real(*args)
+        if rc:
+            return rc
+        torch.cuda.synchronize()
+        calls.append([b - a for a, b in zip(s0, stats())])
+    return 0
+L.pemp_mpn_forward_fully_cap = once
+sums = [step()]
+L.pemp_mpn_forward_fully_cap = real
+print(json.dumps({"per_call": calls, "sums": sums + [step()]}))
 """
 
 
