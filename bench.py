@@ -49,6 +49,7 @@ WORKLOADS = {
 }
 FLIP_INDEX = {17: [0, 2, 1, 4, 3, 6, 5, 8, 7, 10, 9, 12, 11, 14, 13, 16, 15],   # COCO FLIP_CONFIG
               14: [1, 0, 3, 2, 5, 4, 7, 6, 9, 8, 11, 10, 12, 13]}               # CrowdPose
+PREC_CODE = {"fp32": 0, "bf16x3": 1, "f16x3": 2}   # PEMP_PREC_* (include/pemp.h)
 FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: dense f32 MFMA (= f32 vector) peak
 HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 BF16_MFMA_PEAK_TFLOPS = 2500.0     # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
@@ -56,6 +57,7 @@ REF_EDGE_FLOP = 82048              # the reference's FLOP per edge-
 GEMM64 = 2 * 64 * 64                            # one 64x64 GEMM per edge
 EDGE_HEAD_FLOP = 2 * (64 * 64 + 64 * 32 + 32)   # fused edge-classification head
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_latest.json")   # tools/gpu_profile.sh + tools/pmc_json.py
+MFMA_FILE = os.path.join(ROOT, "profiles", "mfma_latest.json")  # tools/mfma_util.py --json over an SQ pass
 PREC_NOTE = {
     "f16x3": "f16x3: f16 MFMA on hi/lo split operands (22 bits each), fp32 accumulate; fp32-level logits",
     "bf16x3": "bf16x3: bf16 MFMA on hi/lo split operands, fp32 accumulate (opt-in, ~2^-16 per product)",
@@ -72,6 +74,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=30.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--profile-steps", action="store_true",
+                    help="for rocprofv3 per-shape traces: the warmup and the K steps strictly serial on one stream, "
+                         "nothing else (no schedule probe, roofline, isolated MPN, e2e, grouping or CPU legs)")
     ap.add_argument("--streams", type=int, default=0,
                     help="batches in flight: step i runs on HIP stream i %% S (serving-style overlap of one "
                          "batch's detection with the previous batch's MPN); 1 = strictly serial steps; 0 (default) "
@@ -204,6 +209,29 @@ def pmc_traffic(kernel_prefix, workload, E):
     return None
 
 
+def mfma_busy(kernel_prefix, workload):
+    """MFMA utilisation of the kernel (SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs), the
+    median over its dispatches) from the committed SQ pass of the same workload (profiles/mfma_latest.json,
+    tools/mfma_util.py; the formula reads 0.86 on the dense-MFMA microbench tools/ubench/mfma_peak.hip)."""
+    try:
+        runs = json.load(open(MFMA_FILE))["runs"]
+    except (OSError, ValueError, KeyError):
+        return None
+    for run in runs:
+        if run.get("workload") == workload:
+            hits = [v for k, v in run["kernels"].items() if kernel_prefix in k]
+            return hits[0]["mfma_busy"] if len(hits) == 1 else None
+    return None
+
+
+def graph_stats():
+    """The capacity-mode forward's HIP-graph counters since the library loaded (pemp_mpn_graph_stats)."""
+    import ctypes
+    out = (ctypes.c_uint64 * 3)()
+    _lib.check(_lib.lib().pemp_mpn_graph_stats(out))
+    return {"captures": out[0], "launches": out[1], "refused": out[2]}
+
+
 def seg_rows_bytes(ei, types):
     """Aggregate-row bytes one edge pass writes: 64 fp32 per non-empty (target, source type) segment."""
     T = int(types.max().item()) + 1 if types.numel() else 1
@@ -230,7 +258,11 @@ def roofline_for(label, stats, E, wl, precision, upd, workload, agg_bytes=0):
         flop, byts = E * f1, E * b1 + agg_bytes
         gbs = byts / avg_s / 1e9
         traffic = pmc_traffic("pemp::edge_step_kernel<0," + ("1" if head else "0"), workload, E)
+        mb = mfma_busy("edge_step_kernel<0, " + ("1" if head else "0") + ", " + str(PREC_CODE[precision]), workload)
         common = {"kernel": label, "avg_launch_us": round(avg_s * 1e6, 2), "launches": n, "traffic": traffic,
+                  "mfma_busy": mb,
+                  "mfma_busy_source": f"profiles/mfma_latest.json ({workload}): SQ_VALU_MFMA_BUSY_CYCLES / "
+                                      f"(1024 SIMDs x GRBM_GUI_ACTIVE / 8)" if mb is not None else None,
                   "traffic_source": f"profiles/pmc_latest.json ({workload}, E={E})" if traffic else None,
                   "algorithmic": f"{f1} FLOP and {b1} B HBM x E={E} edges + {agg_bytes} B of aggregate rows "
                                  f"per launch",
@@ -690,6 +722,21 @@ def main():
         pemp_amd.bind_mpn(model)   # capacity mode: the MPN queued behind the graph build, ahead of the counts
     _lib.lib()
 
+    if args.profile_steps:
+        for _ in range(max(args.warmup, 1)):
+            run_step(wl, gc, model, hm, feats, tags, dev)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            run_step(wl, gc, model, hm, feats, tags, dev)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        if rank == 0:
+            print(json.dumps({"profile_steps": args.steps, "workload": args.workload,
+                              "ms_per_step": round(dt / args.steps * 1e3, 3), "graph_stats": graph_stats()}),
+                  flush=True)
+        return
+
     # batches in flight: each stream has its own library scratch (construct_graph and the MPN are
     # reentrant per (device, stream)); inputs are read-only and resident before the timed region
     S = max(1, args.streams) if args.streams > 0 else 2
@@ -861,6 +908,7 @@ def main():
             "pose_grouping": grouping,
             # the one collective of the sharded path (RCCL all_gather of every rank's grouped poses)
             "pose_all_gather_ms": grouping.get("pose_all_gather_ms") if grouping else None,
+            "capacity_graphs": graph_stats(),
         }
         if cpu:
             rec["speedup_vs_cpu"] = round(value / cpu["value"], 1)

@@ -5,7 +5,9 @@ util = SQ_VALU_MFMA_BUSY_CYCLES / (SIMDs x kernel cycles), kernel cycles = GRBM_
 is summed over every SIMD and counts 16 cycles per v_mfma_f32_16x16x32_{f16,bf16}, calibrated with
 tools/ubench/mfma_peak.hip, where the counter figure equals the event-timed TFLOP/s over the peak at the clock
 the same counters give). 256 CUs x 4 SIMDs, 8 XCDs.
-usage: python tools/mfma_util.py pmc_counter_collection.csv [kernel-regex] [--json]"""
+usage: python tools/mfma_util.py pmc_counter_collection.csv [kernel-regex] [--json]
+       python tools/mfma_util.py pmc_counter_collection.csv --merge profiles/mfma_latest.json --workload c3
+       (adds / replaces the workload's run in the bench's source file)"""
 import csv
 import json
 import re
@@ -43,9 +45,29 @@ def summarize(path, rx=None):
     return out
 
 
+def merge(path, workload, res, source):
+    try:
+        doc = json.load(open(path))
+    except (OSError, ValueError):
+        doc = {"formula": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs), median over dispatches",
+               "runs": []}
+    doc["runs"] = [r for r in doc["runs"] if r.get("workload") != workload]
+    doc["runs"].append({"workload": workload, "source": source, "kernels": res})
+    json.dump(doc, open(path, "w"), indent=1)
+
+
 if __name__ == "__main__":
-    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    argv = sys.argv[1:]
+    opts = {}
+    for key in ("--merge", "--workload"):
+        if key in argv:
+            i = argv.index(key)
+            opts[key] = argv[i + 1]
+            del argv[i:i + 2]
+    args = [a for a in argv if not a.startswith("--")]
     res = summarize(args[0], args[1] if len(args) > 1 else None)
+    if "--merge" in opts:
+        merge(opts["--merge"], opts["--workload"], res, args[0])
     if "--json" in sys.argv:
         print(json.dumps(res, indent=1))
     else:
