@@ -608,7 +608,9 @@ def e2e_pipeline(wl, gc, model, hm, feats, tags, dev, steps, warmup, world):
 def person_structured_probs(wl, out):
     """Edge and node probabilities shaped like a trained network's for construct_graph output `out`: node i of
     an image belongs to person (local index mod persons_per_image); edge probabilities sigmoid(+-2.5 + N(0, 1.5))
-    for same / different persons, drawn per direction; node probabilities sigmoid(2 + N(0, 1))."""
+    for same / different persons, drawn per direction; node probabilities sigmoid(2 + N(0, 1)), except one node in
+    six at sigmoid(-4 + N(0, 1)) (below the grouping's 0.1 node threshold): those joints are missing from their
+    persons, as occluded joints are, so the finishing's refine has joints to search."""
     det, ei, bi = out[7], out[2], out[12]
     N, E = det.shape[0], ei.shape[1]
     node_off = torch.searchsorted(bi, torch.arange(wl["B"] + 1, device=bi.device))
@@ -617,7 +619,8 @@ def person_structured_probs(wl, out):
     with torch.no_grad():
         same = pid[ei[0]] == pid[ei[1]]
         pe_p = torch.sigmoid(torch.where(same, 2.5, -2.5) + 1.5 * torch.randn(E, generator=gen, device=bi.device))
-        pn_p = torch.sigmoid(2.0 + torch.randn(N, generator=gen, device=bi.device))
+        low = torch.rand(N, generator=gen, device=bi.device) < 1.0 / 6.0
+        pn_p = torch.sigmoid(torch.where(low, -4.0, 2.0) + torch.randn(N, generator=gen, device=bi.device))
     return pe_p, pn_p
 
 

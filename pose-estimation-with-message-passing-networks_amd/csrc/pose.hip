@@ -776,13 +776,26 @@ __device__ __forceinline__ unsigned long long refine_key(float v, uint32_t idx) 
 // end are clamped to the last pixel (a true candidate with its own index). A thread visits its pixels in
 // increasing order, so a strict > keeps the first maximum; (value, index) pairs become ordered 64-bit keys
 // only for the cross-thread reduction.
+// Only (person, joint) pairs whose joint is not detected (keypoints[p, i, 2] == 0) are searched: the reference
+// computes the argmax for every pair but keeps it only for those (Utils.py:1096-1101), so the others are skipped
+// (block-uniform branches; a chunk with every person's joint i detected returns at once and stores nothing --
+// refine_finish_kernel reads keys only for the pairs searched).
 template <int PC, int F>
 __global__ __launch_bounds__(256) void refine_argmax_kernel(const float* __restrict__ s, const float* __restrict__ tag,
                                                             int H, int W, const float* __restrict__ mean_tag,
-                                                            int P, unsigned long long* __restrict__ keys, int J) {
+                                                            int P, unsigned long long* __restrict__ keys, int J,
+                                                            const double* __restrict__ kp) {
   const int i = blockIdx.y;
   const int p0 = blockIdx.z * PC;
   const int np_ = min(PC, P - p0);
+  bool need[PC];
+  bool any = false;
+#pragma unroll
+  for (int q = 0; q < PC; ++q) {
+    need[q] = q < np_ && kp[((size_t)(p0 + q) * J + i) * 3 + 2] == 0.0;
+    any |= need[q];
+  }
+  if (!any) return;
   float mt0[PC], mt1[PC], bv[PC];
   uint32_t bi[PC];
   const size_t HW = (size_t)H * W;
@@ -813,6 +826,7 @@ __global__ __launch_bounds__(256) void refine_argmax_kernel(const float* __restr
     for (int u = 0; u < 4; ++u) {
 #pragma unroll
       for (int q = 0; q < PC; ++q) {
+        if (!need[q]) continue;                  // (block-uniform)
         const float d0 = __fsub_rn(t0[u], mt0[q]);
         float k;
         if (F == 2) {
@@ -846,7 +860,10 @@ __global__ __launch_bounds__(256) void refine_argmax_kernel(const float* __restr
     if (lane == 0) red[wv][q] = k;
   }
   __syncthreads();
-  if (threadIdx.x < np_) {  // per-block partial: no cross-XCD atomics on the same few addresses
+  bool mine = false;   // this thread's person (q = threadIdx.x) was searched
+#pragma unroll
+  for (int q = 0; q < PC; ++q) mine |= need[q] && (int)threadIdx.x == q;
+  if (mine) {  // per-block partial: no cross-XCD atomics on the same few addresses
     const int q = threadIdx.x;
     unsigned long long k = red[0][q];
     for (int w2 = 1; w2 < (int)(blockDim.x >> 6); ++w2) k = red[w2][q] > k ? red[w2][q] : k;
@@ -862,6 +879,7 @@ __global__ __launch_bounds__(64) void refine_finish_kernel(const float* __restri
                                                            int P, int J, double* __restrict__ kp) {
   const int t = blockIdx.x;
   const int i = t % J, p = t / J;
+  if (kp[(size_t)t * 3 + 2] != 0.0) return;   // a detected joint: nothing searched, nothing changes
   unsigned long long key = 0ull;
   for (int b = threadIdx.x; b < nblk; b += 64) {
     const unsigned long long k = keys[((size_t)i * nblk + b) * P + p];
@@ -943,10 +961,10 @@ extern "C" int pemp_pose_refine(const float* scoremaps, const float* tag, int J,
   case N:                                                                                                       \
     if (F == 1)                                                                                                 \
       hipLaunchKernelGGL((refine_argmax_kernel<N, 1>), grid, dim3(256), 0, st, scoremaps, tag, H, W, mean_tag, P,  \
-                         keys, J);                                                                              \
+                         keys, J, keypoints);                                                                   \
     else                                                                                                        \
       hipLaunchKernelGGL((refine_argmax_kernel<N, 2>), grid, dim3(256), 0, st, scoremaps, tag, H, W, mean_tag, P,  \
-                         keys, J);                                                                              \
+                         keys, J, keypoints);                                                                   \
     break;
   switch (pc) {
     PEMP_REFINE_LAUNCH(2)

@@ -15,6 +15,7 @@ person assembly run in C++ in the same library, one image per host thread. No nu
 sits on the path. ``greedy`` (``Utils.py:517-626``) runs on the host after the same edge pass
 (``pemp_pose_greedy``). ``MUT`` and ``KL`` are not built (NotImplementedError).
 """
+import functools
 import os
 
 import numpy as np
@@ -514,17 +515,27 @@ def reverse_affine_map(keypoints, img_size_orig, input_size, scaling_type, min_s
     stride, 512 input). img_size_orig = (width, height). Raises NotImplementedError otherwise, as the
     reference ("short_mine" needs a helper missing from the reference itself)."""
     w0, h0 = img_size_orig[0], img_size_orig[1]
+    if scaling_type not in ("short", "short_with_resize", "long", "long_with_multiscale"):
+        raise NotImplementedError(f"reverse_affine_map: scaling_type={scaling_type!r}")
+    mat = _reverse_matrix(w0, h0, input_size, scaling_type, min_scale)
+    pts = keypoints[:, :, :2] * 4 if scaling_type in ("long", "long_with_multiscale") else keypoints[:, :, :2]
+    keypoints[:, :, :2] = apply_affine(pts, mat)
+    return keypoints
+
+
+@functools.lru_cache(maxsize=256)
+def _reverse_matrix(w0, h0, input_size, scaling_type, min_scale):
+    """The [2, 3] map of reverse_affine_map for one image size (the same matrix for every image of that size, so it
+    is solved once: the 6 x 6 solve was most of the call's time)."""
     if scaling_type in ("short", "short_with_resize"):
         size, center, scale = multi_scale_size(h0, w0, input_size, 1.0, min_scale)
         out = (int(size[0] / 2), int(size[1] / 2)) if scaling_type == "short" else (int(size[0]), int(size[1]))
-        keypoints[:, :, :2] = apply_affine(keypoints[:, :, :2], crop_affine(center, scale, out, inv=True))
-        return keypoints
-    if scaling_type in ("long", "long_with_multiscale"):
+        mat = crop_affine(center, scale, out, inv=True)
+    else:
         if input_size != 512:
             raise AssertionError("reverse_affine_map: 'long' scaling needs input_size 512")
         s = max(h0, w0) / 200
         res = (512, 512) if scaling_type == "long" else (1024, 1024)
-        mat = box_transform(np.array((w0 / 2, h0 / 2)), np.array([s, s]), res)
-        keypoints[:, :, :2] = apply_affine(keypoints[:, :, :2] * 4, np.linalg.pinv(mat)[:2])
-        return keypoints
-    raise NotImplementedError(f"reverse_affine_map: scaling_type={scaling_type!r}")
+        mat = np.linalg.pinv(box_transform(np.array((w0 / 2, h0 / 2)), np.array([s, s]), res))[:2]
+    mat.setflags(write=False)
+    return mat
