@@ -522,8 +522,9 @@ def e2e_pipeline(wl, gc, model, hm, feats, tags, dev, steps, warmup, world):
     model_58_4_4.yaml:170-172), reverse_affine_map. The MPN runs in every step; its closed-form weights form
     no person, so the edge / node probabilities the grouping reads are person_structured_probs of the same graph
     (the class probabilities are the MPN's softmax). Pipelined: batch k+1's GPU part (graph, MPN, edge pass,
-    copies) is queued before batch k's host part (GAEC, persons, finishing on a side stream) runs, as a server with
-    one batch in flight on each side would; `serial_*` runs the same steps one after the other."""
+    copies) is queued before batch k's host part (GAEC, persons) runs and queues its finishing (refine / adjust on
+    a side stream), whose keypoints are collected (reverse_affine_map) after batch k+1's grouping, as a server with
+    batches in flight would; `serial_*` runs the same steps one after the other."""
     from pemp_amd import pose as ppose
     J, B, H, W = wl["J"], wl["B"], wl["H"], wl["W"]
     maps, tag_maps = dense_maps(hm, tags)
@@ -560,27 +561,41 @@ def e2e_pipeline(wl, gc, model, hm, feats, tags, dev, steps, warmup, world):
         return job
 
     def host_part(job):
+        """grouping (host GAEC) and the finishing queued on the side stream (not waited for)"""
         t0 = time.perf_counter()
         per_image = job.result()
         t0 = clock("grouping_host", t0)
-        fin = ppose.finish_batch(per_image, maps, tag_maps, adjustment=True, with_refine=True, stream=side)
-        t0 = clock("finish_refine_adjust", t0)
-        res = [None if p is None else ppose.reverse_affine_map(p.copy(), (W, H), W, "short_with_resize") for p in fin]
+        fin = ppose.finish_batch_start(per_image, maps, tag_maps, adjustment=True, with_refine=True, stream=side)
+        clock("finish_queue", t0)
+        return fin
+
+    def collect(fin):
+        t0 = time.perf_counter()
+        done = fin.result()
+        t0 = clock("finish_wait", t0)
+        res = [None if p is None else ppose.reverse_affine_map(p.copy(), (W, H), W, "short_with_resize") for p in done]
         clock("reverse_affine_map", t0)
-        return res
+        return sum(0 if r is None else len(r) for r in res)
 
     def run(n, pipelined):
         persons = 0
         if pipelined:
-            pend = gpu_part()
+            # three batches in flight: batch k+1's GPU part is queued, then batch k's grouping runs on the host and
+            # its finishing is queued on the side stream, then batch k-1's finished keypoints are collected
+            pend, fin_prev = gpu_part(), None
             for _ in range(n - 1):
                 nxt = gpu_part()
-                persons += sum(0 if r is None else len(r) for r in host_part(pend))
-                pend = nxt
-            persons += sum(0 if r is None else len(r) for r in host_part(pend))
+                fin = host_part(pend)
+                if fin_prev is not None:
+                    persons += collect(fin_prev)
+                pend, fin_prev = nxt, fin
+            fin = host_part(pend)
+            if fin_prev is not None:
+                persons += collect(fin_prev)
+            persons += collect(fin)
         else:
             for _ in range(n):
-                persons += sum(0 if r is None else len(r) for r in host_part(gpu_part()))
+                persons += collect(host_part(gpu_part()))
         return persons
 
     rec = {}

@@ -360,8 +360,33 @@ def finish_persons(persons, scoremaps, tags, adjustment, with_refine, with_filte
     return persons
 
 
+class FinishJob:
+    """A batch's finishing queued on the GPU (finish_batch_start): ``result()`` waits for its one read-back (an
+    event) and returns the per-image keypoint arrays, as finish_batch does."""
+
+    def __init__(self, out, fill=None):
+        self._out, self._fill = out, fill
+
+    def result(self):
+        if self._fill is not None:
+            ev, back, live, starts = self._fill
+            ev.synchronize()
+            res = back.numpy()
+            for k, b in enumerate(live):
+                self._out[b][...] = res[starts[k]:starts[k + 1]]
+            self._fill = None
+        return self._out
+
+
 def finish_batch(per_image, scoremaps, tags, adjustment=True, with_refine=False, with_filter=False,
                  fill_mean_=True, stream=None):
+    """finish_persons over a batch; see finish_batch_start (this waits for the result)."""
+    return finish_batch_start(per_image, scoremaps, tags, adjustment, with_refine, with_filter, fill_mean_,
+                              stream).result()
+
+
+def finish_batch_start(per_image, scoremaps, tags, adjustment=True, with_refine=False, with_filter=False,
+                       fill_mean_=True, stream=None):
     """finish_persons over a batch (``pred_to_ann``, ``Utils.py:1460-1478``, once per image): per_image as
     group_persons returns it, scoremaps [B, J, H, W] / tags [B, J, H, W(, F)] device tensors. The filter and
     fill_mean run on the host; then every image's keypoints go up in one pinned copy, the refine and adjust
@@ -385,7 +410,7 @@ def finish_batch(per_image, scoremaps, tags, adjustment=True, with_refine=False,
     live = [b for b, kp in enumerate(out) if kp is not None and kp.shape[0] > 0]
     do_ref = [with_refine and out[b][0, :, 2].sum() != 0 for b in live]
     if not live or not (adjustment or any(do_ref)):
-        return out
+        return FinishJob(out)
     L = _lib.lib()
     dev = scoremaps.device
     st = stream if stream is not None else torch.cuda.current_stream(dev)
@@ -424,11 +449,7 @@ def finish_batch(per_image, scoremaps, tags, adjustment=True, with_refine=False,
         back.copy_(kp, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(st)
-    ev.synchronize()
-    res = back.numpy()
-    for k, b in enumerate(live):
-        out[b][...] = res[starts[k]:starts[k + 1]]
-    return out
+    return FinishJob(out, (ev, back, live, starts))
 
 
 # ----------------------------------------------------------------------------------------------------
