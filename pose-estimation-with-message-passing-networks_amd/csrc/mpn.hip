@@ -1021,22 +1021,118 @@ __device__ __forceinline__ void layer_fixed(const float* smz, const EmbedLayout&
   }
 }
 
+// f16x3 split of the first KB k-blocks (32 features each) of a fragment: split_f16 over 16 KB values per lane instead
+// of 32 (the k-blocks past KB hold the zero padding of a narrower layer input and are not read)
+template <int KB, bool NONNEG>
+__device__ __forceinline__ bool split_f16_kb(const float (&x)[4][4], float s, f16x8_t (&hi)[2], f16x8_t (&lo)[2],
+                                             float& sc) {
+  float m;
+  if constexpr (NONNEG) {
+    int mi = 0;
+#pragma unroll
+    for (int b = 0; b < 2 * KB; ++b)
+      mi = max(mi, max(max(__float_as_int(x[b][0]), __float_as_int(x[b][1])), max(__float_as_int(x[b][2]), __float_as_int(x[b][3]))));
+    m = __int_as_float(mi);
+  } else {
+    m = 0.0f;
+#pragma unroll
+    for (int b = 0; b < 2 * KB; ++b)
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(x[b][0]), fabsf(x[b][1])), fmaxf(fabsf(x[b][2]), fabsf(x[b][3]))));
+  }
+  const bool big = __any(!(m * s < F16_BIG));
+  sc = big ? f16_item_scale(m, s) : 1.0f;
+  const float ss = s * sc;
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    uint32_t h[4], l[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      split_pair(x[2 * kb + (d >> 1)][2 * (d & 1)], x[2 * kb + (d >> 1)][2 * (d & 1) + 1], ss, h[d], l[d]);
+    const u32x4_t hv = {h[0], h[1], h[2], h[3]}, lv = {l[0], l[1], l[2], l[3]};
+    hi[kb] = __builtin_bit_cast(f16x8_t, hv);
+    lo[kb] = __builtin_bit_cast(f16x8_t, lv);
+  }
+  return big;
+}
+
+// One layer of the fixed embedding in the f16x3 domain: input x 2^11 (IN_DOM; the first layer's edge_attr is true),
+// output x 2^11, the biases staged x 2^11 in LDS (edge_embed_kernel FIXED) -- so no per-value scaling on the way in
+// or out, only where an item's range factor applies (BIG, a uniform branch to a second body). The values are
+// bitwise 2^11 times those of layer_fixed (power-of-two scalings are exact). ReLU and the sign of the input are
+// compile-time (NONNEG: the input is a ReLU output, so its range max is one integer max3 chain).
+template <int KB32, int OB, bool RELU, bool NONNEG, bool BIG>
+__device__ __forceinline__ void layer_h3_body(const _Float16* W, int ldw, const float* bias, const f16x8_t (&hh)[2],
+                                              const f16x8_t (&lh)[2], float sc, float (&out)[4][4]) {
+  const int lane = __lane_id(), i = lane & 15, g = lane >> 4;
+  constexpr int lo_off = 32 * KB32;
+  const float isc = BIG ? 1.0f / sc : 1.0f;
+#pragma unroll
+  for (int ob = 0; ob < 4; ++ob) {
+    if (ob < OB) {
+      const float4 bb = ld4(bias + 16 * ob + 4 * g);
+      f32x4 c = {bb.x, bb.y, bb.z, bb.w};
+      if (BIG) c *= sc;
+#pragma unroll
+      for (int kb = 0; kb < KB32; ++kb) {
+        const int o = (16 * ob + i) * ldw + 32 * kb + 8 * g;
+        const f16x8_t ah = *reinterpret_cast<const f16x8_t*>(W + o);
+        const f16x8_t al = *reinterpret_cast<const f16x8_t*>(W + o + lo_off);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, hh[kb], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, lh[kb], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, hh[kb], c, 0, 0, 0);
+      }
+      if (BIG) c *= isc;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[ob][r] = RELU ? fmaxf(c[r], 0.0f) : c[r];
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[ob][r] = 0.0f;
+    }
+  }
+}
+
+template <int KB32, int OB, bool RELU, bool NONNEG, bool IN_DOM>
+__device__ __forceinline__ void layer_h3(const float* smz, const EmbedLayout& Lo, int l, const float (&in)[4][4],
+                                         float (&out)[4][4], Frag<2>* split_out = nullptr) {
+  const _Float16* W = reinterpret_cast<const _Float16*>(smz + Lo.w_off[l]);
+  const float* bias = smz + Lo.b_off[l];
+  f16x8_t hh[2], lh[2];
+  float sc;
+  const bool big = split_f16_kb<KB32, NONNEG>(in, IN_DOM ? dom_inv<2>() : 1.0f, hh, lh, sc);
+  if (split_out) {
+    split_out->hh[0] = hh[0]; split_out->hh[1] = hh[1];
+    split_out->hl[0] = lh[0]; split_out->hl[1] = lh[1];
+    split_out->big = big;
+    split_out->sc = sc;
+  }
+  if (__builtin_expect(big, 0)) layer_h3_body<KB32, OB, RELU, NONNEG, true>(W, Lo.stride[l], bias, hh, lh, sc, out);
+  else layer_h3_body<KB32, OB, RELU, NONNEG, false>(W, Lo.stride[l], bias, hh, lh, 1.0f, out);
+}
+
 template <int PREC>
 __device__ __forceinline__ void embed_tile_fixed(const float* smz, const EmbedLayout& Lo, float (&x)[4][4],
                                                  float (&y)[4][4], Frag<PREC>& fx) {
-  layer_fixed<PREC, 1, 2>(smz, Lo, 0, x, y);   // A -> 32
-  layer_fixed<PREC, 1, 4>(smz, Lo, 1, y, x);   // 32 -> 64
-  layer_fixed<PREC, 2, 4>(smz, Lo, 2, x, y);   // 64 -> 64
-  layer_fixed<PREC, 2, 4>(smz, Lo, 3, y, x);   // 64 -> 64  (e_init in x)
-  layer_fixed<PREC, 2, 4, true>(smz, Lo, 4, x, y, &fx);   // Q0 = W1_e_init e_init + b1 (domain), e_init's split
+  if constexpr (PREC == 2) {   // every activation in the 2^11 domain (edge_attr in: true values)
+    layer_h3<1, 2, true, false, false>(smz, Lo, 0, x, y);   // A -> 32
+    layer_h3<1, 4, true, true, true>(smz, Lo, 1, y, x);     // 32 -> 64
+    layer_h3<2, 4, true, true, true>(smz, Lo, 2, x, y);     // 64 -> 64
+    layer_h3<2, 4, false, true, true>(smz, Lo, 3, y, x);    // 64 -> 64  (e_init in x)
+    layer_h3<2, 4, false, false, true>(smz, Lo, 4, x, y, &fx);   // Q0 = W1_e_init e_init + b1, e_init's split
+  } else {
+    layer_fixed<PREC, 1, 2>(smz, Lo, 0, x, y);   // A -> 32
+    layer_fixed<PREC, 1, 4>(smz, Lo, 1, y, x);   // 32 -> 64
+    layer_fixed<PREC, 2, 4>(smz, Lo, 2, x, y);   // 64 -> 64
+    layer_fixed<PREC, 2, 4>(smz, Lo, 3, y, x);   // 64 -> 64  (e_init in x)
+    layer_fixed<PREC, 2, 4, true>(smz, Lo, 4, x, y, &fx);   // Q0 = W1_e_init e_init + b1 (domain), e_init's split
+  }
 }
 
-// the layout embed_tile_fixed assumes
+// the layout embed_tile_fixed assumes (ReLU after the first three embedding layers, none after the last and Q0)
 static bool embed_fixed_shape(const EmbedLayout& L) {
-  static const int kb[5] = {1, 1, 2, 2, 2}, ob[5] = {2, 4, 4, 4, 4};
+  static const int kb[5] = {1, 1, 2, 2, 2}, ob[5] = {2, 4, 4, 4, 4}, relu[5] = {1, 1, 1, 0, 0};
   if (L.prec == PEMP_PREC_FP32 || L.n != 4) return false;
   for (int l = 0; l < 5; ++l)
-    if (L.kb[l] != kb[l] || L.ob[l] != ob[l]) return false;
+    if (L.kb[l] != kb[l] || L.ob[l] != ob[l] || (L.relu[l] != 0) != (relu[l] != 0)) return false;
   return true;
 }
 
@@ -1097,7 +1193,9 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp em
             *reinterpret_cast<const uint4*>(src + row * ip + c8);
       }
     }
-    for (int idx = threadIdx.x; idx < rows; idx += 64 * EDGE_WAVES) sm[Lo.b_off[l] + idx] = bsrc[idx];
+    // (the fixed f16x3 layers keep every activation in the 2^11 domain: their biases are staged scaled, exactly)
+    const float bscale = (FIXED && PREC == 2) ? dom<2>() : 1.0f;
+    for (int idx = threadIdx.x; idx < rows; idx += 64 * EDGE_WAVES) sm[Lo.b_off[l] + idx] = bsrc[idx] * bscale;
   }
   __syncthreads();
   const int64_t gw = (int64_t)blockIdx.x * EDGE_WAVES + wave, nw = (int64_t)gridDim.x * EDGE_WAVES;
