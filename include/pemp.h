@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define PEMP_ABI_VERSION 17
+#define PEMP_ABI_VERSION 18
 
 enum {
   PEMP_OK = 0,
@@ -321,6 +321,27 @@ size_t pemp_pose_refine_workspace_size(int P, int J, int H, int W, int F);
 int pemp_pose_refine(const float* scoremaps, const float* tag, int J, int H, int W, int F, double* keypoints, int P,
                      void* workspace, size_t workspace_bytes, void* stream);
 int pemp_pose_adjust(const float* det, int J, int H, int W, double* keypoints, int P, void* stream);
+
+/* Batched finishing (finish_batch, the per-image loop of valid.py:101-123 over pred_to_ann's refine / adjust):
+ * every image's persons in one keypoints array [P][J][3] f64, person p of image pimg[p].
+ * pemp_pose_finish_plan (HOST): from counts[B] persons per image and ref[B] (refine image b or not) fills
+ *   pimg[P] and chunks[3 * n] (first person, persons, image; chunks of the refined images only, never across
+ *   two images), out2 = {n, persons-per-chunk width}; at most max_chunks (P suffices).
+ * pemp_pose_finish_batch (GPU, in place): refine (as pemp_pose_refine) for the persons of the images with
+ *   ref[b] != 0, then adjust (adjust != 0) for all, scoremaps [B][J][H][W], tags [B][J][H][W][F] (NULL when
+ *   no image is refined); pimg / chunks / ref in device memory. Workspace:
+ *   pemp_pose_refine_workspace_size(P, J, H, W, F). Same keypoints as the per-image calls. */
+/* pemp_pack_to_host (GPU + copy): the n <= 16 device regions src[i] (bytes[i] bytes each) gathered into the device
+ * buffer staging at offsets off[i] (multiples of 16, off[i] + bytes[i] <= total), then one stream-ordered copy of
+ * staging[0, total) to host_dst (pinned host memory): the grouping's read-back in one copy instead of one per
+ * array. */
+int pemp_pack_to_host(int n, const void* const* src, const size_t* bytes, const size_t* off, size_t total,
+                      void* staging, void* host_dst, void* stream);
+int pemp_pose_finish_plan(int B, const int32_t* counts, const uint8_t* ref, int32_t* pimg, int32_t* chunks,
+                          int max_chunks, int32_t* out2);
+int pemp_pose_finish_batch(const float* scoremaps, const float* tags, int B, int J, int H, int W, int F,
+                           double* keypoints, int P, const int32_t* pimg, const int32_t* chunks, int n_chunks, int pc,
+                           const uint8_t* ref, int adjust, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Message-passing network, inference (eval-mode BatchNorm folded into the next Linear by the

@@ -9,7 +9,7 @@ import os
 
 LIB_PATH = os.environ.get("PEMP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc",
                                                      "libpemp.so")
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 ERR_INVALID_ARG, ERR_HIP, ERR_WORKSPACE, ERR_UNSUPPORTED = -1, -2, -3, -4
 
@@ -114,6 +114,10 @@ SIGNATURES = {
     "pemp_pose_refine_workspace_size": (c_sz, [c_i32, c_i32, c_i32, c_i32, c_i32]),
     "pemp_pose_refine": (c_i32, [c_p, c_p, c_i32, c_i32, c_i32, c_i32, c_p, c_i32, c_p, c_sz, c_p]),
     "pemp_pose_adjust": (c_i32, [c_p, c_i32, c_i32, c_i32, c_p, c_i32, c_p]),
+    "pemp_pack_to_host": (c_i32, [c_i32, c_p, c_p, c_p, c_sz, c_p, c_p, c_p]),
+    "pemp_pose_finish_plan": (c_i32, [c_i32, c_p, c_p, c_p, c_p, c_i32, c_p]),
+    "pemp_pose_finish_batch": (c_i32, [c_p, c_p, c_i32, c_i32, c_i32, c_i32, c_i32, c_p, c_i32, c_p, c_p, c_i32,
+                                       c_i32, c_p, c_i32, c_p, c_sz, c_p]),
     "pemp_prof_enable": (c_i32, [ctypes.c_char_p]),
     "pemp_prof_report": (c_i32, [ctypes.c_char_p, c_sz]),
 }

@@ -724,10 +724,19 @@ __device__ float np_sum_f32(const float* v, int n, bool pairwise) {
 
 // prev_tag[p] = np.mean(tags at the detected joints of person p, axis=0) (float32). One wave per person:
 // lane j loads joint j's flag and tag values (all loads in flight together), lane 0 sums in numpy's order.
+// Batched form (pemp_pose_finish_batch): pimg[p] is person p's image, whose maps start at image * J H W (F) and
+// which is refined only where ref[image] != 0; pimg == nullptr: one image, refined.
 __global__ __launch_bounds__(64) void refine_mean_tag_kernel(const double* __restrict__ kp, int P, int J,
                                                              const float* __restrict__ tag, int H, int W, int F,
-                                                             float* __restrict__ mean_tag) {
+                                                             float* __restrict__ mean_tag,
+                                                             const int32_t* __restrict__ pimg,
+                                                             const uint8_t* __restrict__ ref) {
   const int p = blockIdx.x, j = threadIdx.x;
+  if (pimg) {
+    const int b = pimg[p];
+    if (!ref[b]) return;
+    tag += (size_t)b * J * H * W * F;
+  }
   bool det = false;
   float v0 = 0.f, v1 = 0.f;
   if (j < J) {
@@ -784,10 +793,17 @@ template <int PC, int F>
 __global__ __launch_bounds__(256) void refine_argmax_kernel(const float* __restrict__ s, const float* __restrict__ tag,
                                                             int H, int W, const float* __restrict__ mean_tag,
                                                             int P, unsigned long long* __restrict__ keys, int J,
-                                                            const double* __restrict__ kp) {
+                                                            const double* __restrict__ kp,
+                                                            const int32_t* __restrict__ chunks) {
   const int i = blockIdx.y;
-  const int p0 = blockIdx.z * PC;
-  const int np_ = min(PC, P - p0);
+  int p0 = blockIdx.z * PC, np_ = min(PC, P - p0);
+  if (chunks) {   // batched: chunk z = (first person, persons, image); a chunk never spans two images
+    const int b = chunks[3 * blockIdx.z + 2];
+    p0 = chunks[3 * blockIdx.z];
+    np_ = chunks[3 * blockIdx.z + 1];
+    s += (size_t)b * J * H * W;
+    tag += (size_t)b * J * H * W * F;
+  }
   bool need[PC];
   bool any = false;
 #pragma unroll
@@ -876,10 +892,17 @@ __global__ __launch_bounds__(256) void refine_argmax_kernel(const float* __restr
 // One wave per (person, joint): the lanes reduce the per-block partial keys, lane 0 finishes.
 __global__ __launch_bounds__(64) void refine_finish_kernel(const float* __restrict__ s, int H, int W,
                                                            const unsigned long long* __restrict__ keys, int nblk,
-                                                           int P, int J, double* __restrict__ kp) {
+                                                           int P, int J, double* __restrict__ kp,
+                                                           const int32_t* __restrict__ pimg,
+                                                           const uint8_t* __restrict__ ref) {
   const int t = blockIdx.x;
   const int i = t % J, p = t / J;
   if (kp[(size_t)t * 3 + 2] != 0.0) return;   // a detected joint: nothing searched, nothing changes
+  if (pimg) {
+    const int b = pimg[p];
+    if (!ref[b]) return;                         // an image that is not refined
+    s += (size_t)b * J * H * W;
+  }
   unsigned long long key = 0ull;
   for (int b = threadIdx.x; b < nblk; b += 64) {
     const unsigned long long k = keys[((size_t)i * nblk + b) * P + p];
@@ -907,12 +930,14 @@ __global__ __launch_bounds__(64) void refine_finish_kernel(const float* __restri
 
 // adjust (Utils.py:917-936): for joints with score > 0, quarter-pixel shift toward the larger neighbour of
 // det[joint_id] (indexed [int(kp[1]), int(kp[0])]), then + 0.5.
-__global__ void adjust_kernel(const float* __restrict__ det, int H, int W, int P, int J, double* __restrict__ kp) {
+__global__ void adjust_kernel(const float* __restrict__ det, int H, int W, int P, int J, double* __restrict__ kp,
+                              const int32_t* __restrict__ pimg) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= P * J) return;
   double* q = kp + (size_t)t * 3;
   if (!(q[2] > 0.0)) return;
   const int j = t % J;
+  if (pimg) det += (size_t)pimg[t / J] * J * H * W;
   double y = q[0], x = q[1];
   const int xx = (int)x, yy = (int)y;
   if (xx < 0 || xx >= H || yy < 0 || yy >= W) return;   // rejected by the host wrapper; kept from faulting
@@ -934,6 +959,53 @@ extern "C" size_t pemp_pose_refine_workspace_size(int P, int J, int H, int W, in
   return align_up((size_t)P * F * sizeof(float), 256) + (size_t)J * refine_blocks(J, H, W) * P * 8;
 }
 
+// persons per argmax thread: the smallest instantiated width covering an even split of P into <= 16-wide chunks
+static int refine_pc(int P) {
+  const int chunks = (P + 15) / 16, per = (P + chunks - 1) / chunks;
+  return per <= 2 ? 2 : per <= 4 ? 4 : per <= 6 ? 6 : per <= 8 ? 8 : per <= 10 ? 10 : per <= 12 ? 12 : 16;
+}
+
+// The three refine launches (mean tags, per-block argmax keys, finish) over P persons; pimg / chunks / ref null:
+// one image, n_chunks = ceil(P / pc) chunks of pc persons; else the batched plan of pemp_pose_finish_plan.
+static int refine_launch(const float* scoremaps, const float* tag, int J, int H, int W, int F, double* keypoints,
+                         int P, const int32_t* pimg, const int32_t* chunks, int n_chunks, int pc, const uint8_t* ref,
+                         void* workspace, hipStream_t st) {
+  float* mean_tag = reinterpret_cast<float*>(workspace);
+  unsigned long long* keys =
+      reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(workspace) + align_up((size_t)P * F * 4, 256));
+  ProfScope prof("pose_refine", st);
+  hipLaunchKernelGGL(refine_mean_tag_kernel, dim3(P), dim3(64), 0, st, keypoints, P, J, tag, H, W, F,
+                     mean_tag, pimg, ref);
+  PEMP_LAUNCH_CHECK();
+  const int bx = refine_blocks(J, H, W);
+  const dim3 grid(bx, J, n_chunks);
+#define PEMP_REFINE_LAUNCH(N)                                                                                   \
+  case N:                                                                                                       \
+    if (F == 1)                                                                                                 \
+      hipLaunchKernelGGL((refine_argmax_kernel<N, 1>), grid, dim3(256), 0, st, scoremaps, tag, H, W, mean_tag, P,  \
+                         keys, J, keypoints, chunks);                                                           \
+    else                                                                                                        \
+      hipLaunchKernelGGL((refine_argmax_kernel<N, 2>), grid, dim3(256), 0, st, scoremaps, tag, H, W, mean_tag, P,  \
+                         keys, J, keypoints, chunks);                                                           \
+    break;
+  switch (pc) {
+    PEMP_REFINE_LAUNCH(2)
+    PEMP_REFINE_LAUNCH(4)
+    PEMP_REFINE_LAUNCH(6)
+    PEMP_REFINE_LAUNCH(8)
+    PEMP_REFINE_LAUNCH(10)
+    PEMP_REFINE_LAUNCH(12)
+    PEMP_REFINE_LAUNCH(16)
+    default: set_error("pose refine: persons per chunk %d not instantiated", pc); return PEMP_ERR_INVALID_ARG;
+  }
+#undef PEMP_REFINE_LAUNCH
+  PEMP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(refine_finish_kernel, dim3(P * J), dim3(64), 0, st, scoremaps, H, W, keys, bx, P, J, keypoints,
+                     pimg, ref);
+  PEMP_LAUNCH_CHECK();
+  return PEMP_OK;
+}
+
 extern "C" int pemp_pose_refine(const float* scoremaps, const float* tag, int J, int H, int W, int F, double* keypoints,
                                 int P, void* workspace, size_t workspace_bytes, void* stream) {
   PEMP_CHECK_ARG(J >= 1 && J <= 64 && H >= 1 && W >= 1 && (F == 1 || F == 2) && P >= 0,
@@ -944,41 +1016,124 @@ extern "C" int pemp_pose_refine(const float* scoremaps, const float* tag, int J,
   const size_t need = pemp_pose_refine_workspace_size(P, J, H, W, F);
   PEMP_CHECK_ARG(workspace && workspace_bytes >= need, "pemp_pose_refine: workspace %zu < %zu", workspace_bytes,
                  need);
-  float* mean_tag = reinterpret_cast<float*>(workspace);
-  unsigned long long* keys =
-      reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(workspace) + align_up((size_t)P * F * 4, 256));
-  hipStream_t st = as_stream(stream);
-  ProfScope prof("pose_refine", st);
-  hipLaunchKernelGGL(refine_mean_tag_kernel, dim3(P), dim3(64), 0, st, keypoints, P, J, tag, H, W, F,
-                     mean_tag);
-  PEMP_LAUNCH_CHECK();
-  const int bx = refine_blocks(J, H, W);
-  // persons per thread: the smallest instantiated width covering an even split of P into <= 16-wide chunks
-  const int chunks = (P + 15) / 16, per = (P + chunks - 1) / chunks;
-  const int pc = per <= 2 ? 2 : per <= 4 ? 4 : per <= 6 ? 6 : per <= 8 ? 8 : per <= 10 ? 10 : per <= 12 ? 12 : 16;
-  const dim3 grid(bx, J, (P + pc - 1) / pc);
-#define PEMP_REFINE_LAUNCH(N)                                                                                   \
-  case N:                                                                                                       \
-    if (F == 1)                                                                                                 \
-      hipLaunchKernelGGL((refine_argmax_kernel<N, 1>), grid, dim3(256), 0, st, scoremaps, tag, H, W, mean_tag, P,  \
-                         keys, J, keypoints);                                                                   \
-    else                                                                                                        \
-      hipLaunchKernelGGL((refine_argmax_kernel<N, 2>), grid, dim3(256), 0, st, scoremaps, tag, H, W, mean_tag, P,  \
-                         keys, J, keypoints);                                                                   \
-    break;
-  switch (pc) {
-    PEMP_REFINE_LAUNCH(2)
-    PEMP_REFINE_LAUNCH(4)
-    PEMP_REFINE_LAUNCH(6)
-    PEMP_REFINE_LAUNCH(8)
-    PEMP_REFINE_LAUNCH(10)
-    PEMP_REFINE_LAUNCH(12)
-    PEMP_REFINE_LAUNCH(16)
+  const int pc = refine_pc(P);
+  return refine_launch(scoremaps, tag, J, H, W, F, keypoints, P, nullptr, nullptr, (P + pc - 1) / pc, pc, nullptr,
+                       workspace, as_stream(stream));
+}
+
+extern "C" int pemp_pose_finish_plan(int B, const int32_t* counts, const uint8_t* ref, int32_t* pimg, int32_t* chunks,
+                                     int max_chunks, int32_t* out2) {
+  PEMP_CHECK_ARG(B >= 0 && (B == 0 || (counts && ref)) && out2, "pemp_pose_finish_plan: bad args");
+  int pmax = 0;
+  int64_t P = 0;
+  for (int b = 0; b < B; ++b) {
+    PEMP_CHECK_ARG(counts[b] >= 0, "pemp_pose_finish_plan: counts[%d] < 0", b);
+    if (ref[b]) pmax = std::max(pmax, (int)counts[b]);
+    P += counts[b];
   }
-#undef PEMP_REFINE_LAUNCH
-  PEMP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(refine_finish_kernel, dim3(P * J), dim3(64), 0, st, scoremaps, H, W, keys, bx, P, J, keypoints);
-  PEMP_LAUNCH_CHECK();
+  PEMP_CHECK_ARG(P == 0 || pimg, "pemp_pose_finish_plan: null pimg");
+  const int pc = refine_pc(std::max(pmax, 1));
+  int64_t p = 0;
+  int nc = 0;
+  for (int b = 0; b < B; ++b) {
+    for (int k = 0; k < counts[b]; ++k) pimg[p + k] = b;
+    if (ref[b])
+      for (int q = 0; q < counts[b]; q += pc) {
+        PEMP_CHECK_ARG(nc < max_chunks && chunks, "pemp_pose_finish_plan: more than %d chunks", max_chunks);
+        chunks[3 * nc] = (int32_t)(p + q);
+        chunks[3 * nc + 1] = std::min(pc, (int)counts[b] - q);
+        chunks[3 * nc + 2] = b;
+        ++nc;
+      }
+    p += counts[b];
+  }
+  out2[0] = nc;
+  out2[1] = pc;
+  return PEMP_OK;
+}
+
+extern "C" int pemp_pose_finish_batch(const float* scoremaps, const float* tags, int B, int J, int H, int W, int F,
+                                      double* keypoints, int P, const int32_t* pimg, const int32_t* chunks,
+                                      int n_chunks, int pc, const uint8_t* ref, int adjust, void* workspace,
+                                      size_t workspace_bytes, void* stream) {
+  PEMP_CHECK_ARG(B >= 1 && J >= 1 && J <= 64 && H >= 1 && W >= 1 && (F == 1 || F == 2) && P >= 0 && n_chunks >= 0,
+                 "pemp_pose_finish_batch: bad args (J <= 64, F in {1, 2})");
+  PEMP_CHECK_ARG((size_t)H * W < 0xFFFFFFFFull, "pemp_pose_finish_batch: map too large");
+  if (P == 0) return PEMP_OK;
+  PEMP_CHECK_ARG(scoremaps && keypoints && pimg && ref, "pemp_pose_finish_batch: null pointer");
+  hipStream_t st = as_stream(stream);
+  if (n_chunks > 0) {
+    PEMP_CHECK_ARG(tags && chunks, "pemp_pose_finish_batch: refine needs tags and chunks");
+    const size_t need = pemp_pose_refine_workspace_size(P, J, H, W, F);
+    PEMP_CHECK_ARG(workspace && workspace_bytes >= need, "pemp_pose_finish_batch: workspace %zu < %zu",
+                   workspace_bytes, need);
+    const int r = refine_launch(scoremaps, tags, J, H, W, F, keypoints, P, pimg, chunks, n_chunks, pc, ref,
+                                workspace, st);
+    if (r) return r;
+  }
+  if (adjust) {
+    hipLaunchKernelGGL(adjust_kernel, dim3((P * J + 255) / 256), dim3(256), 0, st, scoremaps, H, W, P, J, keypoints,
+                       pimg);
+    PEMP_LAUNCH_CHECK();
+  }
+  return PEMP_OK;
+}
+
+// ---- pemp_pack_to_host: several device regions gathered into one staging buffer, then one copy to the host ----
+namespace {
+constexpr int PACK_MAX = 16;
+struct PackArgs {
+  const uint8_t* src[PACK_MAX];
+  uint64_t bytes[PACK_MAX];
+  uint64_t off[PACK_MAX];
+  uint8_t* dst;
+};
+
+// blockIdx.y = region; 16-byte moves where the region's source, destination and size allow, else 4 / 1 bytes
+__global__ __launch_bounds__(256) void pack_kernel(PackArgs a) {
+  const int i = blockIdx.y;
+  const uint8_t* src = a.src[i];
+  uint8_t* dst = a.dst + a.off[i];
+  const uint64_t n = a.bytes[i];
+  const uint64_t t0 = (uint64_t)blockIdx.x * 256 + threadIdx.x, step = (uint64_t)gridDim.x * 256;
+  const uint64_t al = (reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) | n);
+  if ((al & 15) == 0) {
+    for (uint64_t k = t0; k < n / 16; k += step)
+      reinterpret_cast<uint4*>(dst)[k] = reinterpret_cast<const uint4*>(src)[k];
+  } else if ((al & 3) == 0) {
+    for (uint64_t k = t0; k < n / 4; k += step)
+      reinterpret_cast<uint32_t*>(dst)[k] = reinterpret_cast<const uint32_t*>(src)[k];
+  } else {
+    for (uint64_t k = t0; k < n; k += step) dst[k] = src[k];
+  }
+}
+}  // namespace
+
+extern "C" int pemp_pack_to_host(int n, const void* const* src, const size_t* bytes, const size_t* off, size_t total,
+                                 void* staging, void* host_dst, void* stream) {
+  PEMP_CHECK_ARG(n >= 0 && n <= PACK_MAX && (n == 0 || (src && bytes && off)), "pemp_pack_to_host: bad args (n <= %d)",
+                 PACK_MAX);
+  if (total == 0) return PEMP_OK;
+  PEMP_CHECK_ARG(staging && host_dst, "pemp_pack_to_host: null buffer");
+  PackArgs a{};
+  uint64_t most = 0;
+  for (int i = 0; i < n; ++i) {
+    PEMP_CHECK_ARG(off[i] % 16 == 0 && off[i] + bytes[i] <= total && (bytes[i] == 0 || src[i]),
+                   "pemp_pack_to_host: region %d (offset %zu, %zu bytes) outside [0, %zu) or unaligned", i, off[i],
+                   bytes[i], total);
+    a.src[i] = static_cast<const uint8_t*>(src[i]);
+    a.bytes[i] = bytes[i];
+    a.off[i] = off[i];
+    most = std::max<uint64_t>(most, bytes[i]);
+  }
+  a.dst = static_cast<uint8_t*>(staging);
+  hipStream_t st = as_stream(stream);
+  if (n > 0 && most > 0) {
+    const unsigned gx = (unsigned)std::min<uint64_t>((most / 16 + 255) / 256 + 1, 1024);
+    hipLaunchKernelGGL(pack_kernel, dim3(gx, n), dim3(256), 0, st, a);
+    PEMP_LAUNCH_CHECK();
+  }
+  PEMP_HIP(hipMemcpyAsync(host_dst, staging, total, hipMemcpyDeviceToHost, st));
   return PEMP_OK;
 }
 
@@ -987,7 +1142,7 @@ extern "C" int pemp_pose_adjust(const float* det, int J, int H, int W, double* k
   if (P == 0) return PEMP_OK;
   PEMP_CHECK_ARG(det && keypoints, "pemp_pose_adjust: null pointer");
   hipLaunchKernelGGL(adjust_kernel, dim3((P * J + 255) / 256), dim3(256), 0, as_stream(stream), det, H, W, P, J,
-                     keypoints);
+                     keypoints, nullptr);
   PEMP_LAUNCH_CHECK();
   return PEMP_OK;
 }

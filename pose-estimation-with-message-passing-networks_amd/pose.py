@@ -15,6 +15,7 @@ person assembly run in C++ in the same library, one image per host thread. No nu
 sits on the path. ``greedy`` (``Utils.py:517-626``) runs on the host after the same edge pass
 (``pemp_pose_greedy``). ``MUT`` and ``KL`` are not built (NotImplementedError).
 """
+import ctypes
 import functools
 import os
 
@@ -36,35 +37,78 @@ def _host_threads():
     return max(1, min(16, os.cpu_count() or 1))
 
 
+_NP = {torch.int64: np.int64, torch.int32: np.int32, torch.float32: np.float32, torch.float64: np.float64,
+       torch.bool: np.bool_, torch.uint8: np.uint8}
+
+
 def _to_host_async(tensors, dev):
-    """Stream-ordered copies of device tensors into pinned host tensors, queued on the current stream of `dev`
-    behind the work that produces them, plus an event recorded after them: the host buffers are valid once the
-    event has completed."""
-    out = []
+    """Stream-ordered read-back of device tensors (contiguous; None entries stay None) into one pinned host
+    buffer: one pemp_pack_to_host call gathers them into a device staging buffer and queues one copy, behind
+    the work that produces them on the current stream of `dev`, then an event is recorded. Returns numpy views
+    of the host buffer (valid once the event has completed), the event, and the buffer (keep it alive)."""
+    L = _lib.lib()
+    live = [t for t in tensors if t is not None]
+    if len(live) > 16:
+        raise ValueError("pemp_amd.pose: at most 16 arrays per read-back")
+    offs, total = [], 0
+    for t in live:
+        offs.append(total)
+        total += (t.numel() * t.element_size() + 15) // 16 * 16
     with torch.cuda.device(dev):
-        for t in tensors:
-            if t is None:
-                out.append(None)
-                continue
-            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
-            h.copy_(t, non_blocking=True)
-            out.append(h)
+        host = torch.empty(max(total, 16), dtype=torch.uint8, pin_memory=True)
+        staging = torch.empty(max(total, 16), dtype=torch.uint8, device=dev)
+        n = len(live)
+        src = (ctypes.c_void_p * max(n, 1))(*[t.data_ptr() for t in live])
+        nb = (ctypes.c_size_t * max(n, 1))(*[t.numel() * t.element_size() for t in live])
+        of = (ctypes.c_size_t * max(n, 1))(*offs)
+        _lib.check(L.pemp_pack_to_host(n, src, nb, of, total, staging.data_ptr(), host.data_ptr(), _lib.stream(dev)),
+                   L)
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(dev))
-    return out, ev
+    hv = host.numpy()
+    out, k = [], 0
+    for t in tensors:
+        if t is None:
+            out.append(None)
+            continue
+        nbytes = t.numel() * t.element_size()
+        out.append(hv[offs[k]:offs[k] + nbytes].view(_NP[t.dtype]).reshape(tuple(t.shape)))
+        k += 1
+    return out, ev, host
+
+
+_WORKER = None
+
+
+def _worker():
+    """The library's grouping thread (one, so jobs finish in submission order): it waits for a job's copies and
+    runs its host part while the caller's thread queues the next batch. The waits and the C++ calls release
+    the GIL (torch event wait, ctypes)."""
+    global _WORKER
+    if _WORKER is None:
+        import concurrent.futures
+        _WORKER = concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="pemp-grouping")
+    return _WORKER
 
 
 class GroupingJob:
     """The grouping of one batch, started on the GPU (group_persons_start / _start): the edge pass and the copies
-    of everything the host part reads are queued on the current stream, nothing waited for. ``result()`` waits for
-    the copies (an event, not a stream sync: work queued after the job keeps running) and runs the host part:
-    GAEC / threshold components and the person assembly (C++, one image per thread)."""
+    of everything the host part reads are queued on the current stream, nothing waited for. The host part
+    (GAEC / threshold components and the person assembly, C++, one image per thread) runs after the copies (an
+    event, not a stream sync: work queued after the job keeps running): on the library's grouping thread as soon
+    as they land (background=True), or in ``result()``. ``result()`` returns it (and raises its errors)."""
 
-    def __init__(self, state, finish):
-        self._state, self._finish, self._out = state, finish, None
+    def __init__(self, state, finish, background=False):
+        self._state, self._finish, self._out, self._fut = state, finish, None, None
+        if background:
+            self._fut = _worker().submit(finish, **state)
+            self._state = None
 
     def result(self):
-        if self._state is not None:
+        if self._fut is not None:
+            self._out = self._fut.result()
+            self._fut = None
+        elif self._state is not None:
             self._out = self._finish(**self._state)
             self._state = None
         return self._out
@@ -106,13 +150,17 @@ def _start(joint_det, joint_scores, edge_index, pred, node_off_d, B, th, use_th,
         t1 = time.perf_counter()
         timings["edge_pass"] = timings.get("edge_pass", 0.0) + t1 - t0
         t0 = t1
-    host, ev = _to_host_async([ei, w, flags, joint_det.to(torch.int64).contiguous(), sc, cls, ps, node_off_d]
-                              + list(extra), dev)
-    return dict(host=host, ev=ev, B=B, N=N, E=E, cc_method=cc_method, num_joints=num_joints,
+    host, ev, buf = _to_host_async([ei, w, flags, joint_det.to(torch.int64).contiguous(), sc, cls, ps, node_off_d]
+                                   + [None if t is None else t.contiguous() for t in extra], dev)
+    return dict(host=host, ev=ev, buf=buf, B=B, N=N, E=E, cc_method=cc_method, num_joints=num_joints,
                 allow_single=allow_single, timings=timings, t0=t0)
 
 
-def _finish(host, ev, B, N, E, cc_method, num_joints, allow_single, timings, t0):
+def _cp(a):
+    return None if a is None else a.ctypes.data
+
+
+def _finish(host, ev, buf, B, N, E, cc_method, num_joints, allow_single, timings, t0):
     """Host part of the shared path. Returns (persons list, mutants, labels, flags, node_off, extra host tensors)."""
     import time
     ev.synchronize()
@@ -124,7 +172,7 @@ def _finish(host, ev, B, N, E, cc_method, num_joints, allow_single, timings, t0)
     method = _method(cc_method)
     h_ei, h_w, h_flags, h_det, h_sc, h_cls, h_ps, h_off = host[:8]
     extra = host[8:]
-    node_off = h_off.numpy()
+    node_off = h_off
     if h_flags[B] & 4:
         raise ValueError("pemp_amd.pose: edge_index holds a node index outside [0, N)")
     if cc_method == "greedy":
@@ -134,17 +182,16 @@ def _finish(host, ev, B, N, E, cc_method, num_joints, allow_single, timings, t0)
         taken = np.empty(N, dtype=np.int32)
         persons = np.empty((cap, num_joints, 3), dtype=np.float64)
         counts = np.empty(B, dtype=np.int32)
-        _lib.check(L.pemp_pose_greedy(B, node_off.ctypes.data, h_ei.data_ptr(), E, h_w.data_ptr(), h_det.data_ptr(),
-                                      h_sc.data_ptr(), None if h_cls is None else h_cls.data_ptr(), num_joints,
-                                      taken.ctypes.data, cap, persons.ctypes.data, counts.ctypes.data), L)
+        _lib.check(L.pemp_pose_greedy(B, node_off.ctypes.data, _cp(h_ei), E, _cp(h_w), _cp(h_det), _cp(h_sc),
+                                      _cp(h_cls), num_joints, taken.ctypes.data, cap, persons.ctypes.data,
+                                      counts.ctypes.data), L)
         starts = np.concatenate([[0], np.cumsum(counts)])
         per_image = [persons[starts[b]:starts[b + 1]].copy() for b in range(B)]
-        return per_image, np.zeros(B, dtype=bool), taken, h_flags.numpy(), node_off, extra
+        return per_image, np.zeros(B, dtype=bool), taken, h_flags.copy(), node_off.copy(), extra
     labels = np.empty(N, dtype=np.int32)
     n_comp = np.empty(B, dtype=np.int32)
-    _lib.check(L.pemp_pose_cluster(B, node_off.ctypes.data, h_ei.data_ptr(), E, h_w.data_ptr(),
-                                   h_flags.data_ptr(), method, _host_threads(), labels.ctypes.data,
-                                   n_comp.ctypes.data), L)
+    _lib.check(L.pemp_pose_cluster(B, node_off.ctypes.data, _cp(h_ei), E, _cp(h_w), _cp(h_flags), method,
+                                   _host_threads(), labels.ctypes.data, n_comp.ctypes.data), L)
     if timings is not None:
         t1 = time.perf_counter()
         timings["cluster"] = timings.get("cluster", 0.0) + t1 - t0
@@ -154,14 +201,13 @@ def _finish(host, ev, B, N, E, cc_method, num_joints, allow_single, timings, t0)
     counts = np.empty(B, dtype=np.int32)
     mutants = np.empty(B, dtype=np.int32)
     _lib.check(L.pemp_pose_persons(B, node_off.ctypes.data, labels.ctypes.data, n_comp.ctypes.data,
-                                   h_det.data_ptr(), h_sc.data_ptr(), None if h_ps is None else h_ps.data_ptr(),
-                                   None if h_cls is None else h_cls.data_ptr(), num_joints, int(allow_single), cap,
+                                   _cp(h_det), _cp(h_sc), _cp(h_ps), _cp(h_cls), num_joints, int(allow_single), cap,
                                    persons.ctypes.data, counts.ctypes.data, mutants.ctypes.data), L)
     if timings is not None:
         timings["persons"] = timings.get("persons", 0.0) + time.perf_counter() - t0
     starts = np.concatenate([[0], np.cumsum(counts)])
     per_image = [persons[starts[b]:starts[b + 1]].copy() for b in range(B)]
-    return per_image, mutants.astype(bool), labels, h_flags.numpy(), node_off, extra
+    return per_image, mutants.astype(bool), labels, h_flags.copy(), node_off.copy(), extra
 
 
 def _run(joint_det, joint_scores, edge_index, pred, node_off, th, use_th, class_pred, cc_method, num_joints,
@@ -200,15 +246,17 @@ def group_persons(joint_det, joint_scores, edge_index, pred, th, class_pred=None
     per image: persons float64 [P, J, 3], or None where ``pred_to_ann`` returns None (no detector score >
     0.1, no edge surviving the node threshold, no person)."""
     return group_persons_start(joint_det, joint_scores, edge_index, pred, th, class_pred, cc_method, num_joints,
-                               batch_index, score_map_scores, num_images, _timings).result()
+                               batch_index, score_map_scores, num_images, _timings, background=False).result()
 
 
 def group_persons_start(joint_det, joint_scores, edge_index, pred, th, class_pred=None, cc_method="GAEC",
-                        num_joints=17, batch_index=None, score_map_scores=None, num_images=None, _timings=None):
+                        num_joints=17, batch_index=None, score_map_scores=None, num_images=None, _timings=None,
+                        background=True):
     """group_persons in two halves for pipelined callers: this queues the GPU part (edge pass, copies to pinned
-    host memory) on the current stream and returns at once; ``.result()`` of the returned job waits for the
-    copies only and runs the host part, so the GPU can run the next batch meanwhile. Same arguments and
-    result as group_persons."""
+    host memory) on the current stream and returns at once; the host part runs on the library's grouping thread
+    once the copies land (background=False: in ``.result()``), so the GPU runs the next batch and the caller
+    queues it meanwhile; ``.result()`` of the returned job returns the persons. Same arguments and result as
+    group_persons."""
     N = joint_det.shape[0]
     dev = edge_index.device
     if batch_index is None:
@@ -231,15 +279,14 @@ def group_persons_start(joint_det, joint_scores, edge_index, pred, th, class_pre
     def finish(**kw):
         per_image, _, _, flags, node_off, (h_bi, h_ok) = _finish(**kw)
         if h_bi is not None:
-            b_np = h_bi.numpy()
+            b_np = h_bi
             if len(b_np) and np.any(b_np[1:] < b_np[:-1]):
                 raise ValueError("pemp_amd.pose: batch_index must be non-decreasing (construct_graph order)")
             if len(b_np) and (b_np[0] < 0 or b_np[-1] >= B):
                 raise ValueError(f"pemp_amd.pose: batch_index outside [0, {B})")
         ok_det = None
         if h_ok is not None:
-            s = h_ok.numpy()
-            ok_det = np.array([s[node_off[b]:node_off[b + 1]].any() for b in range(B)])
+            ok_det = np.array([h_ok[node_off[b]:node_off[b + 1]].any() for b in range(B)])
         out = []
         for b, persons in enumerate(per_image):
             if (ok_det is not None and not ok_det[b]) or not (flags[b] & 2) or len(persons) == 0:
@@ -248,7 +295,7 @@ def group_persons_start(joint_det, joint_scores, edge_index, pred, th, class_pre
                 out.append(persons)
         return out
 
-    return GroupingJob(st, finish)
+    return GroupingJob(st, finish, background=background)
 
 
 # ----------------------------------------------------------------------------------------------------
@@ -388,11 +435,13 @@ def finish_batch(per_image, scoremaps, tags, adjustment=True, with_refine=False,
 def finish_batch_start(per_image, scoremaps, tags, adjustment=True, with_refine=False, with_filter=False,
                        fill_mean_=True, stream=None):
     """finish_persons over a batch (``pred_to_ann``, ``Utils.py:1460-1478``, once per image): per_image as
-    group_persons returns it, scoremaps [B, J, H, W] / tags [B, J, H, W(, F)] device tensors. The filter and
-    fill_mean run on the host; then every image's keypoints go up in one pinned copy, the refine and adjust
-    kernels of all images are queued on `stream` (default: the current stream; one refine workspace, reused in
-    stream order), and one copy back plus one event wait replace the two synchronisations per image of
-    finish_persons. Same results as finish_persons image by image."""
+    group_persons returns it, scoremaps [B, J, H, W] / tags [B, J, H, W(, F)] device tensors. The filter runs
+    per image on the host and fill_mean in one host call over every image's persons (both per person, as the
+    reference's per-image loop); then the keypoints and the batch plan (person -> image, refine chunks,
+    pemp_pose_finish_plan) go up in one pinned copy, one pemp_pose_finish_batch call queues the refine and
+    adjust kernels of all images on `stream` (default: the current stream), and one copy back plus one event
+    wait replace the two synchronisations per image of finish_persons. Same results as finish_persons image
+    by image; the arrays of per_image are updated in place, as finish_persons does."""
     out = [None if p is None else p for p in per_image]
     for b, persons in enumerate(out):
         if persons is None:
@@ -403,13 +452,22 @@ def finish_batch_start(per_image, scoremaps, tags, adjustment=True, with_refine=
             if persons.shape[0] == 0:
                 out[b] = None
                 continue
-        persons = np.ascontiguousarray(persons, dtype=np.float64)
-        if fill_mean_:
-            fill_mean(persons)
-        out[b] = persons
+        out[b] = np.ascontiguousarray(persons, dtype=np.float64)
     live = [b for b, kp in enumerate(out) if kp is not None and kp.shape[0] > 0]
-    do_ref = [with_refine and out[b][0, :, 2].sum() != 0 for b in live]
-    if not live or not (adjustment or any(do_ref)):
+    if not live:
+        return FinishJob(out)
+    starts = np.cumsum([0] + [out[b].shape[0] for b in live])
+    J0 = out[live[0]].shape[1]
+    for b in live:
+        if out[b].ndim != 3 or out[b].shape[1:] != (J0, 3):
+            raise ValueError(f"pemp_amd.pose: keypoints must be [P, {J0}, 3], got {out[b].shape}")
+    kp_all = np.concatenate([out[b] for b in live])
+    if fill_mean_:
+        fill_mean(kp_all)
+        for k, b in enumerate(live):
+            out[b][...] = kp_all[starts[k]:starts[k + 1]]
+    do_ref = np.array([with_refine and kp_all[starts[k], :, 2].sum() != 0 for k in range(len(live))], dtype=bool)
+    if not (adjustment or do_ref.any()):
         return FinishJob(out)
     L = _lib.lib()
     dev = scoremaps.device
@@ -418,35 +476,45 @@ def finish_batch_start(per_image, scoremaps, tags, adjustment=True, with_refine=
     B, J, H, W = d.shape
     if len(out) != B:
         raise ValueError(f"pemp_amd.pose: {len(out)} images of persons for {B} scoremaps")
+    if J0 != J:
+        raise ValueError(f"pemp_amd.pose: keypoints have {J0} joints, maps {J}")
     tg = None
-    if any(do_ref):
+    if do_ref.any():
         tg = _maps(tags, "tags", (4, 5))
         if tg.dim() == 4:
             tg = tg[..., None]
         if tuple(tg.shape[:4]) != (B, J, H, W):
             raise ValueError(f"pemp_amd.pose: tags {tuple(tg.shape)} do not match scoremaps {tuple(d.shape)}")
     F = tg.shape[4] if tg is not None else 1
-    for b in live:
-        if out[b].shape[1] != J:
-            raise ValueError(f"pemp_amd.pose: keypoints have {out[b].shape[1]} joints, maps {J}")
-        _check_coords(out[b], H, W, "refine" if with_refine else "adjust")
-    starts = np.cumsum([0] + [out[b].shape[0] for b in live])
-    host = torch.from_numpy(np.concatenate([out[b] for b in live])).pin_memory()
+    _check_coords(kp_all, H, W, "refine" if with_refine else "adjust")
+    P = int(starts[-1])
+    counts = np.zeros(B, dtype=np.int32)
+    ref = np.zeros(B, dtype=np.uint8)
+    counts[live] = np.diff(starts)
+    ref[live] = do_ref
+    # one pinned upload: keypoints | pimg [P] i32 | chunks [3P] i32 | ref [B] u8
+    o1 = kp_all.nbytes
+    o2 = o1 + 4 * P
+    o3 = o2 + 12 * P
+    host = torch.empty(o3 + B, dtype=torch.uint8, pin_memory=True)
+    hv = host.numpy()
+    hv[:o1] = kp_all.reshape(-1).view(np.uint8)
+    hv[o3:] = ref
+    plan = np.zeros(2, dtype=np.int32)
+    _lib.check(L.pemp_pose_finish_plan(B, counts.ctypes.data, ref.ctypes.data, hv[o1:].ctypes.data,
+                                       hv[o2:].ctypes.data, P, plan.ctypes.data), L)
     with torch.cuda.stream(st):
-        kp = host.to(dev, non_blocking=True)
-        if any(do_ref):
-            pmax = max(out[b].shape[0] for b, r in zip(live, do_ref) if r)
-            ws = torch.empty(L.pemp_pose_refine_workspace_size(pmax, J, H, W, F), dtype=torch.uint8, device=dev)
-        for k, b in enumerate(live):
-            P = int(starts[k + 1] - starts[k])
-            kp_b = kp[starts[k]:starts[k + 1]]
-            if do_ref[k]:
-                _lib.check(L.pemp_pose_refine(d[b].data_ptr(), tg[b].data_ptr(), J, H, W, F, kp_b.data_ptr(), P,
-                                              ws.data_ptr(), ws.numel(), _lib.stream(dev)))
-            if adjustment:
-                _lib.check(L.pemp_pose_adjust(d[b].data_ptr(), J, H, W, kp_b.data_ptr(), P, _lib.stream(dev)))
-        back = torch.empty(host.shape, dtype=torch.float64, pin_memory=True)
-        back.copy_(kp, non_blocking=True)
+        dbuf = host.to(dev, non_blocking=True)
+        base = dbuf.data_ptr()
+        ws = None
+        if plan[0] > 0:
+            ws = torch.empty(L.pemp_pose_refine_workspace_size(P, J, H, W, F), dtype=torch.uint8, device=dev)
+        _lib.check(L.pemp_pose_finish_batch(d.data_ptr(), tg.data_ptr() if tg is not None else None, B, J, H, W, F,
+                                            base, P, base + o1, base + o2, int(plan[0]), int(plan[1]), base + o3,
+                                            int(adjustment), ws.data_ptr() if ws is not None else None,
+                                            ws.numel() if ws is not None else 0, _lib.stream(dev)), L)
+        back = torch.empty(kp_all.shape, dtype=torch.float64, pin_memory=True)
+        back.copy_(dbuf[:o1].view(torch.float64).view(kp_all.shape), non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(st)
     return FinishJob(out, (ev, back, live, starts))

@@ -376,3 +376,42 @@ def test_group_persons_start_pipelined():
             assert (one is None) == (fin[b] is None)
             if one is not None:
                 np.testing.assert_array_equal(fin[b], one)
+
+
+@pytest.mark.parametrize("F", [1, 2])
+def test_finish_batch_mixed_images(F):
+    """finish_batch (one pemp_pose_finish_batch call: refine chunks per image, never across two; adjust for all)
+    equals finish_persons image by image on a batch mixing: no persons, more persons than one 16-wide chunk, an
+    image whose first person has no detected joint (adjusted, not refined), a single person; with and without
+    the max-score filter; the caller's arrays are updated in place as finish_persons updates them."""
+    rng = np.random.default_rng(7 + F)
+    B, J, H, W = 6, 17, 64, 80
+    hm = torch.from_numpy(rng.random((B, J, H, W), dtype=np.float32)).to(DEV)
+    tg = torch.from_numpy(rng.normal(0, 3, (B, J, H, W, F)).astype(np.float32)).to(DEV)
+    counts = [0, 37, 3, 2, 1, 9]
+
+    def persons(P):
+        kp = np.zeros((P, J, 3))
+        kp[:, :, 0] = rng.integers(0, W, (P, J))
+        kp[:, :, 1] = rng.integers(0, H, (P, J))
+        kp[:, :, 2] = np.where(rng.random((P, J)) < 0.6, rng.random((P, J)) * 0.9 + 0.05, 0.0)
+        kp[:, :, :2] *= kp[:, :, 2:3] > 0
+        return kp
+
+    for with_filter in (False, True):
+        per = [None if c == 0 else persons(c) for c in counts]
+        per[3][0, :, 2] = 0.0                         # no refine for image 3 (Utils.py:1472)
+        per[3][0, :, :2] = 0.0
+        ref = [None if p is None else p.copy() for p in per]
+        side = torch.cuda.Stream(DEV)
+        side.wait_stream(torch.cuda.current_stream(DEV))
+        fin = ppose.finish_batch(per, hm, tg if F == 2 else tg[..., 0], adjustment=True, with_refine=True,
+                                 with_filter=with_filter, stream=side)
+        for b in range(B):
+            one = ppose.finish_persons(ref[b], hm[b], tg[b] if F == 2 else tg[b, ..., 0], True, True,
+                                       with_filter=with_filter)
+            assert (one is None) == (fin[b] is None)
+            if one is not None:
+                np.testing.assert_array_equal(fin[b], one)
+                if not with_filter:
+                    np.testing.assert_array_equal(per[b], one)   # in place, as finish_persons

@@ -293,3 +293,30 @@ def test_reverse_affine_map_golden():
         np.testing.assert_array_equal(got, g[f"out_{c}"])
     with pytest.raises(NotImplementedError):
         ppose.reverse_affine_map(np.zeros((1, 17, 3)), (640, 480), 512, "short_mine")
+
+
+def test_finish_plan_chunks():
+    """pemp_pose_finish_plan (host): person -> image map, refine chunks of one image each, covering exactly the
+    persons of the refined images, all chunks pc wide but an image's last."""
+    from pemp_amd import _lib
+    L = _lib.load_cdll() if _lib._LIB is None else _lib._LIB
+    counts = np.array([0, 37, 3, 2, 1, 9, 16], dtype=np.int32)
+    ref = np.array([1, 1, 1, 0, 1, 1, 0], dtype=np.uint8)
+    P = int(counts.sum())
+    pimg = np.full(P, -1, dtype=np.int32)
+    chunks = np.full(3 * P, -1, dtype=np.int32)
+    out2 = np.zeros(2, dtype=np.int32)
+    assert L.pemp_pose_finish_plan(len(counts), counts.ctypes.data, ref.ctypes.data, pimg.ctypes.data,
+                                   chunks.ctypes.data, P, out2.ctypes.data) == 0
+    np.testing.assert_array_equal(pimg, np.repeat(np.arange(len(counts)), counts))
+    n, pc = int(out2[0]), int(out2[1])
+    assert pc in (2, 4, 6, 8, 10, 12, 16) and pc >= (37 + 2) // 3
+    c = chunks[:3 * n].reshape(n, 3)
+    starts = np.concatenate([[0], np.cumsum(counts)])
+    covered = np.zeros(P, dtype=int)
+    for p0, np_, b in c:
+        assert ref[b] and 1 <= np_ <= pc and starts[b] <= p0 and p0 + np_ <= starts[b + 1]
+        covered[p0:p0 + np_] += 1
+    np.testing.assert_array_equal(covered, np.repeat(ref.astype(int), counts))
+    assert L.pemp_pose_finish_plan(len(counts), counts.ctypes.data, ref.ctypes.data, pimg.ctypes.data,
+                                   chunks.ctypes.data, 3, out2.ctypes.data) != 0   # max_chunks too small
