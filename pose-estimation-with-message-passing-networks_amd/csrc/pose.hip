@@ -130,16 +130,23 @@ struct GaecEdge {
   bool operator<(const GaecEdge& o) const { return w < o.w; }
 };
 
+// One image's edges (image-local endpoints, weights) as pemp_pose_cluster buckets them.
+struct EdgeList {
+  const uint32_t* a;
+  const uint32_t* b;
+  const double* w;
+  size_t m;
+};
+
 // Greedy additive edge contraction over n vertices; root[v] = the cluster representative of v.
-void gaec(size_t n, const std::vector<size_t>& ea, const std::vector<size_t>& eb, const std::vector<double>& ew,
-          std::vector<size_t>& root) {
+void gaec(size_t n, const EdgeList& el, std::vector<size_t>& root) {
   std::vector<std::map<size_t, double>> adj(n);
   std::vector<std::map<size_t, size_t>> editions(n);
   std::priority_queue<GaecEdge> q;
-  for (size_t i = 0; i < ea.size(); ++i) {
-    adj[ea[i]][eb[i]] += ew[i];
-    adj[eb[i]][ea[i]] += ew[i];
-    GaecEdge e(ea[i], eb[i], ew[i]);
+  for (size_t i = 0; i < el.m; ++i) {
+    adj[el.a[i]][el.b[i]] += el.w[i];
+    adj[el.b[i]][el.a[i]] += el.w[i];
+    GaecEdge e(el.a[i], el.b[i], el.w[i]);
     e.edition = ++editions[e.a][e.b];
     q.push(e);
   }
@@ -201,8 +208,7 @@ struct GaecEdge16 {
   bool operator<(const GaecEdge16& o) const { return w < o.w; }
 };
 
-void gaec_dense(size_t n, const std::vector<size_t>& ea, const std::vector<size_t>& eb,
-                const std::vector<double>& ew, std::vector<size_t>& root) {
+void gaec_dense(size_t n, const EdgeList& el, std::vector<size_t>& root) {
   // per-thread buffers, reused across images and calls (fresh multi-100 KB blocks are mmap'ed, and their page
   // faults serialise threads that cluster in parallel)
   static thread_local std::vector<double> wt;
@@ -223,13 +229,13 @@ void gaec_dense(size_t n, const std::vector<size_t>& ea, const std::vector<size_
   };
   // the queue's vector reserved up front (initial edges + one push per neighbour per contraction bound)
   qstore.clear();
-  qstore.reserve(ea.size() + n * 8 + 64);
+  qstore.reserve(el.m + n * 8 + 64);
   std::priority_queue<GaecEdge16> q(std::less<GaecEdge16>(), std::move(qstore));
-  for (size_t i = 0; i < ea.size(); ++i) {
-    link(ea[i], eb[i]);
-    wt[ea[i] * n + eb[i]] += ew[i];
-    wt[eb[i] * n + ea[i]] += ew[i];
-    GaecEdge16 e(ea[i], eb[i], ew[i]);
+  for (size_t i = 0; i < el.m; ++i) {
+    link(el.a[i], el.b[i]);
+    wt[el.a[i] * n + el.b[i]] += el.w[i];
+    wt[el.b[i] * n + el.a[i]] += el.w[i];
+    GaecEdge16 e(el.a[i], el.b[i], el.w[i]);
     e.edition = ++ed[e.a * n + e.b];
     q.push(e);
   }
@@ -294,42 +300,47 @@ void gaec_dense(size_t n, const std::vector<size_t>& ea, const std::vector<size_
 // not), a heap of the entries with w >= 0, and at each contraction a check that the next top does not equal the
 // popped weight. On such a tie it returns false and the caller runs gaec_dense (the exact libstdc++ heap order).
 // C3 / C5 shapes: 20-40x fewer heap entries (the fully graph's edges between persons are negative).
-bool gaec_fast(size_t n, const std::vector<size_t>& ea, const std::vector<size_t>& eb, const std::vector<double>& ew,
-               std::vector<size_t>& root) {
-  // One 16-byte cell (weight, edition, existence) per unordered pair, at (min, max) of an n x n array whose upper
-  // triangle alone is used (and cleared): an update of a pair touches one cache line, the initial edges (sorted by
-  // (src, dst), src < dst) fill the rows in order. A merged vertex is only marked dead (its cells are never read
-  // again: scans skip dead vertices, a popped entry with a dead end is stale). Within one contraction every pair is
-  // updated once, so the order of the row scan does not change any weight (the same double additions).
-  struct Cell {
-    double w;
-    uint32_t ed, ex;
-  };
-  static thread_local std::vector<Cell> cell;
+bool gaec_fast(size_t n, const EdgeList& el, std::vector<size_t>& root) {
+  // Per unordered pair (a, b), a < b, at a * n + b of two n x n arrays whose upper triangle alone is used (and
+  // cleared): the weight (double) and the edition counter (uint32; 0 = no edge: every edge's first update counts
+  // one). Split arrays, so the triangle's working set (12 bytes per pair, 1.5 MB at n = 502) stays in a core's
+  // L2 through the row and column walks of the contractions. The initial edges (sorted by (src, dst), src < dst)
+  // fill the rows in order. A merged vertex is only marked dead (its pairs are never read again: the walks visit
+  // the alive vertices, a popped entry with a dead end is stale). Within one contraction every pair is updated
+  // once, so the order of the walk does not change any weight (the same double additions).
+  static thread_local std::vector<double> W;
+  static thread_local std::vector<uint32_t> ED;
   static thread_local std::vector<uint32_t> deg;
   static thread_local std::vector<uint8_t> alive;
+  static thread_local std::vector<uint32_t> live;   // the alive vertices, ascending
   static thread_local std::vector<GaecEdge16> qstore;
-  if (cell.size() < n * n) cell.resize(n * n);
-  for (size_t a = 0; a + 1 < n; ++a) std::fill(cell.begin() + a * n + a + 1, cell.begin() + (a + 1) * n, Cell{0.0, 0, 0});
+  if (W.size() < n * n) {
+    W.resize(n * n);
+    ED.resize(n * n);
+  }
+  for (size_t a = 0; a + 1 < n; ++a) {
+    std::fill(W.begin() + a * n + a + 1, W.begin() + (a + 1) * n, 0.0);
+    std::fill(ED.begin() + a * n + a + 1, ED.begin() + (a + 1) * n, 0u);
+  }
   deg.assign(n, 0);
   alive.assign(n, 1);
-  auto at = [&](size_t a, size_t b) -> Cell& { return a < b ? cell[a * n + b] : cell[b * n + a]; };
+  live.resize(n);
+  for (size_t v = 0; v < n; ++v) live[v] = (uint32_t)v;
+  auto ix = [n](size_t a, size_t b) { return a < b ? a * n + b : b * n + a; };
   qstore.clear();
   std::priority_queue<GaecEdge16> q(std::less<GaecEdge16>(), std::move(qstore));
   struct Drain : std::priority_queue<GaecEdge16> {
     static std::vector<GaecEdge16>& c_of(std::priority_queue<GaecEdge16>& pq) { return pq.*(&Drain::c); }
   };
-  for (size_t i = 0; i < ea.size(); ++i) {
-    const size_t a = ea[i], b = eb[i];
-    Cell& c = at(a, b);
-    if (!c.ex) {
-      c.ex = 1;
+  for (size_t i = 0; i < el.m; ++i) {
+    const size_t a = el.a[i], b = el.b[i], k = ix(a, b);
+    if (!ED[k]) {
       ++deg[a];
       ++deg[b];
     }
-    c.w += ew[i];
-    GaecEdge16 e(a, b, ew[i]);
-    e.edition = ++c.ed;
+    W[k] += el.w[i];
+    GaecEdge16 e(a, b, el.w[i]);
+    e.edition = ++ED[k];
     if (!(e.w < 0.0)) q.push(e);
   }
   std::vector<size_t> parent(n), rank(n, 0);
@@ -346,8 +357,8 @@ bool gaec_fast(size_t n, const std::vector<size_t>& ea, const std::vector<size_t
     const GaecEdge16 e = q.top();
     q.pop();
     if (!alive[e.a] || !alive[e.b]) continue;
-    const Cell& ce = cell[(size_t)e.a * n + e.b];
-    if (!ce.ex || e.edition < ce.ed) continue;
+    const size_t ke = (size_t)e.a * n + e.b;
+    if (!ED[ke] || e.edition < ED[ke]) continue;
     if (!q.empty() && q.top().w == e.w) {   // an equal weight: its pop order is the full heap's to decide
       exact = false;
       break;
@@ -362,25 +373,27 @@ bool gaec_fast(size_t n, const std::vector<size_t>& ea, const std::vector<size_t
         if (rank[rk] == rank[rm]) ++rank[rk];
       }
     }
-    for (size_t p = 0; p < n; ++p) {
-      if (p == merge || !alive[p]) continue;
-      const Cell& mp = at(merge, p);
-      if (!mp.ex) continue;
+    for (const uint32_t pv : live) {
+      const size_t p = pv;
+      if (p == merge) continue;
+      const size_t km = ix(merge, p);
+      if (!ED[km]) continue;
       --deg[p];                      // the edge (p, merge) goes with merge (p == keep included)
       if (p == keep) continue;
-      Cell& kp = at(keep, p);
-      if (!kp.ex) {
-        kp.ex = 1;
+      const size_t kk = ix(keep, p);
+      if (!ED[kk]) {
         ++deg[keep];
         ++deg[p];
       }
-      kp.w += mp.w;
-      GaecEdge16 ne(keep, p, kp.w);
-      ne.edition = ++kp.ed;
-      if (!(ne.w < 0.0)) q.push(ne);
+      const double nw = W[kk] + W[km];
+      W[kk] = nw;
+      GaecEdge16 ne(keep, p, nw);
+      ne.edition = ++ED[kk];
+      if (!(nw < 0.0)) q.push(ne);
     }
     alive[merge] = 0;
     deg[merge] = 0;
+    live.erase(std::lower_bound(live.begin(), live.end(), (uint32_t)merge));
   }
   qstore = std::move(Drain::c_of(q));
   if (!exact) return false;
@@ -544,14 +557,20 @@ extern "C" int pemp_pose_cluster(int B, const int64_t* node_off, const int64_t* 
     const size_t n = (size_t)n64;
     const int64_t lo = std::lower_bound(edge_index, edge_index + E, o) - edge_index;
     const int64_t hi = std::lower_bound(edge_index + lo, edge_index + E, o + n64) - edge_index;
-    static thread_local std::vector<size_t> ua, ub;
+    // image-local edges, written in place (sized for the whole run, then cut to the surviving count)
+    static thread_local std::vector<uint32_t> ua, ub;
     static thread_local std::vector<double> uw;
-    ua.clear();
-    ub.clear();
-    uw.clear();
-    ua.reserve((size_t)(hi - lo));
-    ub.reserve((size_t)(hi - lo));
-    uw.reserve((size_t)(hi - lo));
+    const size_t cap = (size_t)(hi - lo);
+    if (ua.size() < cap) {
+      ua.resize(cap);
+      ub.resize(cap);
+      uw.resize(cap);
+    }
+    size_t m = 0;
+    uint32_t* pa = ua.data();
+    uint32_t* pb = ub.data();
+    double* pw = uw.data();
+    const bool avg = (flags[img] & 1) != 0;
     for (int64_t e = lo; e < hi; ++e) {
       const float we = w[e];
       if (std::isnan(we)) continue;
@@ -563,27 +582,29 @@ extern "C" int pemp_pose_cluster(int B, const int64_t* node_off, const int64_t* 
       }
       double weight;
       if (method == 0) {
-        const float m = (flags[img] & 1) ? we * 0.5f : we;  // extract_edge_matrix: average, or M + M^T
-        weight = (double)(m - 0.5f);                            // cluster_andres_graph: edge_attr - 0.5 (fp32)
+        const float mm = avg ? we * 0.5f : we;   // extract_edge_matrix: average, or M + M^T
+        weight = (double)(mm - 0.5f);             // cluster_andres_graph: edge_attr - 0.5 (fp32)
       } else {
-        if (!(we > 0.8f)) continue;                             // pred_to_person "threshold": pred > 0.8
+        if (!(we > 0.8f)) continue;               // pred_to_person "threshold": pred > 0.8
         weight = 1.0;
       }
-      ua.push_back((size_t)(edge_index[e] - o));
-      ub.push_back((size_t)(d - o));
-      uw.push_back(weight);
+      pa[m] = (uint32_t)(edge_index[e] - o);
+      pb[m] = (uint32_t)(d - o);
+      pw[m] = weight;
+      ++m;
     }
+    const EdgeList el{pa, pb, pw, m};
     std::vector<size_t> root;
     if (method == 0) {
       if (n <= dense_max) {
-        if (exact_only || !gaec_fast(n, ua, ub, uw, root)) gaec_dense(n, ua, ub, uw, root);
+        if (exact_only || !gaec_fast(n, el, root)) gaec_dense(n, el, root);
       } else {
-        gaec(n, ua, ub, uw, root);
+        gaec(n, el, root);
       }
     } else {
       root.resize(n);
       for (size_t v = 0; v < n; ++v) root[v] = v;
-      for (size_t i = 0; i < ua.size(); ++i) union_join(root, ua[i], ub[i]);
+      for (size_t i = 0; i < m; ++i) union_join(root, pa[i], pb[i]);
       for (size_t v = 0; v < n; ++v) {
         size_t r = v;
         while (root[r] != r) r = root[r];
