@@ -190,11 +190,9 @@ class NaiveGraphConstructor:
 
     def _construct(self, L, st, sm, masks, B, J, H, W, use_thr, topk, thr, dev, ws, cap, det, dsc, n_det,
                    counts_h):
-        counts_h.fill(-1)
-        _lib.check(self._detect(L)(self._detect_src(sm), _lib.ptr(masks), B, J, H, W, self.pool_kernel_size, thr,
-                                   int(use_thr), topk, 3, _lib.ptr(ws), ws.numel(), _lib.ptr(det), _lib.ptr(dsc),
-                                   _lib.ptr(n_det), cap, counts_h.ctypes.data, st))
-        # host-side preparation of the graph stage, while the detection kernels run
+        # host-side preparation of the graph stage, before the first launch: with a capacity hint the detection,
+        # the graph build and the MPN are then queued back to back (no host gap between them on the GPU), and in a
+        # loop this preparation overlaps the previous batch's GPU work
         feats = self.features
         projected = isinstance(feats, ProjectedMaps)
         if projected:      # x sampled from the projected maps after the graph build (pemp_gather_projected)
@@ -236,9 +234,8 @@ class NaiveGraphConstructor:
             hint = NaiveGraphConstructor._graph_hint.get(gkey) if fully else None
         built = None
         pending = None
+        launch_mpn = None
         if hint is not None:
-            # capacity mode: the graph build is queued before the counts are read, so the GPU builds
-            # the graph while the host waits for them (pemp_fully_graph_build_cap)
             n_cap, e_cap = hint
             bufs = (torch.empty(n_cap, C, dtype=torch.float32, device=dev),
                     torch.empty(n_cap, 3, dtype=torch.int64, device=dev),
@@ -248,14 +245,24 @@ class NaiveGraphConstructor:
                     torch.empty(2 * e_cap, dtype=torch.int64, device=dev),
                     torch.empty(e_cap, A, dtype=torch.float32, device=dev),
                     torch.empty(B + 1, dtype=torch.int64, device=dev))          # node offsets (MPN fast path)
-            _lib.check(L.pemp_fully_graph_build_cap(
-                _lib.ptr(n_det), B, _lib.ptr(det), _lib.ptr(dsc), cap, _lib.ptr(feats), C, _lib.ptr(tags), F, J, H, W,
-                n_cap, e_cap, norm, mode, *[_lib.ptr(t) for t in bufs], st))
+            build_args = (_lib.ptr(n_det), B, _lib.ptr(det), _lib.ptr(dsc), cap, _lib.ptr(feats), C, _lib.ptr(tags), F,
+                          J, H, W, n_cap, e_cap, norm, mode, *[_lib.ptr(t) for t in bufs], st)
             mpn = NaiveGraphConstructor._bound_mpn
             if mpn is not None and not projected and J == getattr(mpn, "num_types", None):
                 pending_mpn = mpn
-                # the MPN behind the build, before the counts come back (capacity mode)
-                pending = mpn._forward_cap(bufs[0], bufs[6], bufs[1], n_cap, e_cap, n_det, cap, bufs[7], B)
+                launch_mpn = mpn._prepare_cap(bufs[0], bufs[6], bufs[1], n_cap, e_cap, n_det, cap, bufs[7], B)
+        detect = self._detect(L)
+        detect_args = (self._detect_src(sm), _lib.ptr(masks), B, J, H, W, self.pool_kernel_size, thr, int(use_thr), topk, 3,
+                       _lib.ptr(ws), ws.numel(), _lib.ptr(det), _lib.ptr(dsc), _lib.ptr(n_det), cap, counts_h.ctypes.data,
+                       st)
+        counts_h.fill(-1)
+        _lib.check(detect(*detect_args))
+        if hint is not None:
+            # capacity mode: the graph build (and the bound MPN) queued before the counts are read, so the GPU
+            # builds the graph while the host waits for them (pemp_fully_graph_build_cap)
+            _lib.check(L.pemp_fully_graph_build_cap(*build_args))
+            if launch_mpn is not None:
+                pending = launch_mpn()
             counts_l = self._wait_counts(counts_h, dev)
             built = bufs
         else:

@@ -357,6 +357,14 @@ class NodeClassificationMPNSimple(nn.Module):
         Returns the pending result (logit buffer + the key it was computed under) or None when this model / batch
         takes the exact forward (training, type summaries, unfused node MLPs, a detection capacity past the
         closed-form limit, over-size capacities)."""
+        launch = self._prepare_cap(x, edge_attr, joint_det, n_cap, e_cap, n_det, det_cap, node_off, B)
+        return None if launch is None else launch()
+
+    def _prepare_cap(self, x, edge_attr, joint_det, n_cap, e_cap, n_det, det_cap, node_off, B):
+        """_forward_cap in two halves: the host preparation (weights, descriptor, workspace, logit buffer) now,
+        and the returned launch() that queues the call and returns the pending result (or None); None when this
+        model / batch takes the exact forward. The graph constructor prepares before its first launch and calls
+        launch() right after the graph build's, so nothing but the call itself separates the two on the GPU."""
         if self.training or self.node_summary != "not" or _FULLY_OFF or x.device.type != "cuda":
             return None
         if e_cap > self._edge_limit or self.num_types * n_cap > self._node_rows_limit:
@@ -380,14 +388,19 @@ class NodeClassificationMPNSimple(nn.Module):
         a1 = (ne + 63) // 64 * 64
         a2 = a1 + (nn_ + 63) // 64 * 64
         buf = torch.empty(a2 + nn_ * self.num_joints, dtype=torch.float32, device=dev)
-        rc = L.pemp_mpn_forward_fully_cap(desc, fw.struct_ref, x.data_ptr(), edge_attr.data_ptr(),
-                                          node_types.data_ptr(), n_cap, e_cap, n_det.data_ptr(), det_cap,
-                                          node_off.data_ptr(), B, buf.data_ptr(), buf[a1:].data_ptr(),
-                                          buf[a2:].data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream(dev))
-        if rc == _lib.ERR_UNSUPPORTED:
-            return None           # the exact forward runs instead
-        _lib.check(rc)
-        return dict(buf=buf, a1=a1, a2=a2, n_rec=n_rec, key=(dev, self.precision, self._folded_key))
+        bp = buf.data_ptr()
+        args = (desc, fw.struct_ref, x.data_ptr(), edge_attr.data_ptr(), node_types.data_ptr(), n_cap, e_cap,
+                n_det.data_ptr(), det_cap, node_off.data_ptr(), B, bp, bp + 4 * a1, bp + 4 * a2, ws.data_ptr(),
+                ws.numel(), _lib.stream(dev))
+        result = dict(buf=buf, a1=a1, a2=a2, n_rec=n_rec, key=(dev, self.precision, self._folded_key))
+
+        def launch():
+            rc = L.pemp_mpn_forward_fully_cap(*args)
+            if rc == _lib.ERR_UNSUPPORTED:
+                return None           # the exact forward runs instead
+            _lib.check(rc)
+            return result
+        return launch
 
     def _attach_cap(self, pending, x, edge_attr, edge_index, joint_det, N, E):
         """Tag construct_graph's output with the queued result (the capacity batch fit: N, E are its counts)."""
