@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define PEMP_ABI_VERSION 18
+#define PEMP_ABI_VERSION 19
 
 enum {
   PEMP_OK = 0,
@@ -522,7 +522,9 @@ int pemp_mpn_prepare(const pemp_mpn_desc* desc, const int64_t* edge_index, const
 /* The edge passes' weight image (per type: the pass's 64x64 blocks in the kernels' LDS row layout, bias and
  * attention rows, the published edge head), built once per weight set and precision for `desc`
  * (precision, aggregation, num_types) into a caller buffer of pemp_mpn_edge_image_floats() floats;
- * pass it as pemp_mpn_weights.edge_img. No reference counterpart (replaces per-pass weight staging). */
+ * pass it as pemp_mpn_weights.edge_img. The edge embedding's LDS image (its layers, Q0's layer and W1_e_cur, in the
+ * embedding kernel's layout) follows the passes' image in the same buffer, so the embedding stages its weights
+ * with one LDS-DMA round. No reference counterpart (replaces per-pass weight staging). */
 size_t pemp_mpn_edge_image_floats(const pemp_mpn_desc* desc, const pemp_mpn_weights* w);
 int pemp_mpn_edge_image(const pemp_mpn_desc* desc, const pemp_mpn_weights* w, float* image, size_t floats,
                         void* stream);

@@ -9,7 +9,7 @@ import os
 
 LIB_PATH = os.environ.get("PEMP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc",
                                                      "libpemp.so")
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 ERR_INVALID_ARG, ERR_HIP, ERR_WORKSPACE, ERR_UNSUPPORTED = -1, -2, -3, -4
 

@@ -80,15 +80,30 @@ __device__ __forceinline__ float ef_value(int mode, int f, int J, float dx, floa
   return v;
 }
 
+// Granlund-Montgomery constants of an unsigned division by d >= 1 for dividends below 2^31:
+// q = (umulhi(n, m) + n) >> l (3 instructions instead of a 32-bit division's ~15, a 64-bit one's ~100)
+__host__ __device__ inline void graph_fastdiv_consts(unsigned d, uint32_t& m, int& l) {
+  l = 0;
+  while ((1ull << l) < d) ++l;
+  m = (uint32_t)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+}
+__device__ __forceinline__ int graph_fastdiv(int n, uint32_t m, int l) {
+  return (int)((__umulhi((unsigned)n, m) + (unsigned)n) >> l);
+}
+
 __global__ __launch_bounds__(256) void pack_nodes_kernel(
     const float* __restrict__ feat, int C, const float* __restrict__ tags, int F, int B, int J, int H, int W,
     const int64_t* __restrict__ det, const float* __restrict__ det_sc, int cap, const int64_t* __restrict__ node_off,
     int64_t n_total, float* __restrict__ x, int64_t* __restrict__ jdet, float* __restrict__ jsc,
     int64_t* __restrict__ bidx, float* __restrict__ jtag) {
   const int64_t total = n_total * C;
+  uint32_t mC;
+  int lC;
+  graph_fastdiv_consts((unsigned)C, mC, lC);
+  const bool small = total + (int64_t)gridDim.x * blockDim.x < ((int64_t)1 << 31);   // (uniform)
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t g = idx / C;
+    const int64_t g = small ? graph_fastdiv((int)idx, mC, lC) : idx / C;
     const int c = (int)(idx - g * C);
     const int b = find_segment(node_off, B, g);
     const int64_t i = g - node_off[b];
@@ -112,7 +127,15 @@ __global__ __launch_bounds__(256) void fully_graph_kernel(const int64_t* __restr
     const int b = find_segment(edge_off, B, e);
     const int64_t n = node_off[b + 1] - node_off[b];
     const int64_t el = e - edge_off[b];
-    const int64_t i = el / (n - 1), r = el - i * (n - 1);
+    int64_t i, r;
+    if (n <= 46340) {   // the image's n (n - 1) edges below 2^31: 32-bit division
+      const unsigned nm1 = (unsigned)(n - 1), iu = (unsigned)el / nm1;
+      i = iu;
+      r = (unsigned)el - iu * nm1;
+    } else {
+      i = el / (n - 1);
+      r = el - i * (n - 1);
+    }
     const int64_t j = r < i ? r : r + 1;
     ei[e] = node_off[b] + i;
     ei[e_total + e] = node_off[b] + j;
@@ -134,6 +157,9 @@ __global__ __launch_bounds__(256) void edge_features_kernel(const int64_t* __res
     if (e > E) return;
     E = e;
   }
+  uint32_t mA;
+  int lA;
+  graph_fastdiv_consts((unsigned)A, mA, lA);
   for (int64_t base = (int64_t)blockIdx.x * 256; base < E; base += (int64_t)gridDim.x * 256) {
     const int64_t e = base + threadIdx.x;
     if (e < E) {
@@ -150,7 +176,7 @@ __global__ __launch_bounds__(256) void edge_features_kernel(const int64_t* __res
     const int n = (int)min<int64_t>(256, E - base), total = n * A;
     float* o = out + base * A;
     for (int k = threadIdx.x; k < total; k += 256) {
-      const int el = k / A, f = k - el * A;
+      const int el = graph_fastdiv(k, mA, lA), f = k - el * A;
       o[k] = ef_value(mode, f, J, dx_s[el], dy_s[el], aux_s[el], ts_s[el], td_s[el]);
     }
     __syncthreads();
@@ -727,7 +753,10 @@ struct FusedGraphArgs {
   float *x, *jsc, *jtag, *edge_attr;
   int64_t *jdet, *bidx, *ei;
   int64_t* node_off_out;      // [B + 1] or NULL
+  uint32_t mC, mA;            // unsigned division by C and by A for dividends below 2^31 (graph_fastdiv)
+  int lC, lA;
 };
+
 
 // One launch for the whole fully-connected graph after the count read-back: every block derives
 // the per-image node / edge offsets from n_det in LDS; blocks [0, node_blocks) pack nodes
@@ -779,10 +808,11 @@ __global__ __launch_bounds__(256) void fused_fully_graph_kernel(FusedGraphArgs a
     return lo;
   };
   if ((int)blockIdx.x < a.node_blocks) {   // ---- nodes ----
-    const int64_t total = n_total * a.C;
-    for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)a.node_blocks * 256) {
-      const int64_t g = idx / a.C;
-      const int c = (int)(idx - g * a.C);
+    // (32-bit index arithmetic: the host takes this kernel only for n_total * C < 2^30)
+    const int total = (int)(n_total * a.C);
+    for (int idx = blockIdx.x * 256 + threadIdx.x; idx < total; idx += a.node_blocks * 256) {
+      const int g = graph_fastdiv(idx, a.mC, a.lC);
+      const int c = idx - g * a.C;
       const int b = seg(noff, g);
       const int64_t i = g - noff[b];
       const int64_t* d = a.det + ((size_t)b * a.cap + i) * 3;
@@ -805,7 +835,15 @@ __global__ __launch_bounds__(256) void fused_fully_graph_kernel(FusedGraphArgs a
       const int b = seg(eoff, e);
       const int64_t n = noff[b + 1] - noff[b];
       const int64_t el = e - eoff[b];
-      const int64_t i = el / (n - 1), r = el - i * (n - 1);
+      int64_t i, r;
+      if (n <= 46340) {   // the image's n (n - 1) edges below 2^31: 32-bit division (the 64-bit one is ~10x longer)
+        const unsigned nm1 = (unsigned)(n - 1), iu = (unsigned)el / nm1;
+        i = iu;
+        r = (unsigned)el - iu * nm1;
+      } else {
+        i = el / (n - 1);
+        r = el - i * (n - 1);
+      }
       const int64_t j = r < i ? r : r + 1;                 // all (i, j), i != j, sorted by (i, j)
       a.ei[e] = noff[b] + i;
       a.ei[e_total + e] = noff[b] + j;
@@ -829,7 +867,7 @@ __global__ __launch_bounds__(256) void fused_fully_graph_kernel(FusedGraphArgs a
     const int cnt = (int)min<int64_t>(256, e_total - base), total = cnt * a.A;
     float* o = a.edge_attr + base * a.A;
     for (int k = threadIdx.x; k < total; k += 256) {
-      const int el = k / a.A, f = k - el * a.A;
+      const int el = graph_fastdiv(k, a.mA, a.lA), f = k - el * a.A;
       o[k] = ef_value(a.mode, f, a.J, dx_s[el], dy_s[el], aux_s[el], ts_s[el], td_s[el]);
     }
     __syncthreads();
@@ -917,6 +955,11 @@ static int fully_graph_build(const int32_t* n_det, int B, const int64_t* det_xyt
   const int edge_blocks = e_total > 0 ? grid_for(e_total, 256, 8192) : 0;
   a.x = x; a.jsc = joint_scores; a.jtag = joint_tags; a.edge_attr = edge_attr;
   a.jdet = joint_det; a.bidx = batch_index; a.ei = edge_index; a.node_off_out = node_off_out;
+  // the kernel's 32-bit node index arithmetic (below 2^30 elements)
+  PEMP_CHECK_ARG(n_total * (int64_t)C < ((int64_t)1 << 30),
+                 "pemp_fully_graph_build: %lld nodes x %d features past the 32-bit range", (long long)n_total, C);
+  graph_fastdiv_consts((unsigned)C, a.mC, a.lC);
+  graph_fastdiv_consts((unsigned)A, a.mA, a.lA);
   ProfScope prof("graph_build", as_stream(stream));
   hipLaunchKernelGGL(fused_fully_graph_kernel, dim3(a.node_blocks + edge_blocks), dim3(256), 0, as_stream(stream), a);
   PEMP_LAUNCH_CHECK();

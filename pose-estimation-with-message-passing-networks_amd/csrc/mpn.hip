@@ -1154,10 +1154,73 @@ __device__ __forceinline__ void stage_tile64(float* dst, const float* w32, int64
   }
 }
 
+// The edge embedding's LDS image (every embedding layer, Q0's layer and W1_e_cur, biases x 2^11 for the fixed
+// f16x3 layers): written by threads tid, tid + nthreads, ... into dst, which is the kernel's LDS or, once per weight
+// set (pemp_mpn_edge_image, embed_image_kernel), a global buffer of embed_image_floats() floats that the kernel then
+// copies with one LDS-DMA round instead of these loops' dependent global-load rounds (one or two per layer).
+template <int PREC, bool FIXED>
+__device__ __forceinline__ void embed_stage(float* dst, int tid, int nthreads, const pemp_mlp& emb, const EmbedLayout& Lo,
+                                            const uint16_t* __restrict__ emb_bf, const float* __restrict__ q0_w,
+                                            const float* __restrict__ q0_b, const float* __restrict__ e1_w,
+                                            const uint16_t* __restrict__ e1_bf) {
+  // W1_e_cur after the embedding image (stage_tile64's layout)
+  float* d64 = dst + Lo.total;
+  if (PREC == 0) {
+    for (int idx = tid; idx < D * 16; idx += nthreads) {
+      const int row = idx >> 4, c4 = (idx & 15) * 4;
+      *reinterpret_cast<float4*>(&d64[row * LDW + c4]) = ld4(e1_w + row * D + c4);
+    }
+  } else {
+    __bf16* db = reinterpret_cast<__bf16*>(d64);
+    for (int idx = tid; idx < 2 * D * 8; idx += nthreads) {
+      const int row = idx >> 3, c8 = (idx & 7) * 8;
+      *reinterpret_cast<uint4*>(&db[interleaved_slot(row, D, 2 * LDW, D) + c8]) =
+          *reinterpret_cast<const uint4*>(e1_bf + row * D + c8);
+    }
+  }
+  for (int l = 0; l <= Lo.n; ++l) {
+    const float* bsrc = l < Lo.n ? emb.layer[l].b : q0_b;
+    const int rows = 16 * Lo.ob[l];
+    if (PREC == 0) {
+      const float* src = l < Lo.n ? emb.layer[l].w : q0_w;
+      const int ip = 16 * Lo.kb[l], q4 = ip / 4;
+      for (int idx = tid; idx < rows * q4; idx += nthreads) {
+        const int row = idx / q4, c4 = (idx - row * q4) * 4;
+        *reinterpret_cast<float4*>(&dst[Lo.w_off[l] + row * Lo.stride[l] + c4]) = ld4(src + row * ip + c4);
+      }
+    } else {
+      const uint16_t* src = emb_bf + Lo.g_off[l];
+      const int ip = 32 * Lo.kb[l], q8 = ip / 8;
+      __bf16* dstb = reinterpret_cast<__bf16*>(dst + Lo.w_off[l]);
+      for (int idx = tid; idx < 2 * rows * q8; idx += nthreads) {   // hi rows, then lo rows
+        const int row = idx / q8, c8 = (idx - row * q8) * 8;
+        *reinterpret_cast<uint4*>(&dstb[interleaved_slot(row, rows, Lo.stride[l], ip) + c8]) =
+            *reinterpret_cast<const uint4*>(src + row * ip + c8);
+      }
+    }
+    // (the fixed f16x3 layers keep every activation in the 2^11 domain: their biases are staged scaled, exactly)
+    const float bscale = (FIXED && PREC == 2) ? dom<2>() : 1.0f;
+    for (int idx = tid; idx < rows; idx += nthreads) dst[Lo.b_off[l] + idx] = bsrc[idx] * bscale;
+  }
+}
+
+__host__ __device__ inline int embed_image_floats(const EmbedLayout& Lo) { return (Lo.total + D * LDW + 3) & ~3; }
+
+template <int PREC, bool FIXED>
+__global__ __launch_bounds__(256) void embed_image_kernel(pemp_mlp emb, EmbedLayout Lo, const uint16_t* emb_bf,
+                                                          const float* q0_w, const float* q0_b, const float* e1_w,
+                                                          const uint16_t* e1_bf, float* img) {
+  embed_stage<PREC, FIXED>(img, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256, emb, Lo, emb_bf, q0_w, q0_b, e1_w,
+                           e1_bf);
+}
+
+__device__ inline void dma_to_lds(float* __restrict__ lds, const float* __restrict__ src, int n);
+__device__ __forceinline__ void lds_drain();
+
 // Edge embedding (sorted order), the fallback of the fused first pass: e_init = MLP(edge_attr[orig]),
 // Q0 = W1_e_init·e_init + b1 and R0 = Q0 + W1_e_cur·e_init (the first pass's layer-1 input).
-// One 16-wave workgroup per CU, weights staged once in LDS; a wave walks an equal share of the
-// sorted positions in 16-edge tiles.
+// One 16-wave workgroup per CU, weights staged once in LDS (from the prebuilt image when there is one); a wave
+// walks an equal share of the sorted positions in 16-edge tiles.
 template <int PREC, bool FIXED>
 __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp emb, EmbedLayout Lo,
                                                                      const uint16_t* __restrict__ emb_bf,
@@ -1168,34 +1231,16 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp em
                                                                      const float* __restrict__ e1_w,
                                                                      const uint16_t* __restrict__ e1_bf,
                                                                      float* __restrict__ r0, float* __restrict__ q0,
-                                                                     const int64_t* __restrict__ ne) {
+                                                                     const int64_t* __restrict__ ne,
+                                                                     const float* __restrict__ img) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   if (ne) E = ne[1];   // capacity mode: the device-side edge count
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
-  stage_tile64<PREC>(sm + Lo.total, e1_w, D, e1_bf);   // W1_e_cur after the embedding image
-  for (int l = 0; l <= Lo.n; ++l) {
-    const float* bsrc = l < Lo.n ? emb.layer[l].b : q0_b;
-    const int rows = 16 * Lo.ob[l];
-    if (PREC == 0) {
-      const float* src = l < Lo.n ? emb.layer[l].w : q0_w;
-      const int ip = 16 * Lo.kb[l], q4 = ip / 4;
-      for (int idx = threadIdx.x; idx < rows * q4; idx += 64 * EDGE_WAVES) {
-        const int row = idx / q4, c4 = (idx - row * q4) * 4;
-        *reinterpret_cast<float4*>(&sm[Lo.w_off[l] + row * Lo.stride[l] + c4]) = ld4(src + row * ip + c4);
-      }
-    } else {
-      const uint16_t* src = emb_bf + Lo.g_off[l];
-      const int ip = 32 * Lo.kb[l], q8 = ip / 8;
-      __bf16* dstb = reinterpret_cast<__bf16*>(sm + Lo.w_off[l]);
-      for (int idx = threadIdx.x; idx < 2 * rows * q8; idx += 64 * EDGE_WAVES) {   // hi rows, then lo rows
-        const int row = idx / q8, c8 = (idx - row * q8) * 8;
-        *reinterpret_cast<uint4*>(&dstb[interleaved_slot(row, rows, Lo.stride[l], ip) + c8]) =
-            *reinterpret_cast<const uint4*>(src + row * ip + c8);
-      }
-    }
-    // (the fixed f16x3 layers keep every activation in the 2^11 domain: their biases are staged scaled, exactly)
-    const float bscale = (FIXED && PREC == 2) ? dom<2>() : 1.0f;
-    for (int idx = threadIdx.x; idx < rows; idx += 64 * EDGE_WAVES) sm[Lo.b_off[l] + idx] = bsrc[idx] * bscale;
+  if (img) {
+    dma_to_lds(sm, img, embed_image_floats(Lo));
+    lds_drain();
+  } else {
+    embed_stage<PREC, FIXED>(sm, threadIdx.x, 64 * EDGE_WAVES, emb, Lo, emb_bf, q0_w, q0_b, e1_w, e1_bf);
   }
   __syncthreads();
   const int64_t gw = (int64_t)blockIdx.x * EDGE_WAVES + wave, nw = (int64_t)gridDim.x * EDGE_WAVES;
@@ -2954,6 +2999,19 @@ static void launch_edge_step_p(const EdgeStepArgs& a, bool head, bool pub, int g
   else launch_edge_step_s<AGG, PREC, UPD, STAGE_LAST>(a, head, pub, grid, st);
 }
 
+static bool edge_upd_fused(const pemp_mpn_desc& d, const pemp_mpn_weights& w);
+static bool edge_pub_head(const pemp_mpn_desc& d, const pemp_mpn_weights& w);
+// the edge embedding's arithmetic (mpn_forward_impl's emb_prec) and where its LDS image follows the passes' image
+static int embed_prec(const pemp_mpn_desc& d, const pemp_mpn_weights& w) {
+  return d.precision != PEMP_PREC_FP32 && w.emb_bf ? d.precision : PEMP_PREC_FP32;
+}
+static size_t edge_image_base_floats(const pemp_mpn_desc& d, const pemp_mpn_weights& w) {
+  return (size_t)d.num_types * img_stride(edge_upd_fused(d, w), edge_pub_head(d, w));
+}
+static size_t embed_image_offset(const pemp_mpn_desc& d, const pemp_mpn_weights& w) {
+  return (edge_image_base_floats(d, w) + 63) & ~(size_t)63;
+}
+
 static EdgeImgArgs edge_image_args(const pemp_mpn_desc& d, const pemp_mpn_weights& w, bool upd, bool head, float* img) {
   EdgeImgArgs a{};
   a.T = d.num_types; a.prec = d.precision; a.upd = upd ? 1 : 0; a.head = head ? 1 : 0; a.aggr = d.aggr;
@@ -3958,12 +4016,14 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
     ProfScope prof("edge_embed", pst);
     if (emb_lds) {
       const int grid = (int)std::min<int64_t>(num_cus(), (E + 16 * EDGE_WAVES - 1) / (16 * EDGE_WAVES));
-      const size_t lds = (size_t)(emb_lo.total + D * LDW) * sizeof(float);
+      const size_t lds = (size_t)embed_image_floats(emb_lo) * sizeof(float);
       const bool fixed = embed_fixed_shape(emb_lo);
+      // the caller's prebuilt LDS image (pemp_mpn_edge_image appends it to the edge-pass image), else staged here
+      const float* emb_img = w->edge_img ? w->edge_img + embed_image_offset(*desc, *w) : nullptr;
 #define PEMP_EMBED_LAUNCH(P, FX)                                                                                   \
   hipLaunchKernelGGL((edge_embed_kernel<P, FX>), dim3(grid), dim3(64 * EDGE_WAVES), lds, pst, w->edge_emb, emb_lo,  \
                      w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, w->e1_bf, \
-                     ws.EA, ws.Q0, ne)
+                     ws.EA, ws.Q0, ne, emb_img)
       if (emb_prec == PEMP_PREC_F16X3) {
         if (fixed) PEMP_EMBED_LAUNCH(2, true);
         else PEMP_EMBED_LAUNCH(2, false);
@@ -3973,7 +4033,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
       } else
         hipLaunchKernelGGL((edge_embed_kernel<0, false>), dim3(grid), dim3(64 * EDGE_WAVES), lds, pst, w->edge_emb, emb_lo,
                            w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, w->e1_bf,
-                           ws.EA, ws.Q0, ne);
+                           ws.EA, ws.Q0, ne, emb_img);
 #undef PEMP_EMBED_LAUNCH
     } else {
       hipLaunchKernelGGL(edge_embed_wide_kernel, dim3((unsigned)((E + 63) / 64)), dim3(256), 0, pst, w->edge_emb,
@@ -4450,7 +4510,8 @@ extern "C" int pemp_mpn_prepare(const pemp_mpn_desc* desc, const int64_t* edge_i
 
 extern "C" size_t pemp_mpn_edge_image_floats(const pemp_mpn_desc* desc, const pemp_mpn_weights* w) {
   if (!desc || !w || desc->num_types < 1 || desc->num_types > MAXT) return 0;
-  return (size_t)desc->num_types * img_stride(edge_upd_fused(*desc, *w), edge_pub_head(*desc, *w));
+  if (!mlp_ok(w->edge_emb, 64, 64)) return edge_image_base_floats(*desc, *w);
+  return embed_image_offset(*desc, *w) + embed_image_floats(embed_layout(w->edge_emb, embed_prec(*desc, *w)));
 }
 
 extern "C" int pemp_mpn_edge_image(const pemp_mpn_desc* desc, const pemp_mpn_weights* w, float* image, size_t floats,
@@ -4466,6 +4527,26 @@ extern "C" int pemp_mpn_edge_image(const pemp_mpn_desc* desc, const pemp_mpn_wei
   EdgeImgArgs ia = edge_image_args(*desc, *w, edge_upd_fused(*desc, *w), edge_pub_head(*desc, *w), image);
   hipLaunchKernelGGL(edge_image_kernel, dim3(16, (unsigned)desc->num_types), dim3(256), 0, as_stream(stream), ia);
   PEMP_LAUNCH_CHECK();
+  if (mlp_ok(w->edge_emb, 64, 64)) {   // the edge embedding's LDS image, after the passes' (edge_embed_kernel)
+    const int prec = embed_prec(*desc, *w);
+    const EmbedLayout lo = embed_layout(w->edge_emb, prec);
+    float* eimg = image + embed_image_offset(*desc, *w);
+    const bool fixed = embed_fixed_shape(lo);
+#define PEMP_EMBED_IMAGE(P, FX)                                                                                  \
+  hipLaunchKernelGGL((embed_image_kernel<P, FX>), dim3(16), dim3(256), 0, as_stream(stream), w->edge_emb, lo,     \
+                     w->emb_bf, w->q0_w, w->q0_b, w->e1_w, w->e1_bf, eimg)
+    if (prec == PEMP_PREC_F16X3) {
+      if (fixed) PEMP_EMBED_IMAGE(2, true);
+      else PEMP_EMBED_IMAGE(2, false);
+    } else if (prec == PEMP_PREC_BF16X3) {
+      if (fixed) PEMP_EMBED_IMAGE(1, true);
+      else PEMP_EMBED_IMAGE(1, false);
+    } else {
+      PEMP_EMBED_IMAGE(0, false);
+    }
+#undef PEMP_EMBED_IMAGE
+    PEMP_LAUNCH_CHECK();
+  }
   return PEMP_OK;
 }
 
