@@ -38,6 +38,27 @@ constexpr int D = 64;
 constexpr int LDW = 72;     // LDS row stride of a 64x64 weight tile (conflict-free ds_read_b128)
 constexpr int MAXT = 17;
 constexpr int EDGE_WAVES = 16;   // waves per edge-pass / edge-embedding workgroup (one workgroup per CU)
+#ifndef PEMP_RESERVE_CUS_DEFAULT
+#define PEMP_RESERVE_CUS_DEFAULT 64
+#endif
+#ifndef PEMP_RESERVE_MIN_EDGES
+#define PEMP_RESERVE_MIN_EDGES 65536
+#endif
+// CUs that the one-workgroup-per-CU launches of a forward over E edges (edge passes, edge embedding, and the prepares'
+// per-workgroup split) spread over. From PEMP_RESERVE_MIN_EDGES edges on, PEMP_RESERVE_CUS of them (rounded down to
+// a multiple of 8, so the XCD-aware placement still sees whole XCD rows) are left free: with two batches in flight
+// the other batch's small latency-bound kernels run there instead of waiting for the full-chip launches (c3 +4 %,
+// c3knn10 / c5ms +11 % images/s, one batch at a time -1.5 %). Smaller graphs (batch 1) keep
+// every CU.
+static int edge_cus(int64_t E) {
+  static const int reserved = [] {
+    const char* e = getenv("PEMP_RESERVE_CUS");
+    int r = e ? atoi(e) : PEMP_RESERVE_CUS_DEFAULT;
+    r = r < 0 ? 0 : (r & ~7);
+    return std::max(8, num_cus() - r);
+  }();
+  return E >= PEMP_RESERVE_MIN_EDGES ? reserved : num_cus();
+}
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float a, float b, float c, float d) {
@@ -233,7 +254,7 @@ static MpnWs mpn_carve(void* base, int T, int64_t N, int64_t E, size_t* bytes) {
   w.EA = c.take<float>(E * D);
   w.EB = c.take<float>(E * D);
   w.img = c.take<float>(IMG_FLOATS);
-  const int G = std::max(num_cus(), T);       // edge-pass grid
+  const int G = std::max(num_cus(), T);        // edge-pass grid (at most)
   w.ranges = c.take<int4>((size_t)G * (EDGE_WAVES + 12));
   w.eimg = c.take<float>((size_t)T * EIMG_MAX_STRIDE);   // edge-pass weight image when the caller has none
   w.sym = c.take<int>(3 * N);                           // symmetric prepare: row bounds + check flags per node
@@ -3746,7 +3767,7 @@ static int launch_prepare(const pemp_mpn_desc* desc, const int64_t* edge_index, 
                        ws.cnt, ws.err);
     PEMP_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(mpn_scan_kernel, dim3(1), dim3(1024), 0, st, ws.cnt, K, N, T, std::max(num_cus(), T), ws.seg,
+  hipLaunchKernelGGL(mpn_scan_kernel, dim3(1), dim3(1024), 0, st, ws.cnt, K, N, T, std::max(edge_cus(E), T), ws.seg,
                      ws.wg_start);
   PEMP_LAUNCH_CHECK();
   if (E > 0) {
@@ -3773,7 +3794,7 @@ static int launch_prepare_sym(const pemp_mpn_desc* desc, const int64_t* edge_ind
   hipLaunchKernelGGL(sym_rows_kernel, dim3(g), dim3(256), 0, st, edge_index, node_types, tstride, N, E, T, ws.cnt, rows,
                      packed, flags);
   PEMP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(sym_scan_kernel, dim3((unsigned)T), dim3(1024), 0, st, ws.cnt, N, T, std::max(num_cus(), T), ws.seg,
+  hipLaunchKernelGGL(sym_scan_kernel, dim3((unsigned)T), dim3(1024), 0, st, ws.cnt, N, T, std::max(edge_cus(E), T), ws.seg,
                      ws.wg_start, flags, E, ws.err);
   PEMP_LAUNCH_CHECK();
   hipLaunchKernelGGL(sym_place_kernel, dim3(g), dim3(256), 0, st, N, T, ws.seg, rows, packed, ws.s_src, ws.s_dst,
@@ -3952,7 +3973,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   const int emb_prec = desc->precision != PEMP_PREC_FP32 && w->emb_bf ? desc->precision : PEMP_PREC_FP32;
   const EmbedLayout emb_lo = embed_layout(w->edge_emb, emb_prec);
   const bool ept = w->ept_l1_w != nullptr;
-  const int edge_grid = std::max(num_cus(), T);   // >= wg_start[T] (see mpn_scan_kernel)
+  const int edge_grid = std::max(edge_cus(E), T);   // >= wg_start[T] (see mpn_scan_kernel)
   const bool pub_head = edge_pub_head(*desc, *w);
   // the edge-pass weight image: the caller's (pemp_mpn_edge_image, built once per weight set) or built here
   const float* eimg = w->edge_img;
@@ -3967,7 +3988,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   auto edge_prepare = [&]() -> int {
   if (!(desc->flags & PEMP_MPN_PREPARED)) {
     if (fully_node_off && N > 0) {
-      FullyPrepArgs fa{fully_node_off, fully_B, node_types, tstride, N, T, std::max(num_cus(), T),
+      FullyPrepArgs fa{fully_node_off, fully_B, node_types, tstride, N, T, std::max(edge_cus(E), T),
                        ws.seg, ws.wg_start, ws.s_src, ws.s_dst, ws.s_orig, ws.err, ne};
       // one thread per (type, target) segment (a per-edge mapping with binary searches measured 41 us
       // vs 15 us at C3)
@@ -3982,7 +4003,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
       ka.N = N;
       ka.E = E;
       ka.T = T;
-      ka.G = std::max(num_cus(), T);
+      ka.G = std::max(edge_cus(E), T);
       ka.seg = ws.seg;
       ka.wg_start = ws.wg_start;
       ka.s_src = ws.s_src;
@@ -4015,7 +4036,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   if (E > 0 && steps >= 1) {
     ProfScope prof("edge_embed", pst);
     if (emb_lds) {
-      const int grid = (int)std::min<int64_t>(num_cus(), (E + 16 * EDGE_WAVES - 1) / (16 * EDGE_WAVES));
+      const int grid = (int)std::min<int64_t>(edge_cus(E), (E + 16 * EDGE_WAVES - 1) / (16 * EDGE_WAVES));
       const size_t lds = (size_t)embed_image_floats(emb_lo) * sizeof(float);
       const bool fixed = embed_fixed_shape(emb_lo);
       // the caller's prebuilt LDS image (pemp_mpn_edge_image appends it to the edge-pass image), else staged here

@@ -1,0 +1,14 @@
+# round 5, call x: PEMP_RESERVE_CUS default 64 vs 0 on every workload line (alternating pairs)
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+for wl in c3 c5 c5ms c2 c3knn10; do
+  for r in 64 0 64 0; do
+    PEMP_RESERVE_CUS=$r timeout -k 10 200 python bench.py --workload $wl --no-cpu-baseline --no-roofline > gpurun_out/r05x_${wl}_$r.json 2> gpurun_out/r05x_${wl}_$r.err || exit 1
+    python - "$wl" "$r" <<'PY'
+import json, sys
+d = json.loads(open(f'gpurun_out/r05x_{sys.argv[1]}_{sys.argv[2]}.json').read().strip().splitlines()[-1])
+print(sys.argv[1], 'reserve', sys.argv[2], d['value'], d['ms_per_step'], d.get('value_serial_steps'))
+PY
+  done
+done
