@@ -33,6 +33,9 @@ namespace {
 #ifndef NMS_XCD_MAP
 #define NMS_XCD_MAP 1   // XCD-sliced unit windows (1.0x HBM fetch vs 1.5x without)
 #endif
+#ifndef NMS_RESERVE_CUS
+#define NMS_RESERVE_CUS 0   // CUs the strip kernel leaves free (PEMP_NMS_RESERVE_CUS overrides)
+#endif
 #ifndef NMS_PER_CU
 #define NMS_PER_CU 5
 #endif
@@ -1256,7 +1259,12 @@ static void launch_nms(const float* s, const float* masks, const DetectGeom& g, 
     int per_cu = SR > 16 ? 2 : NMS_PER_CU, occ = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, NT1, 0) == hipSuccess && occ > 0)
       per_cu = std::min(per_cu, occ);
-    const int grid = want < per_cu * num_cus() ? want : per_cu * num_cus();
+    static const int cus = [] {   // CUs the strips spread over (PEMP_NMS_RESERVE_CUS left to another batch in flight)
+      const char* e = getenv("PEMP_NMS_RESERVE_CUS");
+      const int r = e ? (atoi(e) & ~7) : NMS_RESERVE_CUS;
+      return std::max(8, num_cus() - std::max(r, 0));
+    }();
+    const int grid = want < per_cu * cus ? want : per_cu * cus;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(NT1), 0, st, s, masks, g, thr, use_thr, w.cand_v, w.cand_i, w.neg_v,
                        w.neg_i, w.tile_count, w.tile_nonneg, w.cbits, pj, w.pflag);
   };
