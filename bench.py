@@ -3,10 +3,9 @@
 
 One step = ``get_graph_constructor(...).construct_graph()`` + ``NodeClassificationMPNSimple``
 forward over one batch of synthetic 640x640 COCO-shaped inputs already resident in HBM (the
-frozen backbone is out of scope). Steps are issued round-robin on ``--streams`` HIP streams (default:
-the fastest of 1, 2 and 3 in a probe before the timed region; with 2, one batch's detection overlaps the
-previous batch's MPN, as a server with requests in flight would run; every step still does the whole path on
-its own batch); ``value_serial_steps`` is the same
+frozen backbone is out of scope). Steps are issued round-robin on ``--streams`` HIP streams (default
+2: one batch's detection overlaps the previous batch's MPN, as a server with two requests in flight
+would run; every step still does the whole path on its own batch); ``value_serial_steps`` is the same
 K steps on one stream. Multi-GPU: one process per GPU (torchrun), each rank owns its
 own images (weak scaling, no data-path collective); barrier + max-over-ranks timing.
 
@@ -758,7 +757,7 @@ def main():
 
     # batches in flight: each stream has its own library scratch (construct_graph and the MPN are
     # reentrant per (device, stream)); inputs are read-only and resident before the timed region
-    S = max(1, args.streams) if args.streams > 0 else 3
+    S = max(1, args.streams) if args.streams > 0 else 2
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
     torch.cuda.synchronize()
     for w in range(S):    # per-stream scratch and side streams allocated outside the timed region
@@ -768,11 +767,10 @@ def main():
     schedule_probe = None
     if args.streams == 0:
         # two batches in flight overlap one batch's detection with the other's MPN, but on some boxes the
-        # interleaving of the two queues serialises worse than one stream, and three in flight pay off only where
-        # the steps are long (c3knn10, c5: +2-3 %; c3: -11 %): time the three schedules here (outside the timed
-        # region, every rank the same choice) and run the fastest
+        # interleaving of the two queues serialises worse than one stream: time both schedules here (outside
+        # the timed region, every rank the same choice) and run the faster one
         probe = {}
-        for S_try in (2, 1, 3, 2, 1, 3):
+        for S_try in (2, 1, 2, 1):
             barrier(world)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -782,7 +780,7 @@ def main():
             torch.cuda.synchronize()
             dt = max_over_ranks(time.perf_counter() - t0, world, dev)
             probe[S_try] = min(probe.get(S_try, dt), dt)
-        S = min(probe, key=probe.get)
+        S = 2 if probe[2] < probe[1] else 1
         schedule_probe = {f"streams_{k}_ms_per_step": round(v / max(args.warmup, 4) * 1e3, 3) for k, v in probe.items()}
 
     # warmup (also finds the dominant kernel with the profiler on for every kernel)
