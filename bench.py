@@ -75,8 +75,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--profile-steps", action="store_true",
-                    help="for rocprofv3 per-shape traces: the warmup and the K steps strictly serial on one stream, "
-                         "nothing else (no schedule probe, roofline, isolated MPN, e2e, grouping or CPU legs)")
+                    help="for rocprofv3 per-shape traces: the warmup and the K steps strictly serial on one stream "
+                         "(round-robin on --streams S streams when given), nothing else (no schedule probe, roofline, "
+                         "isolated MPN, e2e, grouping or CPU legs)")
     ap.add_argument("--streams", type=int, default=0,
                     help="batches in flight: step i runs on HIP stream i %% S (serving-style overlap of one "
                          "batch's detection with the previous batch's MPN); 1 = strictly serial steps; 0 (default) "
@@ -741,12 +742,16 @@ def main():
     _lib.lib()
 
     if args.profile_steps:
-        for _ in range(max(args.warmup, 1)):
-            run_step(wl, gc, model, hm, feats, tags, dev)
+        # (--streams S > 1: the steps round-robin on S streams, as the timed region runs them)
+        ps = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(max(args.streams, 1) - 1)]
+        for i in range(max(args.warmup, len(ps))):
+            with torch.cuda.stream(ps[i % len(ps)]):
+                run_step(wl, gc, model, hm, feats, tags, dev)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            run_step(wl, gc, model, hm, feats, tags, dev)
+        for i in range(args.steps):
+            with torch.cuda.stream(ps[i % len(ps)]):
+                run_step(wl, gc, model, hm, feats, tags, dev)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         if rank == 0:
