@@ -705,3 +705,27 @@ def test_repeated_forward_is_bit_identical(name, prec):
             first = flat.clone()
         assert torch.equal(flat, first)
     assert max_err(pe[-1], torch.from_numpy(a["edge_logits"])) < TOL
+
+
+@pytest.mark.parametrize("prec", PRECS)
+@pytest.mark.parametrize("name", ["mpn_attn_t3", "mpn_max_t3"])
+def test_weight_images_or_staging_identical(name, prec):
+    """The passes' and the edge embedding's weights staged from the prebuilt LDS images (pemp_mpn_edge_image, the
+    fold's default) or, without images (a raw C-ABI caller), by the kernels themselves: bit-identical logits."""
+    meta, a = gu.load(name)
+    cfg = gu.mpn_config(meta)
+    if prec == "bf16x3" and "attn" not in name:
+        pytest.skip("bf16x3 is offered for the attention variant")
+    model, _ = make_model(cfg, meta["salt"], prec, meta.get("attn_gain", 1.0), meta.get("weight_gain", 1.0))
+    inp = [torch.from_numpy(a[k]).to(DEV) for k in ("x", "edge_attr", "edge_index", "node_types")]
+    pe, pn, pc, _ = run(model, *inp)
+    with_img = torch.cat([pe[-1].flatten(), pn[-1].flatten(), pc[-1].flatten()]).clone()
+    s = model._weights(DEV).struct
+    saved = (s.edge_img, s.node_img)
+    try:
+        s.edge_img, s.node_img = None, None
+        pe, pn, pc, _ = run(model, *inp)
+    finally:
+        s.edge_img, s.node_img = saved
+    staged = torch.cat([pe[-1].flatten(), pn[-1].flatten(), pc[-1].flatten()])
+    assert torch.equal(with_img, staged)
