@@ -74,6 +74,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=30.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-backbone", action="store_true",
+                    help="skip the backbone leg (a random-weight HigherHRNet-w48 forward on the batch's 640 px images, "
+                         "torch / MIOpen bf16 channels-last, tools/hrnet_w48.py; its first call compiles MIOpen "
+                         "kernels for ~7 s)")
     ap.add_argument("--profile-steps", action="store_true",
                     help="for rocprofv3 per-shape traces: the warmup and the K steps strictly serial on one stream "
                          "(round-robin on --streams S streams when given), nothing else (no schedule probe, roofline, "
@@ -621,6 +625,41 @@ def e2e_pipeline(wl, gc, model, hm, feats, tags, dev, steps, warmup, world):
     return rec
 
 
+def backbone_leg(wl, dev, steps, step_s, world):
+    """SURVEY 8(d) C3's backbone term: a random-weight HigherHRNet-w48 (tools/hrnet_w48.py, the compute graph of
+    model_58_4_4.yaml) on B x 3 x 640 x 640 images, bf16 channels-last on torch / MIOpen (the backbone stays on
+    PyTorch-ROCm, out of this path's scope), timed like the step; `with_path_images_per_sec` composes it serially
+    with the measured post-backbone step (this leg's ms per batch + ms_per_step)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from hrnet_w48 import HigherHRNetW48
+    dt_name = os.environ.get("PEMP_BB_DTYPE", "bf16")
+    dtype = {"bf16": torch.bfloat16, "f16": torch.float16, "f32": torch.float32}[dt_name]
+    layout = os.environ.get("PEMP_BB_LAYOUT", "nhwc")   # (measured: 19.6 ms per batch vs 25.2 NCHW, bf16)
+    fmt = torch.channels_last if layout == "nhwc" else torch.contiguous_format
+    torch.backends.cudnn.benchmark = True
+    torch.manual_seed(0)
+    net = HigherHRNetW48(wl["J"]).eval().to(dev, dtype=dtype, memory_format=fmt)
+    img = torch.randn(wl["B"], 3, 640, 640, device=dev, dtype=dtype).contiguous(memory_format=fmt)
+    with torch.no_grad():
+        for i in range(3):                     # MIOpen finds / compiles its kernels here
+            t0 = time.perf_counter()
+            net(img)
+            torch.cuda.synchronize()
+            print(f"backbone warm-up {i}: {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
+        barrier(world)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            net(img)
+        torch.cuda.synchronize()
+        dt = max_over_ranks((time.perf_counter() - t0) / steps, world, dev)
+    flop = 154.3e9   # HigherHRNet-w48 at 640 px: 154.3 GFLOP per image (the architecture's published figure)
+    return {"model": "HigherHRNet-w48 (random weights, tools/hrnet_w48.py)", "input": [wl["B"], 3, 640, 640],
+            "dtype": f"{dt_name}, {layout}", "ms_per_batch": round(dt * 1e3, 3),
+            "images_per_sec": round(wl["B"] * world / dt, 1),
+            "tflops": round(flop * wl["B"] / dt / 1e12, 1),
+            "with_path_images_per_sec": round(wl["B"] * world / (dt + step_s), 1)}
+
+
 def person_structured_probs(wl, out):
     """Edge and node probabilities shaped like a trained network's for construct_graph output `out`: node i of
     an image belongs to person (local index mod persons_per_image); edge probabilities sigmoid(+-2.5 + N(0, 1.5))
@@ -900,6 +939,12 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(wl, gc, model, hm, feats, tags, args.cpu_seconds)
+    bb = None
+    if not args.no_backbone and not args.no_roofline:
+        try:   # (an informational leg: never lose the bench line over it)
+            bb = backbone_leg(wl, dev, args.steps, dt_max / args.steps, world)
+        except Exception as exc:
+            bb = {"error": repr(exc)[:200]}
 
     if rank == 0:
         rec = {
@@ -932,6 +977,7 @@ def main():
             # the one collective of the sharded path (RCCL all_gather of every rank's grouped poses)
             "pose_all_gather_ms": grouping.get("pose_all_gather_ms") if grouping else None,
             "capacity_graphs": graph_stats(),
+            "backbone": bb,
         }
         if cpu:
             rec["speedup_vs_cpu"] = round(value / cpu["value"], 1)

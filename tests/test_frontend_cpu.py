@@ -136,3 +136,18 @@ def test_stage_merge_restatement(flip):
     ph = ProjectedHeatmaps(merged, size, J, mflip, fi if flip else None)
     s, t = ph.materialize()
     assert torch.equal(s, ref_s) and torch.equal(t, ref_t)
+
+
+def test_backbone_leg_model_is_higherhrnet_w48():
+    """bench.py's backbone leg times tools/hrnet_w48.py: the HigherHRNet-w48 compute graph of model_58_4_4.yaml (63.8 M
+    parameters, 2 x 17 heatmap + tag channels at 1/4 resolution, 17 heatmaps and the 48-channel features at 1/2)."""
+    import os
+    import sys
+    import torch
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from hrnet_w48 import HigherHRNetW48
+    m = HigherHRNetW48(17).eval()
+    assert abs(sum(p.numel() for p in m.parameters()) / 1e6 - 63.83) < 0.01
+    with torch.no_grad():
+        (y0, y1), f = m(torch.zeros(1, 3, 64, 96))
+    assert y0.shape == (1, 34, 16, 24) and y1.shape == (1, 17, 32, 48) and f.shape == (1, 48, 32, 48)

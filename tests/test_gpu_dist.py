@@ -126,8 +126,8 @@ def test_bench_spawns_ranks():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env.update(PEMP_SHARE_DEVICE="1", PEMP_DIST_BACKEND="gloo")
     res = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
-                          "--no-cpu-baseline", "--streams", "1"], cwd=root, env=env, capture_output=True, text=True,
-                         timeout=400)
+                          "--no-cpu-baseline", "--no-backbone", "--streams", "1"], cwd=root, env=env,
+                         capture_output=True, text=True, timeout=400)
     assert res.returncode == 0, res.stderr[-3000:]
     lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, res.stdout[-2000:]
