@@ -19,6 +19,10 @@ timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_
   --output-format csv -d gpurun_out/${T}_mfma_c3 -o pmc -- python bench.py --workload c3 --steps 3 --warmup 1 --no-cpu-baseline --no-roofline \
   > gpurun_out/${T}_mfma_c3.log 2>&1 || exit 1
 python tools/mfma_util.py gpurun_out/${T}_mfma_c3/pmc_counter_collection.csv --merge profiles/mfma_latest.json --workload c3 > gpurun_out/${T}_mfma_c3.txt || exit 1
+timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE --kernel-include-regex 'edge_step|edge_embed|node_' \
+  --output-format csv -d gpurun_out/${T}_mfma_c3knn10 -o pmc -- python bench.py --workload c3knn10 --steps 3 --warmup 1 --no-cpu-baseline --no-roofline \
+  > gpurun_out/${T}_mfma_c3knn10.log 2>&1 || exit 1
+python tools/mfma_util.py gpurun_out/${T}_mfma_c3knn10/pmc_counter_collection.csv --merge profiles/mfma_latest.json --workload c3knn10 > gpurun_out/${T}_mfma_c3knn10.txt || exit 1
 cp profiles/mfma_latest.json gpurun_out/${T}_mfma_latest.json
 echo "mfma ok"
 bash tools/pmc_edge.sh ${T}_sqedge 'edge_step_kernel' > gpurun_out/${T}_sq_edge.txt 2>&1 || exit 1
