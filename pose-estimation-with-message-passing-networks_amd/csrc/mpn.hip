@@ -4303,7 +4303,10 @@ extern "C" int pemp_mpn_forward_fully(const pemp_mpn_desc* desc, const pemp_mpn_
 // captured into a HIP graph the second time the same arguments come (the first time they launch directly: one-off
 // argument sets never pay a capture) and replayed with one launch from then on -- a serving loop whose allocator
 // hands back the same buffers every step. Keyed by the bytes of every argument; a small LRU.
-// PEMP_NO_GRAPHS disables it; the library profiler (per-kernel events) runs the launches directly.
+// Opt-in (PEMP_GRAPHS=1; PEMP_NO_GRAPHS wins): on this image a replay costs the host more than the direct launches
+// (58-72 vs 44 us per call at c2, where the host bounds the batch-1 step) and gave the GPU nothing measurable at c2,
+// c3 or c3knn10 (tools/experiments/round5/gg.sh, ii.sh). The library profiler (per-kernel
+// events) runs the launches directly.
 struct CapGraph {
   std::string key;
   hipGraphExec_t exec = nullptr;
@@ -4311,7 +4314,10 @@ struct CapGraph {
 };
 
 static bool graphs_off() {
-  static const bool v = getenv("PEMP_NO_GRAPHS") != nullptr;
+  static const bool v = [] {
+    const char* on = getenv("PEMP_GRAPHS");
+    return getenv("PEMP_NO_GRAPHS") != nullptr || !(on && atoi(on) != 0);
+  }();
   return v;
 }
 

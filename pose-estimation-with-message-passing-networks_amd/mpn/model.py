@@ -50,6 +50,15 @@ TYPE_LUTS = {"left_right": [0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8],
              "per_body_part": [0, 0, 0, 0, 0, 1, 1, 2, 3, 2, 3, 4, 5, 4, 5, 4, 5]}
 
 
+def _rows(logits, n):
+    """[logits[r].view(L, 1).squeeze() for r in range(n)] (the per-step logit lists of NodeClassificationMPNSimple.py:
+    81-97) for a [>= n, L] buffer: one unbind instead of three tensor ops per row (host time of the serving loop)."""
+    L = logits.shape[1]
+    if L != 1:   # squeeze of [L, 1] keeps [L]: the unbound row is the same view
+        return list((logits if logits.shape[0] == n else logits[:n]).unbind(0))
+    return [logits[r].view(L, 1).squeeze() for r in range(n)]
+
+
 def _make_mlp(input_dim, hidden_dims, bn=False, end_with_relu=False):
     """Layer indices as ``layers.py:8-29``: Linear, then (ReLU, [BN]) between Linears."""
     mods = [nn.Linear(input_dim, hidden_dims[0])]
@@ -259,9 +268,9 @@ class NodeClassificationMPNSimple(nn.Module):
             for r in range(n_rec + 1):
                 node_logits[r, n0:n1] = pn[r].reshape(-1)
                 class_logits[r, n0:n1] = pc[r]
-        preds_edge = [edge_logits[r].view(E, 1).squeeze() for r in range(n_rec)]
-        preds_node = [node_logits[r].view(N, 1).squeeze() for r in range(n_rec + 1)]
-        preds_class = [class_logits[r] for r in range(n_rec + 1)]
+        preds_edge = _rows(edge_logits, n_rec)
+        preds_node = _rows(node_logits, n_rec + 1)
+        preds_class = list(class_logits.unbind(0))
         return preds_edge, preds_node, preds_class, [None]
 
     def forward(self, x, edge_attr, edge_index, **kwargs):
@@ -344,9 +353,9 @@ class NodeClassificationMPNSimple(nn.Module):
         if kwargs.get("validate", _VALIDATE or (_DEBUG_SYNC and (sym or fully is not None or knn is not None))):
             _lib.check(L.pemp_mpn_status(desc, N, E, _lib.ptr(ws), _lib.stream(dev)))
         # list lengths and .squeeze() semantics of NodeClassificationMPNSimple.py:81-97
-        preds_edge = [edge_logits[r].view(E, 1).squeeze() for r in range(n_rec)]
-        preds_node = [node_logits[r].view(N, 1).squeeze() for r in range(n_rec + 1)]
-        preds_class = [class_logits[r] for r in range(n_rec + 1)]
+        preds_edge = _rows(edge_logits, n_rec)
+        preds_node = _rows(node_logits, n_rec + 1)
+        preds_class = list(class_logits.unbind(0))
         return preds_edge, preds_node, preds_class, [None]
 
 
@@ -427,9 +436,9 @@ class NodeClassificationMPNSimple(nn.Module):
         edge_logits = buf[:max(n_rec, 1) * E].view(max(n_rec, 1), E)
         node_logits = buf[a1:a1 + (n_rec + 1) * N].view(n_rec + 1, N)
         class_logits = buf[a2:a2 + (n_rec + 1) * N * J].view(n_rec + 1, N, J)
-        preds_edge = [edge_logits[r].view(E, 1).squeeze() for r in range(n_rec)]
-        preds_node = [node_logits[r].view(N, 1).squeeze() for r in range(n_rec + 1)]
-        preds_class = [class_logits[r] for r in range(n_rec + 1)]
+        preds_edge = _rows(edge_logits, n_rec)
+        preds_node = _rows(node_logits, n_rec + 1)
+        preds_class = list(class_logits.unbind(0))
         return preds_edge, preds_node, preds_class, [None]
 
 

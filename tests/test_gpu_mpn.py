@@ -344,10 +344,10 @@ def graph_stats():
 
 
 def test_capacity_graphs_single_key_and_debug_sync(tmp_path):
-    """A fresh process with one repeating argument set: the capacity forward is launched directly once, captured
-    the second time and replayed after that; under PEMP_DEBUG_SYNC=1 (synchronise after every launch, which a
-    capturing stream refuses) every call runs directly and computes the same logits. Runs in child processes
-    because both the graph cache and PEMP_DEBUG_SYNC are per process."""
+    """A fresh process with one repeating argument set and graphs on (PEMP_GRAPHS=1, opt-in): the capacity forward is
+    launched directly once, captured the second time and replayed after that; under PEMP_DEBUG_SYNC=1 (synchronise
+    after every launch, which a capturing stream refuses) every call runs directly and computes the same logits. Runs
+    in child processes because the graph cache, PEMP_GRAPHS and PEMP_DEBUG_SYNC are per process."""
     import json
     import os
     import subprocess
@@ -357,7 +357,7 @@ def test_capacity_graphs_single_key_and_debug_sync(tmp_path):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     outs = {}
     for dbg in ("0", "1"):
-        env = dict(os.environ, PEMP_DEBUG_SYNC=dbg, PYTHONPATH=root)
+        env = dict(os.environ, PEMP_DEBUG_SYNC=dbg, PEMP_GRAPHS="1", PYTHONPATH=root)
         r = subprocess.run([sys.executable, str(script)], env=env, cwd=root, capture_output=True, text=True,
                            timeout=240)
         assert r.returncode == 0, r.stderr[-3000:]

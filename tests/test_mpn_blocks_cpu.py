@@ -49,3 +49,17 @@ def test_blocks_refuse_an_indivisible_block():
 def test_blocks_without_edges():
     assert node_blocks(torch.zeros(2, 0, dtype=torch.long), 3, 1, 1) == [(0, 1), (1, 2), (2, 3)]
     assert node_blocks(torch.zeros(2, 0, dtype=torch.long), 0, 1, 1) == []
+
+
+@pytest.mark.parametrize("rows,n,L", [(3, 3, 7), (1, 0, 5), (4, 4, 1), (2, 2, 0), (5, 3, 2)])
+def test_logit_rows_match_view_squeeze(rows, n, L):
+    """mpn/model.py::_rows (one unbind) returns what the reference's per-row view(L, 1).squeeze() returns: same
+    shapes (a 0-d tensor for L == 1), values, strides and storage."""
+    from pemp_amd.mpn.model import _rows
+    buf = torch.arange(rows * L, dtype=torch.float32).view(rows, L)
+    got = _rows(buf, n)
+    ref = [buf[r].view(L, 1).squeeze() for r in range(n)]
+    assert len(got) == len(ref)
+    for a, b in zip(got, ref):
+        assert a.shape == b.shape and a.stride() == b.stride() and a.data_ptr() == b.data_ptr()
+        assert torch.equal(a, b)
