@@ -312,8 +312,8 @@ def test_capacity_mode_mpn(prec, monkeypatch):
                 assert a.shape == b.shape and torch.equal(a, b) and torch.equal(c, b), (seed, persons)
         # the first call sets the capacities (exact build); 6 persons overflow them
         assert used == [False, True, True, False, False, True], used
-        # the same batch again and again: once the allocator hands back the same buffers, the library replays its
-        # captured HIP graph of the forward (second sight of an argument set: capture; then replays)
+        # the same batch again and again (with PEMP_GRAPHS=1 in the environment, once the allocator hands back the same
+        # buffers, the library replays its captured HIP graph of the forward: second sight of an argument set)
         hm = torch.from_numpy(syn.make_heatmaps(2, B, J, H, W, 2, margin=4))
         first = None
         stats0 = graph_stats()
