@@ -476,9 +476,9 @@ int pemp_mpn_forward_fully_cap(const pemp_mpn_desc* desc, const pemp_mpn_weights
 
 /* Counters of pemp_mpn_forward_fully_cap's HIP graphs since the library loaded (no reference counterpart; for
  * tests and servers): out3[0] captures made, out3[1] graph launches (first launch after a capture included),
- * out3[2] captures refused (the forward then ran directly). A repeating argument set is launched directly the
- * first time, captured the second, replayed from then on; PEMP_NO_GRAPHS, PEMP_DEBUG_SYNC and the library
- * profiler run every call directly. */
+ * out3[2] captures refused (the forward then ran directly). Graphs are opt-in (PEMP_GRAPHS=1): a repeating argument
+ * set is then launched directly the first time, captured the second, replayed from then on; without it, and under
+ * PEMP_NO_GRAPHS, PEMP_DEBUG_SYNC or the library profiler, every call runs directly. */
 int pemp_mpn_graph_stats(uint64_t* out3);
 
 /* pemp_mpn_forward for an edge_index sorted by (src, dst) without duplicates and symmetric (every s -> d has
