@@ -2810,9 +2810,10 @@ __global__ __launch_bounds__(256) void node_rows_kernel(NodeRowsArgs a) {
 }
 
 // Node table NT = [x0 | x] · pre_w^T + pre_b for the next edge pass. 1-D grid of
-// (64-node chunk, 64-column group) workgroups, chunk-major; each of the 4 waves owns one 16-column
-// block (weight fragment in registers, loaded before the barrier) and walks the chunk's 4 node
-// tiles from LDS. HBM/L2 traffic ~ X · groups + pre_w · chunks (~24 MB at C3, vs ~55 MB tile-major).
+// (16 TILES-node chunk, 64-column group) workgroups, chunk-major; each of the 4 waves owns one 16-column
+// block (weight fragment in registers, loaded before the barrier) and walks the chunk's TILES node
+// tiles from LDS. L2 traffic ~ X · groups + pre_w · chunks: more tiles per chunk re-read the weights less, fewer
+// give more workgroups to a launch that mostly runs beside the other batch's edge pass (TBL_TILES below).
 // PREC 1: bf16x3 (pre_bf pack, K = 128 = 4 slot blocks).
 struct NodeTableArgs {
   const float* X;
@@ -2839,7 +2840,8 @@ struct NodeTableArgs {
 #define NODE_SUM_TABLE_MAX_MB 16   // ... while its aggregate re-reads (N T 256 B x column groups) stay below this
 #endif
 #ifndef PEMP_TBL_TILES
-#define PEMP_TBL_TILES 4
+#define PEMP_TBL_TILES 2   // (1 / 2 / 4 / 8 measured: 2 gives the shortest isolated MPN, c3knn10 0.423-0.426 vs 0.435 ms
+                           // with 4, c3 0.235 vs 0.239 ms; tools/experiments/round5/nn.sh)
 #endif
 constexpr int TBL_TILES = PEMP_TBL_TILES;   // 16-node tiles per workgroup
 
