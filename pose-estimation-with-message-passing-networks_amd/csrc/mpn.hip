@@ -50,6 +50,9 @@ constexpr int EDGE_WAVES = 16;   // waves per edge-pass / edge-embedding workgro
 // the other batch's small latency-bound kernels run there instead of waiting for the full-chip launches (c3 +4 %,
 // c3knn10 / c5ms +11 % images/s, one batch at a time -1.5 %). Smaller graphs (batch 1) keep
 // every CU.
+#ifndef PEMP_EMBED_RESERVE
+#define PEMP_EMBED_RESERVE 1   // the edge embedding leaves the reserved CUs free too (0: it spreads over every CU)
+#endif
 static int edge_cus(int64_t E) {
   static const int reserved = [] {
     const char* e = getenv("PEMP_RESERVE_CUS");
@@ -4038,7 +4041,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   if (E > 0 && steps >= 1) {
     ProfScope prof("edge_embed", pst);
     if (emb_lds) {
-      const int grid = (int)std::min<int64_t>(edge_cus(E), (E + 16 * EDGE_WAVES - 1) / (16 * EDGE_WAVES));
+      const int grid = (int)std::min<int64_t>(PEMP_EMBED_RESERVE ? edge_cus(E) : num_cus(), (E + 16 * EDGE_WAVES - 1) / (16 * EDGE_WAVES));
       const size_t lds = (size_t)embed_image_floats(emb_lo) * sizeof(float);
       const bool fixed = embed_fixed_shape(emb_lo);
       // the caller's prebuilt LDS image (pemp_mpn_edge_image appends it to the edge-pass image), else staged here
