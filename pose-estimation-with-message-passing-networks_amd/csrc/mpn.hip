@@ -3850,6 +3850,9 @@ static bool serial_prelude() {
 }
 
 // one per (device, launch stream), created on first use and kept; nullptr if HIP refuses (serial then)
+#ifndef PEMP_SIDE_PRIO
+#define PEMP_SIDE_PRIO 0
+#endif
 static SideStream* side_stream_for(hipStream_t st) {
   static std::mutex mu;
   static std::map<std::pair<int, hipStream_t>, SideStream*> table;
@@ -3865,7 +3868,11 @@ static SideStream* side_stream_for(hipStream_t st) {
   if (it != table.end()) return it->second;
   if (dev != cur && hipSetDevice(dev) != hipSuccess) return nullptr;
   SideStream* ss = new SideStream();
-  const bool ok = hipStreamCreateWithFlags(&ss->s, hipStreamNonBlocking) == hipSuccess &&
+  int prio_lo = 0, prio_hi = 0;   // PEMP_SIDE_PRIO: the edge prelude's stream at the device's highest priority
+  if (!PEMP_SIDE_PRIO || hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_hi = 0;
+  const bool ok = (PEMP_SIDE_PRIO && prio_hi != 0
+                       ? hipStreamCreateWithPriority(&ss->s, hipStreamNonBlocking, prio_hi)
+                       : hipStreamCreateWithFlags(&ss->s, hipStreamNonBlocking)) == hipSuccess &&
                   hipEventCreateWithFlags(&ss->fork, hipEventDisableTiming) == hipSuccess &&
                   hipEventCreateWithFlags(&ss->join, hipEventDisableTiming) == hipSuccess;
   if (dev != cur) (void)hipSetDevice(cur);
