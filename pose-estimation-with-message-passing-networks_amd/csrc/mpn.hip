@@ -3124,6 +3124,10 @@ static StagePlan node_image_plan(const pemp_mpn_weights& w) {
 // with E_t = sum_b n_{b,t} (n_b - 1). Identical arrays to launch_prepare's (tested bit for bit).
 constexpr int FULLY_MAXB = 64;      // images per batch
 constexpr int FULLY_MAXN = 2048;    // nodes per image (LDS lists)
+#ifndef PEMP_FULLY_PARTS
+#define PEMP_FULLY_PARTS 4
+#endif
+constexpr int FULLY_PARTS = PEMP_FULLY_PARTS;   // threads per (type, target) segment in fully_prepare_kernel
 // Capacity mode (pemp_mpn_forward_fully_cap): the batch's N = sum n_b and E = sum n_b (n_b - 1) from the detection
 // counts on the device, before the host has them. ne = (N, E, overflow); a batch past any capacity (an image over
 // the detection capacity, N > n_cap or E > e_cap: the capacity graph build wrote nothing) gets (0, 0, 1), and every
@@ -3237,8 +3241,11 @@ __global__ __launch_bounds__(256) void fully_prepare_kernel(FullyPrepArgs a) {
   __syncthreads();
   // segments (t, d): one thread each
   const long long eoff = eoff_sh;
-  for (int q = blockIdx.x * 256 + threadIdx.x; q < T * nb; q += gridDim.x * 256) {
-    const int t = q / nb, dl = q - t * nb;
+  // FULLY_PARTS consecutive threads per segment, entry m of the segment on thread (m - s0) % FULLY_PARTS: its slot is
+  // the segment start + its rank, one less past d when d itself is of type t (d is left out)
+  for (int q = blockIdx.x * 256 + threadIdx.x; q < T * nb * FULLY_PARTS; q += gridDim.x * 256) {
+    const int sq = q / FULLY_PARTS, part = q - sq * FULLY_PARTS;
+    const int t = sq / nb, dl = sq - t * nb;
     const int s0 = tstart_l[t], s1 = tstart_l[t + 1];
     int lo = s0, hi = s1;                              // type-t nodes before dl
     while (lo < hi) {
@@ -3247,15 +3254,16 @@ __global__ __launch_bounds__(256) void fully_prepare_kernel(FullyPrepArgs a) {
     }
     const int before = lo - s0;
     const int64_t d = ob + dl;
-    int pos = tbase[t] + (int)cb_sh[t] + dl * (s1 - s0) - before;
-    a.seg[(int64_t)t * N + d] = pos;
-    for (int m = s0; m < s1; ++m) {                      // the segment: type-t nodes except d, in order
+    const int pos = tbase[t] + (int)cb_sh[t] + dl * (s1 - s0) - before;
+    const bool d_in = lty[dl] == t;
+    if (part == 0) a.seg[(int64_t)t * N + d] = pos;
+    for (int m = s0 + part; m < s1; m += FULLY_PARTS) {   // the segment: type-t nodes except d, in order
       const int i = sorted[m];
       if (i == dl) continue;
-      a.s_src[pos] = ob + i;
-      a.s_dst[pos] = (int)d;
-      a.s_orig[pos] = (int)(eoff + (long long)i * (nb - 1) + (dl < i ? dl : dl - 1));
-      ++pos;
+      const int p = pos + (m - s0) - (d_in && i > dl ? 1 : 0);
+      a.s_src[p] = ob + i;
+      a.s_dst[p] = (int)d;
+      a.s_orig[p] = (int)(eoff + (long long)i * (nb - 1) + (dl < i ? dl : dl - 1));
     }
   }
   if (blockIdx.x == 0 && blockIdx.y == 0) {
@@ -4002,9 +4010,10 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
     if (fully_node_off && N > 0) {
       FullyPrepArgs fa{fully_node_off, fully_B, node_types, tstride, N, T, std::max(edge_cus(E), T),
                        ws.seg, ws.wg_start, ws.s_src, ws.s_dst, ws.s_orig, ws.err, ne};
-      // one thread per (type, target) segment (a per-edge mapping with binary searches measured 41 us
+      // FULLY_PARTS threads per (type, target) segment (a per-edge mapping with binary searches measured 41 us
       // vs 15 us at C3)
-      const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(64, ((int64_t)T * fully_nmax + 511) / 512));
+      const unsigned gx =
+          (unsigned)std::max<int64_t>(1, std::min<int64_t>(64, ((int64_t)T * fully_nmax * FULLY_PARTS + 511) / 512));
       ProfScope prof("mpn_prepare", pst);
       hipLaunchKernelGGL(fully_prepare_kernel, dim3(gx, (unsigned)fully_B), dim3(256), 0, pst, fa);
       PEMP_LAUNCH_CHECK();
