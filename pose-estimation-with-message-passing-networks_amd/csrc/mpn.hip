@@ -3188,16 +3188,28 @@ __global__ __launch_bounds__(256) void fully_prepare_kernel(FullyPrepArgs a) {
   for (int i = threadIdx.x; i < FULLY_MAXB * MAXT; i += 256) (&cnt_bt[0][0])[i] = 0;
   if (threadIdx.x == 0) bad_sh = 0;
   __syncthreads();
-  // per-(image, type) node counts of the whole batch (every block: N is a few thousand at most)
-  for (int64_t n = threadIdx.x; n < N; n += 256) {
-    int lo = 0, hi = B - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (noff[mid] <= n) lo = mid; else hi = mid - 1;
+  // per-(image, type) node counts of the whole batch (every block: N is a few thousand at most); a thread's type
+  // loads go out 8 at a time, ahead of the searches and the LDS counts that use them
+  for (int64_t n0 = threadIdx.x; n0 < N; n0 += 256 * 8) {
+    int64_t tv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t n = n0 + 256 * k;
+      tv[k] = n < N ? a.types[n * a.ts] : 0;
     }
-    const int64_t t = a.types[n * a.ts];
-    if (t >= 0 && t < T) atomicAdd(&cnt_bt[lo][t], 1);
-    else bad_sh = 1;                                 // skipped as a source, like mpn_count_kernel
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t n = n0 + 256 * k;
+      if (n >= N) break;
+      int lo = 0, hi = B - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (noff[mid] <= n) lo = mid; else hi = mid - 1;
+      }
+      const int64_t t = tv[k];
+      if (t >= 0 && t < T) atomicAdd(&cnt_bt[lo][t], 1);
+      else bad_sh = 1;                               // skipped as a source, like mpn_count_kernel
+    }
   }
   __syncthreads();
   if (threadIdx.x < T) {
