@@ -226,7 +226,7 @@ def mfma_busy(kernel_prefix, workload):
     for run in runs:
         if run.get("workload") == workload:
             hits = [v for k, v in run["kernels"].items() if kernel_prefix in k]
-            return hits[0]["mfma_busy"] if len(hits) == 1 else None
+            return hits[0] if len(hits) == 1 else None
     return None
 
 
@@ -266,9 +266,14 @@ def roofline_for(label, stats, E, wl, precision, upd, workload, agg_bytes=0):
         traffic = pmc_traffic("pemp::edge_step_kernel<0," + ("1" if head else "0"), workload, E)
         mb = mfma_busy("edge_step_kernel<0, " + ("1" if head else "0") + ", " + str(PREC_CODE[precision]), workload)
         common = {"kernel": label, "avg_launch_us": round(avg_s * 1e6, 2), "launches": n, "traffic": traffic,
-                  "mfma_busy": mb,
+                  "mfma_busy": mb["mfma_busy"] if mb else None,
+                  # the same over the SIMDs of the CUs the pass occupies (4 x min(256, workgroups): 192 CUs under
+                  # the CU reservation), when the SQ pass recorded it
+                  "mfma_busy_used_simds": mb.get("mfma_busy_used") if mb else None,
+                  "mfma_busy_cus": mb.get("cus_used") if mb else None,
                   "mfma_busy_source": f"profiles/mfma_latest.json ({workload}): SQ_VALU_MFMA_BUSY_CYCLES / "
-                                      f"(1024 SIMDs x GRBM_GUI_ACTIVE / 8)" if mb is not None else None,
+                                      f"(1024 SIMDs x GRBM_GUI_ACTIVE / 8); _used_simds: over 4 x cus SIMDs"
+                                      if mb is not None else None,
                   "traffic_source": f"profiles/pmc_latest.json ({workload}, E={E})" if traffic else None,
                   "algorithmic": f"{f1} FLOP and {b1} B HBM x E={E} edges + {agg_bytes} B of aggregate rows "
                                  f"per launch",
@@ -933,7 +938,8 @@ def main():
             start, _ = pdist.image_block(wl["B"] * world, rank, world)
             barrier(world)
             t2 = time.perf_counter()
-            ids, poses = pdist.gather_poses(_LAST_GROUPING, list(range(start, start + wl["B"])), wl["J"], world, dev)
+            ids, poses = pdist.gather_poses(_LAST_GROUPING, list(range(start, start + wl["B"])), wl["J"], world, dev,
+                                            total_images=wl["B"] * world)
             grouping["pose_all_gather_ms"] = round((time.perf_counter() - t2) * 1e3, 3)
             grouping["gathered_images"] = len(ids)
         except Exception as exc:  # informational field only: never lose the bench line over it

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define PEMP_ABI_VERSION 19
+#define PEMP_ABI_VERSION 20
 
 enum {
   PEMP_OK = 0,
@@ -334,7 +334,7 @@ int pemp_pose_adjust(const float* det, int J, int H, int W, double* keypoints, i
 /* pemp_pack_to_host (GPU + copy): the n <= 16 device regions src[i] (bytes[i] bytes each) gathered into the device
  * buffer staging at offsets off[i] (multiples of 16, off[i] + bytes[i] <= total), then one stream-ordered copy of
  * staging[0, total) to host_dst (pinned host memory): the grouping's read-back in one copy instead of one per
- * array. */
+ * array. host_dst NULL: the gather only (the caller queues the copy itself). */
 int pemp_pack_to_host(int n, const void* const* src, const size_t* bytes, const size_t* off, size_t total,
                       void* staging, void* host_dst, void* stream);
 int pemp_pose_finish_plan(int B, const int32_t* counts, const uint8_t* ref, int32_t* pimg, int32_t* chunks,
@@ -480,6 +480,13 @@ int pemp_mpn_forward_fully_cap(const pemp_mpn_desc* desc, const pemp_mpn_weights
  * set is then launched directly the first time, captured the second, replayed from then on; without it, and under
  * PEMP_NO_GRAPHS, PEMP_DEBUG_SYNC or the library profiler, every call runs directly. */
 int pemp_mpn_graph_stats(uint64_t* out3);
+
+/* The CU-reservation policy of the edge passes and the edge embedding (no reference counterpart; pure host
+ * arithmetic, no device call): the number of CUs a forward over E edges spreads its one-workgroup-per-CU launches
+ * over on a device of num_cus CUs when reserve_request CUs are asked to stay free for another batch in flight
+ * (reserve_request < 0: the library's setting, PEMP_RESERVE_CUS or 64). Graphs below 65,536 edges keep every CU;
+ * above, at most a quarter of the device is reserved (rounded down to a multiple of 8). */
+int pemp_edge_cus_policy(int num_cus, int64_t E, int reserve_request);
 
 /* pemp_mpn_forward for an edge_index sorted by (src, dst) without duplicates and symmetric (every s -> d has
  * its d -> s: PyG to_undirected's coalesced output, as knn_mpn_graph / feature_knn_mpn_graph / score_based_graph

@@ -9,7 +9,7 @@ import os
 
 LIB_PATH = os.environ.get("PEMP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc",
                                                      "libpemp.so")
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 ERR_INVALID_ARG, ERR_HIP, ERR_WORKSPACE, ERR_UNSUPPORTED = -1, -2, -3, -4
 
@@ -94,6 +94,7 @@ SIGNATURES = {
     "pemp_mpn_forward_fully_cap": (c_i32, [ctypes.POINTER(PempMpnDesc), ctypes.POINTER(PempMpnWeights), c_p, c_p,
                                            c_p, c_i64, c_i64, c_p, c_i32, c_p, c_i32, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "pemp_mpn_graph_stats": (c_i32, [c_p]),
+    "pemp_edge_cus_policy": (c_i32, [c_i32, c_i64, c_i32]),
     "pemp_mpn_forward_sym": (c_i32, [ctypes.POINTER(PempMpnDesc), ctypes.POINTER(PempMpnWeights), c_p, c_p, c_p,
                                      c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "pemp_mpn_forward_knn": (c_i32, [ctypes.POINTER(PempMpnDesc), ctypes.POINTER(PempMpnWeights), c_p, c_p, c_p,

@@ -16,6 +16,7 @@
 // Stage 2b (emit_kernel): one workgroup per plane. Offsets from the image's per-plane counts;
 //   emits detections in the reference's order.
 #include <math.h>
+#include <atomic>
 
 #include <type_traits>
 
@@ -1336,18 +1337,21 @@ static int launch_detect(const float* s, const float* masks, const DetectGeom& g
   // next). Checked once per device from the kernel's own occupancy; a device (partition) that cannot hold J takes
   // the two-kernel path, which has no inter-workgroup wait.
   auto fused_fits = [&]() {
-    static int cap_wg[64] = {0};
+    // (relaxed atomics: several host threads may launch detection at once; a race only recomputes the same value)
+    static std::atomic<int> cap_wg[64];
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) { (void)hipGetLastError(); return false; }
-    if (!cap_wg[dev]) {
+    int cap = cap_wg[dev].load(std::memory_order_relaxed);
+    if (!cap) {
       int occ = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, plane_emit_kernel<KMAX>, 256, 0) != hipSuccess) {
         (void)hipGetLastError();
         occ = 0;
       }
-      cap_wg[dev] = std::max(occ, 0) * num_cus() + 1;   // (+1: computed)
+      cap = std::max(occ, 0) * num_cus() + 1;   // (+1: computed)
+      cap_wg[dev].store(cap, std::memory_order_relaxed);
     }
-    return cap_wg[dev] - 1 >= g.J;
+    return cap - 1 >= g.J;
   };
   if ((stages & PEMP_DETECT_SELECT) && PEMP_DETECT_FUSED && g.units <= SEL_UNITS && fused_fits()) {
     if (!(stages & PEMP_DETECT_NMS)) PEMP_HIP(hipMemsetAsync(w.pflag, 0, sizeof(unsigned long long) * g.B * g.J, st));

@@ -53,14 +53,19 @@ constexpr int EDGE_WAVES = 16;   // waves per edge-pass / edge-embedding workgro
 #ifndef PEMP_EMBED_RESERVE
 #define PEMP_EMBED_RESERVE 1   // the edge embedding leaves the reserved CUs free too (0: it spreads over every CU)
 #endif
+// The reservation is capped at a quarter of the device (rounded down to a multiple of 8): 64 of the MI355X's 256
+// CUs, less on a smaller device or a compute partition, where a fixed 64 would take most of the chip.
+static int edge_cus_policy(int cus, int64_t E, int request) {
+  if (E < PEMP_RESERVE_MIN_EDGES || cus <= 8) return cus;
+  const int r = std::min(std::max(request, 0), cus / 4) & ~7;
+  return cus - r;
+}
 static int edge_cus(int64_t E) {
-  static const int reserved = [] {
+  static const int request = [] {
     const char* e = getenv("PEMP_RESERVE_CUS");
-    int r = e ? atoi(e) : PEMP_RESERVE_CUS_DEFAULT;
-    r = r < 0 ? 0 : (r & ~7);
-    return std::max(8, num_cus() - r);
+    return e ? atoi(e) : PEMP_RESERVE_CUS_DEFAULT;
   }();
-  return E >= PEMP_RESERVE_MIN_EDGES ? reserved : num_cus();
+  return edge_cus_policy(num_cus(), E, request);
 }
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -4393,6 +4398,15 @@ static int cap_forward_direct(const pemp_mpn_desc* desc, const pemp_mpn_weights*
 
 // Graph statistics for the tests (pemp_mpn_graph_stats): captures made, replays launched, captures refused.
 static std::atomic<uint64_t> g_graph_captures{0}, g_graph_replays{0}, g_graph_refused{0};
+
+extern "C" int pemp_edge_cus_policy(int num_cus_, int64_t E, int reserve_request) {
+  PEMP_CHECK_ARG(num_cus_ >= 1 && E >= 0, "pemp_edge_cus_policy: bad args");
+  if (reserve_request < 0) {
+    const char* e = getenv("PEMP_RESERVE_CUS");
+    reserve_request = e ? atoi(e) : PEMP_RESERVE_CUS_DEFAULT;
+  }
+  return edge_cus_policy(num_cus_, E, reserve_request);
+}
 
 extern "C" int pemp_mpn_graph_stats(uint64_t* out3) {
   PEMP_CHECK_ARG(out3, "pemp_mpn_graph_stats: null output");

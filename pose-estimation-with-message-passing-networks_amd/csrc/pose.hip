@@ -208,12 +208,33 @@ struct GaecEdge16 {
   bool operator<(const GaecEdge16& o) const { return w < o.w; }
 };
 
+// The n x n per-pair arrays of both GAEC forms: one per-thread arena (gaec_fast and its gaec_dense fallback run one
+// after the other on one thread, never together), reused across images and calls (fresh multi-100 KB blocks are
+// mmap'ed, and their page faults serialise threads that cluster in parallel). An image above GAEC_KEEP_N vertices
+// releases the arena afterwards, so one large image does not pin n^2 x 13 bytes per pool thread for the life of
+// the process (2048 vertices: 54 MB per thread).
+constexpr size_t GAEC_KEEP_N = 1024;
+struct GaecScratch {
+  std::vector<double> w;
+  std::vector<uint32_t> ed;
+  std::vector<uint8_t> ex;
+};
+GaecScratch& gaec_scratch() {
+  static thread_local GaecScratch s;
+  return s;
+}
+void gaec_release_if_large(size_t n) {
+  if (n <= GAEC_KEEP_N) return;
+  GaecScratch& s = gaec_scratch();
+  std::vector<double>().swap(s.w);
+  std::vector<uint32_t>().swap(s.ed);
+  std::vector<uint8_t>().swap(s.ex);
+}
+
 void gaec_dense(size_t n, const EdgeList& el, std::vector<size_t>& root) {
-  // per-thread buffers, reused across images and calls (fresh multi-100 KB blocks are mmap'ed, and their page
-  // faults serialise threads that cluster in parallel)
-  static thread_local std::vector<double> wt;
-  static thread_local std::vector<uint32_t> ed;
-  static thread_local std::vector<uint8_t> ex;
+  std::vector<double>& wt = gaec_scratch().w;
+  std::vector<uint32_t>& ed = gaec_scratch().ed;
+  std::vector<uint8_t>& ex = gaec_scratch().ex;
   static thread_local std::vector<uint32_t> deg;
   static thread_local std::vector<GaecEdge16> qstore;
   wt.assign(n * n, 0.0);
@@ -308,13 +329,13 @@ bool gaec_fast(size_t n, const EdgeList& el, std::vector<size_t>& root) {
   // fill the rows in order. A merged vertex is only marked dead (its pairs are never read again: the walks visit
   // the alive vertices, a popped entry with a dead end is stale). Within one contraction every pair is updated
   // once, so the order of the walk does not change any weight (the same double additions).
-  static thread_local std::vector<double> W;
-  static thread_local std::vector<uint32_t> ED;
+  std::vector<double>& W = gaec_scratch().w;
+  std::vector<uint32_t>& ED = gaec_scratch().ed;
   static thread_local std::vector<uint32_t> deg;
   static thread_local std::vector<uint8_t> alive;
   static thread_local std::vector<uint32_t> live;   // the alive vertices, ascending
   static thread_local std::vector<GaecEdge16> qstore;
-  if (W.size() < n * n) {
+  if (W.size() < n * n || ED.size() < n * n) {
     W.resize(n * n);
     ED.resize(n * n);
   }
@@ -422,13 +443,19 @@ class HostPool {
       next_.store(0);
       active_ = threads - 1;
       running_.store(threads - 1);
+      // adaptive spin (below): the workers spin after this call only if it came within the spin window of the
+      // previous one, i.e. while calls arrive back to back (a serving loop); an occasional caller wakes them
+      // through the condition variable and leaves no thread spinning between its calls
+      const uint64_t t = now_ns();
+      hot_.store(last_call_ns_ != 0 && t - last_call_ns_ < spin_ns(), std::memory_order_relaxed);
+      last_call_ns_ = t;
       gen_.fetch_add(1, std::memory_order_release);
     }
     cv_.notify_all();
     drain(fn);
-    // the caller's share is done: wait for the workers' tasks (spinning first; they are short)
+    // the caller's share is done: wait for the workers' tasks (spinning first, briefly; they are short)
     for (int spin = 0; running_.load(std::memory_order_acquire) != 0; ++spin) {
-      if (spin < 20000) {
+      if (spin < 4000) {
         __builtin_ia32_pause();
       } else {
         std::unique_lock<std::mutex> lk(mu_);
@@ -443,9 +470,12 @@ class HostPool {
   void drain(const std::function<void(int)>& fn) {
     for (int i = next_.fetch_add(1); i < tasks_; i = next_.fetch_add(1)) fn(i);
   }
-  // A worker spins on the generation counter for a while after its last task before it sleeps on the condition
+  // A worker may spin on the generation counter for a while after its last task before it sleeps on the condition
   // variable: a condition-variable wake-up measured 1-4 ms on some hosts (the per-image tasks are 0.1-1 ms), and a
-  // serving loop calls again within a few ms. PEMP_POOL_SPIN_US (default 2000) sets the window, 0 disables it.
+  // serving loop calls again within a few ms. Only while calls arrive within the window of each other (hot_), and
+  // only the first PEMP_POOL_SPIN_WORKERS workers (default 4): the rest sleep at once, so several ranks or
+  // processes on one host do not each keep 15 threads spinning. PEMP_POOL_SPIN_US (default 2000) sets the window,
+  // 0 disables spinning.
   static uint64_t spin_ns() {
     static const uint64_t v = [] {
       const char* e = getenv("PEMP_POOL_SPIN_US");
@@ -453,11 +483,19 @@ class HostPool {
     }();
     return v;
   }
+  static int spin_workers() {
+    static const int v = [] {
+      const char* e = getenv("PEMP_POOL_SPIN_WORKERS");
+      return e ? std::max(0, atoi(e)) : 4;
+    }();
+    return v;
+  }
   void loop(int id) {
     uint64_t seen = 0;
     for (;;) {
       const uint64_t t_idle = now_ns();
-      while (gen_.load(std::memory_order_acquire) == seen && now_ns() - t_idle < spin_ns())
+      const uint64_t window = (id < spin_workers() && hot_.load(std::memory_order_relaxed)) ? spin_ns() : 0;
+      while (gen_.load(std::memory_order_acquire) == seen && now_ns() - t_idle < window)
         for (int k = 0; k < 64; ++k) __builtin_ia32_pause();
       const std::function<void(int)>* fn;
       {
@@ -485,6 +523,8 @@ class HostPool {
   std::atomic<int> next_{0};
   std::atomic<int> running_{0};
   std::atomic<uint64_t> gen_{0};
+  std::atomic<bool> hot_{false};
+  uint64_t last_call_ns_ = 0;   // (under mu_)
   int tasks_ = 0, active_ = 0;
 };
 
@@ -598,6 +638,7 @@ extern "C" int pemp_pose_cluster(int B, const int64_t* node_off, const int64_t* 
     if (method == 0) {
       if (n <= dense_max) {
         if (exact_only || !gaec_fast(n, el, root)) gaec_dense(n, el, root);
+        gaec_release_if_large(n);
       } else {
         gaec(n, el, root);
       }
@@ -1135,7 +1176,7 @@ extern "C" int pemp_pack_to_host(int n, const void* const* src, const size_t* by
   PEMP_CHECK_ARG(n >= 0 && n <= PACK_MAX && (n == 0 || (src && bytes && off)), "pemp_pack_to_host: bad args (n <= %d)",
                  PACK_MAX);
   if (total == 0) return PEMP_OK;
-  PEMP_CHECK_ARG(staging && host_dst, "pemp_pack_to_host: null buffer");
+  PEMP_CHECK_ARG(staging, "pemp_pack_to_host: null staging buffer");
   PackArgs a{};
   uint64_t most = 0;
   for (int i = 0; i < n; ++i) {
@@ -1154,7 +1195,9 @@ extern "C" int pemp_pack_to_host(int n, const void* const* src, const size_t* by
     hipLaunchKernelGGL(pack_kernel, dim3(gx, n), dim3(256), 0, st, a);
     PEMP_LAUNCH_CHECK();
   }
-  PEMP_HIP(hipMemcpyAsync(host_dst, staging, total, hipMemcpyDeviceToHost, st));
+  // host_dst NULL: gather only (the caller copies staging itself, e.g. with torch, whose pinned-memory cache then
+  // records the copy's event before the block can be reused)
+  if (host_dst) PEMP_HIP(hipMemcpyAsync(host_dst, staging, total, hipMemcpyDeviceToHost, st));
   return PEMP_OK;
 }
 

@@ -8,6 +8,7 @@ pose grouping the one pose all-gather of §8(e) (``gather_poses``).
 """
 import os
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -70,46 +71,77 @@ def sum_over_ranks(v, world, dev):
     return _reduce(v, world, dev, dist.ReduceOp.SUM)
 
 
-def gather_poses(per_image, image_ids, num_joints, world, dev):
-    """after each rank has grouped its own image block, one all_gather hands every rank the
+# DATASET.MAX_NUM_PEOPLE (/root/reference/src/config/default_config.py:175): the fixed person capacity of one
+# image's pose record, so that every rank knows the record size without a collective of its own
+MAX_NUM_PEOPLE = 30
+_META = 4   # record header: image id, person count (-1: None), valid flag, spare (all exact in float64)
+
+
+def _pack_records(per_image, image_ids, n_max, cap, num_joints, skip=0):
+    """[n_max, _META + cap*J*3] float64: per image the header and persons skip .. skip+cap-1 of its poses."""
+    stride = cap * num_joints * 3
+    rec = torch.zeros(n_max, _META + stride, dtype=torch.float64)
+    rec[:, 1] = -1
+    for k, (p, iid) in enumerate(zip(per_image, image_ids)):
+        rec[k, 0] = int(iid)
+        rec[k, 2] = 1
+        if p is not None:
+            rec[k, 1] = p.shape[0]
+            part = p[skip:skip + cap]
+            if part.shape[0]:
+                rec[k, _META:_META + part.size] = torch.from_numpy(np.ascontiguousarray(part, dtype=np.float64)).reshape(-1)
+    return rec
+
+
+def _all_gather_records(rec, world, dev):
+    out = torch.empty((world * rec.shape[0], rec.shape[1]), dtype=rec.dtype, device=dev)
+    dist.all_gather_into_tensor(out, rec.to(dev))
+    return out.cpu().numpy().reshape(world, rec.shape[0], rec.shape[1])
+
+
+def gather_poses(per_image, image_ids, num_joints, world, dev, total_images=None, max_people=MAX_NUM_PEOPLE):
+    """after each rank has grouped its own image block, ONE all_gather hands every rank the
     poses of the whole batch, in global image order (rank order of the contiguous blocks).
 
     per_image: this rank's list of float64 [P, J, 3] arrays or None (``pred_to_ann``'s "no poses");
-    image_ids: this rank's int image ids, same length. Returns (ids, poses) over all ranks. Records are
-    fixed-size ([cap, J, 3] f64 + person count + image id, cap = the largest P over all ranks, found by one
-    MAX all-reduce), blocks padded to the largest block; float64 keeps every value exact."""
+    image_ids: this rank's int image ids, same length. Returns (ids, poses) over all ranks.
+
+    Each image is one fixed-size float64 record packed into a single tensor: header (image id, person count,
+    valid) + [max_people, J, 3] poses, max_people = DATASET.MAX_NUM_PEOPLE = 30. Every rank derives the block
+    size from ``total_images`` (the ``image_block`` partition: ceil(total / world) records per rank, shorter
+    blocks padded with invalid records); without it every rank must hold the same number of images. So the
+    common case is exactly one collective, no size agreement first. An image with more than max_people
+    persons (the grouping caps nothing) is still exact: every rank sees the counts after the first gather and
+    the rare overflow persons travel in one more all_gather of the same form. float64 keeps every value exact."""
     n_local = len(per_image)
     if len(image_ids) != n_local:
         raise ValueError("gather_poses: per_image and image_ids differ in length")
     if world == 1:
         return list(image_ids), list(per_image)
-    p_local = max([0] + [0 if p is None else int(p.shape[0]) for p in per_image])
+    n_max = max(1, -(-int(total_images) // world)) if total_images is not None else max(1, n_local)
+    if n_local > n_max:
+        raise ValueError(f"gather_poses: {n_local} images on this rank, block size {n_max}")
+    cap = max(1, int(max_people))
     dev = _coll_dev(dev)
-    t = torch.tensor([p_local, n_local], dtype=torch.int64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    cap, n_max = max(1, int(t[0])), max(1, int(t[1]))
-    rec = torch.zeros(n_max, cap, num_joints, 3, dtype=torch.float64)
-    meta = torch.full((n_max, 3), -1, dtype=torch.int64)   # (image id, person count or -1 for None, valid)
-    meta[:, 2] = 0
-    for k, (p, iid) in enumerate(zip(per_image, image_ids)):
-        meta[k, 0] = int(iid)
-        meta[k, 2] = 1
-        if p is not None:
-            rec[k, :p.shape[0]] = torch.from_numpy(p)
-            meta[k, 1] = p.shape[0]
-    rec, meta = rec.to(dev), meta.to(dev)
-    all_rec = torch.empty((world * n_max,) + tuple(rec.shape[1:]), dtype=rec.dtype, device=dev)
-    all_meta = torch.empty((world * n_max, 3), dtype=meta.dtype, device=dev)
-    dist.all_gather_into_tensor(all_rec, rec)
-    dist.all_gather_into_tensor(all_meta, meta)
-    all_rec = all_rec.cpu().numpy().reshape((world, n_max) + tuple(rec.shape[1:]))
-    all_meta = all_meta.cpu().numpy().reshape(world, n_max, 3)
+    allr = _all_gather_records(_pack_records(per_image, image_ids, n_max, cap, num_joints), world, dev)
+    counts = allr[:, :, 1].astype(np.int64)
+    over = int(max(0, counts.max() - cap))
+    extra = None
+    if over:   # (all ranks take this branch together: they all hold the same counts)
+        extra = _all_gather_records(_pack_records(per_image, image_ids, n_max, over, num_joints, skip=cap),
+                                    world, dev)
     ids, poses = [], []
     for r in range(world):
         for k in range(n_max):
-            iid, cnt, valid = all_meta[r, k]
-            if not valid:
+            if not allr[r, k, 2]:
                 continue
-            ids.append(int(iid))
-            poses.append(None if cnt < 0 else all_rec[r, k, :cnt].copy())
+            ids.append(int(allr[r, k, 0]))
+            cnt = int(counts[r, k])
+            if cnt < 0:
+                poses.append(None)
+                continue
+            p = allr[r, k, _META:].reshape(cap, num_joints, 3)[:min(cnt, cap)]
+            if cnt > cap:
+                p = np.concatenate([p, extra[r, k, _META:].reshape(over, num_joints, 3)[:cnt - cap]])
+            poses.append(p.copy())
     return ids, poses

@@ -43,7 +43,7 @@ _NP = {torch.int64: np.int64, torch.int32: np.int32, torch.float32: np.float32, 
 
 def _to_host_async(tensors, dev):
     """Stream-ordered read-back of device tensors (contiguous; None entries stay None) into one pinned host
-    buffer: one pemp_pack_to_host call gathers them into a device staging buffer and queues one copy, behind
+    buffer: one pemp_pack_to_host call gathers them into a device staging buffer and one torch copy follows, behind
     the work that produces them on the current stream of `dev`, then an event is recorded. Returns numpy views
     of the host buffer (valid once the event has completed), the event, and the buffer (keep it alive)."""
     L = _lib.lib()
@@ -61,8 +61,11 @@ def _to_host_async(tensors, dev):
         src = (ctypes.c_void_p * max(n, 1))(*[t.data_ptr() for t in live])
         nb = (ctypes.c_size_t * max(n, 1))(*[t.numel() * t.element_size() for t in live])
         of = (ctypes.c_size_t * max(n, 1))(*offs)
-        _lib.check(L.pemp_pack_to_host(n, src, nb, of, total, staging.data_ptr(), host.data_ptr(), _lib.stream(dev)),
-                   L)
+        # the library gathers into the staging buffer; the device-to-host copy goes through torch so that its
+        # pinned-memory cache records the copy's event: a job dropped before its copy lands cannot hand the block
+        # to a new allocation while the DMA still writes it
+        _lib.check(L.pemp_pack_to_host(n, src, nb, of, total, staging.data_ptr(), None, _lib.stream(dev)), L)
+        host.copy_(staging, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(dev))
     hv = host.numpy()

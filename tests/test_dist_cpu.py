@@ -82,10 +82,11 @@ def test_gloo_world2_shards_reassemble(tmp_path):
     assert all(p["n_sum"] == full[0].shape[0] for p in parts)
 
 
-def _poses_for(img):
-    """Deterministic per-image pose arrays (None for some images, varying person counts)."""
+def _poses_for(img, crowded=False):
+    """Deterministic per-image pose arrays (None for some images, varying person counts; ``crowded``: image 3
+    holds more persons than MAX_NUM_PEOPLE, the record capacity)."""
     rng = np.random.default_rng(img)
-    n = int(rng.integers(0, 5))
+    n = int(rng.integers(0, 5)) if not (crowded and img == 3) else pdist.MAX_NUM_PEOPLE + 7
     if n == 0:
         return None
     kp = rng.integers(0, 640, size=(n, J, 3)).astype(np.float64) + 0.25
@@ -94,28 +95,37 @@ def _poses_for(img):
     return kp
 
 
-def _pose_worker(rank, world, port, out_dir, total):
+def _pose_worker(rank, world, port, out_dir, total, crowded):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     r, w, dev = pdist.init_from_env("gloo")
     s, e = pdist.image_block(total, r, w)
-    ids, poses = pdist.gather_poses([_poses_for(i) for i in range(s, e)], [1000 + i for i in range(s, e)], J, w, dev)
-    np.savez(os.path.join(out_dir, f"p{r}.npz"), ids=np.array(ids),
+    # count every collective gather_poses issues (one all_gather, nothing to agree a size first)
+    calls = []
+    for name in ("all_gather_into_tensor", "all_gather", "all_reduce", "broadcast", "all_to_all_single"):
+        orig = getattr(torch.distributed, name)
+        setattr(torch.distributed, name, (lambda f, n: (lambda *a, **k: (calls.append(n), f(*a, **k))[1]))(orig, name))
+    ids, poses = pdist.gather_poses([_poses_for(i, crowded) for i in range(s, e)], [1000 + i for i in range(s, e)],
+                                    J, w, dev, total_images=total)
+    np.savez(os.path.join(out_dir, f"p{r}.npz"), ids=np.array(ids), calls=np.array(calls),
              counts=np.array([-1 if p is None else len(p) for p in poses]),
              flat=np.concatenate([p.reshape(-1) for p in poses if p is not None] or [np.zeros(0)]))
     torch.distributed.destroy_process_group()
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("total", [5, 4])
-def test_gloo_world2_gather_poses(tmp_path, total):
-    """The §8(e) pose all-gather: every rank ends with every image's poses, in global order, exact."""
+@pytest.mark.parametrize("total,crowded", [(5, False), (4, False), (5, True)])
+def test_gloo_world2_gather_poses(tmp_path, total, crowded):
+    """The §8(e) pose all-gather: every rank ends with every image's poses, in global order, exact, through
+    exactly one all_gather of fixed [MAX_NUM_PEOPLE x J x 3] records (a second one only for an image with
+    more persons than that: the crowded case)."""
     world = 2
-    mp.start_processes(_pose_worker, args=(world, _free_port(), str(tmp_path), total), nprocs=world, join=True,
-                       start_method="spawn")
-    ref = [_poses_for(i) for i in range(total)]
+    mp.start_processes(_pose_worker, args=(world, _free_port(), str(tmp_path), total, crowded), nprocs=world,
+                       join=True, start_method="spawn")
+    ref = [_poses_for(i, crowded) for i in range(total)]
     for r in range(world):
         z = np.load(tmp_path / f"p{r}.npz")
+        assert z["calls"].tolist() == ["all_gather_into_tensor"] * (2 if crowded else 1)
         assert z["ids"].tolist() == [1000 + i for i in range(total)]
         assert z["counts"].tolist() == [-1 if p is None else len(p) for p in ref]
         flat = np.concatenate([p.reshape(-1) for p in ref if p is not None] or [np.zeros(0)])

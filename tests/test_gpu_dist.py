@@ -66,7 +66,7 @@ def _worker(rank, world, port, out_dir):
     hm, feats, tags = _inputs(dev)
     s, e = pdist.image_block(B, r, w)
     graph, logits, per_image = _path(hm[s:e], feats[s:e], tags[s:e], dev)
-    ids, poses = pdist.gather_poses(per_image, list(range(s, e)), J, w, dev)
+    ids, poses = pdist.gather_poses(per_image, list(range(s, e)), J, w, dev, total_images=B)
     torch.save({"graph": graph, "logits": logits, "start": s, "ids": ids,
                 "local": [None if p is None else torch.from_numpy(np.asarray(p)) for p in per_image],
                 "poses": [None if p is None else torch.from_numpy(np.asarray(p)) for p in poses]},

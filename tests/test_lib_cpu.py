@@ -51,3 +51,23 @@ def test_knn_rows_layout_is_host_only():
         assert offs[0] % 256 == 0 and offs[1] % 256 == 0 and offs[2] % 256 == 0
     nh = np.array([0, 513], np.int64)
     assert L.pemp_knn_rows_layout(nh.ctypes.data_as(ctypes.c_void_p), 1, 0, offs) != 0
+
+
+def test_edge_cu_reservation_is_a_bounded_share():
+    """The edge passes' CU reservation (mpn.hip edge_cus): small graphs keep every CU; large ones leave at most a
+    quarter of the device free (a multiple of 8), whatever is asked, so a small device or a compute partition keeps
+    at least 3/4 of its CUs for the forward (a fixed 64 would take most of such a device)."""
+    L = _lib.load_cdll()
+    pol = L.pemp_edge_cus_policy
+    assert pol(256, 186_048, 64) == 192          # MI355X, c3: 64 reserved (the measured default)
+    assert pol(256, 22_350, 64) == 256           # batch 1: every CU
+    assert pol(256, 186_048, 0) == 256
+    assert pol(256, 186_048, 200) == 192         # capped at a quarter
+    for cus in (8, 16, 38, 40, 64, 80, 120, 152, 228, 256, 304):
+        for E in (0, 65_535, 65_536, 250_000, 10**8):
+            for req in (0, 7, 8, 64, 96, 10**6):
+                n = pol(cus, E, req)
+                assert 0.75 * cus <= n <= cus and (cus - n) % 8 == 0, (cus, E, req, n)
+                if E < 65_536:
+                    assert n == cus
+    assert pol(0, 1000, 64) < 0 and pol(256, -1, 64) < 0

@@ -35,9 +35,8 @@ def main(paths):
             for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
                 if c in d:
                     print(f"  {c + ' / WAVE_CYCLES':40s} {d[c] / w:.3f}")
-        if "SQ_VALU_MFMA_BUSY_CYCLES" in d and "SQ_BUSY_CYCLES" in d and d["SQ_BUSY_CYCLES"]:
-            print(f"  MFMA_BUSY / (BUSY_CYCLES*4 SIMD)  {d['SQ_VALU_MFMA_BUSY_CYCLES'] / (4 * d['SQ_BUSY_CYCLES']):.3f}"
-                  "  (rough; BUSY_CYCLES summed over SEs)")
+        # (MFMA utilisation: tools/mfma_util.py, from SQ_VALU_MFMA_BUSY_CYCLES and GRBM_GUI_ACTIVE; the former
+        # MFMA_BUSY / (BUSY_CYCLES x 4) ratio here was not a utilisation and read above 1)
 
 
 if __name__ == "__main__":
