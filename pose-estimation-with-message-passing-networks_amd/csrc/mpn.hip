@@ -1445,39 +1445,24 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
-// ---- the same scans in hand-placed DPP instructions (PEMP_ASM_SCANS, the default) ----
-// hipcc turns the per-value `fmaf(dpp(v), mask, v)` of seg_sum into a v_mov_b32_dpp per value and a
-// v_pk_fma_f32 per pair (3 instructions per 2 values and step), and every fmaxf of seg_max into a
-// mov_dpp + cndmask + canonicalising max + max. Here: one v_fmac_f32_dpp per value and step (the DPP source
-// reads 0 outside the row, where the mask is 0 anyway), and for the max one v_max_f32_dpp (source lane
-// outside the row: not written) + one v_cndmask on a lane mask per step. The 17 sums go step by step, so
-// every DPP read is 17 instructions behind the write of its source (the 2 VALU-write -> DPP-read wait states
-// are only needed at entry, s_nop 1); the max chain is serial, with an s_nop 1 per step.
-// hipcc inserts no hazard wait states in front of inline asm: an asm block that reads an MFMA result (or writes
-// a register an MFMA still reads) right after the MFMA would see the stale value. Every block below therefore
-// opens with the longest XDL -> VALU distance (19 wait states: a 16-pass MFMA) before its first VALU instruction.
+// ---- the segmented max in hand-placed DPP instructions (PEMP_ASM_SCANS, the default) ----
+// hipcc turns every fmaxf of seg_max into a mov_dpp + cndmask + canonicalising max + max. Here: one v_max_f32_dpp
+// (source lane outside the row: not written) + one v_cndmask on a lane mask per step; the chain is serial, with an
+// s_nop 1 per step. hipcc inserts no hazard wait states in front of inline asm: an asm block that reads an MFMA result
+// (or writes a register an MFMA still reads) right after the MFMA would see the stale value. The block therefore opens
+// with the longest XDL -> VALU distance (19 wait states: a 16-pass MFMA) before its first VALU instruction ...
 #define PEMP_XDL_GUARD "s_nop 7\n\ts_nop 7\n\ts_nop 4\n\t"
 // ... and closes with the 2 VALU-write -> DPP-read wait states: the compiler does not see the asm's last writes
-// either, and its next DPP read of one of them (the carry's row shifts) would otherwise read the stale value
-#ifdef PEMP_ASM_TAILPAD   // diagnostics: a long pad after the asm blocks
-#define PEMP_DPP_TAIL "s_nop 7\n\ts_nop 7\n\ts_nop 7\n\t"
-#else
+// either, and its next DPP read of one of them would otherwise read the stale value
 #define PEMP_DPP_TAIL "s_nop 1\n\t"
-#endif
-#ifdef PEMP_ASM_VOLATILE
-#define PEMP_SCAN_ASM asm volatile
-#else
-#define PEMP_SCAN_ASM asm
-#endif
 #ifndef PEMP_ASM_SCANS
 #define PEMP_ASM_SCANS 1
 #endif
-#ifndef PEMP_ASM_ALL   // diagnostics: the asm sums in every non-max instantiation
-#define PEMP_ASM_ALL 0
-#endif
-#ifdef PEMP_ASM_CHECK
-__device__ unsigned g_asm_check_count = 0;
-#endif
+// (Round 6: the 17 segmented SUMS no longer have an asm form. Through round 5 a hand-placed v_fmac_f32_dpp block
+// (seg_sum17_asm) summed them in the f16x3 attention passes. It computed the same bits as the compiler's scans on every
+// lane, yet any instantiation that carried it outside that path (bf16x3) became timing-dependent across forwards, the
+// same with the DPP moved onto a v_mov_b32 and a plain fmac, and no cause was found. In the default
+// path it was worth <= 1 % of an edge pass (profiles/r06_asm_sums.md), so it was removed: no instantiation carries it.)
 struct ChunkMasks {
   uint64_t f1, f2, f4, f8, b1, b2, b4, b8;   // lanes with d >= k (forward steps) / u >= k (backward steps)
 };
@@ -1504,23 +1489,6 @@ __device__ __forceinline__ float chunk_max_asm(float v, const ChunkMasks& mk) {
   return v;
 }
 
-// segmented inclusive sums of the 16 fragment values and the normaliser l (m: ScanMask, 1.0 where d >= k)
-#define PEMP_FMAC1(i, ctl, m) "v_fmac_f32_dpp %" #i ", %" #i ", %" #m " " ctl " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-#define PEMP_FMAC17(ctl, m)                                                                                       \
-  PEMP_FMAC1(0, ctl, m) PEMP_FMAC1(1, ctl, m) PEMP_FMAC1(2, ctl, m) PEMP_FMAC1(3, ctl, m) PEMP_FMAC1(4, ctl, m) \
-  PEMP_FMAC1(5, ctl, m) PEMP_FMAC1(6, ctl, m) PEMP_FMAC1(7, ctl, m) PEMP_FMAC1(8, ctl, m) PEMP_FMAC1(9, ctl, m) \
-  PEMP_FMAC1(10, ctl, m) PEMP_FMAC1(11, ctl, m) PEMP_FMAC1(12, ctl, m) PEMP_FMAC1(13, ctl, m)                   \
-  PEMP_FMAC1(14, ctl, m) PEMP_FMAC1(15, ctl, m) PEMP_FMAC1(16, ctl, m)
-__device__ __forceinline__ void seg_sum17_asm(float (&v)[4][4], float& l, const ScanMask& m) {
-  PEMP_SCAN_ASM(PEMP_XDL_GUARD PEMP_FMAC17("row_shr:1", 17) PEMP_FMAC17("row_shr:2", 18) PEMP_FMAC17("row_shr:4", 19)
-          PEMP_FMAC17("row_shr:8", 20) PEMP_DPP_TAIL
-      : "+v"(v[0][0]), "+v"(v[0][1]), "+v"(v[0][2]), "+v"(v[0][3]), "+v"(v[1][0]), "+v"(v[1][1]), "+v"(v[1][2]),
-        "+v"(v[1][3]), "+v"(v[2][0]), "+v"(v[2][1]), "+v"(v[2][2]), "+v"(v[2][3]), "+v"(v[3][0]), "+v"(v[3][1]),
-        "+v"(v[3][2]), "+v"(v[3][3]), "+v"(l)
-      : "v"(m.m1), "v"(m.m2), "v"(m.m4), "v"(m.m8));
-}
-#undef PEMP_FMAC17
-#undef PEMP_FMAC1
 
 
 // ---- edge-pass weight image --------------------------------------------------------------------
@@ -2104,58 +2072,7 @@ __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_
       }
     }
     const ScanMask smk = scan_mask(ck.d);
-    // (the hand-placed sums only where the attention weight is folded into the update split, PE_FOLD: with the
-    // weight multiplied in separately -- the bf16x3 / fp32 kernels -- they gave wrong aggregates on the GPU
-    // (bf16x3 logits 1e-3 off), for a reason not found; those kernels keep the compiler's scans)
-    if (PEMP_ASM_SCANS && (PE_FOLD || (PEMP_ASM_ALL && AGG != PEMP_AGGR_MAX))) {
-#ifdef PEMP_ASM_OPAQUE_IN   // diagnostics: the scan inputs pinned in registers by an empty volatile statement
-#pragma unroll
-      for (int ob = 0; ob < 4; ++ob)
-        asm volatile("" : "+v"(v[ob][0]), "+v"(v[ob][1]), "+v"(v[ob][2]), "+v"(v[ob][3]));
-      asm volatile("" : "+v"(l));
-#endif
-#ifdef PEMP_ASM_CHECK   // diagnostics: the asm sums against the compiler's on the same inputs, first mismatches printed
-      float vin[4][4], vc[4][4], lin = l, lc = l;
-#pragma unroll
-      for (int ob = 0; ob < 4; ++ob)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) vin[ob][r] = vc[ob][r] = v[ob][r];
-#endif
-      seg_sum17_asm(v, l, smk);                  // the 64 features and the normaliser / count
-#ifdef PEMP_ASM_CHECK
-      lc = seg_sum(lc, smk);
-      int bad = __float_as_uint(lc) != __float_as_uint(l) ? 16 : -1;
-#pragma unroll
-      for (int ob = 0; ob < 4; ++ob)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          vc[ob][r] = seg_sum(vc[ob][r], smk);
-          if (bad < 0 && __float_as_uint(vc[ob][r]) != __float_as_uint(v[ob][r])) bad = 4 * ob + r;
-        }
-#ifdef PEMP_ASM_USE_COMPILER   // the asm runs, its results are dropped for the compiler's
-      l = lc;
-#pragma unroll
-      for (int ob = 0; ob < 4; ++ob)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[ob][r] = vc[ob][r];
-#endif
-#ifdef PEMP_ASM_POISON         // a mismatch poisons the lane's aggregate (visible in the logits)
-      if (bad >= 0) l = __int_as_float(0x7fc00000);
-#endif
-      if (bad >= 0) {
-        const unsigned k = atomicAdd(&g_asm_check_count, 1u);
-        if (k < 24) {
-          float a_ = l, c_ = lc, i_ = lin;
-#pragma unroll
-          for (int q = 0; q < 16; ++q)
-            if (q == bad) { a_ = v[q >> 2][q & 3]; c_ = vc[q >> 2][q & 3]; i_ = vin[q >> 2][q & 3]; }
-          printf("ASMCHK blk %d wave %d lane %d val %d d %d in %a asm %a cmp %a m %g %g %g %g exec %llx\n",
-                 (int)blockIdx.x, wave, lane, bad, ck.d, i_, a_, c_, smk.m1, smk.m2, smk.m4, smk.m8,
-                 (unsigned long long)__builtin_amdgcn_read_exec());
-        }
-      }
-#endif
-    } else {
+    {
       if (AGG == PEMP_AGGR_ATTN || AGG == PEMP_AGGR_MEAN) l = seg_sum(l, smk);   // normaliser / count
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob)
