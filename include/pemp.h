@@ -418,6 +418,13 @@ typedef struct pemp_mpn_weights {
   const float *ept_l1_w, *ept_l1_b, *ept_l2_w, *ept_l2_b, *ept_o1_w, *ept_o2_w;
   const float* edge_img;   /* edge-pass weight image (pemp_mpn_edge_image for the same desc), or NULL: then every
                               forward builds it in its workspace */
+  /* The edge embedding composed with the first edge-MLP layer (PEMP_PREC_F16X3 and the published embedding shape
+   * A -> 32 -> 64 -> 64 -> 64, ReLU after all but the last layer), or NULL. The last embedding Linear (W4, b4) has no
+   * ReLU, so with h3 the third layer's output: Q0 = Wq h3 + bq, Wq = q0_w W4, bq = q0_w b4 + q0_b, and
+   * R0 = Wr h3 + br, Wr = (q0_w + e1_w) W4, br = (q0_w + e1_w) b4 + q0_b, formed by the caller in fp64.
+   * emb_comp_bf: [2 (Wq, Wr)][2][64][64] f16x3 packs (as e1_bf); emb_comp_b: [2][64] (bq, br). */
+  const uint16_t* emb_comp_bf;
+  const float* emb_comp_b;
 } pemp_mpn_weights;
 
 typedef struct pemp_mpn_desc {
@@ -487,6 +494,10 @@ int pemp_mpn_graph_stats(uint64_t* out3);
  * (reserve_request < 0: the library's setting, PEMP_RESERVE_CUS or 64). Graphs below 65,536 edges keep every CU;
  * above, at most a quarter of the device is reserved (rounded down to a multiple of 8). */
 int pemp_edge_cus_policy(int num_cus, int64_t E, int reserve_request);
+
+/* sizeof of the ABI structs as this library was built (host only; bindings check their mirrors against it):
+ * which = 0 pemp_mpn_weights, 1 pemp_mpn_desc, 2 pemp_mlp, 3 pemp_proj_maps; 0 for any other value. */
+size_t pemp_abi_struct_size(int which);
 
 /* pemp_mpn_forward for an edge_index sorted by (src, dst) without duplicates and symmetric (every s -> d has
  * its d -> s: PyG to_undirected's coalesced output, as knn_mpn_graph / feature_knn_mpn_graph / score_based_graph

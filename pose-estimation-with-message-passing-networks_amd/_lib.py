@@ -34,7 +34,7 @@ class PempMpnWeights(ctypes.Structure):
                 ("upd_bf", c_p), ("pre_bf", c_p), ("node_img", c_p), ("attn_bv", c_p),
                 ("upd_mlp", PempMlp),
                 ("ept_l1_w", c_p), ("ept_l1_b", c_p), ("ept_l2_w", c_p), ("ept_l2_b", c_p), ("ept_o1_w", c_p),
-                ("ept_o2_w", c_p), ("edge_img", c_p)]
+                ("ept_o2_w", c_p), ("edge_img", c_p), ("emb_comp_bf", c_p), ("emb_comp_b", c_p)]
 
 
 class PempProjMaps(ctypes.Structure):
@@ -95,6 +95,7 @@ SIGNATURES = {
                                            c_p, c_i64, c_i64, c_p, c_i32, c_p, c_i32, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "pemp_mpn_graph_stats": (c_i32, [c_p]),
     "pemp_edge_cus_policy": (c_i32, [c_i32, c_i64, c_i32]),
+    "pemp_abi_struct_size": (c_sz, [c_i32]),
     "pemp_mpn_forward_sym": (c_i32, [ctypes.POINTER(PempMpnDesc), ctypes.POINTER(PempMpnWeights), c_p, c_p, c_p,
                                      c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "pemp_mpn_forward_knn": (c_i32, [ctypes.POINTER(PempMpnDesc), ctypes.POINTER(PempMpnWeights), c_p, c_p, c_p,

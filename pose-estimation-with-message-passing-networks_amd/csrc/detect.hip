@@ -560,12 +560,9 @@ __global__ __launch_bounds__(NT1) void nms_strips_kernel(
     nnbits &= vmask;
     if (!use_thr) tbits = 0;
     cbits[(size_t)u * 64 + lane] = (cmask_t)tbits;
-    int cnt = __popc(tbits), nonneg = __popc(nnbits);
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      cnt += __shfl_xor(cnt, off);
-      nonneg += __shfl_xor(nonneg, off);
-    }
+    // both counts (<= 16 x 64 each) in one word, summed over the wave without the LDS pipe
+    const int both = wave_sum_i32((__popc(tbits) << 16) | __popc(nnbits));
+    const int cnt = both >> 16, nonneg = both & 0xffff;
     const bool anypos = __ballot(lane_ok && pmax > 0.0f) != 0;
     if (lane == 0) { tile_count[u] = cnt; tile_nonneg[u] = nonneg; }
     const int base_id = y0 * W + x;

@@ -639,8 +639,7 @@ __device__ __forceinline__ bool f16_big(const float (&x)[4][4], float s) {
 // already in range, so an item's precision never depends on the other items of the wave. m = item max
 // (partial: this lane's values; the cross-lane max is taken here).
 __device__ __forceinline__ float f16_item_scale(float m, float s) {
-  m = fmaxf(m, __shfl_xor(m, 16));
-  m = fmaxf(m, __shfl_xor(m, 32));
+  m = xmax_rows(m);
   m *= s;
   if (m < F16_BIG) return 1.0f;
   if (!(m <= 3.4028235e38f)) return F16_DOWN;      // inf / NaN: any scale (the result is not finite anyway)
@@ -1138,10 +1137,20 @@ __device__ __forceinline__ void layer_h3(const float* smz, const EmbedLayout& Lo
   else layer_h3_body<KB32, OB, RELU, NONNEG, false>(W, Lo.stride[l], bias, hh, lh, 1.0f, out);
 }
 
-template <int PREC>
+template <int PREC, bool COMP = false>
 __device__ __forceinline__ void embed_tile_fixed(const float* smz, const EmbedLayout& Lo, float (&x)[4][4],
                                                  float (&y)[4][4], Frag<PREC>& fx) {
-  if constexpr (PREC == 2) {   // every activation in the 2^11 domain (edge_attr in: true values)
+  if constexpr (PREC == 2 && COMP) {
+    // composed (round 6): the last embedding layer has no ReLU, so e_init = W4 h3 + b4 is linear in h3 and
+    // Q0 = W1_e_init e_init + b1 = (W1_e_init W4) h3 + (W1_e_init b4 + b1); likewise
+    // R0 = Q0 + W1_e_cur e_init = ((W1_e_init + W1_e_cur) W4) h3 + (...). The products are formed once in fp64
+    // (mpn/fold.py, pemp_mpn_weights.emb_comp_bf / emb_comp_b) and staged in slots 3 (Q0) and 4 (R0): e_init is
+    // never computed, one 64x64 GEMM and one split per tile fewer
+    layer_h3<1, 2, true, false, false>(smz, Lo, 0, x, y);   // A -> 32
+    layer_h3<1, 4, true, true, true>(smz, Lo, 1, y, x);     // 32 -> 64
+    layer_h3<2, 4, true, true, true>(smz, Lo, 2, x, y);     // 64 -> 64 (h3 in y, a ReLU output)
+    layer_h3<2, 4, false, true, true>(smz, Lo, 3, y, x, &fx);   // Q0 in x (domain), h3's split in fx
+  } else if constexpr (PREC == 2) {   // every activation in the 2^11 domain (edge_attr in: true values)
     layer_h3<1, 2, true, false, false>(smz, Lo, 0, x, y);   // A -> 32
     layer_h3<1, 4, true, true, true>(smz, Lo, 1, y, x);     // 32 -> 64
     layer_h3<2, 4, true, true, true>(smz, Lo, 2, x, y);     // 64 -> 64
@@ -1163,6 +1172,13 @@ static bool embed_fixed_shape(const EmbedLayout& L) {
   for (int l = 0; l < 5; ++l)
     if (L.kb[l] != kb[l] || L.ob[l] != ob[l] || (L.relu[l] != 0) != (relu[l] != 0)) return false;
   return true;
+}
+// the composed form of the fixed f16x3 embedding (embed_tile_fixed COMP) runs when the caller supplied its packs
+#ifndef PEMP_EMBED_COMPOSE
+#define PEMP_EMBED_COMPOSE 1
+#endif
+static bool embed_composed(const EmbedLayout& L, int prec, const pemp_mpn_weights& w) {
+  return PEMP_EMBED_COMPOSE && prec == PEMP_PREC_F16X3 && embed_fixed_shape(L) && w.emb_comp_bf && w.emb_comp_b;
 }
 
 // Stage one 64x64 edge-pass matrix into LDS (PREC 0: fp32 rows of LDW; PREC 1: interleaved bf16)
@@ -1187,14 +1203,19 @@ __device__ __forceinline__ void stage_tile64(float* dst, const float* w32, int64
 // f16x3 layers): written by threads tid, tid + nthreads, ... into dst, which is the kernel's LDS or, once per weight
 // set (pemp_mpn_edge_image, embed_image_kernel), a global buffer of embed_image_floats() floats that the kernel then
 // copies with one LDS-DMA round instead of these loops' dependent global-load rounds (one or two per layer).
+// comp_bf / comp_b (FIXED f16x3 only, the composed form of embed_tile_fixed): slots 3 and 4 hold the composed Q0 and
+// R0 matrices and biases instead of the last embedding layer and Q0's layer, and the W1_e_cur tile is not staged.
 template <int PREC, bool FIXED>
 __device__ __forceinline__ void embed_stage(float* dst, int tid, int nthreads, const pemp_mlp& emb, const EmbedLayout& Lo,
                                             const uint16_t* __restrict__ emb_bf, const float* __restrict__ q0_w,
                                             const float* __restrict__ q0_b, const float* __restrict__ e1_w,
-                                            const uint16_t* __restrict__ e1_bf) {
+                                            const uint16_t* __restrict__ e1_bf, const uint16_t* __restrict__ comp_bf,
+                                            const float* __restrict__ comp_b) {
+  const bool comp = FIXED && PREC == 2 && comp_bf && comp_b;
   // W1_e_cur after the embedding image (stage_tile64's layout)
   float* d64 = dst + Lo.total;
-  if (PREC == 0) {
+  if (comp) {
+  } else if (PREC == 0) {
     for (int idx = tid; idx < D * 16; idx += nthreads) {
       const int row = idx >> 4, c4 = (idx & 15) * 4;
       *reinterpret_cast<float4*>(&d64[row * LDW + c4]) = ld4(e1_w + row * D + c4);
@@ -1208,7 +1229,8 @@ __device__ __forceinline__ void embed_stage(float* dst, int tid, int nthreads, c
     }
   }
   for (int l = 0; l <= Lo.n; ++l) {
-    const float* bsrc = l < Lo.n ? emb.layer[l].b : q0_b;
+    const bool cl = comp && l >= Lo.n - 1;   // composed slot: 3 = Q0, 4 = R0 (64 x 64 each)
+    const float* bsrc = cl ? comp_b + 64 * (l - (Lo.n - 1)) : l < Lo.n ? emb.layer[l].b : q0_b;
     const int rows = 16 * Lo.ob[l];
     if (PREC == 0) {
       const float* src = l < Lo.n ? emb.layer[l].w : q0_w;
@@ -1218,7 +1240,7 @@ __device__ __forceinline__ void embed_stage(float* dst, int tid, int nthreads, c
         *reinterpret_cast<float4*>(&dst[Lo.w_off[l] + row * Lo.stride[l] + c4]) = ld4(src + row * ip + c4);
       }
     } else {
-      const uint16_t* src = emb_bf + Lo.g_off[l];
+      const uint16_t* src = cl ? comp_bf + 2 * 64 * 64 * (l - (Lo.n - 1)) : emb_bf + Lo.g_off[l];
       const int ip = 32 * Lo.kb[l], q8 = ip / 8;
       __bf16* dstb = reinterpret_cast<__bf16*>(dst + Lo.w_off[l]);
       for (int idx = tid; idx < 2 * rows * q8; idx += nthreads) {   // hi rows, then lo rows
@@ -1238,10 +1260,13 @@ __host__ __device__ inline int embed_image_floats(const EmbedLayout& Lo) { retur
 template <int PREC, bool FIXED>
 __global__ __launch_bounds__(256) void embed_image_kernel(pemp_mlp emb, EmbedLayout Lo, const uint16_t* emb_bf,
                                                           const float* q0_w, const float* q0_b, const float* e1_w,
-                                                          const uint16_t* e1_bf, float* img) {
+                                                          const uint16_t* e1_bf, const uint16_t* comp_bf,
+                                                          const float* comp_b, float* img) {
   embed_stage<PREC, FIXED>(img, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256, emb, Lo, emb_bf, q0_w, q0_b, e1_w,
-                           e1_bf);
+                           e1_bf, comp_bf, comp_b);
 }
+// floats of the composed image the kernel copies (no W1_e_cur tile)
+__host__ __device__ inline int embed_comp_floats(const EmbedLayout& Lo) { return (Lo.total + 3) & ~3; }
 
 __device__ inline void dma_to_lds(float* __restrict__ lds, const float* __restrict__ src, int n);
 __device__ __forceinline__ void lds_drain();
@@ -1250,7 +1275,9 @@ __device__ __forceinline__ void lds_drain();
 // Q0 = W1_e_init·e_init + b1 and R0 = Q0 + W1_e_cur·e_init (the first pass's layer-1 input).
 // One 16-wave workgroup per CU, weights staged once in LDS (from the prebuilt image when there is one); a wave
 // walks an equal share of the sorted positions in 16-edge tiles.
-template <int PREC, bool FIXED>
+// FX: 0 runtime-shaped layers, 1 the fixed published shape, 2 the same composed (embed_tile_fixed COMP: f16x3 only,
+// with the caller's composed packs)
+template <int PREC, int FX>
 __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp emb, EmbedLayout Lo,
                                                                      const uint16_t* __restrict__ emb_bf,
                                                                      const float* __restrict__ ea, int A,
@@ -1261,15 +1288,19 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp em
                                                                      const uint16_t* __restrict__ e1_bf,
                                                                      float* __restrict__ r0, float* __restrict__ q0,
                                                                      const int64_t* __restrict__ ne,
-                                                                     const float* __restrict__ img) {
+                                                                     const float* __restrict__ img,
+                                                                     const uint16_t* __restrict__ comp_bf,
+                                                                     const float* __restrict__ comp_b) {
+  constexpr bool FIXED = FX >= 1, COMP = FX == 2;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   if (ne) E = ne[1];   // capacity mode: the device-side edge count
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
   if (img) {
-    dma_to_lds(sm, img, embed_image_floats(Lo));
+    dma_to_lds(sm, img, COMP ? embed_comp_floats(Lo) : embed_image_floats(Lo));
     lds_drain();
   } else {
-    embed_stage<PREC, FIXED>(sm, threadIdx.x, 64 * EDGE_WAVES, emb, Lo, emb_bf, q0_w, q0_b, e1_w, e1_bf);
+    embed_stage<PREC, FIXED>(sm, threadIdx.x, 64 * EDGE_WAVES, emb, Lo, emb_bf, q0_w, q0_b, e1_w, e1_bf,
+                             COMP ? comp_bf : nullptr, COMP ? comp_b : nullptr);
   }
   __syncthreads();
   const int64_t gw = (int64_t)blockIdx.x * EDGE_WAVES + wave, nw = (int64_t)gridDim.x * EDGE_WAVES;
@@ -1303,6 +1334,23 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp em
       load_edge_attr(rs_ea, A, o, x);
     }
     Frag<PREC> fx;
+    const int vo = valid ? p * 256 + 16 * g : OOB_VOFF;   // masked lanes: stores dropped
+    if constexpr (COMP) {
+      embed_tile_fixed<PREC, true>(smz, Lo, x, y, fx);   // x = Q0 (domain), y = h3, fx = h3's split
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob) bst4(rs_q0, vo + 64 * ob, x[ob][0], x[ob][1], x[ob][2], x[ob][3]);
+      // R0 = W_r h3 + b_r (slot 4, bias staged x 2^11): its own accumulator, no dependence on Q0's
+      const float* br = smz + Lo.b_off[4];
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob) {
+        const float4 bb = ld4(br + 16 * ob + 4 * g);
+        x[ob][0] = bb.x; x[ob][1] = bb.y; x[ob][2] = bb.z; x[ob][3] = bb.w;
+      }
+      gemm_f<PREC, 4>(smz + Lo.w_off[4], y, fx, x);
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob) bst4(rs_r0, vo + 64 * ob, x[ob][0], x[ob][1], x[ob][2], x[ob][3]);
+      continue;
+    }
     if constexpr (FIXED) {
       embed_tile_fixed<PREC>(smz, Lo, x, y, fx);   // x = e_init, y = Q0 in the domain, fx = e_init's split
     } else {
@@ -1315,7 +1363,6 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp em
       }
       prep_true<PREC>(x, fx);
     }
-    const int vo = valid ? p * 256 + 16 * g : OOB_VOFF;   // masked lanes: stores dropped
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob) bst4(rs_q0, vo + 64 * ob, y[ob][0], y[ob][1], y[ob][2], y[ob][3]);
     gemm_f<PREC, 4>(smz + Lo.total, x, fx, y);    // R0 = Q0 + W1_e_cur · e_init
@@ -1942,8 +1989,7 @@ __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_
         av = fmaf(w.x, ep[ob][0], av); av = fmaf(w.y, ep[ob][1], av);
         av = fmaf(w.z, ep[ob][2], av); av = fmaf(w.w, ep[ob][3], av);
       }
-      av += __shfl_xor(av, 16);
-      av += __shfl_xor(av, 32);
+      av = xsum_rows(av);
       av += vec[z + 2 * D];                      // attention bias (re-read: a register copy spills)
     }
     // chunk structure of the tile and each edge's softmax weight pe = exp(a - M), M = its segment's maximum so far
@@ -2022,8 +2068,7 @@ __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_
         lg = fmaf(w.x, h2[ob][0], lg); lg = fmaf(w.y, h2[ob][1], lg);
         lg = fmaf(w.z, h2[ob][2], lg); lg = fmaf(w.w, h2[ob][3], lg);
       }
-      lg += __shfl_xor(lg, 16);
-      lg += __shfl_xor(lg, 32);
+      lg = xsum_rows(lg);
       if (valid && g == 0)   // (descriptor store: an out-of-range id from a contract-breaking list is dropped)
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lg + hb[D + 64]), make_rsrc(logits, E * 4),
                                               4 * orig, 0, 0);
@@ -3992,24 +4037,24 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
     ProfScope prof("edge_embed", pst);
     if (emb_lds) {
       const int grid = (int)std::min<int64_t>(PEMP_EMBED_RESERVE ? edge_cus(E) : num_cus(), (E + 16 * EDGE_WAVES - 1) / (16 * EDGE_WAVES));
-      const size_t lds = (size_t)embed_image_floats(emb_lo) * sizeof(float);
       const bool fixed = embed_fixed_shape(emb_lo);
+      const bool comp = embed_composed(emb_lo, emb_prec, *w);
+      const size_t lds = (size_t)(comp ? embed_comp_floats(emb_lo) : embed_image_floats(emb_lo)) * sizeof(float);
       // the caller's prebuilt LDS image (pemp_mpn_edge_image appends it to the edge-pass image), else staged here
       const float* emb_img = w->edge_img ? w->edge_img + embed_image_offset(*desc, *w) : nullptr;
 #define PEMP_EMBED_LAUNCH(P, FX)                                                                                   \
   hipLaunchKernelGGL((edge_embed_kernel<P, FX>), dim3(grid), dim3(64 * EDGE_WAVES), lds, pst, w->edge_emb, emb_lo,  \
                      w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, w->e1_bf, \
-                     ws.EA, ws.Q0, ne, emb_img)
+                     ws.EA, ws.Q0, ne, emb_img, w->emb_comp_bf, w->emb_comp_b)
       if (emb_prec == PEMP_PREC_F16X3) {
-        if (fixed) PEMP_EMBED_LAUNCH(2, true);
-        else PEMP_EMBED_LAUNCH(2, false);
+        if (comp) PEMP_EMBED_LAUNCH(2, 2);
+        else if (fixed) PEMP_EMBED_LAUNCH(2, 1);
+        else PEMP_EMBED_LAUNCH(2, 0);
       } else if (emb_prec == PEMP_PREC_BF16X3) {
-        if (fixed) PEMP_EMBED_LAUNCH(1, true);
-        else PEMP_EMBED_LAUNCH(1, false);
+        if (fixed) PEMP_EMBED_LAUNCH(1, 1);
+        else PEMP_EMBED_LAUNCH(1, 0);
       } else
-        hipLaunchKernelGGL((edge_embed_kernel<0, false>), dim3(grid), dim3(64 * EDGE_WAVES), lds, pst, w->edge_emb, emb_lo,
-                           w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, w->e1_bf,
-                           ws.EA, ws.Q0, ne, emb_img);
+        PEMP_EMBED_LAUNCH(0, 0);
 #undef PEMP_EMBED_LAUNCH
     } else {
       hipLaunchKernelGGL(edge_embed_wide_kernel, dim3((unsigned)((E + 63) / 64)), dim3(256), 0, pst, w->edge_emb,
@@ -4316,6 +4361,16 @@ static int cap_forward_direct(const pemp_mpn_desc* desc, const pemp_mpn_weights*
 // Graph statistics for the tests (pemp_mpn_graph_stats): captures made, replays launched, captures refused.
 static std::atomic<uint64_t> g_graph_captures{0}, g_graph_replays{0}, g_graph_refused{0};
 
+extern "C" size_t pemp_abi_struct_size(int which) {
+  switch (which) {
+    case 0: return sizeof(pemp_mpn_weights);
+    case 1: return sizeof(pemp_mpn_desc);
+    case 2: return sizeof(pemp_mlp);
+    case 3: return sizeof(pemp_proj_maps);
+    default: return 0;
+  }
+}
+
 extern "C" int pemp_edge_cus_policy(int num_cus_, int64_t E, int reserve_request) {
   PEMP_CHECK_ARG(num_cus_ >= 1 && E >= 0, "pemp_edge_cus_policy: bad args");
   if (reserve_request < 0) {
@@ -4523,9 +4578,11 @@ extern "C" int pemp_mpn_edge_image(const pemp_mpn_desc* desc, const pemp_mpn_wei
     const EmbedLayout lo = embed_layout(w->edge_emb, prec);
     float* eimg = image + embed_image_offset(*desc, *w);
     const bool fixed = embed_fixed_shape(lo);
+    const bool comp = embed_composed(lo, prec, *w);
 #define PEMP_EMBED_IMAGE(P, FX)                                                                                  \
   hipLaunchKernelGGL((embed_image_kernel<P, FX>), dim3(16), dim3(256), 0, as_stream(stream), w->edge_emb, lo,     \
-                     w->emb_bf, w->q0_w, w->q0_b, w->e1_w, w->e1_bf, eimg)
+                     w->emb_bf, w->q0_w, w->q0_b, w->e1_w, w->e1_bf, comp ? w->emb_comp_bf : nullptr,             \
+                     comp ? w->emb_comp_b : nullptr, eimg)
     if (prec == PEMP_PREC_F16X3) {
       if (fixed) PEMP_EMBED_IMAGE(2, true);
       else PEMP_EMBED_IMAGE(2, false);

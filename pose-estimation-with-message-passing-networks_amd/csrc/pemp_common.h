@@ -122,4 +122,51 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// Cross-lane sums without the LDS pipe (gfx950 v_permlane16_swap / v_permlane32_swap, DPP in-row moves). A
+// __shfl_xor lowers to a ds_bpermute (an LDS round trip in the dependency chain); these stay in the VALU.
+// permlane16_swap(x, x) leaves rows (0, 0, 2, 2) in one result and (1, 1, 3, 3) in the other, so their sum is
+// x[lane] + x[lane ^ 16] in every lane; permlane32_swap likewise for lane ^ 32. Each sum is the same two operands as
+// x + __shfl_xor(x, 16 / 32), so the results are bit-identical to the shuffle forms.
+#ifndef PEMP_PERMLANE
+#define PEMP_PERMLANE 1   // 0: the __shfl_xor forms (A/B builds)
+#endif
+__device__ __forceinline__ float xsum16(float v) {
+  if (!PEMP_PERMLANE) return v + __shfl_xor(v, 16);
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(a[0]) + __uint_as_float(a[1]);
+}
+__device__ __forceinline__ float xsum32(float v) {
+  if (!PEMP_PERMLANE) return v + __shfl_xor(v, 32);
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(a[0]) + __uint_as_float(a[1]);
+}
+// v summed over the lanes c, c + 16, c + 32, c + 48 (the four 16-lane rows), in every lane
+__device__ __forceinline__ float xsum_rows(float v) { return xsum32(xsum16(v)); }
+__device__ __forceinline__ float xmax_rows(float v) {
+  if (!PEMP_PERMLANE) {
+    v = fmaxf(v, __shfl_xor(v, 16));
+    return fmaxf(v, __shfl_xor(v, 32));
+  }
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+// integer sum over all 64 lanes, in every lane: xor 1, xor 2 (quad_perm), half-row and row mirrors, then the row swaps
+__device__ __forceinline__ int wave_sum_i32(int v) {
+  if (!PEMP_PERMLANE) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+  }
+  v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
+  v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
+  v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);   // row_half_mirror
+  v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);   // row_mirror
+  const auto a = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+  v = (int)(a[0] + a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+  return (int)(b[0] + b[1]);
+}
+
 }  // namespace pemp

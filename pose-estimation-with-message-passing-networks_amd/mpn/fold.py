@@ -174,6 +174,22 @@ def edge_embedding_layers(emb):
     return layers
 
 
+def composed_embedding(emb, q0, e1, b1):
+    """The published edge embedding (A <= 32 -> 32 -> 64 -> 64 -> 64, ReLU after all but the last Linear) composed
+    with the e_init / e_cur columns of mlp_edge.0 (pemp_mpn_weights.emb_comp_bf / emb_comp_b): the last Linear
+    (W4, b4) is affine, so Q0 = q0 (W4 h3 + b4) + b1 and R0 = Q0 + e1 (W4 h3 + b4) are affine in h3, the third
+    layer's output. Returns ((Wq, bq), (Wr, br)) in fp64, or None for any other shape."""
+    shapes = [(32, None), (64, 32), (64, 64), (64, 64)]
+    if len(emb) != 4 or [bool(r) for _, _, r in emb] != [True, True, True, False]:
+        return None
+    for (W, _, _), (o, i) in zip(emb, shapes):
+        if W.shape[0] != o or (i is not None and W.shape[1] != i) or W.shape[1] > 32 and i is None:
+            return None
+    W4, b4 = emb[3][0].double(), emb[3][1].double()
+    q0, e1, b1 = q0.double(), e1.double(), b1.double()
+    return (q0 @ W4, q0 @ b4 + b1), ((q0 + e1) @ W4, (q0 + e1) @ b4 + b1)
+
+
 def hierarch_dense_layers(upd, T):
     """UPDATE_TYPE hierarch_mlp / hierarch_cnn as dense fp64 layers over agg[n] flattened to [T*64]
     (index t*64 + d), each followed by ReLU as in the reference. Block-sparse structure becomes
@@ -315,6 +331,16 @@ def fold_weights(model, device, precision="f16x3") -> Folded:
     if all(W.shape[0] <= 64 and W.shape[1] <= 64 for W, _, _ in emb):
         packs = [pack(W).reshape(-1) for W, _, _ in emb] + [pack(q0).reshape(-1)]
         s.emb_bf = f.dev_raw(torch.cat(packs), device).data_ptr()
+        comp = composed_embedding(emb, q0, e1, b1) if precision == "f16x3" else None
+        if comp is not None:
+            (Wq, bq), (Wr, br) = comp
+            try:
+                cp = torch.cat([pack(Wq).reshape(-1), pack(Wr).reshape(-1)])
+            except F16RangeError:       # a composed weight past the f16x3 range: the kernel composes nothing
+                cp = None
+            if cp is not None:
+                s.emb_comp_bf = f.dev_raw(cp, device).data_ptr()
+                s.emb_comp_b = f.dev(torch.cat([bq, br]), device).data_ptr()
     attn = getattr(layer, "attn_net", None)
     if attn is not None and attn[0].out_features == 1:       # node_edge_attn: one shared row
         s.attn_w = f.dev(attn[0].weight.detach().double().cpu().reshape(64), device).data_ptr()

@@ -71,3 +71,13 @@ def test_edge_cu_reservation_is_a_bounded_share():
                 if E < 65_536:
                     assert n == cus
     assert pol(0, 1000, 64) < 0 and pol(256, -1, 64) < 0
+
+
+def test_ctypes_struct_mirrors_match_the_library():
+    """The ctypes mirrors of the ABI structs have the library's sizes (a field added on one side only would shift
+    every later field of the struct the kernels read)."""
+    import ctypes
+    L = _lib.load_cdll()
+    for which, cls in enumerate((_lib.PempMpnWeights, _lib.PempMpnDesc, _lib.PempMlp, _lib.PempProjMaps)):
+        assert L.pemp_abi_struct_size(which) == ctypes.sizeof(cls), cls.__name__
+    assert L.pemp_abi_struct_size(7) == 0
