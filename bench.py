@@ -183,6 +183,33 @@ def run_step(wl, gc, model, hm, feats, tags, dev):
     return out, pe, pn, pc
 
 
+def run_steps(n, streams, S, wl, gc, model, hm, feats, tags, dev):
+    """n whole steps, step i on streams[i % S]. S > 1: pipelined as a server with S requests in flight -- step i + 1
+    is queued (construct_graph_start: detection, capacity graph build, MPN) before step i is collected
+    (PendingGraph.result: the count wait, the output views, the model call returning the queued logits), so the
+    host's count wait overlaps the next step's launches; each stream then has at most one step pending. S == 1:
+    run_step one after the other."""
+    if S == 1 or os.environ.get("PEMP_BENCH_NO_PIPELINE"):   # (the latter: round 5's loop, for A/B runs)
+        for i in range(n):
+            with torch.cuda.stream(streams[i % S]):
+                run_step(wl, gc, model, hm, feats, tags, dev)
+        return
+    pend = None
+    for i in range(n + 1):
+        nxt = None
+        if i < n:
+            st = streams[i % S]
+            with torch.cuda.stream(st):
+                nxt = (pemp_amd.get_graph_constructor(
+                    gc, scoremaps=hm, features=feats, tagmaps=tags, joints_gt=None, factor_list=None, masks=None,
+                    device=dev, testing=True, heatmaps=None, num_joints=wl["J"]).construct_graph_start(), st)
+        if pend is not None:
+            with torch.cuda.stream(pend[1]):
+                out = pend[0].result()
+                model(out[0], out[1], out[2], node_types=out[7][:, 2])
+        pend = nxt
+
+
 _BENCH_MAPS = None
 _LAST_GROUPING = None
 ROOF_REPEAT = 8   # back-to-back launches per event pair in the roofline phase
@@ -554,11 +581,19 @@ def e2e_pipeline(wl, gc, model, hm, feats, tags, dev, steps, warmup, world):
         stage[name] = stage.get(name, 0.0) + t1 - t0
         return t1
 
-    def gpu_part():
+    def gpu_start():
+        """batch k+1's launches (detection, capacity graph build, MPN): construct_graph_start, no count wait"""
         t0 = time.perf_counter()
-        out = pemp_amd.get_graph_constructor(gc, scoremaps=hm, features=feats, tagmaps=tags, joints_gt=None,
-                                             factor_list=None, masks=None, device=dev, testing=True, heatmaps=None,
-                                             num_joints=J).construct_graph()
+        p = pemp_amd.get_graph_constructor(gc, scoremaps=hm, features=feats, tagmaps=tags, joints_gt=None,
+                                           factor_list=None, masks=None, device=dev, testing=True, heatmaps=None,
+                                           num_joints=J).construct_graph_start()
+        clock("construct_graph_start", t0)
+        return p
+
+    def gpu_part(p=None):
+        p = gpu_start() if p is None else p
+        t0 = time.perf_counter()
+        out = p.result()
         t0 = clock("construct_graph", t0)
         with torch.no_grad():
             pe, pn, pc, _ = model(out[0], out[1], out[2], node_types=out[7][:, 2])
@@ -592,7 +627,11 @@ def e2e_pipeline(wl, gc, model, hm, feats, tags, dev, steps, warmup, world):
         persons = 0
         if pipelined:
             # three batches in flight: batch k+1's GPU part is queued, then batch k's grouping runs on the host and
-            # its finishing is queued on the side stream, then batch k-1's finished keypoints are collected
+            # its finishing is queued on the side stream, then batch k-1's finished keypoints are collected.
+            # (Round 6 measured the other order -- batch k+1's graph collected only after batch k's host stages, its
+            # count wait overlapped with them -- at 5.6k vs 8.4k images/s at c3: the count wait then became a wait
+            # for batch k's GAEC on the grouping thread, which the old order gives that time to finish;
+            # profiles/r06_pipelined_steps.md.)
             pend, fin_prev = gpu_part(), None
             for _ in range(n - 1):
                 nxt = gpu_part()
@@ -825,9 +864,7 @@ def main():
             barrier(world)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            for i in range(n):
-                with torch.cuda.stream(streams[i % S_try]):
-                    run_step(wl, gc, model, hm, feats, tags, dev)
+            run_steps(n, streams, S_try, wl, gc, model, hm, feats, tags, dev)
             torch.cuda.synchronize()
             return max_over_ranks(time.perf_counter() - t0, world, dev)
         n_probe = max(args.warmup, 4)
@@ -860,16 +897,12 @@ def main():
         dominant_overall = max(totals, key=totals.get) if totals else None
         breakdown = {k: round(v[1] / v[0] * 1e3, 2) for k, v in stats.items()}
 
-    # timed region (value): the path alone, no profiler events; step i on stream i % S
-    for i in range(args.warmup):
-        with torch.cuda.stream(streams[i % S]):
-            run_step(wl, gc, model, hm, feats, tags, dev)
+    # timed region (value): the path alone, no profiler events; step i on stream i % S (run_steps)
+    run_steps(args.warmup, streams, S, wl, gc, model, hm, feats, tags, dev)
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        with torch.cuda.stream(streams[i % S]):
-            run_step(wl, gc, model, hm, feats, tags, dev)
+    run_steps(args.steps, streams, S, wl, gc, model, hm, feats, tags, dev)
     torch.cuda.synchronize()
     barrier(world)
     dt = time.perf_counter() - t0

@@ -59,6 +59,50 @@ def get_graph_constructor(config, **kwargs):
     return NaiveGraphConstructor(config=config, **kwargs)
 
 
+class PendingGraph:
+    """construct_graph_start's handle: result() waits for the detection counts and returns the 15-tuple (once
+    computed, the same tuple on every call)."""
+
+    def __init__(self, gc, gen, dev, counts_ent):
+        self._gc, self._gen, self._dev, self._counts = gc, gen, dev, counts_ent
+        self._out, self._done = None, False
+
+    def _step(self):
+        try:
+            next(self._gen)
+        except StopIteration as stop:
+            self._finish(stop.value)
+        except BaseException:
+            self._fail()
+            raise
+
+    def _finish(self, out):
+        self._out, self._done = out, True
+        NaiveGraphConstructor._host_counts_give(self._dev, self._counts)   # every count was read
+        self._gen = None
+
+    def _fail(self):
+        self._done = True
+        self._gen = None
+        torch.cuda.current_stream(self._dev).synchronize()   # queued kernels may still store counts into it
+        NaiveGraphConstructor._host_counts_give(self._dev, self._counts)
+
+    def result(self):
+        if not self._done:
+            try:
+                next(self._gen)
+                raise RuntimeError("pemp_amd: construct_graph did not finish")   # (the generator yields once)
+            except StopIteration as stop:
+                self._finish(stop.value)
+            except BaseException:
+                if not self._done:
+                    self._fail()
+                raise
+        if self._out is None:
+            raise RuntimeError("pemp_amd: construct_graph failed")
+        return self._out
+
+
 class NaiveGraphConstructor:
     # Shared between instances, threads and streams (SURVEY §8b: reentrant calls). Device scratch is per
     # (device, stream) (_lib.Workspace); each call takes its own mapped host count buffer from a pool and
@@ -144,6 +188,16 @@ class NaiveGraphConstructor:
 
     # ------------------------------------------------------------------------------------
     def construct_graph(self):
+        """ConstructGraph.py:46-68 (inference): the 15-tuple. = construct_graph_start().result()."""
+        return self.construct_graph_start().result()
+
+    def construct_graph_start(self):
+        """The launch half of construct_graph (no reference counterpart): queues the detection and, with a capacity
+        hint, the graph build and the bound MPN, then returns a PendingGraph without waiting for the detection
+        counts. Its result() waits for them and returns construct_graph's 15-tuple. A caller with several batches
+        in flight (a server, bench.py) queues the next batch before it collects the previous one, so the host's
+        count wait overlaps its other work. A pending graph must be collected (result()) before another batch is
+        started on the same stream twice over (the library's scratch is per device and stream)."""
         L = _lib.lib()
         st = _lib.stream(self.device)
         sm = self.scoremaps
@@ -178,15 +232,11 @@ class NaiveGraphConstructor:
         dsc = torch.empty(B, cap, dtype=torch.float32, device=dev)
         n_det = torch.empty(B, dtype=torch.int32, device=dev)
         counts_ent = self._host_counts_take(L, dev, B)
-        try:
-            out = self._construct(L, st, sm, masks, B, J, H, W, use_thr, topk, thr, dev, ws, cap, det, dsc,
-                                  n_det, counts_ent[2][:B])
-        except BaseException:
-            torch.cuda.current_stream(dev).synchronize()   # queued kernels may still store counts into it
-            self._host_counts_give(dev, counts_ent)
-            raise
-        self._host_counts_give(dev, counts_ent)   # every count was read: the device is done with it
-        return out
+        gen = self._construct(L, st, sm, masks, B, J, H, W, use_thr, topk, thr, dev, ws, cap, det, dsc, n_det,
+                              counts_ent[2][:B])
+        pending = PendingGraph(self, gen, dev, counts_ent)
+        pending._step()                             # up to the count wait: everything is queued
+        return pending
 
     def _construct(self, L, st, sm, masks, B, J, H, W, use_thr, topk, thr, dev, ws, cap, det, dsc, n_det,
                    counts_h):
@@ -263,9 +313,11 @@ class NaiveGraphConstructor:
             _lib.check(L.pemp_fully_graph_build_cap(*build_args))
             if launch_mpn is not None:
                 pending = launch_mpn()
+            yield None                                       # (construct_graph_start returns here)
             counts_l = self._wait_counts(counts_h, dev)
             built = bufs
         else:
+            yield None
             counts_l = self._wait_counts(counts_h, dev)      # the one host read-back of the batch
         mx = max(counts_l) if counts_l else 0
         cap_used = cap                                      # the detections the capacity build read

@@ -268,6 +268,66 @@ def test_reentrant_two_streams(graph):
         check(s % 2, out)
 
 
+@pytest.mark.parametrize("graph", ["fully", "knn"])
+def test_construct_graph_start_pipelined(graph):
+    """construct_graph_start / PendingGraph.result (batches in flight): step i + 1 is started on the other stream
+    before step i is collected, with the bound MPN queued in capacity mode; every graph equals the oracle bit for
+    bit and every step's logits equal a plain construct_graph + forward of the same batch. result() is idempotent."""
+    J = 17
+    cfg = pcfg.published_mpn_config(J, 3, "attn")
+    model = pemp_amd.get_mpn_model(cfg)
+    model.load_state_dict(syn.closed_form_state_dict(model, 0.5))
+    model.eval().to(DEV)
+    gc = pcfg.inference_gc_config(graph, 5, False)
+    batches = []
+    for k in range(3):
+        B, H, W = 2 + k % 2, 96, 128
+        hm = torch.from_numpy(syn.make_heatmaps(90 + k, B, J, H, W, 5, margin=4))
+        feats = torch.from_numpy(syn.closed_form((B, 128, H, W), 0.3 + 0.05 * k))
+        tags = torch.from_numpy(syn.closed_form((B, J, H, W, 1), 0.75))
+        batches.append((hm.to(DEV), feats.to(DEV), tags.to(DEV), restate.construct_graph(hm, feats, tags, None, gc, J)))
+    streams = [torch.cuda.Stream(DEV), torch.cuda.Stream(DEV)]
+
+    def make(b):
+        hm, feats, tags, _ = batches[b]
+        return pemp_amd.get_graph_constructor(gc, scoremaps=hm, features=feats, tagmaps=tags, joints_gt=None,
+                                              factor_list=None, masks=None, device=DEV, testing=True, heatmaps=None,
+                                              num_joints=J)
+
+    with torch.no_grad():
+        refs = []
+        for b in range(len(batches)):   # plain calls (also warm the capacity hints)
+            out = make(b).construct_graph()
+            refs.append([t[-1].cpu() for t in model(out[0], out[1], out[2], node_types=out[7][:, 2])[:3]])
+        pemp_amd.bind_mpn(model)
+        try:
+            for rnd in range(2):
+                order = list(range(len(batches))) * 2
+                pend = None
+                got = []
+                for i in range(len(order) + 1):
+                    nxt = None
+                    if i < len(order):
+                        with torch.cuda.stream(streams[i % 2]):
+                            nxt = (make(order[i]).construct_graph_start(), streams[i % 2], order[i])
+                    if pend is not None:
+                        with torch.cuda.stream(pend[1]):
+                            out = pend[0].result()
+                            assert pend[0].result() is out
+                            lg = model(out[0], out[1], out[2], node_types=out[7][:, 2])
+                            got.append((pend[2], out, [t[-1] for t in lg[:3]]))
+                    pend = nxt
+                torch.cuda.synchronize()
+                for b, out, lg in got:
+                    ref = batches[b][3]
+                    for j in (0, 1, 2, 7, 11, 12, 14):
+                        assert torch.equal(out[j].cpu(), ref[j]), (graph, b, j)
+                    for a_, r_ in zip(lg, refs[b]):
+                        assert torch.equal(a_.cpu(), r_), (graph, b)
+        finally:
+            pemp_amd.bind_mpn(None)
+
+
 @pytest.mark.parametrize("graph,persons", [("knn", 5), ("knn", 40)])
 @pytest.mark.parametrize("features", [["position", "angle", "connection_type"], ["ae_normed"],
                                       ["position", "connection_type", "ae_normed"]])
