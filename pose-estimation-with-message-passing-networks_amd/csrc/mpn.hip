@@ -2809,12 +2809,6 @@ struct NodeTableArgs {
 #ifndef NODE_SUM_TABLE_MAX_MB
 #define NODE_SUM_TABLE_MAX_MB 16   // ... while its aggregate re-reads (N T 256 B x column groups) stay below this
 #endif
-#ifndef NODE_SUM_WIDE_WAVES
-#define NODE_SUM_WIDE_WAVES 16   // past that, the wide form (node_table_kernel WAVES): 0 disables it
-#endif
-#ifndef NODE_SUM_WIDE_MAX_MB
-#define NODE_SUM_WIDE_MAX_MB 64  // ... while its re-reads stay below this
-#endif
 #ifndef PEMP_TBL_TILES
 #define PEMP_TBL_TILES 2   // (1 / 2 / 4 / 8 measured: 2 gives the shortest isolated MPN, c3knn10 0.423-0.426 vs 0.435 ms
                            // with 4, c3 0.235 vs 0.239 ms; tools/experiments/round5/nn.sh)
@@ -2824,19 +2818,15 @@ constexpr int TBL_TILES = PEMP_TBL_TILES;   // 16-node tiles per workgroup
 // SUM: the node update x = ReLU(b + sum_t agg[n, t]) (node_rows_kernel ROWS_SUM, same operations and order) is
 // computed here for the tile's 16 rows, by every column group of the tile (the aggregates are re-read from L2 by
 // each group instead of a separate launch writing x and this one reading it back); group 0 also stores x.
-// WAVES (SUM only): 16-column blocks per workgroup, one per wave. The wide form (16 waves, 256 columns) sums a
-// tile's aggregates once per 256 table columns instead of once per 64, so the re-reads shrink 4x (5 groups per
-// 16-node tile at T = 17 instead of 19); the first 4 waves do the sum while the others' weight loads are in flight.
-template <int PREC, int TILES = TBL_TILES, bool SUM = false, int WAVES = 4>
-__global__ __launch_bounds__(64 * WAVES) void node_table_kernel(NodeTableArgs a) {
+template <int PREC, int TILES = TBL_TILES, bool SUM = false>
+__global__ __launch_bounds__(256) void node_table_kernel(NodeTableArgs a) {
   static_assert(!SUM || TILES == 1, "the summing variant takes one 16-node tile per workgroup");
-  static_assert(SUM || WAVES == 4, "the plain table loads its node chunk with 4 waves");
   __shared__ __attribute__((aligned(16))) float xs[16 * TILES * RS];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
   const int chunk = blockIdx.x / a.groups, grp = blockIdx.x - chunk * a.groups;
   const int64_t n0 = (int64_t)chunk * 16 * TILES, N = a.ne ? a.ne[0] : a.N;
   if (n0 >= N) return;   // (capacity grids)
-  const int nob = a.NO / 16, ob = grp * WAVES + wave, obc = min(ob, nob - 1);
+  const int nob = a.NO / 16, ob = grp * 4 + wave, obc = min(ob, nob - 1);
   // this wave's weight fragment (rows 16 ob + c), issued first
   float4 w[8];
   bf16x8_t wh[4], wlo[4];
@@ -2860,7 +2850,7 @@ __global__ __launch_bounds__(64 * WAVES) void node_table_kernel(NodeTableArgs a)
     }
   }
   const float4 bb = ld4(a.pre_b + 16 * obc + 4 * g);
-  if (SUM && threadIdx.x < 256) {
+  if constexpr (SUM) {
     // row r of the tile, features 4 q .. 4 q + 3: x0 and every type's aggregate and segment bounds in flight together
     const int r = threadIdx.x >> 4, q = threadIdx.x & 15;
     const int64_t n = n0 + r, nc = n < N ? n : N - 1;
@@ -2884,7 +2874,7 @@ __global__ __launch_bounds__(64 * WAVES) void node_table_kernel(NodeTableArgs a)
     *reinterpret_cast<float4*>(&xs[r * RS + 4 * q]) = x0;
     *reinterpret_cast<float4*>(&xs[r * RS + 64 + 4 * q]) = v;
     if (grp == 0 && n < N) *reinterpret_cast<float4*>(const_cast<float*>(a.X) + n * 128 + 64 + 4 * q) = v;
-  } else if (!SUM) {
+  } else {
   // X chunk -> LDS: 16 TILES rows x 32 float4, 2 TILES per thread
     float4 t[2 * TILES];
 #pragma unroll
@@ -4087,25 +4077,13 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   // middle steps of the attention model (update block in the edge pass, no heads): the node update runs inside the
   // node-table launch (node_table_kernel<PREC, 1, true>) instead of a launch of its own
   const unsigned table_grid1 = (unsigned)(((N + 15) / 16) * table_groups);
-  constexpr int WW = NODE_SUM_WIDE_WAVES > 0 ? NODE_SUM_WIDE_WAVES : 4;
-  const int wide_groups = (NO / 16 + WW - 1) / WW;
-  const unsigned wide_grid = (unsigned)(((N + 15) / 16) * wide_groups);
   auto node_step = [&](int mode, bool table, int slot, bool dup) -> int {
     // (every column group re-reads the tile's aggregates: worth it while those re-reads stay small -- C2 -- not at
-    // C3, where they are ~100 MB per call and the fused launch only ties the two it replaces; the wide form groups
-    // 256 columns per workgroup, 4x fewer re-reads)
-    const bool sum_ok = mode == ROWS_SUM && table && slot < 0 && !ept && NODE_SUM_TABLE;
-    if (sum_ok && NODE_SUM_WIDE_WAVES > 0 && table_prec == PEMP_PREC_F16X3 &&
-        N * T * 256 * (int64_t)table_groups > (int64_t)NODE_SUM_TABLE_MAX_MB << 20 &&
-        N * T * 256 * (int64_t)wide_groups <= (int64_t)NODE_SUM_WIDE_MAX_MB << 20) {
-      NodeTableArgs ta{ws.X, N, w->pre_w, w->pre_b, w->pre_bf, NO, wide_groups, ws.NT, ne, ws.agg, ws.seg, T,
-                       w->upd_b};
-      ProfScope prof("node_update_table", st);
-      hipLaunchKernelGGL((node_table_kernel<2, 1, true, WW>), dim3(wide_grid), dim3(64 * WW), 0, st, ta);
-      PEMP_LAUNCH_CHECK();
-      return PEMP_OK;
-    }
-    if (sum_ok && N * T * 256 * (int64_t)table_groups <= (int64_t)NODE_SUM_TABLE_MAX_MB << 20) {
+    // C3, where they are ~100 MB per call and the fused launch only ties the two it replaces. Round 6: a wide form,
+    // 16 waves = 256 columns per workgroup so a tile's aggregates are summed 5 instead of 19 times, took 24 us per
+    // call against 8 + 10 us for the two launches at c3 / c3knn10 (profiles/r06_node_sum_wide.md); not kept.)
+    if (mode == ROWS_SUM && table && slot < 0 && !ept && NODE_SUM_TABLE &&
+        N * T * 256 * (int64_t)table_groups <= (int64_t)NODE_SUM_TABLE_MAX_MB << 20) {
       NodeTableArgs ta{ws.X, N, w->pre_w, w->pre_b, w->pre_bf, NO, table_groups, ws.NT, ne, ws.agg, ws.seg, T,
                        w->upd_b};
       ProfScope prof("node_update_table", st);
