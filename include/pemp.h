@@ -161,6 +161,10 @@ int pemp_fully_graph_build(const int32_t* n_det, int B, const int64_t* det_xyt, 
  * e_cap rows and edge_index 2 * e_cap entries written as a contiguous [2, E] array. When the batch
  * exceeds either capacity nothing is written: the caller compares its read-back totals with the
  * capacities and then calls pemp_fully_graph_build with exact sizes. */
+/* mode | PEMP_BUILD_WRITE_COUNTS (capacity mode): node_off holds B + 4 entries and the build also writes the batch's
+ * (N, E, overflow) at node_off[B + 1 .. B + 3] -- (0, 0, 1) for a batch past a capacity -- for
+ * pemp_mpn_forward_fully_cap with PEMP_MPN_COUNTS_IN_OFFSETS */
+#define PEMP_BUILD_WRITE_COUNTS 0x100
 int pemp_fully_graph_build_cap(const int32_t* n_det, int B, const int64_t* det_xyt, const float* det_scores, int cap,
                                const float* features, int C, const float* tagmaps, int F, int J, int H, int W,
                                int64_t n_cap, int64_t e_cap, float norm_factor, int mode, float* x,
@@ -442,6 +446,10 @@ typedef struct pemp_mpn_desc {
 } pemp_mpn_desc;
 
 #define PEMP_MPN_PREPARED 1
+/* pemp_mpn_forward_fully_cap only: node_off holds B + 4 entries, the last three the batch's (N, E, overflow) as
+ * pemp_fully_graph_build_cap wrote them with PEMP_BUILD_WRITE_COUNTS: the forward reads them instead of deriving
+ * them from n_det in a launch of its own */
+#define PEMP_MPN_COUNTS_IN_OFFSETS 2
 
 size_t pemp_mpn_workspace_size(const pemp_mpn_desc* desc, int64_t N, int64_t E);
 /* x [N,node_in_dim], edge_attr [E,edge_attr_dim], edge_index [2,E] (row 0 source j, row 1

@@ -12,6 +12,8 @@ LIB_PATH = os.environ.get("PEMP_LIB") or os.path.join(os.path.dirname(os.path.ab
 ABI_VERSION = 20
 
 ERR_INVALID_ARG, ERR_HIP, ERR_WORKSPACE, ERR_UNSUPPORTED = -1, -2, -3, -4
+BUILD_WRITE_COUNTS = 0x100          # pemp.h PEMP_BUILD_WRITE_COUNTS
+MPN_PREPARED, MPN_COUNTS_IN_OFFSETS = 1, 2   # pemp.h PEMP_MPN_* desc flags
 
 c_i32, c_i64, c_f32, c_sz, c_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 

@@ -749,6 +749,7 @@ struct FusedGraphArgs {
   float norm;
   int64_t n_total, e_total;   // exact totals, or capacities (capacity mode)
   int capacity;               // 1: totals come from n_det on the device; nothing is written if they exceed
+  int write_counts;           // capacity mode, PEMP_BUILD_WRITE_COUNTS: (N, E, overflow) at node_off_out[B + 1 ..]
   int node_blocks;
   float *x, *jsc, *jtag, *edge_attr;
   int64_t *jdet, *bidx, *ei;
@@ -796,6 +797,12 @@ __global__ __launch_bounds__(256) void fused_fully_graph_kernel(FusedGraphArgs a
   // the cap were never written) writes nothing and the host rebuilds it with exact sizes
   const int64_t n_total = a.capacity ? (int64_t)noff[B] : a.n_total;
   const int64_t e_total = a.capacity ? (int64_t)eoff[B] : a.e_total;
+  if (a.write_counts && blockIdx.x == 0 && threadIdx.x == 0) {   // (N, E, overflow) for the capacity-mode MPN
+    const bool over = n_total > a.n_total || e_total > a.e_total || over_cap;
+    a.node_off_out[B + 1] = over ? 0 : n_total;
+    a.node_off_out[B + 2] = over ? 0 : e_total;
+    a.node_off_out[B + 3] = over ? 1 : 0;
+  }
   if (a.capacity && (n_total > a.n_total || e_total > a.e_total || over_cap)) return;
   if (a.node_off_out && blockIdx.x == 0)   // per-image node offsets for pemp_mpn_forward_fully
     for (int i = threadIdx.x; i <= B; i += blockDim.x) a.node_off_out[i] = noff[i];
@@ -943,6 +950,10 @@ static int fully_graph_build(const int32_t* n_det, int B, const int64_t* det_xyt
                  "pemp_fully_graph_build: bad shape (B must be in [1, %d])", FUSED_MAXB);
   PEMP_CHECK_ARG(!tagmaps || (joint_tags && F > 0 && F <= C), "pemp_fully_graph_build: tags need F in [1, C]");
   PEMP_CHECK_ARG(e_total == 0 || (edge_index && edge_attr), "pemp_fully_graph_build: null edge outputs");
+  const int write_counts = (mode & PEMP_BUILD_WRITE_COUNTS) ? 1 : 0;
+  mode &= ~PEMP_BUILD_WRITE_COUNTS;
+  PEMP_CHECK_ARG(!write_counts || (capacity && node_off_out),
+                 "pemp_fully_graph_build: PEMP_BUILD_WRITE_COUNTS needs the capacity build and node_off");
   const int A = ef_width(mode, J);
   if (A < 0) { set_error("pemp_fully_graph_build: unknown edge feature mode %d", mode); return PEMP_ERR_INVALID_ARG; }
   if (const int rc = ef_tag_check(mode, tagmaps, F, "pemp_fully_graph_build")) return rc;
@@ -950,7 +961,7 @@ static int fully_graph_build(const int32_t* n_det, int B, const int64_t* det_xyt
   FusedGraphArgs a{};
   a.n_det = n_det; a.B = B; a.cap = cap; a.C = C; a.F = F; a.J = J; a.H = H; a.W = W; a.mode = mode; a.A = A;
   a.det = det_xyt; a.det_sc = det_scores; a.feat = features; a.tags = tagmaps; a.norm = norm_factor;
-  a.n_total = n_total; a.e_total = e_total; a.capacity = capacity;
+  a.n_total = n_total; a.e_total = e_total; a.capacity = capacity; a.write_counts = write_counts;
   a.node_blocks = grid_for(n_total * C, 256, 4096);
   const int edge_blocks = e_total > 0 ? grid_for(e_total, 256, 8192) : 0;
   a.x = x; a.jsc = joint_scores; a.jtag = joint_tags; a.edge_attr = edge_attr;

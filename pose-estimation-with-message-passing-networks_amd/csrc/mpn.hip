@@ -234,7 +234,7 @@ __device__ __forceinline__ float scan_max_bwd(float v, const SegMask& m) {
 // Workspace
 // ---------------------------------------------------------------------------------------------
 struct MpnWs {
-  int *cnt, *seg, *wg_start, *perm, *s_src, *s_dst, *s_orig, *err, *sym;
+  int *cnt, *seg, *wg_start, *perm, *s_src, *s_dst, *s_orig, *err, *sym, *xcd_map;
   float *X, *NT, *agg, *Q0, *EA, *EB, *img, *eimg;
   int4* ranges;
 };
@@ -264,6 +264,7 @@ static MpnWs mpn_carve(void* base, int T, int64_t N, int64_t E, size_t* bytes) {
   w.img = c.take<float>(IMG_FLOATS);
   const int G = std::max(num_cus(), T);        // edge-pass grid (at most)
   w.ranges = c.take<int4>((size_t)G * (EDGE_WAVES + 12));
+  w.xcd_map = c.take<int>(G);                           // edge passes: physical -> logical workgroup (xcd_map_fill)
   w.eimg = c.take<float>((size_t)T * EIMG_MAX_STRIDE);   // edge-pass weight image when the caller has none
   w.sym = c.take<int>(3 * N);                           // symmetric prepare: row bounds + check flags per node
   if (bytes) *bytes = c.used;
@@ -1390,6 +1391,7 @@ struct EdgeStepArgs {
   unsigned long long* stamps;   // diagnostic builds (-DPEMP_STAMPS) only: per-wave phase timestamps
   const int64_t* ne;            // capacity mode: device-side (N, E); N / E above are then the capacities
   int rec;                      // capacity mode: edge_logits is the base, the pass writes row rec (of E)
+  const int* xcd_map;           // physical -> logical workgroup (xcd_map_fill), or NULL: the contiguous XCD split
 };
 
 // Diagnostic phase timestamps (-DPEMP_STAMPS builds only; tools/edge_timeline.py): lane 0 of each
@@ -1683,9 +1685,58 @@ __device__ inline void edge_ranges_fill(const int* seg, const int* wg_start, con
   }
 }
 
+// XCD-local placement of the edge passes' workgroups (PEMP_XCD_MAP 2, the default). Logical block j of source type t
+// covers the j-th of gt equal shares of the type's edges, which are sorted by target: about the targets
+// [j / gt, (j + 1) / gt) of N. Physical blocks b and b + 8 share an XCD (round-robin dispatch; for speed only), so
+// logical block (t, j) goes to XCD floor(8 (j + 1/2) / gt): each XCD gathers the node-table rows of an eighth of the
+// targets -- one image at C3 -- for every type, instead of the rows of every target for a few types, which every XCD's
+// L2 then fetched again. Each XCD holds G / 8 blocks (G % 8 == 0); a block whose XCD is full takes a free slot of
+// another, in XCD order. Ranks are stable in the logical index (ballots), so the placement is deterministic. One
+// 256-thread block, G <= 256; which workgroup runs a logical block never changes a result.
+__device__ void xcd_map_fill(const int* __restrict__ wg_start, int T, int G, int* __restrict__ map) {
+  __shared__ int per_w[4][8], ovf_w[4];
+  const int lb = threadIdx.x, lane = lb & 63, wave = lb >> 6;
+  const bool on = lb < G;
+  int pref = lb & 7;                                  // blocks past the types' (idle): spread
+  const int used = wg_start[T];
+  if (on && lb < used) {
+    int t = 0;
+    while (t + 1 < T && wg_start[t + 1] <= lb) ++t;
+    const int j = lb - wg_start[t], gt = wg_start[t + 1] - wg_start[t];
+    pref = min(7, (8 * j + 4) / max(gt, 1));
+  }
+  const uint64_t lt = (1ull << lane) - 1ull;
+  int rank = 0;
+#pragma unroll
+  for (int x = 0; x < 8; ++x) {
+    const uint64_t m = __ballot(on && pref == x);
+    if (lane == 0) per_w[wave][x] = __popcll(m);
+    if (pref == x) rank = __popcll(m & lt);
+  }
+  __syncthreads();
+  for (int w2 = 0; w2 < wave; ++w2) rank += per_w[w2][pref];
+  const int cap = G >> 3;
+  const bool placed = on && rank < cap;
+  if (placed) map[8 * rank + pref] = lb;
+  const uint64_t om = __ballot(on && !placed);
+  if (lane == 0) ovf_w[wave] = __popcll(om);
+  __syncthreads();
+  if (on && !placed) {
+    int o = __popcll(om & lt);
+    for (int w2 = 0; w2 < wave; ++w2) o += ovf_w[w2];
+    for (int x = 0; x < 8; ++x) {
+      const int cx = min(cap, per_w[0][x] + per_w[1][x] + per_w[2][x] + per_w[3][x]), f = cap - cx;
+      if (o < f) { map[8 * (cx + o) + x] = lb; break; }
+      o -= f;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void edge_ranges_kernel(const int* seg, const int* wg_start, const int* s_dst, int T,
-                                                          int64_t N, int G, int4* ranges, const int64_t* ne) {
+                                                          int64_t N, int G, int4* ranges, const int64_t* ne,
+                                                          int* xcd_map) {
   if (ne) N = ne[0];   // capacity mode: the device-side node count (N: the capacity)
+  if (xcd_map && blockIdx.x == 0) xcd_map_fill(wg_start, T, G, xcd_map);   // (uniform over block 0)
   edge_ranges_fill(seg, wg_start, s_dst, T, N, G, ranges);
 }
 
@@ -1769,7 +1820,7 @@ __device__ __forceinline__ float pemp_exp(float x) { return PEMP_FAST_EXP ? __ex
 // segment normaliser: IEEE division or v_rcp_f32 (1 ulp)
 __device__ __forceinline__ float pemp_rcp(float x) { return PEMP_FAST_RCP ? __builtin_amdgcn_rcpf(x) : 1.0f / x; }
 #ifndef PEMP_XCD_MAP
-#define PEMP_XCD_MAP 1
+#define PEMP_XCD_MAP 2   // 2: XCD-local target ranges (xcd_map_fill); 1: each XCD a contiguous run of types; 0: none
 #endif
 template <int AGG, int HEAD, int PREC, int UPD, int STAGE>
 __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_kernel(EdgeStepArgs a) {
@@ -1802,7 +1853,8 @@ __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_
   // (b % 8) * G/8 + b / 8 gives each XCD a contiguous run of logical blocks, i.e. few source types,
   // and its L2 holds only those types' node-table columns
   int lb = blockIdx.x;
-  if (PEMP_XCD_MAP && (gridDim.x & 7) == 0) lb = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  if (a.xcd_map) lb = __builtin_amdgcn_readfirstlane(a.xcd_map[blockIdx.x]);
+  else if (PEMP_XCD_MAP && (gridDim.x & 7) == 0) lb = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
   const int4 rg = a.ranges[lb * NW + wave];
   // wave-uniform by construction; readfirstlane tells hipcc (else the tile loop and every buffer access
   // downstream are compiled as divergent)
@@ -3876,7 +3928,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
                             int64_t N, int64_t E, float* edge_logits, float* node_logits, float* class_logits,
                             void* workspace, size_t workspace_bytes, void* stream, const int64_t* fully_node_off,
                             int fully_B, int fully_nmax, bool sym = false, const int32_t* cap_ndet = nullptr,
-                            int cap_det = 0, const KnnPrepArgs* knn = nullptr) {
+                            int cap_det = 0, const KnnPrepArgs* knn = nullptr, const int64_t* cap_ne = nullptr) {
   PEMP_CHECK_ARG(desc && w, "pemp_mpn_forward: null desc/weights");
   const int T = desc->num_types, J = desc->num_joints;
   PEMP_CHECK_ARG(desc->hidden == 64, "pemp_mpn_forward: hidden width must be 64 (got %d)", desc->hidden);
@@ -3940,10 +3992,12 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   const MpnWs ws = mpn_carve(workspace, T, N, E, nullptr);
   const hipStream_t st = as_stream(stream);
   const int64_t tstride = desc->types_stride > 0 ? desc->types_stride : 1;   // node_types may be a strided view
-  // capacity mode (pemp_mpn_forward_fully_cap): N and E are capacities; the device-side counts come first
-  int64_t* const ne = cap_ndet ? reinterpret_cast<int64_t*>(ws.err + 8) : nullptr;
-  if (cap_ndet) {
-    hipLaunchKernelGGL(cap_counts_kernel, dim3(1), dim3(256), 0, st, cap_ndet, fully_B, cap_det, N, E, ne);
+  // capacity mode (pemp_mpn_forward_fully_cap): N and E are capacities; the device-side counts come first -- from
+  // the capacity graph build (cap_ne: PEMP_MPN_COUNTS_IN_OFFSETS) or from a launch of their own
+  const int64_t* const ne = cap_ne ? cap_ne : cap_ndet ? reinterpret_cast<int64_t*>(ws.err + 8) : nullptr;
+  if (cap_ndet && !cap_ne) {
+    hipLaunchKernelGGL(cap_counts_kernel, dim3(1), dim3(256), 0, st, cap_ndet, fully_B, cap_det, N, E,
+                       reinterpret_cast<int64_t*>(ws.err + 8));
     PEMP_LAUNCH_CHECK();
   }
   const int64_t K = (int64_t)T * N;
@@ -3973,6 +4027,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   const EmbedLayout emb_lo = embed_layout(w->edge_emb, emb_prec);
   const bool ept = w->ept_l1_w != nullptr;
   const int edge_grid = std::max(edge_cus(E), T);   // >= wg_start[T] (see mpn_scan_kernel)
+  const bool xcd_local = PEMP_XCD_MAP == 2 && (edge_grid & 7) == 0 && edge_grid <= 256;   // (xcd_map_fill)
   const bool pub_head = edge_pub_head(*desc, *w);
   // the edge-pass weight image: the caller's (pemp_mpn_edge_image, built once per weight set) or built here
   const float* eimg = w->edge_img;
@@ -4026,7 +4081,8 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   // its chains of dependent small loads stay off the edge embedding's workgroups
   if (E > 0 && steps >= 1) {
     hipLaunchKernelGGL(edge_ranges_kernel, dim3((unsigned)std::min(64, (edge_grid * (EDGE_WAVES + 12) + 255) / 256)),
-                       dim3(256), 0, pst, ws.seg, ws.wg_start, ws.s_dst, T, N, edge_grid, ws.ranges, ne);
+                       dim3(256), 0, pst, ws.seg, ws.wg_start, ws.s_dst, T, N, edge_grid, ws.ranges, ne,
+                       xcd_local ? ws.xcd_map : nullptr);
     PEMP_LAUNCH_CHECK();
   }
   return PEMP_OK;
@@ -4241,6 +4297,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
       ea.ne = ne;
       ea.rec = rec;
       ea.write_next = !last;
+      ea.xcd_map = xcd_local ? ws.xcd_map : nullptr;
 #ifdef PEMP_STAMPS
       ea.stamps = it == g_diag_stamp_pass ? g_diag_stamps : nullptr;
 #endif
@@ -4357,7 +4414,7 @@ static int cap_forward_direct(const pemp_mpn_desc* desc, const pemp_mpn_weights*
                               void* stream) {
   return mpn_forward_impl(desc, w, x, edge_attr, nullptr, node_types, n_cap, e_cap, edge_logits, node_logits,
                           class_logits, workspace, workspace_bytes, stream, node_off, B, det_cap, false, n_det,
-                          det_cap);
+                          det_cap, nullptr, (desc->flags & PEMP_MPN_COUNTS_IN_OFFSETS) ? node_off + B + 1 : nullptr);
 }
 
 // Graph statistics for the tests (pemp_mpn_graph_stats): captures made, replays launched, captures refused.

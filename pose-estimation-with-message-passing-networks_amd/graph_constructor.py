@@ -8,6 +8,7 @@ Host synchronisation: one count read-back after detection (the reference syncs a
 ``nonzero``), plus one more for knn graphs.
 """
 import ctypes
+import os
 import threading
 
 import numpy as np
@@ -52,6 +53,11 @@ def _tag_knn(edge_index, ws, offs, node_off, node_off_h):
     alive by the tag, never reused by a later build), offs the byte offsets of its rows / row starts / edge
     counts (pemp_knn_rows_layout); the version detects in-place edits of edge_index."""
     edge_index._pemp_knn = (ws, offs, node_off, node_off_h, edge_index._version)
+
+
+# the capacity graph build hands the capacity-mode MPN the batch's (N, E, overflow) (PEMP_BUILD_WRITE_COUNTS), so the
+# forward starts without a counting launch of its own; PEMP_NO_BUILD_COUNTS=1 restores that launch (A/B runs)
+_BUILD_COUNTS = not os.environ.get("PEMP_NO_BUILD_COUNTS")
 
 
 def get_graph_constructor(config, **kwargs):
@@ -294,13 +300,16 @@ class NaiveGraphConstructor:
                     torch.empty(n_cap, F, dtype=torch.float32, device=dev) if tags is not None else None,
                     torch.empty(2 * e_cap, dtype=torch.int64, device=dev),
                     torch.empty(e_cap, A, dtype=torch.float32, device=dev),
-                    torch.empty(B + 1, dtype=torch.int64, device=dev))          # node offsets (MPN fast path)
+                    # node offsets (MPN fast path), then the batch's (N, E, overflow) for the capacity-mode MPN
+                    torch.empty(B + 4, dtype=torch.int64, device=dev))
             build_args = (_lib.ptr(n_det), B, _lib.ptr(det), _lib.ptr(dsc), cap, _lib.ptr(feats), C, _lib.ptr(tags), F,
-                          J, H, W, n_cap, e_cap, norm, mode, *[_lib.ptr(t) for t in bufs], st)
+                          J, H, W, n_cap, e_cap, norm, mode | (_lib.BUILD_WRITE_COUNTS if _BUILD_COUNTS else 0),
+                          *[_lib.ptr(t) for t in bufs], st)
             mpn = NaiveGraphConstructor._bound_mpn
             if mpn is not None and not projected and J == getattr(mpn, "num_types", None):
                 pending_mpn = mpn
-                launch_mpn = mpn._prepare_cap(bufs[0], bufs[6], bufs[1], n_cap, e_cap, n_det, cap, bufs[7], B)
+                launch_mpn = mpn._prepare_cap(bufs[0], bufs[6], bufs[1], n_cap, e_cap, n_det, cap, bufs[7], B,
+                                              counts_in_off=_BUILD_COUNTS)
         detect = self._detect(L)
         detect_args = (self._detect_src(sm), _lib.ptr(masks), B, J, H, W, self.pool_kernel_size, thr, int(use_thr), topk, 3,
                        _lib.ptr(ws), ws.numel(), _lib.ptr(det), _lib.ptr(dsc), _lib.ptr(n_det), cap, counts_h.ctypes.data,

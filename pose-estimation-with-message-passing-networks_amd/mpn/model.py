@@ -314,6 +314,15 @@ class NodeClassificationMPNSimple(nn.Module):
             self._desc_ref = ctypes.byref(self._desc)
             self._desc_key = dkey
         desc, n_rec = self._desc_ref, self._n_rec
+        if counts_in_off:   # node_off [B + 4]: the build wrote the batch's (N, E, overflow) after the offsets
+            if getattr(self, "_desc_cnt_key", None) != dkey:
+                d = self._desc
+                self._desc_cnt = _lib.PempMpnDesc(d.num_types, d.num_joints, d.steps, d.aux_loss_steps, d.aggr,
+                                                  d.hidden, d.edge_attr_dim, d.node_in_dim, d.precision,
+                                                  d.types_stride, _lib.MPN_COUNTS_IN_OFFSETS)
+                self._desc_cnt_ref = ctypes.byref(self._desc_cnt)
+                self._desc_cnt_key = dkey
+            desc = self._desc_cnt_ref
         ws = self._ws.get(L.pemp_mpn_workspace_size(desc, N, E), dev)
         st = _lib.stream(dev)
         # the three logit arrays share one allocation (one caching-allocator call per forward instead of
@@ -360,16 +369,16 @@ class NodeClassificationMPNSimple(nn.Module):
 
 
     # ---- capacity mode (graph_constructor.bind_mpn): the forward queued before the detection counts are known ----
-    def _forward_cap(self, x, edge_attr, joint_det, n_cap, e_cap, n_det, det_cap, node_off, B):
+    def _forward_cap(self, x, edge_attr, joint_det, n_cap, e_cap, n_det, det_cap, node_off, B, counts_in_off=False):
         """Queue pemp_mpn_forward_fully_cap on the capacity buffers of pemp_fully_graph_build_cap (x [n_cap, C],
         edge_attr [e_cap, A], joint_det [n_cap, 3], node_off [B + 1]) with the detection's device counts n_det.
         Returns the pending result (logit buffer + the key it was computed under) or None when this model / batch
         takes the exact forward (training, type summaries, unfused node MLPs, a detection capacity past the
         closed-form limit, over-size capacities)."""
-        launch = self._prepare_cap(x, edge_attr, joint_det, n_cap, e_cap, n_det, det_cap, node_off, B)
+        launch = self._prepare_cap(x, edge_attr, joint_det, n_cap, e_cap, n_det, det_cap, node_off, B, counts_in_off)
         return None if launch is None else launch()
 
-    def _prepare_cap(self, x, edge_attr, joint_det, n_cap, e_cap, n_det, det_cap, node_off, B):
+    def _prepare_cap(self, x, edge_attr, joint_det, n_cap, e_cap, n_det, det_cap, node_off, B, counts_in_off=False):
         """_forward_cap in two halves: the host preparation (weights, descriptor, workspace, logit buffer) now,
         and the returned launch() that queues the call and returns the pending result (or None); None when this
         model / batch takes the exact forward. The graph constructor prepares before its first launch and calls
@@ -392,6 +401,15 @@ class NodeClassificationMPNSimple(nn.Module):
             self._desc_ref = ctypes.byref(self._desc)
             self._desc_key = dkey
         desc, n_rec = self._desc_ref, self._n_rec
+        if counts_in_off:   # node_off [B + 4]: the build wrote the batch's (N, E, overflow) after the offsets
+            if getattr(self, "_desc_cnt_key", None) != dkey:
+                d = self._desc
+                self._desc_cnt = _lib.PempMpnDesc(d.num_types, d.num_joints, d.steps, d.aux_loss_steps, d.aggr,
+                                                  d.hidden, d.edge_attr_dim, d.node_in_dim, d.precision,
+                                                  d.types_stride, _lib.MPN_COUNTS_IN_OFFSETS)
+                self._desc_cnt_ref = ctypes.byref(self._desc_cnt)
+                self._desc_cnt_key = dkey
+            desc = self._desc_cnt_ref
         ws = self._ws.get(L.pemp_mpn_workspace_size(desc, n_cap, e_cap), dev)
         ne, nn_ = max(n_rec, 1) * e_cap, (n_rec + 1) * n_cap
         a1 = (ne + 63) // 64 * 64
