@@ -314,15 +314,6 @@ class NodeClassificationMPNSimple(nn.Module):
             self._desc_ref = ctypes.byref(self._desc)
             self._desc_key = dkey
         desc, n_rec = self._desc_ref, self._n_rec
-        if counts_in_off:   # node_off [B + 4]: the build wrote the batch's (N, E, overflow) after the offsets
-            if getattr(self, "_desc_cnt_key", None) != dkey:
-                d = self._desc
-                self._desc_cnt = _lib.PempMpnDesc(d.num_types, d.num_joints, d.steps, d.aux_loss_steps, d.aggr,
-                                                  d.hidden, d.edge_attr_dim, d.node_in_dim, d.precision,
-                                                  d.types_stride, _lib.MPN_COUNTS_IN_OFFSETS)
-                self._desc_cnt_ref = ctypes.byref(self._desc_cnt)
-                self._desc_cnt_key = dkey
-            desc = self._desc_cnt_ref
         ws = self._ws.get(L.pemp_mpn_workspace_size(desc, N, E), dev)
         st = _lib.stream(dev)
         # the three logit arrays share one allocation (one caching-allocator call per forward instead of
