@@ -472,13 +472,8 @@ __device__ __forceinline__ void load_unit(const float* __restrict__ s, const Det
 
 // PROJ: 0 dense maps, 1 projected, 2 projected separable. TP: the threshold is positive, so !(v < thr) alone
 // decides a threshold pixel (v = 0 fails it; NaN passes both forms): one compare per pixel fewer.
-#ifdef NMS_WAVES_PER_EU   // (A/B builds: cap the strip kernel's VGPRs for more resident waves per SIMD)
-#define NMS_OCC_ATTR __attribute__((amdgpu_waves_per_eu(NMS_WAVES_PER_EU, NMS_WAVES_PER_EU)))
-#else
-#define NMS_OCC_ATTR
-#endif
 template <int P, int MODE, bool MASKED, int PROJ, bool TP = false>
-__global__ __launch_bounds__(NT1) NMS_OCC_ATTR void nms_strips_kernel(
+__global__ __launch_bounds__(NT1) void nms_strips_kernel(
     const float* __restrict__ s, const float* __restrict__ masks, DetectGeom g, float thr, int use_thr,
     float* __restrict__ cand_v, int* __restrict__ cand_i, float* __restrict__ neg_v, int* __restrict__ neg_i,
     int* __restrict__ tile_count, int* __restrict__ tile_nonneg, cmask_t* __restrict__ cbits, ProjArgs pj,

@@ -234,7 +234,7 @@ __device__ __forceinline__ float scan_max_bwd(float v, const SegMask& m) {
 // Workspace
 // ---------------------------------------------------------------------------------------------
 struct MpnWs {
-  int *cnt, *seg, *wg_start, *perm, *s_src, *s_dst, *s_orig, *err, *sym, *xcd_map;
+  int *cnt, *seg, *wg_start, *perm, *s_src, *s_dst, *s_orig, *err, *sym;
   float *X, *NT, *agg, *Q0, *EA, *EB, *img, *eimg;
   int4* ranges;
 };
@@ -264,7 +264,6 @@ static MpnWs mpn_carve(void* base, int T, int64_t N, int64_t E, size_t* bytes) {
   w.img = c.take<float>(IMG_FLOATS);
   const int G = std::max(num_cus(), T);        // edge-pass grid (at most)
   w.ranges = c.take<int4>((size_t)G * (EDGE_WAVES + 12));
-  w.xcd_map = c.take<int>(G);                           // edge passes: physical -> logical workgroup (xcd_map_fill)
   w.eimg = c.take<float>((size_t)T * EIMG_MAX_STRIDE);   // edge-pass weight image when the caller has none
   w.sym = c.take<int>(3 * N);                           // symmetric prepare: row bounds + check flags per node
   if (bytes) *bytes = c.used;
@@ -1391,7 +1390,6 @@ struct EdgeStepArgs {
   unsigned long long* stamps;   // diagnostic builds (-DPEMP_STAMPS) only: per-wave phase timestamps
   const int64_t* ne;            // capacity mode: device-side (N, E); N / E above are then the capacities
   int rec;                      // capacity mode: edge_logits is the base, the pass writes row rec (of E)
-  const int* xcd_map;           // physical -> logical workgroup (xcd_map_fill), or NULL: the contiguous XCD split
 };
 
 // Diagnostic phase timestamps (-DPEMP_STAMPS builds only; tools/edge_timeline.py): lane 0 of each
@@ -1685,58 +1683,9 @@ __device__ inline void edge_ranges_fill(const int* seg, const int* wg_start, con
   }
 }
 
-// XCD-local placement of the edge passes' workgroups (PEMP_XCD_MAP 2, the default). Logical block j of source type t
-// covers the j-th of gt equal shares of the type's edges, which are sorted by target: about the targets
-// [j / gt, (j + 1) / gt) of N. Physical blocks b and b + 8 share an XCD (round-robin dispatch; for speed only), so
-// logical block (t, j) goes to XCD floor(8 (j + 1/2) / gt): each XCD gathers the node-table rows of an eighth of the
-// targets -- one image at C3 -- for every type, instead of the rows of every target for a few types, which every XCD's
-// L2 then fetched again. Each XCD holds G / 8 blocks (G % 8 == 0); a block whose XCD is full takes a free slot of
-// another, in XCD order. Ranks are stable in the logical index (ballots), so the placement is deterministic. One
-// 256-thread block, G <= 256; which workgroup runs a logical block never changes a result.
-__device__ void xcd_map_fill(const int* __restrict__ wg_start, int T, int G, int* __restrict__ map) {
-  __shared__ int per_w[4][8], ovf_w[4];
-  const int lb = threadIdx.x, lane = lb & 63, wave = lb >> 6;
-  const bool on = lb < G;
-  int pref = lb & 7;                                  // blocks past the types' (idle): spread
-  const int used = wg_start[T];
-  if (on && lb < used) {
-    int t = 0;
-    while (t + 1 < T && wg_start[t + 1] <= lb) ++t;
-    const int j = lb - wg_start[t], gt = wg_start[t + 1] - wg_start[t];
-    pref = min(7, (8 * j + 4) / max(gt, 1));
-  }
-  const uint64_t lt = (1ull << lane) - 1ull;
-  int rank = 0;
-#pragma unroll
-  for (int x = 0; x < 8; ++x) {
-    const uint64_t m = __ballot(on && pref == x);
-    if (lane == 0) per_w[wave][x] = __popcll(m);
-    if (pref == x) rank = __popcll(m & lt);
-  }
-  __syncthreads();
-  for (int w2 = 0; w2 < wave; ++w2) rank += per_w[w2][pref];
-  const int cap = G >> 3;
-  const bool placed = on && rank < cap;
-  if (placed) map[8 * rank + pref] = lb;
-  const uint64_t om = __ballot(on && !placed);
-  if (lane == 0) ovf_w[wave] = __popcll(om);
-  __syncthreads();
-  if (on && !placed) {
-    int o = __popcll(om & lt);
-    for (int w2 = 0; w2 < wave; ++w2) o += ovf_w[w2];
-    for (int x = 0; x < 8; ++x) {
-      const int cx = min(cap, per_w[0][x] + per_w[1][x] + per_w[2][x] + per_w[3][x]), f = cap - cx;
-      if (o < f) { map[8 * (cx + o) + x] = lb; break; }
-      o -= f;
-    }
-  }
-}
-
 __global__ __launch_bounds__(256) void edge_ranges_kernel(const int* seg, const int* wg_start, const int* s_dst, int T,
-                                                          int64_t N, int G, int4* ranges, const int64_t* ne,
-                                                          int* xcd_map) {
+                                                          int64_t N, int G, int4* ranges, const int64_t* ne) {
   if (ne) N = ne[0];   // capacity mode: the device-side node count (N: the capacity)
-  if (xcd_map && blockIdx.x == 0) xcd_map_fill(wg_start, T, G, xcd_map);   // (uniform over block 0)
   edge_ranges_fill(seg, wg_start, s_dst, T, N, G, ranges);
 }
 
@@ -1820,7 +1769,7 @@ __device__ __forceinline__ float pemp_exp(float x) { return PEMP_FAST_EXP ? __ex
 // segment normaliser: IEEE division or v_rcp_f32 (1 ulp)
 __device__ __forceinline__ float pemp_rcp(float x) { return PEMP_FAST_RCP ? __builtin_amdgcn_rcpf(x) : 1.0f / x; }
 #ifndef PEMP_XCD_MAP
-#define PEMP_XCD_MAP 2   // 2: XCD-local target ranges (xcd_map_fill); 1: each XCD a contiguous run of types; 0: none
+#define PEMP_XCD_MAP 1
 #endif
 template <int AGG, int HEAD, int PREC, int UPD, int STAGE>
 __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_kernel(EdgeStepArgs a) {
@@ -1853,8 +1802,9 @@ __global__ __launch_bounds__((64 * edge_waves_s<HEAD, STAGE>())) void edge_step_
   // (b % 8) * G/8 + b / 8 gives each XCD a contiguous run of logical blocks, i.e. few source types,
   // and its L2 holds only those types' node-table columns
   int lb = blockIdx.x;
-  if (a.xcd_map) lb = __builtin_amdgcn_readfirstlane(a.xcd_map[blockIdx.x]);
-  else if (PEMP_XCD_MAP && (gridDim.x & 7) == 0) lb = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  // (round 6: placing each XCD's workgroups on an eighth of the targets for every type instead -- one image's node-table
+  // rows per XCD -- fetched 113.5 vs 107.8 MB per c3 pass and was no faster; profiles/r06_build_counts_xcd.md)
+  if (PEMP_XCD_MAP && (gridDim.x & 7) == 0) lb = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
   const int4 rg = a.ranges[lb * NW + wave];
   // wave-uniform by construction; readfirstlane tells hipcc (else the tile loop and every buffer access
   // downstream are compiled as divergent)
@@ -4027,7 +3977,6 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   const EmbedLayout emb_lo = embed_layout(w->edge_emb, emb_prec);
   const bool ept = w->ept_l1_w != nullptr;
   const int edge_grid = std::max(edge_cus(E), T);   // >= wg_start[T] (see mpn_scan_kernel)
-  const bool xcd_local = PEMP_XCD_MAP == 2 && (edge_grid & 7) == 0 && edge_grid <= 256;   // (xcd_map_fill)
   const bool pub_head = edge_pub_head(*desc, *w);
   // the edge-pass weight image: the caller's (pemp_mpn_edge_image, built once per weight set) or built here
   const float* eimg = w->edge_img;
@@ -4081,8 +4030,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   // its chains of dependent small loads stay off the edge embedding's workgroups
   if (E > 0 && steps >= 1) {
     hipLaunchKernelGGL(edge_ranges_kernel, dim3((unsigned)std::min(64, (edge_grid * (EDGE_WAVES + 12) + 255) / 256)),
-                       dim3(256), 0, pst, ws.seg, ws.wg_start, ws.s_dst, T, N, edge_grid, ws.ranges, ne,
-                       xcd_local ? ws.xcd_map : nullptr);
+                       dim3(256), 0, pst, ws.seg, ws.wg_start, ws.s_dst, T, N, edge_grid, ws.ranges, ne);
     PEMP_LAUNCH_CHECK();
   }
   return PEMP_OK;
@@ -4297,7 +4245,6 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
       ea.ne = ne;
       ea.rec = rec;
       ea.write_next = !last;
-      ea.xcd_map = xcd_local ? ws.xcd_map : nullptr;
 #ifdef PEMP_STAMPS
       ea.stamps = it == g_diag_stamp_pass ? g_diag_stamps : nullptr;
 #endif
