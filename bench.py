@@ -13,6 +13,7 @@ Prints ONE JSON line (rank 0). Extra fields: isolated-MPN edge-updates/s, live r
 dominant kernel (hipEvents on the launch stream), and the CPU oracle baseline (rank 0, N=1).
 """
 import argparse
+import ctypes
 import json
 import math
 import os
@@ -526,7 +527,40 @@ def frontend_heatmaps(wl, gc, feats, dev, reps=5):
         s, t = ph.materialize()
         return graph(s, t)
 
+    # detection alone (the front-end's consumer): the plateau-duplicated peaks of bilinear x2 give ~600 detections
+    # per image, so a whole construct_graph here is dominated by its fully graph build, not by the front-end
+    gcobj = pemp_amd.get_graph_constructor(gc, scoremaps=ph, features=feats, tagmaps=ph, joints_gt=None,
+                                           factor_list=None, masks=None, device=dev, testing=True, heatmaps=None,
+                                           num_joints=J)
+    L, st = _lib.lib(), _lib.stream(dev)
+    use_thr = gcobj.detect_threshold is not None
+    topk = gcobj.hybrid_k if use_thr else 20
+    thr = float(gcobj.detect_threshold) if use_thr else 0.0
+    ws = torch.empty(L.pemp_detect_workspace_size(B, J, H, W, topk), dtype=torch.uint8, device=dev)
+    cap = 64 * J
+    det = torch.empty(B, cap, 3, dtype=torch.int64, device=dev)
+    dsc = torch.empty(B, cap, dtype=torch.float32, device=dev)
+    n_det = torch.empty(B, dtype=torch.int32, device=dev)
+    pc = ph.c_struct()
+
+    def detect(fn, src):
+        _lib.check(fn(src, None, B, J, H, W, gcobj.pool_kernel_size, thr, int(use_thr), topk, 3, _lib.ptr(ws),
+                      ws.numel(), _lib.ptr(det), _lib.ptr(dsc), _lib.ptr(n_det), cap, None, st))
+
+    def dense_detect():
+        s, _ = ph.materialize()
+        detect(L.pemp_detect, _lib.ptr(s))
+
     res = {}
+    for name, fn in (("reference_ops_then_detect_ms", dense_detect),
+                     ("projected_detect_ms", lambda: detect(L.pemp_detect_projected, ctypes.addressof(pc)))):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(4 * reps):
+            fn()
+        torch.cuda.synchronize()
+        res[name] = round((time.perf_counter() - t0) / (4 * reps) * 1e3, 3)
     for name, fn in (("reference_ops_then_construct_graph_ms", dense),
                      ("projected_construct_graph_ms", lambda: graph(ph, ph))):
         fn()
@@ -537,13 +571,18 @@ def frontend_heatmaps(wl, gc, feats, dev, reps=5):
         torch.cuda.synchronize()
         res[name] = round((time.perf_counter() - t0) / reps * 1e3, 3)
         res["nodes"] = int(out[0].shape[0])
-    _lib.prof_enable("detect_nms_projected")
-    graph(ph, ph)
+    s_dense, _ = ph.materialize()
     torch.cuda.synchronize()
-    st = _lib.prof_report()
+    _lib.prof_enable("*")
+    for _ in range(reps):
+        detect(L.pemp_detect, _lib.ptr(s_dense))
+        detect(L.pemp_detect_projected, ctypes.addressof(pc))
+    torch.cuda.synchronize()
+    prof = _lib.prof_report()
     _lib.prof_enable(None)
-    n, ms = st.get("detect_nms_projected", (1, float("nan")))
-    res["detect_nms_projected_us"] = round(ms / n * 1e3, 2)
+    for k in ("detect_nms", "detect_nms_projected"):
+        n, ms = prof.get(k, (1, float("nan")))
+        res[k + "_us"] = round(ms / n * 1e3, 2)
     res["inputs"] = f"2 passes x [{B}, {2 * J}, {h}, {w}] fp32 -> [{B}, {J}, {H}, {W}] scoremaps + [{B}, {J}, {H}, {W}, 2] tags"
     res["dense_bytes_written_by_reference_ops"] = B * J * H * W * 4 * 3
     return res

@@ -2802,6 +2802,13 @@ struct NodeTableArgs {
   const float* upd_b;
 };
 
+#ifndef PEMP_NODE_ON_SIDE
+#define PEMP_NODE_ON_SIDE 1   // the first node step on the prelude side stream, the edge prelude on the launch stream
+#endif
+#ifndef PEMP_NODE_ON_SIDE_MIN_E
+#define PEMP_NODE_ON_SIDE_MIN_E 65536   // below this many edges (capacity) the other order: c2 (one image, ~22k edges)
+                                        // measured a 160 vs 202 us step span with the node step on the side
+#endif
 #ifndef EMBED_ON_SIDE
 #define EMBED_ON_SIDE 1   // capacity mode: the edge embedding on the prelude side stream (see mpn_forward_impl)
 #endif
@@ -4081,6 +4088,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   // middle steps of the attention model (update block in the edge pass, no heads): the node update runs inside the
   // node-table launch (node_table_kernel<PREC, 1, true>) instead of a launch of its own
   const unsigned table_grid1 = (unsigned)(((N + 15) / 16) * table_groups);
+  hipStream_t nst = st;   // stream of the node kernels (the first node step runs on the prelude side stream)
   auto node_step = [&](int mode, bool table, int slot, bool dup) -> int {
     // (every column group re-reads the tile's aggregates: worth it while those re-reads stay small -- C2 -- not at
     // C3, where they are ~100 MB per call and the fused launch only ties the two it replaces. Round 6: a wide form,
@@ -4090,26 +4098,26 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
         N * T * 256 * (int64_t)table_groups <= (int64_t)NODE_SUM_TABLE_MAX_MB << 20) {
       NodeTableArgs ta{ws.X, N, w->pre_w, w->pre_b, w->pre_bf, NO, table_groups, ws.NT, ne, ws.agg, ws.seg, T,
                        w->upd_b};
-      ProfScope prof("node_update_table", st);
+      ProfScope prof("node_update_table", nst);
       if (table_prec == PEMP_PREC_F16X3)
-        hipLaunchKernelGGL((node_table_kernel<2, 1, true>), dim3(table_grid1), dim3(256), 0, st, ta);
+        hipLaunchKernelGGL((node_table_kernel<2, 1, true>), dim3(table_grid1), dim3(256), 0, nst, ta);
       else if (table_prec == PEMP_PREC_BF16X3)
-        hipLaunchKernelGGL((node_table_kernel<1, 1, true>), dim3(table_grid1), dim3(256), 0, st, ta);
+        hipLaunchKernelGGL((node_table_kernel<1, 1, true>), dim3(table_grid1), dim3(256), 0, nst, ta);
       else
-        hipLaunchKernelGGL((node_table_kernel<0, 1, true>), dim3(table_grid1), dim3(256), 0, st, ta);
+        hipLaunchKernelGGL((node_table_kernel<0, 1, true>), dim3(table_grid1), dim3(256), 0, nst, ta);
       PEMP_LAUNCH_CHECK();
       return PEMP_OK;
     }
     if (mode == -1 && w->upd_mlp.n_layers > 0) {     // hierarchical update MLP (dense-folded)
       NodeMlpArgs ma{ws.agg, ws.seg, T, N, w->upd_mlp, nmlp_max_out(w->upd_mlp), ws.X, ne};
-      ProfScope prof("node_update", st);
-      hipLaunchKernelGGL(node_mlp_kernel, dim3(node_grid), dim3(256), nmlp_lds_bytes(T, w->upd_mlp), st, ma);
+      ProfScope prof("node_update", nst);
+      hipLaunchKernelGGL(node_mlp_kernel, dim3(node_grid), dim3(256), nmlp_lds_bytes(T, w->upd_mlp), nst, ma);
       PEMP_LAUNCH_CHECK();
       mode = ROWS_NONE;
     } else if (mode == -1) {                           // update MLP on non-linear aggregates
       NodeUpdateArgs ua{ws.agg, ws.seg, T, N, w->upd_w, w->upd_b, ws.X, ne};
-      ProfScope prof("node_update", st);
-      hipLaunchKernelGGL(node_update_kernel, dim3(node_grid, 4), dim3(64 * UPD_WAVES), 0, st, ua);
+      ProfScope prof("node_update", nst);
+      hipLaunchKernelGGL(node_update_kernel, dim3(node_grid, 4), dim3(64 * UPD_WAVES), 0, nst, ua);
       PEMP_LAUNCH_CHECK();
       mode = ROWS_NONE;
     }
@@ -4136,35 +4144,35 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
     na.head_floats = mlp_lds_floats(w->node_head) + mlp_lds_floats(w->class_head);
     na.emb_whole = mode == ROWS_EMBED && node_emb_whole(w->node_emb);
     if (na.mode != ROWS_NONE || na.node_out) {
-      ProfScope prof(mode == ROWS_EMBED ? "node_embed" : "node_update", st);
-      hipLaunchKernelGGL(node_rows_kernel, dim3(node_grid), dim3(256), node_rows_lds_bytes(na), st, na);
+      ProfScope prof(mode == ROWS_EMBED ? "node_embed" : "node_update", nst);
+      hipLaunchKernelGGL(node_rows_kernel, dim3(node_grid), dim3(256), node_rows_lds_bytes(na), nst, na);
       PEMP_LAUNCH_CHECK();
     }
     if (slot >= 0 && !fused_heads) {
       for (int k = 0; k < (dup ? 2 : 1); ++k) {
         int r2;
-        if ((r2 = rows_mlp("heads", w->node_head, ws.X + 64, 128, N, node_logits + (int64_t)(slot + k) * N, 1, nullptr, 0, st)))
+        if ((r2 = rows_mlp("heads", w->node_head, ws.X + 64, 128, N, node_logits + (int64_t)(slot + k) * N, 1, nullptr, 0, nst)))
           return r2;
         if ((r2 = rows_mlp("heads", w->class_head, ws.X + 64, 128, N, class_logits + (int64_t)(slot + k) * N * J, J,
-                           nullptr, 0, st)))
+                           nullptr, 0, nst)))
           return r2;
       }
     }
     if (table) {
       NodeTableArgs ta{ws.X, N, w->pre_w, w->pre_b, w->pre_bf, NO, table_groups, ws.NT, ne};
-      ProfScope prof("node_table", st);
+      ProfScope prof("node_table", nst);
       if (table_prec == PEMP_PREC_F16X3)
-        hipLaunchKernelGGL(node_table_kernel<2>, dim3(table_grid), dim3(256), 0, st, ta);
+        hipLaunchKernelGGL(node_table_kernel<2>, dim3(table_grid), dim3(256), 0, nst, ta);
       else if (table_prec == PEMP_PREC_BF16X3)
-        hipLaunchKernelGGL(node_table_kernel<1>, dim3(table_grid), dim3(256), 0, st, ta);
+        hipLaunchKernelGGL(node_table_kernel<1>, dim3(table_grid), dim3(256), 0, nst, ta);
       else
-        hipLaunchKernelGGL(node_table_kernel<0>, dim3(table_grid), dim3(256), 0, st, ta);
+        hipLaunchKernelGGL(node_table_kernel<0>, dim3(table_grid), dim3(256), 0, nst, ta);
       PEMP_LAUNCH_CHECK();
       if (ept) {   // columns 0..127 of the table: the per-type node terms (zero rows in pre_w)
         NodeEptArgs xa{ws.X, node_types, tstride, T, N, w->ept_l1_w, w->ept_l1_b, w->ept_l2_w, w->ept_l2_b,
                        w->ept_o1_w, w->ept_o2_w, ws.NT, NO,
                        desc->precision == PEMP_PREC_F16X3 ? dom<2>() : 1.0f, ne};
-        hipLaunchKernelGGL(node_ept_kernel, dim3(node_grid), dim3(256), 0, st, xa);
+        hipLaunchKernelGGL(node_ept_kernel, dim3(node_grid), dim3(256), 0, nst, xa);
         PEMP_LAUNCH_CHECK();
       }
     }
@@ -4196,6 +4204,26 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
     side_lock.unlock();
     ss = nullptr;
   };
+  // PEMP_NODE_ON_SIDE (round 6, the default for E >= PEMP_NODE_ON_SIDE_MIN_E): the node embedding + first node table go to the side stream and the
+  // edge prelude (order, ranges, embedding) stays on the launch stream, so the step's critical path -- graph build ->
+  // order -> ranges -> embedding -> first pass -- carries neither the fork's nor the join's cross-stream wait (the
+  // side chain, ~20 us, is done long before the ~60 us prelude). Otherwise: the order and the range table on the side
+  // stream, the node kernels here, and the edge embedding placed as below.
+  if (ss && PEMP_NODE_ON_SIDE && E >= PEMP_NODE_ON_SIDE_MIN_E) {
+    nst = ss->s;
+    pst = st;
+    if (!fused_embed) {
+      if ((rc = rows_mlp("node_embed", w->node_emb, x, desc->node_in_dim, N, ws.X, 128, ws.X + 64, 128, nst))) {
+        nst = st;
+        join_side();
+        return rc;
+      }
+    }
+    rc = node_step(fused_embed ? ROWS_EMBED : ROWS_NONE, steps > 0, steps > 0 ? -1 : 0, false);
+    nst = st;
+    if (rc || (rc = edge_prepare()) || (rc = edge_embed())) { join_side(); return rc; }
+    join_side();
+  } else {
   // side stream: the edge order and the edge passes' range table behind it; meanwhile the node embedding + first
   // node table here (short kernels with 16-row grids); then, joined, the edge embedding (every CU, all of its LDS)
   if (ss && (rc = edge_prepare())) { join_side(); return rc; }
@@ -4223,6 +4251,7 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
     if ((rc = edge_embed())) return rc;
   } else if ((rc = edge_prepare()) || (rc = edge_embed())) {
     return rc;
+  }
   }
   float* e_cur = ws.EA;                           // r of the pass (R0 from the separate embedding)
   float* e_nxt = ws.EB;
