@@ -16,6 +16,7 @@
 // Stage 2b (emit_kernel): one workgroup per plane. Offsets from the image's per-plane counts;
 //   emits detections in the reference's order.
 #include <math.h>
+#include <cmath>
 #include <atomic>
 
 #include <type_traits>
@@ -240,8 +241,16 @@ struct ProjArgs {
   int h[PEMP_PROJ_MAXS], w[PEMP_PROJ_MAXS];
   const int* fi;                       // [J] or NULL
   float divisor;
+  float rdiv;                          // 1 / divisor when that is exact (a power of two), else 0
   int ch0;                             // first channel read (0: heatmaps; J: tags)
 };
+
+// v / divisor: a product with the exact reciprocal when the divisor is a power of two (the same real, so the
+// same rounding, for every v), the IEEE division otherwise (~10 instructions: the single-scale front-end's
+// divisor 1 took 20 of them per lane and unit)
+__device__ __forceinline__ float proj_div(const ProjArgs& pj, float v) {
+  return pj.rdiv != 0.f ? __fmul_rn(v, pj.rdiv) : div_rn(v, pj.divisor);
+}
 
 struct ProjTaps {   // one axis of the bilinear source index
   int i0, i1;
@@ -287,7 +296,26 @@ __device__ float proj_pixel(const ProjArgs& pj, int b, int j, int Y, int X, int 
     const float v = proj_scale(pj, s, b, j, proj_taps(Y, H, pj.h[s]), proj_taps(X, W, pj.w[s]));
     acc = s == 0 ? v : __fadd_rn(acc, v);
   }
-  return div_rn(acc, pj.divisor);
+  return proj_div(pj, acc);
+}
+
+// r / divisor, -inf outside the plane; the divisor's form decided once per unit, not per row (uniform)
+template <int P>
+__device__ __forceinline__ void proj_finish(const ProjArgs& pj, const DetectGeom& g, int y0, bool xok,
+                                            float (&r)[SR + 2 * P]) {
+  if (pj.rdiv != 0.f) {
+#pragma unroll
+    for (int i = 0; i < SR + 2 * P; ++i) {
+      const int y = y0 - P + i;
+      r[i] = (xok && y >= 0 && y < g.H) ? __fmul_rn(r[i], pj.rdiv) : -INFINITY;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < SR + 2 * P; ++i) {
+      const int y = y0 - P + i;
+      r[i] = (xok && y >= 0 && y < g.H) ? div_rn(r[i], pj.divisor) : -INFINITY;
+    }
+  }
 }
 
 // rows y0 - P .. y0 + SR - 1 + P of the lane's column from the projected maps; -inf outside the plane
@@ -310,99 +338,112 @@ __device__ __forceinline__ void load_unit_proj(const ProjArgs& pj, const DetectG
       r[i] = s == 0 ? v : __fadd_rn(r[i], v);
     }
   }
-#pragma unroll
-  for (int i = 0; i < SR + 2 * P; ++i) {
-    const int y = y0 - P + i;
-    r[i] = (xok && y >= 0 && y < g.H) ? div_rn(r[i], pj.divisor) : -INFINITY;
-  }
+  proj_finish<P>(pj, g, y0, xok, r);
 }
 
 // The same rows, separably: per scale and map, the horizontal interpolation of every low-resolution row
-// the unit's output rows touch (at most PROJ_LR of them: upsampling) is computed once per lane -- its
-// loads issued in groups of 8 rows under one wait -- and staged in the wave's LDS rows; the vertical
-// interpolation of each output row then reads its two staged rows. The values are bitwise those of
-// proj_pixel (same operations on the same operands). Ratios needing more rows take load_unit_proj.
+// the unit's output rows touch (at most PROJ_LR - 1 of them: upsampling) is computed once per lane and
+// staged in the wave's LDS rows; the vertical interpolation of each output row then reads its two staged
+// rows. The values are bitwise those of proj_pixel (same operations on the same operands). Ratios needing
+// more rows take load_unit_proj.
+// Loads: one SGPR buffer descriptor per map, the lane's two source columns as its only VGPR offsets and
+// the (clamped, uniform) source row as the scalar offset -- no per-load address arithmetic. The staged
+// rows run one past the unit's last source row (clamped to the map), so a row's second tap is always the
+// next stage row (i1 = i0 + 1, or at the bottom border the duplicate of row h - 1, whose horizontal value
+// is the same operands'): one ds_read2 per map and output row.
 constexpr int PROJ_LR = 16;
 
-// horizontal interpolation of rows lo .. lo + nr - 1 of both passes' maps (pl1 NULL: forward pass only)
-// into the wave's stage rows; 8 rows of both maps (32 loads) in flight per wait
-__device__ __forceinline__ void proj_rows_maps(const float* __restrict__ pl0, const float* __restrict__ pl1, int w,
-                                               int h, int lo, int nr, int x0, int x1, float lx0, float lx1,
-                                               float* __restrict__ st0, float* __restrict__ st1) {
+// horizontal interpolation of rows lo .. lo + nl - 1 (clamped to the map) of the forward pass and, FLIP,
+// the flipped pass into the wave's stage rows; groups of 4 rows of both maps (16 loads) under one wait
+template <bool FLIP>
+__device__ __forceinline__ void proj_rows_maps(const float* pl0, const float* pl1, int w, int h, int lo, int nl,
+                                               int x0, int x1, float lx0, float lx1, float* __restrict__ st0,
+                                               float* __restrict__ st1) {
   const int lane = threadIdx.x & 63;
-  const int f0 = w - 1 - x0, f1 = w - 1 - x1;   // the flipped pass's mirrored columns
+  const __amdgpu_buffer_rsrc_t r0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(pl0), 0, h * w * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r1 =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(FLIP ? pl1 : pl0), 0, h * w * 4, 0x00020000);
+  const int va = 4 * x0, vb = 4 * x1, vc = 4 * (w - 1 - x0), vd = 4 * (w - 1 - x1);   // flipped: mirrored columns
+  const int rowb = 4 * w;
 #pragma unroll
-  for (int k0 = 0; k0 < PROJ_LR; k0 += 8) {
-    if (k0 < nr) {   // (uniform)
-      float a[8], b[8], c[8], d[8];
+  for (int k0 = 0; k0 < PROJ_LR; k0 += 4) {
+    if (k0 < nl) {   // (uniform)
+      float a[4], b[4], c[4], d[4];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int row = min(lo + k0 + k, h - 1);   // rows past the range: loaded, never read
-        a[k] = pl0[row * w + x0];
-        b[k] = pl0[row * w + x1];
-        if (pl1) {
-          c[k] = pl1[row * w + f0];
-          d[k] = pl1[row * w + f1];
+      for (int k = 0; k < 4; ++k) {
+        const int so = min(lo + k0 + k, h - 1) * rowb;   // rows past the range: loaded, never read
+        a[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r0, va, so, 0));
+        b[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r0, vb, so, 0));
+        if constexpr (FLIP) {
+          c[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r1, vc, so, 0));
+          d[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r1, vd, so, 0));
         }
       }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
+      for (int k = 0; k < 4; ++k) {
         st0[(k0 + k) * 64 + lane] = __fadd_rn(__fmul_rn(a[k], lx0), __fmul_rn(b[k], lx1));
-        if (pl1) st1[(k0 + k) * 64 + lane] = __fadd_rn(__fmul_rn(c[k], lx0), __fmul_rn(d[k], lx1));
+        if constexpr (FLIP) st1[(k0 + k) * 64 + lane] = __fadd_rn(__fmul_rn(c[k], lx0), __fmul_rn(d[k], lx1));
       }
     }
   }
 }
 
-// (the host checks that every unit's rows span at most PROJ_LR low-resolution rows: proj_sep_ok)
+// (the host checks that every unit's rows span at most PROJ_LR - 1 low-resolution rows: proj_sep_ok)
+template <int P, bool FLIP, bool FIRST>
+__device__ __forceinline__ void proj_sep_scale(const ProjArgs& pj, const DetectGeom& g, int s, int b, int j, int y0,
+                                               int xc, float (&r)[SR + 2 * P], float* __restrict__ stage) {
+  const int lane = threadIdx.x & 63;
+  const int h = pj.h[s], w = pj.w[s];
+  const int ya = min(max(y0 - P, 0), g.H - 1), yb = min(max(y0 + SR + P - 1, 0), g.H - 1);
+  const int lo = proj_taps(ya, g.H, h).i0, nl = proj_taps(yb, g.H, h).i1 - lo + 2;
+  const ProjTaps tx = proj_taps(xc, g.W, w);
+  float* st0 = stage;                    // forward pass rows
+  float* st1 = stage + PROJ_LR * 64;     // flipped pass rows
+  __builtin_amdgcn_wave_barrier();   // the previous readers of the wave's rows are done
+  proj_rows_maps<FLIP>(pj.m[s] + ((size_t)b * pj.C + pj.ch0 + j) * h * w,
+                       FLIP ? pj.f[s] + ((size_t)b * pj.C + pj.ch0 + (pj.fi ? pj.fi[j] : j)) * h * w : nullptr, w, h,
+                       lo, nl, tx.i0, tx.i1, tx.l0, tx.l1, st0, st1);
+  // the rows' taps (uniform per row) computed once per unit by lanes 0 .. SR + 2P - 1 and read back as LDS
+  // broadcasts: (byte offset of the first source row in the stage, weights)
+  float4* tap = reinterpret_cast<float4*>(stage + 2 * PROJ_LR * 64);
+  if (lane < SR + 2 * P) {
+    const ProjTaps t = proj_taps(min(max(y0 - P + lane, 0), g.H - 1), g.H, h);
+    tap[lane] = make_float4(__int_as_float((t.i0 - lo) * 256), 0.f, t.l0, t.l1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const char* b0 = reinterpret_cast<const char*>(st0 + lane);
+  const char* b1 = reinterpret_cast<const char*>(st1 + lane);
+#pragma unroll
+  for (int i = 0; i < SR + 2 * P; ++i) {
+    const float4 t = tap[i];
+    const float* p0 = reinterpret_cast<const float*>(b0 + __float_as_int(t.x));
+    float v = __fadd_rn(__fmul_rn(p0[0], t.z), __fmul_rn(p0[64], t.w));
+    if constexpr (FLIP) {
+      const float* p1 = reinterpret_cast<const float*>(b1 + __float_as_int(t.x));
+      v = __fmul_rn(__fadd_rn(v, __fadd_rn(__fmul_rn(p1[0], t.z), __fmul_rn(p1[64], t.w))), 0.5f);
+    }
+    r[i] = FIRST ? v : __fadd_rn(r[i], v);
+  }
+}
+
 template <int P>
 __device__ __forceinline__ void load_unit_proj_sep(const ProjArgs& pj, const DetectGeom& g, int u,
                                                    float (&r)[SR + 2 * P], float* __restrict__ stage) {
   const int lane = threadIdx.x & 63;
-  const int plane = u / g.units, rem = u - plane * g.units, band = rem / g.nsx, strip = rem - band * g.nsx;
-  const int b = plane / g.J, j = plane - b * g.J;
-  const int y0 = band * SR, x = strip * g.sc - P + lane;
+  const UnitPos q = unit_pos(g, u);
+  const int b = q.plane / g.J, j = q.plane - b * g.J;
+  const int y0 = q.band * SR, x = q.strip * g.sc - P + lane;
   const bool xok = x >= 0 && x < g.W;
   const int xc = min(max(x, 0), g.W - 1);
-  const int ya = min(max(y0 - P, 0), g.H - 1), yb = min(max(y0 + SR + P - 1, 0), g.H - 1);
-  float* st0 = stage;                    // forward pass rows
-  float* st1 = stage + PROJ_LR * 64;     // flipped pass rows
-  for (int s = 0; s < pj.S; ++s) {
-    const int h = pj.h[s], w = pj.w[s];
-    const int lo = proj_taps(ya, g.H, h).i0, nr = proj_taps(yb, g.H, h).i1 - lo + 1;
-    const ProjTaps tx = proj_taps(xc, g.W, w);
-    const bool flip = pj.f[s] != nullptr;
-    __builtin_amdgcn_wave_barrier();   // the previous readers of the wave's rows are done
-    proj_rows_maps(pj.m[s] + ((size_t)b * pj.C + pj.ch0 + j) * h * w,
-                   flip ? pj.f[s] + ((size_t)b * pj.C + pj.ch0 + (pj.fi ? pj.fi[j] : j)) * h * w : nullptr, w, h, lo,
-                   nr, tx.i0, tx.i1, tx.l0, tx.l1, st0, st1);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // the rows' taps (uniform per row) computed once per unit by lanes 0 .. SR + 2P - 1 and read back as
-    // LDS broadcasts: (stage offsets of the two source rows, weights)
-    float4* tap = reinterpret_cast<float4*>(stage + 2 * PROJ_LR * 64);
-    if (lane < SR + 2 * P) {
-      const ProjTaps t = proj_taps(min(max(y0 - P + lane, 0), g.H - 1), g.H, h);
-      tap[lane] = make_float4(__int_as_float((t.i0 - lo) * 64), __int_as_float((t.i1 - lo) * 64), t.l0, t.l1);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int i = 0; i < SR + 2 * P; ++i) {
-      const float4 t = tap[i];
-      const int o0 = __float_as_int(t.x) + lane, o1 = __float_as_int(t.y) + lane;
-      float v = __fadd_rn(__fmul_rn(st0[o0], t.z), __fmul_rn(st0[o1], t.w));
-      if (flip) v = __fmul_rn(__fadd_rn(v, __fadd_rn(__fmul_rn(st1[o0], t.z), __fmul_rn(st1[o1], t.w))), 0.5f);
-      r[i] = s == 0 ? v : __fadd_rn(r[i], v);
-    }
+  if (pj.f[0]) proj_sep_scale<P, true, true>(pj, g, 0, b, j, y0, xc, r, stage);
+  else proj_sep_scale<P, false, true>(pj, g, 0, b, j, y0, xc, r, stage);
+  for (int s = 1; s < pj.S; ++s) {
+    if (pj.f[s]) proj_sep_scale<P, true, false>(pj, g, s, b, j, y0, xc, r, stage);
+    else proj_sep_scale<P, false, false>(pj, g, s, b, j, y0, xc, r, stage);
   }
-#pragma unroll
-  for (int i = 0; i < SR + 2 * P; ++i) {
-    const int y = y0 - P + i;
-    r[i] = (xok && y >= 0 && y < g.H) ? div_rn(r[i], pj.divisor) : -INFINITY;
-  }
+  proj_finish<P>(pj, g, y0, xok, r);
 }
 
 // rows y0 - P .. y0 + SR - 1 + P of the lane's column, rows and columns outside the plane CLAMPED to
@@ -1289,7 +1330,7 @@ static void dispatch_nms(const float* s, const float* masks, const DetectGeom& g
 }
 
 // host restatement of proj_taps (same fp32 operations, round to nearest): does every unit's row span
-// fit the separable loader's PROJ_LR staged rows?
+// fit the separable loader's PROJ_LR staged rows (with the one past them)?
 static int proj_taps_host(int dst, int out_size, int in_size, bool upper) {
   const float scale = (float)in_size / (float)out_size;
   volatile float t = (float)dst + 0.5f;   // volatile: one rounded operation each, as on the device
@@ -1302,12 +1343,15 @@ static int proj_taps_host(int dst, int out_size, int in_size, bool upper) {
 
 static bool proj_sep_ok(const ProjArgs& pj, const DetectGeom& g) {
   const int P = g.p;
-  for (int s = 0; s < pj.S; ++s)
+  for (int s = 0; s < pj.S; ++s) {
+    if ((size_t)pj.h[s] * pj.w[s] * 4 >= 0x7fffffffull) return false;   // the buffer descriptors' 32-bit extent
     for (int band = 0; band < g.nb; ++band) {
       const int y0 = band * SR;
       const int ya = std::min(std::max(y0 - P, 0), g.H - 1), yb = std::min(std::max(y0 + SR + P - 1, 0), g.H - 1);
-      if (proj_taps_host(yb, g.H, pj.h[s], true) - proj_taps_host(ya, g.H, pj.h[s], false) + 1 > PROJ_LR) return false;
+      // the unit's source rows plus the one staged past them (the second tap of the bottom border's rows)
+      if (proj_taps_host(yb, g.H, pj.h[s], true) - proj_taps_host(ya, g.H, pj.h[s], false) + 2 > PROJ_LR) return false;
     }
+  }
   return true;
 }
 
@@ -1461,6 +1505,8 @@ static int proj_args(const pemp_proj_maps* m, int J, ProjArgs* pj, const char* f
   }
   a.fi = m->flip_index;
   a.divisor = m->divisor;
+  int ex;
+  a.rdiv = std::frexp(m->divisor, &ex) == 0.5f && ex >= -125 && ex <= 126 ? std::ldexp(1.0f, 1 - ex) : 0.f;
   a.ch0 = 0;
   *pj = a;
   return PEMP_OK;

@@ -2805,9 +2805,10 @@ struct NodeTableArgs {
 #ifndef PEMP_NODE_ON_SIDE
 #define PEMP_NODE_ON_SIDE 1   // the first node step on the prelude side stream, the edge prelude on the launch stream
 #endif
-#ifndef PEMP_NODE_ON_SIDE_MIN_E
-#define PEMP_NODE_ON_SIDE_MIN_E 65536   // below this many edges (capacity) the other order: c2 (one image, ~22k edges)
-                                        // measured a 160 vs 202 us step span with the node step on the side
+#ifndef PEMP_SIDE_MIN_E
+#define PEMP_SIDE_MIN_E 65536   // below this many edges (capacity) the prelude stays on the launch stream: at c2 (one
+                                // image, ~22k edges) the fork and join waits (7 + 11 us) cost more than the overlap
+                                // buys: step span 141 vs 165 us, images/s +18 % (profiles/r06_c2_serial_prelude.md)
 #endif
 #ifndef EMBED_ON_SIDE
 #define EMBED_ON_SIDE 1   // capacity mode: the edge embedding on the prelude side stream (see mpn_forward_impl)
@@ -4183,9 +4184,10 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   const bool fused_embed = fused_embed_;
   // The edge prelude (prepare, wave ranges, edge embedding) needs nothing the node embedding and the first
   // node table produce: it runs on a side stream (forked from and joined back into `st`) while they run
-  // here (their 16-row grids leave most CUs idle). Serial when the library profiler is on (per-kernel
-  // event timing on `st`) or with PEMP_SERIAL_PRELUDE set.
-  SideStream* ss = (E > 0 && steps >= 1 && !prof_active() && !serial_prelude()) ? side_stream_for(st) : nullptr;
+  // here (their 16-row grids leave most CUs idle). Serial below PEMP_SIDE_MIN_E edges, when the library
+  // profiler is on (per-kernel event timing on `st`) or with PEMP_SERIAL_PRELUDE set.
+  SideStream* ss = (E >= PEMP_SIDE_MIN_E && steps >= 1 && !prof_active() && !serial_prelude()) ? side_stream_for(st)
+                                                                                                  : nullptr;
   std::unique_lock<std::mutex> side_lock;
   if (ss) {
     side_lock = std::unique_lock<std::mutex>(ss->mu);
@@ -4204,12 +4206,12 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
     side_lock.unlock();
     ss = nullptr;
   };
-  // PEMP_NODE_ON_SIDE (round 6, the default for E >= PEMP_NODE_ON_SIDE_MIN_E): the node embedding + first node table go to the side stream and the
+  // PEMP_NODE_ON_SIDE (round 6, the default): the node embedding + first node table go to the side stream and the
   // edge prelude (order, ranges, embedding) stays on the launch stream, so the step's critical path -- graph build ->
   // order -> ranges -> embedding -> first pass -- carries neither the fork's nor the join's cross-stream wait (the
   // side chain, ~20 us, is done long before the ~60 us prelude). Otherwise: the order and the range table on the side
   // stream, the node kernels here, and the edge embedding placed as below.
-  if (ss && PEMP_NODE_ON_SIDE && E >= PEMP_NODE_ON_SIDE_MIN_E) {
+  if (ss && PEMP_NODE_ON_SIDE) {
     nst = ss->s;
     pst = st;
     if (!fused_embed) {

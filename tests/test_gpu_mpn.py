@@ -604,7 +604,9 @@ def test_batches_in_flight_on_two_streams():
     model, _ = make_model(cfg, 0.5)
     feats = torch.from_numpy(syn.closed_form((B, 128, H, W), 0.25)).to(DEV)
     tags = torch.from_numpy(syn.closed_form((B, J, H, W, 1), 0.75)).to(DEV)
-    hms = [torch.from_numpy(syn.make_heatmaps(40 + k, B, J, H, W, persons=3 + k % 3, margin=4)).to(DEV)
+    # 8-10 persons: 74k-115k edges per batch, above PEMP_SIDE_MIN_E, so every step also forks its prelude onto
+    # its stream's side stream
+    hms = [torch.from_numpy(syn.make_heatmaps(40 + k, B, J, H, W, persons=8 + k % 3, margin=4)).to(DEV)
            for k in range(6)]
 
     def step(hm):
