@@ -352,6 +352,9 @@ __device__ __forceinline__ void load_unit_proj(const ProjArgs& pj, const DetectG
 // next stage row (i1 = i0 + 1, or at the bottom border the duplicate of row h - 1, whose horizontal value
 // is the same operands'): one ds_read2 per map and output row.
 constexpr int PROJ_LR = 16;
+#ifndef PROJ_X2
+#define PROJ_X2 1   // the register-only loader for interior bands of an exact 2x upsampling (proj_x2_first)
+#endif
 
 // horizontal interpolation of rows lo .. lo + nl - 1 (clamped to the map) of the forward pass and, FLIP,
 // the flipped pass into the wave's stage rows; groups of 4 rows of both maps (16 loads) under one wait
@@ -428,6 +431,60 @@ __device__ __forceinline__ void proj_sep_scale(const ProjArgs& pj, const DetectG
   }
 }
 
+// Exact 2x upsampling (h * 2 == H, the single-scale test front-end of a stride-2 output): out row Y's
+// source index is Y / 2 - 0.25 in fp32 with no rounding, so an even Y reads rows (Y / 2 - 1, Y / 2) with
+// weights (0.25, 0.75) and an odd Y rows ((Y - 1) / 2, (Y + 1) / 2) with (0.75, 0.25) -- what proj_taps
+// computes, as constants. Since y0 is even, the row of every output row i relative to y0 / 2 is a
+// compile-time constant, so a band whose rows need no clamping (y0 - P >= 1, y0 + SR - 1 + P <= H - 3)
+// keeps its NL source rows' horizontal values in registers: no LDS stage, no tap table, no waits on LDS.
+template <int P>
+__host__ __device__ constexpr int x2_row(int i) {   // source row of output row i (tap 0), relative to y0 / 2
+  return ((i - P) & 1) == 0 ? (i - P) / 2 - 1 : (i - P - 1) / 2;
+}
+
+template <int P, bool FLIP>
+__device__ __forceinline__ void proj_x2_first(const ProjArgs& pj, const DetectGeom& g, int b, int j, int y0, int xc,
+                                              float (&r)[SR + 2 * P]) {
+  constexpr int NR = SR + 2 * P, LO = x2_row<P>(0), NL = x2_row<P>(NR - 1) + 2 - LO;
+  const int h = pj.h[0], w = pj.w[0];
+  const ProjTaps tx = proj_taps(xc, g.W, w);
+  const __amdgpu_buffer_rsrc_t r0 = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(pj.m[0] + ((size_t)b * pj.C + pj.ch0 + j) * h * w), 0, h * w * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(FLIP ? pj.f[0] + ((size_t)b * pj.C + pj.ch0 + (pj.fi ? pj.fi[j] : j)) * h * w : pj.m[0]), 0,
+      h * w * 4, 0x00020000);
+  const int va = 4 * tx.i0, vb = 4 * tx.i1, vc = 4 * (w - 1 - tx.i0), vd = 4 * (w - 1 - tx.i1);
+  const int rowb = 4 * w;
+  int so = (y0 / 2 + LO) * rowb;
+  float a[NL], bb[NL], c[NL], d[NL];
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    a[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r0, va, so, 0));
+    bb[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r0, vb, so, 0));
+    if constexpr (FLIP) {
+      c[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r1, vc, so, 0));
+      d[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r1, vd, so, 0));
+    }
+    so += rowb;
+  }
+  float h0[NL], h1[NL];
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    h0[k] = __fadd_rn(__fmul_rn(a[k], tx.l0), __fmul_rn(bb[k], tx.l1));
+    if constexpr (FLIP) h1[k] = __fadd_rn(__fmul_rn(c[k], tx.l0), __fmul_rn(d[k], tx.l1));
+  }
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    constexpr float q = 0.25f, t = 0.75f;
+    const int k = x2_row<P>(i) - LO;
+    const bool even = ((i - P) & 1) == 0;
+    const float w0 = even ? q : t, w1 = even ? t : q;
+    float v = __fadd_rn(__fmul_rn(h0[k], w0), __fmul_rn(h0[k + 1], w1));
+    if constexpr (FLIP) v = __fmul_rn(__fadd_rn(v, __fadd_rn(__fmul_rn(h1[k], w0), __fmul_rn(h1[k + 1], w1))), 0.5f);
+    r[i] = v;
+  }
+}
+
 template <int P>
 __device__ __forceinline__ void load_unit_proj_sep(const ProjArgs& pj, const DetectGeom& g, int u,
                                                    float (&r)[SR + 2 * P], float* __restrict__ stage) {
@@ -437,8 +494,14 @@ __device__ __forceinline__ void load_unit_proj_sep(const ProjArgs& pj, const Det
   const int y0 = q.band * SR, x = q.strip * g.sc - P + lane;
   const bool xok = x >= 0 && x < g.W;
   const int xc = min(max(x, 0), g.W - 1);
-  if (pj.f[0]) proj_sep_scale<P, true, true>(pj, g, 0, b, j, y0, xc, r, stage);
-  else proj_sep_scale<P, false, true>(pj, g, 0, b, j, y0, xc, r, stage);
+  if (PROJ_X2 && pj.h[0] * 2 == g.H && y0 - P >= 1 && y0 + SR - 1 + P <= g.H - 3) {   // (uniform)
+    if (pj.f[0]) proj_x2_first<P, true>(pj, g, b, j, y0, xc, r);
+    else proj_x2_first<P, false>(pj, g, b, j, y0, xc, r);
+  } else if (pj.f[0]) {
+    proj_sep_scale<P, true, true>(pj, g, 0, b, j, y0, xc, r, stage);
+  } else {
+    proj_sep_scale<P, false, true>(pj, g, 0, b, j, y0, xc, r, stage);
+  }
   for (int s = 1; s < pj.S; ++s) {
     if (pj.f[s]) proj_sep_scale<P, true, false>(pj, g, s, b, j, y0, xc, r, stage);
     else proj_sep_scale<P, false, false>(pj, g, s, b, j, y0, xc, r, stage);

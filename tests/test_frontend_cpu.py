@@ -151,3 +151,40 @@ def test_backbone_leg_model_is_higherhrnet_w48():
     with torch.no_grad():
         (y0, y1), f = m(torch.zeros(1, 3, 64, 96))
     assert y0.shape == (1, 34, 16, 24) and y1.shape == (1, 17, 32, 48) and f.shape == (1, 48, 32, 48)
+
+
+def _taps_f32(dst, out_size, in_size):
+    """csrc/detect.hip proj_taps in numpy fp32 (one rounding per operation): (i0, i1, l0, l1)."""
+    f = np.float32
+    scale = f(in_size) / f(out_size)
+    src = f(f(scale * f(f(dst) + f(0.5))) - f(0.5))
+    src = max(src, f(0.0))
+    i0 = int(src)
+    i1 = i0 + (1 if i0 < in_size - 1 else 0)
+    l1 = min(max(f(src - f(i0)), f(0.0)), f(1.0))
+    return i0, i1, f(f(1.0) - l1), l1
+
+
+def _x2_row(i, P):
+    d = i - P
+    return d // 2 - 1 if d % 2 == 0 else (d - 1) // 2
+
+
+@pytest.mark.parametrize("P", [0, 1, 2, 3, 4])
+def test_exact_2x_loader_taps(P):
+    """proj_x2_first (the projected NMS's register-only loader for an exact 2x upsampling) replaces proj_taps by
+    constants: for every interior band (y0 - P >= 1, y0 + SR - 1 + P <= H - 3) of every height, output row i reads
+    rows y0 / 2 + x2_row(i) and the next one with weights (0.25, 0.75) for an even y0 - P + i, (0.75, 0.25) for an
+    odd one -- exactly what proj_taps computes, so its values are bitwise those of the staged loader."""
+    SR = 16
+    for h in list(range(9, 80)) + [160, 320, 321, 512]:
+        H = 2 * h
+        for y0 in range(0, H, SR):
+            if not (y0 - P >= 1 and y0 + SR - 1 + P <= H - 3):
+                continue
+            for i in range(SR + 2 * P):
+                Y = y0 - P + i
+                i0, i1, l0, l1 = _taps_f32(Y, H, h)
+                even = (i - P) % 2 == 0
+                assert i0 == y0 // 2 + _x2_row(i, P) and i1 == i0 + 1, (h, y0, i)
+                assert (l0, l1) == ((0.25, 0.75) if even else (0.75, 0.25)), (h, y0, i)
