@@ -26,4 +26,5 @@ pr.enable()
 bench.e2e_pipeline(wl, gc, model, hm, feats, tags, dev, steps, 5, 1)
 pr.disable()
 st = pstats.Stats(pr)
-st.sort_stats("tottime").print_stats(30)
+st.sort_stats("tottime").print_stats(45)
+st.sort_stats("cumulative").print_stats(60)

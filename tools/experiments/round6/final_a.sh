@@ -22,3 +22,5 @@ for wl in c3 c3knn10; do
 done
 cp profiles/mfma_latest.json gpurun_out/${T}_mfma_latest.json
 echo "mfma ok"
+# keep the merge-back under its 64 MiB cap: the raw traces / counter dumps were summarised above
+find gpurun_out -type f \( -name "*kernel_trace.csv" -o -name "*counter_collection.csv" -o -name "*.db" \) -size +1M -delete

@@ -19,3 +19,5 @@ for wl in c3knn10 c5ms c2 c2fp32 c5; do
 done
 PEMP_SHARE_DEVICE=1 PEMP_DIST_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 --no-cpu-baseline --no-backbone > gpurun_out/${T}_dist2.json 2> gpurun_out/${T}_dist2.err || exit 1
 echo "dist2 ok"
+# keep the merge-back under its 64 MiB cap: the raw traces / counter dumps were summarised above
+find gpurun_out -type f \( -name "*kernel_trace.csv" -o -name "*counter_collection.csv" -o -name "*.db" \) -size +1M -delete
