@@ -489,6 +489,56 @@ int pemp_mpn_forward_fully_cap(const pemp_mpn_desc* desc, const pemp_mpn_weights
                                float* edge_logits, float* node_logits, float* class_logits,
                                void* workspace, size_t workspace_bytes, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * One batch of the inference path in one call (no reference counterpart: a serving entry for a repeated batch
+ * shape; construct_graph_start's capacity mode, ConstructGraph.py:1161-1209 + 206-231 + 376-381 and
+ * NodeClassificationMPNSimple.py:62-97, takes it): pemp_detect (stages ALL, the counts stored into n_det_host) +
+ * pemp_fully_graph_build_cap (PEMP_BUILD_WRITE_COUNTS) + pemp_mpn_forward_fully_cap (PEMP_MPN_COUNTS_IN_OFFSETS;
+ * desc == NULL: none), queued on one stream. The arguments that repeat from batch to batch live in a plan that
+ * pemp_step_layout completes once; every output lives in ONE caller buffer of plan.bytes bytes at the offsets it
+ * computes (off[PEMP_STEP_*], 256-byte aligned):
+ *   DET [B, det_cap, 3] i64, DSC [B, det_cap] f32, NDET [B] i32 (pemp_detect's outputs); X [n_cap, C],
+ *   JDET [n_cap, 3] i64, JSC [n_cap], BIDX [n_cap] i64, JTAGS [n_cap, F] (F > 0), EIDX [2, e_cap] i64 written as a
+ *   contiguous [2, E], EATTR [e_cap, A], NOFF [B + 4] i64 (pemp_fully_graph_build_cap's outputs); LOGITS (desc
+ *   only): edge [max(n_rec, 1)][e_cap], then node [n_rec + 1][n_cap] at element elog_n rounded up to 64, then class
+ *   [n_rec + 1][n_cap][J] likewise (pemp_mpn_forward_fully_cap's three arrays, rows at r * E / r * N).
+ * The caller sets n_det_host[0..B) to -1, calls, and reads the counts as with pemp_detect; a batch past a capacity
+ * leaves the build's and the forward's outputs unwritten (the caller re-runs the exact path, as with the capacity
+ * calls). Returns PEMP_ERR_UNSUPPORTED when only the forward was refused (pemp_mpn_forward_fully_cap's conditions;
+ * the detection and the build are queued). Workspaces: det_workspace >= pemp_detect_workspace_size, mpn_workspace
+ * >= pemp_mpn_workspace_size(desc with PEMP_MPN_COUNTS_IN_OFFSETS, n_cap, e_cap); both stream-ordered like the
+ * outputs. scoremaps: [B, J, H, W] f32, or a pemp_proj_maps* when projected != 0 (pemp_detect_projected). */
+enum {
+  PEMP_STEP_DET = 0, PEMP_STEP_DSC, PEMP_STEP_NDET, PEMP_STEP_X, PEMP_STEP_JDET, PEMP_STEP_JSC, PEMP_STEP_BIDX,
+  PEMP_STEP_JTAGS, PEMP_STEP_EIDX, PEMP_STEP_EATTR, PEMP_STEP_NOFF, PEMP_STEP_LOGITS, PEMP_STEP_NOUT
+};
+typedef struct pemp_step_plan {
+  /* detection */
+  int32_t B, J, H, W, pool_kernel, use_threshold, topk, det_cap, projected;
+  float threshold;
+  void* det_workspace;
+  size_t det_workspace_bytes;
+  /* capacity graph build */
+  int32_t C, F, A, mode;        /* F = 0: no tagmaps; A: edge_attr columns of mode (PEMP_EF_*) */
+  float norm_factor;
+  int64_t n_cap, e_cap;
+  /* forward (desc NULL: none); desc->flags must hold PEMP_MPN_COUNTS_IN_OFFSETS */
+  const pemp_mpn_desc* desc;
+  const pemp_mpn_weights* weights;
+  void* mpn_workspace;
+  size_t mpn_workspace_bytes;
+  /* pemp_step_layout's results */
+  int32_t n_rec;                /* recorded iterations: edge rows max(n_rec, 1), node / class rows n_rec + 1 */
+  int64_t elog_n, nlog_off, clog_off;   /* edge / node / class logits: elements from off[PEMP_STEP_LOGITS] (f32) */
+  size_t off[PEMP_STEP_NOUT];
+  size_t bytes;
+} pemp_step_plan;
+/* Fills plan->off / bytes / n_rec / elog_n / nlog_off / clog_off from the other fields (host arithmetic, no device
+ * call); returns plan->bytes, 0 for an invalid plan (pemp_last_error says why). */
+size_t pemp_step_layout(pemp_step_plan* plan);
+int pemp_step_fully_cap(const pemp_step_plan* plan, const void* scoremaps, const float* masks, const float* features,
+                        const float* tagmaps, void* out, int32_t* n_det_host, void* stream);
+
 /* Counters of pemp_mpn_forward_fully_cap's HIP graphs since the library loaded (no reference counterpart; for
  * tests and servers): out3[0] captures made, out3[1] graph launches (first launch after a capture included),
  * out3[2] captures refused (the forward then ran directly). Graphs are opt-in (PEMP_GRAPHS=1): a repeating argument
@@ -504,7 +554,8 @@ int pemp_mpn_graph_stats(uint64_t* out3);
 int pemp_edge_cus_policy(int num_cus, int64_t E, int reserve_request);
 
 /* sizeof of the ABI structs as this library was built (host only; bindings check their mirrors against it):
- * which = 0 pemp_mpn_weights, 1 pemp_mpn_desc, 2 pemp_mlp, 3 pemp_proj_maps; 0 for any other value. */
+ * which = 0 pemp_mpn_weights, 1 pemp_mpn_desc, 2 pemp_mlp, 3 pemp_proj_maps, 4 pemp_step_plan; 0 for any other
+ * value. */
 size_t pemp_abi_struct_size(int which);
 
 /* pemp_mpn_forward for an edge_index sorted by (src, dst) without duplicates and symmetric (every s -> d has

@@ -50,6 +50,20 @@ class PempMpnDesc(ctypes.Structure):
                 ("precision", c_i32), ("types_stride", c_i32), ("flags", c_i32)]
 
 
+STEP_DET, STEP_DSC, STEP_NDET, STEP_X, STEP_JDET, STEP_JSC, STEP_BIDX, STEP_JTAGS, STEP_EIDX, STEP_EATTR, STEP_NOFF, \
+    STEP_LOGITS, STEP_NOUT = range(13)
+
+
+class PempStepPlan(ctypes.Structure):
+    _fields_ = [("B", c_i32), ("J", c_i32), ("H", c_i32), ("W", c_i32), ("pool_kernel", c_i32), ("use_threshold", c_i32),
+                ("topk", c_i32), ("det_cap", c_i32), ("projected", c_i32), ("threshold", c_f32), ("det_workspace", c_p),
+                ("det_workspace_bytes", c_sz), ("C", c_i32), ("F", c_i32), ("A", c_i32), ("mode", c_i32),
+                ("norm_factor", c_f32), ("n_cap", c_i64), ("e_cap", c_i64), ("desc", ctypes.POINTER(PempMpnDesc)),
+                ("weights", ctypes.POINTER(PempMpnWeights)), ("mpn_workspace", c_p), ("mpn_workspace_bytes", c_sz),
+                ("n_rec", c_i32), ("elog_n", c_i64), ("nlog_off", c_i64), ("clog_off", c_i64),
+                ("off", c_sz * STEP_NOUT), ("bytes", c_sz)]
+
+
 # name -> (restype, argtypes); every symbol of include/pemp.h
 SIGNATURES = {
     "pemp_abi_version": (c_i32, []),
@@ -122,6 +136,8 @@ SIGNATURES = {
     "pemp_pose_finish_plan": (c_i32, [c_i32, c_p, c_p, c_p, c_p, c_i32, c_p]),
     "pemp_pose_finish_batch": (c_i32, [c_p, c_p, c_i32, c_i32, c_i32, c_i32, c_i32, c_p, c_i32, c_p, c_p, c_i32,
                                        c_i32, c_p, c_i32, c_p, c_sz, c_p]),
+    "pemp_step_layout": (c_sz, [ctypes.POINTER(PempStepPlan)]),
+    "pemp_step_fully_cap": (c_i32, [ctypes.POINTER(PempStepPlan), c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "pemp_prof_enable": (c_i32, [ctypes.c_char_p]),
     "pemp_prof_report": (c_i32, [ctypes.c_char_p, c_sz]),
 }

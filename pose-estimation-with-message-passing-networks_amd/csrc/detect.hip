@@ -67,10 +67,17 @@ __device__ __forceinline__ bool better(float v1, int i1, float v2, int i2) {
 
 // Unit grid: nb bands of SR rows x nsx strips of sc = 64 - 2p columns per plane; lane c of a
 // unit owns column x = strip * sc - p + c.
+//
+// Quad layout (NMS_QUAD, dense MODE_POS detection without masks; nms_quad_kernel): units are 16 rows x 64 columns
+// with no halo lanes (sc = 64, p = 0: lane c of a unit <-> column strip * 64 + c), and the pool radius is pr. The NMS
+// pass walks blocks of 16 rows x 256 columns (4 units side by side, 4 columns per lane), nbx per band.
 struct DetectGeom {
   int B, J, H, W, p, K, sc, nsx, nb, units, S;
   unsigned mu, mn;   // unsigned division by units / nsx: q = (umulhi(n, m) + n) >> l (n < 2^31)
   int lu, ln;
+  int pr, quad, nbx, blocks;   // pool radius; quad layout; blocks per band / per plane (quad layout)
+  unsigned mq, mx;             // division by blocks / nbx
+  int lq, lx;
 };
 
 // Granlund-Montgomery constants of an unsigned division by d >= 1 for dividends below 2^31
@@ -97,9 +104,12 @@ __device__ __forceinline__ UnitPos unit_pos(const DetectGeom& g, int u) {
   return q;
 }
 
-static DetectGeom geom(int B, int J, int H, int W, int pool_k, int K) {
+static DetectGeom geom(int B, int J, int H, int W, int pool_k, int K, bool quad = false) {
   DetectGeom g;
   g.B = B; g.J = J; g.H = H; g.W = W; g.p = pool_k / 2; g.K = K;
+  g.pr = pool_k / 2;
+  g.quad = quad ? 1 : 0;
+  if (quad) g.p = 0;
   g.sc = 64 - 2 * g.p;
   g.nsx = (W + g.sc - 1) / g.sc;
   g.nb = (H + SR - 1) / SR;
@@ -107,6 +117,10 @@ static DetectGeom geom(int B, int J, int H, int W, int pool_k, int K) {
   g.S = g.nb;
   fastdiv_consts((unsigned)g.units, g.mu, g.lu);
   fastdiv_consts((unsigned)g.nsx, g.mn, g.ln);
+  g.nbx = (g.nsx + 3) / 4;
+  g.blocks = g.nb * g.nbx;
+  fastdiv_consts((unsigned)g.blocks, g.mq, g.lq);
+  fastdiv_consts((unsigned)g.nbx, g.mx, g.lx);
   return g;
 }
 
@@ -687,11 +701,315 @@ __global__ __launch_bounds__(NT1) void nms_strips_kernel(
   }
 }
 
+// ---- split dense NMS (quad layout, round 6) ------------------------------------------------------------------------
+// nms_quad_kernel: one wave per block of SR rows x 256 columns = 4 units of 16 x 64; lane L owns the columns x0 + 4L ..
+// x0 + 4L + 3 (one buffer_load_dwordx4 per row, columns past the plane set to -inf; a clamped dword per column when
+// W % 4 != 0). The P
+// columns either side of the block come from one more P-dword load per row into the same registers of every lane, of
+// which lanes 0 (left: x0 - P ..) and 63 (right: x0 + 256 ..) are the ones read: the DPP wave shifts that bring the
+// neighbours' columns leave those two lanes' `old` operand in place. Per row the horizontal 2P + 1 window first (6
+// v_max3 for P = 2), then the vertical one over the 2P + 1 row maxima; per pixel v = c * (window max == c), and the
+// threshold, non-negative and maximum bits (shift-add accumulation) and the lane's largest v. No ranking in the loop:
+// a unit holding a positive v (or with fewer than K non-negative pixels) is re-read one column per lane, its maximum
+// bits from LDS, and ranked by nms_strips_kernel's wave top-k; every other unit writes a sentinel candidate list. The
+// negative lists are written only for units with fewer than K non-negative pixels (readers gate them on tile_nonneg).
+#ifndef NMS_QUAD
+#define NMS_QUAD 0   // opt-in (PEMP_NMS_QUAD=1): measured no faster than the strip kernel, see DESIGN.md section 4
+#endif
+#ifndef NMS_QUAD_PER_CU
+#define NMS_QUAD_PER_CU 8
+#endif
+#ifndef NMS_QUAD_PF
+#define NMS_QUAD_PF 6   // rows of a block in flight ahead of the row being reduced
+#endif
+
+template <int P>
+__device__ __forceinline__ void quad_hmax(const float (&q)[4], const float (&h)[P > 0 ? P : 1], float (&o)[4]) {
+  if constexpr (P == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = q[k];
+  } else {
+    float e[4 + 2 * P];
+#pragma unroll
+    for (int i = 0; i < P; ++i) {   // wave_shr:1 / wave_shl:1 with bound_ctrl off: lanes 0 / 63 keep the halo load
+      e[i] = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(h[i]), __float_as_int(q[4 - P + i]), 0x138,
+                                                        0xF, 0xF, false));
+      e[P + 4 + i] = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(h[i]), __float_as_int(q[i]), 0x130, 0xF,
+                                                                0xF, false));
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) e[P + k] = q[k];
+    if constexpr (P == 2) {
+      const float a = fmaxf(fmaxf(q[0], q[1]), q[2]), b = fmaxf(fmaxf(q[1], q[2]), q[3]);
+      o[0] = fmaxf(fmaxf(e[0], e[1]), a);
+      o[1] = fmaxf(fmaxf(e[1], a), q[3]);
+      o[2] = fmaxf(fmaxf(q[0], b), e[6]);
+      o[3] = fmaxf(fmaxf(b, e[6]), e[7]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float m = e[k];
+#pragma unroll
+        for (int d = 1; d <= 2 * P; ++d) m = fmaxf(m, e[k + d]);
+        o[k] = m;
+      }
+    }
+  }
+}
+
+template <int P>
+__device__ __forceinline__ void quad_halo_load(__amdgpu_buffer_rsrc_t rs, int vo, int so, float (&h)[P > 0 ? P : 1]) {
+  if constexpr (P == 1) {
+    h[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, so, 0));
+  } else if constexpr (P == 2) {
+    const auto t = __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, 0);
+    h[0] = __uint_as_float(t[0]); h[1] = __uint_as_float(t[1]);
+  } else if constexpr (P == 3) {
+    const auto t = __builtin_amdgcn_raw_buffer_load_b96(rs, vo, so, 0);
+    h[0] = __uint_as_float(t[0]); h[1] = __uint_as_float(t[1]); h[2] = __uint_as_float(t[2]);
+  } else if constexpr (P == 4) {
+    const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so, 0);
+    h[0] = __uint_as_float(t[0]); h[1] = __uint_as_float(t[1]); h[2] = __uint_as_float(t[2]); h[3] = __uint_as_float(t[3]);
+  }
+}
+
+// One pixel's bits: v = (m == c) ? c : c * 0 (exactly c * (maximum ? 1 : 0)); ab, tb, nb shifted left by one with the
+// maximum, threshold (TP: !(v < thr); else !(v < thr) && v != 0) and non-negative (v >= 0) predicates as the carry-in
+// of v_addc (t + t + carry: one instruction per bit, where the compiler spends a select, a shift and an or).
+template <bool TP>
+__device__ __forceinline__ void quad_px_bits(float c, float m, float thr, float& v, unsigned& ab, unsigned& tb,
+                                             unsigned& nb) {
+  float z;
+  if constexpr (TP) {
+    asm("v_mul_f32_e32 %[z], 0, %[c]\n\t"
+        "v_cmp_eq_f32_e32 vcc, %[m], %[c]\n\t"
+        "v_cndmask_b32_e32 %[v], %[z], %[c], vcc\n\t"
+        "v_addc_co_u32_e32 %[ab], vcc, %[ab], %[ab], vcc\n\t"
+        "v_cmp_nlt_f32_e32 vcc, %[v], %[thr]\n\t"
+        "v_addc_co_u32_e32 %[tb], vcc, %[tb], %[tb], vcc\n\t"
+        "v_cmp_le_f32_e32 vcc, 0, %[v]\n\t"
+        "v_addc_co_u32_e32 %[nb], vcc, %[nb], %[nb], vcc"
+        : [v] "=&v"(v), [z] "=&v"(z), [ab] "+v"(ab), [tb] "+v"(tb), [nb] "+v"(nb)
+        : [c] "v"(c), [m] "v"(m), [thr] "v"(thr)
+        : "vcc");
+  } else {
+    unsigned long long nz;
+    asm("v_mul_f32_e32 %[z], 0, %[c]\n\t"
+        "v_cmp_eq_f32_e32 vcc, %[m], %[c]\n\t"
+        "v_cndmask_b32_e32 %[v], %[z], %[c], vcc\n\t"
+        "v_addc_co_u32_e32 %[ab], vcc, %[ab], %[ab], vcc\n\t"
+        "v_cmp_neq_f32_e64 %[nz], 0, %[v]\n\t"
+        "v_cmp_nlt_f32_e32 vcc, %[v], %[thr]\n\t"
+        "s_and_b64 vcc, vcc, %[nz]\n\t"
+        "v_addc_co_u32_e32 %[tb], vcc, %[tb], %[tb], vcc\n\t"
+        "v_cmp_le_f32_e32 vcc, 0, %[v]\n\t"
+        "v_addc_co_u32_e32 %[nb], vcc, %[nb], %[nb], vcc"
+        : [v] "=&v"(v), [z] "=&v"(z), [ab] "+v"(ab), [tb] "+v"(tb), [nb] "+v"(nb), [nz] "=&s"(nz)
+        : [c] "v"(c), [m] "v"(m), [thr] "v"(thr)
+        : "vcc", "scc");
+  }
+}
+
+// LM: 0 the block lies inside the plane (16-byte loads), 1 it reaches past it and W % 4 == 0 (16-byte loads; the
+// columns past the plane become -inf, MaxPool's padding), 2 W % 4 != 0 (clamped dword per column)
+template <int P, bool TP, int LM>
+__device__ __forceinline__ void quad_block(__amdgpu_buffer_rsrc_t rs, const DetectGeom& g, int y0, int x0, float thr,
+                                           unsigned (&tb)[4], unsigned (&nb)[4], unsigned (&ab)[4], float& pmax) {
+  constexpr int NR = SR + 2 * P, HP = P > 0 ? P : 1, PF = NMS_QUAD_PF < NR ? NMS_QUAD_PF : NR;
+  const int lane = threadIdx.x & 63, H = g.H, W = g.W, rowb = W * 4;
+  // the lane's columns and its halo columns (read in lanes 0 and 63)
+  constexpr bool FAST = LM < 2;
+  const int xq = x0 + 4 * lane;
+  const bool xin = xq < W;
+  int vq[4], vh[HP];
+  if constexpr (FAST) {
+    vq[0] = 4 * xq;
+    vh[0] = 4 * (lane == 63 ? min(x0 + 256, W - P) : max(x0 - P, 0));
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) vq[k] = 4 * min(xq + k, W - 1);
+#pragma unroll
+    for (int i = 0; i < HP; ++i) vh[i] = 4 * (lane == 63 ? min(x0 + 256 + i, W - 1) : max(x0 - P + i, 0));
+  }
+  float qr[NR][4], hr[NR][HP];
+  auto load_row = [&](int r) {
+    const int so = min(max(y0 - P + r, 0), H - 1) * rowb;   // clamped rows: duplicates leave every window max as is
+    if constexpr (FAST) {
+      const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, vq[0], so, 0);
+      qr[r][0] = __uint_as_float(t[0]); qr[r][1] = __uint_as_float(t[1]);
+      qr[r][2] = __uint_as_float(t[2]); qr[r][3] = __uint_as_float(t[3]);
+      if constexpr (LM == 1) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) qr[r][k] = xin ? qr[r][k] : -INFINITY;
+      }
+      quad_halo_load<P>(rs, vh[0], so, hr[r]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) qr[r][k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vq[k], so, 0));
+#pragma unroll
+      for (int i = 0; i < P; ++i) hr[r][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vh[i], so, 0));
+    }
+  };
+#pragma unroll
+  for (int r = 0; r < PF; ++r) load_row(r);
+  float hm[NR][4];
+  // output row j: window max m, centre c = row j + P of the lane's column k
+  auto pixel = [&](int j, int k, float m) {
+    const float c = qr[j + P][k];
+    float v;
+    quad_px_bits<TP>(c, m, thr, v, ab[k], tb[k], nb[k]);   // row j ends at bit 15 - j (reversed by the caller)
+    pmax = fmaxf(pmax, v);
+  };
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    if (r + PF < NR) load_row(r + PF);   // the row PF ahead goes out before this row's wait
+    __builtin_amdgcn_sched_barrier(0);
+    quad_hmax<P>(qr[r], hr[r], hm[r]);
+    if constexpr (P > 0) {
+      // rows in pairs: the two windows share their middle 2P - 1 rows (3 v_max3 per 2 outputs for P = 2)
+      if (r >= 2 * P + 1 && ((r - 2 * P) & 1)) {
+        const int j = r - 2 * P - 1;
+        float t[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          t[k] = hm[j + 1][k];
+#pragma unroll
+          for (int d = 2; d < 2 * P; ++d) t[k] = fmaxf(t[k], hm[j + d][k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) pixel(j, k, fmaxf(fmaxf(hm[j][k], t[k]), hm[j + 2 * P][k]));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) pixel(j + 1, k, fmaxf(fmaxf(t[k], hm[j + 2 * P][k]), hm[j + 2 * P + 1][k]));
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pixel(r, k, hm[r][k]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+#ifndef NMS_QUAD_WAVES
+#define NMS_QUAD_WAVES 4   // waves per SIMD the register allocation targets (the pass is latency-bound: 3 -> 4 waves
+#endif                     // took it from 69 to 49 us at c3)
+template <int P, bool TP>
+__global__ __launch_bounds__(NT1) __attribute__((amdgpu_waves_per_eu(NMS_QUAD_WAVES, 8))) void nms_quad_kernel(
+    const float* __restrict__ s, DetectGeom g, float thr, float* __restrict__ cand_v, int* __restrict__ cand_i,
+    float* __restrict__ neg_v, int* __restrict__ neg_i, int* __restrict__ tile_count, int* __restrict__ tile_nonneg,
+    cmask_t* __restrict__ cbits, unsigned long long* __restrict__ pflag) {
+  static_assert(SR == 16, "quad layout: 16-row units");
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int H = g.H, W = g.W, K = g.K;
+  __shared__ __attribute__((aligned(16))) unsigned short abits_sh[NT1 / 64][4 * 64];
+  if (blockIdx.x == 0)   // the fused select + emit stage's publish flags, for this detection
+    for (int i = threadIdx.x; i < g.B * g.J; i += NT1) pflag[i] = 0ull;
+  const int total = g.B * g.J * g.blocks;
+  const int G = gridDim.x;
+  const int slot = (NMS_XCD_MAP && (G & 7) == 0) ? ((int)(blockIdx.x & 7) * (G >> 3) + (int)(blockIdx.x >> 3)) : (int)blockIdx.x;
+  const int stride = G * (NT1 / 64);
+  for (int q = __builtin_amdgcn_readfirstlane(slot * (NT1 / 64) + wave); q < total; q += stride) {
+    const int plane = fastdiv(q, g.mq, g.lq), rem = q - plane * g.blocks;
+    const int band = fastdiv(rem, g.mx, g.lx), bx = rem - band * g.nbx;
+    const int y0 = band * SR;
+    const int su = 4 * bx;   // first unit of the block
+    const int x0 = su * 64;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(s + (size_t)plane * H * W), 0, H * W * 4, 0x00020000);
+    unsigned tb[4] = {0u, 0u, 0u, 0u}, nb[4] = {0u, 0u, 0u, 0u}, ab[4] = {0u, 0u, 0u, 0u};
+    float pmax = -INFINITY;
+    if ((W & 3) != 0) quad_block<P, TP, 2>(rs, g, y0, x0, thr, tb, nb, ab, pmax);
+    else if (x0 + 256 <= W) quad_block<P, TP, 0>(rs, g, y0, x0, thr, tb, nb, ab, pmax);
+    else quad_block<P, TP, 1>(rs, g, y0, x0, thr, tb, nb, ab, pmax);
+    // validity: rows past the plane (last band), columns and units past it (last block of a band)
+    const int rows = min(SR, H - y0);
+    const unsigned rmask = rows >= 16 ? 0xffffu : ((1u << rows) - 1u);
+    const int ul = lane >> 4, u = su + ul;
+    const bool uok = u < g.nsx;
+    unsigned tk[4], ak[4];
+    int tcnt = 0, ncnt = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const unsigned m = (uok && x0 + 4 * lane + k < W) ? rmask : 0u;
+      tk[k] = (__builtin_bitreverse32(tb[k]) >> 16) & m;
+      ak[k] = (__builtin_bitreverse32(ab[k]) >> 16) & m;
+      tcnt += __popc(tk[k]);
+      ncnt += __popc((__builtin_bitreverse32(nb[k]) >> 16) & m);
+    }
+    // both counts of the lane's unit (its 16-lane DPP row): threshold << 16 | non-negative (each <= 1024)
+    int both = (tcnt << 16) | ncnt;
+    both += __builtin_amdgcn_update_dpp(0, both, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
+    both += __builtin_amdgcn_update_dpp(0, both, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
+    both += __builtin_amdgcn_update_dpp(0, both, 0x141, 0xF, 0xF, false);   // row_half_mirror
+    both += __builtin_amdgcn_update_dpp(0, both, 0x140, 0xF, 0xF, false);   // row_mirror
+    const size_t ub = ((size_t)plane * g.nb + band) * g.nsx;   // first unit of the band
+    if (uok) {
+      uint2 pk;
+      pk.x = tk[0] | (tk[1] << 16);
+      pk.y = tk[2] | (tk[3] << 16);
+      *reinterpret_cast<uint2*>(cbits + (ub + u) * 64 + (lane & 15) * 4) = pk;
+      if ((lane & 15) == 0) { tile_count[ub + u] = both >> 16; tile_nonneg[ub + u] = both & 0xffff; }
+    }
+    // ranking: units holding a positive v (top-K positives) or with fewer than K non-negative pixels (top-K negatives)
+    const unsigned long long posm = __ballot(pmax > 0.0f);
+    unsigned live = 0u, negl = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ui = su + i;
+      if (ui >= g.nsx) continue;   // (uniform)
+      if ((posm >> (16 * i)) & 0xffffull) live |= 1u << i;
+      if ((__builtin_amdgcn_readlane(both, 16 * i) & 0xffff) < K) negl |= 1u << i;
+      if (!((live >> i) & 1u) && lane < K) {     // a unit without a positive value: sentinel list
+        cand_v[(ub + ui) * K + lane] = -INFINITY;
+        cand_i[(ub + ui) * K + lane] = INV;
+      }
+    }
+    if (live | negl) {   // (uniform; MODE_POS: the units around the peaks)
+      uint2 pa;
+      pa.x = ak[0] | (ak[1] << 16);
+      pa.y = ak[2] | (ak[3] << 16);
+      *reinterpret_cast<uint2*>(&abits_sh[wave][ul * 64 + (lane & 15) * 4]) = pa;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int rowb = W * 4;
+#pragma unroll 1
+      for (int i = 0; i < 4; ++i) {
+        if (!(((live | negl) >> i) & 1u)) continue;   // (uniform)
+        const int xu = (su + i) * 64 + lane;
+        const bool xok = xu < W;
+        const int vo = 4 * min(xu, W - 1);
+        const unsigned a = abits_sh[wave][i * 64 + lane];
+        float v[SR];
+#pragma unroll
+        for (int j = 0; j < SR; ++j)
+          v[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, min(y0 + j, H - 1) * rowb, 0));
+#pragma unroll
+        for (int j = 0; j < SR; ++j) {
+          const float c = v[j];
+          v[j] = ((a >> j) & 1u) ? c : c * 0.0f;
+          if (!xok || y0 + j >= H) v[j] = NAN;
+        }
+        const int base_id = y0 * W + xu;
+        const size_t ui = ub + su + i;
+        if ((live >> i) & 1u)
+          wave_topk(v, base_id, W, K, [](float x) { return x > 0.0f; }, cand_v + ui * K, cand_i + ui * K);
+        if ((negl >> i) & 1u)
+          wave_topk(v, base_id, W, K, [](float x) { return x < 0.0f; }, neg_v + ui * K, neg_i + ui * K);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+}
+
 // Wave-level exact top-`take` of n candidates (value desc, index asc) into out (lane 0 writes);
-// returns the number of valid entries written.
+// returns the number of valid entries written. gate (optional): candidate c belongs to list c / K of the plane, which
+// holds entries only when gate[c / K] < K (the negative lists: a unit's non-negative count).
 template <int KMAX>
 __device__ __forceinline__ int merge_candidates(const float* __restrict__ cv, const int* __restrict__ ci, int n,
-                                                int take, float* out_v, int* out_i) {
+                                                int take, float* out_v, int* out_i, const int* __restrict__ gate = nullptr,
+                                                int gk = 1, int goff = 0) {
   const int lane = threadIdx.x & 63;
   float lv[KMAX];
   int li[KMAX];
@@ -702,17 +1020,18 @@ __device__ __forceinline__ int merge_candidates(const float* __restrict__ cv, co
   constexpr int PER = 16;
   for (int c0 = lane; c0 < n; c0 += 64 * PER) {
     float vq[PER];
-    int iq[PER];
+    int iq[PER], gq[PER];
 #pragma unroll
     for (int r = 0; r < PER; ++r) {
       const int c = min(c0 + 64 * r, n - 1);
       vq[r] = cv[c];
       iq[r] = ci[c];
+      gq[r] = gate ? gate[(goff + c) / gk] : 0;
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int r = 0; r < PER; ++r) {
-      if (c0 + 64 * r >= n) iq[r] = INV;
+      if (c0 + 64 * r >= n || gq[r] >= gk) iq[r] = INV;
     }
 #pragma unroll
     for (int r = 0; r < PER; ++r) {
@@ -750,10 +1069,11 @@ __device__ __forceinline__ int merge_candidates(const float* __restrict__ cv, co
 // quarter to its own top-`take` in LDS, wave 0 merges those. Returns the count (all threads).
 template <int KMAX>
 __device__ int block_topk(const float* __restrict__ cv, const int* __restrict__ ci, int n, int take, float* out_v,
-                          int* out_i, float (*lv)[KMAX], int (*li)[KMAX], int* cnt) {
+                          int* out_i, float (*lv)[KMAX], int (*li)[KMAX], int* cnt, const int* __restrict__ gate = nullptr,
+                          int gk = 1) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int q = (n + 3) / 4, lo = min(n, wave * q), hi = min(n, lo + q);
-  const int got = merge_candidates<KMAX>(cv + lo, ci + lo, hi - lo, take, lv[wave], li[wave]);
+  const int got = merge_candidates<KMAX>(cv + lo, ci + lo, hi - lo, take, lv[wave], li[wave], gate, gk, lo);
   for (int k = got + lane; k < KMAX; k += 64) li[wave][k] = INV;
   __syncthreads();
   if (wave == 0) {
@@ -805,7 +1125,9 @@ __global__ __launch_bounds__(256) void plane_top_kernel(DetectGeom g, float thr,
     if (lane == 0) sh[4 + wave] = nn;
     __syncthreads();
     nn = sh[4] + sh[5] + sh[6] + sh[7];
-    if (nn < K) n += block_topk<KMAX>(neg_v + pt * K, neg_i + pt * K, nl * K, K - nn, top_v + n, top_i + n, lv, li, &sh[1]);
+    if (nn < K)   // (a unit's negative list holds entries only when its non-negative count is below K)
+      n += block_topk<KMAX>(neg_v + pt * K, neg_i + pt * K, nl * K, K - nn, top_v + n, top_i + n, lv, li, &sh[1],
+                            tile_nonneg + pt, K);
   }
   if (threadIdx.x == 0) {
     int m = 0;
@@ -1156,7 +1478,8 @@ __global__ __launch_bounds__(256) void plane_emit_kernel(const float* __restrict
   else
     n = block_topk<KMAX>(w.cand_v + pt * K, w.cand_i + pt * K, nl * K, K, top_v, top_i, lv, li, &sh[0]);
   if (use_thr && nn < K)   // degenerate plane (fewer than K non-negative pixels): its top-k also holds negatives
-    n += block_topk<KMAX>(w.neg_v + pt * K, w.neg_i + pt * K, nl * K, K - nn, top_v + n, top_i + n, lv, li, &sh[1]);
+    n += block_topk<KMAX>(w.neg_v + pt * K, w.neg_i + pt * K, nl * K, K - nn, top_v + n, top_i + n, lv, li, &sh[1],
+                          w.tile_nonneg + pt, K);
   PEMP_CLK(2);
   // ---- D: the listed entries (wave 0, one lane per entry) ----
   if (wave == 0) {
@@ -1380,6 +1703,47 @@ static void launch_nms(const float* s, const float* masks, const DetectGeom& g, 
   }
 }
 
+template <int P>
+static void launch_quad(const float* s, const DetectGeom& g, float thr, const DetectWs& w, hipStream_t st) {
+  const int total = g.B * g.J * g.blocks;
+  const int want = (total + NT1 / 64 - 1) / (NT1 / 64);
+  auto launch = [&](auto kern) {
+    int per_cu = NMS_QUAD_PER_CU, occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, NT1, 0) == hipSuccess && occ > 0)
+      per_cu = std::min(per_cu, occ);
+    static const int cus = [] {
+      const char* e = getenv("PEMP_NMS_RESERVE_CUS");
+      const int r = e ? (atoi(e) & ~7) : NMS_RESERVE_CUS;
+      return std::max(8, num_cus() - std::max(r, 0));
+    }();
+    const int grid = want < per_cu * cus ? want : per_cu * cus;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NT1), 0, st, s, g, thr, w.cand_v, w.cand_i, w.neg_v, w.neg_i,
+                       w.tile_count, w.tile_nonneg, w.cbits, w.pflag);
+  };
+  if (thr > 0.0f && NMS_THR_POS) launch(nms_quad_kernel<P, true>);
+  else launch(nms_quad_kernel<P, false>);
+}
+
+static void dispatch_quad(const float* s, const DetectGeom& g, float thr, const DetectWs& w, hipStream_t st) {
+  switch (g.pr) {
+    case 0: launch_quad<0>(s, g, thr, w, st); break;
+    case 1: launch_quad<1>(s, g, thr, w, st); break;
+    case 2: launch_quad<2>(s, g, thr, w, st); break;
+    case 3: launch_quad<3>(s, g, thr, w, st); break;
+    default: launch_quad<4>(s, g, thr, w, st); break;
+  }
+}
+
+// the quad layout takes dense MODE_POS detection without masks (PEMP_NMS_QUAD=0: the strip kernel, A/B runs); the
+// choice depends only on the call's arguments, so a SELECT-only call on the same workspace sees the same layout
+static bool use_quad(bool projected, bool masked, int use_thr) {
+  static const bool on = [] {
+    const char* e = getenv("PEMP_NMS_QUAD");
+    return e ? atoi(e) != 0 : NMS_QUAD != 0;
+  }();
+  return on && !projected && !masked && use_thr;
+}
+
 template <int MODE, int PROJ>
 static void dispatch_nms(const float* s, const float* masks, const DetectGeom& g, float thr, int use_thr,
                          const DetectWs& w, const ProjArgs& pj, hipStream_t st) {
@@ -1424,7 +1788,9 @@ static int launch_detect(const float* s, const float* masks, const DetectGeom& g
                          int32_t* n_host, const ProjArgs& pj, hipStream_t st) {
   if (stages & PEMP_DETECT_NMS) {
     ProfScope prof(pj.S ? "detect_nms_projected" : "detect_nms", st);
-    if (pj.S && proj_sep_ok(pj, g)) {
+    if (g.quad) {
+      dispatch_quad(s, g, thr, w, st);
+    } else if (pj.S && proj_sep_ok(pj, g)) {
       if (use_thr) dispatch_nms<MODE_POS, 2>(s, masks, g, thr, use_thr, w, pj, st);
       else dispatch_nms<MODE_ALL, 2>(s, masks, g, thr, use_thr, w, pj, st);
     } else if (pj.S) {
@@ -1600,7 +1966,7 @@ static int detect_impl(const float* scoremaps, const ProjArgs* proj, const float
   PEMP_CHECK_ARG(cap >= 0, "pemp_detect: cap < 0");
   PEMP_CHECK_ARG((size_t)H * W * 4 < 0x7fffffffull, "pemp_detect: plane too large (H * W * 4 >= 2^31)");
   const int K = topk < H * W ? topk : H * W;
-  const DetectGeom g = geom(B, J, H, W, pool_kernel, K);
+  const DetectGeom g = geom(B, J, H, W, pool_kernel, K, use_quad(proj != nullptr, masks != nullptr, use_threshold));
   PEMP_CHECK_ARG(g.nsx <= 64, "pemp_detect: W=%d too wide (max %d for pool_kernel %d)", W, 64 * g.sc, pool_kernel);
   PEMP_CHECK_ARG(g.nb <= MAXB, "pemp_detect: H=%d too tall (max %d)", H, MAXB * SR);
   size_t need = 0;

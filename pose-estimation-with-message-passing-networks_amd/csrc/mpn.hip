@@ -4404,6 +4404,7 @@ extern "C" size_t pemp_abi_struct_size(int which) {
     case 1: return sizeof(pemp_mpn_desc);
     case 2: return sizeof(pemp_mlp);
     case 3: return sizeof(pemp_proj_maps);
+    case 4: return sizeof(pemp_step_plan);
     default: return 0;
   }
 }

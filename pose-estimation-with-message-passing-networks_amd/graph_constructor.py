@@ -58,6 +58,68 @@ def _tag_knn(edge_index, ws, offs, node_off, node_off_h):
 # the capacity graph build hands the capacity-mode MPN the batch's (N, E, overflow) (PEMP_BUILD_WRITE_COUNTS), so the
 # forward starts without a counting launch of its own; PEMP_NO_BUILD_COUNTS=1 restores that launch (A/B runs)
 _BUILD_COUNTS = not os.environ.get("PEMP_NO_BUILD_COUNTS")
+# a repeated fully-graph batch shape goes through the batch-step entry (pemp_step_fully_cap: one C call, one output
+# buffer) under PEMP_STEP_ENTRY=1 (A/B runs until measured)
+_STEP_ENTRY = _BUILD_COUNTS and os.environ.get("PEMP_STEP_ENTRY", "0") not in ("", "0")
+
+
+class _StepPlan:
+    """A pemp_step_plan (include/pemp.h) for one batch shape, capacity set and forward, with the workspaces it names
+    kept alive; outputs() cuts one call's output buffer into construct_graph's tensors."""
+
+    def __init__(self, L, B, J, H, W, pool, use_thr, topk, thr, cap, det_ws, C, F, A, mode, norm, n_cap, e_cap, mi,
+                 proj):
+        p = _lib.PempStepPlan(B=B, J=J, H=H, W=W, pool_kernel=pool, use_threshold=int(use_thr), topk=topk,
+                              det_cap=cap, projected=int(proj), threshold=thr, det_workspace=det_ws.data_ptr(),
+                              det_workspace_bytes=det_ws.numel(), C=C, F=F, A=A, mode=mode, norm_factor=norm,
+                              n_cap=n_cap, e_cap=e_cap)
+        self.mi = mi                                     # (desc, folded weights, workspace, key): kept alive here
+        if mi is not None:
+            p.desc = ctypes.pointer(mi[0])
+            p.weights = ctypes.pointer(mi[1].struct)
+            p.mpn_workspace = mi[2].data_ptr()
+            p.mpn_workspace_bytes = mi[2].numel()
+        if not L.pemp_step_layout(ctypes.byref(p)):
+            raise ValueError(L.pemp_last_error().decode())
+        self.struct, self.ref, self.det_ws = p, ctypes.byref(p), det_ws
+        self.B, self.cap, self.C, self.F, self.A = B, cap, C, F, A
+        self.off = [p.off[i] for i in range(_lib.STEP_NOUT)]
+
+    def detections(self, flat):
+        """(det_xyt [B, cap, 3], det_scores [B, cap], n_det [B]) of the call that wrote flat."""
+        o, B, cap = self.off, self.B, self.cap
+        i64, f32, i32 = flat.view(torch.int64), flat.view(torch.float32), flat.view(torch.int32)
+        return (i64.as_strided((B, cap, 3), (3 * cap, 3, 1), o[_lib.STEP_DET] // 8),
+                f32.as_strided((B, cap), (cap, 1), o[_lib.STEP_DSC] // 4),
+                i32.as_strided((B,), (1,), o[_lib.STEP_NDET] // 4))
+
+    def outputs(self, flat, counts_l, cap, tags, mpn, mi):
+        """construct_graph's 15-tuple from the call's buffer when the batch fit the capacities (else None); with a
+        forward, its queued logits are attached to edge_index for the model call to take."""
+        p = self.struct
+        N = sum(counts_l)
+        E = sum(c * (c - 1) for c in counts_l if c > 1)
+        if (max(counts_l) if counts_l else 0) > cap or N > p.n_cap or E > p.e_cap:
+            return None
+        o, C, F, A = self.off, self.C, self.F, self.A
+        i64, f32 = flat.view(torch.int64), flat.view(torch.float32)
+        x = f32.as_strided((N, C), (C, 1), o[_lib.STEP_X] // 4)
+        joint_det = i64.as_strided((N, 3), (3, 1), o[_lib.STEP_JDET] // 8)
+        joint_scores = f32.as_strided((N,), (1,), o[_lib.STEP_JSC] // 4)
+        batch_index = i64.as_strided((N,), (1,), o[_lib.STEP_BIDX] // 8)
+        joint_tags = None
+        if tags is not None:   # [N, F] as the reference's tagmaps[b, type, y, x] rows: [N, *tags.shape[4:]] or [N]
+            joint_tags = f32.as_strided((N, F), (F, 1), o[_lib.STEP_JTAGS] // 4).view(
+                (N,) + tuple(tags.shape[4:]) if tags.dim() > 4 else (N,))
+        edge_index = i64.as_strided((2, E), (E, 1), o[_lib.STEP_EIDX] // 8)
+        edge_attr = f32.as_strided((E, A), (A, 1), o[_lib.STEP_EATTR] // 4)
+        node_off = i64.as_strided((self.B + 4,), (1,), o[_lib.STEP_NOFF] // 8)
+        _tag_fully(edge_index, node_off, counts_l, joint_det)
+        if mpn is not None:
+            res = dict(buf=f32[o[_lib.STEP_LOGITS] // 4:], a1=p.nlog_off, a2=p.clog_off, n_rec=p.n_rec, key=mi[3])
+            mpn._attach_cap(res, x, edge_attr, edge_index, joint_det, N, E)
+        return (x, edge_attr, edge_index, None, None, None, None, joint_det, None, None, None, joint_scores,
+                batch_index, None, joint_tags)
 
 
 def get_graph_constructor(config, **kwargs):
@@ -230,22 +292,13 @@ class NaiveGraphConstructor:
         dev = sm.device
 
         # ---- detection (pemp_detect): one read-back of the per-image counts ----
-        ws_bytes = L.pemp_detect_workspace_size(B, J, H, W, topk)
-        ws = self._ws_detect.get(ws_bytes, dev)
-        with NaiveGraphConstructor._mu:
-            cap = NaiveGraphConstructor._cap
-        det = torch.empty(B, cap, 3, dtype=torch.int64, device=dev)
-        dsc = torch.empty(B, cap, dtype=torch.float32, device=dev)
-        n_det = torch.empty(B, dtype=torch.int32, device=dev)
         counts_ent = self._host_counts_take(L, dev, B)
-        gen = self._construct(L, st, sm, masks, B, J, H, W, use_thr, topk, thr, dev, ws, cap, det, dsc, n_det,
-                              counts_ent[2][:B])
+        gen = self._construct(L, st, sm, masks, B, J, H, W, use_thr, topk, thr, dev, counts_ent[2][:B])
         pending = PendingGraph(self, gen, dev, counts_ent)
         pending._step()                             # up to the count wait: everything is queued
         return pending
 
-    def _construct(self, L, st, sm, masks, B, J, H, W, use_thr, topk, thr, dev, ws, cap, det, dsc, n_det,
-                   counts_h):
+    def _construct(self, L, st, sm, masks, B, J, H, W, use_thr, topk, thr, dev, counts_h):
         # host-side preparation of the graph stage, before the first launch: with a capacity hint the detection,
         # the graph build and the MPN are then queued back to back (no host gap between them on the GPU), and in a
         # loop this preparation overlaps the previous batch's GPU work
@@ -288,9 +341,47 @@ class NaiveGraphConstructor:
         gkey = (B, J, H, W, C, F, A, dev)
         with NaiveGraphConstructor._mu:
             hint = NaiveGraphConstructor._graph_hint.get(gkey) if fully else None
+            cap = NaiveGraphConstructor._cap
         built = None
         pending = None
         launch_mpn = None
+        step = hint is not None and _STEP_ENTRY and not projected
+        if step:
+            # the batch-step entry: detection + capacity build + the bound MPN in one call, outputs in one buffer
+            n_cap, e_cap = hint
+            mpn = NaiveGraphConstructor._bound_mpn
+            mi = None
+            if mpn is not None and J == getattr(mpn, "num_types", None) and getattr(mpn, "_cap_ok", True):
+                mi = mpn._cap_info(C, A, n_cap, e_cap, dev)
+            plan = self._step_plan(L, dev, st, B, J, H, W, use_thr, topk, thr, cap, C, F if tags is not None else 0,
+                                   A, mode, norm, n_cap, e_cap, mi, self._proj is not None)
+            flat = torch.empty(plan.struct.bytes, dtype=torch.uint8, device=dev)
+            counts_h.fill(-1)
+            rc = L.pemp_step_fully_cap(plan.ref, self._detect_src(sm), _lib.ptr(masks), _lib.ptr(feats), _lib.ptr(tags),
+                                       flat.data_ptr(), counts_h.ctypes.data, st)
+            if rc == _lib.ERR_UNSUPPORTED and mi is not None:
+                mpn._cap_ok = False     # the forward's conditions refused this model: the exact forward from now on
+                mi = None
+            else:
+                _lib.check(rc)
+            yield None                                       # (construct_graph_start returns here)
+            counts_l = self._wait_counts(counts_h, dev)
+            out = plan.outputs(flat, counts_l, cap, tags, mpn if mi is not None else None, mi)
+            if out is not None:
+                self._update_hint(gkey, counts_l)
+                if proj_tags is not None:   # sampled at the detections (pemp_gather_projected_tags)
+                    out = out[:14] + (self._gather_proj_tags(L, st, proj_tags, J, H, W, out[7], out[12],
+                                                             out[0].shape[0], dev),)
+                return out
+            # a capacity was exceeded: the exact path below on the step's detections
+            ws = plan.det_ws
+            det, dsc, n_det = plan.detections(flat)
+            hint = None
+        else:
+            ws = self._ws_detect.get(L.pemp_detect_workspace_size(B, J, H, W, topk), dev)
+            det = torch.empty(B, cap, 3, dtype=torch.int64, device=dev)
+            dsc = torch.empty(B, cap, dtype=torch.float32, device=dev)
+            n_det = torch.empty(B, dtype=torch.int32, device=dev)
         if hint is not None:
             n_cap, e_cap = hint
             bufs = (torch.empty(n_cap, C, dtype=torch.float32, device=dev),
@@ -310,15 +401,12 @@ class NaiveGraphConstructor:
                 pending_mpn = mpn
                 launch_mpn = mpn._prepare_cap(bufs[0], bufs[6], bufs[1], n_cap, e_cap, n_det, cap, bufs[7], B,
                                               counts_in_off=_BUILD_COUNTS)
-        detect = self._detect(L)
-        detect_args = (self._detect_src(sm), _lib.ptr(masks), B, J, H, W, self.pool_kernel_size, thr, int(use_thr), topk, 3,
-                       _lib.ptr(ws), ws.numel(), _lib.ptr(det), _lib.ptr(dsc), _lib.ptr(n_det), cap, counts_h.ctypes.data,
-                       st)
-        counts_h.fill(-1)
-        _lib.check(detect(*detect_args))
-        if hint is not None:
+        if step:
+            pass                                             # (queued, and the counts read, above)
+        elif hint is not None:
             # capacity mode: the graph build (and the bound MPN) queued before the counts are read, so the GPU
             # builds the graph while the host waits for them (pemp_fully_graph_build_cap)
+            self._detect_launch(L, st, sm, masks, B, J, H, W, use_thr, topk, thr, ws, det, dsc, n_det, cap, counts_h)
             _lib.check(L.pemp_fully_graph_build_cap(*build_args))
             if launch_mpn is not None:
                 pending = launch_mpn()
@@ -326,6 +414,7 @@ class NaiveGraphConstructor:
             counts_l = self._wait_counts(counts_h, dev)
             built = bufs
         else:
+            self._detect_launch(L, st, sm, masks, B, J, H, W, use_thr, topk, thr, ws, det, dsc, n_det, cap, counts_h)
             yield None
             counts_l = self._wait_counts(counts_h, dev)      # the one host read-back of the batch
         mx = max(counts_l) if counts_l else 0
@@ -341,12 +430,8 @@ class NaiveGraphConstructor:
                                        _lib.ptr(n_det), cap, None, st))
         N = sum(counts_l)
         E_fully = sum(c * (c - 1) for c in counts_l if c > 1)
-        if fully:   # capacities for the next batch of this shape: 25 % headroom over this one
-            n_hint = (N + N // 4 + 16, E_fully + E_fully // 4 + 256)
-            with NaiveGraphConstructor._mu:
-                old = NaiveGraphConstructor._graph_hint.get(gkey)
-                NaiveGraphConstructor._graph_hint[gkey] = n_hint if old is None else (
-                    max(old[0], n_hint[0]), max(old[1], n_hint[1]))
+        if fully:
+            self._update_hint(gkey, counts_l)
         if built is not None and mx <= cap_used and N <= built[0].shape[0] and E_fully <= built[6].shape[0]:
             # the capacity build fit: the outputs are leading (contiguous) slices of its buffers
             x, joint_det, joint_scores, batch_index = built[0][:N], built[1][:N], built[2][:N], built[3][:N]
@@ -420,6 +505,43 @@ class NaiveGraphConstructor:
             joint_tags = self._gather_proj_tags(L, st, proj_tags, J, H, W, joint_det, batch_index, N, dev)
         return (x, edge_attr, edge_index, None, None, None, None, joint_det, None, None, None, joint_scores,
                 batch_index, None, joint_tags)
+
+    @staticmethod
+    def _update_hint(gkey, counts_l):
+        """Capacities for the next batch of this shape: 25 % headroom over this one (grow-only)."""
+        N = sum(counts_l)
+        E = sum(c * (c - 1) for c in counts_l if c > 1)
+        n_hint = (N + N // 4 + 16, E + E // 4 + 256)
+        with NaiveGraphConstructor._mu:
+            old = NaiveGraphConstructor._graph_hint.get(gkey)
+            NaiveGraphConstructor._graph_hint[gkey] = n_hint if old is None else (
+                max(old[0], n_hint[0]), max(old[1], n_hint[1]))
+
+    def _detect_launch(self, L, st, sm, masks, B, J, H, W, use_thr, topk, thr, ws, det, dsc, n_det, cap, counts_h):
+        counts_h.fill(-1)
+        _lib.check(self._detect(L)(self._detect_src(sm), _lib.ptr(masks), B, J, H, W, self.pool_kernel_size, thr,
+                                   int(use_thr), topk, 3, _lib.ptr(ws), ws.numel(), _lib.ptr(det), _lib.ptr(dsc),
+                                   _lib.ptr(n_det), cap, counts_h.ctypes.data, st))
+
+    _plans = {}   # (device, stream, batch shape, capacities, forward) -> _StepPlan (under _mu)
+
+    def _step_plan(self, L, dev, st, B, J, H, W, use_thr, topk, thr, cap, C, F, A, mode, norm, n_cap, e_cap, mi,
+                   proj):
+        """The pemp_step_fully_cap plan of this call's arguments (cached per device, stream and shape)."""
+        fkey = None if mi is None else (id(mi[1]), mi[2].data_ptr(), mi[2].numel(), ctypes.addressof(mi[0]))
+        key = (dev.index, st, B, J, H, W, self.pool_kernel_size, use_thr, topk, thr, cap, C, F, A, mode, norm, n_cap,
+               e_cap, fkey, proj)
+        with NaiveGraphConstructor._mu:
+            plan = NaiveGraphConstructor._plans.get(key)
+        if plan is None:
+            ws = self._ws_detect.get(L.pemp_detect_workspace_size(B, J, H, W, topk), dev)
+            plan = _StepPlan(L, B, J, H, W, self.pool_kernel_size, use_thr, topk, thr, cap, ws, C, F, A, mode, norm,
+                             n_cap, e_cap, mi, proj)
+            with NaiveGraphConstructor._mu:
+                if len(NaiveGraphConstructor._plans) >= 64:
+                    NaiveGraphConstructor._plans.clear()
+                NaiveGraphConstructor._plans[key] = plan
+        return plan
 
     def _detect(self, L):
         return L.pemp_detect_projected if self._proj is not None else L.pemp_detect

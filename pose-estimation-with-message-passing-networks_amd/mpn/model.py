@@ -209,6 +209,7 @@ class NodeClassificationMPNSimple(nn.Module):
         self._tensors = None
         self._ws = _lib.Workspace()
         self._desc_key = None
+        self._cap_ok = True   # pemp_step_fully_cap may queue this model's forward (cleared when the library refuses it)
         # one libpemp call addresses r, Q0 and the aggregates with 32-bit byte offsets (pemp_mpn_forward: E, T N
         # < 2^23); larger calls are cut into node blocks no edge crosses (image blocks for construct_graph output)
         self._edge_limit = _EDGE_LIMIT
@@ -419,6 +420,27 @@ class NodeClassificationMPNSimple(nn.Module):
             _lib.check(rc)
             return result
         return launch
+
+    def _cap_info(self, C, A, n_cap, e_cap, dev):
+        """The forward's part of a pemp_step_fully_cap plan (graph_constructor's batch-step entry): (descriptor with
+        PEMP_MPN_COUNTS_IN_OFFSETS, folded weights, workspace, key of the weights it was planned under), or None when
+        this model / capacity takes the exact forward (the conditions of _prepare_cap)."""
+        if self.training or self.node_summary != "not" or _FULLY_OFF or dev.type != "cuda":
+            return None
+        if e_cap > self._edge_limit or self.num_types * n_cap > self._node_rows_limit:
+            return None
+        fw = self._weights(dev)
+        dkey = (A, C, self.precision, 3)
+        if getattr(self, "_desc_cnt_key", None) != dkey:
+            steps, aux = self.edge_steps, self.aux_loss_steps
+            self._n_rec = sum(1 for i in range(steps) if i >= steps - aux - 1)
+            self._desc_cnt = _lib.PempMpnDesc(self.num_types, self.num_joints, steps, aux, self.aggr_code, 64, A, C,
+                                              PRECISIONS[self.precision], 3, _lib.MPN_COUNTS_IN_OFFSETS)
+            self._desc_cnt_ref = ctypes.byref(self._desc_cnt)
+            self._desc_cnt_key = dkey
+        L = _lib.lib()
+        ws = self._ws.get(L.pemp_mpn_workspace_size(self._desc_cnt_ref, n_cap, e_cap), dev)
+        return self._desc_cnt, fw, ws, (dev, self.precision, self._folded_key)
 
     def _attach_cap(self, pending, x, edge_attr, edge_index, joint_det, N, E):
         """Tag construct_graph's output with the queued result (the capacity batch fit: N, E are its counts)."""

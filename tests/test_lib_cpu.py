@@ -78,6 +78,31 @@ def test_ctypes_struct_mirrors_match_the_library():
     every later field of the struct the kernels read)."""
     import ctypes
     L = _lib.load_cdll()
-    for which, cls in enumerate((_lib.PempMpnWeights, _lib.PempMpnDesc, _lib.PempMlp, _lib.PempProjMaps)):
+    for which, cls in enumerate((_lib.PempMpnWeights, _lib.PempMpnDesc, _lib.PempMlp, _lib.PempProjMaps,
+                                 _lib.PempStepPlan)):
         assert L.pemp_abi_struct_size(which) == ctypes.sizeof(cls), cls.__name__
     assert L.pemp_abi_struct_size(7) == 0
+
+
+def test_step_layout_is_host_arithmetic():
+    """pemp_step_layout (host only): every output of the batch-step entry at a 256-byte aligned offset, in order,
+    without overlap; the logit arrays laid out as mpn/model.py's forward lays them (64-element boundaries)."""
+    import ctypes
+    L = _lib.load_cdll()
+    desc = _lib.PempMpnDesc(17, 17, 3, 1, 3, 64, 19, 128, 2, 3, _lib.MPN_COUNTS_IN_OFFSETS)
+    p = _lib.PempStepPlan(B=8, J=17, H=640, W=640, pool_kernel=5, use_threshold=1, topk=5, det_cap=512, threshold=0.1,
+                          C=128, F=1, A=19, mode=0, norm_factor=640.0, n_cap=1546, e_cap=232_846)
+    p.desc = ctypes.pointer(desc)
+    n = L.pemp_step_layout(ctypes.byref(p))
+    assert n == p.bytes and n % 256 == 0
+    sizes = [8 * 512 * 3 * 8, 8 * 512 * 4, 8 * 4, 1546 * 128 * 4, 1546 * 24, 1546 * 4, 1546 * 8, 1546 * 4,
+             2 * 232_846 * 8, 232_846 * 19 * 4, 12 * 8]
+    for i, sz in enumerate(sizes):
+        assert p.off[i] % 256 == 0 and p.off[i] + sz <= p.off[i + 1], i
+    assert p.n_rec == 2                          # T = 3, AUX_LOSS_STEPS 1: iterations 1 and 2 recorded
+    ne, nn = 2 * 232_846, 3 * 1546
+    assert (p.elog_n, p.nlog_off) == (ne, (ne + 63) // 64 * 64)
+    assert p.clog_off == p.nlog_off + (nn + 63) // 64 * 64
+    assert p.off[_lib.STEP_LOGITS] + 4 * (p.clog_off + nn * 17) <= n
+    p.B = 0
+    assert L.pemp_step_layout(ctypes.byref(p)) == 0
