@@ -59,8 +59,9 @@ def _tag_knn(edge_index, ws, offs, node_off, node_off_h):
 # forward starts without a counting launch of its own; PEMP_NO_BUILD_COUNTS=1 restores that launch (A/B runs)
 _BUILD_COUNTS = not os.environ.get("PEMP_NO_BUILD_COUNTS")
 # a repeated fully-graph batch shape goes through the batch-step entry (pemp_step_fully_cap: one C call, one output
-# buffer) under PEMP_STEP_ENTRY=1 (A/B runs until measured)
-_STEP_ENTRY = _BUILD_COUNTS and os.environ.get("PEMP_STEP_ENTRY", "0") not in ("", "0")
+# buffer; c2 0.17 -> 0.13 ms per step, profiles/r06_step_entry.md); PEMP_STEP_ENTRY=0 restores the three calls and
+# the per-output allocations (A/B runs)
+_STEP_ENTRY = _BUILD_COUNTS and os.environ.get("PEMP_STEP_ENTRY", "1") not in ("", "0")
 
 
 class _StepPlan:

@@ -357,7 +357,8 @@ def test_capacity_graphs_single_key_and_debug_sync(tmp_path):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     outs = {}
     for dbg in ("0", "1"):
-        env = dict(os.environ, PEMP_DEBUG_SYNC=dbg, PEMP_GRAPHS="1", PYTHONPATH=root)
+        # (the script counts the forward's calls through its Python binding: the three-call capacity path)
+        env = dict(os.environ, PEMP_DEBUG_SYNC=dbg, PEMP_GRAPHS="1", PEMP_STEP_ENTRY="0", PYTHONPATH=root)
         r = subprocess.run([sys.executable, str(script)], env=env, cwd=root, capture_output=True, text=True,
                            timeout=240)
         assert r.returncode == 0, r.stderr[-3000:]
