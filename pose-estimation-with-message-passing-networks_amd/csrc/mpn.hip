@@ -37,7 +37,17 @@ namespace {
 constexpr int D = 64;
 constexpr int LDW = 72;     // LDS row stride of a 64x64 weight tile (conflict-free ds_read_b128)
 constexpr int MAXT = 17;
-constexpr int EDGE_WAVES = 16;   // waves per edge-pass / edge-embedding workgroup (one workgroup per CU)
+constexpr int EDGE_WAVES = 16;   // waves per edge-pass workgroup (one workgroup per CU)
+// edge embedding: EMB_WAVES waves per workgroup, EMB_PER_CU workgroups per CU (each with its own LDS image; the
+// register target follows: EMB_WAVES x EMB_PER_CU / 4 waves per SIMD)
+#ifndef PEMP_EMB_WAVES
+#define PEMP_EMB_WAVES 16
+#endif
+#ifndef PEMP_EMB_PER_CU
+#define PEMP_EMB_PER_CU 1
+#endif
+constexpr int EMB_WAVES = PEMP_EMB_WAVES, EMB_PER_CU = PEMP_EMB_PER_CU;
+constexpr int EMB_MIN_WAVES_EU = EMB_WAVES * EMB_PER_CU / 4 > 1 ? EMB_WAVES * EMB_PER_CU / 4 : 1;
 #ifndef PEMP_RESERVE_CUS_DEFAULT
 #define PEMP_RESERVE_CUS_DEFAULT 64
 #endif
@@ -1278,7 +1288,8 @@ __device__ __forceinline__ void lds_drain();
 // FX: 0 runtime-shaped layers, 1 the fixed published shape, 2 the same composed (embed_tile_fixed COMP: f16x3 only,
 // with the caller's composed packs)
 template <int PREC, int FX>
-__global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp emb, EmbedLayout Lo,
+__global__ __launch_bounds__(64 * EMB_WAVES) __attribute__((amdgpu_waves_per_eu(EMB_MIN_WAVES_EU, 8)))
+void edge_embed_kernel(pemp_mlp emb, EmbedLayout Lo,
                                                                      const uint16_t* __restrict__ emb_bf,
                                                                      const float* __restrict__ ea, int A,
                                                                      const int* __restrict__ s_orig, int64_t E,
@@ -1299,11 +1310,11 @@ __global__ __launch_bounds__(64 * EDGE_WAVES) void edge_embed_kernel(pemp_mlp em
     dma_to_lds(sm, img, COMP ? embed_comp_floats(Lo) : embed_image_floats(Lo));
     lds_drain();
   } else {
-    embed_stage<PREC, FIXED>(sm, threadIdx.x, 64 * EDGE_WAVES, emb, Lo, emb_bf, q0_w, q0_b, e1_w, e1_bf,
+    embed_stage<PREC, FIXED>(sm, threadIdx.x, 64 * EMB_WAVES, emb, Lo, emb_bf, q0_w, q0_b, e1_w, e1_bf,
                              COMP ? comp_bf : nullptr, COMP ? comp_b : nullptr);
   }
   __syncthreads();
-  const int64_t gw = (int64_t)blockIdx.x * EDGE_WAVES + wave, nw = (int64_t)gridDim.x * EDGE_WAVES;
+  const int64_t gw = (int64_t)blockIdx.x * EMB_WAVES + wave, nw = (int64_t)gridDim.x * EMB_WAVES;
   const int first = __builtin_amdgcn_readfirstlane((int)(E * gw / nw));
   const int end = __builtin_amdgcn_readfirstlane((int)(E * (gw + 1) / nw));
   // buffer descriptors + 32-bit offsets: no 64-bit lane pointers live across the tile loop
@@ -4048,14 +4059,15 @@ static int mpn_forward_impl(const pemp_mpn_desc* desc, const pemp_mpn_weights* w
   if (E > 0 && steps >= 1) {
     ProfScope prof("edge_embed", pst);
     if (emb_lds) {
-      const int grid = (int)std::min<int64_t>(PEMP_EMBED_RESERVE ? edge_cus(E) : num_cus(), (E + 16 * EDGE_WAVES - 1) / (16 * EDGE_WAVES));
+      const int grid = (int)std::min<int64_t>((int64_t)(PEMP_EMBED_RESERVE ? edge_cus(E) : num_cus()) * EMB_PER_CU,
+                                              (E + 16 * EMB_WAVES - 1) / (16 * EMB_WAVES));
       const bool fixed = embed_fixed_shape(emb_lo);
       const bool comp = embed_composed(emb_lo, emb_prec, *w);
       const size_t lds = (size_t)(comp ? embed_comp_floats(emb_lo) : embed_image_floats(emb_lo)) * sizeof(float);
       // the caller's prebuilt LDS image (pemp_mpn_edge_image appends it to the edge-pass image), else staged here
       const float* emb_img = w->edge_img ? w->edge_img + embed_image_offset(*desc, *w) : nullptr;
 #define PEMP_EMBED_LAUNCH(P, FX)                                                                                   \
-  hipLaunchKernelGGL((edge_embed_kernel<P, FX>), dim3(grid), dim3(64 * EDGE_WAVES), lds, pst, w->edge_emb, emb_lo,  \
+  hipLaunchKernelGGL((edge_embed_kernel<P, FX>), dim3(grid), dim3(64 * EMB_WAVES), lds, pst, w->edge_emb, emb_lo,   \
                      w->emb_bf, edge_attr, desc->edge_attr_dim, ws.s_orig, E, w->q0_w, w->q0_b, w->e1_w, w->e1_bf, \
                      ws.EA, ws.Q0, ne, emb_img, w->emb_comp_bf, w->emb_comp_b)
       if (emb_prec == PEMP_PREC_F16X3) {

@@ -517,3 +517,42 @@ def test_projected_frontend_from_stages(flip, half_sizes, size):
                                          num_joints=J).construct_graph()
     for i in (7, 11, 12, 14, 2, 0, 1):
         assert torch.equal(out[i].cpu(), ref[i]), i
+
+
+QUAD_SCRIPT = r"""
+import json, sys, numpy as np, torch
+from oracle import restate
+from pemp_amd import config as pcfg, synthetic as syn
+from tests.test_gpu_graph import _edge_maps, run_gc
+bad = []
+for H, W, pool in [(50, 1000, 9), (37, 8, 1), (16, 252, 5), (33, 17, 5), (64, 640, 5), (40, 516, 3)]:
+    B, J = 3, 17
+    hm = _edge_maps(B, J, H, W, H * W + pool)
+    feats = torch.from_numpy(syn.closed_form((B, 16, H, W), 0.25))
+    tags = torch.from_numpy(syn.closed_form((B, J, H, W, 1), 0.75))
+    gc = pcfg.inference_gc_config("fully", pool, False)
+    out = run_gc(gc, J, hm, feats, tags, None)
+    ref = restate.construct_graph(hm, feats, tags, None, gc, J)
+    for i in (7, 11, 12, 14, 2):
+        if not torch.equal(out[i].cpu(), ref[i]):
+            bad.append([H, W, pool, i])
+print(json.dumps({"bad": bad}))
+"""
+
+
+def test_detection_quad_nms_variant(tmp_path):
+    """The split dense NMS (nms_quad_kernel, 4 columns per lane, opt-in PEMP_NMS_QUAD=1; the library reads the switch
+    once per process, so it runs in a child) gives the oracle's detections bit for bit on the edge-case maps: W not a
+    multiple of 4 (the clamped loader), blocks past the plane's right edge, planes narrower than a wave, every pool
+    radius, negative planes with fewer than top-k non-negative pixels, plateaus, border maxima."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "quad.py"
+    script.write_text(QUAD_SCRIPT)
+    env = dict(os.environ, PEMP_NMS_QUAD="1", PYTHONPATH=root)
+    r = subprocess.run([sys.executable, str(script)], env=env, cwd=root, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert json.loads(r.stdout.strip().splitlines()[-1])["bad"] == []
