@@ -591,6 +591,10 @@ def frontend_heatmaps(wl, gc, feats, dev, reps=5):
 E2E_NODE_TH = 0.1     # node-probability threshold of the grouping (pred_to_ann th; bench's grouping leg uses the same)
 
 
+E2E_DEPTH = int(os.environ.get("PEMP_E2E_DEPTH", "2"))   # batches whose grouping is in flight (e2e leg)
+E2E_EARLY = os.environ.get("PEMP_E2E_EARLY", "0") not in ("", "0")   # (A/B) launches before the older host parts
+
+
 def e2e_pipeline(wl, gc, model, hm, feats, tags, dev, steps, warmup, world):
     """The post-backbone step valid.py runs per image (valid.py:101-123), for a whole batch: the test front-end's
     maps (ProjectedHeatmaps for the multi-scale workload) -> construct_graph -> MPN -> sigmoid / softmax
@@ -671,17 +675,32 @@ def e2e_pipeline(wl, gc, model, hm, feats, tags, dev, steps, warmup, world):
             # count wait overlapped with them -- at 5.6k vs 8.4k images/s at c3: the count wait then became a wait
             # for batch k's GAEC on the grouping thread, which the old order gives that time to finish;
             # profiles/r06_pipelined_steps.md.)
-            pend, fin_prev = gpu_part(), None
-            for _ in range(n - 1):
-                nxt = gpu_part()
-                fin = host_part(pend)
-                if fin_prev is not None:
-                    persons += collect(fin_prev)
-                pend, fin_prev = nxt, fin
-            fin = host_part(pend)
-            if fin_prev is not None:
-                persons += collect(fin_prev)
-            persons += collect(fin)
+            # E2E_DEPTH batches' groupings in flight: batch k's host part runs once batch k + E2E_DEPTH is queued,
+            # so its GPU edge pass, read-back and GAEC (on the grouping thread) have that many iterations to finish
+            # (depth 1: the host part waited ~0.2 ms per batch for the GAEC, ~0.13 ms for the finishing,
+            # profiles/r06_e2e_depth.md)
+            # E2E_EARLY: batch k+1's launches go out first and its count wait comes after the older batches' host
+            # parts and collection, which it then overlaps
+            from collections import deque
+            jobs, fins = deque(), deque()
+            for _ in range(n):
+                if E2E_EARLY:
+                    p = gpu_start()
+                    if len(jobs) >= E2E_DEPTH:
+                        fins.append(host_part(jobs.popleft()))
+                    if len(fins) > 1:
+                        persons += collect(fins.popleft())
+                    jobs.append(gpu_part(p))
+                    continue
+                jobs.append(gpu_part())
+                if len(jobs) > E2E_DEPTH:
+                    fins.append(host_part(jobs.popleft()))
+                if len(fins) > 1:
+                    persons += collect(fins.popleft())
+            while jobs:
+                fins.append(host_part(jobs.popleft()))
+            while fins:
+                persons += collect(fins.popleft())
         else:
             for _ in range(n):
                 persons += collect(host_part(gpu_part()))

@@ -1,5 +1,7 @@
 """The e2e leg of bench.py alone, interleaved over variants in one process (the leg is bound by host Python and its
-spread between runs and boxes is large): batch-step entry on / off (graph_constructor._STEP_ENTRY), alternating.
+spread between runs and boxes is large): groupings in flight (bench.E2E_DEPTH) x launches first (bench.E2E_EARLY), or
+with E2E_AB_ENTRY=1
+batch-step entry on / off (graph_constructor._STEP_ENTRY) x depth 1 / 2, alternating.
 usage: python tools/e2e_ab.py [workload] [rounds]
 -> one line per (variant, round) and the per-variant medians"""
 import os
@@ -27,11 +29,15 @@ for _ in range(3):
     bench.run_step(wl, gc, model, hm, feats, tags, dev)
 torch.cuda.synchronize()
 res = {}
+variants = [(e, d, 1) for e in (True, False) for d in (1, 2)] if os.environ.get("E2E_AB_ENTRY") else \
+    [(True, 1, 0), (True, 2, 0), (True, 1, 1), (True, 2, 1), (True, 3, 1)]
 for r in range(rounds):
-    for entry in (True, False):
+    for entry, depth, early in variants:
         gcm._STEP_ENTRY = entry
+        bench.E2E_DEPTH = depth
+        bench.E2E_EARLY = bool(early)
         rec = bench.e2e_pipeline(wl, gc, model, hm, feats, tags, dev, 20, 5, 1)
-        key = f"entry={int(entry)}"
+        key = f"entry={int(entry)} depth={depth} early={early}"
         res.setdefault(key, []).append(rec["images_per_sec"])
         print(name, key, r, rec["images_per_sec"], rec["stage_host_ms_per_batch"], flush=True)
 for k, v in res.items():
