@@ -28,3 +28,5 @@ pr.disable()
 st = pstats.Stats(pr)
 st.sort_stats("tottime").print_stats(45)
 st.sort_stats("cumulative").print_stats(60)
+# where the queueing stages spend it (callees of the pose / constructor entry points)
+st.sort_stats("cumulative").print_callees("finish_batch_start|group_persons_start|_construct|gpu_part")
