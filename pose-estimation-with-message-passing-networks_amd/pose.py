@@ -325,13 +325,14 @@ def _check_coords(kp, H, W, name):
     """Detected joints (score > 0) must index inside the [H, W] map: the reference indexes numpy arrays at
     int(x), int(y) there (IndexError past the end; a negative index would wrap around, which pemp rejects
     as well)."""
-    live = kp[:, :, 2] > 0
-    if not live.any():
-        return
+    # int(v) truncates toward zero: int(v) in [0, n) <=> -1 < v < n, and NaN / inf fail both compares (their int64
+    # cast is out of range too); one pass over the coordinates instead of masked copies and casts
+    x, y = kp[:, :, 0], kp[:, :, 1]
+    if kp.size and kp[:, :, :2].min() > -1 and x.max() < W and y.max() < H:
+        return   # every joint inside, detected or not (a NaN fails the compares and takes the full test)
     with np.errstate(invalid="ignore"):
-        x = kp[:, :, 0][live].astype(np.int64)
-        y = kp[:, :, 1][live].astype(np.int64)
-    if (x < 0).any() or (x >= W).any() or (y < 0).any() or (y >= H).any():
+        ok = (x > -1) & (x < W) & (y > -1) & (y < H)
+    if not ok[kp[:, :, 2] > 0].all():
         raise IndexError(f"pemp_amd.pose.{name}: a detected keypoint lies outside the {H}x{W} map")
 
 
@@ -469,7 +470,8 @@ def finish_batch_start(per_image, scoremaps, tags, adjustment=True, with_refine=
         fill_mean(kp_all)
         for k, b in enumerate(live):
             out[b][...] = kp_all[starts[k]:starts[k + 1]]
-    do_ref = np.array([with_refine and kp_all[starts[k], :, 2].sum() != 0 for k in range(len(live))], dtype=bool)
+    # (refine only where the image's first person has a score, Utils.py:1471)
+    do_ref = (kp_all[starts[:-1], :, 2].sum(axis=1) != 0) if with_refine else np.zeros(len(live), dtype=bool)
     if not (adjustment or do_ref.any()):
         return FinishJob(out)
     L = _lib.lib()
@@ -495,11 +497,14 @@ def finish_batch_start(per_image, scoremaps, tags, adjustment=True, with_refine=
     ref = np.zeros(B, dtype=np.uint8)
     counts[live] = np.diff(starts)
     ref[live] = do_ref
-    # one pinned upload: keypoints | pimg [P] i32 | chunks [3P] i32 | ref [B] u8
+    # one pinned buffer: the upload (keypoints | pimg [P] i32 | chunks [3P] i32 | ref [B] u8), then the keypoints'
+    # read-back at an 8-byte boundary
     o1 = kp_all.nbytes
     o2 = o1 + 4 * P
     o3 = o2 + 12 * P
-    host = torch.empty(o3 + B, dtype=torch.uint8, pin_memory=True)
+    ob = (o3 + B + 7) // 8 * 8
+    pin = torch.empty(ob + o1, dtype=torch.uint8, pin_memory=True)
+    host = pin[:o3 + B]
     hv = host.numpy()
     hv[:o1] = kp_all.reshape(-1).view(np.uint8)
     hv[o3:] = ref
@@ -516,7 +521,7 @@ def finish_batch_start(per_image, scoremaps, tags, adjustment=True, with_refine=
                                             base, P, base + o1, base + o2, int(plan[0]), int(plan[1]), base + o3,
                                             int(adjustment), ws.data_ptr() if ws is not None else None,
                                             ws.numel() if ws is not None else 0, _lib.stream(dev)), L)
-        back = torch.empty(kp_all.shape, dtype=torch.float64, pin_memory=True)
+        back = pin[ob:].view(torch.float64).view(kp_all.shape)
         back.copy_(dbuf[:o1].view(torch.float64).view(kp_all.shape), non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(st)

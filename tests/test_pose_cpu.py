@@ -320,3 +320,35 @@ def test_finish_plan_chunks():
     np.testing.assert_array_equal(covered, np.repeat(ref.astype(int), counts))
     assert L.pemp_pose_finish_plan(len(counts), counts.ctypes.data, ref.ctypes.data, pimg.ctypes.data,
                                    chunks.ctypes.data, 3, out2.ctypes.data) != 0   # max_chunks too small
+
+
+def test_check_coords_matches_int_indexing():
+    """pose._check_coords (refine / adjust: every detected joint must index the map at int(x), int(y), Utils.py:1096)
+    accepts exactly the keypoints whose truncated coordinates lie in [0, W) x [0, H): borders, values in (-1, 0),
+    NaN / inf, undetected joints outside the map."""
+    from pemp_amd import pose as pp
+
+    def reference(kp, H, W):   # the masked int casts the check replaces
+        live = kp[:, :, 2] > 0
+        with np.errstate(invalid="ignore"):
+            x = kp[:, :, 0][live].astype(np.int64)
+            y = kp[:, :, 1][live].astype(np.int64)
+        return not ((x < 0).any() or (x >= W).any() or (y < 0).any() or (y >= H).any())
+
+    rng = np.random.default_rng(5)
+    H, W = 48, 64
+    specials = [-1.0, -0.999, -0.5, -0.0, 0.0, W - 0.5, W - 1e-9, W, W + 0.5, H - 0.5, H, np.nan, np.inf, -np.inf]
+    for trial in range(300):
+        kp = np.stack([rng.uniform(-2, W + 2, (3, 5)), rng.uniform(-2, H + 2, (3, 5)),
+                       (rng.random((3, 5)) > 0.5).astype(np.float64)], -1)
+        if trial % 3 == 0:
+            kp[:, :, 0] = rng.uniform(0, W - 1, (3, 5))
+            kp[:, :, 1] = rng.uniform(0, H - 1, (3, 5))
+        for _ in range(trial % 4):
+            kp[rng.integers(3), rng.integers(5), rng.integers(2)] = specials[rng.integers(len(specials))]
+        try:
+            pp._check_coords(kp, H, W, "test")
+            got = True
+        except IndexError:
+            got = False
+        assert got == reference(kp, H, W), kp
